@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 DDP bf16 training throughput (images/sec, whole node).
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP bf16 at 1/2/4/8
+MI355X".  One process per GPU (torchrun for N>1), synthetic 3x224x224 inputs
+and random-init weights (no datasets / checkpoints are available offline),
+fixed per-GPU batch (weak scaling).  Every timed step is a full training step:
+forward, fp32 cross-entropy, backward with the native C++ reducer doing
+bucketed RCCL all-reduces (25 MB buckets, ncclAvg) overlapped with backward,
+one fused flat-SGD (momentum 0.9, wd 1e-4) launch per dtype group.
+
+  python bench.py --gpus N --steps K --warmup W
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Time = max over ranks of the K-step wall time,
+bracketed by a barrier + device synchronize on both sides.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_model_parallel_amd.comm.rccl import default_communicator  # noqa: E402
+from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
+from distributed_model_parallel_amd.utils.env import destroy_distributed, init_distributed  # noqa: E402
+from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
+
+BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference images/sec figure exists
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--parallel", default="ddp", choices=["ddp", "syncbn", "dp", "none"])
+    ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=1.0)
+    ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--miopen-benchmark", type=int, default=int(os.environ.get("DMP_MIOPEN_BENCHMARK", "0")))
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    env = init_distributed()
+    if env.world_size != args.gpus and env.is_main:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
+    dev = env.device
+    cfg = StepConfig(model=args.model, batch_size=args.batch_size, image_size=args.image_size,
+                     dtype=parse_dtype(args.dtype), channels_last=not args.no_channels_last,
+                     parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
+                     first_bucket_mb=args.first_bucket_mb)
+    st = build_train_state(cfg, dev)
+    comm = default_communicator(dev)
+
+    t_warm0 = time.time()
+    for i in range(args.warmup):
+        loss = st.step()
+        if i == 0 and env.is_main:
+            torch.cuda.synchronize() if dev.type == "cuda" else None
+            print(f"[bench] first step done in {time.time() - t_warm0:.1f}s loss={loss.item():.4f}",
+                  file=sys.stderr, flush=True)
+    comm.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = st.step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = comm.max_scalar(elapsed)
+    final_loss = float(loss.item())
+
+    n = env.world_size
+    global_batch = args.batch_size * n
+    img_s = global_batch * args.steps / elapsed
+    par = {"ddp": "dp", "syncbn": "dp", "dp": "dp-single-process", "none": "none"}[args.parallel]
+    metric = f"images/sec (whole node) {'ResNet-50' if args.model == 'resnet50' else args.model} " \
+             f"{'DDP' if args.parallel in ('ddp', 'syncbn') else args.parallel.upper()} {args.dtype}"
+    result = {
+        "metric": metric,
+        "value": round(img_s, 2),
+        "unit": "images/sec",
+        "n_gpus": n,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (img_s / BASELINE_VALUE) if BASELINE_VALUE else None,
+        "dtype": args.dtype,
+        "data": "synthetic (random 3x%dx%d inputs, random labels, random-init weights)"
+                % (args.image_size, args.image_size),
+        "config": {
+            "model": args.model,
+            "global_batch": global_batch,
+            "per_gpu_batch": args.batch_size,
+            "seq_len": None,
+            "image_size": args.image_size,
+            "parallelism": f"{par}{n}",
+            "sync_bn": args.parallel == "syncbn",
+            "bucket_cap_mb": args.bucket_cap_mb,
+            "channels_last": not args.no_channels_last,
+            "final_loss": round(final_loss, 4),
+        },
+    }
+    if env.is_main:
+        line = json.dumps(result)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    destroy_distributed()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

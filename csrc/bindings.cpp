@@ -1,0 +1,121 @@
+// Python bindings of the native runtime (module distributed_model_parallel_amd._C).
+#include <torch/extension.h>
+
+#include "comm/rccl_comm.h"
+#include "ddp/reducer.h"
+
+namespace dmp {
+// batchnorm.hip
+at::Tensor bn_local_moments(const at::Tensor& x, int64_t C);
+std::vector<at::Tensor> bn_forward_finalize(const at::Tensor& sums, int64_t C,
+                                            const c10::optional<at::Tensor>& weight,
+                                            const c10::optional<at::Tensor>& bias,
+                                            const c10::optional<at::Tensor>& running_mean,
+                                            const c10::optional<at::Tensor>& running_var,
+                                            double momentum, double eps);
+std::vector<at::Tensor> bn_eval_coeffs(const at::Tensor& running_mean, const at::Tensor& running_var,
+                                       const c10::optional<at::Tensor>& weight,
+                                       const c10::optional<at::Tensor>& bias, double eps);
+at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
+                    const c10::optional<at::Tensor>& residual, bool relu, int64_t C);
+at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
+                               const c10::optional<at::Tensor>& y, const at::Tensor& mean,
+                               bool relu, int64_t C);
+std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor& x,
+                                          const c10::optional<at::Tensor>& y,
+                                          const at::Tensor& sums, const at::Tensor& count,
+                                          const c10::optional<at::Tensor>& weight,
+                                          const at::Tensor& mean, const at::Tensor& invstd,
+                                          bool training, bool relu, bool want_dres, int64_t C);
+// fused_sgd.hip
+void sgd_flat_step(const c10::optional<at::Tensor>& master, const at::Tensor& mom,
+                   const at::Tensor& grad, const at::Tensor& param, double lr, double wd,
+                   double momentum, double dampening, bool nesterov, double grad_scale,
+                   bool first_step);
+// coalesced.hip
+void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
+void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
+void gather_slabs(const std::vector<at::Tensor>& inputs, at::Tensor& out, bool along_inner);
+void enable_peer_access(int64_t num_devices);
+}  // namespace dmp
+
+namespace py = pybind11;
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X-native runtime: RCCL communicator, DDP reducer, HIP kernels (gfx950)";
+
+  // ---- batch norm ----
+  m.def("bn_local_moments", &dmp::bn_local_moments);
+  m.def("bn_forward_finalize", &dmp::bn_forward_finalize);
+  m.def("bn_eval_coeffs", &dmp::bn_eval_coeffs);
+  m.def("bn_apply", &dmp::bn_apply);
+  m.def("bn_backward_moments", &dmp::bn_backward_moments);
+  m.def("bn_backward_apply", &dmp::bn_backward_apply);
+
+  // ---- optimizer ----
+  m.def("sgd_flat_step", &dmp::sgd_flat_step);
+
+  // ---- coalesced movement ----
+  m.def("multi_copy", &dmp::multi_copy);
+  m.def("reduce_add_into", &dmp::reduce_add_into);
+  m.def("gather_slabs", &dmp::gather_slabs);
+  m.def("enable_peer_access", &dmp::enable_peer_access);
+
+  // ---- RCCL ----
+  py::class_<dmp::RcclComm, std::shared_ptr<dmp::RcclComm>>(m, "RcclComm")
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t>(), py::arg("unique_id"),
+           py::arg("nranks"), py::arg("rank"), py::arg("device"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_static("new_unique_id", [] { return py::bytes(dmp::RcclComm::new_unique_id()); })
+      .def_property_readonly("rank", &dmp::RcclComm::rank)
+      .def_property_readonly("size", &dmp::RcclComm::size)
+      .def_property_readonly("device", &dmp::RcclComm::device)
+      .def("all_reduce", &dmp::RcclComm::all_reduce, py::arg("tensor"), py::arg("op") = "sum",
+           py::call_guard<py::gil_scoped_release>())
+      .def("all_reduce_coalesced", &dmp::RcclComm::all_reduce_coalesced, py::arg("tensors"),
+           py::arg("op") = "sum", py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &dmp::RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("reduce", &dmp::RcclComm::reduce, py::arg("tensor"), py::arg("root"),
+           py::arg("op") = "sum", py::call_guard<py::gil_scoped_release>())
+      .def("all_gather", &dmp::RcclComm::all_gather, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &dmp::RcclComm::reduce_scatter, py::arg("out"), py::arg("inp"),
+           py::arg("op") = "sum", py::call_guard<py::gil_scoped_release>())
+      .def("all_to_all", &dmp::RcclComm::all_to_all, py::call_guard<py::gil_scoped_release>())
+      .def("send", &dmp::RcclComm::send, py::call_guard<py::gil_scoped_release>())
+      .def("recv", &dmp::RcclComm::recv, py::call_guard<py::gil_scoped_release>())
+      .def("batch_p2p", &dmp::RcclComm::batch_p2p, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &dmp::RcclComm::wait, py::call_guard<py::gil_scoped_release>())
+      .def("synchronize", &dmp::RcclComm::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("stream_handle",
+           [](const dmp::RcclComm& c) { return reinterpret_cast<uintptr_t>(c.stream()); });
+
+  // ---- DDP reducer ----
+  py::class_<dmp::ReduceBackend, std::shared_ptr<dmp::ReduceBackend>>(m, "ReduceBackend");
+  py::class_<dmp::RcclReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::RcclReduceBackend>>(
+      m, "RcclReduceBackend")
+      .def(py::init<std::shared_ptr<dmp::RcclComm>>());
+  py::class_<dmp::PyReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::PyReduceBackend>>(
+      m, "PyReduceBackend")
+      .def(py::init<py::object>());
+
+  py::class_<dmp::Reducer, std::shared_ptr<dmp::Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>,
+                    std::shared_ptr<dmp::ReduceBackend>, bool>(),
+           py::arg("params"), py::arg("buckets"), py::arg("backend"), py::arg("find_unused"))
+      .def("prepare_for_backward", &dmp::Reducer::prepare_for_backward,
+           py::call_guard<py::gil_scoped_release>())
+      .def("disarm", &dmp::Reducer::disarm)
+      .def("rebuild", &dmp::Reducer::rebuild, py::call_guard<py::gil_scoped_release>())
+      .def("buckets", &dmp::Reducer::buckets)
+      .def("ready_order", &dmp::Reducer::ready_order)
+      .def("group_flats", &dmp::Reducer::group_flats)
+      .def("layout", &dmp::Reducer::layout)
+      .def("grad_views", &dmp::Reducer::grad_views)
+      .def("unused_params", &dmp::Reducer::unused_params)
+      .def("num_launched", &dmp::Reducer::num_launched)
+      .def("set_backend", &dmp::Reducer::set_backend)
+      .def("zero_grad", &dmp::Reducer::zero_grad, py::call_guard<py::gil_scoped_release>());
+
+  m.def("compute_bucket_assignment", &dmp::compute_bucket_assignment, py::arg("params"),
+        py::arg("cap_bytes"), py::arg("first_cap_bytes"));
+}

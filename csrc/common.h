@@ -1,0 +1,84 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of this package.
+//
+// Conventions used by every kernel here:
+//   * wave64: lane = threadIdx.x & 63, never & 31.
+//   * memory-bound kernels move 16 bytes per lane per access (bf16x8 / f32x4),
+//     which is the coalescing sweet spot on CDNA4 (1 KiB per wave instruction).
+//   * bf16 <-> f32 conversions use clang's native __bf16, which hipcc lowers to
+//     v_cvt_pk_bf16_f32 / shifts on gfx950 (round-to-nearest-even).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dmp {
+
+using f32x4 = float __attribute__((ext_vector_type(4)));
+using f32x8 = float __attribute__((ext_vector_type(8)));
+using bf16x8 = __bf16 __attribute__((ext_vector_type(8)));
+using bf16x4 = __bf16 __attribute__((ext_vector_type(4)));
+using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+// ---- 16-byte vector of "VEC" elements of type T, converted to/from f32 ----
+template <typename T> struct Vec16;
+
+template <> struct Vec16<float> {
+  static constexpr int N = 4;
+  using raw = f32x4;
+  __device__ __forceinline__ static void load(const float* p, float (&v)[4]) {
+    f32x4 r = *reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = r[i];
+  }
+  __device__ __forceinline__ static void store(float* p, const float (&v)[4]) {
+    f32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = v[i];
+    *reinterpret_cast<f32x4*>(p) = r;
+  }
+};
+
+template <> struct Vec16<__bf16> {
+  static constexpr int N = 8;
+  using raw = bf16x8;
+  __device__ __forceinline__ static void load(const __bf16* p, float (&v)[8]) {
+    bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+    f32x8 f = __builtin_convertvector(r, f32x8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = f[i];
+  }
+  __device__ __forceinline__ static void store(__bf16* p, const float (&v)[8]) {
+    f32x8 f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = v[i];
+    *reinterpret_cast<bf16x8*>(p) = __builtin_convertvector(f, bf16x8);
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5.5 T1):
+// consecutive logical tiles land on the same XCD (same L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int nxcd = 8;
+  if (nblocks < nxcd) return bid;
+  int q = nblocks / nxcd, r = nblocks % nxcd;
+  int xcd = bid % nxcd, idx = bid / nxcd;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace dmp
+
+#include "check.h"

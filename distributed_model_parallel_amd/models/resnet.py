@@ -1,0 +1,145 @@
+"""ResNet-18/34/50/101/152 (ImageNet layout, torchvision-compatible parameter
+shapes and counts: ResNet-18 = 11,689,512, ResNet-50 = 25,557,032).
+
+The BASELINE.json north-star workloads (ResNet-18 DP plumbing, ResNet-50 DDP /
+DP / SyncBN) -- torchvision is not installed, so the models are our own.
+MI355X-first choices:
+  * every BN+ReLU and the bottleneck's BN+residual-add+ReLU run as ONE fused
+    channels-last kernel (:class:`~..ops.batchnorm.BatchNormAct2d`), i.e. the
+    residual add and both activations cost no extra HBM pass;
+  * meant to run in ``torch.channels_last`` so convolutions and BN see NHWC;
+  * ``zero_init_residual`` as in the usual large-batch recipe.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Type, Union
+
+import torch
+import torch.nn as nn
+
+from ..ops.batchnorm import BatchNormAct2d
+
+
+def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+
+
+def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
+    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin: int, planes: int, stride: int = 1,
+                 downsample: Optional[nn.Module] = None):
+        super().__init__()
+        self.conv1 = _conv3x3(cin, planes, stride)
+        self.bn1 = BatchNormAct2d(planes, act="relu")
+        self.conv2 = _conv3x3(planes, planes)
+        self.bn2 = BatchNormAct2d(planes, act="relu")  # fused: relu(bn2(x) + identity)
+        self.downsample = downsample
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), identity)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, planes: int, stride: int = 1,
+                 downsample: Optional[nn.Module] = None):
+        super().__init__()
+        self.conv1 = _conv1x1(cin, planes)
+        self.bn1 = BatchNormAct2d(planes, act="relu")
+        self.conv2 = _conv3x3(planes, planes, stride)  # stride on the 3x3 (ResNet v1.5)
+        self.bn2 = BatchNormAct2d(planes, act="relu")
+        self.conv3 = _conv1x1(planes, planes * 4)
+        self.bn3 = BatchNormAct2d(planes * 4, act="relu")  # fused residual add + relu
+        self.downsample = downsample
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        identity = x if self.downsample is None else self.downsample(x)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: Sequence[int],
+                 num_classes: int = 1000, zero_init_residual: bool = False,
+                 stem_channels: int = 64):
+        super().__init__()
+        self.inplanes = stem_channels
+        self.conv1 = nn.Conv2d(3, stem_channels, 7, stride=2, padding=3, bias=False)
+        self.bn1 = BatchNormAct2d(stem_channels, act="relu")
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make_layer(block, 64, layers[0])
+        self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
+        self.layer3 = self._make_layer(block, 256, layers[2], stride=2)
+        self.layer4 = self._make_layer(block, 512, layers[3], stride=2)
+        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+                elif isinstance(m, BasicBlock):
+                    nn.init.zeros_(m.bn2.weight)
+
+    def _make_layer(self, block, planes: int, blocks: int, stride: int = 1) -> nn.Sequential:
+        downsample = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            downsample = nn.Sequential(
+                _conv1x1(self.inplanes, planes * block.expansion, stride),
+                BatchNormAct2d(planes * block.expansion, act=None),
+            )
+        mods: List[nn.Module] = [block(self.inplanes, planes, stride, downsample)]
+        self.inplanes = planes * block.expansion
+        for _ in range(1, blocks):
+            mods.append(block(self.inplanes, planes))
+        return nn.Sequential(*mods)
+
+    def forward_features(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return torch.flatten(self.avgpool(x), 1)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.fc(self.forward_features(x))
+
+    def as_sequential(self) -> nn.Sequential:
+        """Atoms for the pipeline partitioner: stem, every block, head."""
+        atoms: List[nn.Module] = [nn.Sequential(self.conv1, self.bn1, self.maxpool)]
+        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+            atoms.extend(list(layer))
+        atoms.append(nn.Sequential(self.avgpool, nn.Flatten(1), self.fc))
+        return nn.Sequential(*atoms)
+
+
+def resnet18(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, **kw)
+
+
+def resnet34(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet50(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, **kw)
+
+
+def resnet101(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes, **kw)
+
+
+def resnet152(num_classes: int = 1000, **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 8, 36, 3], num_classes, **kw)

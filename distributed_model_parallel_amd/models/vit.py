@@ -1,0 +1,108 @@
+"""Vision Transformer ViT-B/16 (86,567,656 parameters at 1000 classes, the
+torchvision layout: conv patch embedding, class token, learned positional
+embedding, 12 pre-LN encoder blocks, LayerNorm + linear head).
+
+BASELINE.json config 5 ("ViT-B/16 DDP bf16 ... large-grad bucket fusion, MFMA
+GEMM path").  The encoder is written so that all matmuls are plain GEMMs on
+[B*T, D] activations (qkv, proj, fc1, fc2 land on hipBLASLt/MFMA) and
+attention uses the fused SDPA kernel; no per-head Python loops.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class MLP(nn.Module):
+    def __init__(self, dim: int, hidden: int, dropout: float = 0.0):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+        self.dropout = dropout
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = F.gelu(self.fc1(x))
+        x = F.dropout(x, self.dropout, self.training)
+        return F.dropout(self.fc2(x), self.dropout, self.training)
+
+
+class SelfAttention(nn.Module):
+    def __init__(self, dim: int, heads: int, dropout: float = 0.0):
+        super().__init__()
+        assert dim % heads == 0
+        self.heads = heads
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+        self.dropout = dropout
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        b, t, d = x.shape
+        qkv = self.qkv(x).view(b, t, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv.unbind(0)
+        o = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
+        return self.proj(o.transpose(1, 2).reshape(b, t, d))
+
+
+class EncoderBlock(nn.Module):
+    def __init__(self, dim: int, heads: int, mlp_dim: int, dropout: float = 0.0):
+        super().__init__()
+        self.ln1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = SelfAttention(dim, heads, dropout)
+        self.ln2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = MLP(dim, mlp_dim, dropout)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x + self.attn(self.ln1(x))
+        return x + self.mlp(self.ln2(x))
+
+
+class VisionTransformer(nn.Module):
+    def __init__(self, image_size: int = 224, patch_size: int = 16, num_layers: int = 12,
+                 num_heads: int = 12, hidden_dim: int = 768, mlp_dim: int = 3072,
+                 num_classes: int = 1000, dropout: float = 0.0):
+        super().__init__()
+        assert image_size % patch_size == 0
+        self.patch_size = patch_size
+        self.hidden_dim = hidden_dim
+        self.patch_embed = nn.Conv2d(3, hidden_dim, patch_size, stride=patch_size)
+        n_tokens = (image_size // patch_size) ** 2 + 1
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_dim))
+        self.pos_embedding = nn.Parameter(torch.empty(1, n_tokens, hidden_dim).normal_(std=0.02))
+        self.blocks = nn.Sequential(*[EncoderBlock(hidden_dim, num_heads, mlp_dim, dropout)
+                                      for _ in range(num_layers)])
+        self.ln = nn.LayerNorm(hidden_dim, eps=1e-6)
+        self.head = nn.Linear(hidden_dim, num_classes)
+        self._init()
+
+    def _init(self):
+        fan_in = 3 * self.patch_size ** 2
+        nn.init.trunc_normal_(self.patch_embed.weight, std=math.sqrt(1.0 / fan_in))
+        nn.init.zeros_(self.patch_embed.bias)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                nn.init.normal_(m.bias, std=1e-6)
+        nn.init.zeros_(self.head.weight)
+        nn.init.zeros_(self.head.bias)
+
+    def tokens(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.patch_embed(x).flatten(2).transpose(1, 2)  # [B, T, D]
+        cls = self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype)
+        return torch.cat([cls, x], 1) + self.pos_embedding.to(x.dtype)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = self.blocks(self.tokens(x))
+        return self.head(self.ln(x)[:, 0])
+
+
+def vit_b_16(num_classes: int = 1000, image_size: int = 224, **kw) -> VisionTransformer:
+    return VisionTransformer(image_size, 16, 12, 12, 768, 3072, num_classes, **kw)
+
+
+def vit_tiny(num_classes: int = 10, image_size: int = 32, **kw) -> VisionTransformer:
+    """Small config for CPU tests."""
+    return VisionTransformer(image_size, 8, 2, 2, 32, 64, num_classes, **kw)

@@ -1,0 +1,279 @@
+"""Fused BatchNorm(+residual)(+ReLU) for channels-last activations.
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers
+and state_dict keys) whose forward can also add a residual and apply ReLU in
+the same pass.  On MI355X it runs the HIP kernels of ``csrc/bn/batchnorm.hip``
+on the [N*H*W, C] view of a channels-last tensor (2 HBM passes forward, 2
+backward, ReLU re-derived from the saved output).  On CPU the same two-phase
+algorithm runs in PyTorch ops, which is also what makes the SyncBatchNorm
+variant testable over gloo.
+
+The two-phase structure (local moments -> optional all-reduce -> finalize ->
+apply) is shared with :class:`..parallel.sync_batchnorm.SyncBatchNorm`,
+which plugs a cross-rank reduction between the phases (SURVEY.md D11;
+reference Readme.md:151).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native
+
+# A moment reducer maps local fp64 moments [2C+1] = (sum x, sum x^2, rows) to
+# the global ones (an all-reduce SUM); identity for plain BN.  The row count
+# travels inside the tensor, so nothing ever syncs the host.
+MomentReducer = Callable[[torch.Tensor], torch.Tensor]
+GradReducer = Callable[[torch.Tensor], torch.Tensor]
+
+_STATS = {"native_fwd": 0, "torch_fwd": 0}
+
+
+def stats() -> dict:
+    return dict(_STATS)
+
+
+# --------------------------------------------------------------------------- #
+# Layout helpers
+# --------------------------------------------------------------------------- #
+def _as_rows(x: torch.Tensor) -> Tuple[torch.Tensor, Callable[[torch.Tensor], torch.Tensor]]:
+    """View/convert x to a row-major [M, C] matrix and return an inverse map."""
+    if x.dim() == 2:
+        x2 = x.contiguous()
+        return x2, lambda t: t
+    if x.dim() == 4:
+        n, c, h, w = x.shape
+        xl = x.contiguous(memory_format=torch.channels_last)
+        x2 = xl.permute(0, 2, 3, 1).reshape(-1, c)
+        return x2, lambda t: t.view(n, h, w, c).permute(0, 3, 1, 2)
+    if x.dim() == 3:  # [N, C, L] (BatchNorm1d on sequences)
+        n, c, l = x.shape
+        x2 = x.transpose(1, 2).contiguous().reshape(-1, c)
+        return x2, lambda t: t.view(n, l, c).transpose(1, 2)
+    raise ValueError(f"BatchNorm expects 2-D, 3-D or 4-D input, got {x.dim()}-D")
+
+
+def _native_ok(x2: torch.Tensor) -> bool:
+    if not _native.gpu_path(x2):
+        return False
+    c = x2.shape[1]
+    vec = 8 if x2.dtype == torch.bfloat16 else 4
+    return (x2.dtype in (torch.float32, torch.bfloat16) and c % vec == 0
+            and x2.data_ptr() % 16 == 0 and x2.is_contiguous())
+
+
+# --------------------------------------------------------------------------- #
+# Primitive ops: native (HIP) or PyTorch reference, identical math
+# --------------------------------------------------------------------------- #
+def local_moments(x2: torch.Tensor, native: bool) -> torch.Tensor:
+    c = x2.shape[1]
+    if native:
+        return _native.require("bn").bn_local_moments(x2, c)
+    xd = x2.double()
+    return torch.cat([xd.sum(0), (xd * xd).sum(0), xd.new_tensor([float(x2.shape[0])])])
+
+
+def forward_finalize(sums, weight, bias, rm, rv, momentum, eps, native):
+    c = (sums.numel() - 1) // 2
+    if native:
+        return _native.require("bn").bn_forward_finalize(sums, c, weight, bias, rm, rv,
+                                                          float(momentum), float(eps))
+    count = sums[2 * c]
+    mean = sums[:c] / count
+    var = (sums[c:2 * c] / count - mean * mean).clamp_min(0)
+    invstd = torch.rsqrt(var + eps).float()
+    w = weight.float() if weight is not None else torch.ones_like(invstd)
+    b = bias.float() if bias is not None else torch.zeros_like(invstd)
+    scale = w * invstd
+    shift = b - mean.float() * scale
+    if rm is not None:
+        unbiased = var * count / (count - 1.0).clamp_min(1.0)
+        rm.mul_(1 - momentum).add_(mean.to(rm.dtype), alpha=momentum)
+        rv.mul_(1 - momentum).add_(unbiased.to(rv.dtype), alpha=momentum)
+    return [mean.float(), invstd, scale, shift]
+
+
+def eval_coeffs(rm, rv, weight, bias, eps, native):
+    if native:
+        return _native.require("bn").bn_eval_coeffs(rm.float(), rv.float(), weight, bias, float(eps))
+    invstd = torch.rsqrt(rv.float() + eps)
+    w = weight.float() if weight is not None else torch.ones_like(invstd)
+    b = bias.float() if bias is not None else torch.zeros_like(invstd)
+    scale = w * invstd
+    return [rm.float(), invstd, scale, b - rm.float() * scale]
+
+
+def apply(x2, scale, shift, res2, relu, native):
+    c = x2.shape[1]
+    if native:
+        return _native.require("bn").bn_apply(x2, scale, shift, res2, relu, c)
+    y = x2.float() * scale + shift
+    if res2 is not None:
+        y = y + res2.float()
+    if relu:
+        y = y.clamp_min(0)
+    return y.to(x2.dtype)
+
+
+def backward_moments(dy2, x2, y2, mean, relu, native):
+    c = x2.shape[1]
+    if native:
+        return _native.require("bn").bn_backward_moments(dy2, x2, y2, mean, relu, c)
+    dz = dy2.double()
+    if relu:
+        dz = dz * (y2 > 0)
+    return torch.cat([dz.sum(0), (dz * (x2.double() - mean.double())).sum(0)])
+
+
+def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, relu, want_dres, native):
+    """`count` is a 1-element fp64 tensor (global rows)."""
+    c = x2.shape[1]
+    if native:
+        return _native.require("bn").bn_backward_apply(dy2, x2, y2, sums, count, weight, mean,
+                                                        invstd, training, relu, want_dres, c)
+    count = count.reshape(()).to(torch.float64)
+    sdz, sdzx = sums[:c], sums[c:]
+    w = weight.double() if weight is not None else torch.ones_like(sdz)
+    istd = invstd.double()
+    dz = dy2.double()
+    if relu:
+        dz = dz * (y2 > 0)
+    a = w * istd
+    if training:
+        b = -a * istd * istd * sdzx / count
+        cc = -a * sdz / count - b * mean.double()
+        dx = a * dz + b * x2.double() + cc
+    else:
+        dx = a * dz
+    dres = dz.to(x2.dtype) if want_dres else None
+    return [dx.to(x2.dtype), (sdzx * istd).float(), sdz.float(), dres]
+
+
+# --------------------------------------------------------------------------- #
+# Autograd function
+# --------------------------------------------------------------------------- #
+class _BatchNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
+                relu, reduce_moments, reduce_grads):
+        x2, back = _as_rows(x)
+        native = _native_ok(x2)
+        _STATS["native_fwd" if native else "torch_fwd"] += 1
+        res2 = None
+        if residual is not None:
+            res2, _ = _as_rows(residual.to(x.dtype))
+        w32 = weight.float() if weight is not None else None
+        b32 = bias.float() if bias is not None else None
+        if training:
+            sums = local_moments(x2, native)
+            if reduce_moments is not None:
+                sums = reduce_moments(sums)
+            count = sums[-1:]
+            upd_rm = running_mean if (running_mean is not None and running_mean.dtype == torch.float32) else None
+            upd_rv = running_var if upd_rm is not None else None
+            mean, invstd, scale, shift = forward_finalize(sums, w32, b32, upd_rm, upd_rv,
+                                                          momentum, eps, native)
+            if running_mean is not None and upd_rm is None:  # low-precision buffers
+                c = x2.shape[1]
+                n = sums[2 * c]
+                unbiased = (sums[c:2 * c] / n - mean.double() ** 2) * n / (n - 1).clamp_min(1)
+                running_mean.mul_(1 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
+                running_var.mul_(1 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
+        else:
+            count = torch.full((1,), float(x2.shape[0]), dtype=torch.float64, device=x2.device)
+            mean, invstd, scale, shift = eval_coeffs(running_mean, running_var, w32, b32, eps, native)
+        y2 = apply(x2, scale, shift, res2, relu, native)
+        ctx.save_for_backward(x2, y2 if relu else None, w32, mean, invstd, count)
+        ctx.meta = (native, training, relu, residual is not None, back,
+                    weight is not None, bias is not None, reduce_grads,
+                    weight.dtype if weight is not None else None, x.dim())
+        return back(y2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, y2, w32, mean, invstd, count = ctx.saved_tensors
+        (native, training, relu, has_res, back, has_w, has_b, reduce_grads, wdtype,
+         ndim) = ctx.meta
+        dy2, _ = _as_rows(dy.to(x2.dtype))
+        sums = backward_moments(dy2, x2, y2, mean, relu, native)
+        local_sums = sums
+        if training and reduce_grads is not None:
+            sums = reduce_grads(sums)
+        dx2, dw, db, dres2 = backward_apply(dy2, x2, y2, sums, count, w32, mean, invstd, training,
+                                            relu, has_res, native)
+        if reduce_grads is not None and training:
+            # weight/bias grads are per-rank quantities (DDP averages them)
+            c = x2.shape[1]
+            dw = (local_sums[c:] * invstd.double()).float()
+            db = local_sums[:c].float()
+        gx = back(dx2)
+        gres = back(dres2) if has_res else None
+        gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
+        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
+        return gx, gres, gw, gb, None, None, None, None, None, None, None, None
+
+
+def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
+                   running_var: Optional[torch.Tensor], weight: Optional[torch.Tensor],
+                   bias: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
+                   relu: bool = False, residual: Optional[torch.Tensor] = None,
+                   reduce_moments: Optional[MomentReducer] = None,
+                   reduce_grads: Optional[GradReducer] = None) -> torch.Tensor:
+    """Functional fused BN(+residual)(+ReLU)."""
+    return _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
+                                 momentum, eps, relu, reduce_moments, reduce_grads)
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` with optional fused residual add and ReLU.
+
+    ``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.
+    """
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: Optional[float] = 0.1,
+                 affine: bool = True, track_running_stats: bool = True, act: Optional[str] = None,
+                 device=None, dtype=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, device, dtype)
+        if act not in (None, "relu"):
+            raise ValueError(f"unsupported activation {act!r}")
+        self.act = act
+
+    def _check_input_dim(self, x):
+        if x.dim() not in (2, 3, 4):
+            raise ValueError(f"expected 2D-4D input (got {x.dim()}D input)")
+
+    def _momentum(self) -> float:
+        if self.momentum is None:
+            return 1.0 / float(self.num_batches_tracked) if self.num_batches_tracked is not None else 0.0
+        return float(self.momentum)
+
+    def _moment_reducers(self):
+        return None, None
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        self._check_input_dim(x)
+        use_batch = self.training or not self.track_running_stats
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+            self.num_batches_tracked.add_(1)
+        momentum = self._momentum() if (self.training and self.track_running_stats) else 0.0
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        rmom, rgrad = self._moment_reducers() if use_batch else (None, None)
+        return batch_norm_act(x, rm if self.track_running_stats else None,
+                              rv if self.track_running_stats else None, self.weight, self.bias,
+                              use_batch, momentum, self.eps, relu=self.act == "relu",
+                              residual=residual, reduce_moments=rmom, reduce_grads=rgrad)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (f", act={self.act}" if self.act else "")
+
+
+def reference_bn_act(x, rm, rv, w, b, training, momentum, eps, relu=False, residual=None):
+    """Plain PyTorch composition used as the numerics oracle in tests."""
+    y = F.batch_norm(x, rm, rv, w, b, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y

@@ -1,0 +1,122 @@
+"""FlatSGD: torch.optim.SGD semantics, one HIP launch per dtype group.
+
+Works on the flat parameter / gradient buffers of
+``DistributedDataParallel(..., flat_parameters=True)``: gradients there are
+already RCCL-averaged bucket views, parameters are views of a flat buffer with
+the same layout, so the update of all 161 ResNet-50 tensors is a single
+vectorised pass (``csrc/optim/fused_sgd.hip``).  bf16 parameter groups keep an
+fp32 master copy and fp32 momentum inside the optimizer; the kernel writes the
+bf16 working weights back in the same pass.
+
+Reference parity: SGD(lr, momentum 0.9, weight_decay 1e-4) at
+``model_parallel.py:105`` / ``data_parallel.py:90``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+from .. import _native
+
+
+class FlatSGD(torch.optim.Optimizer):
+    def __init__(self, ddp, lr: float, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, master_weights: bool = True):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        params = list(ddp._params)
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov)
+        super().__init__(params, defaults)
+        self.ddp = ddp
+        self.master_weights = master_weights
+        self._version = -1
+        self._flat_state: List[dict] = []
+        self._steps = 0
+
+    # ------------------------------------------------------------------ #
+    def _ensure_state(self) -> None:
+        if self._version == self.ddp.layout_version:
+            return
+        groups = self.ddp.flat_groups()
+        old = self._flat_state
+        old_layout = getattr(self.ddp, "_last_old_layout", None)
+        new_state = []
+        for pflat, gflat in groups:
+            st = {"param": pflat, "grad": gflat}
+            if pflat.dtype != torch.float32 and self.master_weights:
+                st["master"] = pflat.float()
+            st["momentum"] = torch.zeros(pflat.numel(), dtype=torch.float32, device=pflat.device)
+            new_state.append(st)
+        if old and old_layout is not None:
+            self._remap(old, new_state, old_layout, self.ddp.param_layout())
+        self._flat_state = new_state
+        self._version = self.ddp.layout_version
+
+    @torch.no_grad()
+    def _remap(self, old, new, old_layout, new_layout) -> None:
+        """Carry momentum / master buffers across a bucket rebuild."""
+        for p, (og, oo), (ng, no) in zip(self.ddp._params, old_layout, new_layout):
+            n = p.numel()
+            for key in ("momentum", "master"):
+                if key in old[og] and key in new[ng]:
+                    new[ng][key].narrow(0, no, n).copy_(old[og][key].narrow(0, oo, n))
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        self._ensure_state()
+        g = self.param_groups[0]
+        first = self._steps == 0
+        for st in self._flat_state:
+            pflat, gflat = st["param"], st["grad"]
+            master = st.get("master")
+            if pflat.is_cuda:
+                _native.require("FlatSGD").sgd_flat_step(
+                    master, st["momentum"], gflat, pflat, float(g["lr"]), float(g["weight_decay"]),
+                    float(g["momentum"]), float(g["dampening"]), bool(g["nesterov"]), 1.0, first)
+            else:
+                _sgd_reference(master, st["momentum"], gflat, pflat, g, first)
+        self._steps += 1
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        self.ddp.zero_grad()
+
+    def state_dict(self):
+        self._ensure_state()
+        return {"steps": self._steps, "param_groups": [{k: v for k, v in g.items() if k != "params"}
+                                                       for g in self.param_groups],
+                "flat_state": [{k: v for k, v in st.items() if k in ("momentum", "master")}
+                               for st in self._flat_state],
+                "layout": self.ddp.param_layout()}
+
+    def load_state_dict(self, sd):
+        self._ensure_state()
+        self._steps = sd["steps"]
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            g.update(sg)
+        for st, sst in zip(self._flat_state, sd["flat_state"]):
+            for k, v in sst.items():
+                if k in st:
+                    st[k].copy_(v)
+
+
+def _sgd_reference(master: Optional[torch.Tensor], mom: torch.Tensor, grad: torch.Tensor,
+                   param: torch.Tensor, g: dict, first: bool) -> None:
+    """PyTorch implementation of the flat kernel (CPU path / test oracle)."""
+    w = master if master is not None else param
+    d = grad.float() + g["weight_decay"] * w.float()
+    if g["momentum"] != 0:
+        if first:
+            mom.copy_(d)
+        else:
+            mom.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
+        d = d + g["momentum"] * mom if g["nesterov"] else mom
+    w.add_(d.to(w.dtype), alpha=-g["lr"])
+    if master is not None:
+        param.copy_(master.to(param.dtype))

@@ -1,0 +1,320 @@
+"""DataParallel: single process, many GPUs (parity with ``nn.DataParallel`` as
+used by the reference, ``data_parallel.py:74-78``, and dissected in
+Readme.md:17-143).
+
+``forward`` = scatter -> replicate -> parallel_apply -> gather, each an
+autograd-aware step built on the native pull-copy / N-way-add kernels of
+:mod:`.comm_ops`:
+
+* ``Scatter``   fwd: split along ``dim``, each GPU pulls its chunk;
+                bwd: gather the chunk gradients back (LDS-staged gather).
+* ``Replicate`` fwd: parameters of ``device_ids[0]`` flattened once, pulled by
+                every GPU, unflattened as views (no per-tensor copies);
+                bwd: per-GPU gradient flats summed on ``device_ids[0]`` by ONE
+                N-way add kernel reading peers (upstream ReduceAddCoalesced).
+* ``Gather``    fwd: outputs concatenated on ``output_device``;
+                bwd: scatter of the output gradient.
+* ``parallel_apply``: one thread per replica with the replica's device and
+  current stream set, grad-mode/autocast propagated, exceptions re-raised with
+  the replica/device in the message (upstream ExceptionWrapper semantics); a
+  single replica runs inline.
+
+The device-0 hot-spot the README warns about (Readme.md:15) is reduced because
+every peer pulls over its own xGMI link and the reduction is one kernel.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import _native
+from . import comm_ops
+
+
+# --------------------------------------------------------------------------- #
+# autograd functions
+# --------------------------------------------------------------------------- #
+class Scatter(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, devices, dim, chunk_sizes, x):
+        ctx.dim = dim
+        ctx.src = x.device
+        outs = comm_ops.scatter_tensor(x, devices, dim, chunk_sizes)
+        ctx.sizes = [o.shape[dim] for o in outs]
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        grads = [g if g is not None else None for g in grads]
+        if any(g is None for g in grads):
+            return None, None, None, None
+        return None, None, None, comm_ops.gather_tensors(grads, ctx.src, ctx.dim)
+
+
+class Gather(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, target, dim, *inputs):
+        ctx.dim = dim
+        ctx.devices = [i.device for i in inputs]
+        ctx.sizes = [i.shape[dim] if i.dim() > 0 else 1 for i in inputs]
+        ctx.scalar = inputs[0].dim() == 0
+        return comm_ops.gather_tensors(list(inputs), target, dim)
+
+    @staticmethod
+    def backward(ctx, g):
+        parts = comm_ops.scatter_tensor(g.contiguous(), ctx.devices, ctx.dim, ctx.sizes)
+        if ctx.scalar:
+            parts = [p.view(()) for p in parts]
+        return (None, None) + tuple(parts)
+
+
+class Replicate(torch.autograd.Function):
+    """params on devices[0] -> flattened replicas on every device (non-leaf)."""
+
+    @staticmethod
+    def forward(ctx, devices, *params):
+        ctx.src = params[0].device
+        ctx.n = len(params)
+        per_dev = comm_ops.broadcast_coalesced(list(params), devices)
+        flat_out = []
+        for i, lst in enumerate(per_dev):
+            if i == 0:
+                # devices[0] replica must be a distinct autograd output
+                flat_out.extend(p.view_as(p) for p in lst)
+            else:
+                flat_out.extend(lst)
+        return tuple(flat_out)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        n = ctx.n
+        per_dev = [list(grads[i:i + n]) for i in range(0, len(grads), n)]
+        # missing grads (unused params on some replica) -> zeros on that device
+        for lst in per_dev:
+            dev = next((g.device for g in lst if g is not None), ctx.src)
+            for j, g in enumerate(lst):
+                if g is None:
+                    ref = next(l[j] for l in per_dev if l[j] is not None) if any(
+                        l[j] is not None for l in per_dev) else None
+                    lst[j] = torch.zeros_like(ref, device=dev) if ref is not None else None
+        if any(g is None for g in per_dev[0]):
+            # a parameter with no grad anywhere
+            keep = [j for j in range(n) if per_dev[0][j] is not None]
+            sub = [[lst[j] for j in keep] for lst in per_dev]
+            red = comm_ops.reduce_add_coalesced(sub, ctx.src) if keep else []
+            out: List[Optional[torch.Tensor]] = [None] * n
+            for j, r in zip(keep, red):
+                out[j] = r
+        else:
+            out = comm_ops.reduce_add_coalesced(per_dev, ctx.src)
+        return (None,) + tuple(out)
+
+
+# --------------------------------------------------------------------------- #
+# functional building blocks (upstream names)
+# --------------------------------------------------------------------------- #
+def scatter(inputs: Any, target_gpus: Sequence, dim: int = 0):
+    """Recursively scatter tensors in nested tuples/lists/dicts; others are copied by ref."""
+    def rec(obj):
+        if isinstance(obj, torch.Tensor):
+            return Scatter.apply(list(target_gpus), dim, None, obj)
+        if isinstance(obj, tuple) and len(obj) > 0:
+            return list(zip(*map(rec, obj)))
+        if isinstance(obj, list) and len(obj) > 0:
+            return [list(i) for i in zip(*map(rec, obj))]
+        if isinstance(obj, dict) and len(obj) > 0:
+            return [type(obj)(i) for i in zip(*map(rec, obj.items()))]
+        return [obj for _ in target_gpus]
+    try:
+        return rec(inputs)
+    finally:
+        rec = None  # break the reference cycle
+
+
+def scatter_kwargs(inputs: Tuple, kwargs: Optional[Dict], target_gpus: Sequence, dim: int = 0):
+    ins = scatter(inputs, target_gpus, dim) if inputs else []
+    kws = scatter(kwargs, target_gpus, dim) if kwargs else []
+    if len(ins) < len(kws):
+        ins.extend(() for _ in range(len(kws) - len(ins)))
+    elif len(kws) < len(ins):
+        kws.extend({} for _ in range(len(ins) - len(kws)))
+    return tuple(tuple(i) for i in ins), tuple(kws)
+
+
+def replicate(network: nn.Module, devices: Sequence, detach: bool = False) -> List[nn.Module]:
+    devices = [comm_ops._dev(d) for d in devices]
+    params = list(network.parameters())
+    pidx = {id(p): i for i, p in enumerate(params)}
+    if params:
+        if detach or not torch.is_grad_enabled():
+            per_dev = comm_ops.broadcast_coalesced([p.detach() for p in params], devices)
+        else:
+            flat = Replicate.apply(devices, *params)
+            n = len(params)
+            per_dev = [list(flat[i * n:(i + 1) * n]) for i in range(len(devices))]
+    else:
+        per_dev = [[] for _ in devices]
+    bufs = list(network.buffers())
+    bidx = {id(b): i for i, b in enumerate(bufs)}
+    per_dev_b = comm_ops.broadcast_coalesced([b.detach() for b in bufs], devices) if bufs else \
+        [[] for _ in devices]
+
+    modules = list(network.modules())
+    replicas: List[List[nn.Module]] = []
+    for d in range(len(devices)):
+        mods = []
+        for m in modules:
+            r = m.__new__(type(m))
+            r.__dict__ = m.__dict__.copy()
+            r._parameters = {}
+            r._buffers = {}
+            r._modules = {}
+            r._is_replica = True
+            mods.append(r)
+        replicas.append(mods)
+    midx = {id(m): i for i, m in enumerate(modules)}
+    for i, m in enumerate(modules):
+        for d in range(len(devices)):
+            r = replicas[d][i]
+            for k, child in m._modules.items():
+                r._modules[k] = None if child is None else replicas[d][midx[id(child)]]
+            for k, p in m._parameters.items():
+                r._parameters[k] = None if p is None else per_dev[d][pidx[id(p)]]
+            for k, b in m._buffers.items():
+                if b is None:
+                    r._buffers[k] = None
+                elif d == 0:
+                    r._buffers[k] = b  # device 0 shares the real buffers (running stats)
+                else:
+                    r._buffers[k] = per_dev_b[d][bidx[id(b)]]
+    return [replicas[d][0] for d in range(len(devices))]
+
+
+class ReplicaError(RuntimeError):
+    pass
+
+
+def parallel_apply(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=None,
+                   devices: Optional[Sequence] = None) -> List[Any]:
+    n = len(modules)
+    kwargs_tup = kwargs_tup or tuple({} for _ in range(n))
+    if devices is None:
+        devices = [next(m.parameters()).device if any(True for _ in m.parameters()) else None
+                   for m in modules]
+    results: Dict[int, Any] = {}
+    lock = threading.Lock()
+    grad_enabled = torch.is_grad_enabled()
+    autocast_enabled = torch.is_autocast_enabled()
+
+    def worker(i, module, inp, kw, device):
+        torch.set_grad_enabled(grad_enabled)
+        try:
+            dev = comm_ops._dev(device) if device is not None else None
+            ctx = torch.cuda.device(dev) if (dev is not None and dev.type == "cuda") else comm_ops._null()
+            with ctx, torch.autocast("cuda", enabled=autocast_enabled):
+                if not isinstance(inp, (list, tuple)):
+                    inp = (inp,)
+                out = module(*inp, **kw)
+            with lock:
+                results[i] = out
+        except Exception as e:  # noqa: BLE001 - re-raised below with replica info
+            with lock:
+                results[i] = ReplicaError(f"Caught {type(e).__name__} in replica {i} on device "
+                                          f"{device}: {e}")
+                results[i].__cause__ = e
+
+    if n == 1:
+        worker(0, modules[0], inputs[0], kwargs_tup[0], devices[0])
+    else:
+        threads = [threading.Thread(target=worker, args=(i, m, x, k, d))
+                   for i, (m, x, k, d) in enumerate(zip(modules, inputs, kwargs_tup, devices))]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    outs = []
+    for i in range(n):
+        r = results[i]
+        if isinstance(r, ReplicaError):
+            raise r
+        outs.append(r)
+    return outs
+
+
+def gather(outputs: Sequence, target_device, dim: int = 0):
+    def rec(outs):
+        o = outs[0]
+        if isinstance(o, torch.Tensor):
+            return Gather.apply(target_device, dim, *outs)
+        if o is None:
+            return None
+        if isinstance(o, dict):
+            return type(o)((k, rec([d[k] for d in outs])) for k in o)
+        return type(o)(map(rec, zip(*outs)))
+    try:
+        return rec(outputs)
+    finally:
+        rec = None
+
+
+# --------------------------------------------------------------------------- #
+class DataParallel(nn.Module):
+    """Drop-in ``nn.DataParallel`` over the native scatter/replicate/gather kernels."""
+
+    def __init__(self, module: nn.Module, device_ids: Optional[Sequence[int]] = None,
+                 output_device: Optional[int] = None, dim: int = 0):
+        super().__init__()
+        self.module = module
+        self.dim = dim
+        if not torch.cuda.is_available():
+            self.device_ids: List[int] = []
+            self.output_device = None
+            return
+        if device_ids is None:
+            device_ids = list(range(torch.cuda.device_count()))
+        self.device_ids = [int(d.index if isinstance(d, torch.device) else d) for d in device_ids]
+        self.output_device = int(output_device) if output_device is not None else self.device_ids[0]
+        self.src_device_obj = torch.device("cuda", self.device_ids[0])
+        for t in list(module.parameters()) + list(module.buffers()):
+            if t.device != self.src_device_obj:
+                raise RuntimeError(f"module must have its parameters and buffers on device "
+                                   f"{self.src_device_obj} (device_ids[0]) but found one on {t.device}")
+        if len(set(self.device_ids)) > 1:
+            _native.require("DataParallel peer access").enable_peer_access(
+                max(self.device_ids) + 1)
+
+    def forward(self, *inputs, **kwargs):
+        if not self.device_ids:
+            return self.module(*inputs, **kwargs)
+        ins, kws = scatter_kwargs(inputs, kwargs, self.device_ids, self.dim)
+        if not ins and not kws:
+            ins, kws = ((),), ({},)
+        if len(self.device_ids) == 1:
+            return self.module(*ins[0], **kws[0])
+        replicas = self.replicate(self.module, self.device_ids[:len(ins)])
+        outs = self.parallel_apply(replicas, ins, kws)
+        return self.gather(outs, self.output_device)
+
+    def replicate(self, module, device_ids):
+        return replicate(module, device_ids, not torch.is_grad_enabled())
+
+    def scatter(self, inputs, kwargs, device_ids):
+        return scatter_kwargs(inputs, kwargs, device_ids, self.dim)
+
+    def parallel_apply(self, replicas, inputs, kwargs):
+        return parallel_apply(replicas, inputs, kwargs, self.device_ids[:len(replicas)])
+
+    def gather(self, outputs, output_device):
+        return gather(outputs, output_device, self.dim)
+
+
+def data_parallel(module: nn.Module, inputs, device_ids=None, output_device=None, dim: int = 0,
+                  module_kwargs=None):
+    """Functional form (upstream ``torch.nn.parallel.data_parallel``)."""
+    if not isinstance(inputs, tuple):
+        inputs = (inputs,) if inputs is not None else ()
+    dp = DataParallel(module, device_ids, output_device, dim)
+    return dp(*inputs, **(module_kwargs or {}))

@@ -1,0 +1,78 @@
+"""SyncBatchNorm: batch statistics over all ranks with ONE RCCL all-reduce of
+the fp64 moments [sum x, sum x^2, rows] per layer forward and one all-reduce of
+[sum dz, sum dz*(x-mean)] per layer backward.
+
+Parity: upstream SyncBatchNorm as "prepared for" by DDP's init helper
+(reference Readme.md:151).  Upstream all-gathers per-rank
+mean/invstd/count and combines them; here the moments are additive, so a single
+in-place all-reduce (north star: "SyncBatchNorm as an RCCL all-reduce of
+mean/var") replaces gather + combine, and the global row count rides in the
+same buffer so no host synchronisation is needed.  The kernels are the fused
+channels-last BN(+residual)(+ReLU) ones of :mod:`..ops.batchnorm`.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..comm.rccl import Communicator, default_communicator
+from ..ops.batchnorm import BatchNormAct2d
+
+
+class SyncBatchNorm(BatchNormAct2d):
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: Optional[float] = 0.1,
+                 affine: bool = True, track_running_stats: bool = True,
+                 process_group: Optional[dist.ProcessGroup] = None, act: Optional[str] = None,
+                 device=None, dtype=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, act,
+                         device, dtype)
+        self.process_group = process_group
+        self._comm: Optional[Communicator] = None
+
+    def _communicator(self, device: torch.device) -> Communicator:
+        if self._comm is None:
+            if self.process_group is None:
+                self._comm = default_communicator(device if device.type == "cuda" else None)
+            else:
+                self._comm = Communicator(device, self.process_group)
+        return self._comm
+
+    def _moment_reducers(self):
+        if not (dist.is_available() and dist.is_initialized()):
+            return None, None
+        if dist.get_world_size(self.process_group) == 1:
+            return None, None
+        dev = self.weight.device if self.weight is not None else self.running_mean.device
+        comm = self._communicator(dev)
+
+        def reduce(t: torch.Tensor) -> torch.Tensor:
+            t = t.contiguous()
+            comm.all_reduce(t, "sum")
+            comm.wait()
+            return t
+
+        return reduce, reduce
+
+    @classmethod
+    def convert_sync_batchnorm(cls, module: nn.Module,
+                               process_group: Optional[dist.ProcessGroup] = None) -> nn.Module:
+        """Recursively replace every BatchNorm*d (ours or torch's) by SyncBatchNorm."""
+        out = module
+        if isinstance(module, nn.modules.batchnorm._BatchNorm) and not isinstance(module, cls):
+            out = cls(module.num_features, module.eps, module.momentum, module.affine,
+                      module.track_running_stats, process_group,
+                      act=getattr(module, "act", None))
+            if module.affine:
+                with torch.no_grad():
+                    out.weight = module.weight
+                    out.bias = module.bias
+            out.running_mean = module.running_mean
+            out.running_var = module.running_var
+            out.num_batches_tracked = module.num_batches_tracked
+            out.training = module.training
+        for name, child in module.named_children():
+            out.add_module(name, cls.convert_sync_batchnorm(child, process_group))
+        return out

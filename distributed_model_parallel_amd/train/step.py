@@ -1,0 +1,124 @@
+"""One data-parallel training step, shared by bench.py, smoke() and the CLI.
+
+Per step (DDP mode): forward of the local micro-batch (bf16, channels-last),
+cross-entropy in fp32, backward with bucketed RCCL all-reduce overlapped by
+the C++ reducer, one fused flat SGD launch per dtype group, one fill per
+group to zero the gradient buckets.  Nothing is skipped or cached: every step
+reads the input batch, runs the full model and updates every parameter.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..models import INPUT_SHAPES, build_model
+from ..ops.optim import FlatSGD
+from ..utils.precision import cast_model
+
+
+@dataclass
+class StepConfig:
+    model: str = "resnet50"
+    batch_size: int = 256            # per GPU
+    image_size: Optional[int] = None
+    num_classes: Optional[int] = None
+    dtype: torch.dtype = torch.bfloat16
+    channels_last: bool = True
+    parallel: str = "ddp"           # ddp | syncbn | dp | none
+    bucket_cap_mb: float = 25.0
+    first_bucket_mb: float = 1.0
+    lr: float = 0.1
+    momentum: float = 0.9
+    weight_decay: float = 1e-4
+    seed: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+@dataclass
+class TrainState:
+    cfg: StepConfig
+    model: nn.Module
+    wrapped: nn.Module
+    optimizer: torch.optim.Optimizer
+    step: Callable[[], torch.Tensor]
+    images: torch.Tensor
+    labels: torch.Tensor
+
+
+def synthetic_batch(cfg: StepConfig, device: torch.device, generator_seed: int = 1234):
+    (c, h, w), ncls = INPUT_SHAPES[cfg.model]
+    if cfg.image_size:
+        h = w = cfg.image_size
+    ncls = cfg.num_classes or ncls
+    g = torch.Generator(device="cpu").manual_seed(generator_seed)
+    x = torch.randn(cfg.batch_size, c, h, w, generator=g).to(device=device, dtype=cfg.dtype)
+    if cfg.channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, ncls, (cfg.batch_size,), generator=g).to(device)
+    return x, y
+
+
+def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
+    from ..parallel.distributed import DistributedDataParallel
+    from ..parallel.sync_batchnorm import SyncBatchNorm
+
+    torch.manual_seed(cfg.seed)
+    kw = {}
+    if cfg.num_classes:
+        kw["num_classes"] = cfg.num_classes
+    if cfg.image_size and cfg.model.startswith("vit"):
+        kw["image_size"] = cfg.image_size
+    model = build_model(cfg.model, **kw)
+    if cfg.parallel == "syncbn":
+        model = SyncBatchNorm.convert_sync_batchnorm(model)
+    model = model.to(device)
+    if cfg.channels_last:
+        model = model.to(memory_format=torch.channels_last)
+    if cfg.dtype != torch.float32:
+        cast_model(model, cfg.dtype)
+    x, y = synthetic_batch(cfg, device)
+
+    if cfg.parallel in ("ddp", "syncbn"):
+        wrapped = DistributedDataParallel(model, bucket_cap_mb=cfg.bucket_cap_mb,
+                                          first_bucket_mb=cfg.first_bucket_mb,
+                                          flat_parameters=True)
+        opt = FlatSGD(wrapped, lr=cfg.lr, momentum=cfg.momentum, weight_decay=cfg.weight_decay)
+
+        def step() -> torch.Tensor:
+            out = wrapped(x)
+            loss = F.cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+            return loss
+    elif cfg.parallel == "dp":
+        from ..parallel.data_parallel import DataParallel
+        wrapped = DataParallel(model)
+        opt = torch.optim.SGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
+                              weight_decay=cfg.weight_decay, foreach=True)
+
+        def step() -> torch.Tensor:
+            out = wrapped(x)
+            loss = F.cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            return loss
+    else:
+        wrapped = model
+        opt = torch.optim.SGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
+                              weight_decay=cfg.weight_decay, foreach=True)
+
+        def step() -> torch.Tensor:
+            out = model(x)
+            loss = F.cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            return loss
+
+    return TrainState(cfg, model, wrapped, opt, step, x, y)

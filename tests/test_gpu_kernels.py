@@ -1,0 +1,145 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32/fp64 reference.
+
+Runs on the MI355X box (``pytest -m gpu``).  The native extension MUST be the
+code path: every test asserts the op went through ``_C``.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd import _native
+from distributed_model_parallel_amd.ops import batchnorm as bn
+from distributed_model_parallel_amd.ops import flat as flatops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _C():
+    return _native.require("gpu tests")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(8, 64, 14, 14), (3, 24, 9, 7), (2, 2048, 7, 7), (4, 4096, 2, 2),
+                                   (64, 96)])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_bn_act_forward_backward(dtype, shape, relu, res):
+    torch.manual_seed(0)
+    C = shape[1]
+    x = (torch.randn(shape, device=DEV) * 2 + 0.5).to(dtype)
+    if x.dim() == 4:
+        x = x.contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x) if res else None
+    w = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    rm2, rv2 = rm.clone(), rv.clone()
+    xr = x.detach().float().requires_grad_()
+    wr = w.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    x1 = x.detach().requires_grad_()
+    w1 = w.clone().requires_grad_()
+    b1 = b.clone().requires_grad_()
+    r1 = r.detach().requires_grad_() if res else None
+    before = bn.stats()["native_fwd"]
+    y = bn.batch_norm_act(x1, rm, rv, w1, b1, True, 0.1, 1e-5, relu=relu, residual=r1)
+    assert bn.stats()["native_fwd"] == before + 1, "HIP BN kernel not used"
+    yr = bn.reference_bn_act(xr, rm2, rv2, wr, br, True, 0.1, 1e-5, relu=relu, residual=rr)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    torch.testing.assert_close(rm, rm2, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(rv, rv2, atol=1e-3, rtol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    gt = 5e-2 if dtype == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(x1.grad.float(), xr.grad, atol=gt, rtol=gt)
+    torch.testing.assert_close(w1.grad, wr.grad, atol=gt * 10, rtol=gt)
+    torch.testing.assert_close(b1.grad, br.grad, atol=gt * 10, rtol=gt)
+    if res:
+        torch.testing.assert_close(r1.grad.float(), rr.grad, atol=gt, rtol=gt)
+
+
+def test_bn_eval_mode():
+    C = 64
+    x = torch.randn(4, C, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)
+    rm = torch.randn(C, device=DEV)
+    rv = torch.rand(C, device=DEV) + 0.5
+    w = torch.rand(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    y = bn.batch_norm_act(x, rm, rv, w, b, False, 0.1, 1e-5, relu=True)
+    yr = F.relu(F.batch_norm(x, rm, rv, w, b, False, 0.1, 1e-5))
+    torch.testing.assert_close(y, yr, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("gdtype,pdtype", [(torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32)])
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_flat_sgd_matches_torch(gdtype, pdtype, nesterov):
+    n = 1000 * 8
+    torch.manual_seed(1)
+    p32 = torch.randn(n, device=DEV)
+    ref = p32.clone().requires_grad_()
+    opt = torch.optim.SGD([ref], lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=nesterov)
+    master = p32.clone() if pdtype == torch.bfloat16 else None
+    param = p32.to(pdtype)
+    mom = torch.zeros(n, device=DEV)
+    for step in range(3):
+        g = torch.randn(n, device=DEV).to(gdtype)
+        ref.grad = g.float()
+        opt.step()
+        _C().sgd_flat_step(master, mom, g, param, 0.1, 1e-4, 0.9, 0.0, nesterov, 1.0, step == 0)
+    got = master if master is not None else param
+    torch.testing.assert_close(got, ref.detach(), atol=1e-5, rtol=1e-5)
+    if pdtype == torch.bfloat16:
+        torch.testing.assert_close(param.float(), ref.detach(), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.int64])
+def test_multi_copy_flatten_roundtrip(dtype):
+    shapes = [(3,), (17, 5), (64, 3, 3, 3), (1,), (1000, 7)]
+    ts = [torch.randint(-100, 100, s, device=DEV).to(dtype) for s in shapes]
+    flat = flatops.flatten(ts)
+    outs = [torch.empty_like(t) for t in ts]
+    flatops.unflatten_into(flat, outs)
+    for a, b in zip(ts, outs):
+        assert torch.equal(a, b)
+
+
+def test_multi_copy_channels_last():
+    t = torch.randn(8, 16, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)
+    flat = flatops.flatten([t])
+    out = torch.empty_like(t)
+    flatops.unflatten_into(flat, [out])
+    assert torch.equal(out, t)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k", [1, 2, 5, 8])
+def test_reduce_add(dtype, k):
+    n = 10007
+    ins = [torch.randn(n, device=DEV).to(dtype) for _ in range(k)]
+    out = torch.empty(n, device=DEV, dtype=dtype)
+    _C().reduce_add_into(ins, out)
+    ref = torch.stack([i.float() for i in ins]).sum(0)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("dim", [0, 1, 2])
+def test_gather_slabs(dim):
+    from distributed_model_parallel_amd.parallel import comm_ops
+    parts = [torch.randn(5, 7, 9, device=DEV), torch.randn(5, 7, 9, device=DEV),
+             torch.randn(5, 7, 9, device=DEV)]
+    if dim == 0:
+        parts[1] = torch.randn(3, 7, 9, device=DEV)
+    out = comm_ops.gather_tensors(parts, "cuda:0", dim)
+    assert torch.equal(out, torch.cat(parts, dim))
+
+
+def test_gather_slabs_large_aligned():
+    from distributed_model_parallel_amd.parallel import comm_ops
+    parts = [torch.randn(300, 1000, device=DEV).bfloat16() for _ in range(4)]
+    assert torch.equal(comm_ops.gather_tensors(parts, "cuda:0", 0), torch.cat(parts, 0))
+    assert torch.equal(comm_ops.gather_tensors(parts, "cuda:0", 1), torch.cat(parts, 1))
