@@ -50,6 +50,7 @@ def main() -> int:
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--miopen-benchmark", type=int, default=int(os.environ.get("DMP_MIOPEN_BENCHMARK", "0")))
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
     args = ap.parse_args()
 
     env = init_distributed()
@@ -66,11 +67,12 @@ def main() -> int:
 
     t_warm0 = time.time()
     for i in range(args.warmup):
+        ts = time.perf_counter()
         loss = st.step()
-        if i == 0 and env.is_main:
+        if (i == 0 or args.trace_steps) and env.is_main:
             torch.cuda.synchronize() if dev.type == "cuda" else None
-            print(f"[bench] first step done in {time.time() - t_warm0:.1f}s loss={loss.item():.4f}",
-                  file=sys.stderr, flush=True)
+            print(f"[bench] warmup step {i} {1e3 * (time.perf_counter() - ts):.1f} ms "
+                  f"(t={time.time() - t_warm0:.1f}s) loss={loss.item():.4f}", file=sys.stderr, flush=True)
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()

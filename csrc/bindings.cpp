@@ -7,17 +7,20 @@
 namespace dmp {
 // batchnorm.hip
 at::Tensor bn_local_moments(const at::Tensor& x, int64_t C);
-std::vector<at::Tensor> bn_forward_finalize(const at::Tensor& sums, int64_t C,
-                                            const c10::optional<at::Tensor>& weight,
-                                            const c10::optional<at::Tensor>& bias,
-                                            const c10::optional<at::Tensor>& running_mean,
-                                            const c10::optional<at::Tensor>& running_var,
-                                            double momentum, double eps);
-std::vector<at::Tensor> bn_eval_coeffs(const at::Tensor& running_mean, const at::Tensor& running_var,
-                                       const c10::optional<at::Tensor>& weight,
-                                       const c10::optional<at::Tensor>& bias, double eps);
-at::Tensor bn_apply(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift,
-                    const c10::optional<at::Tensor>& residual, bool relu, int64_t C);
+std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& sums,
+                                         const c10::optional<at::Tensor>& weight,
+                                         const c10::optional<at::Tensor>& bias,
+                                         const c10::optional<at::Tensor>& running_mean,
+                                         const c10::optional<at::Tensor>& running_var,
+                                         double momentum, double eps,
+                                         const c10::optional<at::Tensor>& residual, bool relu,
+                                         int64_t C);
+std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& running_mean,
+                                      const at::Tensor& running_var,
+                                      const c10::optional<at::Tensor>& weight,
+                                      const c10::optional<at::Tensor>& bias, double eps,
+                                      const c10::optional<at::Tensor>& residual, bool relu,
+                                      int64_t C);
 at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                                const c10::optional<at::Tensor>& y, const at::Tensor& mean,
                                bool relu, int64_t C);
@@ -46,9 +49,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- batch norm ----
   m.def("bn_local_moments", &dmp::bn_local_moments);
-  m.def("bn_forward_finalize", &dmp::bn_forward_finalize);
-  m.def("bn_eval_coeffs", &dmp::bn_eval_coeffs);
-  m.def("bn_apply", &dmp::bn_apply);
+  m.def("bn_forward_apply", &dmp::bn_forward_apply);
+  m.def("bn_eval_apply", &dmp::bn_eval_apply);
   m.def("bn_backward_moments", &dmp::bn_backward_moments);
   m.def("bn_backward_apply", &dmp::bn_backward_apply);
 

@@ -76,11 +76,33 @@ def local_moments(x2: torch.Tensor, native: bool) -> torch.Tensor:
     return torch.cat([xd.sum(0), (xd * xd).sum(0), xd.new_tensor([float(x2.shape[0])])])
 
 
-def forward_finalize(sums, weight, bias, rm, rv, momentum, eps, native):
-    c = (sums.numel() - 1) // 2
+def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, native):
+    """Training-mode normalise from (global) moments; updates running stats.
+
+    Returns (y, mean, invstd)."""
+    c = x2.shape[1]
     if native:
-        return _native.require("bn").bn_forward_finalize(sums, c, weight, bias, rm, rv,
-                                                          float(momentum), float(eps))
+        return _native.require("bn").bn_forward_apply(x2, sums, weight, bias, rm, rv,
+                                                       float(momentum), float(eps), res2, relu, c)
+    mean, invstd, scale, shift = _finalize_torch(sums, weight, bias, rm, rv, momentum, eps)
+    return [_apply_torch(x2, scale, shift, res2, relu), mean, invstd]
+
+
+def eval_apply(x2, rm, rv, weight, bias, eps, res2, relu, native):
+    c = x2.shape[1]
+    if native:
+        return _native.require("bn").bn_eval_apply(x2, rm, rv, weight, bias, float(eps), res2,
+                                                    relu, c)
+    invstd = torch.rsqrt(rv.float() + eps)
+    w = weight.float() if weight is not None else torch.ones_like(invstd)
+    b = bias.float() if bias is not None else torch.zeros_like(invstd)
+    scale = w * invstd
+    shift = b - rm.float() * scale
+    return [_apply_torch(x2, scale, shift, res2, relu), rm.float(), invstd]
+
+
+def _finalize_torch(sums, weight, bias, rm, rv, momentum, eps):
+    c = (sums.numel() - 1) // 2
     count = sums[2 * c]
     mean = sums[:c] / count
     var = (sums[c:2 * c] / count - mean * mean).clamp_min(0)
@@ -96,20 +118,7 @@ def forward_finalize(sums, weight, bias, rm, rv, momentum, eps, native):
     return [mean.float(), invstd, scale, shift]
 
 
-def eval_coeffs(rm, rv, weight, bias, eps, native):
-    if native:
-        return _native.require("bn").bn_eval_coeffs(rm.float(), rv.float(), weight, bias, float(eps))
-    invstd = torch.rsqrt(rv.float() + eps)
-    w = weight.float() if weight is not None else torch.ones_like(invstd)
-    b = bias.float() if bias is not None else torch.zeros_like(invstd)
-    scale = w * invstd
-    return [rm.float(), invstd, scale, b - rm.float() * scale]
-
-
-def apply(x2, scale, shift, res2, relu, native):
-    c = x2.shape[1]
-    if native:
-        return _native.require("bn").bn_apply(x2, scale, shift, res2, relu, c)
+def _apply_torch(x2, scale, shift, res2, relu):
     y = x2.float() * scale + shift
     if res2 is not None:
         y = y + res2.float()
@@ -174,8 +183,8 @@ class _BatchNormActFn(torch.autograd.Function):
             count = sums[-1:]
             upd_rm = running_mean if (running_mean is not None and running_mean.dtype == torch.float32) else None
             upd_rv = running_var if upd_rm is not None else None
-            mean, invstd, scale, shift = forward_finalize(sums, w32, b32, upd_rm, upd_rv,
-                                                          momentum, eps, native)
+            y2, mean, invstd = forward_apply(x2, sums, w32, b32, upd_rm, upd_rv, momentum, eps,
+                                             res2, relu, native)
             if running_mean is not None and upd_rm is None:  # low-precision buffers
                 c = x2.shape[1]
                 n = sums[2 * c]
@@ -184,8 +193,8 @@ class _BatchNormActFn(torch.autograd.Function):
                 running_var.mul_(1 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
         else:
             count = torch.full((1,), float(x2.shape[0]), dtype=torch.float64, device=x2.device)
-            mean, invstd, scale, shift = eval_coeffs(running_mean, running_var, w32, b32, eps, native)
-        y2 = apply(x2, scale, shift, res2, relu, native)
+            y2, mean, invstd = eval_apply(x2, running_mean, running_var, w32, b32, eps, res2, relu,
+                                          native)
         ctx.save_for_backward(x2, y2 if relu else None, w32, mean, invstd, count)
         ctx.meta = (native, training, relu, residual is not None, back,
                     weight is not None, bias is not None, reduce_grads,
@@ -201,6 +210,7 @@ class _BatchNormActFn(torch.autograd.Function):
         sums = backward_moments(dy2, x2, y2, mean, relu, native)
         local_sums = sums
         if training and reduce_grads is not None:
+            local_sums = sums.clone()  # the reducer works in place
             sums = reduce_grads(sums)
         dx2, dw, db, dres2 = backward_apply(dy2, x2, y2, sums, count, w32, mean, invstd, training,
                                             relu, has_res, native)

@@ -194,8 +194,10 @@ class DistributedDataParallel(nn.Module):
     def _verify_params_across_ranks(self) -> None:
         if self.world_size == 1:
             return
-        sig = torch.tensor([len(self._params)] + [hash((tuple(p.shape), str(p.dtype))) % (2 ** 31)
-                                                   for p in self._params], dtype=torch.float64)
+        import zlib
+        sig = torch.tensor([len(self._params)] + [
+            zlib.crc32(repr((tuple(p.shape), str(p.dtype), i)).encode()) % (2 ** 24)
+            for i, p in enumerate(self._params)], dtype=torch.float64)
         s = torch.tensor([sig.sum().item(), float(len(self._params))], dtype=torch.float64,
                          device=self.device if self.device.type == "cuda" else "cpu")
         mx = s.clone()

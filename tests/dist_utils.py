@@ -1,0 +1,57 @@
+"""Spawn a local gloo world (127.0.0.1) and collect per-rank results."""
+from __future__ import annotations
+
+import os
+import socket
+import tempfile
+import traceback
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _entry(rank, world, port, fn, args, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        res = fn(rank, world, *args)
+        torch.save({"ok": True, "res": res}, os.path.join(outdir, f"r{rank}.pt"))
+    except Exception:  # noqa: BLE001
+        torch.save({"ok": False, "err": traceback.format_exc()}, os.path.join(outdir, f"r{rank}.pt"))
+        raise
+    finally:
+        if dist.is_initialized():
+            from distributed_model_parallel_amd.comm.rccl import reset_default_communicator
+            reset_default_communicator()
+            dist.destroy_process_group()
+
+
+def run_world(fn, world: int, *args):
+    """Run fn(rank, world, *args) in `world` gloo processes; return list of results."""
+    with tempfile.TemporaryDirectory() as d:
+        port = free_port()
+        try:
+            mp.spawn(_entry, args=(world, port, fn, args, d), nprocs=world, join=True)
+        except Exception:
+            errs = []
+            for r in range(world):
+                p = os.path.join(d, f"r{r}.pt")
+                if os.path.exists(p):
+                    o = torch.load(p, weights_only=False)
+                    if not o["ok"]:
+                        errs.append(f"rank {r}:\n{o['err']}")
+            raise AssertionError("\n".join(errs) or "worker failed")
+        out = []
+        for r in range(world):
+            o = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
+            out.append(o["res"])
+        return out

@@ -1,0 +1,152 @@
+"""DDP oracle (SURVEY.md §4 layer 2): W ranks x per-rank batch b must match one
+process on batch W*b with mean-reduced gradients, for the native C++ reducer
+over gloo (CPU).  Also covers no_sync, find_unused_parameters, bucket rebuild,
+flat parameters + FlatSGD, comm hooks and module-state broadcast."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from tests.dist_utils import run_world
+
+WORLD = 2
+B = 4
+
+
+class Net(nn.Module):
+    def __init__(self, unused_branch=False):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 8, 3, padding=1)
+        self.fc1 = nn.Linear(8 * 4 * 4, 32)
+        self.fc2 = nn.Linear(32, 5)
+        self.unused = nn.Linear(32, 5) if unused_branch else None
+
+    def forward(self, x):
+        x = F.relu(self.conv(x))
+        x = F.adaptive_avg_pool2d(x, 4).flatten(1)
+        return self.fc2(F.relu(self.fc1(x)))
+
+
+def _data(steps):
+    g = torch.Generator().manual_seed(123)
+    xs = [torch.randn(WORLD * B, 3, 8, 8, generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 5, (WORLD * B,), generator=g) for _ in range(steps)]
+    return xs, ys
+
+
+def _reference(steps, flat_opt=False, accumulate=1):
+    torch.manual_seed(0)
+    m = Net()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    xs, ys = _data(steps * accumulate)
+    for s in range(steps):
+        opt.zero_grad()
+        for a in range(accumulate):
+            i = s * accumulate + a
+            loss = F.cross_entropy(m(xs[i]), ys[i]) / accumulate
+            loss.backward()
+        opt.step()
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def _ddp_worker(rank, world, steps, flat, find_unused, accumulate, hook, bucket_mb):
+    from distributed_model_parallel_amd.ops.optim import FlatSGD
+    from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel, allreduce_hook
+    torch.manual_seed(rank + 17)  # different init per rank: DDP must broadcast rank 0's
+    if rank == 0:
+        torch.manual_seed(0)
+    m = Net(unused_branch=find_unused)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=bucket_mb, first_bucket_mb=bucket_mb / 4,
+                                  find_unused_parameters=find_unused, flat_parameters=flat)
+    if hook:
+        import torch.distributed as dist
+        ddp.register_comm_hook(None, allreduce_hook(dist.group.WORLD))
+    if flat:
+        opt = FlatSGD(ddp, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    else:
+        opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    xs, ys = _data(steps * accumulate)
+    sl = slice(rank * B, (rank + 1) * B)
+    nbuckets = len(ddp.reducer.buckets())
+    for s in range(steps):
+        opt.zero_grad()
+        for a in range(accumulate):
+            i = s * accumulate + a
+            last = a == accumulate - 1
+            ctx = ddp.no_sync() if not last else _Null()
+            with ctx:
+                loss = F.cross_entropy(ddp(xs[i][sl]), ys[i][sl]) / accumulate
+                loss.backward()
+        opt.step()
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items() if not k.startswith("unused")}
+    return {"sd": sd, "nbuckets": nbuckets, "unused": list(ddp.reducer.unused_params()),
+            "buckets": ddp.reducer.buckets()}
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+@pytest.mark.parametrize("flat", [False, True])
+def test_ddp_matches_single_process(flat):
+    steps = 3
+    ref = _reference(steps)
+    res = run_world(_ddp_worker, WORLD, steps, flat, False, 1, False, 0.002)
+    assert res[0]["nbuckets"] > 1, "test should exercise several buckets"
+    for r in res:
+        for k, v in ref.items():
+            torch.testing.assert_close(r["sd"][k], v, atol=2e-5, rtol=1e-5, msg=k)
+    # rebuilt buckets are identical on every rank
+    assert res[0]["buckets"] == res[1]["buckets"]
+
+
+def test_ddp_no_sync_accumulation():
+    ref = _reference(2, accumulate=2)
+    res = run_world(_ddp_worker, WORLD, 2, False, False, 2, False, 0.002)
+    for k, v in ref.items():
+        torch.testing.assert_close(res[0]["sd"][k], v, atol=2e-5, rtol=1e-5, msg=k)
+
+
+def test_ddp_find_unused_parameters():
+    ref = _reference(2)
+    res = run_world(_ddp_worker, WORLD, 2, True, True, 1, False, 0.002)
+    assert len(res[0]["unused"]) == 2  # unused.weight, unused.bias
+    for k, v in ref.items():
+        torch.testing.assert_close(res[1]["sd"][k], v, atol=2e-5, rtol=1e-5, msg=k)
+
+
+def test_ddp_comm_hook():
+    ref = _reference(2)
+    res = run_world(_ddp_worker, WORLD, 2, False, False, 1, True, 25.0)
+    for k, v in ref.items():
+        torch.testing.assert_close(res[0]["sd"][k], v, atol=2e-5, rtol=1e-5, msg=k)
+
+
+def _unused_without_flag(rank, world):
+    from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
+    m = Net(unused_branch=True)
+    ddp = DistributedDataParallel(m)
+    try:
+        ddp(torch.randn(2, 3, 8, 8)).sum().backward()
+    except RuntimeError as e:
+        return str(e)
+    return ""
+
+
+def test_ddp_unused_without_flag_raises():
+    res = run_world(_unused_without_flag, WORLD)
+    assert "find_unused_parameters" in res[0]
+
+
+def test_bucket_assignment_caps_and_order():
+    from distributed_model_parallel_amd import _native
+    C = _native.require("bucket test")
+    ps = [torch.zeros(1000, requires_grad=True) for _ in range(10)]  # 4000 B each (+pad)
+    b = C.compute_bucket_assignment(ps, 10000, 4000)
+    assert b[0] == [9]
+    assert sorted(i for bb in b for i in bb) == list(range(10))
+    assert all(len(bb) <= 3 for bb in b)
