@@ -48,11 +48,14 @@ __host__ __device__ inline Layout make_layout(int C, int vec) {
   return l;
 }
 
-// Combine the rpi row-lanes of each channel through LDS and atomically add
-// the block's totals (fp64) into out[c] and out[C + c].
+// Combine the rpi row-lanes of each channel through LDS and write the block's
+// totals to its partial row: part[blockIdx.x][c] (sum) and part[rb + blockIdx.x][c].
+// (Same-address fp64 atomics from ~1000 blocks serialise at ~100 ns each at
+// the memory side -- measured 115 us per call -- so the cross-block sum is a
+// separate wide, deterministic reduce kernel instead.)
 template <int VEC>
-__device__ __forceinline__ void block_combine_atomic(const float (&s)[VEC], const float (&q)[VEC],
-                                                     const Layout& L, int C, double* out) {
+__device__ __forceinline__ void block_combine_store(const float (&s)[VEC], const float (&q)[VEC],
+                                                    const Layout& L, int C, float* part) {
   __shared__ float lds_s[kThreads * VEC];
   __shared__ float lds_q[kThreads * VEC];
   const int tid = threadIdx.x;
@@ -72,18 +75,62 @@ __device__ __forceinline__ void block_combine_atomic(const float (&s)[VEC], cons
       ss += lds_s[e * kThreads + rr * L.tc + c_l];
       qq += lds_q[e * kThreads + rr * L.tc + c_l];
     }
-    atomicAdd(out + cg, (double)ss);
-    atomicAdd(out + C + cg, (double)qq);
+    part[(int64_t)blockIdx.x * C + cg] = ss;
+    part[(int64_t)(gridDim.x + blockIdx.x) * C + cg] = qq;
   }
 }
 
+// Deterministic fp64 reduction of the [2][rb][C] partials into sums[0:2C];
+// one 1024-thread block per 32 channels (32 row-groups x 32 channels), so each
+// lane sums only rb/32 partial rows.  Writes sums[2C] = count when count >= 0.
+constexpr int kRedCh = 32, kRedGroups = 32;
+__global__ __launch_bounds__(1024) void bn_reduce_partials_kernel(const float* __restrict__ part,
+                                                                  int rb, int C,
+                                                                  double* __restrict__ sums,
+                                                                  double count) {
+  const int cl = threadIdx.x % kRedCh, g = threadIdx.x / kRedCh;
+  const int c = blockIdx.x * kRedCh + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    const float* pa = part + c;
+    const float* pb = part + (int64_t)rb * C + c;
+    int i = g;
+    for (; i + kRedGroups < rb; i += 2 * kRedGroups) {
+      const float a0 = pa[(int64_t)i * C], a1 = pa[(int64_t)(i + kRedGroups) * C];
+      const float b0 = pb[(int64_t)i * C], b1 = pb[(int64_t)(i + kRedGroups) * C];
+      a += (double)a0 + (double)a1;
+      b += (double)b0 + (double)b1;
+    }
+    if (i < rb) {
+      a += (double)pa[(int64_t)i * C];
+      b += (double)pb[(int64_t)i * C];
+    }
+  }
+  __shared__ double la[1024], lb[1024];
+  la[threadIdx.x] = a;
+  lb[threadIdx.x] = b;
+  __syncthreads();
+  for (int s = kRedGroups / 2; s > 0; s >>= 1) {
+    if (g < s) {
+      la[threadIdx.x] += la[threadIdx.x + s * kRedCh];
+      lb[threadIdx.x] += lb[threadIdx.x + s * kRedCh];
+    }
+    __syncthreads();
+  }
+  if (g == 0 && c < C) {
+    sums[c] = la[threadIdx.x];
+    sums[C + c] = lb[threadIdx.x];
+  }
+  if (count >= 0.0 && blockIdx.x == 0 && threadIdx.x == 0) sums[2 * C] = count;
+}
+
 // -------------------------------------------------------------------------
-// Forward moments: sums[c] += sum x, sums[C+c] += sum x^2, sums[2C] = rows.
-// grid = (row_blocks, channel_chunks)
+// Forward moments, phase 1: per-block partial sum / sum of squares.
+// grid = (row_blocks, channel_chunks); 4 rows in flight per lane.
 // -------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_moments_kernel(
-    const T* __restrict__ x, int64_t M, int C, int64_t rows_per_block, double* __restrict__ sums) {
+    const T* __restrict__ x, int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -98,26 +145,29 @@ __global__ __launch_bounds__(kThreads) void bn_moments_kernel(
   for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; }
   if (active) {
     const T* p = x + (int64_t)cvec * VEC;
+    const int64_t st = (int64_t)L.rpi * C;
     int64_t r = r0 + lr;
-    for (; r + L.rpi < r1; r += 2 * L.rpi) {
-      float a[VEC], b[VEC];
-      Vec16<T>::load(p + r * C, a);
-      Vec16<T>::load(p + (r + L.rpi) * C, b);
+    for (; r + 3 * L.rpi < r1; r += 4 * L.rpi) {
+      float a[VEC], b[VEC], c[VEC], d[VEC];
+      const T* pr = p + r * C;
+      Vec16<T>::load(pr, a);
+      Vec16<T>::load(pr + st, b);
+      Vec16<T>::load(pr + 2 * st, c);
+      Vec16<T>::load(pr + 3 * st, d);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
-        s[i] += a[i] + b[i];
-        q[i] = fmaf(a[i], a[i], fmaf(b[i], b[i], q[i]));
+        s[i] += (a[i] + b[i]) + (c[i] + d[i]);
+        q[i] = fmaf(a[i], a[i], fmaf(b[i], b[i], fmaf(c[i], c[i], fmaf(d[i], d[i], q[i]))));
       }
     }
-    if (r < r1) {
+    for (; r < r1; r += L.rpi) {
       float a[VEC];
       Vec16<T>::load(p + r * C, a);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) { s[i] += a[i]; q[i] = fmaf(a[i], a[i], q[i]); }
     }
   }
-  block_combine_atomic<VEC>(s, q, L, C, sums);
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) sums[2 * C] = (double)M;
+  block_combine_store<VEC>(s, q, L, C, part);
 }
 
 // Per-channel forward coefficients from (possibly all-reduced) moments.
@@ -222,13 +272,13 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
 }
 
 // -------------------------------------------------------------------------
-// Backward pass 1: sums[c] += sum dz, sums[C+c] += sum dz*(x-mean).
+// Backward pass 1 (per-block partials of sum dz and sum dz*(x-mean)).
 // -------------------------------------------------------------------------
 template <typename T, bool RELU>
 __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block,
-    double* __restrict__ sums) {
+    float* __restrict__ part) {
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -262,7 +312,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
       }
     }
   }
-  block_combine_atomic<VEC>(s, q, L, C, sums);
+  block_combine_store<VEC>(s, q, L, C, part);
 }
 
 // -------------------------------------------------------------------------
@@ -380,14 +430,18 @@ at::Tensor bn_local_moments(const at::Tensor& x, int64_t C) {
   check_input(x, C, "x");
   const int64_t M = x.numel() / C;
   auto stream = at::hip::getCurrentHIPStream();
-  auto sums = at::zeros({2 * C + 1}, x.options().dtype(at::kDouble));
-  if (M == 0) return sums;
+  if (M == 0) return at::zeros({2 * C + 1}, x.options().dtype(at::kDouble));
+  auto sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
   Grid g = plan(M, (int)C, vec_of(x));
+  auto part = at::empty({2, (int64_t)g.grid.x, C}, x.options().dtype(at::kFloat));
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL(bn_moments_kernel<T>, g.grid, dim3(kThreads), 0, stream, ptr<T>(x), M,
-                       (int)C, g.rows_per_block, sums.data_ptr<double>());
+                       (int)C, g.rows_per_block, part.data_ptr<float>());
   });
+  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh), dim3(1024), 0,
+                     stream, part.data_ptr<float>(), (int)g.grid.x, (int)C,
+                     sums.data_ptr<double>(), (double)M);
   return sums;
 }
 
@@ -473,22 +527,26 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
   check_input(x, C, "x");
   const int64_t M = x.numel() / C;
   auto stream = at::hip::getCurrentHIPStream();
-  auto sums = at::zeros({2 * C}, x.options().dtype(at::kDouble));
-  if (M == 0) return sums;
+  if (M == 0) return at::zeros({2 * C}, x.options().dtype(at::kDouble));
+  auto sums = at::empty({2 * C}, x.options().dtype(at::kDouble));
   Grid g = plan(M, (int)C, vec_of(x));
+  auto part = at::empty({2, (int64_t)g.grid.x, C}, x.options().dtype(at::kFloat));
+  float* pp = part.data_ptr<float>();
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
     if (relu) {
       TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
       hipLaunchKernelGGL((bn_bwd_moments_kernel<T, true>), g.grid, dim3(kThreads), 0, stream,
                          ptr<T>(dy), ptr<T>(x), ptr<T>(*y), mean.data_ptr<float>(), M, (int)C,
-                         g.rows_per_block, sums.data_ptr<double>());
+                         g.rows_per_block, pp);
     } else {
       hipLaunchKernelGGL((bn_bwd_moments_kernel<T, false>), g.grid, dim3(kThreads), 0, stream,
                          ptr<T>(dy), ptr<T>(x), (const T*)nullptr, mean.data_ptr<float>(), M,
-                         (int)C, g.rows_per_block, sums.data_ptr<double>());
+                         (int)C, g.rows_per_block, pp);
     }
   });
+  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh), dim3(1024), 0,
+                     stream, pp, (int)g.grid.x, (int)C, sums.data_ptr<double>(), -1.0);
   return sums;
 }
 
@@ -503,7 +561,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
   check_input(dy, C, "grad");
   const int64_t M = x.numel() / C;
   auto stream = at::hip::getCurrentHIPStream();
-  auto dwb = at::zeros({2, C}, x.options().dtype(at::kFloat));
+  auto dwb = at::empty({2, C}, x.options().dtype(at::kFloat));
   auto dx = at::empty_like(x);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x);

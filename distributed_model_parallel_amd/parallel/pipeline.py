@@ -1,0 +1,507 @@
+"""Inter-layer model parallelism (pipeline) over point-to-point RCCL / gloo.
+
+Reference capability: MobileNetV2 split across 4 GPU
+processes, activations forwarded and gradients returned through autograd
+functions that wrap blocking ``dist.send/recv`` (``distributed_layers.py:7-62``,
+loops in ``utils.py:34-210``, partition at ``model_parallel.py:101-104,
+129-130,143-145``).  What changes here, MI355X-first:
+
+* **Any world size.**  :func:`balanced_partition` cuts a model's atom
+  sequence (``model.as_sequential()``) into contiguous stages minimising the
+  largest stage cost (FLOPs measured with hooks, or parameters), instead of
+  the reference's hard-coded 4-way slicing (defect 2); the stem keeps its ReLU
+  (defect 3).
+* **No host round-trips.**  The reference sends ``ndim`` and ``shape`` as fp32
+  tensors before every payload and receives them with two device->host syncs
+  (``distributed_layers.py:40-47``).  Here shapes are a static contract
+  computed once per micro-batch size by a probe (:meth:`Pipeline._probe`), so
+  every hop moves only the payload, in the activation dtype (bf16 works;
+  reference defect 8 forced fp32 via ``torch.rand`` buffers).
+* **Micro-batching.**  ``schedule="naive"`` reproduces the reference (one
+  micro-batch, fully serialised); ``"gpipe"`` runs all forwards then all
+  backwards over M micro-batches; ``"1f1b"`` (PipeDream-flush) interleaves
+  one forward / one backward in steady state with batched send+recv pairs
+  (one RCCL group each) so that stages overlap and activation memory is
+  bounded by the stage depth.
+* **Loss placement.**  ``loss_on="last"`` ships the targets to the last stage
+  once per batch and returns [loss, top1, top5] to rank 0 (3 floats);
+  ``loss_on="first"`` keeps the reference's ring (logits back to rank 0, loss
+  there, dlogits to the last stage; gpipe/naive only).
+* **Transport.**  :class:`~..comm.rccl.Communicator` -- RCCL send/recv on its
+  own HIP stream on GPU (ordered with events, no blocking), gloo on CPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..comm.rccl import Communicator
+
+
+# --------------------------------------------------------------------------- #
+# Partitioning
+# --------------------------------------------------------------------------- #
+def atom_costs(atoms: nn.Sequential, sample: torch.Tensor, kind: str = "flops") -> List[float]:
+    """Per-atom cost: forward FLOPs of conv/linear layers (measured on `sample`) or params."""
+    if kind == "params":
+        return [float(sum(p.numel() for p in a.parameters())) or 1.0 for a in atoms]
+    costs: List[float] = []
+    flops = [0.0]
+
+    def hook(mod, inp, out):
+        if isinstance(mod, nn.Conv2d):
+            k = mod.weight.numel() // mod.out_channels  # cin/groups * kh * kw
+            flops[0] += 2.0 * out.numel() * k
+        elif isinstance(mod, nn.Linear):
+            flops[0] += 2.0 * out.numel() * mod.in_features
+        else:
+            flops[0] += float(out.numel()) if isinstance(out, torch.Tensor) else 0.0
+
+    x = sample
+    with torch.no_grad():
+        was = [a.training for a in atoms]
+        for a in atoms:
+            a.eval()
+        for a in atoms:
+            hs = [m.register_forward_hook(hook) for m in a.modules()
+                  if isinstance(m, (nn.Conv2d, nn.Linear)) or len(list(m.children())) == 0]
+            flops[0] = 0.0
+            x = a(x)
+            for h in hs:
+                h.remove()
+            costs.append(max(flops[0], 1.0))
+        for a, w in zip(atoms, was):
+            a.train(w)
+    return costs
+
+
+def balanced_partition(costs: Sequence[float], stages: int) -> List[Tuple[int, int]]:
+    """Contiguous split of `costs` into `stages` non-empty ranges minimising the max sum."""
+    n = len(costs)
+    if stages > n:
+        raise ValueError(f"cannot cut {n} atoms into {stages} stages")
+    pref = [0.0]
+    for c in costs:
+        pref.append(pref[-1] + c)
+    INF = float("inf")
+    # best[k][i] = minimal max-cost splitting first i atoms into k stages
+    best = [[INF] * (n + 1) for _ in range(stages + 1)]
+    arg = [[0] * (n + 1) for _ in range(stages + 1)]
+    best[0][0] = 0.0
+    for k in range(1, stages + 1):
+        for i in range(k, n + 1):
+            for j in range(k - 1, i):
+                v = max(best[k - 1][j], pref[i] - pref[j])
+                if v < best[k][i]:
+                    best[k][i] = v
+                    arg[k][i] = j
+    bounds = []
+    i = n
+    for k in range(stages, 0, -1):
+        j = arg[k][i]
+        bounds.append((j, i))
+        i = j
+    return bounds[::-1]
+
+
+# --------------------------------------------------------------------------- #
+# P2P autograd functions (payload only; shapes are a static contract)
+# --------------------------------------------------------------------------- #
+class SendForwardRecvBackward(torch.autograd.Function):
+    """forward: send x to `peer`, return x; backward: receive dL/dx from `peer`.
+
+    Capability of the reference's ForwardSend_BackwardReceive
+    (distributed_layers.py:7-26) without the 3-message shape handshake."""
+
+    @staticmethod
+    def forward(ctx, x, comm: Communicator, peer: int):
+        ctx.comm, ctx.peer = comm, peer
+        ctx.shape, ctx.dtype, ctx.device = x.shape, x.dtype, x.device
+        comm.send(x.contiguous(), peer)
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        buf = torch.empty(ctx.shape, dtype=ctx.dtype, device=ctx.device)
+        ctx.comm.recv(buf, ctx.peer)
+        ctx.comm.wait()
+        return buf, None, None
+
+
+class RecvForwardSendBackward(torch.autograd.Function):
+    """forward: receive the activation from `peer`; backward: send dL/dx to `peer`.
+
+    Capability of the reference's generate_recv + ForwardReceive_BackwardSend
+    (distributed_layers.py:40-62)."""
+
+    @staticmethod
+    def forward(ctx, anchor, shape, dtype, comm: Communicator, peer: int):
+        ctx.comm, ctx.peer = comm, peer
+        buf = torch.empty(shape, dtype=dtype, device=anchor.device)
+        comm.recv(buf, peer)
+        comm.wait()
+        return buf
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.comm.send(g.contiguous(), ctx.peer)
+        return None, None, None, None, None
+
+
+def recv_activation(shape, dtype, device, comm: Communicator, peer: int) -> torch.Tensor:
+    anchor = torch.empty(0, device=device, requires_grad=True)
+    return RecvForwardSendBackward.apply(anchor, tuple(shape), dtype, comm, peer)
+
+
+# --------------------------------------------------------------------------- #
+# Pipeline engine
+# --------------------------------------------------------------------------- #
+@dataclass
+class StepResult:
+    loss: Optional[float]
+    top1: Optional[float]
+    top5: Optional[float]
+
+
+def _topk_correct(logits: torch.Tensor, target: torch.Tensor, ks=(1, 5)) -> List[torch.Tensor]:
+    maxk = min(max(ks), logits.shape[1])
+    pred = logits.topk(maxk, 1, True, True).indices.t()
+    correct = pred.eq(target.view(1, -1))
+    return [correct[:min(k, maxk)].reshape(-1).float().sum() for k in ks]
+
+
+class Pipeline:
+    """One pipeline stage of a model cut across `comm.size` ranks.
+
+    Every rank constructs the same full model (same seed) and keeps only its
+    slice: ``Pipeline(model.as_sequential(), comm, sample_shape=(3, 32, 32))``.
+    """
+
+    def __init__(self, atoms: nn.Sequential, comm: Communicator, sample_shape: Sequence[int],
+                 micro_batches: int = 1, schedule: str = "1f1b",
+                 loss_fn: Callable = F.cross_entropy, loss_on: str = "last",
+                 partition: Optional[List[Tuple[int, int]]] = None, balance: str = "flops",
+                 device: Optional[torch.device] = None, dtype: torch.dtype = torch.float32,
+                 channels_last: bool = False):
+        if schedule not in ("naive", "gpipe", "1f1b"):
+            raise ValueError(f"unknown schedule {schedule!r}")
+        if loss_on not in ("last", "first"):
+            raise ValueError("loss_on must be 'last' or 'first'")
+        if loss_on == "first" and schedule == "1f1b":
+            raise ValueError("loss_on='first' (reference ring) supports schedule naive/gpipe")
+        self.comm = comm
+        self.rank, self.world = comm.rank, comm.size
+        self.schedule = schedule
+        self.micro_batches = 1 if schedule == "naive" else micro_batches
+        self.loss_fn = loss_fn
+        self.loss_on = loss_on if self.world > 1 else "last"
+        self.device = torch.device(device) if device is not None else comm.device
+        self.dtype = dtype
+        self.channels_last = channels_last
+        self.sample_shape = tuple(sample_shape)
+        if partition is None:
+            costs = atom_costs(atoms, torch.zeros((2,) + self.sample_shape), balance)
+            partition = balanced_partition(costs, self.world)
+        self.partition = partition
+        self.is_first = self.rank == 0
+        self.is_last = self.rank == self.world - 1
+        self._tails = self._probe_tails(atoms)  # before our slice moves to the device
+        lo, hi = partition[self.rank]
+        self.module = nn.Sequential(*[atoms[i] for i in range(lo, hi)]).to(self.device)
+        if dtype != torch.float32:
+            from ..utils.precision import cast_model
+            cast_model(self.module, dtype)
+        if channels_last:
+            self.module = self.module.to(memory_format=torch.channels_last)
+
+    # ---- static shape contract ------------------------------------------------
+    def _probe_tails(self, atoms: nn.Sequential) -> List[Tuple[int, ...]]:
+        """Per-stage output shape without the batch dim (computed locally on CPU from the
+        full model every rank holds, so no shape message ever crosses the wire)."""
+        tails = []
+        x = torch.zeros((2,) + self.sample_shape)
+        with torch.no_grad():
+            for lo, hi in self.partition:
+                for i in range(lo, hi):
+                    a = atoms[i]
+                    was = a.training
+                    a.eval()
+                    x = a(x)
+                    a.train(was)
+                tails.append(tuple(x.shape[1:]))
+        return tails
+
+    def _in_shape(self, mb: int) -> Tuple[int, ...]:
+        return (mb,) + (self.sample_shape if self.is_first else self._tails[self.rank - 1])
+
+    def _out_shape(self, mb: int) -> Tuple[int, ...]:
+        return (mb,) + self._tails[self.rank]
+
+    # ---- comm helpers ------------------------------------------------------------
+    def _recv_fwd(self, mb: int) -> torch.Tensor:
+        x = recv_activation(self._in_shape(mb), self.dtype, self.device, self.comm, self.rank - 1)
+        return x
+
+    def _split(self, t: torch.Tensor) -> List[torch.Tensor]:
+        return list(torch.chunk(t, self.micro_batches, 0))
+
+    def _mb_sizes(self, batch: int) -> List[int]:
+        base = -(-batch // self.micro_batches)
+        sizes, left = [], batch
+        while left > 0:
+            sizes.append(min(base, left))
+            left -= sizes[-1]
+        return sizes
+
+    def _batch_size(self, inputs: Optional[torch.Tensor]) -> int:
+        """Rank 0 knows the batch; broadcast it along the pipeline (one int)."""
+        t = torch.zeros(1, dtype=torch.int64, device=self.device)
+        if self.is_first:
+            t[0] = inputs.shape[0]
+        if self.world > 1:
+            if self.is_first:
+                self.comm.send(t, 1)
+            else:
+                self.comm.recv(t, self.rank - 1)
+                self.comm.synchronize()
+                if not self.is_last:
+                    self.comm.send(t, self.rank + 1)
+        return int(t.item()) if not self.is_first else inputs.shape[0]
+
+    # ---- compute helpers -----------------------------------------------------------
+    def _prep_input(self, x: torch.Tensor) -> torch.Tensor:
+        x = x.to(self.device, self.dtype, non_blocking=True)
+        if self.channels_last and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x
+
+    def _forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.module(x)
+
+    # ---- public API -----------------------------------------------------------------
+    def train_step(self, inputs: Optional[torch.Tensor] = None,
+                   targets: Optional[torch.Tensor] = None) -> StepResult:
+        """Forward + backward of one batch (inputs/targets needed on rank 0 only).
+        Gradients accumulate in ``self.module``; step your stage optimizer after."""
+        self.module.train()
+        batch = self._batch_size(inputs)
+        sizes = self._mb_sizes(batch)
+        if self.is_first:
+            xs = list(torch.split(inputs, sizes, 0))
+            ts = list(torch.split(targets, sizes, 0))
+        else:
+            xs, ts = None, None
+        # targets to the last stage (loss_on="last")
+        tgt = None
+        if self.loss_on == "last":
+            if self.world == 1:
+                tgt = targets.to(self.device)
+            elif self.is_first:
+                self.comm.send(targets.to(self.device, torch.int64).contiguous(), self.world - 1)
+            elif self.is_last:
+                tgt = torch.empty(batch, dtype=torch.int64, device=self.device)
+                self.comm.recv(tgt, 0)
+                self.comm.wait()
+            tgt_mbs = list(torch.split(tgt, sizes, 0)) if tgt is not None else None
+        else:
+            tgt_mbs = [t.to(self.device) for t in ts] if self.is_first else None
+        stats = torch.zeros(3, dtype=torch.float64, device=self.device)
+        if self.schedule == "1f1b":
+            self._run_1f1b(xs, tgt_mbs, sizes, stats)
+        else:
+            self._run_gpipe(xs, tgt_mbs, sizes, stats)
+        return self._finish_stats(stats, batch)
+
+    def _finish_stats(self, stats: torch.Tensor, batch: int) -> StepResult:
+        holder = self.world - 1 if self.loss_on == "last" else 0
+        if self.world > 1 and holder != 0:
+            if self.is_last:
+                self.comm.send(stats, 0)
+            elif self.is_first:
+                self.comm.recv(stats, holder)
+                self.comm.synchronize()
+        if self.is_first or self.world == 1 or (self.rank == holder):
+            s = stats.tolist()
+            return StepResult(s[0], 100.0 * s[1] / batch, 100.0 * s[2] / batch)
+        return StepResult(None, None, None)
+
+    def _loss_and_stats(self, y: torch.Tensor, t: torch.Tensor, stats: torch.Tensor) -> torch.Tensor:
+        logits = y.float()
+        loss = self.loss_fn(logits, t) / self.micro_batches
+        with torch.no_grad():
+            c1, c5 = _topk_correct(logits, t)
+            stats[0] += loss.detach().double()
+            stats[1] += c1.double()
+            stats[2] += c5.double()
+        return loss
+
+    # GPipe / naive: all forwards, then all backwards ----------------------------------
+    def _run_gpipe(self, xs, tgts, sizes, stats):
+        saved = []
+        for m, mb in enumerate(sizes):
+            x = self._prep_input(xs[m]) if self.is_first else self._recv_fwd(mb)
+            y = self._forward(x)
+            if self.is_last:
+                if self.loss_on == "last":
+                    saved.append(self._loss_and_stats(y, tgts[m], stats))
+                else:  # ring: logits back to rank 0
+                    saved.append(SendForwardRecvBackward.apply(y, self.comm, 0))
+            else:
+                saved.append(SendForwardRecvBackward.apply(y, self.comm, self.rank + 1))
+            if self.is_first and self.loss_on == "first" and self.world > 1:
+                saved[-1] = (saved[-1], m)
+        if self.is_first and self.loss_on == "first" and self.world > 1:
+            # receive logits of every micro-batch from the last stage, compute loss there
+            losses = []
+            for m, mb in enumerate(sizes):
+                logits = recv_activation((mb,) + self._tails[-1], self.dtype, self.device,
+                                         self.comm, self.world - 1)
+                losses.append(self._loss_and_stats(logits, tgts[m], stats))
+            for m in range(len(sizes)):
+                losses[m].backward()  # sends dlogits to the last stage first (deadlock-free order)
+                out, _ = saved[m]
+                out.backward(torch.zeros_like(out))  # receives dL/dy from rank 1
+            return
+        for m in range(len(sizes)):
+            out = saved[m]
+            if self.is_last and self.loss_on == "last":
+                out.backward()
+            else:
+                out.backward(torch.zeros_like(out))
+
+    # 1F1B (PipeDream-flush) ------------------------------------------------------------
+    def _run_1f1b(self, xs, tgts, sizes, stats):
+        M = len(sizes)
+        S, r = self.world, self.rank
+        warm = min(S - r - 1, M)
+        queue: List[Tuple[torch.Tensor, torch.Tensor]] = []
+        fwd_i = 0
+
+        def fwd_compute(x):
+            nonlocal fwd_i
+            m = fwd_i
+            fwd_i += 1
+            y = self._forward(x)
+            if self.is_last:
+                return x, self._loss_and_stats(y, tgts[m], stats)
+            return x, y
+
+        def get_input(m):
+            if self.is_first:
+                return self._prep_input(xs[m])
+            buf = torch.empty(self._in_shape(sizes[m]), dtype=self.dtype, device=self.device)
+            self.comm.recv(buf, r - 1)
+            self.comm.wait()
+            return buf.requires_grad_()
+
+        def bwd(x, y, g):
+            if self.is_last:
+                y.backward()
+            else:
+                y.backward(g)
+            return x.grad if not self.is_first else None
+
+        for m in range(warm):
+            x, y = fwd_compute(get_input(m))
+            if not self.is_last:
+                self.comm.send(y.detach().contiguous(), r + 1)
+            queue.append((x, y))
+        remaining = M - warm
+        x_next = get_input(warm) if remaining > 0 else None
+        b_i = 0
+        for i in range(remaining):
+            x, y = fwd_compute(x_next)
+            queue.append((x, y))
+            # send y forward, receive grad for the oldest in-flight micro-batch
+            g = None
+            if not self.is_last:
+                g = torch.empty(self._out_shape(sizes[b_i]), dtype=self.dtype, device=self.device)
+                self.comm.batch_p2p([(y.detach().contiguous(), r + 1, True), (g, r + 1, False)])
+                self.comm.wait()
+            xo, yo = queue.pop(0)
+            gx = bwd(xo, yo, g)
+            b_i += 1
+            last_iter = i == remaining - 1
+            if last_iter:
+                if not self.is_first:
+                    self.comm.send(gx.contiguous(), r - 1)
+                x_next = None
+            else:
+                m_next = warm + i + 1
+                if self.is_first:
+                    x_next = get_input(m_next)
+                else:
+                    buf = torch.empty(self._in_shape(sizes[m_next]), dtype=self.dtype,
+                                      device=self.device)
+                    self.comm.batch_p2p([(gx.contiguous(), r - 1, True), (buf, r - 1, False)])
+                    self.comm.wait()
+                    x_next = buf.requires_grad_()
+        for _ in range(warm):
+            xo, yo = queue.pop(0)
+            g = None
+            if not self.is_last:
+                g = torch.empty(self._out_shape(sizes[b_i]), dtype=self.dtype, device=self.device)
+                self.comm.recv(g, r + 1)
+                self.comm.wait()
+            gx = bwd(xo, yo, g)
+            b_i += 1
+            if not self.is_first:
+                self.comm.send(gx.contiguous(), r - 1)
+
+    @torch.no_grad()
+    def eval_step(self, inputs: Optional[torch.Tensor] = None,
+                  targets: Optional[torch.Tensor] = None) -> StepResult:
+        """Forward-only pass over the pipeline (reference val_* loops)."""
+        self.module.eval()
+        batch = self._batch_size(inputs)
+        sizes = self._mb_sizes(batch)
+        stats = torch.zeros(3, dtype=torch.float64, device=self.device)
+        tgt = None
+        if self.world == 1:
+            tgt = targets.to(self.device)
+        elif self.is_first:
+            self.comm.send(targets.to(self.device, torch.int64).contiguous(), self.world - 1)
+        elif self.is_last:
+            tgt = torch.empty(batch, dtype=torch.int64, device=self.device)
+            self.comm.recv(tgt, 0)
+            self.comm.wait()
+        xs = list(torch.split(inputs, sizes, 0)) if self.is_first else None
+        tg = list(torch.split(tgt, sizes, 0)) if tgt is not None else None
+        for m, mb in enumerate(sizes):
+            if self.is_first:
+                x = self._prep_input(xs[m])
+            else:
+                x = torch.empty(self._in_shape(mb), dtype=self.dtype, device=self.device)
+                self.comm.recv(x, self.rank - 1)
+                self.comm.wait()
+            y = self._forward(x)
+            if self.is_last:
+                logits = y.float()
+                stats[0] += self.loss_fn(logits, tg[m]).double() * mb / batch
+                c1, c5 = _topk_correct(logits, tg[m])
+                stats[1] += c1.double()
+                stats[2] += c5.double()
+            else:
+                self.comm.send(y.contiguous(), self.rank + 1)
+        saved_mb = self.micro_batches
+        self.micro_batches = 1  # stats[0] is already batch-weighted
+        res = self._finish_stats_eval(stats, batch)
+        self.micro_batches = saved_mb
+        return res
+
+    def _finish_stats_eval(self, stats, batch):
+        if self.world > 1:
+            if self.is_last:
+                self.comm.send(stats, 0)
+            elif self.is_first:
+                self.comm.recv(stats, self.world - 1)
+                self.comm.synchronize()
+        if self.is_first:
+            s = stats.tolist()
+            return StepResult(s[0], 100.0 * s[1] / batch, 100.0 * s[2] / batch)
+        return StepResult(None, None, None)
+

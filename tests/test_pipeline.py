@@ -1,0 +1,112 @@
+"""Pipeline model-parallel oracle: an N-stage P2P
+pipeline must produce the same loss and per-stage parameter gradients as the
+sequential model in one process -- for any world size (reference defect 2),
+every schedule, and the reference's ring loss placement."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd.parallel.pipeline import atom_costs, balanced_partition
+from tests.dist_utils import run_world
+
+
+def _mlp_atoms():
+    torch.manual_seed(0)
+    return nn.Sequential(nn.Sequential(nn.Flatten(), nn.Linear(48, 32), nn.ReLU()),
+                         nn.Sequential(nn.Linear(32, 32), nn.Tanh()),
+                         nn.Sequential(nn.Linear(32, 32), nn.ReLU()),
+                         nn.Sequential(nn.Linear(32, 24), nn.ReLU()),
+                         nn.Linear(24, 7))
+
+
+def _mnv2_atoms():
+    from distributed_model_parallel_amd.models import MobileNetV2
+    torch.manual_seed(0)
+    return MobileNetV2(num_classes=10).as_sequential()
+
+
+def _data(kind, batch):
+    g = torch.Generator().manual_seed(5)
+    if kind == "mlp":
+        return torch.randn(batch, 3, 4, 4, generator=g), torch.randint(0, 7, (batch,), generator=g)
+    return torch.randn(batch, 3, 32, 32, generator=g), torch.randint(0, 10, (batch,), generator=g)
+
+
+def _sequential_grads(kind, batch, micro):
+    # the workers run single-threaded; match the CPU kernels' reduction order
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        atoms = _mlp_atoms() if kind == "mlp" else _mnv2_atoms()
+        x, y = _data(kind, batch)
+        total = 0.0
+        for xs, ys in zip(torch.chunk(x, micro), torch.chunk(y, micro)):
+            loss = F.cross_entropy(atoms(xs), ys) / micro
+            loss.backward()
+            total += float(loss.detach())
+        return total, [[p.grad.clone() for p in a.parameters()] for a in atoms]
+    finally:
+        torch.set_num_threads(nt)
+
+
+def _pipe_worker(rank, world, kind, batch, micro, schedule, loss_on):
+    from distributed_model_parallel_amd.comm.rccl import Communicator
+    from distributed_model_parallel_amd.parallel.pipeline import Pipeline
+    atoms = _mlp_atoms() if kind == "mlp" else _mnv2_atoms()
+    shape = (3, 4, 4) if kind == "mlp" else (3, 32, 32)
+    comm = Communicator(torch.device("cpu"))
+    pipe = Pipeline(atoms, comm, shape, micro_batches=micro, schedule=schedule, loss_on=loss_on)
+    x, y = _data(kind, batch)
+    res = pipe.train_step(x if rank == 0 else None, y if rank == 0 else None)
+    lo, hi = pipe.partition[rank]
+    grads = {i: [p.grad.clone() for p in atoms[i].parameters()] for i in range(lo, hi)}
+    ev = pipe.eval_step(x if rank == 0 else None, y if rank == 0 else None)
+    return {"loss": res.loss, "grads": grads, "partition": pipe.partition, "eval": ev.loss,
+            "top1": res.top1}
+
+
+@pytest.mark.parametrize("world,schedule,micro,loss_on", [
+    (2, "naive", 1, "last"), (3, "gpipe", 4, "last"), (4, "1f1b", 4, "last"),
+    (2, "1f1b", 6, "last"), (3, "gpipe", 2, "first"), (4, "naive", 1, "first")])
+def test_pipeline_mlp_matches_sequential(world, schedule, micro, loss_on):
+    batch = 12
+    ref_loss, ref_grads = _sequential_grads("mlp", batch, micro)
+    res = run_world(_pipe_worker, world, "mlp", batch, micro, schedule, loss_on)
+    assert res[0]["loss"] == pytest.approx(ref_loss, rel=1e-5, abs=1e-6)
+    for r in res:
+        for i, gs in r["grads"].items():
+            for g, rg in zip(gs, ref_grads[i]):
+                torch.testing.assert_close(g, rg, atol=1e-6, rtol=1e-5)
+    assert res[0]["eval"] is not None
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_pipeline_mobilenetv2_any_world_size(world):
+    """The reference's MobileNetV2 pipeline, at world sizes it could not run (2, 3)."""
+    batch = 4
+    ref_loss, ref_grads = _sequential_grads("mnv2", batch, 1)
+    res = run_world(_pipe_worker, world, "mnv2", batch, 1, "naive", "last")
+    assert res[0]["loss"] == pytest.approx(ref_loss, rel=1e-4)
+    for r in res:
+        for i, gs in r["grads"].items():
+            for g, rg in zip(gs, ref_grads[i]):
+                torch.testing.assert_close(g, rg, atol=1e-4, rtol=1e-3)
+    covered = sorted(i for r in res for i in r["grads"])
+    assert covered == list(range(len(ref_grads)))
+
+
+def test_balanced_partition_properties():
+    costs = [5, 1, 1, 1, 1, 1, 5, 2, 2]
+    for k in range(1, len(costs) + 1):
+        parts = balanced_partition(costs, k)
+        assert len(parts) == k and parts[0][0] == 0 and parts[-1][1] == len(costs)
+        assert all(a < b for a, b in parts)
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(k - 1))
+    assert max(sum(costs[a:b]) for a, b in balanced_partition(costs, 3)) == 8  # brute-force optimum
+
+
+def test_atom_costs_mobilenet():
+    atoms = _mnv2_atoms()
+    c = atom_costs(atoms, torch.zeros(2, 3, 32, 32))
+    assert len(c) == 20 and all(v > 0 for v in c)
