@@ -1,0 +1,115 @@
+"""Learning-rate schedules of the reference recipe:
+``CosineAnnealingLR(T_max=epochs)`` stepped per epoch plus
+``pytorch_warmup.LinearWarmup(warmup_period=10)`` with ``dampen()`` -- the
+latter package is not installed, so :class:`LinearWarmup` reimplements its
+semantics: the scheduled lr is multiplied by ``min(1, (step+1)/period)``.
+
+Reference defect 11 (T_max=90 while training 100 epochs) is avoided by
+:func:`build_schedule` using the real epoch count.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+
+
+class LinearWarmup:
+    """Multiplicative linear warm-up applied on top of another schedule.
+
+    Usage (reference order): ``scheduler.step(); warmup.dampen()`` once per
+    epoch (or per iteration).  ``dampen`` rescales every param group's lr by
+    ``omega = min(1, (t+1)/warmup_period)`` where t counts dampen calls,
+    starting with the first call at construction time (like pytorch_warmup).
+    """
+
+    def __init__(self, optimizer: torch.optim.Optimizer, warmup_period: int, last_step: int = -1):
+        if warmup_period < 1:
+            raise ValueError("warmup_period must be >= 1")
+        self.optimizer = optimizer
+        self.warmup_period = warmup_period
+        self.last_step = last_step
+        self.lrs: List[float] = [g["lr"] for g in optimizer.param_groups]
+        self.dampen()
+
+    def warmup_factor(self, step: int) -> float:
+        return min(1.0, (step + 1) / self.warmup_period)
+
+    def dampen(self, step: Optional[int] = None) -> None:
+        if step is None:
+            step = self.last_step + 1
+        self.last_step = step
+        omega = self.warmup_factor(step)
+        self.lrs = [g["lr"] for g in self.optimizer.param_groups]  # undampened values
+        for g in self.optimizer.param_groups:
+            # the underlying scheduler has just written g["lr"]; scale it
+            g["lr"] = g["lr"] * omega
+
+    class _Dampening:
+        def __init__(self, w: "LinearWarmup"):
+            self.w = w
+
+        def __enter__(self):
+            for g, lr in zip(self.w.optimizer.param_groups, self.w.lrs):
+                g["lr"] = lr  # let the wrapped scheduler see the undampened lr
+            return self
+
+        def __exit__(self, *exc):
+            self.w.dampen()
+            return False
+
+    def dampening(self) -> "_Dampening":
+        """``with warmup.dampening(): scheduler.step()`` -- exact for chainable schedulers."""
+        return LinearWarmup._Dampening(self)
+
+    def state_dict(self):
+        return {"last_step": self.last_step, "warmup_period": self.warmup_period}
+
+    def load_state_dict(self, sd):
+        self.last_step = sd["last_step"]
+        self.warmup_period = sd["warmup_period"]
+
+
+def cosine_lr(base_lr: float, epoch: float, total: float, min_lr: float = 0.0) -> float:
+    return min_lr + 0.5 * (base_lr - min_lr) * (1.0 + math.cos(math.pi * min(epoch, total) / total))
+
+
+class WarmupCosine:
+    """Closed-form per-epoch schedule: lr(e) = cosine(base, e, epochs) * min(1, (e+1)/warmup)."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer, epochs: int, warmup_epochs: int = 10,
+                 min_lr: float = 0.0):
+        self.optimizer = optimizer
+        self.epochs = max(1, epochs)
+        self.warmup = max(1, warmup_epochs)
+        self.min_lr = min_lr
+        self.base = [g.get("initial_lr", g["lr"]) for g in optimizer.param_groups]
+        for g, b in zip(optimizer.param_groups, self.base):
+            g["initial_lr"] = b
+        self.epoch = 0
+        self._apply()
+
+    def _apply(self) -> None:
+        w = min(1.0, (self.epoch + 1) / self.warmup)
+        for g, b in zip(self.optimizer.param_groups, self.base):
+            g["lr"] = cosine_lr(b, self.epoch, self.epochs, self.min_lr) * w
+
+    def step(self, epoch: Optional[int] = None) -> None:
+        self.epoch = self.epoch + 1 if epoch is None else epoch
+        self._apply()
+
+    def get_last_lr(self) -> List[float]:
+        return [g["lr"] for g in self.optimizer.param_groups]
+
+    def state_dict(self):
+        return {"epoch": self.epoch, "base": self.base, "epochs": self.epochs, "warmup": self.warmup}
+
+    def load_state_dict(self, sd):
+        self.epoch, self.base, self.epochs, self.warmup = sd["epoch"], sd["base"], sd["epochs"], sd["warmup"]
+        self._apply()
+
+
+def build_schedule(optimizer: torch.optim.Optimizer, epochs: int, warmup_epochs: int = 10):
+    """Cosine over `epochs` (not a mismatched T_max, defect 11) + linear warm-up."""
+    return WarmupCosine(optimizer, epochs, warmup_epochs)
