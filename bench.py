@@ -116,6 +116,7 @@ def main() -> int:
             "sync_bn": args.parallel == "syncbn",
             "bucket_cap_mb": args.bucket_cap_mb,
             "channels_last": not args.no_channels_last,
+            "grad_comm": getattr(st.wrapped, "comm_backend", None),
             "final_loss": round(final_loss, 4),
         },
     }

@@ -65,8 +65,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- RCCL ----
   py::class_<dmp::RcclComm, std::shared_ptr<dmp::RcclComm>>(m, "RcclComm")
-      .def(py::init<const std::string&, int64_t, int64_t, int64_t>(), py::arg("unique_id"),
-           py::arg("nranks"), py::arg("rank"), py::arg("device"),
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t, bool>(), py::arg("unique_id"),
+           py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("high_priority") = true,
            py::call_guard<py::gil_scoped_release>())
       .def_static("new_unique_id", [] { return py::bytes(dmp::RcclComm::new_unique_id()); })
       .def_property_readonly("rank", &dmp::RcclComm::rank)
@@ -96,6 +96,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<dmp::RcclReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::RcclReduceBackend>>(
       m, "RcclReduceBackend")
       .def(py::init<std::shared_ptr<dmp::RcclComm>>());
+  py::class_<dmp::NullReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::NullReduceBackend>>(
+      m, "NullReduceBackend")
+      .def(py::init<>());
   py::class_<dmp::PyReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::PyReduceBackend>>(
       m, "PyReduceBackend")
       .def(py::init<py::object>());

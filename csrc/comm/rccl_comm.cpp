@@ -45,11 +45,12 @@ std::string RcclComm::new_unique_id() {
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-RcclComm::RcclComm(const std::string& unique_id, int64_t nranks, int64_t rank, int64_t device)
+RcclComm::RcclComm(const std::string& unique_id, int64_t nranks, int64_t rank, int64_t device,
+                   bool high_priority)
     : nranks_(nranks),
       rank_(rank),
       device_(device),
-      stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)) {
+      stream_(c10::hip::getStreamFromPool(high_priority, (c10::DeviceIndex)device)) {
   TORCH_CHECK(unique_id.size() == sizeof(ncclUniqueId), "bad ncclUniqueId length");
   c10::hip::HIPGuard guard((c10::DeviceIndex)device);
   ncclUniqueId id;

@@ -23,7 +23,8 @@ namespace dmp {
 
 class RcclComm {
  public:
-  RcclComm(const std::string& unique_id, int64_t nranks, int64_t rank, int64_t device);
+  RcclComm(const std::string& unique_id, int64_t nranks, int64_t rank, int64_t device,
+           bool high_priority = true);
   ~RcclComm();
 
   static std::string new_unique_id();

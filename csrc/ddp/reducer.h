@@ -54,6 +54,13 @@ class RcclReduceBackend : public ReduceBackend {
   std::shared_ptr<RcclComm> comm_;
 };
 
+// world_size == 1: the average over one rank is the identity, nothing to move.
+class NullReduceBackend : public ReduceBackend {
+ public:
+  void launch(int64_t, at::Tensor&) override {}
+  void wait_all() override {}
+};
+
 // hook(index, tensor) -> object with .wait(); the hook must leave the AVERAGED
 // gradient in `tensor` once wait() returns.
 class PyReduceBackend : public ReduceBackend {

@@ -13,6 +13,7 @@ same Python code runs in CPU tests.
 from __future__ import annotations
 
 import itertools
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -50,7 +51,8 @@ class Communicator:
                 store.set(key, uid)
             else:
                 uid = store.get(key)
-            self._comm = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index)
+            high = os.environ.get("DMP_COMM_PRIORITY", "high") == "high"
+            self._comm = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high)
 
     # ------------------------------------------------------------------ #
     @property

@@ -24,6 +24,7 @@ MI355X-first design (one process per GPU, torchrun):
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import torch
@@ -170,8 +171,14 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------------ #
     def _make_backend(self):
         C = _native.native()
+        if self.world_size == 1 and os.environ.get("DMP_DDP_SINGLE_RANK_COMM", "0") != "1":
+            # averaging over one rank is the identity: no collective to launch
+            self.comm_backend = "none(world_size=1)"
+            return C.NullReduceBackend()
         if self.comm.native is not None:
+            self.comm_backend = "rccl"
             return C.RcclReduceBackend(self.comm.native)
+        self.comm_backend = "process_group"
         return C.PyReduceBackend(_PyHookBackend(self.group, self.world_size))
 
     def register_comm_hook(self, state: Any, hook: Callable) -> None:

@@ -1,0 +1,285 @@
+"""Training CLI: data parallel (DDP / single-process DP) and pipeline model
+parallel, flag-compatible with the reference scripts.
+
+Reference entry points (§5.6):
+  ``python model_parallel.py DIR --world-size 4 --dist-url tcp://127.0.0.1:1224
+  --dist-backend nccl --lr 0.4 --epochs 90 -type Imagenet -b 512 -j 12 --wd 1e-4
+  --momentum 0.9`` and ``python data_parallel.py --lr 0.4 [-r]``.
+
+Equivalents here::
+
+  torchrun --nproc-per-node 8 -m distributed_model_parallel_amd.train.cli DIR \\
+      --parallel ddp --arch resnet50 -type Imagenet -b 256 --epochs 90
+  python -m distributed_model_parallel_amd.train.cli --parallel dp --arch mobilenetv2 \\
+      -type CIFAR10 DIR -b 512 -r
+  python -m distributed_model_parallel_amd.train.cli --parallel pipe --world-size 4 \\
+      --arch mobilenetv2 -type CIFAR10 DIR --micro-batches 8 --schedule 1f1b
+
+``--synthetic`` (or no DIR) trains on synthetic data of the dataset's shape.
+Honoured flags the reference parsed but ignored (defect 4): ``-b``, ``-j``,
+``-type`` and ``DIR``.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="MI355X-native data / model parallel training")
+    p.add_argument("data", nargs="?", default="", metavar="DIR", help="dataset root (empty: synthetic)")
+    p.add_argument("--dist-url", default=None, help="init method (default env:// from torchrun)")
+    p.add_argument("--world-size", default=None, type=int,
+                   help="processes to spawn for --parallel pipe without torchrun")
+    p.add_argument("--dist-backend", default=None, help="nccl (=RCCL) on GPU, gloo on CPU")
+    p.add_argument("--lr", "--learning-rate", default=0.4, type=float, dest="lr")
+    p.add_argument("--epochs", default=90, type=int)
+    p.add_argument("-type", "--dataset-type", default="CIFAR10", dest="dataset_type")
+    p.add_argument("-b", "--batch-size", default=512, type=int,
+                   help="per-process batch for ddp; total batch for dp and pipe")
+    p.add_argument("-j", "--workers", default=4, type=int)
+    p.add_argument("--wd", "--weight-decay", default=1e-4, type=float, dest="weight_decay")
+    p.add_argument("--momentum", default=0.9, type=float)
+    p.add_argument("-r", "--resume", action="store_true")
+    p.add_argument("--arch", default="mobilenetv2")
+    p.add_argument("--parallel", default="ddp", choices=["ddp", "dp", "pipe", "none"])
+    p.add_argument("--bucket-cap-mb", default=25.0, type=float)
+    p.add_argument("--sync-bn", action="store_true")
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    p.add_argument("--channels-last", action="store_true")
+    p.add_argument("--synthetic", action="store_true")
+    p.add_argument("--micro-batches", default=1, type=int)
+    p.add_argument("--schedule", default="1f1b", choices=["naive", "gpipe", "1f1b"])
+    p.add_argument("--warmup-epochs", default=10, type=int)
+    p.add_argument("--steps-per-epoch", default=0, type=int, help="cap iterations per epoch (0 = all)")
+    p.add_argument("--log-dir", default="./log")
+    p.add_argument("--checkpoint", default="./checkpoint/ckpt.pth")
+    p.add_argument("--seed", default=0, type=int)
+    return p
+
+
+def _datasets(args):
+    from ..data import DatasetCollection, transforms as T
+    cifar = args.dataset_type in ("CIFAR10", "SyntheticCIFAR")
+    if args.synthetic or not args.data:
+        kind = "SyntheticCIFAR" if cifar or args.arch.startswith("mobilenet") else "Synthetic"
+        return DatasetCollection(kind, "").init()
+    if cifar:
+        tr, va = T.cifar_train_transform(), T.cifar_test_transform()
+    else:
+        tr, va = T.imagenet_train_transform(), T.imagenet_val_transform()
+    return DatasetCollection(args.dataset_type, args.data, tr, va).init()
+
+
+def _num_classes(args) -> int:
+    return {"CIFAR10": 10, "SyntheticCIFAR": 10, "CUB200": 200, "Place365": 365}.get(
+        args.dataset_type, 10 if (args.synthetic or not args.data) and args.arch.startswith("mobilenet") else 1000)
+
+
+# --------------------------------------------------------------------------- #
+def run_data_parallel(args, env) -> None:
+    from ..data import prepare_dataloaders
+    from ..models import build_model
+    from ..ops.optim import FlatSGD
+    from ..parallel.data_parallel import DataParallel
+    from ..parallel.distributed import DistributedDataParallel
+    from ..parallel.sync_batchnorm import SyncBatchNorm
+    from ..utils.checkpoint import load_checkpoint, save_checkpoint
+    from ..utils.logging import MetricsLogger
+    from ..utils.metrics import AverageMeter, accuracy
+    from ..utils.precision import cast_model, parse_dtype
+    from ..utils.schedule import build_schedule
+
+    dev = env.device
+    dtype = parse_dtype(args.dtype)
+    model = build_model(args.arch, num_classes=_num_classes(args))
+    if args.sync_bn and args.parallel == "ddp":
+        model = SyncBatchNorm.convert_sync_batchnorm(model)
+    model = model.to(dev)
+    if args.channels_last:
+        model = model.to(memory_format=torch.channels_last)
+    if dtype != torch.float32:
+        cast_model(model, dtype)
+    if args.parallel == "ddp":
+        net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, flat_parameters=True)
+        opt = FlatSGD(net, lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
+    else:
+        net = DataParallel(model) if args.parallel == "dp" else model
+        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum,
+                              weight_decay=args.weight_decay)
+    sched = build_schedule(opt, args.epochs, args.warmup_epochs)
+    train_ds, val_ds = _datasets(args)
+    sampler, train_loader, val_loader = prepare_dataloaders(
+        train_ds, val_ds, args.batch_size, args.workers, distributed=args.parallel == "ddp" and env.distributed,
+        pin_memory=dev.type == "cuda", seed=args.seed)
+    start_epoch, best = 0, 0.0
+    if args.resume and os.path.exists(args.checkpoint):
+        meta = load_checkpoint(args.checkpoint, net, opt, sched, map_location=dev)
+        start_epoch, best = meta["epoch"] + 1, meta["acc"]
+    logger = MetricsLogger(args.log_dir, f"{args.parallel}_{args.arch}", env.rank,
+                           text_file=f"{args.parallel}_{args.batch_size}.txt")
+
+    def to_dev(x, y):
+        x = x.to(dev, dtype, non_blocking=True)
+        if args.channels_last and x.dim() == 4:
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x, y.to(dev, non_blocking=True)
+
+    for epoch in range(start_epoch, args.epochs):
+        if sampler is not None:
+            sampler.set_epoch(epoch)
+        net.train()
+        lm, am, bt, dt = AverageMeter(), AverageMeter(), AverageMeter(), AverageMeter()
+        t = time.perf_counter()
+        for i, (x, y) in enumerate(train_loader):
+            if args.steps_per_epoch and i >= args.steps_per_epoch:
+                break
+            x, y = to_dev(x, y)
+            dt.update(time.perf_counter() - t)
+            out = net(x)
+            loss = F.cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+            lm.update(loss.detach(), y.shape[0])
+            am.update(accuracy(out, y)[0], y.shape[0])
+            bt.update(time.perf_counter() - t)
+            t = time.perf_counter()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        vl, va = evaluate(net, val_loader, to_dev, args)
+        sched.step()
+        if env.is_main and va > best:
+            best = va
+            save_checkpoint(args.checkpoint, net, opt, sched, epoch, best)
+        logger.log(epoch, loss_train=lm.avg, acc1_train=am.avg, loss_val=vl, acc1_val=va,
+                   time_per_batch=bt.avg, time_load_perbatch=dt.avg,
+                   images_per_sec=(args.batch_size * max(1, env.world_size if args.parallel == "ddp" else 1))
+                   / max(bt.avg, 1e-9), lr=opt.param_groups[0]["lr"])
+
+
+@torch.no_grad()
+def evaluate(net, loader, to_dev, args):
+    from ..utils.metrics import AverageMeter, accuracy
+    net.eval()
+    lm, am = AverageMeter(), AverageMeter()
+    for i, (x, y) in enumerate(loader):
+        if args.steps_per_epoch and i >= args.steps_per_epoch:
+            break
+        x, y = to_dev(x, y)
+        out = net(x)
+        lm.update(F.cross_entropy(out.float(), y), y.shape[0])
+        am.update(accuracy(out, y)[0], y.shape[0])
+    return lm.avg, am.avg
+
+
+# --------------------------------------------------------------------------- #
+def run_pipeline(args, env) -> None:
+    from ..comm.rccl import Communicator
+    from ..data import prepare_dataloaders
+    from ..models import INPUT_SHAPES, build_model
+    from ..parallel.pipeline import Pipeline
+    from ..utils.checkpoint import save_checkpoint, stage_checkpoint_path
+    from ..utils.logging import MetricsLogger
+    from ..utils.precision import parse_dtype
+    from ..utils.schedule import build_schedule
+
+    torch.manual_seed(args.seed)  # every rank builds the same full model (reference: unseeded)
+    model = build_model(args.arch, num_classes=_num_classes(args))
+    (c, h, w), _ = INPUT_SHAPES.get(args.arch, ((3, 32, 32), 10))
+    comm = Communicator(env.device)
+    pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=args.micro_batches,
+                    schedule=args.schedule, dtype=parse_dtype(args.dtype),
+                    channels_last=args.channels_last)
+    opt = torch.optim.SGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
+                          weight_decay=args.weight_decay)
+    sched = build_schedule(opt, args.epochs, args.warmup_epochs)
+    logger = MetricsLogger(args.log_dir, f"pipe_{args.arch}", env.rank, text_file=f"{args.batch_size}.txt")
+    if env.rank == 0:
+        train_ds, val_ds = _datasets(args)
+        _, train_loader, val_loader = prepare_dataloaders(train_ds, val_ds, args.batch_size, args.workers,
+                                                          pin_memory=env.device.type == "cuda")
+        n_train, n_val = len(train_loader), len(val_loader)
+    else:
+        train_loader = val_loader = None
+        n_train = n_val = 0
+    # only rank 0 loads data; the others learn the iteration counts (defect 6)
+    counts = torch.tensor([n_train, n_val], dtype=torch.int64, device=env.device)
+    comm.broadcast(counts, 0)
+    comm.synchronize()
+    n_train, n_val = (int(v) for v in counts.tolist())
+    if args.steps_per_epoch:
+        n_train, n_val = min(n_train, args.steps_per_epoch), min(n_val, args.steps_per_epoch)
+    for epoch in range(args.epochs):
+        it = iter(train_loader) if train_loader is not None else None
+        tot_t, tot_d, loss_s, acc_s = 0.0, 0.0, 0.0, 0.0
+        t = time.perf_counter()
+        for i in range(n_train):
+            x, y = next(it) if it is not None else (None, None)
+            tot_d += time.perf_counter() - t
+            r = pipe.train_step(x, y)
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            if r.loss is not None:
+                loss_s += r.loss
+                acc_s += r.top1
+            tot_t += time.perf_counter() - t
+            t = time.perf_counter()
+        vit = iter(val_loader) if val_loader is not None else None
+        vl, va = 0.0, 0.0
+        for i in range(n_val):
+            x, y = next(vit) if vit is not None else (None, None)
+            r = pipe.eval_step(x, y)
+            if r.loss is not None:
+                vl += r.loss
+                va += r.top1
+        sched.step()
+        save_checkpoint(stage_checkpoint_path(args.checkpoint, env.rank), pipe.module, opt, sched, epoch,
+                        all_ranks=True)
+        if env.rank == 0:
+            logger.log(epoch, loss_train=loss_s / max(n_train, 1), acc1_train=acc_s / max(n_train, 1),
+                       loss_val=vl / max(n_val, 1), acc1_val=va / max(n_val, 1),
+                       time_per_batch=tot_t / max(n_train, 1), time_load_perbatch=tot_d / max(n_train, 1))
+
+
+def _spawn_entry(rank: int, world: int, args) -> None:
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      LOCAL_WORLD_SIZE=str(world))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    main_worker(args)
+
+
+def main_worker(args) -> None:
+    from ..utils.env import destroy_distributed, init_distributed, seed_everything
+    env = init_distributed(backend=args.dist_backend, dist_url=args.dist_url)
+    seed_everything(args.seed + (env.rank if args.parallel == "ddp" else 0))
+    try:
+        if args.parallel == "pipe":
+            run_pipeline(args, env)
+        else:
+            run_data_parallel(args, env)
+    finally:
+        destroy_distributed()
+
+
+def main(argv: Optional[list] = None) -> int:
+    args = build_parser().parse_args(argv)
+    if args.parallel == "pipe" and args.world_size and "RANK" not in os.environ:
+        import torch.multiprocessing as mp
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        mp.spawn(_spawn_entry, args=(args.world_size, args), nprocs=args.world_size, join=True)
+        return 0
+    main_worker(args)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
