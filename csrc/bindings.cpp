@@ -66,7 +66,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // ---- RCCL ----
   py::class_<dmp::RcclComm, std::shared_ptr<dmp::RcclComm>>(m, "RcclComm")
       .def(py::init<const std::string&, int64_t, int64_t, int64_t, bool>(), py::arg("unique_id"),
-           py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("high_priority") = true,
+           py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("high_priority") = false,
            py::call_guard<py::gil_scoped_release>())
       .def_static("new_unique_id", [] { return py::bytes(dmp::RcclComm::new_unique_id()); })
       .def_property_readonly("rank", &dmp::RcclComm::rank)

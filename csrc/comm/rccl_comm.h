@@ -1,6 +1,6 @@
 // Native RCCL communicator: one process per GPU, bootstrapped from an
 // ncclUniqueId that the Python layer distributes through the torch.distributed
-// store.  Collectives run on a dedicated HIGH-PRIORITY HIP stream per
+// store.  Collectives run on a dedicated (normal-priority) HIP stream per
 // communicator so that gradient all-reduces overlap with backward kernels on
 // the compute stream (xGMI transfers + RCCL kernels on their own queue).
 //
@@ -24,7 +24,7 @@ namespace dmp {
 class RcclComm {
  public:
   RcclComm(const std::string& unique_id, int64_t nranks, int64_t rank, int64_t device,
-           bool high_priority = true);
+           bool high_priority = false);
   ~RcclComm();
 
   static std::string new_unique_id();

@@ -14,7 +14,7 @@
 //     backward path).  When the last gradient of a bucket lands, the bucket's
 //     all-reduce is launched -- strictly in bucket order so every rank issues
 //     identical RCCL calls -- on the backend's side stream.
-//   * The backend is pluggable: native RCCL (ncclAvg on a high-priority HIP
+//   * The backend is pluggable: native RCCL (ncclAvg on a dedicated HIP
 //     stream) for MI355X, or a Python comm hook (gloo / any process group)
 //     for CPU tests and custom compression hooks (upstream register_comm_hook).
 //   * find_unused_parameters: a C++ walk of the autograd graph from the

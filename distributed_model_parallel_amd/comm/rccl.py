@@ -3,7 +3,7 @@ torch.distributed store.
 
 Why our own communicator instead of the process group's collectives: the DDP
 reducer issues all-reduces from C++ autograd hooks on a dedicated
-high-priority HIP stream and never touches Python or the c10d work objects in
+dedicated HIP stream and never touches Python or the c10d work objects in
 the backward path; pipeline P2P uses the same communicator with a static
 shape contract (no host round-trips).
 
@@ -51,7 +51,9 @@ class Communicator:
                 store.set(key, uid)
             else:
                 uid = store.get(key)
-            high = os.environ.get("DMP_COMM_PRIORITY", "high") == "high"
+            # NOT high priority by default: a high-priority HIP stream slowed the whole
+            # ResNet-50 step 1.9x on MI355X (67.3 vs 36.5 ms, profiles/README.md)
+            high = os.environ.get("DMP_COMM_PRIORITY", "normal") == "high"
             self._comm = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high)
 
     # ------------------------------------------------------------------ #

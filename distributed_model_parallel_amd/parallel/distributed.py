@@ -11,7 +11,7 @@ gradient_as_bucket_view=True, ...)``, ``no_sync()``, ``register_comm_hook``,
 MI355X-first design (one process per GPU, torchrun):
   * gradients are bucket views of one flat buffer per dtype; buckets (25 MB
     default, 1 MB first bucket -- SURVEY.md §5.8 sizing for 7 xGMI links) are
-    all-reduced by C++ hooks with RCCL ``ncclAvg`` on a high-priority HIP
+    all-reduced by C++ hooks with RCCL ``ncclAvg`` on a dedicated HIP
     stream while backward continues on the compute stream;
   * ``flat_parameters=True`` additionally makes every parameter a view into a
     flat parameter buffer laid out exactly like the gradient buckets, so

@@ -43,7 +43,7 @@ def test_replica_error_is_wrapped():
     class Bad(nn.Module):
         def forward(self, x):
             raise ValueError("boom")
-    with pytest.raises(RuntimeError, match="replica 1"):
+    with pytest.raises(RuntimeError, match="in replica 0 on device None: boom"):
         parallel_apply([Bad(), Bad()], [(torch.zeros(1),), (torch.zeros(1),)], devices=[None, None])
 
 
