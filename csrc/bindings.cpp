@@ -35,6 +35,13 @@ void sgd_flat_step(const c10::optional<at::Tensor>& master, const at::Tensor& mo
                    const at::Tensor& grad, const at::Tensor& param, double lr, double wd,
                    double momentum, double dampening, bool nesterov, double grad_scale,
                    bool first_step);
+// gemm_bf16.hip
+std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
+                                const c10::optional<at::Tensor>& pro_scale,
+                                const c10::optional<at::Tensor>& pro_shift, const std::string& mode,
+                                const c10::optional<at::Tensor>& epi_scale,
+                                const c10::optional<at::Tensor>& epi_shift,
+                                const c10::optional<at::Tensor>& residual, bool relu);
 // coalesced.hip
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
@@ -53,6 +60,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_eval_apply", &dmp::bn_eval_apply);
   m.def("bn_backward_moments", &dmp::bn_backward_moments);
   m.def("bn_backward_apply", &dmp::bn_backward_apply);
+
+  // ---- MFMA GEMM (1x1 conv) with fused BN prologue/epilogues ----
+  m.def("gemm_nt", &dmp::gemm_nt, py::arg("A"), py::arg("B"), py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
+        py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
+        py::arg("residual") = py::none(), py::arg("relu") = false);
 
   // ---- optimizer ----
   m.def("sgd_flat_step", &dmp::sgd_flat_step);

@@ -425,6 +425,13 @@ float* fptr(const c10::optional<at::Tensor>& t) {
 
 }  // namespace
 
+// Shared with the GEMM moments epilogue (csrc/conv/gemm_bf16.hip).
+void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
+                               hipStream_t stream) {
+  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh), dim3(1024), 0,
+                     stream, part, rb, C, sums, count);
+}
+
 // Local moments: fp64 [2C+1] = (sum x, sum x^2, rows) over the local rows.
 at::Tensor bn_local_moments(const at::Tensor& x, int64_t C) {
   check_input(x, C, "x");

@@ -63,5 +63,32 @@ def main():
         print(f"{k:45s} {v:10.3f}")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--gemm" not in sys.argv:
     main()
+
+
+def gemm_bench():
+    """Our MFMA NT GEMM (1x1 conv) vs MIOpen conv vs hipBLASLt on ResNet-50 1x1 shapes."""
+    from distributed_model_parallel_amd import _native
+    C = _native.require("gemm bench")
+    dev, dt = "cuda", torch.bfloat16
+    shapes = [(802816, 256, 64), (802816, 64, 256), (200704, 512, 128), (200704, 128, 512),
+              (50176, 1024, 256), (50176, 256, 1024), (12544, 2048, 512), (12544, 512, 2048)]
+    print(f"{'M':>7} {'N':>5} {'K':>5} | {'ours':>8} {'ours+mom':>8} {'miopen':>8} {'blaslt':>8}  ms | ours TB/s  TF/s")
+    for M, N, K in shapes:
+        a = torch.randn(M, K, device=dev, dtype=dt)
+        w = torch.randn(N, K, device=dev, dtype=dt)
+        t_o = timeit(lambda: C.gemm_nt(a, w))
+        t_m = timeit(lambda: C.gemm_nt(a, w, mode="moments"))
+        x4 = a.view(M // 3136 if M % 3136 == 0 else 1, -1, 1, K) if False else None
+        hw = {802816: 56, 200704: 28, 50176: 14, 12544: 7}[M]
+        x = a.view(256, hw, hw, K).permute(0, 3, 1, 2)
+        w4 = w.view(N, K, 1, 1).contiguous(memory_format=torch.channels_last)
+        t_c = timeit(lambda: F.conv2d(x, w4))
+        t_b = timeit(lambda: a @ w.t())
+        by = 2 * (M * K + N * K + M * N)
+        print(f"{M:7d} {N:5d} {K:5d} | {t_o:8.3f} {t_m:8.3f} {t_c:8.3f} {t_b:8.3f}     | {by / t_o / 1e9:6.2f} {2 * M * N * K / t_o / 1e9:7.1f}")
+
+
+if __name__ == "__main__" and "--gemm" in sys.argv:
+    gemm_bench()
