@@ -42,6 +42,13 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
                                 const c10::optional<at::Tensor>& residual, bool relu);
+// depthwise.hip
+std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride,
+                                          bool moments);
+at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t stride, int64_t H,
+                           int64_t W);
+at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride,
+                           at::ScalarType out_dtype);
 // coalesced.hip
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
@@ -66,6 +73,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
         py::arg("residual") = py::none(), py::arg("relu") = false);
+
+  // ---- depthwise 3x3 (NHWC) ----
+  m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),
+        py::arg("stride"), py::arg("moments") = false);
+  m.def("dwconv3x3_dgrad", &dmp::dwconv3x3_dgrad);
+  m.def("dwconv3x3_wgrad", &dmp::dwconv3x3_wgrad);
 
   // ---- optimizer ----
   m.def("sgd_flat_step", &dmp::sgd_flat_step);

@@ -25,6 +25,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv1x1 import Conv1x1
+from ..ops.depthwise import DepthwiseConv2d
+from ..ops.fused import conv_bn
 
 # (expansion t, output channels c, repeats n, first stride s) -- CIFAR strides.
 CIFAR_SETTINGS: Tuple[Tuple[int, int, int, int], ...] = (
@@ -57,17 +60,18 @@ class InvertedResidual(nn.Module):
         super().__init__()
         hidden = cin * expansion
         self.stride = stride
-        self.conv1 = nn.Conv2d(cin, hidden, 1, bias=False)
+        # 1x1 convs run as the MFMA GEMM and the depthwise as the NHWC kernel on
+        # MI355X, each emitting the following BN's statistics from its epilogue
+        self.conv1 = Conv1x1(cin, hidden)
         self.bn1 = _norm(hidden, use_bn, act=True)
-        self.conv2 = nn.Conv2d(hidden, hidden, 3, stride=stride, padding=1,
-                               groups=hidden, bias=False)
+        self.conv2 = DepthwiseConv2d(hidden, stride=stride)
         self.bn2 = _norm(hidden, use_bn, act=True)
-        self.conv3 = nn.Conv2d(hidden, cout, 1, bias=False)
+        self.conv3 = Conv1x1(hidden, cout)
         self.bn3 = _norm(cout, use_bn, act=False)
         self.has_residual = stride == 1
         sc_bn = use_bn if shortcut_bn is None else shortcut_bn
         if stride == 1 and cin != cout:
-            mods: List[nn.Module] = [nn.Conv2d(cin, cout, 1, bias=False)]
+            mods: List[nn.Module] = [Conv1x1(cin, cout)]
             if sc_bn:
                 mods.append(BatchNormAct2d(cout, act=None))
             self.shortcut = nn.Sequential(*mods)
@@ -75,12 +79,18 @@ class InvertedResidual(nn.Module):
             self.shortcut = nn.Sequential()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = self.bn1(self.conv1(x))
-        y = self.bn2(self.conv2(y))
-        y = self.bn3(self.conv3(y))
+        y = conv_bn(self.conv1, self.bn1, x)
+        y = conv_bn(self.conv2, self.bn2, y)
+        res = None
         if self.has_residual:
-            y = y + self.shortcut(x)
-        return y
+            if len(self.shortcut) == 0:
+                res = x
+            elif len(self.shortcut) == 2:
+                res = conv_bn(self.shortcut[0], self.shortcut[1], x)
+            else:
+                res = self.shortcut(x)
+        # bn3 has no activation: the residual add is fused into its apply pass
+        return conv_bn(self.conv3, self.bn3, y, res)
 
 
 class HeadPool(nn.Module):
@@ -116,7 +126,7 @@ class MobileNetV2(nn.Module):
                                                use_bn=use_bn, shortcut_bn=sc_bn))
                 cin = c
         self.layers = nn.Sequential(*blocks)
-        self.conv2 = nn.Conv2d(cin, 1280, 1, bias=False)
+        self.conv2 = Conv1x1(cin, 1280)
         self.bn2 = _norm(1280, use_bn, act=True)
         self.pool = HeadPool(apply_relu=False)
         self.linear = nn.Linear(1280, num_classes)
@@ -124,7 +134,7 @@ class MobileNetV2(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = self.bn1(self.conv1(x))
         x = self.layers(x)
-        x = self.bn2(self.conv2(x))
+        x = conv_bn(self.conv2, self.bn2, x)
         return self.linear(self.pool(x))
 
     # ------------------------------------------------------------------ #

@@ -18,6 +18,8 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv1x1 import Conv1x1
+from ..ops.fused import conv_bn
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -25,7 +27,16 @@ def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
 
 
 def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+    # MFMA GEMM on MI355X (channels-last bf16) with BN moments fused in its epilogue
+    return Conv1x1(cin, cout, stride)
+
+
+def _shortcut(ds: Optional[nn.Module], x: torch.Tensor) -> torch.Tensor:
+    if ds is None:
+        return x
+    if isinstance(ds, nn.Sequential) and len(ds) == 2:
+        return conv_bn(ds[0], ds[1], x)
+    return ds(x)
 
 
 class BasicBlock(nn.Module):
@@ -41,7 +52,7 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
+        identity = _shortcut(self.downsample, x)
         out = self.bn1(self.conv1(x))
         return self.bn2(self.conv2(out), identity)
 
@@ -61,10 +72,10 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
+        identity = _shortcut(self.downsample, x)
+        out = conv_bn(self.conv1, self.bn1, x)
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), identity)
+        return conv_bn(self.conv3, self.bn3, out, identity)
 
 
 class ResNet(nn.Module):

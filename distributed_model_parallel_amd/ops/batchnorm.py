@@ -167,17 +167,20 @@ def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, rel
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
-                relu, reduce_moments, reduce_grads):
+                relu, reduce_moments, reduce_grads, pre_sums=None):
         x2, back = _as_rows(x)
         native = _native_ok(x2)
         _STATS["native_fwd" if native else "torch_fwd"] += 1
+        if pre_sums is not None:
+            _STATS["fused_moments"] = _STATS.get("fused_moments", 0) + 1
         res2 = None
         if residual is not None:
             res2, _ = _as_rows(residual.to(x.dtype))
         w32 = weight.float() if weight is not None else None
         b32 = bias.float() if bias is not None else None
         if training:
-            sums = local_moments(x2, native)
+            # moments may come fused from the producing conv's epilogue (GEMM / depthwise)
+            sums = pre_sums if pre_sums is not None else local_moments(x2, native)
             if reduce_moments is not None:
                 sums = reduce_moments(sums)
             count = sums[-1:]
@@ -223,7 +226,7 @@ class _BatchNormActFn(torch.autograd.Function):
         gres = back(dres2) if has_res else None
         gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
         gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
-        return gx, gres, gw, gb, None, None, None, None, None, None, None, None
+        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
@@ -231,10 +234,12 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
                    bias: Optional[torch.Tensor], training: bool, momentum: float, eps: float,
                    relu: bool = False, residual: Optional[torch.Tensor] = None,
                    reduce_moments: Optional[MomentReducer] = None,
-                   reduce_grads: Optional[GradReducer] = None) -> torch.Tensor:
-    """Functional fused BN(+residual)(+ReLU)."""
+                   reduce_grads: Optional[GradReducer] = None,
+                   sums: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Functional fused BN(+residual)(+ReLU).  `sums`: precomputed local moments
+    [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode."""
     return _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
-                                 momentum, eps, relu, reduce_moments, reduce_grads)
+                                 momentum, eps, relu, reduce_moments, reduce_grads, sums)
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -263,7 +268,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
     def _moment_reducers(self):
         return None, None
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                sums: Optional[torch.Tensor] = None) -> torch.Tensor:
         self._check_input_dim(x)
         use_batch = self.training or not self.track_running_stats
         if self.training and self.track_running_stats and self.num_batches_tracked is not None:
@@ -275,7 +281,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return batch_norm_act(x, rm if self.track_running_stats else None,
                               rv if self.track_running_stats else None, self.weight, self.bias,
                               use_batch, momentum, self.eps, relu=self.act == "relu",
-                              residual=residual, reduce_moments=rmom, reduce_grads=rgrad)
+                              residual=residual, reduce_moments=rmom, reduce_grads=rgrad,
+                              sums=sums if use_batch else None)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (f", act={self.act}" if self.act else "")

@@ -1,0 +1,107 @@
+"""1x1 convolution on channels-last activations as an MFMA GEMM
+(``csrc/conv/gemm_bf16.hip``), optionally emitting the BatchNorm moments of its
+output so the following BN skips its statistics pass.
+
+  forward   y[M, Cout] = x[M, Cin] @ W[Cout, Cin]^T        (our MFMA kernel,
+            optional fused per-channel (sum, sum^2) of y)
+  dgrad     dx[M, Cin] = dy[M, Cout] @ W                    (our MFMA kernel)
+  wgrad     dW[Cout, Cin] = dy^T @ x                        (hipBLASLt: a plain
+            library GEMM with a huge reduction dim, no fusion to gain)
+
+Stride-2 1x1 convs (ResNet downsample) subsample rows first.  Anything the
+kernel does not cover (CPU, fp32, channel counts not multiple of 8) uses
+``F.conv2d``.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native
+
+_STATS = {"native": 0, "torch": 0}
+
+
+def _native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    if not _native.gpu_path(x):
+        return False
+    return (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 4
+            and x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _unrows(y2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
+    return y2.view(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, moments):
+        C = _native.require("conv1x1")
+        if stride != 1:
+            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
+        n, cin, h, w = x.shape
+        w2 = weight.reshape(weight.shape[0], cin)
+        y2, mom = C.gemm_nt(_rows(x), w2, mode="moments" if moments else "store")
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        if mom is None:
+            mom = torch.empty(0, device=x.device, dtype=torch.float64)
+        ctx.mark_non_differentiable(mom)
+        return _unrows(y2, n, h, w), mom
+
+    @staticmethod
+    def backward(ctx, dy, _dmom):
+        x, weight = ctx.saved_tensors
+        C = _native.require("conv1x1 backward")
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        dy2 = _rows(dy.contiguous(memory_format=torch.channels_last).to(x.dtype))
+        w2 = weight.reshape(cout, cin)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx2, _ = C.gemm_nt(dy2, w2.t().contiguous())
+            dx = _unrows(dx2, n, h, w)
+            if ctx.stride != 1:
+                full = torch.zeros((n, cin, h * ctx.stride, w * ctx.stride), dtype=dx.dtype,
+                                   device=dx.device).contiguous(memory_format=torch.channels_last)
+                # (callers guarantee even spatial sizes for strided 1x1 convs)
+                full[:, :, ::ctx.stride, ::ctx.stride] = dx
+                dx = full
+        if ctx.needs_input_grad[1]:
+            dw = (dy2.t() @ _rows(x)).view(cout, cin, 1, 1).to(weight.dtype)
+            if weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous(memory_format=torch.channels_last)
+        return dx, dw, None, None
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
+            moments: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
+    if _native_ok(x, weight) and (stride == 1 or (x.shape[2] % stride == 0 and x.shape[3] % stride == 0)):
+        _STATS["native"] += 1
+        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments)
+        return y, (mom if moments else None)
+    _STATS["torch"] += 1
+    return F.conv2d(x, weight, None, stride), None
+
+
+class Conv1x1(nn.Conv2d):
+    """Drop-in ``nn.Conv2d(cin, cout, 1, stride, bias=False)``."""
+
+    def __init__(self, cin: int, cout: int, stride: int = 1, device=None, dtype=None):
+        super().__init__(cin, cout, 1, stride=stride, bias=False, device=device, dtype=dtype)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return conv1x1(x, self.weight, self.stride[0])[0]
+
+    def forward_with_moments(self, x: torch.Tensor):
+        return conv1x1(x, self.weight, self.stride[0], moments=True)

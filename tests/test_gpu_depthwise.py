@@ -1,0 +1,48 @@
+"""Native 3x3 depthwise conv (forward, data grad, weight grad, output moments)
+against fp32 PyTorch conv2d(groups=C)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd import _native
+from distributed_model_parallel_amd.ops.depthwise import _STATS, DepthwiseConv2d
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("N,C,H,W,stride", [(4, 96, 32, 32, 1), (3, 144, 32, 32, 2), (2, 960, 4, 4, 1),
+                                            (5, 8, 9, 7, 2), (2, 24, 7, 9, 1), (1, 384, 8, 8, 2)])
+def test_depthwise_fwd_bwd(dtype, N, C, H, W, stride):
+    torch.manual_seed(0)
+    x = torch.randn(N, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    m = DepthwiseConv2d(C, stride).to(DEV)
+    w32 = m.weight.detach().clone().float()
+    m = m.to(dtype)
+    xr = x.detach().float().requires_grad_()
+    wr = w32.clone().requires_grad_()
+    xi = x.detach().requires_grad_()
+    before = _STATS["native"]
+    y = m(xi)
+    assert _STATS["native"] == before + 1
+    yr = F.conv2d(xr, wr, None, stride, 1, 1, C)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype).contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol * 3, rtol=tol)
+    wtol = 0.05 * (N * H * W / stride ** 2) ** 0.5 if dtype == torch.bfloat16 else 1e-2
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, atol=wtol, rtol=tol * 3)
+
+
+def test_depthwise_forward_moments():
+    C = _native.require("dw")
+    x = torch.randn(8, 64, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    w = torch.randn(64, 1, 3, 3, device=DEV).bfloat16()
+    y, mom = C.dwconv3x3_forward(x, w, 1, True)
+    yf = y.float().double().permute(0, 2, 3, 1).reshape(-1, 64)
+    torch.testing.assert_close(mom[:64], yf.sum(0), atol=1e-2, rtol=1e-4)
+    torch.testing.assert_close(mom[64:128], (yf * yf).sum(0), atol=1e-2, rtol=1e-4)
+    assert mom[128].item() == 8 * 16 * 16
