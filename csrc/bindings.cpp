@@ -42,6 +42,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
                                 const c10::optional<at::Tensor>& residual, bool relu);
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
 // depthwise.hip
 std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                           bool moments);
@@ -73,6 +74,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
         py::arg("residual") = py::none(), py::arg("relu") = false);
+
+  m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"));
 
   // ---- depthwise 3x3 (NHWC) ----
   m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),

@@ -275,6 +275,160 @@ void dispatch_tile(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int 
 
 int tile_m_for(int N) { return N <= 64 ? 256 : 128; }
 
+// ---------------------------------------------------------------------------
+// Weight gradient of a 1x1 conv: C[N, K] = sum_m A[m, n] * B[m, k]
+// (A = dy [M, N], B = x [M, K], both row-major).  The reduction runs over the
+// huge M = batch*H*W, the output is tiny, so the M range is split across
+// blocks (split-M) and each block writes an fp32 partial tile; a column
+// reduce sums the partials deterministically.  MFMA operands need 8
+// consecutive m per lane, i.e. a transpose of the row-major tiles: staged
+// row-major in LDS (16-B writes) and read with ds_read_b64_tr_b16 (gfx950's
+// transposing LDS read, cdna_hip_programming.md §5.5 T10), with a 32-B chunk
+// XOR swizzle so the 4-row x 32-B blocks of the two 16-lane groups of a
+// half-wave hit distinct banks.
+// ---------------------------------------------------------------------------
+constexpr int TN_BM = 64;  // m rows per LDS stage (two MFMA k-steps)
+
+__device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
+  // byte offset of element (row, col) [bf16] with the 32-B-chunk swizzle
+  const int byte = col * 2;
+  const int chunk = (byte >> 5) ^ ((row + 4 * (row >> 3)) & 7);
+  return row * row_bytes + (chunk << 5) + (byte & 31);
+}
+
+template <int BNT, int BKT>
+__global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
+    const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N,
+    int K, int64_t rows_per_split, float* __restrict__ part) {
+  // 4 waves as 2 x 2, each wave (BNT/2) x (BKT/2) outputs
+  constexpr int WTN = BNT / 2, WTK = BKT / 2;
+  constexpr int MI = WTN / 16, NI = WTK / 16;
+  constexpr int A_ROWB = BNT * 2, B_ROWB = BKT * 2;  // LDS row bytes
+  constexpr int A_BYTES = TN_BM * A_ROWB, B_BYTES = TN_BM * B_ROWB;
+  constexpr int A_VPR = BNT / 8, B_VPR = BKT / 8;    // 16-B vectors per row
+  constexpr int A_VECS = TN_BM * A_VPR / kThreads, B_VECS = TN_BM * B_VPR / kThreads;
+  static_assert(A_VECS >= 1 && B_VECS >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  using v4i16 = short __attribute__((ext_vector_type(4)));
+  using lds_v4 = __attribute__((address_space(3))) v4i16;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int ntiles = (N + BNT - 1) / BNT, ktiles = (K + BKT - 1) / BKT;
+  const int tile = blockIdx.x % (ntiles * ktiles);
+  const int split = blockIdx.x / (ntiles * ktiles);
+  const int n0 = (tile / ktiles) * BNT, k0 = (tile % ktiles) * BKT;
+  const int64_t mb = (int64_t)split * rows_per_split;
+  const int64_t me = min((int64_t)M, mb + rows_per_split);
+  const int nstages = (int)((me - mb + TN_BM - 1) / TN_BM);
+
+  bf16x8 ra[A_VECS], rb[B_VECS];
+  auto load = [&](int s) {
+    const int64_t m0 = mb + (int64_t)s * TN_BM;
+#pragma unroll
+    for (int i = 0; i < A_VECS; ++i) {
+      const int v = tid + i * kThreads, r = v / A_VPR, c = (v % A_VPR) * 8;
+      const int64_t m = m0 + r;
+      ra[i] = (m < me && n0 + c < N) ? *reinterpret_cast<const bf16x8*>(A + m * lda + n0 + c) : bf16x8{};
+    }
+#pragma unroll
+    for (int i = 0; i < B_VECS; ++i) {
+      const int v = tid + i * kThreads, r = v / B_VPR, c = (v % B_VPR) * 8;
+      const int64_t m = m0 + r;
+      rb[i] = (m < me && k0 + c < K) ? *reinterpret_cast<const bf16x8*>(B + m * ldb + k0 + c) : bf16x8{};
+    }
+  };
+  auto store = [&](int buf) {
+    char* as = smem + buf * (A_BYTES + B_BYTES);
+    char* bs = as + A_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_VECS; ++i) {
+      const int v = tid + i * kThreads, r = v / A_VPR, c = (v % A_VPR) * 8;
+      *reinterpret_cast<bf16x8*>(as + tn_off(r, c, A_ROWB)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_VECS; ++i) {
+      const int v = tid + i * kThreads, r = v / B_VPR, c = (v % B_VPR) * 8;
+      *reinterpret_cast<bf16x8*>(bs + tn_off(r, c, B_ROWB)) = rb[i];
+    }
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // tr-read lane roles: group g = lane>>4 covers m rows 8g..8g+7 of a k-step,
+  // lane i = 4q+p of the group addresses row q, columns 4p..4p+3 of the block
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  if (nstages > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nstages; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nstages) load(s + 1);
+    const char* as = smem + cur * (A_BYTES + B_BYTES);
+    const char* bs = as + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < TN_BM / 32; ++ks) {
+      bf16x8 fa[MI], fb[NI];
+      const int rbase = ks * 32 + 8 * g + q;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int col = wn * WTN + i * 16 + 4 * p;
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(as + tn_off(rbase, col, A_ROWB)));
+        v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(as + tn_off(rbase + 4, col, A_ROWB)));
+        short __attribute__((ext_vector_type(8))) t8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fa[i] = __builtin_bit_cast(bf16x8, t8);
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = wk * WTK + j * 16 + 4 * p;
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(bs + tn_off(rbase, col, B_ROWB)));
+        v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(bs + tn_off(rbase + 4, col, B_ROWB)));
+        short __attribute__((ext_vector_type(8))) t8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        fb[j] = __builtin_bit_cast(bf16x8, t8);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nstages) store(cur ^ 1);
+    __syncthreads();
+  }
+  // fp32 partial tile: part[split][n][k]
+  float* out = part + (int64_t)split * N * K;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int k = k0 + wk * WTK + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wn * WTN + i * 16 + (lane >> 4) * 4 + e;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[i][j][e];
+      }
+    }
+}
+
+// out[c] = sum_s part[s][c], written as bf16 or fp32
+template <typename OT>
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ part, int splits,
+                                                           int64_t n, OT* __restrict__ out) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i >= n) return;
+  f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < splits; ++s) a += *reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i);
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (i + e < n) out[i + e] = (OT)a[e];
+}
+
 void check_operand(const at::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
   TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be a row-major 2-D view");
@@ -282,7 +436,51 @@ void check_operand(const at::Tensor& t, const char* name) {
               " rows must be 16-B aligned");
 }
 
+template <int BNT, int BKT>
+void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, float* part,
+               int splits, int64_t rps, hipStream_t s) {
+  const int tiles = ((N + BNT - 1) / BNT) * ((K + BKT - 1) / BKT);
+  hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT>), dim3(tiles * splits), dim3(kThreads), 0, s,
+                     reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
+                     reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part);
+}
+
 }  // namespace
+
+// Weight gradient of a 1x1 conv: C[N, K] = A^T B with A [M, N], B [M, K] (bf16,
+// row-major).  Output dtype bf16 or fp32.
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype) {
+  check_operand(A, "A");
+  check_operand(B, "B");
+  TORCH_CHECK(A.size(0) == B.size(0), "A/B M mismatch");
+  const int M = (int)A.size(0), N = (int)A.size(1), K = (int)B.size(1);
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "N and K must be multiples of 8");
+  auto stream = at::hip::getCurrentHIPStream();
+  auto out = at::empty({N, K}, A.options().dtype(out_dtype));
+  if (M == 0) return out.zero_();
+  const int bnt = N >= 128 ? 128 : 64, bkt = K >= 128 ? 128 : 64;
+  const int tiles = ((N + bnt - 1) / bnt) * ((K + bkt - 1) / bkt);
+  const int max_splits = std::max(1, (M + TN_BM - 1) / TN_BM);
+  int splits = std::min(max_splits, std::max(1, (1024 + tiles - 1) / tiles));
+  int64_t rps = ((int64_t)M + splits - 1) / splits;
+  rps = (rps + TN_BM - 1) / TN_BM * TN_BM;
+  splits = (int)(((int64_t)M + rps - 1) / rps);
+  auto part = at::empty({splits, N, K}, A.options().dtype(at::kFloat));
+  float* pp = part.data_ptr<float>();
+  if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, stream);
+  else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, stream);
+  else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, stream);
+  else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, stream);
+  const int64_t n = (int64_t)N * K;
+  const unsigned blocks = (unsigned)((n / 4 + 255) / 256);
+  if (out_dtype == at::kBFloat16)
+    hipLaunchKernelGGL((split_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
+                       reinterpret_cast<bf16*>(out.data_ptr()));
+  else
+    hipLaunchKernelGGL((split_reduce_kernel<float>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
+                       out.data_ptr<float>());
+  return out;
+}
 
 // C = prologue(A) @ B^T with an optional fused epilogue.  Returns (C, moments-or-undefined).
 //   A [M, K] bf16, B [N, K] bf16 (both K-contiguous), K % 8 == 0, N % 8 == 0.

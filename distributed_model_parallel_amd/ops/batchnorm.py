@@ -22,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from ..utils.checkpointing import in_recompute
 
 # A moment reducer maps local fp64 moments [2C+1] = (sum x, sum x^2, rows) to
 # the global ones (an all-reduce SUM); identity for plain BN.  The row count
@@ -272,9 +273,13 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 sums: Optional[torch.Tensor] = None) -> torch.Tensor:
         self._check_input_dim(x)
         use_batch = self.training or not self.track_running_stats
-        if self.training and self.track_running_stats and self.num_batches_tracked is not None:
+        recompute = in_recompute()  # activation-checkpoint recompute: no second stat update
+        if self.training and self.track_running_stats and self.num_batches_tracked is not None \
+                and not recompute:
             self.num_batches_tracked.add_(1)
         momentum = self._momentum() if (self.training and self.track_running_stats) else 0.0
+        if recompute:
+            momentum = 0.0
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         rmom, rgrad = self._moment_reducers() if use_batch else (None, None)

@@ -5,8 +5,8 @@ output so the following BN skips its statistics pass.
   forward   y[M, Cout] = x[M, Cin] @ W[Cout, Cin]^T        (our MFMA kernel,
             optional fused per-channel (sum, sum^2) of y)
   dgrad     dx[M, Cin] = dy[M, Cout] @ W                    (our MFMA kernel)
-  wgrad     dW[Cout, Cin] = dy^T @ x                        (hipBLASLt: a plain
-            library GEMM with a huge reduction dim, no fusion to gain)
+  wgrad     dW[Cout, Cin] = dy^T @ x                        (our split-M MFMA
+            kernel with ds_read_b64_tr_b16 transposes; fp32 partials)
 
 Stride-2 1x1 convs (ResNet downsample) subsample rows first.  Anything the
 kernel does not cover (CPU, fp32, channel counts not multiple of 8) uses
@@ -77,7 +77,9 @@ class _Conv1x1Fn(torch.autograd.Function):
                 full[:, :, ::ctx.stride, ::ctx.stride] = dx
                 dx = full
         if ctx.needs_input_grad[1]:
-            dw = (dy2.t() @ _rows(x)).view(cout, cin, 1, 1).to(weight.dtype)
+            # split-M MFMA GEMM with transposing LDS reads (hipBLASLt picks a 4-tile,
+            # no-split kernel for this tiny-output / huge-reduction shape)
+            dw = C.gemm_tn(dy2, _rows(x), weight.dtype).view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
         return dx, dw, None, None

@@ -1,0 +1,85 @@
+"""Tracing ranges and profiler helpers.
+
+``trace_range(name)`` emits an roctx range (visible in ``rocprofv3
+--marker-trace`` / ``--sys-trace`` timelines) around scatter / replicate /
+apply / gather, each DDP bucket, pipeline hops, etc.  roctx is called through
+ctypes on the ``libroctx64`` PyTorch already ships, so there is no build-time
+dependency; when the library is missing the ranges are no-ops.
+``torch_profile`` wraps ``torch.profiler`` for a quick operator table.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import os
+from typing import Iterator, Optional
+
+_roctx = None
+_tried = False
+
+
+def _lib():
+    global _roctx, _tried
+    if _tried:
+        return _roctx
+    _tried = True
+    if os.environ.get("DMP_DISABLE_ROCTX") == "1":
+        return None
+    cands = []
+    try:
+        import torch
+        cands.append(os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"))
+    except Exception:  # noqa: BLE001
+        pass
+    cands += ["libroctx64.so", "/opt/rocm/lib/libroctx64.so"]
+    for c in cands:
+        try:
+            lib = ctypes.CDLL(c)
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+            lib.roctxRangePushA.restype = ctypes.c_int
+            lib.roctxRangePop.restype = ctypes.c_int
+            lib.roctxMarkA.argtypes = [ctypes.c_char_p]
+            _roctx = lib
+            break
+        except (OSError, AttributeError):
+            continue
+    return _roctx
+
+
+def available() -> bool:
+    return _lib() is not None
+
+
+def mark(msg: str) -> None:
+    lib = _lib()
+    if lib is not None:
+        lib.roctxMarkA(msg.encode())
+
+
+@contextlib.contextmanager
+def trace_range(name: str) -> Iterator[None]:
+    lib = _lib()
+    if lib is None:
+        yield
+        return
+    lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        lib.roctxRangePop()
+
+
+@contextlib.contextmanager
+def torch_profile(path: Optional[str] = None, cuda: bool = True, row_limit: int = 30):
+    """Profile the enclosed region with torch.profiler; print a table and
+    optionally export a chrome trace to `path`."""
+    import torch
+    acts = [torch.profiler.ProfilerActivity.CPU]
+    if cuda and torch.cuda.is_available():
+        acts.append(torch.profiler.ProfilerActivity.CUDA)
+    with torch.profiler.profile(activities=acts, record_shapes=False) as prof:
+        yield prof
+    key = "self_cuda_time_total" if len(acts) > 1 else "self_cpu_time_total"
+    print(prof.key_averages().table(sort_by=key, row_limit=row_limit))
+    if path:
+        prof.export_chrome_trace(path)

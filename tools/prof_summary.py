@@ -17,7 +17,8 @@ CATS = [
     ("dmp BN (ours)", ("bn_moments", "bn_apply", "bn_bwd", "bn_reduce")),
     ("dmp fused SGD (ours)", ("sgd_flat",)),
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
-    ("dmp GEMM/conv (ours)", ("dmp_gemm", "conv1x1")),
+    ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "split_reduce", "dw_fwd",
+                              "dw_dgrad", "dw_wgrad", "column_reduce")),
     ("MIOpen conv (igemm/ck)", ("igemm", "conv", "ck::", "naive_conv", "gridwise")),
     ("MIOpen tensor ops", ("SubTensorOp", "Op1dTensor", "Op2dTensor", "Op4dTensor")),
     ("hipBLASLt / rocBLAS GEMM", ("Cijk", "gemm", "Gemm")),
