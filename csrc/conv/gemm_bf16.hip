@@ -290,9 +290,11 @@ int tile_m_for(int N) { return N <= 64 ? 256 : 128; }
 constexpr int TN_BM = 64;  // m rows per LDS stage (two MFMA k-steps)
 
 __device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
-  // byte offset of element (row, col) [bf16] with the 32-B-chunk swizzle
+  // byte offset of element (row, col) [bf16] with the 32-B-chunk swizzle; the
+  // XOR stays inside the row (row_bytes / 32 chunks: 8 for 256-B, 4 for 128-B rows)
   const int byte = col * 2;
-  const int chunk = (byte >> 5) ^ ((row + 4 * (row >> 3)) & 7);
+  const int mask = (row_bytes >> 5) - 1;
+  const int chunk = (byte >> 5) ^ ((row + 4 * (row >> 3)) & mask);
   return row * row_bytes + (chunk << 5) + (byte & 31);
 }
 
