@@ -41,8 +41,11 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& pro_shift, const std::string& mode,
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
-                                const c10::optional<at::Tensor>& residual, bool relu);
-at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
+                                const c10::optional<at::Tensor>& residual, bool relu,
+                                const std::vector<int64_t>& a_map,
+                                const std::vector<int64_t>& c_map);
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
+                   const std::vector<int64_t>& b_map);
 // depthwise.hip
 std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                           bool moments);
@@ -73,9 +76,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt", &dmp::gemm_nt, py::arg("A"), py::arg("B"), py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
-        py::arg("residual") = py::none(), py::arg("relu") = false);
+        py::arg("residual") = py::none(), py::arg("relu") = false,
+        py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{});
 
-  m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"));
+  m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
+        py::arg("b_map") = std::vector<int64_t>{});
 
   // ---- depthwise 3x3 (NHWC) ----
   m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),

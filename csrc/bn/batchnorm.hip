@@ -12,10 +12,12 @@
 //     per-channel coefficients live in registers and every global access is a
 //     16-B coalesced load; a block walks a contiguous slab of rows with two
 //     rows in flight per lane.
-//   * moments: fp32 per-lane partial sums -> LDS combine -> ONE fp64 atomic add
-//     per channel per block into a [2C+1] fp64 buffer (sum, sum of squares,
-//     row count).  fp64 accumulation across blocks avoids E[x^2]-E[x]^2
-//     cancellation at M = 3.2M rows; the buffer is what SyncBN all-reduces.
+//   * moments: fp32 per-lane partial sums -> LDS combine -> one fp32 partial
+//     row per block ([2][blocks][C]) -> a 2-D fp64 reduce kernel into a [2C+1]
+//     fp64 buffer (sum, sum of squares, row count).  Same-address fp64 atomics
+//     from ~1000 blocks serialise (~100 ns each, measured), hence the partials.
+//     fp64 accumulation across blocks avoids E[x^2]-E[x]^2 cancellation at
+//     M = 3.2M rows; the buffer is what SyncBN all-reduces.
 //   * the apply kernel derives scale/shift from the moments itself (no
 //     finalize launch); the blocks of row-slab 0 also write the saved
 //     mean/invstd and update the running statistics.
@@ -24,7 +26,8 @@
 //     extra stored); pass 2 computes dx = a*dz + b*x + c with per-lane
 //     coefficients, writes d(residual) = dz when the residual was fused, and
 //     row-slab-0 blocks write dweight/dbias.
-// Forward = 2 launches (+1 zero-fill), backward = 2 launches (+1 zero-fill).
+// Forward = moments + reduce + apply, backward = moments + reduce + apply (the
+// moments pass disappears when the producing GEMM/depthwise kernel emits them).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "../common.h"
@@ -80,28 +83,32 @@ __device__ __forceinline__ void block_combine_store(const float (&s)[VEC], const
   }
 }
 
-// Deterministic fp64 reduction of the [2][rb][C] partials into sums[0:2C];
-// one 1024-thread block per 32 channels (32 row-groups x 32 channels), so each
-// lane sums only rb/32 partial rows.  Writes sums[2C] = count when count >= 0.
-constexpr int kRedCh = 32, kRedGroups = 32;
+// fp64 reduction of the [2][rb][C] partials into sums[0:2C].  Grid is
+// (ceil(C/32), ceil(rb/kRedRows)): each 1024-thread block (32 row-groups x 32
+// channels) folds kRedRows partial rows.  With one row-chunk the block stores
+// the result (deterministic); otherwise the caller zeroes sums and each chunk
+// adds with an fp64 atomic (<= rb/kRedRows adds per address, so no same-address
+// serialisation worth speaking of).  Writes sums[2C] = count when count >= 0.
+constexpr int kRedCh = 32, kRedGroups = 32, kRedRows = 256;
 __global__ __launch_bounds__(1024) void bn_reduce_partials_kernel(const float* __restrict__ part,
                                                                   int rb, int C,
                                                                   double* __restrict__ sums,
                                                                   double count) {
   const int cl = threadIdx.x % kRedCh, g = threadIdx.x / kRedCh;
   const int c = blockIdx.x * kRedCh + cl;
+  const int r0 = blockIdx.y * kRedRows, r1 = min(rb, r0 + kRedRows);
   double a = 0.0, b = 0.0;
   if (c < C) {
     const float* pa = part + c;
     const float* pb = part + (int64_t)rb * C + c;
-    int i = g;
-    for (; i + kRedGroups < rb; i += 2 * kRedGroups) {
+    int i = r0 + g;
+    for (; i + kRedGroups < r1; i += 2 * kRedGroups) {
       const float a0 = pa[(int64_t)i * C], a1 = pa[(int64_t)(i + kRedGroups) * C];
       const float b0 = pb[(int64_t)i * C], b1 = pb[(int64_t)(i + kRedGroups) * C];
       a += (double)a0 + (double)a1;
       b += (double)b0 + (double)b1;
     }
-    if (i < rb) {
+    if (i < r1) {
       a += (double)pa[(int64_t)i * C];
       b += (double)pb[(int64_t)i * C];
     }
@@ -118,10 +125,15 @@ __global__ __launch_bounds__(1024) void bn_reduce_partials_kernel(const float* _
     __syncthreads();
   }
   if (g == 0 && c < C) {
-    sums[c] = la[threadIdx.x];
-    sums[C + c] = lb[threadIdx.x];
+    if (gridDim.y == 1) {
+      sums[c] = la[threadIdx.x];
+      sums[C + c] = lb[threadIdx.x];
+    } else {
+      atomicAdd(sums + c, la[threadIdx.x]);
+      atomicAdd(sums + C + c, lb[threadIdx.x]);
+    }
   }
-  if (count >= 0.0 && blockIdx.x == 0 && threadIdx.x == 0) sums[2 * C] = count;
+  if (count >= 0.0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) sums[2 * C] = count;
 }
 
 // -------------------------------------------------------------------------
@@ -428,8 +440,11 @@ float* fptr(const c10::optional<at::Tensor>& t) {
 // Shared with the GEMM moments epilogue (csrc/conv/gemm_bf16.hip).
 void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
                                hipStream_t stream) {
-  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh), dim3(1024), 0,
-                     stream, part, rb, C, sums, count);
+  const int chunks = (rb + kRedRows - 1) / kRedRows;
+  if (chunks > 1)
+    DMP_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(double) * 2 * (size_t)C, stream));
+  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh, chunks), dim3(1024),
+                     0, stream, part, rb, C, sums, count);
 }
 
 // Local moments: fp64 [2C+1] = (sum x, sum x^2, rows) over the local rows.
@@ -446,9 +461,8 @@ at::Tensor bn_local_moments(const at::Tensor& x, int64_t C) {
     hipLaunchKernelGGL(bn_moments_kernel<T>, g.grid, dim3(kThreads), 0, stream, ptr<T>(x), M,
                        (int)C, g.rows_per_block, part.data_ptr<float>());
   });
-  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh), dim3(1024), 0,
-                     stream, part.data_ptr<float>(), (int)g.grid.x, (int)C,
-                     sums.data_ptr<double>(), (double)M);
+  bn_reduce_partials_launch(part.data_ptr<float>(), (int)g.grid.x, (int)C, sums.data_ptr<double>(),
+                            (double)M, stream);
   return sums;
 }
 
@@ -552,8 +566,7 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                          (int)C, g.rows_per_block, pp);
     }
   });
-  hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh), dim3(1024), 0,
-                     stream, pp, (int)g.grid.x, (int)C, sums.data_ptr<double>(), -1.0);
+  bn_reduce_partials_launch(pp, (int)g.grid.x, (int)C, sums.data_ptr<double>(), -1.0, stream);
   return sums;
 }
 

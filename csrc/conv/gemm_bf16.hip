@@ -44,6 +44,24 @@ constexpr int kThreads = 256;
 
 enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2 };
 
+// Logical GEMM row -> physical activation row for strided 1x1 convs: logical
+// row (n, oh, ow) of an [N, Ho, Wo] output grid reads/writes physical row
+// (n, oh*s, ow*s) of an [N, Hi, Wi] tensor.  s == 1 is the identity, so the
+// stride-2 ResNet shortcut needs no subsample copy (forward / wgrad) and no
+// scatter pass (dgrad).
+struct RowMap {
+  int s = 1, ho = 1, wo = 1, hi = 1, wi = 1;
+};
+
+__device__ __forceinline__ int64_t map_row(const RowMap& g, int64_t m) {
+  if (g.s == 1) return m;
+  const int64_t hw = (int64_t)g.ho * g.wo;
+  const int64_t n = m / hw;
+  const int r = (int)(m - n * hw);
+  const int oh = r / g.wo, ow = r - oh * g.wo;
+  return (n * g.hi + (int64_t)oh * g.s) * g.wi + (int64_t)ow * g.s;
+}
+
 __device__ __forceinline__ int swz(int row, int kvec) {
   // byte offset of 16-B vector `kvec` (0..7) of row `row` in a [rows][64] bf16 tile
   return row * (BK * 2) + ((kvec ^ ((row >> 1) & 7)) << 4);
@@ -55,7 +73,8 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
     bf16* __restrict__ C, int64_t ldc, int M, int N, int K,
     const float* __restrict__ pro_s, const float* __restrict__ pro_t,
     const float* __restrict__ epi_s, const float* __restrict__ epi_t,
-    const bf16* __restrict__ R, int64_t ldr, int epi_relu, float* __restrict__ part) {
+    const bf16* __restrict__ R, int64_t ldr, int epi_relu, float* __restrict__ part, RowMap amap,
+    RowMap cmap) {
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int A_VECS = BM * BK / 8 / kThreads;  // 16-B vectors per thread per A tile
@@ -85,14 +104,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
   constexpr int ROWS_PER_PASS = kThreads / (BK / 8);
 
   bf16x8 ra[A_VECS], rb[B_VECS];
+  const bf16* arow[A_VECS];  // this thread's A rows are fixed for the whole K loop
+#pragma unroll
+  for (int i = 0; i < A_VECS; ++i) {
+    const int row = m0 + r0 + i * ROWS_PER_PASS;
+    arow[i] = row < M ? A + map_row(amap, row) * lda : nullptr;
+  }
 
   auto load_tile = [&](int kt) {
     const int k = kt * BK + kv * 8;
     const bool kin = k < K;
 #pragma unroll
     for (int i = 0; i < A_VECS; ++i) {
-      const int row = m0 + r0 + i * ROWS_PER_PASS;
-      if (kin && row < M) ra[i] = *reinterpret_cast<const bf16x8*>(A + (int64_t)row * lda + k);
+      if (kin && arow[i]) ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + k);
       else ra[i] = bf16x8{};
     }
 #pragma unroll
@@ -216,7 +240,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
         }
         v = __builtin_convertvector(f, bf16x8);
       }
-      *reinterpret_cast<bf16x8*>(C + (int64_t)row * ldc + col) = v;
+      *reinterpret_cast<bf16x8*>(C + map_row(cmap, row) * ldc + col) = v;
       if constexpr (EPI == EPI_MOMENTS) {
         f32x8 f = __builtin_convertvector(v, f32x8);
 #pragma unroll
@@ -251,26 +275,38 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
 template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
 void launch(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int M, int N, int K,
             const float* ps, const float* pt, const float* es, const float* et, const bf16* R,
-            int64_t ldr, bool relu, float* part, hipStream_t stream) {
+            int64_t ldr, bool relu, float* part, const RowMap& am, const RowMap& cm,
+            hipStream_t stream) {
   const int mtiles = (M + BM - 1) / BM, ntiles = (N + BN - 1) / BN;
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI>), dim3(mtiles * ntiles),
                      dim3(kThreads), 0, stream, reinterpret_cast<const bf16*>(A.data_ptr()),
                      A.stride(0), reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0),
                      reinterpret_cast<bf16*>(C.data_ptr()), C.stride(0), M, N, K, ps, pt, es, et, R,
-                     ldr, (int)relu, part);
+                     ldr, (int)relu, part, am, cm);
 }
 
 template <bool PRO, int EPI>
 void dispatch_tile(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int M, int N, int K,
                    const float* ps, const float* pt, const float* es, const float* et,
-                   const bf16* R, int64_t ldr, bool relu, float* part, int bm, hipStream_t s) {
+                   const bf16* R, int64_t ldr, bool relu, float* part, const RowMap& am,
+                   const RowMap& cm, int bm, hipStream_t s) {
   // bm selects the M tile (128 or 256 rows) ; BN follows N.
   if (N <= 64) {
-    if (bm == 256) launch<256, 64, 4, 1, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, s);
-    else launch<128, 64, 2, 2, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, s);
+    if (bm == 256) launch<256, 64, 4, 1, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, am, cm, s);
+    else launch<128, 64, 2, 2, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, am, cm, s);
   } else {
-    launch<128, 128, 2, 2, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, s);
+    launch<128, 128, 2, 2, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, am, cm, s);
   }
+}
+
+RowMap parse_map(const std::vector<int64_t>& g, const char* name) {
+  RowMap m;
+  if (g.empty()) return m;
+  TORCH_CHECK(g.size() == 5, name, " must be [stride, Ho, Wo, Hi, Wi]");
+  m.s = (int)g[0]; m.ho = (int)g[1]; m.wo = (int)g[2]; m.hi = (int)g[3]; m.wi = (int)g[4];
+  TORCH_CHECK(m.s >= 1 && (m.ho - 1) * m.s < m.hi && (m.wo - 1) * m.s < m.wi && m.ho > 0 && m.wo > 0,
+              name, ": output grid does not fit the input grid");
+  return m;
 }
 
 int tile_m_for(int N) { return N <= 64 ? 256 : 128; }
@@ -301,7 +337,7 @@ __device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
 template <int BNT, int BKT>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N,
-    int K, int64_t rows_per_split, float* __restrict__ part) {
+    int K, int64_t rows_per_split, float* __restrict__ part, RowMap bmap) {
   // 4 waves as 2 x 2, each wave (BNT/2) x (BKT/2) outputs
   constexpr int WTN = BNT / 2, WTK = BKT / 2;
   constexpr int MI = WTN / 16, NI = WTK / 16;
@@ -337,7 +373,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
     for (int i = 0; i < B_VECS; ++i) {
       const int v = tid + i * kThreads, r = v / B_VPR, c = (v % B_VPR) * 8;
       const int64_t m = m0 + r;
-      rb[i] = (m < me && k0 + c < K) ? *reinterpret_cast<const bf16x8*>(B + m * ldb + k0 + c) : bf16x8{};
+      rb[i] = (m < me && k0 + c < K)
+                  ? *reinterpret_cast<const bf16x8*>(B + map_row(bmap, m) * ldb + k0 + c)
+                  : bf16x8{};
     }
   };
   auto store = [&](int buf) {
@@ -418,17 +456,39 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
     }
 }
 
-// out[c] = sum_s part[s][c], written as bf16 or fp32
+// out[c] = sum_s part[s][c], written as bf16 or fp32.  A 256-thread block owns
+// 256/SL float4 columns and splits them over SL "split lanes" (thread t reads
+// splits t/cols, t/cols + SL, ...), then folds the SL lanes in LDS.  SL is
+// chosen on the host so small outputs with many splits still fill the chip
+// (a 64x64 weight with 1024 splits would otherwise be 4 blocks of serial loads).
 template <typename OT>
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ part, int splits,
-                                                           int64_t n, OT* __restrict__ out) {
-  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i >= n) return;
+                                                           int64_t n, int sl, OT* __restrict__ out) {
+  const int cols = 256 / sl;
+  const int cl = threadIdx.x % cols, lane_s = threadIdx.x / cols;
+  const int64_t i = ((int64_t)blockIdx.x * cols + cl) * 4;
   f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < splits; ++s) a += *reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i);
+  if (i < n) {
+    int s = lane_s;
+    for (; s + sl < splits; s += 2 * sl) {
+      const f32x4 p0 = *reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i);
+      const f32x4 p1 = *reinterpret_cast<const f32x4*>(part + (int64_t)(s + sl) * n + i);
+      a += p0 + p1;
+    }
+    if (s < splits) a += *reinterpret_cast<const f32x4*>(part + (int64_t)s * n + i);
+  }
+  __shared__ f32x4 red[256];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int h = sl / 2; h > 0; h >>= 1) {
+    if (lane_s < h) red[threadIdx.x] += red[threadIdx.x + h * cols];
+    __syncthreads();
+  }
+  if (lane_s == 0 && i < n) {
+    a = red[threadIdx.x];
 #pragma unroll
-  for (int e = 0; e < 4; ++e)
-    if (i + e < n) out[i + e] = (OT)a[e];
+    for (int e = 0; e < 4; ++e) out[i + e] = (OT)a[e];
+  }
 }
 
 void check_operand(const at::Tensor& t, const char* name) {
@@ -440,21 +500,30 @@ void check_operand(const at::Tensor& t, const char* name) {
 
 template <int BNT, int BKT>
 void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, float* part,
-               int splits, int64_t rps, hipStream_t s) {
+               int splits, int64_t rps, const RowMap& bm, hipStream_t s) {
   const int tiles = ((N + BNT - 1) / BNT) * ((K + BKT - 1) / BKT);
   hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT>), dim3(tiles * splits), dim3(kThreads), 0, s,
                      reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
-                     reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part);
+                     reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part, bm);
 }
 
 }  // namespace
 
 // Weight gradient of a 1x1 conv: C[N, K] = A^T B with A [M, N], B [M, K] (bf16,
-// row-major).  Output dtype bf16 or fp32.
-at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype) {
+// row-major).  Output dtype bf16 or fp32.  b_map ([s, Ho, Wo, Hi, Wi]) reads
+// B's logical row m from the strided physical row (stride-s 1x1 conv input).
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
+                   const std::vector<int64_t>& b_map) {
   check_operand(A, "A");
   check_operand(B, "B");
-  TORCH_CHECK(A.size(0) == B.size(0), "A/B M mismatch");
+  const RowMap bmap = parse_map(b_map, "b_map");
+  if (bmap.s == 1) {
+    TORCH_CHECK(A.size(0) == B.size(0), "A/B M mismatch");
+  } else {
+    TORCH_CHECK(B.size(0) % ((int64_t)bmap.hi * bmap.wi) == 0 &&
+                    A.size(0) == B.size(0) / ((int64_t)bmap.hi * bmap.wi) * bmap.ho * bmap.wo,
+                "b_map does not match the A/B row counts");
+  }
   const int M = (int)A.size(0), N = (int)A.size(1), K = (int)B.size(1);
   TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "N and K must be multiples of 8");
   auto stream = at::hip::getCurrentHIPStream();
@@ -462,25 +531,32 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
   if (M == 0) return out.zero_();
   const int bnt = N >= 128 ? 128 : 64, bkt = K >= 128 ? 128 : 64;
   const int tiles = ((N + bnt - 1) / bnt) * ((K + bkt - 1) / bkt);
+  // ~4 blocks per CU, but keep the fp32 partial traffic well under the operand
+  // traffic (the GEMM streams (N+K)*M bf16; partials cost 2 * splits*N*K*4 B).
   const int max_splits = std::max(1, (M + TN_BM - 1) / TN_BM);
-  int splits = std::min(max_splits, std::max(1, (1024 + tiles - 1) / tiles));
+  const int64_t operand_bytes = (int64_t)M * (N + K) * 2;
+  const int64_t part_cap = std::max<int64_t>(operand_bytes / 4, 8 << 20);
+  const int by_bytes = (int)std::max<int64_t>(1, part_cap / ((int64_t)N * K * 8));
+  int splits = std::min({max_splits, by_bytes, std::max(1, (1024 + tiles - 1) / tiles)});
   int64_t rps = ((int64_t)M + splits - 1) / splits;
   rps = (rps + TN_BM - 1) / TN_BM * TN_BM;
   splits = (int)(((int64_t)M + rps - 1) / rps);
   auto part = at::empty({splits, N, K}, A.options().dtype(at::kFloat));
   float* pp = part.data_ptr<float>();
-  if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, stream);
-  else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, stream);
-  else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, stream);
-  else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, stream);
+  if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, bmap, stream);
+  else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, stream);
+  else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, stream);
+  else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, bmap, stream);
   const int64_t n = (int64_t)N * K;
-  const unsigned blocks = (unsigned)((n / 4 + 255) / 256);
+  int sl = 1;  // split lanes per column: grow until >= 512 blocks or lanes cover the splits
+  while (sl < 64 && sl < splits && (n / 4 + 256 / sl - 1) / (256 / sl) < 512) sl *= 2;
+  const unsigned blocks = (unsigned)((n / 4 + 256 / sl - 1) / (256 / sl));
   if (out_dtype == at::kBFloat16)
     hipLaunchKernelGGL((split_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
-                       reinterpret_cast<bf16*>(out.data_ptr()));
+                       sl, reinterpret_cast<bf16*>(out.data_ptr()));
   else
     hipLaunchKernelGGL((split_reduce_kernel<float>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
-                       out.data_ptr<float>());
+                       sl, out.data_ptr<float>());
   return out;
 }
 
@@ -494,14 +570,29 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& pro_shift, const std::string& mode,
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
-                                const c10::optional<at::Tensor>& residual, bool relu) {
+                                const c10::optional<at::Tensor>& residual, bool relu,
+                                const std::vector<int64_t>& a_map,
+                                const std::vector<int64_t>& c_map) {
   check_operand(A, "A");
   check_operand(B, "B");
-  const int M = (int)A.size(0), K = (int)A.size(1), N = (int)B.size(0);
+  const RowMap am = parse_map(a_map, "a_map"), cm = parse_map(c_map, "c_map");
+  int64_t m64 = A.size(0);
+  if (am.s != 1) {
+    TORCH_CHECK(m64 % ((int64_t)am.hi * am.wi) == 0, "a_map does not match A's rows");
+    m64 = m64 / ((int64_t)am.hi * am.wi) * am.ho * am.wo;
+  }
+  const int M = (int)m64, K = (int)A.size(1), N = (int)B.size(0);
   TORCH_CHECK(B.size(1) == K, "A/B K mismatch");
   TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "K and N must be multiples of 8");
   auto stream = at::hip::getCurrentHIPStream();
-  auto C = at::empty({M, N}, A.options());
+  at::Tensor C;
+  if (cm.s == 1) {
+    C = at::empty({M, N}, A.options());
+  } else {
+    // rows the strided scatter does not reach are exactly zero (dgrad of a strided 1x1 conv)
+    TORCH_CHECK(M % ((int64_t)cm.ho * cm.wo) == 0, "c_map does not match the GEMM rows");
+    C = at::zeros({(int64_t)M / ((int64_t)cm.ho * cm.wo) * cm.hi * cm.wi, N}, A.options());
+  }
   const bool pro = pro_scale.has_value() && pro_scale->defined();
   const float* ps = pro ? pro_scale->data_ptr<float>() : nullptr;
   const float* pt = pro ? pro_shift->data_ptr<float>() : nullptr;
@@ -509,13 +600,13 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
   if (M == 0) return {C, moments};
   const int bm = tile_m_for(N);
   if (mode == "store") {
-    if (pro) dispatch_tile<true, EPI_STORE>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, nullptr, bm, stream);
-    else dispatch_tile<false, EPI_STORE>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, nullptr, bm, stream);
+    if (pro) dispatch_tile<true, EPI_STORE>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, nullptr, am, cm, bm, stream);
+    else dispatch_tile<false, EPI_STORE>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, nullptr, am, cm, bm, stream);
   } else if (mode == "moments") {
     const int mtiles = (M + bm - 1) / bm;
     auto part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
-    if (pro) dispatch_tile<true, EPI_MOMENTS>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, part.data_ptr<float>(), bm, stream);
-    else dispatch_tile<false, EPI_MOMENTS>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, part.data_ptr<float>(), bm, stream);
+    if (pro) dispatch_tile<true, EPI_MOMENTS>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, part.data_ptr<float>(), am, cm, bm, stream);
+    else dispatch_tile<false, EPI_MOMENTS>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, part.data_ptr<float>(), am, cm, bm, stream);
     moments = at::empty({2 * (int64_t)N + 1}, A.options().dtype(at::kDouble));
     bn_reduce_partials_launch(part.data_ptr<float>(), mtiles, N, moments.data_ptr<double>(),
                               (double)M, stream);
@@ -529,8 +620,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
       R = reinterpret_cast<const bf16*>(residual->data_ptr());
       ldr = residual->stride(0);
     }
-    if (pro) dispatch_tile<true, EPI_AFFINE>(A, B, C, M, N, K, ps, pt, epi_scale->data_ptr<float>(), epi_shift->data_ptr<float>(), R, ldr, relu, nullptr, bm, stream);
-    else dispatch_tile<false, EPI_AFFINE>(A, B, C, M, N, K, ps, pt, epi_scale->data_ptr<float>(), epi_shift->data_ptr<float>(), R, ldr, relu, nullptr, bm, stream);
+    if (pro) dispatch_tile<true, EPI_AFFINE>(A, B, C, M, N, K, ps, pt, epi_scale->data_ptr<float>(), epi_shift->data_ptr<float>(), R, ldr, relu, nullptr, am, cm, bm, stream);
+    else dispatch_tile<false, EPI_AFFINE>(A, B, C, M, N, K, ps, pt, epi_scale->data_ptr<float>(), epi_shift->data_ptr<float>(), R, ldr, relu, nullptr, am, cm, bm, stream);
   } else {
     TORCH_CHECK(false, "unknown epilogue mode ", mode);
   }

@@ -8,8 +8,9 @@ output so the following BN skips its statistics pass.
   wgrad     dW[Cout, Cin] = dy^T @ x                        (our split-M MFMA
             kernel with ds_read_b64_tr_b16 transposes; fp32 partials)
 
-Stride-2 1x1 convs (ResNet downsample) subsample rows first.  Anything the
-kernel does not cover (CPU, fp32, channel counts not multiple of 8) uses
+Stride-2 1x1 convs (ResNet downsample) address the sampled rows in place
+through a row map (forward / wgrad read them, dgrad scatters into them): no
+subsample copy, no scatter pass.  Anything the kernel does not cover (CPU, fp32, channel counts not multiple of 8) uses
 ``F.conv2d``.
 """
 from __future__ import annotations
@@ -42,21 +43,29 @@ def _unrows(y2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return y2.view(n, h, w, -1).permute(0, 3, 1, 2)
 
 
+def _geom(stride: int, hi: int, wi: int):
+    """Row map [s, Ho, Wo, Hi, Wi] the kernels use to address a stride-s grid in place."""
+    if stride == 1:
+        return []
+    return [stride, (hi - 1) // stride + 1, (wi - 1) // stride + 1, hi, wi]
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, stride, moments):
         C = _native.require("conv1x1")
-        if stride != 1:
-            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
         n, cin, h, w = x.shape
+        geom = _geom(stride, h, w)
+        ho, wo = (geom[1], geom[2]) if geom else (h, w)
         w2 = weight.reshape(weight.shape[0], cin)
-        y2, mom = C.gemm_nt(_rows(x), w2, mode="moments" if moments else "store")
+        # strided convs read the sampled rows in place (no subsample copy)
+        y2, mom = C.gemm_nt(_rows(x), w2, mode="moments" if moments else "store", a_map=geom)
         ctx.save_for_backward(x, weight)
-        ctx.stride = stride
+        ctx.geom = geom
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
-        return _unrows(y2, n, h, w), mom
+        return _unrows(y2, n, ho, wo), mom
 
     @staticmethod
     def backward(ctx, dy, _dmom):
@@ -68,18 +77,13 @@ class _Conv1x1Fn(torch.autograd.Function):
         w2 = weight.reshape(cout, cin)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx2, _ = C.gemm_nt(dy2, w2.t().contiguous())
+            # strided: the GEMM scatters into the sampled rows of a zeroed full-size grad
+            dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), c_map=ctx.geom)
             dx = _unrows(dx2, n, h, w)
-            if ctx.stride != 1:
-                full = torch.zeros((n, cin, h * ctx.stride, w * ctx.stride), dtype=dx.dtype,
-                                   device=dx.device).contiguous(memory_format=torch.channels_last)
-                # (callers guarantee even spatial sizes for strided 1x1 convs)
-                full[:, :, ::ctx.stride, ::ctx.stride] = dx
-                dx = full
         if ctx.needs_input_grad[1]:
             # split-M MFMA GEMM with transposing LDS reads (hipBLASLt picks a 4-tile,
             # no-split kernel for this tiny-output / huge-reduction shape)
-            dw = C.gemm_tn(dy2, _rows(x), weight.dtype).view(cout, cin, 1, 1)
+            dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
         return dx, dw, None, None
@@ -88,7 +92,7 @@ class _Conv1x1Fn(torch.autograd.Function):
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
             moments: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
-    if _native_ok(x, weight) and (stride == 1 or (x.shape[2] % stride == 0 and x.shape[3] % stride == 0)):
+    if _native_ok(x, weight):
         _STATS["native"] += 1
         y, mom = _Conv1x1Fn.apply(x, weight, stride, moments)
         return y, (mom if moments else None)

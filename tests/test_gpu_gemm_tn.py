@@ -52,3 +52,47 @@ def test_conv1x1_autograd_matches_conv2d(stride):
     yr.backward(g)
     torch.testing.assert_close(xi.grad.float(), xr.grad, atol=0.1, rtol=2e-2)
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, atol=0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("hw", [(14, 14), (15, 9), (7, 8)])
+def test_strided_row_maps(hw):
+    """a_map (strided A read), c_map (strided scatter into zeros), b_map (strided wgrad
+    operand) against explicit subsample / scatter in fp32."""
+    C = _native.require("gemm_nt")
+    torch.manual_seed(2)
+    n, h, w, cin, cout, s = 3, hw[0], hw[1], 64, 96, 2
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    geom = [s, ho, wo, h, w]
+    x = torch.randn(n, h, w, cin, device=DEV).bfloat16()
+    wt = torch.randn(cout, cin, device=DEV).bfloat16()
+    xs = x[:, ::s, ::s].reshape(-1, cin)
+    y, _ = C.gemm_nt(x.reshape(-1, cin), wt, a_map=geom)
+    torch.testing.assert_close(y.float(), xs.float() @ wt.float().t(), atol=0.1, rtol=2e-2)
+    ym, mom = C.gemm_nt(x.reshape(-1, cin), wt, mode="moments", a_map=geom)
+    yf = ym.float()
+    torch.testing.assert_close(mom[:cout].float(), yf.sum(0), atol=1e-2 * yf.shape[0] ** 0.5, rtol=1e-3)
+    assert mom[-1].item() == n * ho * wo
+    dy = torch.randn(n * ho * wo, cout, device=DEV).bfloat16()
+    dx, _ = C.gemm_nt(dy, wt.t().contiguous(), c_map=geom)
+    ref = torch.zeros(n, h, w, cin, device=DEV)
+    ref[:, ::s, ::s] = (dy.float() @ wt.float()).view(n, ho, wo, cin)
+    torch.testing.assert_close(dx.float().view(n, h, w, cin), ref, atol=0.1, rtol=2e-2)
+    dw = C.gemm_tn(dy, x.reshape(-1, cin), torch.float32, b_map=geom)
+    torch.testing.assert_close(dw, dy.float().t() @ xs.float(), atol=1e-3 * dy.shape[0] ** 0.5, rtol=1e-2)
+
+
+def test_conv1x1_stride2_odd_spatial():
+    torch.manual_seed(3)
+    m = Conv1x1(32, 64, 2).cuda().bfloat16()
+    x = torch.randn(2, 32, 9, 11, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    xi = x.detach().requires_grad_()
+    xr = x.detach().float().requires_grad_()
+    wr = m.weight.detach().float().requires_grad_()
+    y = m(xi)
+    yr = F.conv2d(xr, wr, None, 2)
+    torch.testing.assert_close(y.float(), yr, atol=0.1, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=0.1, rtol=2e-2)
+    torch.testing.assert_close(m.weight.grad.float(), wr.grad, atol=0.5, rtol=2e-2)
