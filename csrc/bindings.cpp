@@ -46,6 +46,17 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const std::vector<int64_t>& c_map);
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map);
+std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int64_t kh,
+                                int64_t kw, int64_t stride, int64_t pad, int64_t ho, int64_t wo,
+                                bool transposed, const c10::optional<at::Tensor>& pro_scale,
+                                const c10::optional<at::Tensor>& pro_shift,
+                                const std::string& mode,
+                                const c10::optional<at::Tensor>& epi_scale,
+                                const c10::optional<at::Tensor>& epi_shift,
+                                const c10::optional<at::Tensor>& residual, bool relu);
+at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
+                      int64_t stride, int64_t pad, int64_t ho, int64_t wo,
+                      at::ScalarType out_dtype);
 // depthwise.hip
 std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                           bool moments);
@@ -81,6 +92,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{});
+
+  // ---- implicit-GEMM convolution (kh x kw taps) on the same MFMA kernels ----
+  m.def("conv_nt", &dmp::conv_nt, py::arg("x"), py::arg("wmat"), py::arg("kh"), py::arg("kw"),
+        py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"),
+        py::arg("transposed") = false, py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
+        py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
+        py::arg("residual") = py::none(), py::arg("relu") = false);
+  m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
+        py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"));
 
   // ---- depthwise 3x3 (NHWC) ----
   m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),

@@ -67,14 +67,47 @@ __device__ __forceinline__ int swz(int row, int kvec) {
   return row * (BK * 2) + ((kvec ^ ((row >> 1) & 7)) << 4);
 }
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool PRO_BN, int EPI>
-__global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
-    const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb,
-    bf16* __restrict__ C, int64_t ldc, int M, int N, int K,
-    const float* __restrict__ pro_s, const float* __restrict__ pro_t,
-    const float* __restrict__ epi_s, const float* __restrict__ epi_t,
-    const bf16* __restrict__ R, int64_t ldr, int epi_relu, float* __restrict__ part, RowMap amap,
-    RowMap cmap) {
+// Implicit-GEMM convolution geometry (kh x kw taps, NHWC activations).
+// GEMM rows are the pixels of the (ho, wo) grid; A is the (hi, wi) tensor.
+//   forward    : A pixel = (oh*stride - pad + r, ow*stride - pad + c)
+//   transposed : A pixel = ((oh + pad - r) / stride, ...) when divisible --
+//                the data gradient of a strided conv, no flipped weights.
+// kc = channels per tap (a multiple of BK so a K tile never straddles taps).
+struct ConvMap {
+  int kw = 1, stride = 1, pad = 0, hi = 1, wi = 1, ho = 1, wo = 1, kc = 0, transposed = 0;
+};
+
+struct NtArgs {
+  const bf16* A; int64_t lda;
+  const bf16* B; int64_t ldb;
+  bf16* C; int64_t ldc;
+  int M, N, K;
+  const float *pro_s, *pro_t;   // PRO_BN prologue (per A channel)
+  const float *epi_s, *epi_t;   // EPI_AFFINE (per output column)
+  const bf16* R; int64_t ldr;   // EPI_AFFINE residual
+  int epi_relu;
+  float* part;                  // EPI_MOMENTS partials [2][mtiles][N]
+  RowMap amap, cmap;            // strided 1x1 row maps (non-CONV)
+  ConvMap cv;                   // implicit-GEMM conv geometry (CONV)
+};
+
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool PRO_BN, int EPI, bool CONV>
+__global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
+  const bf16* __restrict__ A = p.A;
+  const bf16* __restrict__ B = p.B;
+  bf16* __restrict__ C = p.C;
+  const int64_t lda = p.lda, ldb = p.ldb, ldc = p.ldc, ldr = p.ldr;
+  const int M = p.M, N = p.N, K = p.K;
+  const float* __restrict__ pro_s = p.pro_s;
+  const float* __restrict__ pro_t = p.pro_t;
+  const float* __restrict__ epi_s = p.epi_s;
+  const float* __restrict__ epi_t = p.epi_t;
+  const bf16* __restrict__ R = p.R;
+  const int epi_relu = p.epi_relu;
+  float* __restrict__ part = p.part;
+  const RowMap& amap = p.amap;
+  const RowMap& cmap = p.cmap;
+  const ConvMap& cv = p.cv;
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int A_VECS = BM * BK / 8 / kThreads;  // 16-B vectors per thread per A tile
@@ -104,20 +137,68 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
   constexpr int ROWS_PER_PASS = kThreads / (BK / 8);
 
   bf16x8 ra[A_VECS], rb[B_VECS];
-  const bf16* arow[A_VECS];  // this thread's A rows are fixed for the whole K loop
+  // This thread's A rows are fixed for the whole K loop.  Plain / strided 1x1:
+  // one row pointer each.  Implicit-GEMM conv: the output pixel (n, oh, ow) of
+  // each row; the tap of a K tile picks the input pixel (or zero padding).
+  const bf16* arow[A_VECS];
+  int pn[A_VECS], ph[A_VECS], pw[A_VECS];
 #pragma unroll
   for (int i = 0; i < A_VECS; ++i) {
     const int row = m0 + r0 + i * ROWS_PER_PASS;
-    arow[i] = row < M ? A + map_row(amap, row) * lda : nullptr;
+    if constexpr (CONV) {
+      if (row < M) {
+        const int hw = cv.ho * cv.wo;
+        pn[i] = row / hw;
+        const int r = row - pn[i] * hw;
+        ph[i] = r / cv.wo;
+        pw[i] = r - ph[i] * cv.wo;
+      } else {
+        pn[i] = -1; ph[i] = pw[i] = 0;
+      }
+    } else {
+      arow[i] = row < M ? A + map_row(amap, row) * lda : nullptr;
+    }
   }
+  bool aval[A_VECS];
 
   auto load_tile = [&](int kt) {
     const int k = kt * BK + kv * 8;
     const bool kin = k < K;
+    int kch = k;  // channel index of this thread's 8-vector (prologue coefficients)
+    if constexpr (CONV) {
+      // K = taps * kc with kc % BK == 0: a K tile lies inside one tap
+      const int tap = (kt * BK) / cv.kc;
+      kch = k - tap * cv.kc;
+      const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
 #pragma unroll
-    for (int i = 0; i < A_VECS; ++i) {
-      if (kin && arow[i]) ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + k);
-      else ra[i] = bf16x8{};
+      for (int i = 0; i < A_VECS; ++i) {
+        int ih, iw;
+        bool ok = kin && pn[i] >= 0;
+        if (cv.transposed) {  // data gradient: input pixel (ph, pw) gathers dy at (ph+pad-r)/s
+          const int th = ph[i] + cv.pad - tr, tw = pw[i] + cv.pad - tc;
+          ih = th / cv.stride;
+          iw = tw / cv.stride;
+          ok = ok && th >= 0 && tw >= 0 && ih * cv.stride == th && iw * cv.stride == tw;
+        } else {
+          ih = ph[i] * cv.stride - cv.pad + tr;
+          iw = pw[i] * cv.stride - cv.pad + tc;
+          ok = ok && ih >= 0 && iw >= 0;
+        }
+        ok = ok && ih < cv.hi && iw < cv.wi;
+        aval[i] = ok;
+        if (ok)
+          ra[i] = *reinterpret_cast<const bf16x8*>(
+              A + (((int64_t)pn[i] * cv.hi + ih) * cv.wi + iw) * lda + kch);
+        else
+          ra[i] = bf16x8{};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_VECS; ++i) {
+        aval[i] = kin && arow[i];
+        if (aval[i]) ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + k);
+        else ra[i] = bf16x8{};
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_VECS; ++i) {
@@ -129,15 +210,14 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
       if (kin) {
         float s[8], t[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { s[j] = pro_s[k + j]; t[j] = pro_t[k + j]; }
+        for (int j = 0; j < 8; ++j) { s[j] = pro_s[kch + j]; t[j] = pro_t[kch + j]; }
 #pragma unroll
         for (int i = 0; i < A_VECS; ++i) {
-          const int row = m0 + r0 + i * ROWS_PER_PASS;
           f32x8 f = __builtin_convertvector(ra[i], f32x8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], s[j], t[j]), 0.f);
-          // rows beyond M stay exactly zero (they are never stored)
-          ra[i] = row < M ? __builtin_convertvector(f, bf16x8) : bf16x8{};
+          // rows beyond M and zero-padding taps stay exactly zero
+          ra[i] = aval[i] ? __builtin_convertvector(f, bf16x8) : bf16x8{};
         }
       }
     }
@@ -272,30 +352,21 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool PRO, int EPI>
-void launch(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int M, int N, int K,
-            const float* ps, const float* pt, const float* es, const float* et, const bf16* R,
-            int64_t ldr, bool relu, float* part, const RowMap& am, const RowMap& cm,
-            hipStream_t stream) {
-  const int mtiles = (M + BM - 1) / BM, ntiles = (N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI>), dim3(mtiles * ntiles),
-                     dim3(kThreads), 0, stream, reinterpret_cast<const bf16*>(A.data_ptr()),
-                     A.stride(0), reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0),
-                     reinterpret_cast<bf16*>(C.data_ptr()), C.stride(0), M, N, K, ps, pt, es, et, R,
-                     ldr, (int)relu, part, am, cm);
+template <int BM, int BN, int WM, int WN, bool PRO, int EPI, bool CONV>
+void launch(const NtArgs& a, hipStream_t stream) {
+  const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI, CONV>), dim3(mtiles * ntiles),
+                     dim3(kThreads), 0, stream, a);
 }
 
-template <bool PRO, int EPI>
-void dispatch_tile(const at::Tensor& A, const at::Tensor& B, at::Tensor& C, int M, int N, int K,
-                   const float* ps, const float* pt, const float* es, const float* et,
-                   const bf16* R, int64_t ldr, bool relu, float* part, const RowMap& am,
-                   const RowMap& cm, int bm, hipStream_t s) {
+template <bool PRO, int EPI, bool CONV>
+void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {
   // bm selects the M tile (128 or 256 rows) ; BN follows N.
-  if (N <= 64) {
-    if (bm == 256) launch<256, 64, 4, 1, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, am, cm, s);
-    else launch<128, 64, 2, 2, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, am, cm, s);
+  if (a.N <= 64) {
+    if (bm == 256) launch<256, 64, 4, 1, PRO, EPI, CONV>(a, s);
+    else launch<128, 64, 2, 2, PRO, EPI, CONV>(a, s);
   } else {
-    launch<128, 128, 2, 2, PRO, EPI>(A, B, C, M, N, K, ps, pt, es, et, R, ldr, relu, part, am, cm, s);
+    launch<128, 128, 2, 2, PRO, EPI, CONV>(a, s);
   }
 }
 
@@ -337,7 +408,7 @@ __device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
 template <int BNT, int BKT>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N,
-    int K, int64_t rows_per_split, float* __restrict__ part, RowMap bmap) {
+    int K, int64_t rows_per_split, float* __restrict__ part, ConvMap bmap) {
   // 4 waves as 2 x 2, each wave (BNT/2) x (BKT/2) outputs
   constexpr int WTN = BNT / 2, WTK = BKT / 2;
   constexpr int MI = WTN / 16, NI = WTK / 16;
@@ -359,6 +430,14 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
   const int64_t mb = (int64_t)split * rows_per_split;
   const int64_t me = min((int64_t)M, mb + rows_per_split);
   const int nstages = (int)((me - mb + TN_BM - 1) / TN_BM);
+  // implicit-GEMM wgrad: K = taps * kc, this block's K tile lies in one tap
+  int tr = 0, tc = 0, kc0 = k0;
+  if (bmap.kc != 0) {
+    const int tap = k0 / bmap.kc;
+    tr = tap / bmap.kw;
+    tc = tap - tr * bmap.kw;
+    kc0 = k0 - tap * bmap.kc;
+  }
 
   bf16x8 ra[A_VECS], rb[B_VECS];
   auto load = [&](int s) {
@@ -373,9 +452,21 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
     for (int i = 0; i < B_VECS; ++i) {
       const int v = tid + i * kThreads, r = v / B_VPR, c = (v % B_VPR) * 8;
       const int64_t m = m0 + r;
-      rb[i] = (m < me && k0 + c < K)
-                  ? *reinterpret_cast<const bf16x8*>(B + map_row(bmap, m) * ldb + k0 + c)
-                  : bf16x8{};
+      const bf16* src = nullptr;
+      if (m < me && k0 + c < K) {
+        if (bmap.kc == 0) {
+          src = B + m * ldb + k0 + c;
+        } else {  // conv input pixel feeding output pixel m through tap (tr, tc), or padding
+          const int hw = bmap.ho * bmap.wo;
+          const int n = (int)(m / hw);
+          const int rr = (int)(m - (int64_t)n * hw);
+          const int oh = rr / bmap.wo, ow = rr - oh * bmap.wo;
+          const int ih = oh * bmap.stride - bmap.pad + tr, iw = ow * bmap.stride - bmap.pad + tc;
+          if (ih >= 0 && iw >= 0 && ih < bmap.hi && iw < bmap.wi)
+            src = B + (((int64_t)n * bmap.hi + ih) * bmap.wi + iw) * ldb + kc0 + c;
+        }
+      }
+      rb[i] = src ? *reinterpret_cast<const bf16x8*>(src) : bf16x8{};
     }
   };
   auto store = [&](int buf) {
@@ -500,7 +591,7 @@ void check_operand(const at::Tensor& t, const char* name) {
 
 template <int BNT, int BKT>
 void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, float* part,
-               int splits, int64_t rps, const RowMap& bm, hipStream_t s) {
+               int splits, int64_t rps, const ConvMap& bm, hipStream_t s) {
   const int tiles = ((N + BNT - 1) / BNT) * ((K + BKT - 1) / BKT);
   hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT>), dim3(tiles * splits), dim3(kThreads), 0, s,
                      reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
@@ -509,27 +600,15 @@ void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, fl
 
 }  // namespace
 
-// Weight gradient of a 1x1 conv: C[N, K] = A^T B with A [M, N], B [M, K] (bf16,
-// row-major).  Output dtype bf16 or fp32.  b_map ([s, Ho, Wo, Hi, Wi]) reads
-// B's logical row m from the strided physical row (stride-s 1x1 conv input).
-at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
-                   const std::vector<int64_t>& b_map) {
-  check_operand(A, "A");
-  check_operand(B, "B");
-  const RowMap bmap = parse_map(b_map, "b_map");
-  if (bmap.s == 1) {
-    TORCH_CHECK(A.size(0) == B.size(0), "A/B M mismatch");
-  } else {
-    TORCH_CHECK(B.size(0) % ((int64_t)bmap.hi * bmap.wi) == 0 &&
-                    A.size(0) == B.size(0) / ((int64_t)bmap.hi * bmap.wi) * bmap.ho * bmap.wo,
-                "b_map does not match the A/B row counts");
-  }
-  const int M = (int)A.size(0), N = (int)A.size(1), K = (int)B.size(1);
-  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "N and K must be multiples of 8");
+namespace {
+
+// C[N, K] = sum_m A[m, :]^T Bmapped[m, :]  -> out [N, K] (bf16 or fp32)
+at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
+                  at::ScalarType out_dtype, const ConvMap& bmap, int kgran) {
   auto stream = at::hip::getCurrentHIPStream();
   auto out = at::empty({N, K}, A.options().dtype(out_dtype));
   if (M == 0) return out.zero_();
-  const int bnt = N >= 128 ? 128 : 64, bkt = K >= 128 ? 128 : 64;
+  const int bnt = N >= 128 ? 128 : 64, bkt = (K >= 128 && kgran % 128 == 0) ? 128 : 64;
   const int tiles = ((N + bnt - 1) / bnt) * ((K + bkt - 1) / bkt);
   // ~4 blocks per CU, but keep the fp32 partial traffic well under the operand
   // traffic (the GEMM streams (N+K)*M bf16; partials cost 2 * splits*N*K*4 B).
@@ -537,7 +616,10 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
   const int64_t operand_bytes = (int64_t)M * (N + K) * 2;
   const int64_t part_cap = std::max<int64_t>(operand_bytes / 4, 8 << 20);
   const int by_bytes = (int)std::max<int64_t>(1, part_cap / ((int64_t)N * K * 8));
-  int splits = std::min({max_splits, by_bytes, std::max(1, (1024 + tiles - 1) / tiles)});
+  // at least ~2 blocks per CU even when that exceeds the byte budget (big N*K
+  // with few tiles would otherwise leave most of the 256 CUs idle)
+  const int fill = (512 + tiles - 1) / tiles, target = (1024 + tiles - 1) / tiles;
+  int splits = std::min(max_splits, std::max({1, fill, std::min(by_bytes, target)}));
   int64_t rps = ((int64_t)M + splits - 1) / splits;
   rps = (rps + TN_BM - 1) / TN_BM * TN_BM;
   splits = (int)(((int64_t)M + rps - 1) / rps);
@@ -560,11 +642,132 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
   return out;
 }
 
+}  // namespace
+
+// Weight gradient of a 1x1 conv: C[N, K] = A^T B with A [M, N], B [M, K] (bf16,
+// row-major).  Output dtype bf16 or fp32.  b_map ([s, Ho, Wo, Hi, Wi]) reads
+// B's logical row m from the strided physical row (stride-s 1x1 conv input).
+at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
+                   const std::vector<int64_t>& b_map) {
+  check_operand(A, "A");
+  check_operand(B, "B");
+  const RowMap rm = parse_map(b_map, "b_map");
+  ConvMap cm;  // kc == 0: identity rows
+  if (rm.s == 1) {
+    TORCH_CHECK(A.size(0) == B.size(0), "A/B M mismatch");
+  } else {
+    TORCH_CHECK(B.size(0) % ((int64_t)rm.hi * rm.wi) == 0 &&
+                    A.size(0) == B.size(0) / ((int64_t)rm.hi * rm.wi) * rm.ho * rm.wo,
+                "b_map does not match the A/B row counts");
+    cm.kw = 1; cm.stride = rm.s; cm.pad = 0;
+    cm.hi = rm.hi; cm.wi = rm.wi; cm.ho = rm.ho; cm.wo = rm.wo;
+    cm.kc = (int)B.size(1);
+  }
+  const int M = (int)A.size(0), N = (int)A.size(1), K = (int)B.size(1);
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "N and K must be multiples of 8");
+  return run_tn(A, B, M, N, K, out_dtype, cm, 128);
+}
+
+// Weight gradient of an implicit-GEMM conv: dy [N*Ho*Wo, Cout] rows, x NHWC
+// [N, Hi, Wi, Cin] -> dW [Cout, kh*kw*Cin] (channels_last weight memory).
+at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
+                      int64_t stride, int64_t pad, int64_t ho, int64_t wo,
+                      at::ScalarType out_dtype) {
+  check_operand(dy, "dy");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "x must be a channels_last bf16 GPU tensor");
+  const int64_t nb = x.size(0), cin = x.size(1);
+  TORCH_CHECK(cin % 64 == 0, "conv_wgrad needs input channels % 64 == 0");
+  TORCH_CHECK(dy.size(0) == nb * ho * wo, "dy rows must be N*Ho*Wo");
+  TORCH_CHECK(dy.size(1) % 8 == 0, "output channels must be a multiple of 8");
+  ConvMap cm;
+  cm.kw = (int)kw; cm.stride = (int)stride; cm.pad = (int)pad;
+  cm.hi = (int)x.size(2); cm.wi = (int)x.size(3); cm.ho = (int)ho; cm.wo = (int)wo;
+  cm.kc = (int)cin;
+  const int M = (int)dy.size(0), N = (int)dy.size(1), K = (int)(kh * kw * cin);
+  // B rows are addressed through the map; ldb = Cin
+  auto xv = x.permute({0, 2, 3, 1}).reshape({-1, cin});
+  return run_tn(dy, xv, M, N, K, out_dtype, cm, (int)(cin % 128 == 0 ? 128 : 64));
+}
+
+namespace {
+
+template <bool CONV>
+void dispatch_mode(const NtArgs& a, bool pro, int epi, int bm, hipStream_t s) {
+  if (epi == EPI_STORE) {
+    if (pro) dispatch_tile<true, EPI_STORE, CONV>(a, bm, s);
+    else dispatch_tile<false, EPI_STORE, CONV>(a, bm, s);
+  } else if (epi == EPI_MOMENTS) {
+    if (pro) dispatch_tile<true, EPI_MOMENTS, CONV>(a, bm, s);
+    else dispatch_tile<false, EPI_MOMENTS, CONV>(a, bm, s);
+  } else {
+    if (pro) dispatch_tile<true, EPI_AFFINE, CONV>(a, bm, s);
+    else dispatch_tile<false, EPI_AFFINE, CONV>(a, bm, s);
+  }
+}
+
+// Shared tail of gemm_nt / conv_nt: prologue / epilogue arguments, launch,
+// moments reduction.  a.A/B/C, M/N/K and the maps are already set.
+std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
+                               const c10::optional<at::Tensor>& pro_scale,
+                               const c10::optional<at::Tensor>& pro_shift, const std::string& mode,
+                               const c10::optional<at::Tensor>& epi_scale,
+                               const c10::optional<at::Tensor>& epi_shift,
+                               const c10::optional<at::Tensor>& residual, bool relu,
+                               at::Tensor C) {
+  auto stream = at::hip::getCurrentHIPStream();
+  const bool pro = pro_scale.has_value() && pro_scale->defined();
+  if (pro) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined(), "prologue needs scale and shift");
+    TORCH_CHECK(pro_scale->scalar_type() == at::kFloat && pro_shift->scalar_type() == at::kFloat,
+                "prologue coefficients must be fp32");
+  }
+  a.pro_s = pro ? pro_scale->data_ptr<float>() : nullptr;
+  a.pro_t = pro ? pro_shift->data_ptr<float>() : nullptr;
+  at::Tensor moments;
+  if (a.M == 0) return {C, moments};
+  const int bm = tile_m_for(a.N);
+  int epi = EPI_STORE;
+  at::Tensor part;
+  if (mode == "store") {
+  } else if (mode == "moments") {
+    epi = EPI_MOMENTS;
+    const int mtiles = (a.M + bm - 1) / bm;
+    part = at::empty({2, mtiles, a.N}, like.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+    moments = at::empty({2 * (int64_t)a.N + 1}, like.options().dtype(at::kDouble));
+  } else if (mode == "affine") {
+    epi = EPI_AFFINE;
+    TORCH_CHECK(epi_scale.has_value() && epi_shift.has_value(), "affine epilogue needs scale/shift");
+    a.epi_s = epi_scale->data_ptr<float>();
+    a.epi_t = epi_shift->data_ptr<float>();
+    if (residual.has_value() && residual->defined()) {
+      check_operand(*residual, "residual");
+      TORCH_CHECK(residual->size(0) == a.M && residual->size(1) == a.N, "residual shape");
+      a.R = reinterpret_cast<const bf16*>(residual->data_ptr());
+      a.ldr = residual->stride(0);
+    }
+    a.epi_relu = relu;
+  } else {
+    TORCH_CHECK(false, "unknown epilogue mode ", mode);
+  }
+  if (conv) dispatch_mode<true>(a, pro, epi, bm, stream);
+  else dispatch_mode<false>(a, pro, epi, bm, stream);
+  if (epi == EPI_MOMENTS)
+    bn_reduce_partials_launch(a.part, (a.M + bm - 1) / bm, a.N, moments.data_ptr<double>(),
+                              (double)a.M, stream);
+  return {C, moments};
+}
+
+}  // namespace
+
 // C = prologue(A) @ B^T with an optional fused epilogue.  Returns (C, moments-or-undefined).
 //   A [M, K] bf16, B [N, K] bf16 (both K-contiguous), K % 8 == 0, N % 8 == 0.
 //   pro_scale/pro_shift [K] fp32: A' = relu(A*s + t)
 //   mode "store" | "moments" (returns fp64 [2N+1] = (sum, sumsq, M)) | "affine"
 //   (epi_scale/epi_shift [N], optional residual [M, N], relu flag).
+//   a_map / c_map: [s, Ho, Wo, Hi, Wi] strided row maps for A reads / C writes.
 std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& pro_scale,
                                 const c10::optional<at::Tensor>& pro_shift, const std::string& mode,
@@ -575,57 +778,91 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const std::vector<int64_t>& c_map) {
   check_operand(A, "A");
   check_operand(B, "B");
-  const RowMap am = parse_map(a_map, "a_map"), cm = parse_map(c_map, "c_map");
+  NtArgs a{};
+  a.amap = parse_map(a_map, "a_map");
+  a.cmap = parse_map(c_map, "c_map");
+  const RowMap& am = a.amap;
+  const RowMap& cm = a.cmap;
   int64_t m64 = A.size(0);
   if (am.s != 1) {
     TORCH_CHECK(m64 % ((int64_t)am.hi * am.wi) == 0, "a_map does not match A's rows");
     m64 = m64 / ((int64_t)am.hi * am.wi) * am.ho * am.wo;
   }
-  const int M = (int)m64, K = (int)A.size(1), N = (int)B.size(0);
-  TORCH_CHECK(B.size(1) == K, "A/B K mismatch");
-  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "K and N must be multiples of 8");
-  auto stream = at::hip::getCurrentHIPStream();
+  a.M = (int)m64;
+  a.K = (int)A.size(1);
+  a.N = (int)B.size(0);
+  TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
+  TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
+  if (pro_scale.has_value() && pro_scale->defined())
+    TORCH_CHECK(pro_scale->numel() == a.K, "prologue coefficients must have K entries");
   at::Tensor C;
   if (cm.s == 1) {
-    C = at::empty({M, N}, A.options());
+    C = at::empty({a.M, a.N}, A.options());
   } else {
     // rows the strided scatter does not reach are exactly zero (dgrad of a strided 1x1 conv)
-    TORCH_CHECK(M % ((int64_t)cm.ho * cm.wo) == 0, "c_map does not match the GEMM rows");
-    C = at::zeros({(int64_t)M / ((int64_t)cm.ho * cm.wo) * cm.hi * cm.wi, N}, A.options());
+    TORCH_CHECK(a.M % ((int64_t)cm.ho * cm.wo) == 0, "c_map does not match the GEMM rows");
+    C = at::zeros({(int64_t)a.M / ((int64_t)cm.ho * cm.wo) * cm.hi * cm.wi, a.N}, A.options());
   }
-  const bool pro = pro_scale.has_value() && pro_scale->defined();
-  const float* ps = pro ? pro_scale->data_ptr<float>() : nullptr;
-  const float* pt = pro ? pro_shift->data_ptr<float>() : nullptr;
-  at::Tensor moments;
-  if (M == 0) return {C, moments};
-  const int bm = tile_m_for(N);
-  if (mode == "store") {
-    if (pro) dispatch_tile<true, EPI_STORE>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, nullptr, am, cm, bm, stream);
-    else dispatch_tile<false, EPI_STORE>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, nullptr, am, cm, bm, stream);
-  } else if (mode == "moments") {
-    const int mtiles = (M + bm - 1) / bm;
-    auto part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
-    if (pro) dispatch_tile<true, EPI_MOMENTS>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, part.data_ptr<float>(), am, cm, bm, stream);
-    else dispatch_tile<false, EPI_MOMENTS>(A, B, C, M, N, K, ps, pt, nullptr, nullptr, nullptr, 0, false, part.data_ptr<float>(), am, cm, bm, stream);
-    moments = at::empty({2 * (int64_t)N + 1}, A.options().dtype(at::kDouble));
-    bn_reduce_partials_launch(part.data_ptr<float>(), mtiles, N, moments.data_ptr<double>(),
-                              (double)M, stream);
-  } else if (mode == "affine") {
-    TORCH_CHECK(epi_scale.has_value() && epi_shift.has_value(), "affine epilogue needs scale/shift");
-    const bf16* R = nullptr;
-    int64_t ldr = 0;
-    if (residual.has_value() && residual->defined()) {
-      check_operand(*residual, "residual");
-      TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "residual shape");
-      R = reinterpret_cast<const bf16*>(residual->data_ptr());
-      ldr = residual->stride(0);
-    }
-    if (pro) dispatch_tile<true, EPI_AFFINE>(A, B, C, M, N, K, ps, pt, epi_scale->data_ptr<float>(), epi_shift->data_ptr<float>(), R, ldr, relu, nullptr, am, cm, bm, stream);
-    else dispatch_tile<false, EPI_AFFINE>(A, B, C, M, N, K, ps, pt, epi_scale->data_ptr<float>(), epi_shift->data_ptr<float>(), R, ldr, relu, nullptr, am, cm, bm, stream);
-  } else {
-    TORCH_CHECK(false, "unknown epilogue mode ", mode);
-  }
-  return {C, moments};
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr());
+  a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr());
+  a.ldb = B.stride(0);
+  a.C = reinterpret_cast<bf16*>(C.data_ptr());
+  a.ldc = C.stride(0);
+  return run_nt(a, false, A, pro_scale, pro_shift, mode, epi_scale, epi_shift, residual, relu, C);
+}
+
+// Implicit-GEMM convolution on NHWC bf16 activations (kh x kw taps, any
+// stride / padding), MFMA NT kernel with the tap gather in the A staging:
+//   x    [N, Hi, Wi, Cin] (rows of Cin, channels_last memory)
+//   wmat [Cout, kh*kw*Cin] (channels_last weight memory: [Cout][kh][kw][Cin])
+//   -> y [N*Ho*Wo, Cout] (+ moments / affine epilogue like gemm_nt).
+// transposed=true computes the data gradient of a conv with geometry
+// (stride, pad): x is dy on the (hi, wi) grid, the output grid (ho, wo) is the
+// conv input, wmat is [Cin][kh][kw][Cout] (weight permuted, not flipped).
+// Cin % 64 == 0 (a K tile of 64 never straddles two taps).
+std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int64_t kh,
+                                int64_t kw, int64_t stride, int64_t pad, int64_t ho, int64_t wo,
+                                bool transposed,
+                                const c10::optional<at::Tensor>& pro_scale,
+                                const c10::optional<at::Tensor>& pro_shift,
+                                const std::string& mode,
+                                const c10::optional<at::Tensor>& epi_scale,
+                                const c10::optional<at::Tensor>& epi_shift,
+                                const c10::optional<at::Tensor>& residual, bool relu) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4,
+              "x must be a 4-D bf16 GPU tensor");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last");
+  check_operand(wmat, "wmat");
+  const int64_t nb = x.size(0), cin = x.size(1), hi = x.size(2), wi = x.size(3);
+  TORCH_CHECK(cin % BK == 0, "conv_nt needs input channels % 64 == 0");
+  TORCH_CHECK(wmat.size(1) == kh * kw * cin, "wmat must be [Cout, kh*kw*Cin]");
+  TORCH_CHECK(wmat.size(0) % 8 == 0, "output channels must be a multiple of 8");
+  TORCH_CHECK(ho > 0 && wo > 0 && stride >= 1 && pad >= 0, "bad conv geometry");
+  if (pro_scale.has_value() && pro_scale->defined())
+    TORCH_CHECK(pro_scale->numel() == cin, "prologue coefficients must have Cin entries");
+  NtArgs a{};
+  a.cv.kw = (int)kw;
+  a.cv.stride = (int)stride;
+  a.cv.pad = (int)pad;
+  a.cv.hi = (int)hi;
+  a.cv.wi = (int)wi;
+  a.cv.ho = (int)ho;
+  a.cv.wo = (int)wo;
+  a.cv.kc = (int)cin;
+  a.cv.transposed = transposed;
+  TORCH_CHECK(nb * ho * wo < (1LL << 31), "too many output pixels");
+  a.M = (int)(nb * ho * wo);
+  a.N = (int)wmat.size(0);
+  a.K = (int)(kh * kw * cin);
+  auto C = at::empty({a.M, a.N}, x.options());
+  a.A = reinterpret_cast<const bf16*>(x.data_ptr());
+  a.lda = cin;
+  a.B = reinterpret_cast<const bf16*>(wmat.data_ptr());
+  a.ldb = wmat.stride(0);
+  a.C = reinterpret_cast<bf16*>(C.data_ptr());
+  a.ldc = C.stride(0);
+  return run_nt(a, true, x, pro_scale, pro_shift, mode, epi_scale, epi_shift, residual, relu, C);
 }
 
 }  // namespace dmp

@@ -19,11 +19,13 @@ import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
+from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import conv_bn
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
-    return nn.Conv2d(cin, cout, 3, stride=stride, padding=1, bias=False)
+    # implicit-GEMM MFMA conv on MI355X (channels-last bf16, Cin % 64 == 0), BN moments fused
+    return ConvIG2d(cin, cout, 3, stride=stride, padding=1)
 
 
 def _conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -53,8 +55,8 @@ class BasicBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = _shortcut(self.downsample, x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), identity)
+        out = conv_bn(self.conv1, self.bn1, x)
+        return conv_bn(self.conv2, self.bn2, out, identity)
 
 
 class Bottleneck(nn.Module):
@@ -74,7 +76,7 @@ class Bottleneck(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         identity = _shortcut(self.downsample, x)
         out = conv_bn(self.conv1, self.bn1, x)
-        out = self.bn2(self.conv2(out))
+        out = conv_bn(self.conv2, self.bn2, out)
         return conv_bn(self.conv3, self.bn3, out, identity)
 
 

@@ -1,0 +1,130 @@
+"""kh x kw convolution (ResNet's 3x3s) as an implicit GEMM on our MFMA kernels
+(``csrc/conv/gemm_bf16.hip`` ``conv_nt`` / ``conv_wgrad``), optionally
+emitting the BatchNorm moments of its output like the 1x1 path.
+
+  forward   y[N*Ho*Wo, Cout] = im2col(x) @ W^T      tap gather in the A staging,
+            K = kh*kw*Cin, W read in its channels_last memory [Cout][kh][kw][Cin]
+  (backward defaults to MIOpen -- see NATIVE_BWD -- our kernels below are
+   selectable and tested)
+  dgrad     dx = "transposed" implicit GEMM over dy with W permuted to
+            [Cin][kh][kw][Cout] (no flip; strided convs handled by the
+            divisibility test in the gather)
+  wgrad     dW[Cout, kh*kw*Cin] = dy^T @ im2col(x)   split-M TN kernel with the
+            tap gather in its B staging (channels_last weight memory directly)
+
+Native for bf16 channels_last activations with Cin % 64 == 0 and Cout % 64 == 0
+(every ResNet 3x3 except the 7x7 stem, which stays on MIOpen); anything else
+uses ``F.conv2d``.  The reference uses torchvision's cuDNN convolutions
+(torchvision.models.resnet50 in the DDP scripts).
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _native
+
+_STATS = {"native": 0, "torch": 0}
+# DMP_IGEMM=0 routes these convs to MIOpen (A/B comparisons, debugging)
+ENABLED = os.environ.get("DMP_IGEMM", "1") != "0"
+# Backward on our kernels (DMP_IGEMM_BWD=1) or MIOpen (default).  Measured on
+# MI355X at the ResNet-50 bs256 shapes (profiles/conv3x3_igemm.md): our forward
+# beats MIOpen at every shape (and emits the BN moments for free); MIOpen's
+# data / weight gradients are still faster (stride-2 dgrad by ~3x: our
+# transposed gather multiplies zero taps).
+NATIVE_BWD = os.environ.get("DMP_IGEMM_BWD", "0") == "1"
+
+
+def _out_size(h: int, k: int, s: int, p: int) -> int:
+    return (h + 2 * p - k) // s + 1
+
+
+def _native_ok(x: torch.Tensor, w: torch.Tensor, groups: int, dilation) -> bool:
+    if not ENABLED or not _native.gpu_path(x):
+        return False
+    return (groups == 1 and tuple(dilation) == (1, 1) and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 64 == 0
+            and w.shape[0] % 64 == 0 and x.is_contiguous(memory_format=torch.channels_last))
+
+
+def _wmat(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin, kh, kw] -> [Cout, kh*kw*Cin] (a view for channels_last weights)."""
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+
+class _ConvIGFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride, pad, moments):
+        C = _native.require("conv_igemm")
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        ho, wo = _out_size(h, kh, stride, pad), _out_size(w, kw, stride, pad)
+        y2, mom = C.conv_nt(x, _wmat(weight), kh, kw, stride, pad, ho, wo,
+                            mode="moments" if moments else "store")
+        ctx.save_for_backward(x, weight)
+        ctx.geo = (stride, pad, ho, wo)
+        if mom is None:
+            mom = torch.empty(0, device=x.device, dtype=torch.float64)
+        ctx.mark_non_differentiable(mom)
+        return y2.view(n, ho, wo, cout).permute(0, 3, 1, 2), mom
+
+    @staticmethod
+    def backward(ctx, dy, _dmom):
+        x, weight = ctx.saved_tensors
+        C = _native.require("conv_igemm backward")
+        stride, pad, ho, wo = ctx.geo
+        n, cin, h, w = x.shape
+        cout, _, kh, kw = weight.shape
+        dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if not NATIVE_BWD:
+            dx, dw, _ = torch.ops.aten.convolution_backward(
+                dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
+            return dx, dw, None, None, None
+        if ctx.needs_input_grad[0]:
+            wt = weight.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()  # [Cin][kh][kw][Cout]
+            dx2, _ = C.conv_nt(dy, wt, kh, kw, stride, pad, h, w, transposed=True)
+            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+            g = C.conv_wgrad(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
+            dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
+            if not weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous()
+        return dx, dw, None, None, None
+
+
+def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0,
+                 moments: bool = False, groups: int = 1,
+                 dilation=(1, 1)) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
+    if _native_ok(x, weight, groups, dilation):
+        _STATS["native"] += 1
+        y, mom = _ConvIGFn.apply(x, weight, stride, padding, moments)
+        return y, (mom if moments else None)
+    _STATS["torch"] += 1
+    return F.conv2d(x, weight, None, stride, padding, dilation, groups), None
+
+
+class ConvIG2d(nn.Conv2d):
+    """Drop-in bias-free ``nn.Conv2d`` (square kernel, symmetric padding) routed
+    through the implicit-GEMM MFMA kernels when the shape allows."""
+
+    def __init__(self, cin: int, cout: int, kernel_size: int, stride: int = 1, padding: int = 0,
+                 device=None, dtype=None):
+        super().__init__(cin, cout, kernel_size, stride=stride, padding=padding, bias=False,
+                         device=device, dtype=dtype)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return conv2d_igemm(x, self.weight, self.stride[0], self.padding[0], False,
+                            self.groups, self.dilation)[0]
+
+    def forward_with_moments(self, x: torch.Tensor):
+        return conv2d_igemm(x, self.weight, self.stride[0], self.padding[0], True,
+                            self.groups, self.dilation)

@@ -63,7 +63,7 @@ def main():
         print(f"{k:45s} {v:10.3f}")
 
 
-if __name__ == "__main__" and "--gemm" not in sys.argv:
+if __name__ == "__main__" and "--gemm" not in sys.argv and "--conv" not in sys.argv:
     main()
 
 
@@ -72,7 +72,8 @@ def gemm_bench():
     from distributed_model_parallel_amd import _native
     C = _native.require("gemm bench")
     dev, dt = "cuda", torch.bfloat16
-    shapes = [(802816, 256, 64), (802816, 64, 256), (200704, 512, 128), (200704, 128, 512),
+    shapes = [(8192, 8192, 8192), (802816, 64, 576), (200704, 128, 1152), (50176, 256, 2304),
+              (802816, 256, 64), (802816, 64, 256), (200704, 512, 128), (200704, 128, 512),
               (50176, 1024, 256), (50176, 256, 1024), (12544, 2048, 512), (12544, 512, 2048)]
     print(f"{'M':>7} {'N':>5} {'K':>5} | {'ours':>8} {'ours+mom':>8} {'miopen':>8} {'blaslt':>8}  ms | ours TB/s  TF/s")
     for M, N, K in shapes:
@@ -80,15 +81,44 @@ def gemm_bench():
         w = torch.randn(N, K, device=dev, dtype=dt)
         t_o = timeit(lambda: C.gemm_nt(a, w))
         t_m = timeit(lambda: C.gemm_nt(a, w, mode="moments"))
-        x4 = a.view(M // 3136 if M % 3136 == 0 else 1, -1, 1, K) if False else None
-        hw = {802816: 56, 200704: 28, 50176: 14, 12544: 7}[M]
-        x = a.view(256, hw, hw, K).permute(0, 3, 1, 2)
-        w4 = w.view(N, K, 1, 1).contiguous(memory_format=torch.channels_last)
-        t_c = timeit(lambda: F.conv2d(x, w4))
+        hw = {802816: 56, 200704: 28, 50176: 14, 12544: 7}.get(M)
+        t_c = float("nan")
+        if hw:
+            x = a.view(256, hw, hw, K).permute(0, 3, 1, 2)
+            w4 = w.view(N, K, 1, 1).contiguous(memory_format=torch.channels_last)
+            t_c = timeit(lambda: F.conv2d(x, w4))
         t_b = timeit(lambda: a @ w.t())
         by = 2 * (M * K + N * K + M * N)
         print(f"{M:7d} {N:5d} {K:5d} | {t_o:8.3f} {t_m:8.3f} {t_c:8.3f} {t_b:8.3f}     | {by / t_o / 1e9:6.2f} {2 * M * N * K / t_o / 1e9:7.1f}")
 
 
+def conv_bench():
+    """Implicit-GEMM 3x3 conv (ours) vs MIOpen on the ResNet-50 bs256 3x3 shapes:
+    forward, data gradient, weight gradient."""
+    from distributed_model_parallel_amd import _native
+    from distributed_model_parallel_amd.ops.conv_igemm import _wmat
+    C = _native.require("conv bench")
+    dev, dt, cl = "cuda", torch.bfloat16, torch.channels_last
+    shapes = [(64, 56, 1), (128, 56, 2), (128, 28, 1), (256, 28, 2), (256, 14, 1), (512, 14, 2), (512, 7, 1)]
+    print(f"{'C':>4} {'H':>3} {'s':>2} | {'fwd':>7} {'miopen':>7} | {'dgrad':>7} {'miopen':>7} | {'wgrad':>7} {'miopen':>7} ms | fwd TF/s")
+    for c, h, s in shapes:
+        x = torch.randn(256, c, h, h, device=dev, dtype=dt).contiguous(memory_format=cl)
+        w = (torch.randn(c, c, 3, 3, device=dev, dtype=dt) * 0.05).contiguous(memory_format=cl)
+        ho = (h + 2 - 3) // s + 1
+        dy = torch.randn(256, c, ho, ho, device=dev, dtype=dt).contiguous(memory_format=cl)
+        t_f = timeit(lambda: C.conv_nt(x, _wmat(w), 3, 3, s, 1, ho, ho))
+        t_fm = timeit(lambda: F.conv2d(x, w, None, s, 1))
+        wt = w.permute(1, 2, 3, 0).reshape(c, -1).contiguous()
+        t_d = timeit(lambda: C.conv_nt(dy, wt, 3, 3, s, 1, h, h, transposed=True))
+        t_dm = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (1, 1), (1, 1), False, (0, 0), 1, (True, False, False)))
+        dy2 = dy.permute(0, 2, 3, 1).reshape(-1, c)
+        t_w = timeit(lambda: C.conv_wgrad(dy2, x, 3, 3, s, 1, ho, ho, dt))
+        t_wm = timeit(lambda: torch.ops.aten.convolution_backward(dy, x, w, None, (s, s), (1, 1), (1, 1), False, (0, 0), 1, (False, True, False)))
+        fl = 2 * 256 * ho * ho * c * c * 9
+        print(f"{c:4d} {h:3d} {s:2d} | {t_f:7.3f} {t_fm:7.3f} | {t_d:7.3f} {t_dm:7.3f} | {t_w:7.3f} {t_wm:7.3f}    | {fl / t_f / 1e9:7.1f}")
+
+
 if __name__ == "__main__" and "--gemm" in sys.argv:
     gemm_bench()
+if __name__ == "__main__" and "--conv" in sys.argv:
+    conv_bench()
