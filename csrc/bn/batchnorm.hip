@@ -88,8 +88,9 @@ __device__ __forceinline__ void block_combine_store(const float (&s)[VEC], const
 // channels) folds kRedRows partial rows.  With one row-chunk the block stores
 // the result (deterministic); otherwise the caller zeroes sums and each chunk
 // adds with an fp64 atomic (<= rb/kRedRows adds per address, so no same-address
-// serialisation worth speaking of).  Writes sums[2C] = count when count >= 0.
-constexpr int kRedCh = 32, kRedGroups = 32, kRedRows = 256;
+// serialisation worth speaking of; the producer zeroed sums, see common.h).
+// Writes sums[2C] = count when count >= 0.
+constexpr int kRedCh = 32, kRedGroups = 32, kRedRows = kBnRedRows;
 __global__ __launch_bounds__(1024) void bn_reduce_partials_kernel(const float* __restrict__ part,
                                                                   int rb, int C,
                                                                   double* __restrict__ sums,
@@ -142,7 +143,9 @@ __global__ __launch_bounds__(1024) void bn_reduce_partials_kernel(const float* _
 // -------------------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_moments_kernel(
-    const T* __restrict__ x, int64_t M, int C, int64_t rows_per_block, float* __restrict__ part) {
+    const T* __restrict__ x, int64_t M, int C, int64_t rows_per_block, float* __restrict__ part,
+    double* __restrict__ zsums) {
+  zero_moments(zsums, 2 * C);
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -290,7 +293,8 @@ template <typename T, bool RELU>
 __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block,
-    float* __restrict__ part) {
+    float* __restrict__ part, double* __restrict__ zsums) {
+  zero_moments(zsums, 2 * C);
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -440,9 +444,7 @@ float* fptr(const c10::optional<at::Tensor>& t) {
 // Shared with the GEMM moments epilogue (csrc/conv/gemm_bf16.hip).
 void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
                                hipStream_t stream) {
-  const int chunks = (rb + kRedRows - 1) / kRedRows;
-  if (chunks > 1)
-    DMP_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(double) * 2 * (size_t)C, stream));
+  const int chunks = (rb + kRedRows - 1) / kRedRows;  // > 1: producer zeroed sums
   hipLaunchKernelGGL(bn_reduce_partials_kernel, dim3((C + kRedCh - 1) / kRedCh, chunks), dim3(1024),
                      0, stream, part, rb, C, sums, count);
 }
@@ -459,7 +461,8 @@ at::Tensor bn_local_moments(const at::Tensor& x, int64_t C) {
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL(bn_moments_kernel<T>, g.grid, dim3(kThreads), 0, stream, ptr<T>(x), M,
-                       (int)C, g.rows_per_block, part.data_ptr<float>());
+                       (int)C, g.rows_per_block, part.data_ptr<float>(),
+                       moments_zero_target(sums.data_ptr<double>(), (int)g.grid.x));
   });
   bn_reduce_partials_launch(part.data_ptr<float>(), (int)g.grid.x, (int)C, sums.data_ptr<double>(),
                             (double)M, stream);
@@ -553,17 +556,18 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
   Grid g = plan(M, (int)C, vec_of(x));
   auto part = at::empty({2, (int64_t)g.grid.x, C}, x.options().dtype(at::kFloat));
   float* pp = part.data_ptr<float>();
+  double* zt = moments_zero_target(sums.data_ptr<double>(), (int)g.grid.x);
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
     if (relu) {
       TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
       hipLaunchKernelGGL((bn_bwd_moments_kernel<T, true>), g.grid, dim3(kThreads), 0, stream,
                          ptr<T>(dy), ptr<T>(x), ptr<T>(*y), mean.data_ptr<float>(), M, (int)C,
-                         g.rows_per_block, pp);
+                         g.rows_per_block, pp, zt);
     } else {
       hipLaunchKernelGGL((bn_bwd_moments_kernel<T, false>), g.grid, dim3(kThreads), 0, stream,
                          ptr<T>(dy), ptr<T>(x), (const T*)nullptr, mean.data_ptr<float>(), M,
-                         (int)C, g.rows_per_block, pp);
+                         (int)C, g.rows_per_block, pp, zt);
     }
   });
   bn_reduce_partials_launch(pp, (int)g.grid.x, (int)C, sums.data_ptr<double>(), -1.0, stream);

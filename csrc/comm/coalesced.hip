@@ -173,7 +173,12 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
   for (size_t i = 0; i < srcs.size(); ++i) {
     const auto& s = srcs[i];
     const auto& d = dsts[i];
-    TORCH_CHECK(s.is_contiguous() && d.is_contiguous(), "multi_copy needs contiguous tensors");
+    // raw byte copy: both contiguous, or both dense with identical shape/strides
+    // (e.g. channels_last grads into channels_last bucket views)
+    TORCH_CHECK((s.is_contiguous() && d.is_contiguous()) ||
+                    (s.is_non_overlapping_and_dense() && d.is_non_overlapping_and_dense() &&
+                     s.sizes() == d.sizes() && s.strides() == d.strides()),
+                "multi_copy needs contiguous tensors or dense ones with identical strides");
     const int64_t nb = s.numel() * s.element_size();
     TORCH_CHECK(nb == d.numel() * d.element_size(), "multi_copy: byte size mismatch at ", i);
     TORCH_CHECK(d.device() == dev, "multi_copy: all destinations must share one device");

@@ -69,6 +69,18 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// ---- BN moments plumbing shared by every producer of [2][rb][C] partials ----
+// bn_reduce_partials_launch (batchnorm.hip) folds the partial rows in chunks of
+// kBnRedRows; with more than one chunk it accumulates into sums with fp64
+// atomics, so sums[0:2C] must be zero first.  The PRODUCER kernel zeroes it
+// (block 0, before the reduce launch in stream order) -- no memset launch.
+constexpr int kBnRedRows = 256;
+inline double* moments_zero_target(double* sums, int rb) { return rb > kBnRedRows ? sums : nullptr; }
+__device__ __forceinline__ void zero_moments(double* z, int n) {
+  if (z != nullptr && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < n; i += blockDim.x) z[i] = 0.0;
+}
+
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5.5 T1):
 // consecutive logical tiles land on the same XCD (same L2).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

@@ -56,7 +56,9 @@ template <typename T, bool MOMENTS>
 __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ x,
                                                          const float* __restrict__ w9,
                                                          T* __restrict__ y, Geo g,
-                                                         float* __restrict__ part) {
+                                                         float* __restrict__ part,
+                                                         double* __restrict__ zsums) {
+  if (MOMENTS) zero_moments(zsums, 2 * g.C);
   constexpr int VEC = Vec16<T>::N;
   const int tid = threadIdx.x;
   const int lc = tid % g.tc, ls = tid / g.tc;
@@ -384,20 +386,24 @@ std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor&
   const int cchunks = (g.cv + g.tc - 1) / g.tc;
   dim3 grid((unsigned)((total + g.spp - 1) / g.spp), (unsigned)cchunks);
   at::Tensor mom, part;
-  if (moments) part = at::empty({2, (int64_t)grid.x, g.C}, x.options().dtype(at::kFloat));
+  double* zt = nullptr;
+  if (moments) {
+    part = at::empty({2, (int64_t)grid.x, g.C}, x.options().dtype(at::kFloat));
+    mom = at::empty({2 * (int64_t)g.C + 1}, x.options().dtype(at::kDouble));
+    zt = moments_zero_target(mom.data_ptr<double>(), (int)grid.x);
+  }
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
     if (moments)
       hipLaunchKernelGGL((dw_fwd_kernel<T, true>), grid, dim3(kThreads), 0, stream,
                          reinterpret_cast<const T*>(x.data_ptr()), w9.data_ptr<float>(),
-                         reinterpret_cast<T*>(y.data_ptr()), g, part.data_ptr<float>());
+                         reinterpret_cast<T*>(y.data_ptr()), g, part.data_ptr<float>(), zt);
     else
       hipLaunchKernelGGL((dw_fwd_kernel<T, false>), grid, dim3(kThreads), 0, stream,
                          reinterpret_cast<const T*>(x.data_ptr()), w9.data_ptr<float>(),
-                         reinterpret_cast<T*>(y.data_ptr()), g, nullptr);
+                         reinterpret_cast<T*>(y.data_ptr()), g, nullptr, nullptr);
   });
   if (moments) {
-    mom = at::empty({2 * (int64_t)g.C + 1}, x.options().dtype(at::kDouble));
     bn_reduce_partials_launch(part.data_ptr<float>(), (int)grid.x, g.C, mom.data_ptr<double>(),
                               (double)g.N * g.OH * g.OW, stream);
   }

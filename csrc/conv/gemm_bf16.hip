@@ -16,6 +16,8 @@
 //                             of the STORED values per M-tile -> BN statistics
 //                             without a separate read pass over C;
 //             EPI_AFFINE    : C = act(acc * s[n] + t[n] (+ R))  -- eval-mode
+//                             (s, t null: C = acc + R -- a data gradient
+//                             summed with another branch's, see ops/fused.py)
 //                             conv + folded BN (+ residual) + ReLU in one kernel.
 //
 // Structure (cdna_hip_programming.md §5): 256 threads = 4 waves in a
@@ -87,6 +89,7 @@ struct NtArgs {
   const bf16* R; int64_t ldr;   // EPI_AFFINE residual
   int epi_relu;
   float* part;                  // EPI_MOMENTS partials [2][mtiles][N]
+  double* zsums;                // EPI_MOMENTS: fp64 moments to zero (see common.h) or null
   RowMap amap, cmap;            // strided 1x1 row maps (non-CONV)
   ConvMap cv;                   // implicit-GEMM conv geometry (CONV)
 };
@@ -108,6 +111,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
   const RowMap& amap = p.amap;
   const RowMap& cmap = p.cmap;
   const ConvMap& cv = p.cv;
+  if constexpr (EPI == EPI_MOMENTS) zero_moments(p.zsums, 2 * N);
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int A_VECS = BM * BK / 8 / kThreads;  // 16-B vectors per thread per A tile
@@ -296,8 +300,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
   if constexpr (EPI == EPI_AFFINE) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      es[j] = col_ok ? epi_s[col + j] : 0.f;
-      et[j] = col_ok ? epi_t[col + j] : 0.f;
+      // null scale/shift = identity ("add" mode: C = acc + R)
+      es[j] = (col_ok && epi_s) ? epi_s[col + j] : 1.f;
+      et[j] = (col_ok && epi_t) ? epi_t[col + j] : 0.f;
     }
   }
   float msum[8], msq[8];
@@ -737,11 +742,16 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
     part = at::empty({2, mtiles, a.N}, like.options().dtype(at::kFloat));
     a.part = part.data_ptr<float>();
     moments = at::empty({2 * (int64_t)a.N + 1}, like.options().dtype(at::kDouble));
-  } else if (mode == "affine") {
+    a.zsums = moments_zero_target(moments.data_ptr<double>(), mtiles);
+  } else if (mode == "affine" || mode == "add") {
     epi = EPI_AFFINE;
-    TORCH_CHECK(epi_scale.has_value() && epi_shift.has_value(), "affine epilogue needs scale/shift");
-    a.epi_s = epi_scale->data_ptr<float>();
-    a.epi_t = epi_shift->data_ptr<float>();
+    if (mode == "affine") {
+      TORCH_CHECK(epi_scale.has_value() && epi_shift.has_value(), "affine epilogue needs scale/shift");
+      a.epi_s = epi_scale->data_ptr<float>();
+      a.epi_t = epi_shift->data_ptr<float>();
+    } else {
+      TORCH_CHECK(residual.has_value() && residual->defined(), "add epilogue needs a residual");
+    }
     if (residual.has_value() && residual->defined()) {
       check_operand(*residual, "residual");
       TORCH_CHECK(residual->size(0) == a.M && residual->size(1) == a.N, "residual shape");
@@ -766,7 +776,8 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
 //   A [M, K] bf16, B [N, K] bf16 (both K-contiguous), K % 8 == 0, N % 8 == 0.
 //   pro_scale/pro_shift [K] fp32: A' = relu(A*s + t)
 //   mode "store" | "moments" (returns fp64 [2N+1] = (sum, sumsq, M)) | "affine"
-//   (epi_scale/epi_shift [N], optional residual [M, N], relu flag).
+//   (epi_scale/epi_shift [N], optional residual [M, N], relu flag) | "add"
+//   (C = acc + residual).
 //   a_map / c_map: [s, Ho, Wo, Hi, Wi] strided row maps for A reads / C writes.
 std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& pro_scale,
@@ -781,6 +792,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
   NtArgs a{};
   a.amap = parse_map(a_map, "a_map");
   a.cmap = parse_map(c_map, "c_map");
+  TORCH_CHECK(a.cmap.s == 1 || !(residual.has_value() && residual->defined()),
+              "a residual epilogue cannot be combined with a strided c_map");
   const RowMap& am = a.amap;
   const RowMap& cm = a.cmap;
   int64_t m64 = A.size(0);

@@ -10,6 +10,10 @@
 
 namespace dmp {
 
+// coalesced.hip: one launch copying many dense tensors (same shapes/strides)
+void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
+
+
 namespace py = pybind11;
 using torch::autograd::Node;
 using torch::autograd::variable_list;
@@ -230,11 +234,26 @@ void Reducer::zero_grad() {
   torch::autograd::AutoGradMode no_grad(false);
   for (auto& f : group_flats_) f.zero_();
   for (size_t i = 0; i < params_.size(); ++i) params_[i].mutable_grad() = views_[i];
+  views_zeroed_ = true;
 }
 
 void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
   std::lock_guard<std::mutex> lk(mu_);
-  install_views_locked(/*zero_undefined=*/true);
+  // Steal mode iff no parameter carries gradient data the backward must add to.
+  bool can_steal = true;
+  for (size_t i = 0; i < params_.size() && can_steal; ++i) {
+    const auto& g = params_[i].grad();
+    if (g.defined() && !(views_zeroed_ && g.data_ptr() == views_[i].data_ptr())) can_steal = false;
+  }
+  steal_mode_ = can_steal;
+  if (steal_mode_) {
+    torch::autograd::AutoGradMode no_grad(false);
+    for (auto& p : params_) p.mutable_grad() = at::Tensor();
+    stolen_.assign(params_.size(), at::Tensor());
+  } else {
+    install_views_locked(/*zero_undefined=*/true);
+  }
+  views_zeroed_ = false;
   std::fill(ready_.begin(), ready_.end(), 0);
   for (auto& b : buckets_) b.pending = (int64_t)b.params.size();
   next_launch_ = 0;
@@ -272,6 +291,7 @@ void Reducer::prepare_for_backward(const std::vector<at::Tensor>& outputs) {
   // Unused parameters contribute zero gradients to their buckets.
   for (int64_t i : last_unused_) {
     views_[i].zero_();
+    if (steal_mode_) params_[i].mutable_grad() = views_[i];
     mark_ready_locked(i);
   }
 }
@@ -283,6 +303,7 @@ void Reducer::disarm() {
 
 void Reducer::on_grad_ready(int64_t idx) {
   std::lock_guard<std::mutex> lk(mu_);
+  views_zeroed_ = false;  // (also under no_sync: the views now hold data to accumulate into)
   if (!armed_) return;
   TORCH_CHECK(!ready_[idx], "Reducer: gradient of parameter ", idx,
               " became ready twice in one backward (reentrant backward or shared parameter "
@@ -291,8 +312,12 @@ void Reducer::on_grad_ready(int64_t idx) {
   const auto& g = p.grad();
   torch::autograd::AutoGradMode no_grad(false);
   if (g.defined() && g.data_ptr() != views_[idx].data_ptr()) {
-    views_[idx].copy_(g);
-    p.mutable_grad() = views_[idx];
+    if (steal_mode_) {
+      stolen_[idx] = g;  // copied into the bucket with its siblings in one launch
+    } else {
+      views_[idx].copy_(g);
+      p.mutable_grad() = views_[idx];
+    }
   }
   if (!callback_queued_) {
     callback_queued_ = true;
@@ -306,7 +331,36 @@ void Reducer::mark_ready_locked(int64_t idx) {
   if (record_order_) ready_order_.push_back(idx);
   auto& b = buckets_[param_bucket_[idx]];
   b.pending -= 1;
-  if (b.pending == 0) launch_ready_prefix_locked();
+  if (b.pending == 0) {
+    if (steal_mode_) flush_bucket_locked(param_bucket_[idx]);
+    launch_ready_prefix_locked();
+  }
+}
+
+void Reducer::flush_bucket_locked(int64_t bi) {
+  std::vector<at::Tensor> srcs, dsts;
+  for (int64_t i : buckets_[bi].params) {
+    if (!stolen_[i].defined()) continue;
+    srcs.push_back(stolen_[i]);
+    dsts.push_back(views_[i]);
+  }
+  torch::autograd::AutoGradMode no_grad(false);
+  if (!srcs.empty()) {
+    bool same_layout = srcs[0].is_cuda();
+    for (size_t k = 0; k < srcs.size() && same_layout; ++k)
+      same_layout = srcs[k].strides() == dsts[k].strides() &&
+                    srcs[k].scalar_type() == dsts[k].scalar_type() &&
+                    srcs[k].is_non_overlapping_and_dense();
+    if (same_layout) {
+      multi_copy(srcs, dsts);
+    } else {
+      for (size_t k = 0; k < srcs.size(); ++k) dsts[k].copy_(srcs[k]);
+    }
+  }
+  for (int64_t i : buckets_[bi].params) {
+    stolen_[i] = at::Tensor();
+    params_[i].mutable_grad() = views_[i];
+  }
 }
 
 void Reducer::launch_ready_prefix_locked() {

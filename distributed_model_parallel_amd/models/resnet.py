@@ -20,7 +20,7 @@ import torch.nn as nn
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
-from ..ops.fused import conv_bn
+from ..ops.fused import GradSlot, conv_bn, grad_tap
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -74,8 +74,12 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        identity = _shortcut(self.downsample, x)
-        out = conv_bn(self.conv1, self.bn1, x)
+        # x feeds conv1 and the shortcut: conv1's data-gradient GEMM absorbs the
+        # shortcut's gradient (ops/fused.py GradSlot) instead of an add kernel.
+        # The shortcut is built AFTER conv1 so its backward nodes run first.
+        slot = GradSlot() if (self.training and torch.is_grad_enabled()) else None
+        out = conv_bn(self.conv1, self.bn1, x, grad_slot=slot)
+        identity = _shortcut(self.downsample, grad_tap(x, slot))
         out = conv_bn(self.conv2, self.bn2, out)
         return conv_bn(self.conv3, self.bn3, out, identity)
 

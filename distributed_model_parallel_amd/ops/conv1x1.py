@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0}
+_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0}
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -52,7 +52,7 @@ def _geom(stride: int, hi: int, wi: int):
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, moments):
+    def forward(ctx, x, weight, stride, moments, slot):
         C = _native.require("conv1x1")
         n, cin, h, w = x.shape
         geom = _geom(stride, h, w)
@@ -62,6 +62,9 @@ class _Conv1x1Fn(torch.autograd.Function):
         y2, mom = C.gemm_nt(_rows(x), w2, mode="moments" if moments else "store", a_map=geom)
         ctx.save_for_backward(x, weight)
         ctx.geom = geom
+        ctx.slot = slot
+        if slot is not None and not geom:
+            slot.consumer = True  # our dgrad epilogue will absorb the shortcut's gradient
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
@@ -78,7 +81,13 @@ class _Conv1x1Fn(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             # strided: the GEMM scatters into the sampled rows of a zeroed full-size grad
-            dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), c_map=ctx.geom)
+            extra = ctx.slot.take() if (ctx.slot is not None and ctx.slot.consumer) else None
+            if extra is not None:  # dx = dy @ W + (the shortcut branch's gradient), one pass
+                _STATS["fused_dgrad"] += 1
+                extra = _rows(extra.to(x.dtype).contiguous(memory_format=torch.channels_last))
+                dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), mode="add", residual=extra)
+            else:
+                dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), c_map=ctx.geom)
             dx = _unrows(dx2, n, h, w)
         if ctx.needs_input_grad[1]:
             # split-M MFMA GEMM with transposing LDS reads (hipBLASLt picks a 4-tile,
@@ -86,15 +95,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
-            moments: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
-    """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
+            moments: bool = False, grad_slot=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d).
+    grad_slot (ops.fused.GradSlot): absorb a shortcut branch's gradient of x
+    into this conv's data-gradient epilogue."""
     if _native_ok(x, weight):
         _STATS["native"] += 1
-        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments)
+        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments, grad_slot)
         return y, (mom if moments else None)
     _STATS["torch"] += 1
     return F.conv2d(x, weight, None, stride), None
@@ -102,6 +113,7 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
 
 class Conv1x1(nn.Conv2d):
     """Drop-in ``nn.Conv2d(cin, cout, 1, stride, bias=False)``."""
+    accepts_grad_slot = True
 
     def __init__(self, cin: int, cout: int, stride: int = 1, device=None, dtype=None):
         super().__init__(cin, cout, 1, stride=stride, bias=False, device=device, dtype=dtype)
@@ -109,5 +121,5 @@ class Conv1x1(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return conv1x1(x, self.weight, self.stride[0])[0]
 
-    def forward_with_moments(self, x: torch.Tensor):
-        return conv1x1(x, self.weight, self.stride[0], moments=True)
+    def forward_with_moments(self, x: torch.Tensor, grad_slot=None):
+        return conv1x1(x, self.weight, self.stride[0], moments=True, grad_slot=grad_slot)

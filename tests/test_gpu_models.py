@@ -91,3 +91,39 @@ def test_igemm_vs_miopen_in_model(name):
     finally:
         conv_igemm.ENABLED = True
     _compare(l_a, g_a, l_b, g_b, min_cos=0.97, median_cos=0.995)
+
+
+@pytest.mark.parametrize("stride,ds", [(1, False), (2, True), (1, True)])
+def test_bottleneck_fused_shortcut_grad(stride, ds):
+    """conv1's dgrad epilogue absorbs the shortcut gradient (GradSlot): same x.grad
+    as the unfused composition of the same modules (which adds in a separate kernel)."""
+    from distributed_model_parallel_amd.models.resnet import Bottleneck
+    torch.manual_seed(0)
+    cin, planes = (256, 64) if not ds else (128, 64)
+    down = None
+    if ds:
+        down = torch.nn.Sequential(conv1x1.Conv1x1(cin, planes * 4, stride),
+                                   __import__("distributed_model_parallel_amd.ops.batchnorm", fromlist=["x"]).BatchNormAct2d(planes * 4))
+    blk = cast_model(Bottleneck(cin, planes, stride, down).to(DEV).to(memory_format=torch.channels_last))
+    blk.train()
+    x = torch.randn(8, cin, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    g = None
+    outs = []
+    for fused in (True, False):
+        xi = x.detach().requires_grad_()
+        n0 = conv1x1._STATS["fused_dgrad"]
+        if fused:
+            y = blk(xi)
+        else:
+            idn = xi if down is None else down[1](down[0](xi))
+            out = blk.bn1(blk.conv1(xi))
+            out = blk.bn2(blk.conv2(out))
+            y = blk.bn3(blk.conv3(out), idn)
+        if g is None:
+            g = torch.randn_like(y)
+        y.backward(g)
+        if fused:
+            assert conv1x1._STATS["fused_dgrad"] == n0 + 1, "shortcut gradient was not fused"
+        outs.append(xi.grad.float())
+    err = (outs[0] - outs[1]).norm() / outs[1].norm()
+    assert err < 2e-2, err
