@@ -64,6 +64,10 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
                            int64_t W);
 at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride,
                            at::ScalarType out_dtype);
+// maxpool.hip
+std::vector<at::Tensor> maxpool2d_forward(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
+at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W,
+                              int64_t k, int64_t s, int64_t p);
 // coalesced.hip
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
@@ -102,6 +106,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("relu") = false);
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"));
+
+  // ---- NHWC max pooling with byte argmax ----
+  m.def("maxpool2d_forward", &dmp::maxpool2d_forward);
+  m.def("maxpool2d_backward", &dmp::maxpool2d_backward);
 
   // ---- depthwise 3x3 (NHWC) ----
   m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),

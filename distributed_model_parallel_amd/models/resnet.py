@@ -21,6 +21,7 @@ from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import GradSlot, conv_bn, grad_tap
+from ..ops.pool import MaxPool2d
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -92,7 +93,7 @@ class ResNet(nn.Module):
         self.inplanes = stem_channels
         self.conv1 = nn.Conv2d(3, stem_channels, 7, stride=2, padding=3, bias=False)
         self.bn1 = BatchNormAct2d(stem_channels, act="relu")
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool2d(3, stride=2, padding=1)  # NHWC kernel, byte argmax
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

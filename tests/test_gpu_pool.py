@@ -1,0 +1,39 @@
+"""NHWC max pooling (byte argmax, gather backward) vs F.max_pool2d."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd.ops.pool import _STATS, max_pool2d
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,k,s,p", [((2, 64, 112, 112), 3, 2, 1), ((3, 16, 9, 7), 3, 2, 1),
+                                         ((2, 8, 10, 10), 2, 2, 0), ((1, 32, 11, 13), 3, 1, 1),
+                                         ((2, 24, 8, 8), 5, 3, 2)])
+def test_maxpool_matches_torch(dtype, shape, k, s, p):
+    torch.manual_seed(0)
+    # distinct values per window so argmax ties cannot differ in tie-breaking
+    x = torch.randn(*shape, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    xi = x.detach().requires_grad_()
+    xr = x.detach().float().requires_grad_()
+    n0 = _STATS["native"]
+    y = max_pool2d(xi, k, s, p)
+    assert _STATS["native"] == n0 + 1
+    yr = F.max_pool2d(xr, k, s, p)
+    torch.testing.assert_close(y.float(), yr)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-6
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+def test_maxpool_ties_first_wins():
+    x = torch.zeros(1, 8, 4, 4, device="cuda").contiguous(memory_format=torch.channels_last)
+    xi = x.detach().requires_grad_()
+    xr = x.detach().requires_grad_()
+    max_pool2d(xi, 2, 2, 0).sum().backward()
+    F.max_pool2d(xr, 2, 2, 0).sum().backward()
+    torch.testing.assert_close(xi.grad, xr.grad)
