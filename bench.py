@@ -12,6 +12,14 @@ one fused flat-SGD (momentum 0.9, wd 1e-4) launch per dtype group.
   python bench.py --gpus N --steps K --warmup W
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+Other BASELINE.json configs:
+  DP (scatter/replicate/gather, one process): python bench.py --parallel dp --gpus N
+  DDP + SyncBatchNorm:                        ... bench.py --parallel syncbn --gpus N
+  ViT-B/16 DDP:                               ... bench.py --model vit_b_16 --batch-size 128
+  ResNet-18 CPU/gloo plumbing (ws 2):         torchrun --nproc-per-node 2 bench.py --device cpu
+                                              --model resnet18 --dtype fp32 --batch-size 8
+                                              --steps 2 --warmup 1 --no-channels-last
+
 Rank 0 prints ONE JSON line.  Time = max over ranks of the K-step wall time,
 bracketed by a barrier + device synchronize on both sides.
 """
@@ -49,11 +57,14 @@ def main() -> int:
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--miopen-benchmark", type=int, default=int(os.environ.get("DMP_MIOPEN_BENCHMARK", "0")))
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="cpu: gloo plumbing run (BASELINE config 1), fp32 recommended")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
     args = ap.parse_args()
 
-    env = init_distributed()
+    use_gpu = None if args.device == "auto" else args.device == "cuda"
+    env = init_distributed(use_gpu=use_gpu)
     if env.world_size != args.gpus and env.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
@@ -61,7 +72,11 @@ def main() -> int:
     cfg = StepConfig(model=args.model, batch_size=args.batch_size, image_size=args.image_size,
                      dtype=parse_dtype(args.dtype), channels_last=not args.no_channels_last,
                      parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
-                     first_bucket_mb=args.first_bucket_mb)
+                     first_bucket_mb=args.first_bucket_mb,
+                     dp_devices=args.gpus if args.parallel == "dp" else 1)
+    if args.parallel == "dp" and env.world_size > 1:
+        raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
+                         "--gpus N` without torchrun")
     st = build_train_state(cfg, dev)
     comm = default_communicator(dev)
 
@@ -87,6 +102,8 @@ def main() -> int:
     final_loss = float(loss.item())
 
     n = env.world_size
+    if args.parallel == "dp" and dev.type == "cuda":
+        n = args.gpus  # one process driving N GPUs
     global_batch = args.batch_size * n
     img_s = global_batch * args.steps / elapsed
     par = {"ddp": "dp", "syncbn": "dp", "dp": "dp-single-process", "none": "none"}[args.parallel]
@@ -108,6 +125,7 @@ def main() -> int:
                 % (args.image_size, args.image_size),
         "config": {
             "model": args.model,
+            "device": dev.type,
             "global_batch": global_batch,
             "per_gpu_batch": args.batch_size,
             "seq_len": None,

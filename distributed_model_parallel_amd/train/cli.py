@@ -57,6 +57,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--micro-batches", default=1, type=int)
     p.add_argument("--schedule", default="1f1b", choices=["naive", "gpipe", "1f1b"])
+    p.add_argument("--partition", default="balanced", choices=["balanced", "reference"],
+                   help="pipeline stage cut: FLOP-balanced (any ws) or the reference's MobileNetV2 cut")
     p.add_argument("--warmup-epochs", default=10, type=int)
     p.add_argument("--steps-per-epoch", default=0, type=int, help="cap iterations per epoch (0 = all)")
     p.add_argument("--log-dir", default="./log")
@@ -197,7 +199,7 @@ def run_pipeline(args, env) -> None:
     comm = Communicator(env.device)
     pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=args.micro_batches,
                     schedule=args.schedule, dtype=parse_dtype(args.dtype),
-                    channels_last=args.channels_last)
+                    channels_last=args.channels_last, partition=args.partition)
     opt = torch.optim.SGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
                           weight_decay=args.weight_decay)
     sched = build_schedule(opt, args.epochs, args.warmup_epochs)

@@ -31,6 +31,7 @@ class StepConfig:
     parallel: str = "ddp"           # ddp | syncbn | dp | none
     bucket_cap_mb: float = 25.0
     first_bucket_mb: float = 1.0
+    dp_devices: int = 1             # parallel == "dp": GPUs driven by the single process
     lr: float = 0.1
     momentum: float = 0.9
     weight_decay: float = 1e-4
@@ -49,16 +50,18 @@ class TrainState:
     labels: torch.Tensor
 
 
-def synthetic_batch(cfg: StepConfig, device: torch.device, generator_seed: int = 1234):
+def synthetic_batch(cfg: StepConfig, device: torch.device, generator_seed: int = 1234,
+                    batch: Optional[int] = None):
     (c, h, w), ncls = INPUT_SHAPES[cfg.model]
     if cfg.image_size:
         h = w = cfg.image_size
     ncls = cfg.num_classes or ncls
+    b = batch or cfg.batch_size
     g = torch.Generator(device="cpu").manual_seed(generator_seed)
-    x = torch.randn(cfg.batch_size, c, h, w, generator=g).to(device=device, dtype=cfg.dtype)
+    x = torch.randn(b, c, h, w, generator=g).to(device=device, dtype=cfg.dtype)
     if cfg.channels_last:
         x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, ncls, (cfg.batch_size,), generator=g).to(device)
+    y = torch.randint(0, ncls, (b,), generator=g).to(device)
     return x, y
 
 
@@ -80,7 +83,10 @@ def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
         model = model.to(memory_format=torch.channels_last)
     if cfg.dtype != torch.float32:
         cast_model(model, cfg.dtype)
-    x, y = synthetic_batch(cfg, device)
+    ndp = max(1, cfg.dp_devices) if (cfg.parallel == "dp" and device.type == "cuda") else 1
+    # DP: the single process feeds batch_size images PER GPU (weak scaling, same
+    # per-GPU work as DDP), scattered from device_ids[0]
+    x, y = synthetic_batch(cfg, device, batch=cfg.batch_size * ndp)
 
     if cfg.parallel in ("ddp", "syncbn"):
         wrapped = DistributedDataParallel(model, bucket_cap_mb=cfg.bucket_cap_mb,
@@ -97,7 +103,7 @@ def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
             return loss
     elif cfg.parallel == "dp":
         from ..parallel.data_parallel import DataParallel
-        wrapped = DataParallel(model)
+        wrapped = DataParallel(model, device_ids=list(range(ndp)) if device.type == "cuda" else None)
         opt = torch.optim.SGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
                               weight_decay=cfg.weight_decay, foreach=True)
 

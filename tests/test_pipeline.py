@@ -110,3 +110,38 @@ def test_atom_costs_mobilenet():
     atoms = _mnv2_atoms()
     c = atom_costs(atoms, torch.zeros(2, 3, 32, 32))
     assert len(c) == 20 and all(v > 0 for v in c)
+
+
+def _ragged_worker(rank, world, partition):
+    from distributed_model_parallel_amd.comm.rccl import Communicator
+    from distributed_model_parallel_amd.parallel.pipeline import Pipeline
+    atoms = _mnv2_atoms() if partition == "reference" else _mlp_atoms()
+    shape = (3, 32, 32) if partition == "reference" else (3, 4, 4)
+    kind = "mnv2" if partition == "reference" else "mlp"
+    comm = Communicator(torch.device("cpu"))
+    pipe = Pipeline(atoms, comm, shape, micro_batches=4, schedule="gpipe", partition=partition)
+    x, y = _data(kind, 12)
+    pipe.train_step(x if rank == 0 else None, y if rank == 0 else None)
+    for p in atoms.parameters():
+        p.grad = None
+    x, y = _data(kind, 7)           # dynamic last batch: 7 rows over 4 micro-batches
+    res = pipe.train_step(x if rank == 0 else None, y if rank == 0 else None)
+    lo, hi = pipe.partition[rank]
+    return {"loss": res.loss, "partition": pipe.partition,
+            "grads": {i: [p.grad.clone() for p in atoms[i].parameters()] for i in range(lo, hi)}}
+
+
+@pytest.mark.parametrize("world,partition", [(3, None), (4, "reference")])
+def test_pipeline_dynamic_last_batch(world, partition):
+    """A smaller final batch after a full one (SURVEY §4.2 pipeline oracle) -- and the
+    reference's own 4-way MobileNetV2 cut."""
+    kind = "mnv2" if partition == "reference" else "mlp"
+    ref_loss, ref_grads = _sequential_grads(kind, 7, 4)
+    res = run_world(_ragged_worker, world, partition)
+    if partition == "reference":
+        assert res[0]["partition"] == [(0, 4), (4, 10), (10, 16), (16, 20)]
+    assert res[0]["loss"] == pytest.approx(ref_loss, rel=1e-4, abs=1e-6)
+    for r in res:
+        for i, gs in r["grads"].items():
+            for g, rg in zip(gs, ref_grads[i]):
+                torch.testing.assert_close(g, rg, atol=1e-4, rtol=1e-3)
