@@ -1,0 +1,58 @@
+"""The RCCL path of DDP / SyncBN on one MI355X (world size 1, so no peers): the
+reducer is forced onto the RCCL backend (ncclAllReduce avg over one rank) and
+must give the same parameters after a training step as the no-op world-1
+backend; SyncBatchNorm's moment all-reduce goes through RCCL too.  Runs in a
+subprocess because the process group is process-global."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = r'''
+import os, sys, torch
+sys.path.insert(0, os.environ["ROOT"])
+from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed
+from distributed_model_parallel_amd.train.step import StepConfig, build_train_state
+env = init_distributed()
+out = {}
+for parallel in ("ddp", "syncbn"):
+    for forced in ("0", "1"):
+        os.environ["DMP_DDP_SINGLE_RANK_COMM"] = forced
+        cfg = StepConfig(model="resnet18", batch_size=8, image_size=64, parallel=parallel)
+        st = build_train_state(cfg, env.device)
+        for _ in range(2):
+            loss = st.step()
+        torch.cuda.synchronize()
+        out[(parallel, forced)] = (loss.item(), [p.detach().float().clone() for p in st.model.parameters()],
+                                   getattr(st.wrapped, "comm_backend", None))
+for parallel in ("ddp", "syncbn"):
+    a, b = out[(parallel, "0")], out[(parallel, "1")]
+    assert "rccl" in str(b[2]).lower(), b[2]
+    assert abs(a[0] - b[0]) < 1e-3 * max(1.0, abs(a[0])), (parallel, a[0], b[0])
+    worst = max(((x - y).abs().max() / (y.abs().max() + 1e-6)).item() for x, y in zip(a[1], b[1]))
+    assert worst < 2e-2, (parallel, worst)
+    print(parallel, "ok", a[0], b[0], b[2], worst)
+destroy_distributed()
+'''
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_ddp_and_syncbn_rccl_backend_world1():
+    env = dict(os.environ, ROOT=ROOT, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    assert "ddp ok" in r.stdout and "syncbn ok" in r.stdout
