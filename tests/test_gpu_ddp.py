@@ -25,18 +25,19 @@ for parallel in ("ddp", "syncbn"):
         os.environ["DMP_DDP_SINGLE_RANK_COMM"] = forced
         cfg = StepConfig(model="resnet18", batch_size=8, image_size=64, parallel=parallel)
         st = build_train_state(cfg, env.device)
-        for _ in range(2):
-            loss = st.step()
+        before = [p.detach().float().clone() for p in st.model.parameters()]
+        loss = st.step()          # one step: the update carries the (averaged) gradient
         torch.cuda.synchronize()
-        out[(parallel, forced)] = (loss.item(), [p.detach().float().clone() for p in st.model.parameters()],
-                                   getattr(st.wrapped, "comm_backend", None))
+        delta = [p.detach().float() - b for p, b in zip(st.model.parameters(), before)]
+        out[(parallel, forced)] = (loss.item(), delta, getattr(st.wrapped, "comm_backend", None))
 for parallel in ("ddp", "syncbn"):
     a, b = out[(parallel, "0")], out[(parallel, "1")]
     assert "rccl" in str(b[2]).lower(), b[2]
     assert abs(a[0] - b[0]) < 1e-3 * max(1.0, abs(a[0])), (parallel, a[0], b[0])
-    worst = max(((x - y).abs().max() / (y.abs().max() + 1e-6)).item() for x, y in zip(a[1], b[1]))
-    assert worst < 2e-2, (parallel, worst)
-    print(parallel, "ok", a[0], b[0], b[2], worst)
+    cos = min(torch.nn.functional.cosine_similarity(x.flatten(), y.flatten(), dim=0).item()
+              for x, y in zip(a[1], b[1]) if y.norm() > 0)
+    assert cos > 0.98, (parallel, cos)
+    print(parallel, "ok", a[0], b[0], b[2], cos)
 destroy_distributed()
 '''
 
@@ -54,5 +55,8 @@ def test_ddp_and_syncbn_rccl_backend_world1():
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     r = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True,
                        timeout=900)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    if r.returncode != 0:
+        print(r.stdout[-3000:])
+        print(r.stderr[-6000:])
+    assert r.returncode == 0, "subprocess failed (output above)"
     assert "ddp ok" in r.stdout and "syncbn ok" in r.stdout
