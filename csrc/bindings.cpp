@@ -131,6 +131,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<const std::string&, int64_t, int64_t, int64_t, bool>(), py::arg("unique_id"),
            py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("high_priority") = false,
            py::call_guard<py::gil_scoped_release>())
+      .def("set_inline", &dmp::RcclComm::set_inline)
+      .def("is_inline", &dmp::RcclComm::is_inline)
       .def_static("new_unique_id", [] { return py::bytes(dmp::RcclComm::new_unique_id()); })
       .def_property_readonly("rank", &dmp::RcclComm::rank)
       .def_property_readonly("size", &dmp::RcclComm::size)

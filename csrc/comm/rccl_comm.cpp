@@ -71,7 +71,12 @@ RcclComm::~RcclComm() {
   if (ev_out_) hipEventDestroy(ev_out_);
 }
 
+hipStream_t RcclComm::st() const {
+  return inline_ ? at::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream() : stream_.stream();
+}
+
 void RcclComm::sync_from_current() {
+  if (inline_) return;
   auto cur = at::hip::getCurrentHIPStream((c10::DeviceIndex)device_);
   if (cur.stream() == stream_.stream()) return;
   DMP_HIP_CHECK(hipEventRecord(ev_in_, cur.stream()));
@@ -79,7 +84,7 @@ void RcclComm::sync_from_current() {
 }
 
 void RcclComm::record_usage(const at::Tensor& t) {
-  if (t.defined() && t.is_cuda())
+  if (!inline_ && t.defined() && t.is_cuda())
     c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
 }
 
@@ -90,7 +95,7 @@ void RcclComm::all_reduce(at::Tensor& t, const std::string& op) {
   sync_from_current();
   record_usage(t);
   DMP_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl_dtype(t),
-                               to_nccl_op(op), comm_, stream_.stream()));
+                               to_nccl_op(op), comm_, st()));
 }
 
 void RcclComm::all_reduce_coalesced(std::vector<at::Tensor>& ts, const std::string& op) {
@@ -102,7 +107,7 @@ void RcclComm::all_reduce_coalesced(std::vector<at::Tensor>& ts, const std::stri
     TORCH_CHECK(t.is_contiguous(), "all_reduce needs contiguous tensors");
     record_usage(t);
     DMP_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl_dtype(t),
-                                 to_nccl_op(op), comm_, stream_.stream()));
+                                 to_nccl_op(op), comm_, st()));
   }
   DMP_NCCL_CHECK(ncclGroupEnd());
 }
@@ -113,7 +118,7 @@ void RcclComm::broadcast(at::Tensor& t, int64_t root) {
   sync_from_current();
   record_usage(t);
   DMP_NCCL_CHECK(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl_dtype(t), (int)root,
-                               comm_, stream_.stream()));
+                               comm_, st()));
 }
 
 void RcclComm::reduce(at::Tensor& t, int64_t root, const std::string& op) {
@@ -122,7 +127,7 @@ void RcclComm::reduce(at::Tensor& t, int64_t root, const std::string& op) {
   sync_from_current();
   record_usage(t);
   DMP_NCCL_CHECK(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl_dtype(t),
-                            to_nccl_op(op), (int)root, comm_, stream_.stream()));
+                            to_nccl_op(op), (int)root, comm_, st()));
 }
 
 void RcclComm::all_gather(at::Tensor& out, const at::Tensor& in) {
@@ -133,7 +138,7 @@ void RcclComm::all_gather(at::Tensor& out, const at::Tensor& in) {
   record_usage(out);
   record_usage(in);
   DMP_NCCL_CHECK(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), to_nccl_dtype(in), comm_,
-                               stream_.stream()));
+                               st()));
 }
 
 void RcclComm::reduce_scatter(at::Tensor& out, const at::Tensor& in, const std::string& op) {
@@ -144,7 +149,7 @@ void RcclComm::reduce_scatter(at::Tensor& out, const at::Tensor& in, const std::
   record_usage(out);
   record_usage(in);
   DMP_NCCL_CHECK(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), to_nccl_dtype(in),
-                                   to_nccl_op(op), comm_, stream_.stream()));
+                                   to_nccl_op(op), comm_, st()));
 }
 
 void RcclComm::all_to_all(at::Tensor& out, const at::Tensor& in) {
@@ -160,9 +165,9 @@ void RcclComm::all_to_all(at::Tensor& out, const at::Tensor& in) {
   DMP_NCCL_CHECK(ncclGroupStart());
   for (int64_t p = 0; p < nranks_; ++p) {
     DMP_NCCL_CHECK(ncclSend(static_cast<const char*>(in.data_ptr()) + p * bytes, chunk, dt, (int)p,
-                            comm_, stream_.stream()));
+                            comm_, st()));
     DMP_NCCL_CHECK(ncclRecv(static_cast<char*>(out.data_ptr()) + p * bytes, chunk, dt, (int)p,
-                            comm_, stream_.stream()));
+                            comm_, st()));
   }
   DMP_NCCL_CHECK(ncclGroupEnd());
 }
@@ -173,7 +178,7 @@ void RcclComm::send(const at::Tensor& t, int64_t peer) {
   sync_from_current();
   record_usage(t);
   DMP_NCCL_CHECK(ncclSend(t.data_ptr(), t.numel(), to_nccl_dtype(t), (int)peer, comm_,
-                          stream_.stream()));
+                          st()));
 }
 
 void RcclComm::recv(at::Tensor& t, int64_t peer) {
@@ -182,7 +187,7 @@ void RcclComm::recv(at::Tensor& t, int64_t peer) {
   sync_from_current();
   record_usage(t);
   DMP_NCCL_CHECK(ncclRecv(t.data_ptr(), t.numel(), to_nccl_dtype(t), (int)peer, comm_,
-                          stream_.stream()));
+                          st()));
 }
 
 void RcclComm::batch_p2p(std::vector<at::Tensor>& ts, const std::vector<int64_t>& peers,
@@ -196,10 +201,10 @@ void RcclComm::batch_p2p(std::vector<at::Tensor>& ts, const std::vector<int64_t>
     record_usage(ts[i]);
     if (is_send[i])
       DMP_NCCL_CHECK(ncclSend(ts[i].data_ptr(), ts[i].numel(), to_nccl_dtype(ts[i]), (int)peers[i],
-                              comm_, stream_.stream()));
+                              comm_, st()));
     else
       DMP_NCCL_CHECK(ncclRecv(ts[i].data_ptr(), ts[i].numel(), to_nccl_dtype(ts[i]), (int)peers[i],
-                              comm_, stream_.stream()));
+                              comm_, st()));
   }
   DMP_NCCL_CHECK(ncclGroupEnd());
 }
@@ -207,6 +212,7 @@ void RcclComm::batch_p2p(std::vector<at::Tensor>& ts, const std::vector<int64_t>
 void RcclComm::wait() {
   std::lock_guard<std::mutex> lk(mu_);
   c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
+  if (inline_) return;  // collectives already ran on the current stream
   auto cur = at::hip::getCurrentHIPStream((c10::DeviceIndex)device_);
   if (cur.stream() == stream_.stream()) return;
   DMP_HIP_CHECK(hipEventRecord(ev_out_, stream_.stream()));
@@ -215,7 +221,7 @@ void RcclComm::wait() {
 
 void RcclComm::synchronize() {
   c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
-  DMP_HIP_CHECK(hipStreamSynchronize(stream_.stream()));
+  DMP_HIP_CHECK(hipStreamSynchronize(st()));
 }
 
 }  // namespace dmp

@@ -58,12 +58,19 @@ class RcclComm {
 
   // Make the comm stream wait on the caller's current stream.
   void sync_from_current();
+  // Inline mode: collectives run on the caller's current stream (no side
+  // stream, no cross-stream events) -- no overlap with compute, no queue
+  // interplay; chosen per process via DMP_COMM_INLINE (comm/rccl.py).
+  void set_inline(bool v) { inline_ = v; }
+  bool is_inline() const { return inline_; }
   void record_usage(const at::Tensor& t);
 
  private:
   ncclComm_t comm_ = nullptr;
   int64_t nranks_, rank_, device_;
   c10::hip::HIPStream stream_;
+  bool inline_ = false;
+  hipStream_t st() const;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;
   std::mutex mu_;
 };

@@ -55,6 +55,9 @@ class Communicator:
             # ResNet-50 step 1.9x on MI355X (67.3 vs 36.5 ms, profiles/README.md)
             high = os.environ.get("DMP_COMM_PRIORITY", "normal") == "high"
             self._comm = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high)
+            # DMP_COMM_INLINE=1: collectives on the compute stream (no overlap, no side queue)
+            if os.environ.get("DMP_COMM_INLINE", "0") == "1":
+                self._comm.set_inline(True)
 
     # ------------------------------------------------------------------ #
     @property
