@@ -337,6 +337,17 @@ void Reducer::mark_ready_locked(int64_t idx) {
   }
 }
 
+namespace {
+bool same_dense_layout(const at::Tensor& a, const at::Tensor& b) {
+  if (!a.is_cuda() || !b.is_cuda() || a.scalar_type() != b.scalar_type() || a.sizes() != b.sizes())
+    return false;
+  if (!a.is_non_overlapping_and_dense() || !b.is_non_overlapping_and_dense()) return false;
+  for (int64_t d = 0; d < a.dim(); ++d)
+    if (a.size(d) > 1 && a.stride(d) != b.stride(d)) return false;
+  return true;
+}
+}  // namespace
+
 void Reducer::flush_bucket_locked(int64_t bi) {
   std::vector<at::Tensor> srcs, dsts;
   for (int64_t i : buckets_[bi].params) {
@@ -345,18 +356,19 @@ void Reducer::flush_bucket_locked(int64_t bi) {
     dsts.push_back(views_[i]);
   }
   torch::autograd::AutoGradMode no_grad(false);
-  if (!srcs.empty()) {
-    bool same_layout = srcs[0].is_cuda();
-    for (size_t k = 0; k < srcs.size() && same_layout; ++k)
-      same_layout = srcs[k].strides() == dsts[k].strides() &&
-                    srcs[k].scalar_type() == dsts[k].scalar_type() &&
-                    srcs[k].is_non_overlapping_and_dense();
-    if (same_layout) {
-      multi_copy(srcs, dsts);
+  // One coalesced launch for every pair with the same dense memory layout
+  // (strides of size-1 dims do not matter: a [C,K,1,1] grad may carry either
+  // contiguous or channels_last strides there); anything else copies alone.
+  std::vector<at::Tensor> ms, md;
+  for (size_t k = 0; k < srcs.size(); ++k) {
+    if (same_dense_layout(srcs[k], dsts[k])) {
+      ms.push_back(srcs[k]);
+      md.push_back(dsts[k].as_strided(srcs[k].sizes(), srcs[k].strides()));
     } else {
-      for (size_t k = 0; k < srcs.size(); ++k) dsts[k].copy_(srcs[k]);
+      dsts[k].copy_(srcs[k]);
     }
   }
+  if (!ms.empty()) multi_copy(ms, md);
   for (int64_t i : buckets_[bi].params) {
     stolen_[i] = at::Tensor();
     params_[i].mutable_grad() = views_[i];
