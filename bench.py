@@ -56,7 +56,8 @@ def main() -> int:
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
     ap.add_argument("--no-channels-last", action="store_true")
-    ap.add_argument("--miopen-benchmark", type=int, default=int(os.environ.get("DMP_MIOPEN_BENCHMARK", "0")))
+    ap.add_argument("--miopen-benchmark", type=int, default=int(os.environ.get("DMP_MIOPEN_BENCHMARK", "1")),
+                    help="MIOpen find mode for the convs left on MIOpen (first step pays the search)")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
                     help="cpu: gloo plumbing run (BASELINE config 1), fp32 recommended")
     ap.add_argument("--json-out", default=None)

@@ -54,6 +54,7 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
                                 const c10::optional<at::Tensor>& residual, bool relu);
+void set_gemm_tile(int64_t t);
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
                       at::ScalarType out_dtype);
@@ -96,6 +97,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{});
+
+  m.def("set_gemm_tile", &dmp::set_gemm_tile,
+        "debug: force the NT GEMM tile variant (-1 auto, 0 256x64, 1 128x64, 2 128x128, "
+        "3 128x64/4x1, 4 64x128, 5 64x64)");
 
   // ---- implicit-GEMM convolution (kh x kw taps) on the same MFMA kernels ----
   m.def("conv_nt", &dmp::conv_nt, py::arg("x"), py::arg("wmat"), py::arg("kh"), py::arg("kw"),

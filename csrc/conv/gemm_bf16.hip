@@ -94,7 +94,7 @@ struct NtArgs {
   ConvMap cv;                   // implicit-GEMM conv geometry (CONV)
 };
 
-template <int BM, int BN, int WAVES_M, int WAVES_N, bool PRO_BN, int EPI, bool CONV>
+template <int BM, int BN, int WAVES_M, int WAVES_N, bool PRO_BN, int EPI, bool CONV, int NSTAGE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
   const bf16* __restrict__ A = p.A;
   const bf16* __restrict__ B = p.B;
@@ -121,7 +121,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
   constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   constexpr int CT_STRIDE = BN + 8;  // +16 B per row: epilogue tile writes spread over banks
   constexpr int EPI_BYTES = BM * CT_STRIDE * 2;
-  constexpr int LDS_BYTES = (2 * STAGE_BYTES > EPI_BYTES ? 2 * STAGE_BYTES : EPI_BYTES);
+  // NSTAGE == 1: the host guarantees K <= BK (one K tile), so no second
+  // staging buffer -- half the LDS, more resident blocks for these
+  // memory-bound shapes
+  constexpr int LDS_BYTES = (NSTAGE * STAGE_BYTES > EPI_BYTES ? NSTAGE * STAGE_BYTES : EPI_BYTES);
   __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
 
   const int tid = threadIdx.x;
@@ -293,6 +296,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
   // ---- store pass: each thread moves 8 contiguous columns of a row ----
   constexpr int CV = BN / 8;                  // 16-B vectors per row
   constexpr int RPP = kThreads / CV;          // rows per pass
+  static_assert(EPI != EPI_MOMENTS || 2 * RPP * BN * 4 <= LDS_BYTES, "moments scratch exceeds LDS");
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
   const bool col_ok = col < N;
@@ -360,18 +364,42 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
 template <int BM, int BN, int WM, int WN, bool PRO, int EPI, bool CONV>
 void launch(const NtArgs& a, hipStream_t stream) {
   const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI, CONV>), dim3(mtiles * ntiles),
+  if constexpr (!CONV) {
+    if (a.K <= BK) {
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI, CONV, 1>), dim3(mtiles * ntiles),
+                         dim3(kThreads), 0, stream, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI, CONV, 2>), dim3(mtiles * ntiles),
                      dim3(kThreads), 0, stream, a);
 }
 
+// Tile override for experiments (set_gemm_tile; -1 = automatic).
+int g_tile_override = -1;
+
 template <bool PRO, int EPI, bool CONV>
 void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {
-  // bm selects the M tile (128 or 256 rows) ; BN follows N.
-  if (a.N <= 64) {
-    if (bm == 256) launch<256, 64, 4, 1, PRO, EPI, CONV>(a, s);
-    else launch<128, 64, 2, 2, PRO, EPI, CONV>(a, s);
-  } else {
-    launch<128, 128, 2, 2, PRO, EPI, CONV>(a, s);
+  int t = g_tile_override;
+  if (t < 0) t = a.N <= 64 ? (bm == 256 ? 0 : 1) : 2;
+  switch (t) {
+    case 0: launch<256, 64, 4, 1, PRO, EPI, CONV>(a, s); break;
+    case 1: launch<128, 64, 2, 2, PRO, EPI, CONV>(a, s); break;
+    case 3: launch<128, 64, 4, 1, PRO, EPI, CONV>(a, s); break;
+    case 4: launch<64, 128, 2, 2, PRO, EPI, CONV>(a, s); break;
+    case 5: launch<64, 64, 2, 2, PRO, EPI, CONV>(a, s); break;
+    default: launch<128, 128, 2, 2, PRO, EPI, CONV>(a, s); break;
+  }
+}
+
+// M tile of the selected variant (moments partial rows = M tiles)
+int tile_bm(int N, int bm) {
+  int t = g_tile_override;
+  if (t < 0) t = N <= 64 ? (bm == 256 ? 0 : 1) : 2;
+  switch (t) {
+    case 0: return 256;
+    case 4: case 5: return 64;
+    default: return 128;
   }
 }
 
@@ -733,12 +761,13 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   at::Tensor moments;
   if (a.M == 0) return {C, moments};
   const int bm = tile_m_for(a.N);
+  const int tbm = tile_bm(a.N, bm);
   int epi = EPI_STORE;
   at::Tensor part;
   if (mode == "store") {
   } else if (mode == "moments") {
     epi = EPI_MOMENTS;
-    const int mtiles = (a.M + bm - 1) / bm;
+    const int mtiles = (a.M + tbm - 1) / tbm;
     part = at::empty({2, mtiles, a.N}, like.options().dtype(at::kFloat));
     a.part = part.data_ptr<float>();
     moments = at::empty({2 * (int64_t)a.N + 1}, like.options().dtype(at::kDouble));
@@ -765,7 +794,7 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   if (conv) dispatch_mode<true>(a, pro, epi, bm, stream);
   else dispatch_mode<false>(a, pro, epi, bm, stream);
   if (epi == EPI_MOMENTS)
-    bn_reduce_partials_launch(a.part, (a.M + bm - 1) / bm, a.N, moments.data_ptr<double>(),
+    bn_reduce_partials_launch(a.part, (a.M + tbm - 1) / tbm, a.N, moments.data_ptr<double>(),
                               (double)a.M, stream);
   return {C, moments};
 }
@@ -877,5 +906,7 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
   a.ldc = C.stride(0);
   return run_nt(a, true, x, pro_scale, pro_shift, mode, epi_scale, epi_shift, residual, relu, C);
 }
+
+void set_gemm_tile(int64_t t) { g_tile_override = (int)t; }
 
 }  // namespace dmp
