@@ -36,6 +36,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_model_parallel_amd.comm.rccl import default_communicator  # noqa: E402
+from distributed_model_parallel_amd.models import INPUT_SHAPES  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
 from distributed_model_parallel_amd.utils.env import destroy_distributed, init_distributed  # noqa: E402
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
@@ -50,7 +51,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch-size", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--image-size", type=int, default=None, help="default: the model's native size")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--parallel", default="ddp", choices=["ddp", "syncbn", "dp", "none"])
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
@@ -80,6 +81,9 @@ def main() -> int:
                          "--gpus N` without torchrun")
     st = build_train_state(cfg, dev)
     comm = default_communicator(dev)
+
+    (_, img_h, _), _ = INPUT_SHAPES[args.model]
+    image_size = args.image_size or img_h
 
     t_warm0 = time.time()
     for i in range(args.warmup):
@@ -123,14 +127,14 @@ def main() -> int:
         "vs_baseline": (img_s / BASELINE_VALUE) if BASELINE_VALUE else None,
         "dtype": args.dtype,
         "data": "synthetic (random 3x%dx%d inputs, random labels, random-init weights)"
-                % (args.image_size, args.image_size),
+                % (image_size, image_size),
         "config": {
             "model": args.model,
             "device": dev.type,
             "global_batch": global_batch,
             "per_gpu_batch": args.batch_size,
             "seq_len": None,
-            "image_size": args.image_size,
+            "image_size": image_size,
             "parallelism": f"{par}{n}",
             "sync_bn": args.parallel == "syncbn",
             "bucket_cap_mb": args.bucket_cap_mb,

@@ -52,7 +52,10 @@ __device__ __forceinline__ void ldv(const T* p, float (&v)[Vec16<T>::N]) { Vec16
 // forward: y[n,oh,ow,c] = sum_{kh,kw} x[n, oh*s-1+kh, ow*s-1+kw, c] * w[kh,kw,c]
 // grid.x = ceil(N*OH*strips / spp), grid.y = channel chunks
 // ---------------------------------------------------------------------------
-template <typename T, bool MOMENTS>
+// S = stride as a template constant: every tap index in the unrolled loops is
+// then a compile-time constant, so wr/acc stay in registers (a runtime stride
+// made the compiler index them dynamically -> scratch memory, measured 2-4x).
+template <typename T, bool MOMENTS, int S>
 __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ x,
                                                          const float* __restrict__ w9,
                                                          T* __restrict__ y, Geo g,
@@ -89,20 +92,20 @@ __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ 
     constexpr int MAXW = (TW - 1) * 2 + 3;  // input columns touched (stride <= 2)
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
-      const int ih = oh * g.stride - 1 + kh;
+      const int ih = oh * S - 1 + kh;
       if (ih < 0 || ih >= g.H) continue;
       const T* row = x + (((int64_t)n * g.H + ih) * g.W) * g.C + c0;
-      const int iw0 = ow0 * g.stride - 1;
+      const int iw0 = ow0 * S - 1;
 #pragma unroll
       for (int ci = 0; ci < MAXW; ++ci) {
         const int iw = iw0 + ci;
-        if (ci >= (TW - 1) * g.stride + 3) break;
+        if (ci >= (TW - 1) * S + 3) break;
         if (iw < 0 || iw >= g.W) continue;
         float v[VEC];
         ldv<T>(row + (int64_t)iw * g.C, v);
 #pragma unroll
         for (int o = 0; o < TW; ++o) {
-          const int kw = ci - o * g.stride;
+          const int kw = ci - o * S;
           if (kw < 0 || kw > 2) continue;
 #pragma unroll
           for (int j = 0; j < VEC; ++j) acc[o][j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[o][j]);
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(kThreads) void dw_dgrad_kernel(const T* __restrict_
 // weight gradient partials: part[block][t*C + c] = sum over the block's output
 // strips of dy * x (tap t).  Lanes of one channel vector combine in LDS.
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int S>
 __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(const T* __restrict__ dy,
                                                            const T* __restrict__ x, Geo g,
                                                            int strips_per_lane,
@@ -271,20 +274,20 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(const T* __restrict_
       }
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
-        const int ih = oh * g.stride - 1 + kh;
+        const int ih = oh * S - 1 + kh;
         if (ih < 0 || ih >= g.H) continue;
         const T* row = x + (((int64_t)n * g.H + ih) * g.W) * g.C + c0;
-        const int iw0 = ow0 * g.stride - 1;
+        const int iw0 = ow0 * S - 1;
 #pragma unroll
         for (int ci = 0; ci < (TW - 1) * 2 + 3; ++ci) {
-          if (ci >= (TW - 1) * g.stride + 3) break;
+          if (ci >= (TW - 1) * S + 3) break;
           const int iw = iw0 + ci;
           if (iw < 0 || iw >= g.W) continue;
           float v[VEC];
           ldv<T>(row + (int64_t)iw * g.C, v);
 #pragma unroll
           for (int o = 0; o < TW; ++o) {
-            const int kw = ci - o * g.stride;
+            const int kw = ci - o * S;
             if (kw < 0 || kw > 2) continue;
 #pragma unroll
             for (int j = 0; j < VEC; ++j) acc[kh * 3 + kw][j] = fmaf(v[j], gv[o][j], acc[kh * 3 + kw][j]);
@@ -395,11 +398,11 @@ std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor&
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
     if (moments)
-      hipLaunchKernelGGL((dw_fwd_kernel<T, true>), grid, dim3(kThreads), 0, stream,
+      hipLaunchKernelGGL((g.stride == 1 ? dw_fwd_kernel<T, true, 1> : dw_fwd_kernel<T, true, 2>), grid, dim3(kThreads), 0, stream,
                          reinterpret_cast<const T*>(x.data_ptr()), w9.data_ptr<float>(),
                          reinterpret_cast<T*>(y.data_ptr()), g, part.data_ptr<float>(), zt);
     else
-      hipLaunchKernelGGL((dw_fwd_kernel<T, false>), grid, dim3(kThreads), 0, stream,
+      hipLaunchKernelGGL((g.stride == 1 ? dw_fwd_kernel<T, false, 1> : dw_fwd_kernel<T, false, 2>), grid, dim3(kThreads), 0, stream,
                          reinterpret_cast<const T*>(x.data_ptr()), w9.data_ptr<float>(),
                          reinterpret_cast<T*>(y.data_ptr()), g, nullptr, nullptr);
   });
@@ -452,7 +455,7 @@ at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t st
   auto part = at::empty({(int64_t)grid.x, 9 * (int64_t)g.C}, x.options().dtype(at::kFloat));
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
-    hipLaunchKernelGGL((dw_wgrad_kernel<T>), grid, dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((g.stride == 1 ? dw_wgrad_kernel<T, 1> : dw_wgrad_kernel<T, 2>), grid, dim3(kThreads), 0, stream,
                        reinterpret_cast<const T*>(dy.data_ptr()),
                        reinterpret_cast<const T*>(x.data_ptr()), g, spl, part.data_ptr<float>());
   });
