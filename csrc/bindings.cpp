@@ -14,7 +14,8 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                                          const c10::optional<at::Tensor>& running_var,
                                          double momentum, double eps,
                                          const c10::optional<at::Tensor>& residual, bool relu,
-                                         int64_t C);
+                                         int64_t C,
+                                         const c10::optional<at::Tensor>& num_batches_tracked);
 std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& running_mean,
                                       const at::Tensor& running_var,
                                       const c10::optional<at::Tensor>& weight,
@@ -83,7 +84,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- batch norm ----
   m.def("bn_local_moments", &dmp::bn_local_moments);
-  m.def("bn_forward_apply", &dmp::bn_forward_apply);
+  m.def("bn_forward_apply", &dmp::bn_forward_apply, py::arg("x"), py::arg("sums"), py::arg("weight"),
+        py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
+        py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("C"),
+        py::arg("num_batches_tracked") = py::none());
   m.def("bn_eval_apply", &dmp::bn_eval_apply);
   m.def("bn_backward_moments", &dmp::bn_backward_moments);
   m.def("bn_backward_apply", &dmp::bn_backward_apply);

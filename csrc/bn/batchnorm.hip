@@ -214,7 +214,10 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const float* __restrict__ weight, const float* __restrict__ bias,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
     int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
-    float* __restrict__ save_invstd) {
+    float* __restrict__ save_invstd, int64_t* __restrict__ num_batches_tracked) {
+  // BatchNorm's step counter rides along (one lane), instead of its own launch
+  if (num_batches_tracked != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    *num_batches_tracked += 1;
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -477,9 +480,16 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                                          const c10::optional<at::Tensor>& running_var,
                                          double momentum, double eps,
                                          const c10::optional<at::Tensor>& residual, bool relu,
-                                         int64_t C) {
+                                         int64_t C,
+                                         const c10::optional<at::Tensor>& num_batches_tracked) {
   check_input(x, C, "x");
   TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.numel() == 2 * C + 1, "bad moments");
+  int64_t* nbt = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong && num_batches_tracked->numel() == 1 &&
+                    num_batches_tracked->is_cuda(), "num_batches_tracked must be a 1-element int64 GPU tensor");
+    nbt = num_batches_tracked->data_ptr<int64_t>();
+  }
   const int64_t M = x.numel() / C;
   auto y = at::empty_like(x);
   auto saved = at::empty({2, C}, x.options().dtype(at::kFloat));
@@ -496,7 +506,7 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                      ptr<T>(x), r, sums.data_ptr<double>(), fptr(weight), fptr(bias),            \
                      fptr(running_mean), fptr(running_var), (float)momentum, (float)eps, M,      \
                      (int)C, g.rows_per_block, ptr<T>(y), saved.data_ptr<float>(),               \
-                     saved.data_ptr<float>() + C)
+                     saved.data_ptr<float>() + C, nbt)
       if (relu && has_res) DMP_BN_FWD(true, true);
       else if (relu) DMP_BN_FWD(true, false);
       else if (has_res) DMP_BN_FWD(false, true);
@@ -532,7 +542,7 @@ std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& run
   hipLaunchKernelGGL((bn_apply_kernel<T, RELU, RES, false>), g.grid, dim3(kThreads), 0, stream,  \
                      ptr<T>(x), r, nullptr, fptr(weight), fptr(bias), rm.data_ptr<float>(),      \
                      rv.data_ptr<float>(), 0.f, (float)eps, M, (int)C, g.rows_per_block,         \
-                     ptr<T>(y), saved.data_ptr<float>(), saved.data_ptr<float>() + C)
+                     ptr<T>(y), saved.data_ptr<float>(), saved.data_ptr<float>() + C, nullptr)
       if (relu && has_res) DMP_BN_EVAL(true, true);
       else if (relu) DMP_BN_EVAL(true, false);
       else if (has_res) DMP_BN_EVAL(false, true);

@@ -77,14 +77,18 @@ def local_moments(x2: torch.Tensor, native: bool) -> torch.Tensor:
     return torch.cat([xd.sum(0), (xd * xd).sum(0), xd.new_tensor([float(x2.shape[0])])])
 
 
-def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, native):
-    """Training-mode normalise from (global) moments; updates running stats.
+def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, native, nbt=None):
+    """Training-mode normalise from (global) moments; updates running stats and
+    increments `nbt` (num_batches_tracked) -- inside the kernel when native.
 
     Returns (y, mean, invstd)."""
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_forward_apply(x2, sums, weight, bias, rm, rv,
-                                                       float(momentum), float(eps), res2, relu, c)
+                                                       float(momentum), float(eps), res2, relu, c,
+                                                       nbt)
+    if nbt is not None:
+        nbt.add_(1)
     mean, invstd, scale, shift = _finalize_torch(sums, weight, bias, rm, rv, momentum, eps)
     return [_apply_torch(x2, scale, shift, res2, relu), mean, invstd]
 
@@ -168,7 +172,7 @@ def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, rel
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
-                relu, reduce_moments, reduce_grads, pre_sums=None):
+                relu, reduce_moments, reduce_grads, pre_sums=None, nbt=None):
         x2, back = _as_rows(x)
         native = _native_ok(x2)
         _STATS["native_fwd" if native else "torch_fwd"] += 1
@@ -188,7 +192,7 @@ class _BatchNormActFn(torch.autograd.Function):
             upd_rm = running_mean if (running_mean is not None and running_mean.dtype == torch.float32) else None
             upd_rv = running_var if upd_rm is not None else None
             y2, mean, invstd = forward_apply(x2, sums, w32, b32, upd_rm, upd_rv, momentum, eps,
-                                             res2, relu, native)
+                                             res2, relu, native, nbt)
             if running_mean is not None and upd_rm is None:  # low-precision buffers
                 c = x2.shape[1]
                 n = sums[2 * c]
@@ -227,7 +231,7 @@ class _BatchNormActFn(torch.autograd.Function):
         gres = back(dres2) if has_res else None
         gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
         gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
-        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None
+        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
@@ -236,11 +240,14 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
                    relu: bool = False, residual: Optional[torch.Tensor] = None,
                    reduce_moments: Optional[MomentReducer] = None,
                    reduce_grads: Optional[GradReducer] = None,
-                   sums: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   sums: Optional[torch.Tensor] = None,
+                   num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Functional fused BN(+residual)(+ReLU).  `sums`: precomputed local moments
-    [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode."""
+    [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode.
+    `num_batches_tracked`: incremented once (training mode), in-kernel when native."""
     return _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
-                                 momentum, eps, relu, reduce_moments, reduce_grads, sums)
+                                 momentum, eps, relu, reduce_moments, reduce_grads, sums,
+                                 num_batches_tracked if training else None)
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -274,9 +281,13 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self._check_input_dim(x)
         use_batch = self.training or not self.track_running_stats
         recompute = in_recompute()  # activation-checkpoint recompute: no second stat update
+        nbt = None
         if self.training and self.track_running_stats and self.num_batches_tracked is not None \
                 and not recompute:
-            self.num_batches_tracked.add_(1)
+            if self.momentum is None:  # cumulative average needs the count now (host read)
+                self.num_batches_tracked.add_(1)
+            else:                      # counted inside the BN apply kernel
+                nbt = self.num_batches_tracked
         momentum = self._momentum() if (self.training and self.track_running_stats) else 0.0
         if recompute:
             momentum = 0.0
@@ -287,7 +298,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
                               rv if self.track_running_stats else None, self.weight, self.bias,
                               use_batch, momentum, self.eps, relu=self.act == "relu",
                               residual=residual, reduce_moments=rmom, reduce_grads=rgrad,
-                              sums=sums if use_batch else None)
+                              sums=sums if use_batch else None,
+                              num_batches_tracked=nbt if use_batch else None)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (f", act={self.act}" if self.act else "")

@@ -68,10 +68,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
+        # the moments output never gets a gradient: do not let autograd build a
+        # zero [2C+1] fp64 tensor for it every backward (one fill launch per layer)
+        ctx.set_materialize_grads(False)
         return _unrows(y2, n, ho, wo), mom
 
     @staticmethod
     def backward(ctx, dy, _dmom):
+        if dy is None:
+            return (None,) * 5
         x, weight = ctx.saved_tensors
         C = _native.require("conv1x1 backward")
         n, cin, h, w = x.shape

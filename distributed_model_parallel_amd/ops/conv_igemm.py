@@ -71,10 +71,15 @@ class _ConvIGFn(torch.autograd.Function):
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
+        # the moments output never gets a gradient: do not let autograd build a
+        # zero [2C+1] fp64 tensor for it every backward (one fill launch per layer)
+        ctx.set_materialize_grads(False)
         return y2.view(n, ho, wo, cout).permute(0, 3, 1, 2), mom
 
     @staticmethod
     def backward(ctx, dy, _dmom):
+        if dy is None:
+            return (None,) * 5
         x, weight = ctx.saved_tensors
         C = _native.require("conv_igemm backward")
         stride, pad, ho, wo = ctx.geo

@@ -34,10 +34,15 @@ class _DWConvFn(torch.autograd.Function):
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
+        # the moments output never gets a gradient: do not let autograd build a
+        # zero [2C+1] fp64 tensor for it every backward (one fill launch per layer)
+        ctx.set_materialize_grads(False)
         return y, mom
 
     @staticmethod
     def backward(ctx, dy, _dmom=None):
+        if dy is None:
+            return None, None, None, None
         x, w = ctx.saved_tensors
         C = _native.require("depthwise conv backward")
         dy = dy.contiguous(memory_format=torch.channels_last).to(x.dtype)

@@ -143,3 +143,18 @@ def test_gather_slabs_large_aligned():
     parts = [torch.randn(300, 1000, device=DEV).bfloat16() for _ in range(4)]
     assert torch.equal(comm_ops.gather_tensors(parts, "cuda:0", 0), torch.cat(parts, 0))
     assert torch.equal(comm_ops.gather_tensors(parts, "cuda:0", 1), torch.cat(parts, 1))
+
+
+def test_bn_num_batches_tracked_counted_in_kernel():
+    from distributed_model_parallel_amd.ops.batchnorm import BatchNormAct2d
+    m = BatchNormAct2d(16, act="relu").cuda()
+    x = torch.randn(4, 16, 5, 5, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    for _ in range(3):
+        m(x)
+    assert int(m.num_batches_tracked) == 3
+    m.momentum = None  # cumulative average path counts on the host
+    m(x)
+    assert int(m.num_batches_tracked) == 4
+    m.eval()
+    m(x)
+    assert int(m.num_batches_tracked) == 4
