@@ -61,6 +61,8 @@ def main() -> int:
                     help="MIOpen find mode for the convs left on MIOpen (first step pays the search)")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
                     help="cpu: gloo plumbing run (BASELINE config 1), fp32 recommended")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the whole training step as one captured hipGraph")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
     args = ap.parse_args()
@@ -75,7 +77,7 @@ def main() -> int:
                      dtype=parse_dtype(args.dtype), channels_last=not args.no_channels_last,
                      parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
                      first_bucket_mb=args.first_bucket_mb,
-                     dp_devices=args.gpus if args.parallel == "dp" else 1)
+                     dp_devices=args.gpus if args.parallel == "dp" else 1, graph=args.graph)
     if args.parallel == "dp" and env.world_size > 1:
         raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
                          "--gpus N` without torchrun")
@@ -140,6 +142,7 @@ def main() -> int:
             "bucket_cap_mb": args.bucket_cap_mb,
             "channels_last": not args.no_channels_last,
             "grad_comm": getattr(st.wrapped, "comm_backend", None),
+            "hip_graph": args.graph,
             "final_loss": round(final_loss, 4),
         },
     }

@@ -15,6 +15,7 @@
 //                   where the output rows are strided and a direct copy would
 //                   be uncoalesced on one side.
 #include <torch/extension.h>
+#include <mutex>
 #include <ATen/hip/HIPContext.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include "../common.h"
@@ -151,6 +152,12 @@ __global__ __launch_bounds__(256) void gather_slabs_kernel(const SlabDesc* __res
   }
 }
 
+// Tables uploaded while a stream is being captured into a hipGraph: the graph's
+// memcpy node re-reads the pinned source on every replay, so the source must
+// outlive the graph (the caching host allocator would otherwise recycle it).
+std::mutex g_graph_tables_mu;
+std::vector<at::Tensor> g_graph_tables;
+
 // Upload a POD table to the device through pinned memory on the current stream.
 template <typename T>
 at::Tensor upload_table(const std::vector<T>& host, const at::Device& dev) {
@@ -158,7 +165,15 @@ at::Tensor upload_table(const std::vector<T>& host, const at::Device& dev) {
   auto pinned = at::empty({std::max<int64_t>(bytes, 1)},
                           at::TensorOptions().dtype(at::kByte).pinned_memory(true));
   std::memcpy(pinned.data_ptr(), host.data(), bytes);
-  return pinned.to(dev, /*non_blocking=*/true);
+  auto dev_table = pinned.to(dev, /*non_blocking=*/true);
+  hipStreamCaptureStatus status = hipStreamCaptureStatusNone;
+  DMP_HIP_CHECK(hipStreamIsCapturing(at::hip::getCurrentHIPStream(dev.index()).stream(), &status));
+  if (status != hipStreamCaptureStatusNone) {
+    std::lock_guard<std::mutex> lk(g_graph_tables_mu);
+    g_graph_tables.push_back(pinned);
+    g_graph_tables.push_back(dev_table);  // graph-pool memory: keep the address stable too
+  }
+  return dev_table;
 }
 
 }  // namespace

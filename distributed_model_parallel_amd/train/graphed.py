@@ -20,22 +20,31 @@ import torch
 
 
 class GraphedStep:
+    """Callable training step: the first ``warmup`` calls run eagerly (on a side
+    stream, as capture requires), the next call captures the step into a
+    hipGraph and replays it; every later call is one replay.  Each call advances
+    the training state by exactly one step and returns the (static) loss."""
+
     def __init__(self, step_fn: Callable[[], torch.Tensor], warmup: int = 3,
                  comm_sync: Optional[Callable[[], None]] = None):
         self.step_fn = step_fn
-        self.warmup = warmup
+        self.warmup = max(1, warmup)
         self.comm_sync = comm_sync
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.static_out: Optional[torch.Tensor] = None
         self._calls = 0
+        self._side = None
+
+    def _eager(self) -> torch.Tensor:
+        if self._side is None:
+            self._side = torch.cuda.Stream()
+        self._side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self._side):
+            out = self.step_fn()
+        torch.cuda.current_stream().wait_stream(self._side)
+        return out
 
     def capture(self) -> None:
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(self.warmup):
-                self.step_fn()
-        torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         if self.comm_sync is not None:
             self.comm_sync()
@@ -47,7 +56,10 @@ class GraphedStep:
         self.static_out = out
 
     def __call__(self) -> torch.Tensor:
+        self._calls += 1
+        if self._calls <= self.warmup:
+            return self._eager()
         if self.graph is None:
-            self.capture()
+            self.capture()  # records only; the replay below executes the step
         self.graph.replay()
         return self.static_out

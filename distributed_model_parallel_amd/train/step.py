@@ -32,6 +32,7 @@ class StepConfig:
     bucket_cap_mb: float = 25.0
     first_bucket_mb: float = 1.0
     dp_devices: int = 1             # parallel == "dp": GPUs driven by the single process
+    graph: bool = False             # capture the whole step in a hipGraph (constant LR, static data)
     lr: float = 0.1
     momentum: float = 0.9
     weight_decay: float = 1e-4
@@ -127,4 +128,9 @@ def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
             opt.zero_grad(set_to_none=True)
             return loss
 
+    if cfg.graph:
+        if device.type != "cuda":
+            raise ValueError("graph capture needs a GPU")
+        from .graphed import GraphedStep
+        step = GraphedStep(step, warmup=3)
     return TrainState(cfg, model, wrapped, opt, step, x, y)
