@@ -23,25 +23,29 @@
 namespace dmp {
 namespace {
 
-struct CopyChunk {
-  const uint8_t* src;
-  uint8_t* dst;
-  int64_t nbytes;
-};
-
 constexpr int64_t kChunkBytes = 64 * 1024;
 
-__global__ __launch_bounds__(256) void multi_copy_kernel(const CopyChunk* __restrict__ chunks,
-                                                         int nchunks) {
-  const int cid = blockIdx.x;
-  if (cid >= nchunks) return;
-  const CopyChunk c = chunks[cid];
-  const uintptr_t a = reinterpret_cast<uintptr_t>(c.src) | reinterpret_cast<uintptr_t>(c.dst) |
-                      (uintptr_t)c.nbytes;
+// The copy table travels in the kernel arguments (no pinned-memory upload, no
+// H2D copy: one launch is self-contained, and safe inside hipGraph capture).
+// Up to kMaxCopy tensors per launch; block b copies 64 KiB chunk b of the
+// concatenated byte stream and finds its tensor by binary search over the
+// chunk prefix (scalar loads from the argument segment).
+constexpr int kMaxCopy = 96;
+struct CopyTable {
+  const uint8_t* src[kMaxCopy];
+  uint8_t* dst[kMaxCopy];
+  int64_t nbytes[kMaxCopy];
+  int first_chunk[kMaxCopy + 1];
+  int n;
+};
+
+__device__ __forceinline__ void copy_range(const uint8_t* src, uint8_t* dst, int64_t nbytes) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                      (uintptr_t)nbytes;
   if ((a & 15) == 0) {
-    const u32x4* s = reinterpret_cast<const u32x4*>(c.src);
-    u32x4* d = reinterpret_cast<u32x4*>(c.dst);
-    const int64_t n = c.nbytes >> 4;
+    const u32x4* s = reinterpret_cast<const u32x4*>(src);
+    u32x4* d = reinterpret_cast<u32x4*>(dst);
+    const int64_t n = nbytes >> 4;
     int64_t i = threadIdx.x;
     // 4 x 16 B in flight per lane.
     for (; i + 3 * 256 < n; i += 4 * 256) {
@@ -50,16 +54,29 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyChunk* __rest
     }
     for (; i < n; i += 256) d[i] = s[i];
   } else if ((a & 3) == 0) {
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(c.src);
-    uint32_t* d = reinterpret_cast<uint32_t*>(c.dst);
-    for (int64_t i = threadIdx.x; i < (c.nbytes >> 2); i += 256) d[i] = s[i];
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (int64_t i = threadIdx.x; i < (nbytes >> 2); i += 256) d[i] = s[i];
   } else if ((a & 1) == 0) {
-    const uint16_t* s = reinterpret_cast<const uint16_t*>(c.src);
-    uint16_t* d = reinterpret_cast<uint16_t*>(c.dst);
-    for (int64_t i = threadIdx.x; i < (c.nbytes >> 1); i += 256) d[i] = s[i];
+    const uint16_t* s = reinterpret_cast<const uint16_t*>(src);
+    uint16_t* d = reinterpret_cast<uint16_t*>(dst);
+    for (int64_t i = threadIdx.x; i < (nbytes >> 1); i += 256) d[i] = s[i];
   } else {
-    for (int64_t i = threadIdx.x; i < c.nbytes; i += 256) c.dst[i] = c.src[i];
+    for (int64_t i = threadIdx.x; i < nbytes; i += 256) dst[i] = src[i];
   }
+}
+
+__global__ __launch_bounds__(256) void multi_copy_kernel(const CopyTable t) {
+  const int cid = blockIdx.x;
+  int lo = 0, hi = t.n - 1;  // last entry with first_chunk <= cid
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.first_chunk[mid] <= cid) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t off = (int64_t)(cid - t.first_chunk[lo]) * kChunkBytes;
+  if (off >= t.nbytes[lo]) return;
+  copy_range(t.src[lo] + off, t.dst[lo] + off, min(kChunkBytes, t.nbytes[lo] - off));
 }
 
 constexpr int kMaxReduceInputs = 16;
@@ -184,7 +201,16 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
   TORCH_CHECK(srcs.size() == dsts.size(), "multi_copy: list length mismatch");
   if (srcs.empty()) return;
   const at::Device dev = dsts[0].device();
-  std::vector<CopyChunk> chunks;
+  auto stream = at::hip::getCurrentHIPStream(dev.index());
+  CopyTable t{};
+  int chunks = 0;
+  auto flush = [&]() {
+    if (t.n == 0) return;
+    t.first_chunk[t.n] = chunks;
+    hipLaunchKernelGGL(multi_copy_kernel, dim3((unsigned)chunks), dim3(256), 0, stream, t);
+    t = CopyTable{};
+    chunks = 0;
+  };
   for (size_t i = 0; i < srcs.size(); ++i) {
     const auto& s = srcs[i];
     const auto& d = dsts[i];
@@ -197,16 +223,18 @@ void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tenso
     const int64_t nb = s.numel() * s.element_size();
     TORCH_CHECK(nb == d.numel() * d.element_size(), "multi_copy: byte size mismatch at ", i);
     TORCH_CHECK(d.device() == dev, "multi_copy: all destinations must share one device");
-    const uint8_t* sp = static_cast<const uint8_t*>(s.data_ptr());
-    uint8_t* dp = static_cast<uint8_t*>(d.data_ptr());
-    for (int64_t o = 0; o < nb; o += kChunkBytes)
-      chunks.push_back({sp + o, dp + o, std::min<int64_t>(kChunkBytes, nb - o)});
+    if (nb == 0) continue;
+    const int64_t nchunk = (nb + kChunkBytes - 1) / kChunkBytes;
+    TORCH_CHECK(nchunk < (1LL << 30), "multi_copy: tensor too large");
+    if (t.n == kMaxCopy || chunks + nchunk >= (1LL << 31) - 1) flush();
+    t.src[t.n] = static_cast<const uint8_t*>(s.data_ptr());
+    t.dst[t.n] = static_cast<uint8_t*>(d.data_ptr());
+    t.nbytes[t.n] = nb;
+    t.first_chunk[t.n] = chunks;
+    chunks += (int)nchunk;
+    ++t.n;
   }
-  if (chunks.empty()) return;
-  auto table = upload_table(chunks, dev);
-  auto stream = at::hip::getCurrentHIPStream(dev.index());
-  hipLaunchKernelGGL(multi_copy_kernel, dim3((unsigned)chunks.size()), dim3(256), 0, stream,
-                     reinterpret_cast<const CopyChunk*>(table.data_ptr()), (int)chunks.size());
+  flush();
 }
 
 // out = sum(inputs); inputs may live on peer devices (peer access must be enabled).
