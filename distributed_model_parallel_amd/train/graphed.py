@@ -26,14 +26,15 @@ class GraphedStep:
     the training state by exactly one step and returns the (static) loss."""
 
     def __init__(self, step_fn: Callable[[], torch.Tensor], warmup: int = 3,
-                 comm_sync: Optional[Callable[[], None]] = None):
+                 comm_sync: Optional[Callable[[], None]] = None,
+                 stream: Optional[torch.cuda.Stream] = None):
         self.step_fn = step_fn
         self.warmup = max(1, warmup)
         self.comm_sync = comm_sync
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.static_out: Optional[torch.Tensor] = None
         self._calls = 0
-        self._side = None
+        self._side = stream  # warm-up and capture stream (the model/DDP should be built on it)
 
     def _eager(self) -> torch.Tensor:
         if self._side is None:
@@ -45,11 +46,13 @@ class GraphedStep:
         return out
 
     def capture(self) -> None:
+        if self._side is None:
+            self._side = torch.cuda.Stream()
         torch.cuda.synchronize()
         if self.comm_sync is not None:
             self.comm_sync()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=self._side):
             out = self.step_fn()
         torch.cuda.synchronize()
         self.graph = g

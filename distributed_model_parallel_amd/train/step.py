@@ -67,6 +67,23 @@ def synthetic_batch(cfg: StepConfig, device: torch.device, generator_seed: int =
 
 
 def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
+    if cfg.graph:
+        if device.type != "cuda":
+            raise ValueError("graph capture needs a GPU")
+        # Build (and later warm up / capture) on ONE side stream: the DDP reducer
+        # keeps the parameters' AccumulateGrad nodes alive, and a node created on
+        # the default stream would sync against it inside the capture.
+        side = torch.cuda.Stream(device=device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            st = _build_train_state(cfg, device)
+        from .graphed import GraphedStep
+        st.step = GraphedStep(st.step, warmup=3, stream=side)
+        return st
+    return _build_train_state(cfg, device)
+
+
+def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
     from ..parallel.distributed import DistributedDataParallel
     from ..parallel.sync_batchnorm import SyncBatchNorm
 
@@ -128,9 +145,4 @@ def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
             opt.zero_grad(set_to_none=True)
             return loss
 
-    if cfg.graph:
-        if device.type != "cuda":
-            raise ValueError("graph capture needs a GPU")
-        from .graphed import GraphedStep
-        step = GraphedStep(step, warmup=3)
     return TrainState(cfg, model, wrapped, opt, step, x, y)

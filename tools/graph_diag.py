@@ -21,9 +21,10 @@ ap.add_argument("--bs", type=int, default=16)
 a = ap.parse_args()
 env = init_distributed()
 cfg = StepConfig(model=a.model, batch_size=a.bs, image_size=a.img, parallel=a.parallel, lr=0.01)
-st = build_train_state(cfg, env.device)
-step = st.step
 side = torch.cuda.Stream()
+with torch.cuda.stream(side):  # build on the capture stream (see train/step.py)
+    st = build_train_state(cfg, env.device)
+step = st.step
 for i in range(3):
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -33,7 +34,7 @@ for i in range(3):
     print(f"warmup {i} loss {float(loss):.4f}", flush=True)
 g = torch.cuda.CUDAGraph()
 print("capture begin", flush=True)
-with torch.cuda.graph(g):
+with torch.cuda.graph(g, stream=side):
     out = step()
 print("capture end", flush=True)
 torch.cuda.synchronize()
