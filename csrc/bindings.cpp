@@ -24,13 +24,16 @@ std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& run
                                       int64_t C);
 at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                                const c10::optional<at::Tensor>& y, const at::Tensor& mean,
-                               bool relu, int64_t C);
+                               bool relu, int64_t C, const c10::optional<at::Tensor>& weight,
+                               const c10::optional<at::Tensor>& bias,
+                               const c10::optional<at::Tensor>& invstd);
 std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor& x,
                                           const c10::optional<at::Tensor>& y,
                                           const at::Tensor& sums, const at::Tensor& count,
                                           const c10::optional<at::Tensor>& weight,
                                           const at::Tensor& mean, const at::Tensor& invstd,
-                                          bool training, bool relu, bool want_dres, int64_t C);
+                                          bool training, bool relu, bool want_dres, int64_t C,
+                                          const c10::optional<at::Tensor>& bias);
 // fused_sgd.hip
 void sgd_flat_step(const c10::optional<at::Tensor>& master, const at::Tensor& mom,
                    const at::Tensor& grad, const at::Tensor& param, double lr, double wd,
@@ -89,8 +92,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("C"),
         py::arg("num_batches_tracked") = py::none());
   m.def("bn_eval_apply", &dmp::bn_eval_apply);
-  m.def("bn_backward_moments", &dmp::bn_backward_moments);
-  m.def("bn_backward_apply", &dmp::bn_backward_apply);
+  m.def("bn_backward_moments", &dmp::bn_backward_moments, py::arg("dy"), py::arg("x"), py::arg("y"),
+        py::arg("mean"), py::arg("relu"), py::arg("C"), py::arg("weight") = py::none(),
+        py::arg("bias") = py::none(), py::arg("invstd") = py::none());
+  m.def("bn_backward_apply", &dmp::bn_backward_apply, py::arg("dy"), py::arg("x"), py::arg("y"),
+        py::arg("sums"), py::arg("count"), py::arg("weight"), py::arg("mean"), py::arg("invstd"),
+        py::arg("training"), py::arg("relu"), py::arg("want_dres"), py::arg("C"),
+        py::arg("bias") = py::none());
 
   // ---- MFMA GEMM (1x1 conv) with fused BN prologue/epilogues ----
   m.def("gemm_nt", &dmp::gemm_nt, py::arg("A"), py::arg("B"), py::arg("pro_scale") = py::none(),

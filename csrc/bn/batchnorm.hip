@@ -292,11 +292,15 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
 // -------------------------------------------------------------------------
 // Backward pass 1 (per-block partials of sum dz and sum dz*(x-mean)).
 // -------------------------------------------------------------------------
-template <typename T, bool RELU>
+// RELU: 0 none; 1 mask from the saved output (y > 0); 2 mask re-derived from
+// x and the forward's per-channel affine (x*w*invstd + b - mean*w*invstd > 0)
+// -- one full-tensor read fewer, used whenever no residual was fused.
+template <typename T, int RELU>
 __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
-    const float* __restrict__ mean, int64_t M, int C, int64_t rows_per_block,
-    float* __restrict__ part, double* __restrict__ zsums) {
+    const float* __restrict__ mean, const float* __restrict__ weight,
+    const float* __restrict__ bias, const float* __restrict__ invstd, int64_t M, int C,
+    int64_t rows_per_block, float* __restrict__ part, double* __restrict__ zsums) {
   zero_moments(zsums, 2 * C);
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
@@ -306,23 +310,33 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
   const bool active = lr < L.rpi && cvec < L.cv;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = min(M, r0 + rows_per_block);
-  float s[VEC], q[VEC], mu[VEC];
+  float s[VEC], q[VEC], mu[VEC], msc[VEC], msh[VEC];
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; mu[i] = 0.f; }
+  for (int i = 0; i < VEC; ++i) { s[i] = 0.f; q[i] = 0.f; mu[i] = 0.f; msc[i] = 0.f; msh[i] = 0.f; }
   if (active) {
 #pragma unroll
-    for (int i = 0; i < VEC; ++i) mu[i] = mean[cvec * VEC + i];
+    for (int i = 0; i < VEC; ++i) {
+      const int ch = cvec * VEC + i;
+      mu[i] = mean[ch];
+      if (RELU == 2) {
+        msc[i] = (weight ? weight[ch] : 1.f) * invstd[ch];
+        msh[i] = (bias ? bias[ch] : 0.f) - mu[i] * msc[i];
+      }
+    }
     const int64_t off0 = (int64_t)cvec * VEC;
     for (int64_t r = r0 + lr; r < r1; r += L.rpi) {
       const int64_t o = r * C + off0;
       float g[VEC], xv[VEC];
       Vec16<T>::load(dy + o, g);
       Vec16<T>::load(x + o, xv);
-      if (RELU) {
+      if (RELU == 1) {
         float yv[VEC];
         Vec16<T>::load(y + o, yv);
 #pragma unroll
         for (int i = 0; i < VEC; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+      } else if (RELU == 2) {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
@@ -338,11 +352,11 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
 // Backward pass 2: dx = a*dz + b*x + c ; dres = dz (residual fused); the
 // row-slab-0 blocks write dweight = sum(dz*(x-mean))*invstd, dbias = sum(dz).
 // -------------------------------------------------------------------------
-template <typename T, bool RELU, bool DRES>
+template <typename T, int RELU, bool DRES>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const double* __restrict__ sums, const double* __restrict__ count_ptr,
-    const float* __restrict__ weight, const float* __restrict__ mean,
+    const float* __restrict__ weight, const float* __restrict__ bias, const float* __restrict__ mean,
     const float* __restrict__ invstd, int training, int64_t M, int C, int64_t rows_per_block,
     T* __restrict__ dx, T* __restrict__ dres, float* __restrict__ dweight,
     float* __restrict__ dbias) {
@@ -353,13 +367,19 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   const int cvec = blockIdx.y * L.tc + lc;
   if (lr >= L.rpi || cvec >= L.cv) return;
   const double n = *count_ptr;
-  float a[VEC], b[VEC], c[VEC];
+  float a[VEC], b[VEC], c[VEC], msc[VEC], msh[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     const int ch = cvec * VEC + i;
     const double sdz = sums[ch], sdzx = sums[C + ch];
     const double is = invstd[ch];
     const double aa = (double)(weight ? weight[ch] : 1.f) * is;
+    if (RELU == 2) {  // the forward's affine, as in bn_bwd_moments_kernel
+      msc[i] = (weight ? weight[ch] : 1.f) * invstd[ch];
+      msh[i] = (bias ? bias[ch] : 0.f) - mean[ch] * msc[i];
+    } else {
+      msc[i] = msh[i] = 0.f;
+    }
     if (training) {
       const double bb = -aa * is * is * sdzx / n;
       a[i] = (float)aa;
@@ -383,11 +403,14 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     float g[VEC], xv[VEC];
     Vec16<T>::load(dy + o, g);
     Vec16<T>::load(x + o, xv);
-    if (RELU) {
+    if (RELU == 1) {
       float yv[VEC];
       Vec16<T>::load(y + o, yv);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+    } else if (RELU == 2) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
     }
     if (DRES) Vec16<T>::store(dres + o, g);
 #pragma unroll
@@ -554,9 +577,13 @@ std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& run
 }
 
 // Backward local moments: fp64 [2C] = (sum dz, sum dz*(x-mean)).
+// relu with y undefined: the ReLU mask is re-derived from x with the forward's
+// affine (needs invstd; weight/bias optional) -- see bn_bwd_moments_kernel.
 at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                                const c10::optional<at::Tensor>& y, const at::Tensor& mean,
-                               bool relu, int64_t C) {
+                               bool relu, int64_t C, const c10::optional<at::Tensor>& weight,
+                               const c10::optional<at::Tensor>& bias,
+                               const c10::optional<at::Tensor>& invstd) {
   check_input(dy, C, "grad");
   check_input(x, C, "x");
   const int64_t M = x.numel() / C;
@@ -567,18 +594,21 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
   auto part = at::empty({2, (int64_t)g.grid.x, C}, x.options().dtype(at::kFloat));
   float* pp = part.data_ptr<float>();
   double* zt = moments_zero_target(sums.data_ptr<double>(), (int)g.grid.x);
+  const bool from_y = relu && y.has_value() && y->defined();
+  if (relu && !from_y)
+    TORCH_CHECK(invstd.has_value() && invstd->defined(), "relu mask from x needs invstd");
+  const float* ip = fptr(invstd);
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
-    if (relu) {
-      TORCH_CHECK(y.has_value() && y->defined(), "relu backward needs the saved output");
-      hipLaunchKernelGGL((bn_bwd_moments_kernel<T, true>), g.grid, dim3(kThreads), 0, stream,
-                         ptr<T>(dy), ptr<T>(x), ptr<T>(*y), mean.data_ptr<float>(), M, (int)C,
-                         g.rows_per_block, pp, zt);
-    } else {
-      hipLaunchKernelGGL((bn_bwd_moments_kernel<T, false>), g.grid, dim3(kThreads), 0, stream,
-                         ptr<T>(dy), ptr<T>(x), (const T*)nullptr, mean.data_ptr<float>(), M,
-                         (int)C, g.rows_per_block, pp, zt);
-    }
+    const T* yp = from_y ? ptr<T>(*y) : nullptr;
+#define DMP_BN_BM(MODE)                                                                          \
+  hipLaunchKernelGGL((bn_bwd_moments_kernel<T, MODE>), g.grid, dim3(kThreads), 0, stream,        \
+                     ptr<T>(dy), ptr<T>(x), yp, mean.data_ptr<float>(), fptr(weight), fptr(bias), \
+                     ip, M, (int)C, g.rows_per_block, pp, zt)
+    if (!relu) DMP_BN_BM(0);
+    else if (from_y) DMP_BN_BM(1);
+    else DMP_BN_BM(2);
+#undef DMP_BN_BM
   });
   bn_reduce_partials_launch(pp, (int)g.grid.x, (int)C, sums.data_ptr<double>(), -1.0, stream);
   return sums;
@@ -590,7 +620,8 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                                           const at::Tensor& sums, const at::Tensor& count,
                                           const c10::optional<at::Tensor>& weight,
                                           const at::Tensor& mean, const at::Tensor& invstd,
-                                          bool training, bool relu, bool want_dres, int64_t C) {
+                                          bool training, bool relu, bool want_dres, int64_t C,
+                                          const c10::optional<at::Tensor>& bias) {
   TORCH_CHECK(count.scalar_type() == at::kDouble && count.numel() >= 1, "count must be fp64");
   check_input(dy, C, "grad");
   const int64_t M = x.numel() / C;
@@ -603,18 +634,22 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
     Grid g = plan(M, (int)C, vec_of(x));
     dispatch_t(x, [&](auto tag) {
       using T = decltype(tag);
-      const T* yp = relu ? ptr<T>(*y) : nullptr;
+      const bool from_y = relu && y.has_value() && y->defined();
+      const T* yp = from_y ? ptr<T>(*y) : nullptr;
       T* dr = want_dres ? ptr<T>(dres) : nullptr;
 #define DMP_BN_BWD(RELU, DRES)                                                                    \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU, DRES>), g.grid, dim3(kThreads), 0, stream,     \
                      ptr<T>(dy), ptr<T>(x), yp, sums.data_ptr<double>(), count.data_ptr<double>(), \
-                     fptr(weight), mean.data_ptr<float>(), invstd.data_ptr<float>(),              \
+                     fptr(weight), fptr(bias), mean.data_ptr<float>(), invstd.data_ptr<float>(),  \
                      (int)training, M, (int)C, g.rows_per_block, ptr<T>(dx), dr,                  \
                      dwb.data_ptr<float>(), dwb.data_ptr<float>() + C)
-      if (relu && want_dres) DMP_BN_BWD(true, true);
-      else if (relu) DMP_BN_BWD(true, false);
-      else if (want_dres) DMP_BN_BWD(false, true);
-      else DMP_BN_BWD(false, false);
+      const int mode = !relu ? 0 : (from_y ? 1 : 2);
+      if (mode == 1 && want_dres) DMP_BN_BWD(1, true);
+      else if (mode == 1) DMP_BN_BWD(1, false);
+      else if (mode == 2 && want_dres) DMP_BN_BWD(2, true);
+      else if (mode == 2) DMP_BN_BWD(2, false);
+      else if (want_dres) DMP_BN_BWD(0, true);
+      else DMP_BN_BWD(0, false);
 #undef DMP_BN_BWD
     });
   }

@@ -132,29 +132,42 @@ def _apply_torch(x2, scale, shift, res2, relu):
     return y.to(x2.dtype)
 
 
-def backward_moments(dy2, x2, y2, mean, relu, native):
+def _relu_mask(x2, y2, mean, invstd, weight, bias):
+    """ReLU mask of the forward output: y > 0, or -- when y was not saved (no
+    residual fused) -- re-derived from x with the forward's per-channel affine."""
+    if y2 is not None:
+        return y2 > 0
+    sc = invstd * (weight if weight is not None else 1.0)
+    sh = (bias if bias is not None else 0.0) - mean * sc
+    return torch.addcmul(sh, x2.float(), sc) > 0
+
+
+def backward_moments(dy2, x2, y2, mean, relu, native, weight=None, bias=None, invstd=None):
     c = x2.shape[1]
     if native:
-        return _native.require("bn").bn_backward_moments(dy2, x2, y2, mean, relu, c)
+        return _native.require("bn").bn_backward_moments(dy2, x2, y2, mean, relu, c, weight, bias,
+                                                          invstd)
     dz = dy2.double()
     if relu:
-        dz = dz * (y2 > 0)
+        dz = dz * _relu_mask(x2, y2, mean, invstd, weight, bias)
     return torch.cat([dz.sum(0), (dz * (x2.double() - mean.double())).sum(0)])
 
 
-def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, relu, want_dres, native):
-    """`count` is a 1-element fp64 tensor (global rows)."""
+def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, relu, want_dres, native,
+                   bias=None):
+    """`count` is a 1-element fp64 tensor (global rows).  y2 None with relu:
+    mask from x (see _relu_mask)."""
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_backward_apply(dy2, x2, y2, sums, count, weight, mean,
-                                                        invstd, training, relu, want_dres, c)
+                                                        invstd, training, relu, want_dres, c, bias)
     count = count.reshape(()).to(torch.float64)
     sdz, sdzx = sums[:c], sums[c:]
     w = weight.double() if weight is not None else torch.ones_like(sdz)
     istd = invstd.double()
     dz = dy2.double()
     if relu:
-        dz = dz * (y2 > 0)
+        dz = dz * _relu_mask(x2, y2, mean, invstd, weight, bias)
     a = w * istd
     if training:
         b = -a * istd * istd * sdzx / count
@@ -203,7 +216,10 @@ class _BatchNormActFn(torch.autograd.Function):
             count = torch.full((1,), float(x2.shape[0]), dtype=torch.float64, device=x2.device)
             y2, mean, invstd = eval_apply(x2, running_mean, running_var, w32, b32, eps, res2, relu,
                                           native)
-        ctx.save_for_backward(x2, y2 if relu else None, w32, mean, invstd, count)
+        # the ReLU mask needs the output only when a residual was added before the
+        # ReLU; otherwise backward re-derives it from x (one tensor read fewer)
+        ctx.save_for_backward(x2, y2 if (relu and residual is not None) else None, w32, b32, mean,
+                              invstd, count)
         ctx.meta = (native, training, relu, residual is not None, back,
                     weight is not None, bias is not None, reduce_grads,
                     weight.dtype if weight is not None else None, x.dim())
@@ -211,17 +227,17 @@ class _BatchNormActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x2, y2, w32, mean, invstd, count = ctx.saved_tensors
+        x2, y2, w32, b32, mean, invstd, count = ctx.saved_tensors
         (native, training, relu, has_res, back, has_w, has_b, reduce_grads, wdtype,
          ndim) = ctx.meta
         dy2, _ = _as_rows(dy.to(x2.dtype))
-        sums = backward_moments(dy2, x2, y2, mean, relu, native)
+        sums = backward_moments(dy2, x2, y2, mean, relu, native, w32, b32, invstd)
         local_sums = sums
         if training and reduce_grads is not None:
             local_sums = sums.clone()  # the reducer works in place
             sums = reduce_grads(sums)
         dx2, dw, db, dres2 = backward_apply(dy2, x2, y2, sums, count, w32, mean, invstd, training,
-                                            relu, has_res, native)
+                                            relu, has_res, native, b32)
         if reduce_grads is not None and training:
             # weight/bias grads are per-rank quantities (DDP averages them)
             c = x2.shape[1]
