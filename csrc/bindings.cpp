@@ -27,6 +27,11 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                                bool relu, int64_t C, const c10::optional<at::Tensor>& weight,
                                const c10::optional<at::Tensor>& bias,
                                const c10::optional<at::Tensor>& invstd);
+at::Tensor bn_finalize(const at::Tensor& sums, const c10::optional<at::Tensor>& weight,
+                       const c10::optional<at::Tensor>& bias,
+                       const c10::optional<at::Tensor>& running_mean,
+                       const c10::optional<at::Tensor>& running_var, double momentum, double eps,
+                       int64_t C, const c10::optional<at::Tensor>& num_batches_tracked);
 std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor& x,
                                           const c10::optional<at::Tensor>& y,
                                           const at::Tensor& sums, const at::Tensor& count,
@@ -49,7 +54,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const std::vector<int64_t>& a_map,
                                 const std::vector<int64_t>& c_map);
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
-                   const std::vector<int64_t>& b_map);
+                   const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
+                   const c10::optional<at::Tensor>& pro_shift);
 std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int64_t kh,
                                 int64_t kw, int64_t stride, int64_t pad, int64_t ho, int64_t wo,
                                 bool transposed, const c10::optional<at::Tensor>& pro_scale,
@@ -92,6 +98,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("C"),
         py::arg("num_batches_tracked") = py::none());
   m.def("bn_eval_apply", &dmp::bn_eval_apply);
+  m.def("bn_finalize", &dmp::bn_finalize, py::arg("sums"), py::arg("weight"), py::arg("bias"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
+        py::arg("C"), py::arg("num_batches_tracked") = py::none());
   m.def("bn_backward_moments", &dmp::bn_backward_moments, py::arg("dy"), py::arg("x"), py::arg("y"),
         py::arg("mean"), py::arg("relu"), py::arg("C"), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(), py::arg("invstd") = py::none());
@@ -108,7 +117,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{});
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
-        py::arg("b_map") = std::vector<int64_t>{});
+        py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
+        py::arg("pro_shift") = py::none());
 
   m.def("set_gemm_tile", &dmp::set_gemm_tile,
         "debug: force the NT GEMM tile variant (-1 auto, 0 256x64, 1 128x64, 2 128x128, "

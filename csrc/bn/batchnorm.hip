@@ -202,6 +202,32 @@ __device__ __forceinline__ void fwd_coeffs(const double* __restrict__ sums, int 
   shift = bb - mean * scale;
 }
 
+// Coefficients only (no pass over x): when the BN apply + ReLU is fused into
+// the consuming GEMM's operand staging (ops/fused.py bn_relu_conv1x1), the BN
+// output is never materialised.  coef = [scale, shift, mean, invstd] x C;
+// running stats and the step counter are updated here.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const double* __restrict__ sums, const float* __restrict__ weight,
+    const float* __restrict__ bias, float* __restrict__ running_mean,
+    float* __restrict__ running_var, float momentum, float eps, int C, float* __restrict__ coef,
+    int64_t* __restrict__ num_batches_tracked) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (num_batches_tracked != nullptr && c == 0) *num_batches_tracked += 1;
+  if (c >= C) return;
+  float mean, invstd, var_b, sc, sh;
+  fwd_coeffs(sums, C, c, weight, bias, eps, mean, invstd, var_b, sc, sh);
+  coef[c] = sc;
+  coef[C + c] = sh;
+  coef[2 * C + c] = mean;
+  coef[3 * C + c] = invstd;
+  if (running_mean) {
+    const double n = sums[2 * C];
+    const float unb = n > 1.0 ? (float)((double)var_b * n / (n - 1.0)) : var_b;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  }
+}
+
 // -------------------------------------------------------------------------
 // Forward apply: y = act(x*scale + shift [+ residual]).
 // FROM_SUMS: training mode -- coefficients from the moments; row-slab-0 blocks
@@ -538,6 +564,30 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
     });
   }
   return {y, saved[0], saved[1]};
+}
+
+// Training-mode coefficients from (global) moments without touching x.
+// Returns coef [4, C] fp32 = (scale, shift, mean, invstd).
+at::Tensor bn_finalize(const at::Tensor& sums, const c10::optional<at::Tensor>& weight,
+                       const c10::optional<at::Tensor>& bias,
+                       const c10::optional<at::Tensor>& running_mean,
+                       const c10::optional<at::Tensor>& running_var, double momentum, double eps,
+                       int64_t C, const c10::optional<at::Tensor>& num_batches_tracked) {
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.numel() == 2 * C + 1,
+              "bad moments");
+  auto coef = at::empty({4, C}, sums.options().dtype(at::kFloat));
+  int64_t* nbt = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong && num_batches_tracked->numel() == 1,
+                "num_batches_tracked must be a 1-element int64 tensor");
+    nbt = num_batches_tracked->data_ptr<int64_t>();
+  }
+  auto stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, stream,
+                     sums.data_ptr<double>(), fptr(weight), fptr(bias), fptr(running_mean),
+                     fptr(running_var), (float)momentum, (float)eps, (int)C, coef.data_ptr<float>(),
+                     nbt);
+  return coef;
 }
 
 // Eval-mode apply from running statistics.  Returns (y, mean, invstd).

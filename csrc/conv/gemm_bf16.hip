@@ -438,10 +438,14 @@ __device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
   return row * row_bytes + (chunk << 5) + (byte & 31);
 }
 
-template <int BNT, int BKT>
+// PRO_B: B' = relu(B * s[k] + t[k]) applied while staging B (the weight
+// gradient of a conv whose input is a BN+ReLU output that was never
+// materialised -- ops/fused.py bn_relu_conv1x1).
+template <int BNT, int BKT, bool PRO_B>
 __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N,
-    int K, int64_t rows_per_split, float* __restrict__ part, ConvMap bmap) {
+    int K, int64_t rows_per_split, float* __restrict__ part, ConvMap bmap,
+    const float* __restrict__ bps, const float* __restrict__ bpt) {
   // 4 waves as 2 x 2, each wave (BNT/2) x (BKT/2) outputs
   constexpr int WTN = BNT / 2, WTK = BKT / 2;
   constexpr int MI = WTN / 16, NI = WTK / 16;
@@ -500,6 +504,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
         }
       }
       rb[i] = src ? *reinterpret_cast<const bf16x8*>(src) : bf16x8{};
+      if constexpr (PRO_B) {
+        if (src) {
+          const int kk = (bmap.kc == 0 ? k0 : kc0) + c;  // channel of this 8-vector
+          f32x8 f = __builtin_convertvector(rb[i], f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(fmaf(f[j], bps[kk + j], bpt[kk + j]), 0.f);
+          rb[i] = __builtin_convertvector(f, bf16x8);
+        }
+      }
     }
   };
   auto store = [&](int buf) {
@@ -624,11 +637,19 @@ void check_operand(const at::Tensor& t, const char* name) {
 
 template <int BNT, int BKT>
 void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, float* part,
-               int splits, int64_t rps, const ConvMap& bm, hipStream_t s) {
+               int splits, int64_t rps, const ConvMap& bm, const float* bps, const float* bpt,
+               hipStream_t s) {
   const int tiles = ((N + BNT - 1) / BNT) * ((K + BKT - 1) / BKT);
-  hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT>), dim3(tiles * splits), dim3(kThreads), 0, s,
-                     reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
-                     reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part, bm);
+  if (bps)
+    hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT, true>), dim3(tiles * splits), dim3(kThreads), 0, s,
+                       reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
+                       reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part,
+                       bm, bps, bpt);
+  else
+    hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT, false>), dim3(tiles * splits), dim3(kThreads), 0, s,
+                       reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
+                       reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part,
+                       bm, nullptr, nullptr);
 }
 
 }  // namespace
@@ -637,7 +658,8 @@ namespace {
 
 // C[N, K] = sum_m A[m, :]^T Bmapped[m, :]  -> out [N, K] (bf16 or fp32)
 at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
-                  at::ScalarType out_dtype, const ConvMap& bmap, int kgran) {
+                  at::ScalarType out_dtype, const ConvMap& bmap, int kgran,
+                  const float* bps = nullptr, const float* bpt = nullptr) {
   auto stream = at::hip::getCurrentHIPStream();
   auto out = at::empty({N, K}, A.options().dtype(out_dtype));
   if (M == 0) return out.zero_();
@@ -658,10 +680,10 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   splits = (int)(((int64_t)M + rps - 1) / rps);
   auto part = at::empty({splits, N, K}, A.options().dtype(at::kFloat));
   float* pp = part.data_ptr<float>();
-  if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, bmap, stream);
-  else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, stream);
-  else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, stream);
-  else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, bmap, stream);
+  if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
+  else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
+  else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
+  else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   const int64_t n = (int64_t)N * K;
   int sl = 1;  // split lanes per column: grow until >= 512 blocks or lanes cover the splits
   while (sl < 64 && sl < splits && (n / 4 + 256 / sl - 1) / (256 / sl) < 512) sl *= 2;
@@ -681,7 +703,8 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
 // row-major).  Output dtype bf16 or fp32.  b_map ([s, Ho, Wo, Hi, Wi]) reads
 // B's logical row m from the strided physical row (stride-s 1x1 conv input).
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
-                   const std::vector<int64_t>& b_map) {
+                   const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
+                   const c10::optional<at::Tensor>& pro_shift) {
   check_operand(A, "A");
   check_operand(B, "B");
   const RowMap rm = parse_map(b_map, "b_map");
@@ -698,7 +721,17 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
   }
   const int M = (int)A.size(0), N = (int)A.size(1), K = (int)B.size(1);
   TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "N and K must be multiples of 8");
-  return run_tn(A, B, M, N, K, out_dtype, cm, 128);
+  const float* bps = nullptr;
+  const float* bpt = nullptr;
+  if (pro_scale.has_value() && pro_scale->defined()) {
+    TORCH_CHECK(pro_shift.has_value() && pro_shift->defined() && pro_scale->numel() == K &&
+                    pro_shift->numel() == K && pro_scale->scalar_type() == at::kFloat &&
+                    pro_shift->scalar_type() == at::kFloat,
+                "B prologue needs fp32 scale and shift of length K");
+    bps = pro_scale->data_ptr<float>();
+    bpt = pro_shift->data_ptr<float>();
+  }
+  return run_tn(A, B, M, N, K, out_dtype, cm, 128, bps, bpt);
 }
 
 // Weight gradient of an implicit-GEMM conv: dy [N*Ho*Wo, Cout] rows, x NHWC

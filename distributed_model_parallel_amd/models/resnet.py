@@ -20,7 +20,7 @@ import torch.nn as nn
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
-from ..ops.fused import GradSlot, conv_bn, grad_tap
+from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, grad_tap
 from ..ops.pool import MaxPool2d
 
 
@@ -81,6 +81,11 @@ class Bottleneck(nn.Module):
         slot = GradSlot() if (self.training and torch.is_grad_enabled()) else None
         out = conv_bn(self.conv1, self.bn1, x, grad_slot=slot)
         identity = _shortcut(self.downsample, grad_tap(x, slot))
+        if self.training and isinstance(self.bn3, BatchNormAct2d) and hasattr(self.conv2, "forward_with_moments"):
+            # bn2's apply + ReLU runs inside conv3's GEMM (never materialised)
+            raw, sums2 = self.conv2.forward_with_moments(out)
+            out, sums3 = bn_relu_conv1x1(self.bn2, self.conv3, raw, sums2)
+            return self.bn3(out, identity, sums=sums3)
         out = conv_bn(self.conv2, self.bn2, out)
         return conv_bn(self.conv3, self.bn3, out, identity)
 

@@ -79,3 +79,107 @@ def conv_bn(conv: nn.Module, bn: nn.Module, x: torch.Tensor,
     if residual is not None:
         return bn(y) + residual
     return bn(y)
+
+
+# --------------------------------------------------------------------------- #
+# BN(+ReLU) applied inside the consuming 1x1 conv (training)
+# --------------------------------------------------------------------------- #
+class _BNReLUConv1x1Fn(torch.autograd.Function):
+    """y = conv1x1(relu(bn(x))) with the BN output never materialised:
+
+    forward   bn_finalize (coefficients from the fused moments, running stats),
+              then the MFMA GEMM applies relu(x*scale + shift) while staging A
+              (optionally emitting the moments of y for the next BN);
+    backward  dgrad GEMM -> d(bn out); weight gradient GEMM re-applies the
+              prologue while staging B; BN backward with the ReLU mask
+              re-derived from x.  (Capability: conv(bn_relu(x)) as in the
+              reference's torchvision ResNet-50; design: ours.)"""
+
+    @staticmethod
+    def forward(ctx, x, bn_w, bn_b, conv_w, sums, running_mean, running_var, momentum, eps, nbt,
+                reduce_moments, reduce_grads, moments_out):
+        from .. import _native
+        from .conv1x1 import _rows, _unrows
+        C = _native.require("bn_relu_conv1x1")
+        n, cin, h, w = x.shape
+        x2 = _rows(x)
+        if reduce_moments is not None:
+            sums = reduce_moments(sums)
+        w32 = bn_w.float() if bn_w is not None else None
+        b32 = bn_b.float() if bn_b is not None else None
+        coef = C.bn_finalize(sums, w32, b32, running_mean, running_var, float(momentum), float(eps),
+                             cin, nbt)
+        scale, shift, mean, invstd = coef[0], coef[1], coef[2], coef[3]
+        cout = conv_w.shape[0]
+        y2, mom = C.gemm_nt(x2, conv_w.reshape(cout, cin), pro_scale=scale, pro_shift=shift,
+                            mode="moments" if moments_out else "store")
+        ctx.save_for_backward(x, conv_w, w32, b32, coef, sums[-1:])
+        ctx.meta = (reduce_grads, bn_w.dtype if bn_w is not None else None, bn_w is not None,
+                    bn_b is not None)
+        if mom is None:
+            mom = torch.empty(0, device=x.device, dtype=torch.float64)
+        ctx.mark_non_differentiable(mom)
+        ctx.set_materialize_grads(False)
+        return _unrows(y2, n, h, w), mom
+
+    @staticmethod
+    def backward(ctx, dy, _dmom):
+        if dy is None:
+            return (None,) * 13
+        from .. import _native
+        from .conv1x1 import _rows, _unrows
+        C = _native.require("bn_relu_conv1x1 backward")
+        x, conv_w, w32, b32, coef, count = ctx.saved_tensors
+        reduce_grads, wdtype, has_w, has_b = ctx.meta
+        n, cin, h, w = x.shape
+        cout = conv_w.shape[0]
+        scale, shift, mean, invstd = coef[0], coef[1], coef[2], coef[3]
+        x2 = _rows(x)
+        dy2 = _rows(dy.contiguous(memory_format=torch.channels_last).to(x.dtype))
+        w2 = conv_w.reshape(cout, cin)
+        g2, _ = C.gemm_nt(dy2, w2.t().contiguous())            # d(relu(bn(x)))
+        dw = C.gemm_tn(dy2, x2, conv_w.dtype, pro_scale=scale, pro_shift=shift).view(cout, cin, 1, 1)
+        if conv_w.is_contiguous(memory_format=torch.channels_last):
+            dw = dw.contiguous(memory_format=torch.channels_last)
+        sums = C.bn_backward_moments(g2, x2, None, mean, True, cin, w32, b32, invstd)
+        local = sums
+        if reduce_grads is not None:
+            local = sums.clone()  # the reducer works in place
+            sums = reduce_grads(sums)
+        dx2, dg, db, _ = C.bn_backward_apply(g2, x2, None, sums, count, w32, mean, invstd, True,
+                                             True, False, cin, b32)
+        if reduce_grads is not None:
+            dg = (local[cin:] * invstd.double()).float()
+            db = local[:cin].float()
+        gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[1] else None
+        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[2] else None
+        return (_unrows(dx2, n, h, w), gw, gb, dw, None, None, None, None, None, None, None, None,
+                None)
+
+
+def bn_relu_conv1x1(bn: nn.Module, conv: nn.Module, x: torch.Tensor,
+                    sums: Optional[torch.Tensor], moments_out: bool = True):
+    """conv(relu(bn(x))) -> (y, moments-of-y or None).  Fused (BN apply + ReLU in
+    the GEMM's operand staging) when training natively with fused input moments;
+    otherwise the two modules run as usual."""
+    from .. import _native
+    from ..utils.checkpointing import in_recompute
+    from .conv1x1 import Conv1x1, _native_ok
+    fusable = (sums is not None and isinstance(bn, BatchNormAct2d) and bn.act == "relu"
+               and bn.training and bn.track_running_stats and bn.momentum is not None
+               and not in_recompute() and isinstance(conv, Conv1x1) and conv.stride[0] == 1
+               and bn.running_mean is not None and bn.running_mean.dtype == torch.float32
+               and _native_ok(x, conv.weight) and torch.is_grad_enabled())
+    if not fusable:
+        y = bn(x, sums=sums)
+        return conv.forward_with_moments(y) if moments_out else (conv(y), None)
+    rmom, rgrad = bn._moment_reducers()
+    nbt = bn.num_batches_tracked
+    y, mom = _BNReLUConv1x1Fn.apply(x, bn.weight, bn.bias, conv.weight, sums, bn.running_mean,
+                                    bn.running_var, bn.momentum, bn.eps, nbt, rmom, rgrad,
+                                    moments_out)
+    _STATS_FUSED["bn_relu_conv1x1"] += 1
+    return y, (mom if moments_out else None)
+
+
+_STATS_FUSED = {"bn_relu_conv1x1": 0}

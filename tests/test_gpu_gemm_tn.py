@@ -96,3 +96,17 @@ def test_conv1x1_stride2_odd_spatial():
     yr.backward(g)
     torch.testing.assert_close(xi.grad.float(), xr.grad, atol=0.1, rtol=2e-2)
     torch.testing.assert_close(m.weight.grad.float(), wr.grad, atol=0.5, rtol=2e-2)
+
+
+def test_gemm_tn_b_prologue():
+    """B' = relu(B*s + t) per column, applied while staging (bn_relu_conv1x1 weight grad)."""
+    C = _native.require("gemm_tn")
+    torch.manual_seed(5)
+    M, N, K = 3000, 64, 192
+    a = torch.randn(M, N, device=DEV).bfloat16()
+    b = torch.randn(M, K, device=DEV).bfloat16()
+    s = torch.rand(K, device=DEV) + 0.5
+    t = torch.randn(K, device=DEV) * 0.2
+    got = C.gemm_tn(a, b, torch.float32, pro_scale=s, pro_shift=t)
+    bp = torch.relu(b.float() * s + t).bfloat16().float()
+    torch.testing.assert_close(got, a.float().t() @ bp, atol=1e-3 * M ** 0.5, rtol=1e-2)

@@ -127,3 +127,44 @@ def test_bottleneck_fused_shortcut_grad(stride, ds):
         outs.append(xi.grad.float())
     err = (outs[0] - outs[1]).norm() / outs[1].norm()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_bottleneck_bn_relu_fused_into_conv3(stride):
+    """bn2's apply + ReLU inside conv3's GEMM (ops/fused.py bn_relu_conv1x1): same output,
+    gradients and running statistics as the unfused composition of the same modules."""
+    from distributed_model_parallel_amd.models.resnet import Bottleneck
+    from distributed_model_parallel_amd.ops import fused
+    from distributed_model_parallel_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(0)
+    cin, planes = 256, 64
+    down = None
+    if stride != 1:
+        down = torch.nn.Sequential(conv1x1.Conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4))
+    blk = cast_model(Bottleneck(cin, planes, stride, down).to(DEV).to(memory_format=torch.channels_last))
+    ref = copy.deepcopy(blk)
+    blk.train()
+    ref.train()
+    for m in (blk, ref):
+        torch.nn.init.normal_(m.bn3.weight, 1.0, 0.1)  # not zero-init, so conv3's path matters
+    x = torch.randn(8, cin, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    xa, xb = x.detach().requires_grad_(), x.detach().requires_grad_()
+    n0 = fused._STATS_FUSED["bn_relu_conv1x1"]
+    ya = blk(xa)
+    assert fused._STATS_FUSED["bn_relu_conv1x1"] == n0 + 1
+    idn = xb if down is None else ref.downsample[1](ref.downsample[0](xb))
+    out = ref.bn1(ref.conv1(xb))
+    out = ref.bn2(ref.conv2(out))
+    yb = ref.bn3(ref.conv3(out), idn)
+    torch.testing.assert_close(ya.float(), yb.float(), atol=5e-2, rtol=5e-2)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    for (na, pa), (nb, pb) in zip(blk.named_parameters(), ref.named_parameters()):
+        cos = F.cosine_similarity(pa.grad.float().flatten(), pb.grad.float().flatten(), dim=0).item()
+        assert cos > 0.99, (na, cos)
+    cos = F.cosine_similarity(xa.grad.float().flatten(), xb.grad.float().flatten(), dim=0).item()
+    assert cos > 0.99, cos
+    torch.testing.assert_close(blk.bn2.running_mean, ref.bn2.running_mean, atol=1e-3, rtol=1e-2)
+    torch.testing.assert_close(blk.bn2.running_var, ref.bn2.running_var, atol=1e-3, rtol=1e-2)
+    assert int(blk.bn2.num_batches_tracked) == int(ref.bn2.num_batches_tracked) == 1
