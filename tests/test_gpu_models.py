@@ -142,11 +142,11 @@ def test_bottleneck_bn_relu_fused_into_conv3(stride):
     if stride != 1:
         down = torch.nn.Sequential(conv1x1.Conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4))
     blk = cast_model(Bottleneck(cin, planes, stride, down).to(DEV).to(memory_format=torch.channels_last))
+    with torch.no_grad():
+        blk.bn3.weight.normal_(1.0, 0.1)  # not zero-init, so conv3's path matters
     ref = copy.deepcopy(blk)
     blk.train()
     ref.train()
-    for m in (blk, ref):
-        torch.nn.init.normal_(m.bn3.weight, 1.0, 0.1)  # not zero-init, so conv3's path matters
     x = torch.randn(8, cin, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
     xa, xb = x.detach().requires_grad_(), x.detach().requires_grad_()
     n0 = fused._STATS_FUSED["bn_relu_conv1x1"]

@@ -45,7 +45,8 @@ def main() -> int:
                 if k.strip().startswith("LDS Size"):
                     name = subprocess.run(["c++filt", cur["name"]],
                                           capture_output=True, text=True).stdout.strip()
-                    name = re.sub(r"\(.*", "", name).replace("dmp::(anonymous namespace)::", "")
+                    name = name.replace("dmp::(anonymous namespace)::", "").replace("void ", "")
+                    name = re.sub(r"\(.*", "", name)
                     scratch = cur.get("ScratchSize [bytes/lane]", "?")
                     bad += scratch not in ("0", "?")
                     print(f"| {os.path.relpath(src, ROOT)} | `{name[:90]}` | {cur.get('VGPRs', '?')} | "
