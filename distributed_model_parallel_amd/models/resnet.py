@@ -12,6 +12,7 @@ MI355X-first choices:
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Type, Union
 
 import torch
@@ -22,6 +23,13 @@ from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, grad_tap
 from ..ops.pool import MaxPool2d
+
+
+# bn2 -> conv3 prologue fusion (ops/fused.py bn_relu_conv1x1).  Off by default:
+# measured on MI355X (profiles/README.md finding 6) the per-element BN+ReLU in
+# the GEMM operand staging costs more (+0.2 ms forward GEMM, +0.5 ms weight
+# gradient) than the removed BN apply pass saves (0.39 ms).
+_FUSE_BN2_CONV3 = os.environ.get("DMP_FUSE_BN_CONV", "0") == "1"
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -81,7 +89,8 @@ class Bottleneck(nn.Module):
         slot = GradSlot() if (self.training and torch.is_grad_enabled()) else None
         out = conv_bn(self.conv1, self.bn1, x, grad_slot=slot)
         identity = _shortcut(self.downsample, grad_tap(x, slot))
-        if self.training and isinstance(self.bn3, BatchNormAct2d) and hasattr(self.conv2, "forward_with_moments"):
+        if _FUSE_BN2_CONV3 and self.training and isinstance(self.bn3, BatchNormAct2d) \
+                and hasattr(self.conv2, "forward_with_moments"):
             # bn2's apply + ReLU runs inside conv3's GEMM (never materialised)
             raw, sums2 = self.conv2.forward_with_moments(out)
             out, sums3 = bn_relu_conv1x1(self.bn2, self.conv3, raw, sums2)

@@ -141,6 +141,8 @@ def test_bottleneck_bn_relu_fused_into_conv3(stride):
     down = None
     if stride != 1:
         down = torch.nn.Sequential(conv1x1.Conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4))
+    from distributed_model_parallel_amd.models import resnet as resnet_mod
+    old_flag, resnet_mod._FUSE_BN2_CONV3 = resnet_mod._FUSE_BN2_CONV3, True
     blk = cast_model(Bottleneck(cin, planes, stride, down).to(DEV).to(memory_format=torch.channels_last))
     with torch.no_grad():
         blk.bn3.weight.normal_(1.0, 0.1)  # not zero-init, so conv3's path matters
@@ -150,7 +152,10 @@ def test_bottleneck_bn_relu_fused_into_conv3(stride):
     x = torch.randn(8, cin, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
     xa, xb = x.detach().requires_grad_(), x.detach().requires_grad_()
     n0 = fused._STATS_FUSED["bn_relu_conv1x1"]
-    ya = blk(xa)
+    try:
+        ya = blk(xa)
+    finally:
+        resnet_mod._FUSE_BN2_CONV3 = old_flag
     assert fused._STATS_FUSED["bn_relu_conv1x1"] == n0 + 1
     idn = xb if down is None else ref.downsample[1](ref.downsample[0](xb))
     out = ref.bn1(ref.conv1(xb))
