@@ -75,6 +75,15 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
                            int64_t W);
 at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride,
                            at::ScalarType out_dtype);
+// layernorm.hip
+std::vector<at::Tensor> layernorm_forward(const at::Tensor& x, const c10::optional<at::Tensor>& w,
+                                          const c10::optional<at::Tensor>& b, int64_t D,
+                                          double eps);
+std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tensor& x,
+                                           const c10::optional<at::Tensor>& w,
+                                           const at::Tensor& mean, const at::Tensor& rstd,
+                                           int64_t D, at::ScalarType param_dtype);
+bool layernorm_supported(int64_t D);
 // maxpool.hip
 std::vector<at::Tensor> maxpool2d_forward(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
 at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W,
@@ -133,6 +142,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("relu") = false);
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"));
+
+  // ---- LayerNorm (last dim) ----
+  m.def("layernorm_forward", &dmp::layernorm_forward);
+  m.def("layernorm_backward", &dmp::layernorm_backward);
+  m.def("layernorm_supported", &dmp::layernorm_supported);
 
   // ---- NHWC max pooling with byte argmax ----
   m.def("maxpool2d_forward", &dmp::maxpool2d_forward);

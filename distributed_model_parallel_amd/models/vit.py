@@ -16,6 +16,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.layernorm import LayerNorm
+
 
 class MLP(nn.Module):
     def __init__(self, dim: int, hidden: int, dropout: float = 0.0):
@@ -50,9 +52,9 @@ class SelfAttention(nn.Module):
 class EncoderBlock(nn.Module):
     def __init__(self, dim: int, heads: int, mlp_dim: int, dropout: float = 0.0):
         super().__init__()
-        self.ln1 = nn.LayerNorm(dim, eps=1e-6)
+        self.ln1 = LayerNorm(dim, eps=1e-6)
         self.attn = SelfAttention(dim, heads, dropout)
-        self.ln2 = nn.LayerNorm(dim, eps=1e-6)
+        self.ln2 = LayerNorm(dim, eps=1e-6)
         self.mlp = MLP(dim, mlp_dim, dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -74,7 +76,7 @@ class VisionTransformer(nn.Module):
         self.pos_embedding = nn.Parameter(torch.empty(1, n_tokens, hidden_dim).normal_(std=0.02))
         self.blocks = nn.Sequential(*[EncoderBlock(hidden_dim, num_heads, mlp_dim, dropout)
                                       for _ in range(num_layers)])
-        self.ln = nn.LayerNorm(hidden_dim, eps=1e-6)
+        self.ln = LayerNorm(hidden_dim, eps=1e-6)
         self.head = nn.Linear(hidden_dim, num_classes)
         self._init()
 

@@ -1,0 +1,37 @@
+"""Native LayerNorm (one wave per row) vs an fp32 F.layer_norm reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd.ops.layernorm import _STATS, layer_norm
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype,pdtype", [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
+                                          (torch.float32, torch.float32)])
+@pytest.mark.parametrize("shape", [(128, 197, 768), (7, 1024), (3, 5, 1536), (2, 2048), (1000, 64)])
+def test_layernorm_fwd_bwd(dtype, pdtype, shape):
+    torch.manual_seed(0)
+    d = shape[-1]
+    x = (torch.randn(*shape, device="cuda") * 2 + 0.5).to(dtype)
+    w = (torch.rand(d, device="cuda") + 0.5).to(pdtype).requires_grad_()
+    b = torch.randn(d, device="cuda").to(pdtype).requires_grad_()
+    xi = x.detach().requires_grad_()
+    n0 = _STATS["native"]
+    y = layer_norm(xi, (d,), w, b, 1e-6)
+    assert _STATS["native"] == n0 + 1
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    br = b.detach().float().requires_grad_()
+    yr = F.layer_norm(xr, (d,), wr, br, 1e-6)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol * 2, rtol=tol)
+    rows = x.numel() // d
+    gtol = (2e-2 if pdtype == torch.bfloat16 else 1e-3) * rows ** 0.5
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=gtol, rtol=2e-2)
+    torch.testing.assert_close(b.grad.float(), br.grad, atol=gtol, rtol=2e-2)
