@@ -179,7 +179,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_property_readonly("size", &dmp::RcclComm::size)
       .def_property_readonly("device", &dmp::RcclComm::device)
       .def("all_reduce", &dmp::RcclComm::all_reduce, py::arg("tensor"), py::arg("op") = "sum",
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("on_current_stream") = false, py::call_guard<py::gil_scoped_release>())
       .def("all_reduce_coalesced", &dmp::RcclComm::all_reduce_coalesced, py::arg("tensors"),
            py::arg("op") = "sum", py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &dmp::RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())

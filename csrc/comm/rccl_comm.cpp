@@ -88,14 +88,22 @@ void RcclComm::record_usage(const at::Tensor& t) {
     c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
 }
 
-void RcclComm::all_reduce(at::Tensor& t, const std::string& op) {
+void RcclComm::all_reduce(at::Tensor& t, const std::string& op, bool on_current_stream) {
   std::lock_guard<std::mutex> lk(mu_);
   TORCH_CHECK(t.is_contiguous(), "all_reduce needs a contiguous tensor");
   c10::hip::HIPGuard guard((c10::DeviceIndex)device_);
-  sync_from_current();
-  record_usage(t);
+  hipStream_t s;
+  if (on_current_stream) {
+    // a small collective whose result the very next kernel needs (SyncBN
+    // moments): no side stream, no event pair, nothing to overlap anyway
+    s = at::hip::getCurrentHIPStream((c10::DeviceIndex)device_).stream();
+  } else {
+    sync_from_current();
+    record_usage(t);
+    s = st();
+  }
   DMP_NCCL_CHECK(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), to_nccl_dtype(t),
-                               to_nccl_op(op), comm_, st()));
+                               to_nccl_op(op), comm_, s));
 }
 
 void RcclComm::all_reduce_coalesced(std::vector<at::Tensor>& ts, const std::string& op) {

@@ -35,7 +35,7 @@ class RcclComm {
 
   // All ops: the comm stream first waits for the caller's current stream, then
   // enqueues the collective.  They return immediately (asynchronous).
-  void all_reduce(at::Tensor& t, const std::string& op);
+  void all_reduce(at::Tensor& t, const std::string& op = "sum", bool on_current_stream = false);
   void all_reduce_coalesced(std::vector<at::Tensor>& ts, const std::string& op);
   void broadcast(at::Tensor& t, int64_t root);
   void reduce(at::Tensor& t, int64_t root, const std::string& op);

@@ -65,9 +65,12 @@ class Communicator:
         """The underlying ``_C.RcclComm`` (None on CPU)."""
         return self._comm
 
-    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", on_current_stream: bool = False) -> torch.Tensor:
+        """In place.  Default: on the communicator's side stream (call wait()
+        before consuming).  on_current_stream: enqueued on the caller's stream
+        (for small collectives needed immediately; no wait() required)."""
         if self._comm is not None:
-            self._comm.all_reduce(t, op)
+            self._comm.all_reduce(t, op, on_current_stream)
             return t
         if op == "avg":
             dist.all_reduce(t, group=self.group)

@@ -49,9 +49,10 @@ class SyncBatchNorm(BatchNormAct2d):
         comm = self._communicator(dev)
 
         def reduce(t: torch.Tensor) -> torch.Tensor:
+            # tiny ([2C+1] fp64) and needed by the very next kernel: enqueue on the
+            # compute stream itself (no side stream / event pair per layer)
             t = t.contiguous()
-            comm.all_reduce(t, "sum")
-            comm.wait()
+            comm.all_reduce(t, "sum", on_current_stream=True)
             return t
 
         return reduce, reduce

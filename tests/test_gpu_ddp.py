@@ -38,6 +38,16 @@ for parallel in ("ddp", "syncbn"):
               for x, y in zip(a[1], b[1]) if y.norm() > 0)
     assert cos > 0.98, (parallel, cos)
     print(parallel, "ok", a[0], b[0], b[2], cos)
+from distributed_model_parallel_amd.comm.rccl import default_communicator
+comm = default_communicator(env.device)
+t = torch.arange(10, dtype=torch.float64, device=env.device)
+comm.all_reduce(t, "sum", on_current_stream=True)   # SyncBN's path
+u = torch.arange(10, dtype=torch.float32, device=env.device)
+comm.all_reduce(u, "avg")
+comm.wait()
+torch.cuda.synchronize()
+assert torch.equal(t.cpu(), torch.arange(10, dtype=torch.float64)) and torch.equal(u.cpu(), torch.arange(10.0))
+print("rccl on-current-stream ok")
 destroy_distributed()
 '''
 
@@ -60,3 +70,4 @@ def test_ddp_and_syncbn_rccl_backend_world1():
         print(r.stderr[-6000:])
     assert r.returncode == 0, "subprocess failed (output above)"
     assert "ddp ok" in r.stdout and "syncbn ok" in r.stdout
+    assert "rccl on-current-stream ok" in r.stdout
