@@ -44,6 +44,18 @@ def _wait_for(src_dev: torch.device, dst_dev: torch.device) -> None:
     torch.cuda.current_stream(dst_dev).wait_event(ev)
 
 
+def _keep_alive(srcs: Sequence[torch.Tensor], consumer: torch.device) -> None:
+    """A kernel on `consumer` reads these peer tensors: tell each source device's
+    caching allocator not to reuse the memory before the consumer stream is done
+    (the Python references may die as soon as the launch returns)."""
+    if consumer.type != "cuda":
+        return
+    stream = torch.cuda.current_stream(consumer)
+    for t in srcs:
+        if t.is_cuda and t.device != consumer:
+            t.record_stream(stream)
+
+
 def pull_copy(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> None:
     """dst[i] <- src[i]; one kernel on dst's device reading (possibly peer) sources."""
     if not srcs:
@@ -51,6 +63,7 @@ def pull_copy(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> Non
     dd = dsts[0].device
     for s in {t.device for t in srcs}:
         _wait_for(s, dd)
+    _keep_alive(srcs, dd)
     if dd.type == "cuda":
         with torch.cuda.device(dd):
             _native.require("DataParallel pull copy").multi_copy(list(srcs), list(dsts))
@@ -129,6 +142,7 @@ def reduce_add_coalesced(grads_per_device: Sequence[Sequence[torch.Tensor]],
         res = torch.empty(total, dtype=flats[0].dtype, device=dst)
         for f in flats:
             _wait_for(f.device, dst)
+        _keep_alive(flats, dst)
         if dst.type == "cuda":
             with torch.cuda.device(dst):
                 _native.require("reduce_add").reduce_add_into(flats, res)
@@ -195,6 +209,7 @@ def gather_tensors(ts: Sequence[torch.Tensor], destination, dim: int = 0) -> tor
     for t in ts:
         _wait_for(t.device, dst)
     srcs = [t.contiguous() for t in ts]
+    _keep_alive(srcs, dst)
     if dim == 0:
         views = [s.view(s.shape[0], -1) for s in srcs]
         out2 = out.view(shape[0], -1)
