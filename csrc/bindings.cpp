@@ -82,7 +82,8 @@ std::vector<at::Tensor> layernorm_forward(const at::Tensor& x, const c10::option
 std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tensor& x,
                                            const c10::optional<at::Tensor>& w,
                                            const at::Tensor& mean, const at::Tensor& rstd,
-                                           int64_t D, at::ScalarType param_dtype);
+                                           int64_t D, at::ScalarType param_dtype,
+                                           const c10::optional<at::Tensor>& dres);
 bool layernorm_supported(int64_t D);
 // maxpool.hip
 std::vector<at::Tensor> maxpool2d_forward(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
@@ -145,7 +146,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- LayerNorm (last dim) ----
   m.def("layernorm_forward", &dmp::layernorm_forward);
-  m.def("layernorm_backward", &dmp::layernorm_backward);
+  m.def("layernorm_backward", &dmp::layernorm_backward, py::arg("dy"), py::arg("x"), py::arg("w"),
+        py::arg("mean"), py::arg("rstd"), py::arg("D"), py::arg("param_dtype"),
+        py::arg("dres") = py::none());
   m.def("layernorm_supported", &dmp::layernorm_supported);
 
   // ---- NHWC max pooling with byte argmax ----

@@ -136,7 +136,7 @@ template <typename T, typename P, int kMaxV>
 __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const P* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows, int D,
-    T* __restrict__ dx, float* __restrict__ part) {
+    T* __restrict__ dx, float* __restrict__ part, const T* __restrict__ dres) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nv = D / 8;
   const int64_t wave = (int64_t)blockIdx.x * (kLnThreads / 64) + wid;
@@ -179,6 +179,12 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
         float o[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = rstd * (g[k][i] - xh[k][i] * c1 - c2);
+        if (dres) {  // + the residual branch's gradient of the same input (one pass)
+          float rv[8];
+          ld8<T>(dres + r * D + c * 8, rv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += rv[i];
+        }
         st8<T>(dx + r * D + c * 8, o);
       }
     }
@@ -283,12 +289,18 @@ std::vector<at::Tensor> layernorm_forward(const at::Tensor& x, const c10::option
 std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tensor& x,
                                            const c10::optional<at::Tensor>& w,
                                            const at::Tensor& mean, const at::Tensor& rstd,
-                                           int64_t D, at::ScalarType param_dtype) {
+                                           int64_t D, at::ScalarType param_dtype,
+                                           const c10::optional<at::Tensor>& dres) {
   check_ln(x, D, "x");
   check_ln(dy, D, "dy");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "dy/x dtype mismatch");
   TORCH_CHECK(layernorm_supported(D), "layernorm: D must be a multiple of 8 and <= 2048");
   const bool hw = w.has_value() && w->defined();
+  const bool hr = dres.has_value() && dres->defined();
+  if (hr) {
+    check_ln(*dres, D, "dres");
+    TORCH_CHECK(dres->scalar_type() == x.scalar_type() && dres->numel() == x.numel(), "bad dres");
+  }
   const int64_t rows = x.numel() / D;
   auto dx = at::empty_like(x);
   auto dwb = at::empty({2, D}, x.options().dtype(param_dtype));
@@ -303,7 +315,8 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
                      reinterpret_cast<const T*>(x.data_ptr()),                                  \
                      hw ? reinterpret_cast<const P*>(w->data_ptr()) : nullptr,                  \
                      mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)D,               \
-                     reinterpret_cast<T*>(dx.data_ptr()), part.data_ptr<float>())
+                     reinterpret_cast<T*>(dx.data_ptr()), part.data_ptr<float>(),             \
+                     hr ? reinterpret_cast<const T*>(dres->data_ptr()) : nullptr)
   if (x.scalar_type() == at::kBFloat16) {
     if (pbf) DMP_LN_BWD(__bf16, __bf16); else DMP_LN_BWD(__bf16, float);
   } else {

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.fused import GradSlot, grad_tap
 from ..ops.layernorm import LayerNorm
 
 
@@ -58,8 +59,16 @@ class EncoderBlock(nn.Module):
         self.mlp = MLP(dim, mlp_dim, dropout)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = x + self.attn(self.ln1(x))
-        return x + self.mlp(self.ln2(x))
+        # pre-LN residuals: each LayerNorm's backward also adds the residual
+        # branch's gradient of its input (ops/fused.py GradSlot) -- no add kernel.
+        # The tap is created after the LN so its backward node runs first.
+        train = self.training and torch.is_grad_enabled()
+        s1 = GradSlot() if train else None
+        h = self.ln1(x, s1)
+        x = grad_tap(x, s1) + self.attn(h)
+        s2 = GradSlot() if train else None
+        h = self.ln2(x, s2)
+        return grad_tap(x, s2) + self.mlp(h)
 
 
 class VisionTransformer(nn.Module):

@@ -35,3 +35,26 @@ def test_layernorm_fwd_bwd(dtype, pdtype, shape):
     gtol = (2e-2 if pdtype == torch.bfloat16 else 1e-3) * rows ** 0.5
     torch.testing.assert_close(w.grad.float(), wr.grad, atol=gtol, rtol=2e-2)
     torch.testing.assert_close(b.grad.float(), br.grad, atol=gtol, rtol=2e-2)
+
+
+def test_vit_block_residual_grad_fused_into_layernorm():
+    """Pre-LN block: each LayerNorm's backward absorbs the residual branch's gradient
+    (GradSlot); x.grad must match the plain composition of the same modules."""
+    import copy
+    from distributed_model_parallel_amd.models.vit import EncoderBlock
+    torch.manual_seed(0)
+    blk = EncoderBlock(768, 12, 3072).cuda().bfloat16().train()
+    ref = copy.deepcopy(blk)
+    x = torch.randn(4, 197, 768, device="cuda").bfloat16()
+    xa, xb = x.detach().requires_grad_(), x.detach().requires_grad_()
+    n0 = _STATS["fused_residual_grad"]
+    ya = blk(xa)
+    h = xb + ref.attn(ref.ln1(xb))
+    yb = h + ref.mlp(ref.ln2(h))
+    torch.testing.assert_close(ya.float(), yb.float(), atol=2e-2, rtol=2e-2)
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    assert _STATS["fused_residual_grad"] == n0 + 2
+    err = (xa.grad.float() - xb.grad.float()).norm() / xb.grad.float().norm()
+    assert err < 2e-2, err
