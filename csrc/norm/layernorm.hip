@@ -306,7 +306,7 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
   auto dwb = at::empty({2, D}, x.options().dtype(param_dtype));
   if (rows == 0) return {dx, dwb[0].zero_(), dwb[1].zero_()};
   auto stream = at::hip::getCurrentHIPStream();
-  const int nb = ln_blocks(rows, 512);  // partial rows for dgamma/dbeta
+  const int nb = ln_blocks(rows, 256);  // one block per CU: partial rows for dgamma/dbeta
   auto part = at::empty({nb, 2 * D}, x.options().dtype(at::kFloat));
   const bool pbf = hw && w->scalar_type() == at::kBFloat16;
 #define DMP_LN_BWD(T, P)                                                                        \
