@@ -43,6 +43,13 @@ def _unrows(y2: torch.Tensor, n: int, h: int, w: int) -> torch.Tensor:
     return y2.view(n, h, w, -1).permute(0, 3, 1, 2)
 
 
+def _blaslt_dgrad(m: int, cin: int, cout: int) -> bool:
+    """Plain data gradients (no fused epilogue) where hipBLASLt measured faster than
+    our NT kernel on MI355X (tools/microbench.py --wgrad, profiles/conv1x1_backends.md):
+    reduction depth (cout) >= 1024 over <= 64K rows -- ResNet-50 layer3/4 conv3."""
+    return cout >= 1024 and m <= 65536
+
+
 def _geom(stride: int, hi: int, wi: int):
     """Row map [s, Ho, Wo, Hi, Wi] the kernels use to address a stride-s grid in place."""
     if stride == 1:
@@ -91,6 +98,8 @@ class _Conv1x1Fn(torch.autograd.Function):
                 _STATS["fused_dgrad"] += 1
                 extra = _rows(extra.to(x.dtype).contiguous(memory_format=torch.channels_last))
                 dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), mode="add", residual=extra)
+            elif not ctx.geom and _blaslt_dgrad(dy2.shape[0], cin, cout):
+                dx2 = dy2 @ w2  # deep-K / short-M: hipBLASLt's stream-K tiles win here
             else:
                 dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), c_map=ctx.geom)
             dx = _unrows(dx2, n, h, w)

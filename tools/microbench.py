@@ -63,7 +63,7 @@ def main():
         print(f"{k:45s} {v:10.3f}")
 
 
-if __name__ == "__main__" and "--gemm" not in sys.argv and "--conv" not in sys.argv:
+if __name__ == "__main__" and not {"--gemm", "--conv", "--wgrad"} & set(sys.argv):
     main()
 
 
@@ -122,3 +122,32 @@ if __name__ == "__main__" and "--gemm" in sys.argv:
     gemm_bench()
 if __name__ == "__main__" and "--conv" in sys.argv:
     conv_bench()
+
+
+def wgrad_bench():
+    """1x1-conv weight / data gradients: our TN / NT kernels vs hipBLASLt (torch.mm)
+    at every ResNet-50 bs256 1x1 shape -- the data behind ops/conv1x1.py's
+    per-shape backend choice."""
+    from distributed_model_parallel_amd import _native
+    C = _native.require("wgrad bench")
+    dev, dt = "cuda", torch.bfloat16
+    # (M, Cin, Cout) of every distinct 1x1 conv in ResNet-50 at batch 256
+    convs = [(802816, 64, 64), (802816, 64, 256), (802816, 256, 64), (200704, 256, 128),
+             (200704, 128, 512), (200704, 512, 128), (50176, 512, 256), (50176, 256, 1024),
+             (50176, 1024, 256), (12544, 1024, 512), (12544, 512, 2048), (12544, 2048, 512),
+             (200704, 256, 512), (50176, 512, 1024), (12544, 1024, 2048)]
+    print(f"{'M':>7} {'Cin':>5} {'Cout':>5} | {'wgrad ours':>10} {'blaslt':>8} | {'dgrad ours':>10} {'blaslt':>8} ms")
+    for M, cin, cout in convs:
+        x = torch.randn(M, cin, device=dev, dtype=dt)
+        dy = torch.randn(M, cout, device=dev, dtype=dt)
+        w = torch.randn(cout, cin, device=dev, dtype=dt)
+        wt = w.t().contiguous()
+        t_w = timeit(lambda: C.gemm_tn(dy, x, dt))
+        t_wb = timeit(lambda: dy.t() @ x)
+        t_d = timeit(lambda: C.gemm_nt(dy, wt))
+        t_db = timeit(lambda: dy @ w)
+        print(f"{M:7d} {cin:5d} {cout:5d} | {t_w:10.3f} {t_wb:8.3f} | {t_d:10.3f} {t_db:8.3f}")
+
+
+if __name__ == "__main__" and "--wgrad" in sys.argv:
+    wgrad_bench()
