@@ -94,8 +94,13 @@ struct NtArgs {
   ConvMap cv;                   // implicit-GEMM conv geometry (CONV)
 };
 
+// NT = WAVES_M*WAVES_N*64 threads: 4 waves (2 blocks/CU) or 8 waves (256-row
+// tiles, 1 block/CU: 1.36x the FLOPs per staged byte of 128x128, for the
+// L2-bandwidth-bound deep-K shapes).
 template <int BM, int BN, int WAVES_M, int WAVES_N, bool PRO_BN, int EPI, bool CONV, int NSTAGE>
-__global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
+__global__ __launch_bounds__(WAVES_M * WAVES_N * 64, (WAVES_M * WAVES_N == 8 ? 1 : 2))
+void gemm_nt_kernel(const NtArgs p) {
+  constexpr int kThreads = WAVES_M * WAVES_N * 64;
   const bf16* __restrict__ A = p.A;
   const bf16* __restrict__ B = p.B;
   bf16* __restrict__ C = p.C;
@@ -370,15 +375,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(const NtArgs p) {
 template <int BM, int BN, int WM, int WN, bool PRO, int EPI, bool CONV>
 void launch(const NtArgs& a, hipStream_t stream) {
   const int mtiles = (a.M + BM - 1) / BM, ntiles = (a.N + BN - 1) / BN;
+  constexpr int threads = WM * WN * 64;
   if constexpr (!CONV) {
     if (a.K <= BK) {
       hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI, CONV, 1>), dim3(mtiles * ntiles),
-                         dim3(kThreads), 0, stream, a);
+                         dim3(threads), 0, stream, a);
       return;
     }
   }
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, WM, WN, PRO, EPI, CONV, 2>), dim3(mtiles * ntiles),
-                     dim3(kThreads), 0, stream, a);
+                     dim3(threads), 0, stream, a);
 }
 
 // Tile override for experiments (set_gemm_tile; -1 = automatic).
@@ -394,6 +400,7 @@ void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {
     case 3: launch<128, 64, 4, 1, PRO, EPI, CONV>(a, s); break;
     case 4: launch<64, 128, 2, 2, PRO, EPI, CONV>(a, s); break;
     case 5: launch<64, 64, 2, 2, PRO, EPI, CONV>(a, s); break;
+    case 6: launch<256, 128, 4, 2, PRO, EPI, CONV>(a, s); break;
     default: launch<128, 128, 2, 2, PRO, EPI, CONV>(a, s); break;
   }
 }
@@ -405,6 +412,7 @@ int tile_bm(int N, int bm) {
   switch (t) {
     case 0: return 256;
     case 4: case 5: return 64;
+    case 6: return 256;
     default: return 128;
   }
 }

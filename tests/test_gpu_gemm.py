@@ -80,3 +80,24 @@ def test_gemm_affine_epilogue(res):
     if res:
         ref = ref + r.float()
     torch.testing.assert_close(c.float(), torch.relu(ref), atol=0.05 * K ** 0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("mode", ["store", "moments"])
+def test_gemm_tile_variants(tile, mode):
+    """Every NT tile variant (set_gemm_tile) against fp32, incl. the 8-wave 256x128 one."""
+    c = C()
+    torch.manual_seed(tile)
+    M, N, K = 1000, 192, 320
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    c.set_gemm_tile(tile)
+    try:
+        y, mom = c.gemm_nt(a, b, mode=mode)
+    finally:
+        c.set_gemm_tile(-1)
+    ref = a.float() @ b.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=0.05 * K ** 0.5, rtol=2e-2)
+    if mode == "moments":
+        yf = y.float()
+        torch.testing.assert_close(mom[:N].float(), yf.sum(0), atol=1e-2 * M ** 0.5, rtol=1e-3)
