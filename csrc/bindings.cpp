@@ -68,6 +68,11 @@ void set_gemm_tile(int64_t t);
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
                       at::ScalarType out_dtype);
+// gemm_xl.hip
+at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
+                   const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
+                   const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out);
+void set_gemm_xl_bn(int bn, int pipe, int group_m);
 // depthwise.hip
 std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                           bool moments);
@@ -143,6 +148,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("relu") = false);
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"));
+
+  // ---- large-tile transformer GEMM with fused bias / GELU / residual epilogues ----
+  m.def("gemm_xl", &dmp::gemm_xl, py::arg("A"), py::arg("B"), py::arg("mode") = "store",
+        py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("residual") = py::none(), py::arg("out") = py::none());
+  m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 1, py::arg("group_m") = 0,
+        "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
 
   // ---- LayerNorm (last dim) ----
   m.def("layernorm_forward", &dmp::layernorm_forward);

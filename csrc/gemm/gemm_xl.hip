@@ -1,0 +1,722 @@
+// Large-tile MFMA bf16 GEMM for the transformer linears (ViT-B/16 qkv / proj /
+// fc1 / fc2 in forward and data-gradient form), with fused epilogues.
+//
+//   C[M, N] = epi( A[M, K] * B[N, K]^T )        (both operands K-contiguous)
+//
+// Forward of nn.Linear: A = x [T, in], B = W [out, in].  Data gradient:
+// A = dy [T, out], B = W^T [in, out] (a 4.7 MB transposed copy of W per step).
+//
+// Epilogues (what hipBLASLt + separate torch kernels would do in 2-3 passes):
+//   XL_STORE     C = bf16(acc)
+//   XL_BIAS      C = bf16(acc + b[n])
+//   XL_BIAS_GELU Aux = bf16(acc + b[n]);  C = bf16(gelu(Aux))     (fc1 forward)
+//   XL_DGELU     C = bf16(bf16(acc) * gelu'(Aux))                  (fc2 dgrad ->
+//                the gradient at fc1's pre-activation: no GELU-backward pass)
+//   XL_BIAS_RES  C = bf16(bf16(acc + b[n]) + R)                    (proj / fc2
+//                forward + residual add)
+// Rounding points match the unfused torch sequence (addmm -> bf16 -> gelu).
+//
+// Structure (cdna_hip_programming.md §5 "256² template" and T1-T5):
+//   * 256 x BN tile (BN = 256 or 128), BK = 64, 512 threads = 8 waves as
+//     2 (M) x 4 (N); each wave owns 128 x BN/4 outputs = 8 x BN/64 16x16
+//     accumulators (v_mfma_f32_16x16x32_bf16);
+//   * operands staged global -> LDS by global_load_lds_dwordx4 (no VGPR
+//     round trip); the LDS image is lane-linear, so the bank swizzle is applied
+//     to the per-lane SOURCE address and undone on the ds_read (rule 21);
+//   * every K tile is split into two k32 halves living in their own LDS
+//     regions ([A|B] x [k0|k1] x 2 buffers = 128 KB at BN = 256); one K tile is
+//     4 phases (k-half x M-half of the wave tile, 16 / 8 MFMAs each), and each
+//     phase issues the global->LDS copy of one region as soon as that region's
+//     previous contents were consumed: the k0 halves of tile t+2 are issued
+//     while tile t computes its k1 half, so ~5 phases of loads stay in flight
+//     across the barriers (counted s_waitcnt vmcnt, raw s_barrier -- never
+//     __syncthreads, whose fence would drain the DMA queue);
+//   * one raw s_barrier per phase; the region written in phase p was last read
+//     before the previous phase's barrier (WAR), and a region is read one phase
+//     after the vmcnt that retired it (RAW);
+//   * bijective XCD-aware block remap (T1); the N tiles of an M tile are
+//     adjacent (they share the A panel in L2);
+//   * epilogue restages the tile through LDS for 16-B row-contiguous stores.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "../common.h"
+
+namespace dmp {
+namespace {
+
+using bf16 = __bf16;
+constexpr int XBM = 256, XBK = 64, XTHREADS = 512;
+
+enum XlEpi { XL_STORE = 0, XL_BIAS = 1, XL_BIAS_GELU = 2, XL_DGELU = 3, XL_BIAS_RES = 4 };
+
+using gptr_t = const __attribute__((address_space(1))) void*;
+using lptr_t = __attribute__((address_space(3))) void*;
+
+__device__ __forceinline__ void glds16(const void* g, char* l) {
+  __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)l, 16, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// 16-B chunk swizzle of a k32 region (rows of 64 B = 4 chunks, 4 rows per
+// 256-B bank row).  ds_read_b128 is serviced in four 16-lane groups
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} and their +32 images
+// (MI355X_MICROARCH.md §LDS); an MFMA fragment read has lane l on row l & 15,
+// chunk l >> 4, so each group holds rows {0-3,12-15} of one chunk and rows
+// 4-11 of the neighbouring chunk.  XOR-ing the chunk with g(row >> 2) for
+// g = {0, 2, 3, 1} gives every group 16 distinct bank slots (a plain
+// XOR with row >> 2 leaves 2-way conflicts: rows 0-3 and 4-7 collide).
+__device__ __forceinline__ int chunk_xor(int q) { return (0x78 >> (2 * (q & 3))) & 3; }
+
+// Tile order: bijective XCD remap (consecutive logical ids share an XCD and
+// run concurrently), then groups of GM M-tiles walked column by column, so
+// the ~32 tiles resident on one XCD form a GM x 32/GM patch whose A and B
+// panels are both reused from that XCD's L2.
+__device__ __forceinline__ void tile_coords(int nblocks, int mtiles, int ntiles, int gm_max,
+                                            int& mt, int& nt) {
+  const int bid = xcd_remap(blockIdx.x, nblocks);
+  const int per_group = gm_max * ntiles;
+  const int g = bid / per_group, r = bid - g * per_group;
+  const int gm = min(gm_max, mtiles - g * gm_max);
+  mt = g * gm_max + r % gm;
+  nt = r / gm;
+}
+
+template <int N>
+__device__ __forceinline__ void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+struct XlArgs {
+  const bf16* A; int64_t lda;
+  const bf16* B; int64_t ldb;
+  bf16* C; int64_t ldc;
+  int M, N, K;
+  const bf16* bias;             // [N] (XL_BIAS*)
+  bf16* aux; int64_t ldaux;     // XL_BIAS_GELU: pre-activation out; XL_DGELU: pre-activation in
+  const bf16* R; int64_t ldr;   // XL_BIAS_RES residual
+  int group_m;                  // tile-order group height (M tiles)
+};
+
+template <int BN, int EPI, int PIPE>
+__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p) {
+  constexpr int WTM = 128, WTN = BN / 4;
+  constexpr int MI = WTM / 16, NI = WTN / 16;       // 8 x (4 | 2) accumulators
+  constexpr int RA = XBM * 64, RB = BN * 64;        // bytes of one k32 region
+  constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;  // glds per wave per region
+  constexpr int STAGE_LDS = 4 * RA + 4 * RB;
+  constexpr int CT_STRIDE = BN + 8;
+  constexpr int EPI_LDS = XBM * CT_STRIDE * 2;
+  constexpr int LDS = STAGE_LDS > EPI_LDS ? STAGE_LDS : EPI_LDS;
+  constexpr int W2 = 2 * (NA + NB);  // glds per wave per K tile
+  static_assert(NA >= 1 && NB >= 1, "region smaller than one glds round");
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+
+  const bf16* __restrict__ A = p.A;
+  const bf16* __restrict__ B = p.B;
+  const int64_t lda = p.lda, ldb = p.ldb;
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + BN - 1) / BN;
+  int mt, nt;
+  tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
+  const int m0 = mt * XBM, n0 = nt * BN;
+  const int ktiles = K / XBK;
+
+  // ---- staging: lane L of a 1 KB glds instruction writes LDS bytes L*16..+16
+  // of 16 rows x 64 B; the logical 16-B chunk it carries is the physical one
+  // XOR swz(row) (row & 15 = L >> 2, so the XOR depends on L >> 4 only).
+  const int srow = lane >> 2;
+  const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
+  const bf16* asrc[NA];
+  const bf16* bsrc[NB];
+#pragma unroll
+  for (int q = 0; q < NA; ++q) {
+    const int r = (wave * NA + q) * 16 + srow;
+    asrc[q] = A + (int64_t)min(m0 + r, M - 1) * lda + schunk * 8;
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int r = (wave * NB + q) * 16 + srow;
+    bsrc[q] = B + (int64_t)min(n0 + r, N - 1) * ldb + schunk * 8;
+  }
+  auto a_region = [&](int ks, int buf) { return smem + (buf * 2 + ks) * RA; };
+  auto b_region = [&](int ks, int buf) { return smem + 4 * RA + (buf * 2 + ks) * RB; };
+  auto stage_a = [&](int ks, int kt, int buf) {
+    char* dst = a_region(ks, buf) + wave * NA * 1024;
+    const int koff = kt * XBK + ks * 32;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) glds16(asrc[q] + koff, dst + q * 1024);
+  };
+  auto stage_b = [&](int ks, int kt, int buf) {
+    char* dst = b_region(ks, buf) + wave * NB * 1024;
+    const int koff = kt * XBK + ks * 32;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) glds16(bsrc[q] + koff, dst + q * 1024);
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lrow = lane & 15, lk = lane >> 4;
+  // fragment byte offset of row r (multiple of 16 + lrow) in a k32 region
+  const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
+  bf16x8 fb[NI];
+
+  auto phase = [&](int ks, int mh, int buf) {
+    const char* ar = a_region(ks, buf) + (wr * WTM + mh * 64) * 64 + frag_off;
+    bf16x8 fa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
+    if (mh == 0) {
+      const char* br = b_region(ks, buf) + (wc * WTN) * 64 + frag_off;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[mh * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if constexpr (PIPE == 0) {
+  // ---- prologue: tile 0 (both halves) and tile 1's k0 half in flight ----
+  stage_a(0, 0, 0);
+  stage_b(0, 0, 0);
+  stage_a(1, 0, 0);
+  stage_b(1, 0, 0);
+  if (ktiles > 1) {
+    stage_a(0, 1, 1);
+    stage_b(0, 1, 1);
+    vmcnt<W2>();
+  } else {
+    vmcnt<NA + NB>();
+  }
+  barrier();
+
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
+    // phase 0: k0 half, M half 0; stage tile kt+1's A k1 half
+    if (has1) stage_a(1, kt + 1, buf ^ 1);
+    phase(0, 0, buf);
+    barrier();
+    // phase 1: k0, M half 1; stage tile kt+1's B k1; retire tile kt's k1 half
+    if (has1) stage_b(1, kt + 1, buf ^ 1);
+    phase(0, 1, buf);
+    if (has1) vmcnt<W2>(); else vmcnt<0>();
+    barrier();
+    // phase 2: k1, M half 0; this tile's k0 regions are free: stage tile kt+2's A k0
+    if (has2) stage_a(0, kt + 2, buf);
+    phase(1, 0, buf);
+    barrier();
+    // phase 3: k1, M half 1; stage kt+2's B k0; retire tile kt+1's k0 half
+    if (has2) stage_b(0, kt + 2, buf);
+    phase(1, 1, buf);
+    if (has2) vmcnt<W2>(); else if (has1) vmcnt<NA + NB>(); else vmcnt<0>();
+    barrier();
+  }
+  } else {
+  // ---- PIPE 1: half-step ring.  Half-step s (K tile s/2, k32 half s%2) lives
+  // in LDS region s%4.  During half-step s: stage region s%4 with the data of
+  // half-step s+4 (its fragments were read in s-1 and retired before that
+  // step's barrier), ds_read the fragments of s+1 into the other register set
+  // (retired by the vmcnt at the end of s-1), run the 32 MFMAs of s.  One
+  // barrier per half-step; three half-steps of copies in flight.
+  const int S = 2 * ktiles;
+  auto stage_h = [&](int h) {
+    stage_a(h & 1, h >> 1, (h >> 1) & 1);
+    stage_b(h & 1, h >> 1, (h >> 1) & 1);
+  };
+  bf16x8 xa[MI], xb[NI], ya[MI], yb[NI];
+  auto read_frags = [&](bf16x8 (&fa)[MI], bf16x8 (&fbb)[NI], int h) {
+    const char* ar = smem + (h & 3) * RA + (wr * WTM) * 64 + frag_off;
+    const char* br = smem + 4 * RA + (h & 3) * RB + (wc * WTN) * 64 + frag_off;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) fbb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fbb)[NI]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  // prologue: half-steps 0..3 in flight; retire 0, read it, retire 1
+  stage_h(0);
+  stage_h(1);
+  if (S >= 4) {
+    stage_h(2);
+    stage_h(3);
+    vmcnt<3 * (NA + NB)>();
+  } else {
+    vmcnt<NA + NB>();
+  }
+  barrier();
+  read_frags(xa, xb, 0);
+  if (S >= 4) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+  lgkm0();
+  barrier();
+  // PIPE 2..4 are timing-only ablations (wrong results): 2 = no copies in the
+  // loop, 3 = no fragment reads in the loop, 4 = MFMAs only
+  constexpr bool kStage = PIPE != 2 && PIPE != 4, kRead = PIPE != 3 && PIPE != 4;  // 5: no epilogue
+  if constexpr (!kRead) read_frags(ya, yb, 1);
+  for (int s = 0; s < S; s += 2) {
+    if (kStage && s + 4 < S) stage_h(s + 4);
+    if (kRead) read_frags(ya, yb, s + 1);
+    mfmas(xa, xb);
+    if (s + 4 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+    lgkm0();
+    barrier();
+    if (kStage && s + 5 < S) stage_h(s + 5);
+    if (kRead && s + 2 < S) read_frags(xa, xb, s + 2);
+    mfmas(ya, yb);
+    if (s + 5 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+    lgkm0();
+    barrier();
+  }
+  }
+
+  // ---- epilogue: (acc [+ bias]) -> bf16 tile in LDS, then row-contiguous pass ----
+  if constexpr (PIPE == 5) {  // timing-only ablation: no epilogue (acc kept live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 12345.678f) p.C[tid] = (bf16)t;
+    return;
+  }
+  bf16* ct = reinterpret_cast<bf16*>(smem);
+  float bv[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int col = n0 + wc * WTN + j * 16 + (lane & 15);
+    bv[j] = 0.f;
+    if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES)
+      bv[j] = col < N ? (float)p.bias[col] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = wc * WTN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wr * WTM + i * 16 + (lane >> 4) * 4 + e;
+        ct[row * CT_STRIDE + col] = (bf16)(acc[i][j][e] + bv[j]);
+      }
+    }
+  __syncthreads();
+  constexpr int CV = BN / 8, RPP = XTHREADS / CV;
+  const int cvi = tid % CV, rr0 = tid / CV;
+  const int col = n0 + cvi * 8;
+  if (col < N) {
+#pragma unroll 4
+    for (int pr = 0; pr < XBM / RPP; ++pr) {
+      const int lr = rr0 + pr * RPP;
+      const int row = m0 + lr;
+      if (row >= M) break;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
+      if constexpr (EPI == XL_BIAS_GELU) {
+        *reinterpret_cast<bf16x8*>(p.aux + (int64_t)row * p.ldaux + col) = v;
+        f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+        v = __builtin_convertvector(f, bf16x8);
+      } else if constexpr (EPI == XL_DGELU) {
+        f32x8 f = __builtin_convertvector(v, f32x8);
+        const f32x8 x = __builtin_convertvector(
+            *reinterpret_cast<const bf16x8*>(p.aux + (int64_t)row * p.ldaux + col), f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
+        v = __builtin_convertvector(f, bf16x8);
+      } else if constexpr (EPI == XL_BIAS_RES) {
+        f32x8 f = __builtin_convertvector(v, f32x8);
+        const f32x8 r = __builtin_convertvector(
+            *reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+        f += r;
+        v = __builtin_convertvector(f, bf16x8);
+      }
+      *reinterpret_cast<bf16x8*>(p.C + (int64_t)row * p.ldc + col) = v;
+    }
+  }
+}
+
+// Epilogue transform of one 8-column bf16 vector of row `row` (already holding
+// bf16(acc [+ bias])); writes the side output of XL_BIAS_GELU.
+template <int EPI>
+__device__ __forceinline__ bf16x8 epi_vec(bf16x8 v, int64_t row, int col, const XlArgs& p) {
+  if constexpr (EPI == XL_BIAS_GELU) {
+    *reinterpret_cast<bf16x8*>(p.aux + row * p.ldaux + col) = v;
+    f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+    return __builtin_convertvector(f, bf16x8);
+  } else if constexpr (EPI == XL_DGELU) {
+    f32x8 f = __builtin_convertvector(v, f32x8);
+    const f32x8 x = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.aux + row * p.ldaux + col), f32x8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
+    return __builtin_convertvector(f, bf16x8);
+  } else if constexpr (EPI == XL_BIAS_RES) {
+    f32x8 f = __builtin_convertvector(v, f32x8);
+    f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + row * p.ldr + col), f32x8);
+    return __builtin_convertvector(f, bf16x8);
+  } else {
+    return v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent form: one 512-thread block per CU walks the tiles
+// L = i * gridDim.x + pos(block) (pos = XCD-aware, so each round's tiles on one
+// XCD are 32 consecutive ids of the grouped order).  The half-step ring runs
+// straight across tile boundaries -- the next tile's first K tiles are in
+// flight while the current tile finishes and stores -- which removes the
+// per-tile pipeline fill and the synchronized all-CU prologue burst that
+// dominate short-K (K = 768) transformer GEMMs.  The epilogue cannot use the
+// ring's LDS (it holds the next tile's operands), so each wave stores its
+// 128 x WTN sub-tile through a private 16-row LDS scratch.  It runs at the
+// start of the next tile's first half-step, BEFORE that step's copies: the
+// half-step's closing vmcnt then still retires everything it must (all ops
+// older than the 2 x (NA+NB) youngest are complete), only more conservatively.
+// ---------------------------------------------------------------------------
+template <int BN, int EPI>
+__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_persistent_kernel(const XlArgs p) {
+  constexpr int WTM = 128, WTN = BN / 4;
+  constexpr int MI = WTM / 16, NI = WTN / 16;
+  constexpr int RA = XBM * 64, RB = BN * 64;
+  constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;
+  constexpr int RING = 4 * RA + 4 * RB;
+  constexpr int SCR_STRIDE = WTN + 8;                 // bf16 elements per scratch row
+  constexpr int SCR_WAVE = 16 * SCR_STRIDE * 2;       // bytes per wave
+  __shared__ __attribute__((aligned(16))) char smem[RING + 8 * SCR_WAVE];
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + BN - 1) / BN;
+  const int total = mtiles * ntiles;
+  const int G = gridDim.x;
+  const int pos = xcd_remap(blockIdx.x, G);
+  const int my_tiles = pos < total ? (total - pos + G - 1) / G : 0;
+  const int ktiles = K / XBK;
+  const int HS = 2 * ktiles;                // half-steps per tile
+  const int S = my_tiles * HS;
+  if (S == 0) return;
+
+  auto coords = [&](int ti, int& m0, int& n0) {
+    const int L = ti * G + pos;
+    const int per_group = p.group_m * ntiles;
+    const int g = L / per_group, r = L - g * per_group;
+    const int gm = min(p.group_m, mtiles - g * p.group_m);
+    m0 = (g * p.group_m + r % gm) * XBM;
+    n0 = (r / gm) * BN;
+  };
+
+  const int srow = lane >> 2;
+  const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
+  // staging cursor: tile of the most recent stage call (advanced monotonically)
+  int st_tile = -1, st_m0 = 0, st_n0 = 0;
+  auto stage_h = [&](int h) {
+    const int ti = h / HS, rem = h - ti * HS;
+    if (ti != st_tile) { st_tile = ti; coords(ti, st_m0, st_n0); }
+    const int koff = (rem >> 1) * XBK + (rem & 1) * 32 + schunk * 8;
+    char* da = smem + (h & 3) * RA + wave * NA * 1024;
+    char* db = smem + 4 * RA + (h & 3) * RB + wave * NB * 1024;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int r = min(st_m0 + (wave * NA + q) * 16 + srow, M - 1);
+      glds16(p.A + (int64_t)r * p.lda + koff, da + q * 1024);
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int r = min(st_n0 + (wave * NB + q) * 16 + srow, N - 1);
+      glds16(p.B + (int64_t)r * p.ldb + koff, db + q * 1024);
+    }
+  };
+
+  const int lrow = lane & 15, lk = lane >> 4;
+  const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
+  f32x4 acc[MI][NI];
+  bf16x8 xa[MI], xb[NI], ya[MI], yb[NI];
+  auto zero_acc = [&] {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto read_frags = [&](bf16x8 (&fa)[MI], bf16x8 (&fbb)[NI], int h) {
+    const char* ar = smem + (h & 3) * RA + (wr * WTM) * 64 + frag_off;
+    const char* br = smem + 4 * RA + (h & 3) * RB + (wc * WTN) * 64 + frag_off;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) fbb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fbb)[NI]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  bf16* scr = reinterpret_cast<bf16*>(smem + RING + wave * SCR_WAVE);
+  auto epilogue = [&](int ti) {
+    int m0, n0;
+    coords(ti, m0, n0);
+    float bv[NI];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = n0 + wc * WTN + j * 16 + (lane & 15);
+      bv[j] = 0.f;
+      if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES)
+        bv[j] = col < N ? (float)p.bias[col] : 0.f;
+    }
+    constexpr int VPR = WTN / 8;          // 16-B vectors per scratch row
+    constexpr int VPL = 16 * VPR / 64;    // vectors per lane per 16-row block
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          scr[((lane >> 4) * 4 + e) * SCR_STRIDE + j * 16 + (lane & 15)] = (bf16)(acc[i][j][e] + bv[j]);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const int idx = lane + v * 64, r = idx / VPR, cv = idx % VPR;
+        bf16x8 val = *reinterpret_cast<const bf16x8*>(scr + r * SCR_STRIDE + cv * 8);
+        const int64_t row = m0 + wr * WTM + i * 16 + r;
+        const int col = n0 + wc * WTN + cv * 8;
+        if (row < M && col < N) {
+          val = epi_vec<EPI>(val, row, col, p);
+          *reinterpret_cast<bf16x8*>(p.C + row * p.ldc + col) = val;
+        }
+      }
+    }
+  };
+
+  zero_acc();
+  // prologue: half-steps 0..3 in flight; retire 0, read it, retire 1
+  stage_h(0);
+  stage_h(1);
+  if (S >= 4) {
+    stage_h(2);
+    stage_h(3);
+    vmcnt<3 * (NA + NB)>();
+  } else {
+    vmcnt<NA + NB>();
+  }
+  barrier();
+  read_frags(xa, xb, 0);
+  if (S >= 4) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  barrier();
+  int tile_left = HS;  // half-steps left in the current tile
+  int cur_tile = 0;
+  // After an interior tile's epilogue (issued right after the step's copies),
+  // the next three half-step closings may leave its MI*VPL C stores in flight:
+  // every op younger than the copies being retired still includes them.
+  constexpr int W = 2 * (NA + NB), E = MI * ((16 * WTN / 8) / 64);
+  int credit = 0;
+  auto close_step = [&](bool more) {
+    if (!more) vmcnt<0>();
+    else if (credit > 0) vmcnt<W + E>();
+    else vmcnt<W>();
+    credit = credit > 0 ? credit - 1 : 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier();
+  };
+  for (int s = 0; s < S; s += 2) {
+    if (s + 4 < S) stage_h(s + 4);
+    if (tile_left == 0) {  // previous tile done: store it, start the next
+      int m0, n0;
+      coords(cur_tile, m0, n0);
+      epilogue(cur_tile);
+      credit = (m0 + XBM <= M && n0 + BN <= N) ? 3 : 0;
+      zero_acc();
+      ++cur_tile;
+      tile_left = HS;
+    }
+    read_frags(ya, yb, s + 1);
+    mfmas(xa, xb);
+    close_step(s + 4 < S);
+    if (s + 5 < S) stage_h(s + 5);
+    if (s + 2 < S) read_frags(xa, xb, s + 2);
+    mfmas(ya, yb);
+    close_step(s + 5 < S);
+    tile_left -= 2;
+  }
+  epilogue(cur_tile);
+}
+
+int g_num_cus = 0;
+
+int g_xl_pipe = 1;
+
+template <int BN, int EPI>
+void launch_xl(const XlArgs& a, hipStream_t s) {
+  const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + BN - 1) / BN);
+  if constexpr (EPI == XL_STORE) {
+    switch (g_xl_pipe) {  // timing-only ablations of the ring pipeline
+      case 2: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 2>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
+      case 3: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 3>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
+      case 4: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 4>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
+      case 5: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 5>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
+      default: break;
+    }
+  }
+  if (g_xl_pipe == 6) {
+    if (g_num_cus == 0) {
+      int dev = 0;
+      DMP_HIP_CHECK(hipGetDevice(&dev));
+      DMP_HIP_CHECK(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int grid = std::min(blocks, g_num_cus);
+    hipLaunchKernelGGL((gemm_xl_persistent_kernel<BN, EPI>), dim3(grid), dim3(XTHREADS), 0, s, a);
+    return;
+  }
+  if (g_xl_pipe == 0)
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 0>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+}
+
+template <int EPI>
+void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
+  if (bn == 128) launch_xl<128, EPI>(a, s);
+  else launch_xl<256, EPI>(a, s);
+}
+
+int g_xl_bn_override = 0;
+int g_xl_group_m = 0;
+
+// BN choice: 256-wide tiles unless that leaves the last round of a 1-block/CU
+// grid mostly empty (N = 768: 3 column tiles -> 128-wide gives 2x the blocks).
+int pick_bn(int M, int N) {
+  if (g_xl_bn_override) return g_xl_bn_override;
+  const int cus = 256;
+  auto eff = [&](int bn) {
+    const double blocks = (double)((M + XBM - 1) / XBM) * ((N + bn - 1) / bn);
+    const double rounds = std::ceil(blocks / cus);
+    // useful work / (rounds x tile work), with the smaller tile paying ~12%
+    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : 0.88);
+  };
+  return eff(128) > eff(256) ? 128 : 256;
+}
+
+void check_bf16_2d(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2, name,
+              " must be a 2-D bf16 GPU tensor");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0, name, " rows must be contiguous and 16-B aligned");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-B aligned");
+}
+
+}  // namespace
+
+// C = epi(A @ B^T).  mode: "store" | "bias" | "bias_gelu" | "dgelu" | "bias_res".
+// Returns C ("bias_gelu": also fills aux with the pre-activation).
+at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
+                   const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
+                   const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out) {
+  check_bf16_2d(A, "A");
+  check_bf16_2d(B, "B");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "gemm_xl: A/B K mismatch");
+  TORCH_CHECK(K % XBK == 0 && K >= XBK, "gemm_xl: K must be a positive multiple of 64");
+  TORCH_CHECK(N % 8 == 0, "gemm_xl: N must be a multiple of 8");
+  TORCH_CHECK(M > 0 && M < (1LL << 31) && N < (1LL << 31), "gemm_xl: size out of range");
+  TORCH_CHECK(A.device() == B.device(), "gemm_xl: device mismatch");
+  int epi;
+  if (mode == "store") epi = XL_STORE;
+  else if (mode == "bias") epi = XL_BIAS;
+  else if (mode == "bias_gelu") epi = XL_BIAS_GELU;
+  else if (mode == "dgelu") epi = XL_DGELU;
+  else if (mode == "bias_res") epi = XL_BIAS_RES;
+  else TORCH_CHECK(false, "gemm_xl: unknown mode ", mode);
+  at::Tensor C;
+  if (out) {
+    C = *out;
+    check_bf16_2d(C, "out");
+    TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm_xl: out shape");
+  } else {
+    C = at::empty({M, N}, A.options());
+  }
+  XlArgs a{};
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr());
+  a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr());
+  a.ldb = B.stride(0);
+  a.C = reinterpret_cast<bf16*>(C.data_ptr());
+  a.ldc = C.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  if (epi == XL_BIAS || epi == XL_BIAS_GELU || epi == XL_BIAS_RES) {
+    TORCH_CHECK(bias && bias->scalar_type() == at::kBFloat16 && bias->numel() == N && bias->is_contiguous(),
+                "gemm_xl: bias must be a contiguous bf16 [N]");
+    a.bias = reinterpret_cast<const bf16*>(bias->data_ptr());
+  }
+  if (epi == XL_BIAS_GELU || epi == XL_DGELU) {
+    TORCH_CHECK(aux.has_value(), "gemm_xl: mode needs aux");
+    check_bf16_2d(*aux, "aux");
+    TORCH_CHECK(aux->size(0) == M && aux->size(1) == N, "gemm_xl: aux shape");
+    a.aux = reinterpret_cast<bf16*>(aux->data_ptr());
+    a.ldaux = aux->stride(0);
+  }
+  if (epi == XL_BIAS_RES) {
+    TORCH_CHECK(residual.has_value(), "gemm_xl: bias_res needs residual");
+    check_bf16_2d(*residual, "residual");
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_xl: residual shape");
+    a.R = reinterpret_cast<const bf16*>(residual->data_ptr());
+    a.ldr = residual->stride(0);
+  }
+  const int bn = pick_bn((int)M, (int)N);
+  a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+  hipStream_t s = at::hip::getCurrentHIPStream();
+  switch (epi) {
+    case XL_STORE: dispatch_bn<XL_STORE>(a, bn, s); break;
+    case XL_BIAS: dispatch_bn<XL_BIAS>(a, bn, s); break;
+    case XL_BIAS_GELU: dispatch_bn<XL_BIAS_GELU>(a, bn, s); break;
+    case XL_DGELU: dispatch_bn<XL_DGELU>(a, bn, s); break;
+    default: dispatch_bn<XL_BIAS_RES>(a, bn, s); break;
+  }
+  DMP_HIP_CHECK(hipGetLastError());
+  return C;
+}
+
+void set_gemm_xl_bn(int bn, int pipe, int group_m) {
+  TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");
+  g_xl_group_m = group_m;
+  TORCH_CHECK(bn == 0 || bn == 128 || bn == 256, "bn must be 0 (auto), 128 or 256");
+  TORCH_CHECK(pipe >= 0 && pipe <= 6, "pipe must be 0..6 (2..5: timing-only ablations, 6: persistent)");
+  g_xl_bn_override = bn;
+  g_xl_pipe = pipe;
+}
+
+}  // namespace dmp
