@@ -38,6 +38,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_model_parallel_amd.comm.rccl import default_communicator  # noqa: E402
 from distributed_model_parallel_amd.models import INPUT_SHAPES  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
+from distributed_model_parallel_amd.utils import gemm_tuning  # noqa: E402
 from distributed_model_parallel_amd.utils.env import destroy_distributed, init_distributed  # noqa: E402
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
 
@@ -65,6 +66,10 @@ def main() -> int:
                     help="replay the whole training step as one captured hipGraph")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
+    ap.add_argument("--gemm-tuning", default=os.environ.get("DMP_GEMM_TUNING", "use"),
+                    choices=["use", "tune", "off"],
+                    help="library-GEMM solutions from profiles/tunableop/<model>_gfx950.csv "
+                         "(use), re-tune and write that file (tune), or library defaults (off)")
     args = ap.parse_args()
 
     use_gpu = None if args.device == "auto" else args.device == "cuda"
@@ -73,6 +78,7 @@ def main() -> int:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
     dev = env.device
+    tuning_file = gemm_tuning.configure(args.gemm_tuning, args.model) if dev.type == "cuda" else None
     cfg = StepConfig(model=args.model, batch_size=args.batch_size, image_size=args.image_size,
                      dtype=parse_dtype(args.dtype), channels_last=not args.no_channels_last,
                      parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
@@ -143,6 +149,8 @@ def main() -> int:
             "channels_last": not args.no_channels_last,
             "grad_comm": getattr(st.wrapped, "comm_backend", None),
             "hip_graph": args.graph,
+            "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
+            if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,
             "final_loss": round(final_loss, 4),
         },
     }
