@@ -64,6 +64,9 @@ def main() -> int:
                     help="cpu: gloo plumbing run (BASELINE config 1), fp32 recommended")
     ap.add_argument("--graph", action="store_true",
                     help="replay the whole training step as one captured hipGraph")
+    ap.add_argument("--lr", type=float, default=None,
+                    help="SGD learning rate (default 0.1 for CNNs, 0.005 for ViT: plain SGD at 0.1 "
+                         "diverges on a transformer, which would make the reported loss meaningless)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
     ap.add_argument("--gemm-tuning", default=os.environ.get("DMP_GEMM_TUNING", "use"),
@@ -83,7 +86,8 @@ def main() -> int:
                      dtype=parse_dtype(args.dtype), channels_last=not args.no_channels_last,
                      parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
                      first_bucket_mb=args.first_bucket_mb,
-                     dp_devices=args.gpus if args.parallel == "dp" else 1, graph=args.graph)
+                     dp_devices=args.gpus if args.parallel == "dp" else 1, graph=args.graph,
+                     lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1))
     if args.parallel == "dp" and env.world_size > 1:
         raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
                          "--gpus N` without torchrun")

@@ -1,0 +1,373 @@
+// Fused multi-head self-attention for ViT-sized sequences (S <= 256, head
+// dim 64) on gfx950: forward and backward, reading the packed qkv GEMM output
+// and writing the packed dqkv gradient directly.
+//
+// Why not the generic flash-attention kernels: at ViT-B/16's S = 197 the
+// sequence fits one workgroup's LDS whole, and the generic path costs
+//   * three layout copies per layer: q/k/v split + head permute before the
+//     kernel, the output transpose after it, and a concatenation of dq/dk/dv
+//     back into the qkv gradient (profiles/vit_b16_bs128_1gpu_v2.md: 2.6 ms
+//     of a 37 ms step);
+//   * flash kernels tiled for long sequences running at ~100-175 TF/s here.
+// Layout contract (torchvision ViT): qkv[t, :] of token t = b*S + s holds
+// [q | k | v], each [H, 64]; o[t, h*64 + d]; dqkv like qkv.
+//
+// One workgroup (4 waves) per (batch, head).  MFMA v_mfma_f32_16x16x32_bf16
+// throughout, with every product arranged so that no register transposes are
+// needed (cdna_hip_programming.md §5.5 T10/T12):
+//   * a D tile (lane l holds rows 4*(l>>4)+e, column l&15) feeds the next MFMA
+//     directly as the operand whose contraction index is D's ROW index, with
+//     the k order pi = {4g..4g+3, 16+4g..16+4g+3} over two stacked D tiles;
+//   * the matching other operand is read from LDS with ds_read_b64_tr_b16 in
+//     the same pi order (row-major [token][64] image, no transposed copies);
+//   * forward computes S^T = K Q^T so the softmax runs over a D tile's rows
+//     and P^T feeds O^T = V^T P^T; the output lands 4 consecutive head dims
+//     per lane (8-byte stores into o).
+// Backward (one kernel, 2 workgroups/CU): D_i = rowsum(dO * O) and the saved base-2 logsumexp
+// recompute P in-kernel; phase A (per 16-key block) accumulates dV^T = dO^T P
+// and dK^T = Q^T dS over all queries, phase B (per 16-query tile)
+// dQ^T = K^T dS^T over all keys -- no atomics, no dq/dkv kernel split.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "../common.h"
+
+namespace dmp {
+namespace {
+
+using bf16 = __bf16;
+using v4i16 = short __attribute__((ext_vector_type(4)));
+using lds_v4 = __attribute__((address_space(3))) v4i16;
+constexpr int DH = 64;
+constexpr int LROW = DH + 8;  // LDS row stride (bf16): 144 B, 16-B aligned rows, spreads banks
+constexpr int kThreads = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ bf16x8 lds8(const bf16* base, int row, int col) {
+  return *reinterpret_cast<const bf16x8*>(base + row * LROW + col);
+}
+
+// pi-ordered transposed read: lane (group g, index i) gets column col0 + i of
+// rows rbase + 4g + {0..3} (elements 0-3) and rbase + 16 + 4g + {0..3} (4-7).
+__device__ __forceinline__ bf16x8 lds_tr8(const bf16* base, int rbase, int col0, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const bf16* a = base + (rbase + 4 * g + q) * LROW + col0 + 4 * p;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a);
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a + 16 * LROW));
+  short __attribute__((ext_vector_type(8))) t = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, t);
+}
+
+// two stacked D tiles -> one pi-ordered MFMA operand
+__device__ __forceinline__ bf16x8 pack_pi(const float (&a)[4], const float (&b)[4]) {
+  f32x8 f = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_convertvector(f, bf16x8);
+}
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// rows [0, S) of a [S, 64] strided matrix into a zero-padded [SP][LROW] LDS image
+template <int SP>
+__device__ __forceinline__ void stage(bf16* dst, const bf16* src, int64_t ld, int S) {
+  for (int v = threadIdx.x; v < SP * (DH / 8); v += kThreads) {
+    const int r = v >> 3, c = (v & 7) * 8;
+    bf16x8 x = r < S ? *reinterpret_cast<const bf16x8*>(src + (int64_t)r * ld + c) : bf16x8{};
+    *reinterpret_cast<bf16x8*>(dst + r * LROW + c) = x;
+  }
+}
+
+__device__ __forceinline__ void store4(bf16* p, const f32x4& v, float s) {
+  bf16x4 o = {(bf16)(v[0] * s), (bf16)(v[1] * s), (bf16)(v[2] * s), (bf16)(v[3] * s)};
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+
+template <int SP>
+__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const bf16* __restrict__ qkv, int64_t ld,
+                                                            int S, int H, float scale,
+                                                            bf16* __restrict__ o, int64_t ldo,
+                                                            float* __restrict__ lse) {
+  constexpr int NKT = SP / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * SP * LROW];
+  bf16* Ks = smem;
+  bf16* Vs = smem + SP * LROW;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * DH;
+  const bf16* qb = qkv + (int64_t)b * S * ld + h * DH;
+  stage<SP>(Ks, qb + D, ld, S);
+  stage<SP>(Vs, qb + 2 * D, ld, S);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const float sl2 = scale * kLog2e;
+  const int nqt = (S + 15) / 16;
+  for (int qt = wave; qt < nqt; qt += kThreads / 64) {
+    const int q = qt * 16 + li;
+    const int qc = min(q, S - 1);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)qc * ld + ks * 32 + g * 8);
+    f32x4 st[NKT];
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) a = mfma(lds8(Ks, kt * 16 + li, ks * 32 + g * 8), qf[ks], a);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (kt * 16 + 4 * g + e >= S) a[e] = -INFINITY;
+        m = fmaxf(m, a[e]);
+      }
+      st[kt] = a;
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mb = m * sl2;
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float p = exp2f(st[kt][e] * sl2 - mb);
+        st[kt][e] = p;
+        l += p;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < NKT / 2; ++kc) {
+      float p0[4], p1[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { p0[e] = st[2 * kc][e]; p1[e] = st[2 * kc + 1][e]; }
+      const bf16x8 pb = pack_pi(p0, p1);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = mfma(lds_tr8(Vs, kc * 32, t * 16, lane), pb, acc[t]);
+    }
+    if (q < S) {
+      const float inv = 1.f / l;
+      bf16* orow = o + ((int64_t)b * S + q) * ldo + h * DH;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) store4(orow + t * 16 + 4 * g, acc[t], inv);
+      if (g == 0) lse[(int64_t)bh * SP + q] = mb + log2f(l);  // base-2 logsumexp of the scaled scores
+    }
+  }
+}
+
+template <int SP>
+__global__ __launch_bounds__(kThreads, 2) void attn_bwd_kernel(
+    const bf16* __restrict__ qkv, int64_t ld, const bf16* __restrict__ dout, int64_t ldd,
+    const bf16* __restrict__ o, int64_t ldo, const float* __restrict__ lse, int S, int H, float scale,
+    bf16* __restrict__ dqkv, int64_t lddq) {
+  // Two LDS images, reused: phase A holds Q and dO (K / V rows of the wave's
+  // key block come straight from L2 into registers), phase B holds K and V
+  // (Q / dO rows of the query tile from L2).  64 KB + 2 KB -> 2 workgroups/CU.
+  __shared__ __attribute__((aligned(16))) char smem[2 * SP * LROW * 2 + 2 * SP * 4];
+  bf16* X0 = reinterpret_cast<bf16*>(smem);
+  bf16* X1 = X0 + SP * LROW;
+  float* lse_s = reinterpret_cast<float*>(X1 + SP * LROW);
+  float* dd_s = lse_s + SP;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * DH;
+  const bf16* qb = qkv + (int64_t)b * S * ld + h * DH;
+  const bf16* db = dout + (int64_t)b * S * ldd + h * DH;
+  stage<SP>(X0, qb, ld, S);    // Q
+  stage<SP>(X1, db, ldd, S);   // dO
+  __syncthreads();
+  // D_i = sum_d dO[i][d] * O[i][d]  (fp32): O from global, dO from LDS
+  for (int r = threadIdx.x; r < SP; r += kThreads) {
+    float acc = 0.f;
+    if (r < S) {
+      const bf16* orow = o + ((int64_t)b * S + r) * ldo + h * DH;
+#pragma unroll
+      for (int c = 0; c < DH; c += 8) {
+        const f32x8 x = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(orow + c), f32x8);
+        const f32x8 y = __builtin_convertvector(lds8(X1, r, c), f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = fmaf(x[j], y[j], acc);
+      }
+    }
+    dd_s[r] = acc;
+    lse_s[r] = r < S ? lse[(int64_t)bh * SP + r] : INFINITY;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const float sl2 = scale * kLog2e;
+  const int nt = (S + 15) / 16;
+  bf16* dq_base = dqkv + (int64_t)b * S * lddq + h * DH;
+  const bf16* Qs = X0;
+  const bf16* dOs = X1;
+
+  // ---- phase A: per 16-key block, dV^T = dO^T P and dK^T = Q^T dS over all queries ----
+  for (int kb = wave; kb < nt; kb += kThreads / 64) {
+    const int key = kb * 16 + li;
+    const bool kin = key < S;
+    const int kr = min(key, S - 1);
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)kr * ld + D + ks * 32 + g * 8);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)kr * ld + 2 * D + ks * 32 + g * 8);
+    }
+    f32x4 dv[4], dk[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
+#pragma unroll 1
+    for (int qc = 0; qc < SP / 32; ++qc) {
+      float pp[2][4], dss[2][4];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int q0 = qc * 32 + hf * 16;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s = mfma(lds8(Qs, q0 + li, ks * 32 + g * 8), kf[ks], s);
+          dp = mfma(lds8(dOs, q0 + li, ks * 32 + g * 8), vf[ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = q0 + 4 * g + e;
+          const float p = kin ? exp2f(s[e] * sl2 - lse_s[q]) : 0.f;
+          pp[hf][e] = p;
+          dss[hf][e] = p * (dp[e] - dd_s[q]);
+        }
+      }
+      const bf16x8 pb = pack_pi(pp[0], pp[1]);
+      const bf16x8 dsb = pack_pi(dss[0], dss[1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dv[t] = mfma(lds_tr8(dOs, qc * 32, t * 16, lane), pb, dv[t]);
+        dk[t] = mfma(lds_tr8(Qs, qc * 32, t * 16, lane), dsb, dk[t]);
+      }
+    }
+    if (kin) {
+      bf16* row = dq_base + (int64_t)key * lddq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        store4(row + D + t * 16 + 4 * g, dk[t], scale);
+        store4(row + 2 * D + t * 16 + 4 * g, dv[t], 1.f);
+      }
+    }
+  }
+
+  // ---- phase B: K and V replace Q and dO in LDS ----
+  __syncthreads();
+  stage<SP>(X0, qb + D, ld, S);      // K
+  stage<SP>(X1, qb + 2 * D, ld, S);  // V
+  __syncthreads();
+  const bf16* Ks = X0;
+  const bf16* Vs = X1;
+  // per 16-query tile, dQ^T = K^T dS^T over all keys
+  for (int qt = wave; qt < nt; qt += kThreads / 64) {
+    const int q = qt * 16 + li;
+    const int qr = min(q, S - 1);
+    bf16x8 qf[2], dof[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)qr * ld + ks * 32 + g * 8);
+      dof[ks] = *reinterpret_cast<const bf16x8*>(db + (int64_t)qr * ldd + ks * 32 + g * 8);
+    }
+    const float lq = lse_s[q], dq_d = dd_s[q];
+    f32x4 dq[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kc = 0; kc < SP / 32; ++kc) {
+      float dss[2][4];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int k0 = kc * 32 + hf * 16;
+        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s = mfma(lds8(Ks, k0 + li, ks * 32 + g * 8), qf[ks], s);
+          dp = mfma(lds8(Vs, k0 + li, ks * 32 + g * 8), dof[ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int key = k0 + 4 * g + e;
+          const float p = key < S ? exp2f(s[e] * sl2 - lq) : 0.f;
+          dss[hf][e] = p * (dp[e] - dq_d);
+        }
+      }
+      const bf16x8 dsb = pack_pi(dss[0], dss[1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dq[t] = mfma(lds_tr8(Ks, kc * 32, t * 16, lane), dsb, dq[t]);
+    }
+    if (q < S) {
+      bf16* row = dq_base + (int64_t)q * lddq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) store4(row + t * 16 + 4 * g, dq[t], scale);
+    }
+  }
+}
+
+int pad_seq(int64_t S) {
+  const int sp = (int)((S + 31) / 32 * 32);
+  return sp <= 64 ? 64 : sp <= 128 ? 128 : sp <= 160 ? 160 : sp <= 192 ? 192 : sp <= 224 ? 224 : 256;
+}
+
+void check_2d(const at::Tensor& t, const char* name, int64_t rows, int64_t min_cols) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.dim() == 2, name,
+              " must be a 2-D bf16 GPU tensor");
+  TORCH_CHECK(t.size(0) == rows && t.size(1) >= min_cols, name, " has the wrong shape");
+  TORCH_CHECK(t.stride(1) == 1 && t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " rows must be contiguous and 16-byte aligned");
+}
+
+#define DMP_ATTN_DISPATCH(SP_, ...)                                        \
+  switch (SP_) {                                                           \
+    case 64: { constexpr int SPC = 64; __VA_ARGS__; break; }               \
+    case 128: { constexpr int SPC = 128; __VA_ARGS__; break; }             \
+    case 160: { constexpr int SPC = 160; __VA_ARGS__; break; }             \
+    case 192: { constexpr int SPC = 192; __VA_ARGS__; break; }             \
+    case 224: { constexpr int SPC = 224; __VA_ARGS__; break; }             \
+    default: { constexpr int SPC = 256; __VA_ARGS__; break; }              \
+  }
+
+}  // namespace
+
+bool attention_supported(int64_t S, int64_t head_dim) { return head_dim == DH && S >= 1 && S <= 256; }
+
+// qkv [B*S, >= 3*H*64] -> (o [B*S, H*64], lse [B*H, SP] fp32, base-2)
+std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale) {
+  TORCH_CHECK(attention_supported(S, DH), "attention: S must be in [1, 256]");
+  check_2d(qkv, "qkv", B * S, 3 * H * DH);
+  const int sp = pad_seq(S);
+  auto o = at::empty({B * S, H * DH}, qkv.options());
+  auto lse = at::empty({B * H, sp}, qkv.options().dtype(at::kFloat));
+  hipStream_t st = at::hip::getCurrentHIPStream();
+  DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_fwd_kernel<SPC>), dim3(B * H), dim3(kThreads), 0, st,
+                                           (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,
+                                           (float)scale, (bf16*)o.data_ptr(), o.stride(0),
+                                           lse.data_ptr<float>()));
+  DMP_HIP_CHECK(hipGetLastError());
+  return {o, lse};
+}
+
+at::Tensor attention_backward(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o,
+                              const at::Tensor& lse, int64_t B, int64_t S, int64_t H, double scale) {
+  TORCH_CHECK(attention_supported(S, DH), "attention: S must be in [1, 256]");
+  check_2d(qkv, "qkv", B * S, 3 * H * DH);
+  check_2d(dout, "dout", B * S, H * DH);
+  check_2d(o, "o", B * S, H * DH);
+  const int sp = pad_seq(S);
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
+                  lse.size(0) == B * H && lse.size(1) == sp, "attention: lse shape");
+  auto dqkv = at::empty({B * S, 3 * H * DH}, qkv.options());
+  hipStream_t st = at::hip::getCurrentHIPStream();
+  DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_bwd_kernel<SPC>), dim3(B * H), dim3(kThreads), 0, st,
+                                           (const bf16*)qkv.data_ptr(), qkv.stride(0),
+                                           (const bf16*)dout.data_ptr(), dout.stride(0),
+                                           (const bf16*)o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
+                                           (int)S, (int)H, (float)scale, (bf16*)dqkv.data_ptr(),
+                                           dqkv.stride(0)));
+  DMP_HIP_CHECK(hipGetLastError());
+  return dqkv;
+}
+
+}  // namespace dmp

@@ -73,6 +73,11 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out);
 void set_gemm_xl_bn(int bn, int pipe, int group_m);
+// attention.hip
+bool attention_supported(int64_t S, int64_t head_dim);
+std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale);
+at::Tensor attention_backward(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o,
+                              const at::Tensor& lse, int64_t B, int64_t S, int64_t H, double scale);
 // depthwise.hip
 std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor& w, int64_t stride,
                                           bool moments);
@@ -155,6 +160,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("out") = py::none());
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
+
+  // ---- fused self-attention on packed qkv (ViT) ----
+  m.def("attention_supported", &dmp::attention_supported);
+  m.def("attention_forward", &dmp::attention_forward, py::arg("qkv"), py::arg("B"), py::arg("S"),
+        py::arg("H"), py::arg("scale"));
+  m.def("attention_backward", &dmp::attention_backward, py::arg("dout"), py::arg("qkv"), py::arg("o"),
+        py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("scale"));
 
   // ---- LayerNorm (last dim) ----
   m.def("layernorm_forward", &dmp::layernorm_forward);

@@ -5,7 +5,8 @@ embedding, 12 pre-LN encoder blocks, LayerNorm + linear head).
 BASELINE.json config 5 ("ViT-B/16 DDP bf16 ... large-grad bucket fusion, MFMA
 GEMM path").  The encoder is written so that all matmuls are plain GEMMs on
 [B*T, D] activations (qkv, proj, fc1, fc2 land on hipBLASLt/MFMA) and
-attention uses the fused SDPA kernel; no per-head Python loops.
+attention runs on the packed-qkv HIP kernels (ops/attention.py) with no
+head split / merge copies; no per-head Python loops.
 """
 from __future__ import annotations
 
@@ -16,6 +17,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.attention import self_attention_packed
 from ..ops.fused import GradSlot, grad_tap
 from ..ops.layernorm import LayerNorm
 
@@ -43,11 +45,10 @@ class SelfAttention(nn.Module):
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        b, t, d = x.shape
-        qkv = self.qkv(x).view(b, t, 3, self.heads, d // self.heads).permute(2, 0, 3, 1, 4)
-        q, k, v = qkv.unbind(0)
-        o = F.scaled_dot_product_attention(q, k, v, dropout_p=self.dropout if self.training else 0.0)
-        return self.proj(o.transpose(1, 2).reshape(b, t, d))
+        # packed-qkv attention (ops/attention.py): the fused HIP kernels read the
+        # qkv GEMM output and write the proj GEMM input / the qkv gradient as is
+        o = self_attention_packed(self.qkv(x), self.heads, self.dropout if self.training else 0.0)
+        return self.proj(o)
 
 
 class EncoderBlock(nn.Module):

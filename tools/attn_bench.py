@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""ViT-B/16 attention (B=128, S=197, H=12, Dh=64): packed-qkv HIP kernels vs
+the SDPA path including its layout copies.  HIP-event timing."""
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_model_parallel_amd.ops import attention as A  # noqa: E402
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def sdpa_path(qkv, heads):
+    b, s, d3 = qkv.shape
+    d = d3 // 3
+    q, k, v = qkv.view(b, s, 3, heads, d // heads).permute(2, 0, 3, 1, 4).unbind(0)
+    o = F.scaled_dot_product_attention(q, k, v)
+    return o.transpose(1, 2).reshape(b, s, d)
+
+
+def main():
+    B, S, H = int(os.environ.get("B", 128)), 197, 12
+    qkv = torch.randn(B, S, 3 * H * 64, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    go = torch.randn(B, S, H * 64, device="cuda", dtype=torch.bfloat16)
+    for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("packed hip", lambda: A.self_attention_packed(qkv, H))):
+        tf = timeit(lambda: fn())
+        o = fn()
+        tb = timeit(lambda: torch.autograd.grad(o, qkv, go, retain_graph=True))
+        fl = 4.0 * B * H * S * S * 64
+        print(f"{name:12s} fwd {tf:.3f} ms ({fl / tf / 1e9:.0f} TF/s)  bwd {tb:.3f} ms ({2.5 * fl / tb / 1e9:.0f} TF/s)"
+              f"  total {tf + tb:.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
