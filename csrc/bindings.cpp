@@ -85,6 +85,10 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
                            int64_t W);
 at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride,
                            at::ScalarType out_dtype);
+// bias_act.hip
+bool colsum_supported(int64_t N);
+at::Tensor bias_grad(const at::Tensor& dy, at::ScalarType out_dtype);
+std::vector<at::Tensor> gelu_bwd_bias_grad(const at::Tensor& dy, const at::Tensor& h, at::ScalarType out_dtype);
 // layernorm.hip
 std::vector<at::Tensor> layernorm_forward(const at::Tensor& x, const c10::optional<at::Tensor>& w,
                                           const c10::optional<at::Tensor>& b, int64_t D,
@@ -167,6 +171,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("H"), py::arg("scale"));
   m.def("attention_backward", &dmp::attention_backward, py::arg("dout"), py::arg("qkv"), py::arg("o"),
         py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("scale"));
+
+  // ---- Linear side passes: bias gradient, GELU backward + bias gradient ----
+  m.def("colsum_supported", &dmp::colsum_supported);
+  m.def("bias_grad", &dmp::bias_grad, py::arg("dy"), py::arg("out_dtype"));
+  m.def("gelu_bwd_bias_grad", &dmp::gelu_bwd_bias_grad, py::arg("dy"), py::arg("h"), py::arg("out_dtype"));
 
   // ---- LayerNorm (last dim) ----
   m.def("layernorm_forward", &dmp::layernorm_forward);

@@ -16,6 +16,7 @@
 //     one partial row per block -> a column reduce launch.
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
+#include "../colreduce.h"
 #include "../common.h"
 
 namespace dmp {
@@ -131,7 +132,34 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
   }
 }
 
-// dgamma/dbeta partials: part[block][0:D] = sum dy*xhat, part[block][D:2D] = sum dy
+// raw 8-element activation vectors held across a row (the prefetch buffer)
+template <typename T> struct Raw8;
+template <> struct Raw8<__bf16> {
+  bf16x8 v;
+  __device__ void load(const __bf16* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+  __device__ void get(float (&o)[8]) const {
+    const f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = f[i];
+  }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  __device__ void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  __device__ void get(float (&o)[8]) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[i + 4] = b[i]; }
+  }
+};
+
+// dgamma/dbeta partials: part[block][0:D] = sum dy*xhat, part[block][D:2D] = sum dy.
+// The next row's x / dy / residual-gradient vectors are loaded before the
+// current row is reduced and written (one row of loads always in flight per
+// wave): with one wave per row the kernel is otherwise latency-bound, not
+// bandwidth-bound (85 us -> see profiles/vit_b16_bs128_1gpu_v3.md).
 template <typename T, typename P, int kMaxV>
 __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const P* __restrict__ w,
@@ -149,17 +177,34 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
     for (int i = 0; i < 8; ++i) { accw[k][i] = 0.f; accb[k][i] = 0.f; gw[k][i] = 1.f; }
     if (c < nv && w) PVec<P>::load(w + c * 8, gw[k]);
   }
+  Raw8<T> nx[kMaxV], ndy[kMaxV], nres[kMaxV];
+  float nmean = 0.f, nrstd = 0.f;
+  auto fetch = [&](int64_t r) {
+    nmean = mean_in[r];
+    nrstd = rstd_in[r];
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nv) {
+        nx[k].load(x + r * D + c * 8);
+        ndy[k].load(dy + r * D + c * 8);
+        if (dres) nres[k].load(dres + r * D + c * 8);
+      }
+    }
+  };
+  if (wave < rows) fetch(wave);
   for (int64_t r = wave; r < rows; r += nwaves) {
-    const float mean = mean_in[r], rstd = rstd_in[r];
-    float xh[kMaxV][8], g[kMaxV][8];
+    const float mean = nmean, rstd = nrstd;
+    float xh[kMaxV][8], g[kMaxV][8], rv[kMaxV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int c = lane + 64 * k;
       if (c < nv) {
         float dv[8];
-        ld8<T>(x + r * D + c * 8, xh[k]);
-        ld8<T>(dy + r * D + c * 8, dv);
+        nx[k].get(xh[k]);
+        ndy[k].get(dv);
+        if (dres) nres[k].get(rv[k]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           xh[k][i] = (xh[k][i] - mean) * rstd;
@@ -171,6 +216,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
         }
       }
     }
+    if (r + nwaves < rows) fetch(r + nwaves);  // next row in flight during the reduce + store
     const float c1 = wave_sum(s1) / (float)D, c2 = wave_sum(s2) / (float)D;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
@@ -180,10 +226,8 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] = rstd * (g[k][i] - xh[k][i] * c1 - c2);
         if (dres) {  // + the residual branch's gradient of the same input (one pass)
-          float rv[8];
-          ld8<T>(dres + r * D + c * 8, rv);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += rv[i];
+          for (int i = 0; i < 8; ++i) o[i] += rv[k][i];
         }
         st8<T>(dx + r * D + c * 8, o);
       }
@@ -216,25 +260,6 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
   }
 }
 
-// out[c] = sum_b part[b][c]: 256 threads = 32 columns x 8 row groups, LDS fold.
-template <typename OT>
-__global__ __launch_bounds__(256) void ln_col_reduce_kernel(const float* __restrict__ part, int nb,
-                                                            int n, OT* __restrict__ out) {
-  const int cl = threadIdx.x % 32, g = threadIdx.x / 32;
-  const int c = blockIdx.x * 32 + cl;
-  float s = 0.f;
-  if (c < n)
-    for (int b = g; b < nb; b += 8) s += part[(int64_t)b * n + c];
-  __shared__ float red[256];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  if (g == 0 && c < n) {
-    float t = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) t += red[q * 32 + cl];
-    out[c] = (OT)t;
-  }
-}
 
 void check_ln(const at::Tensor& x, int64_t D, const char* name) {
   TORCH_CHECK(x.is_cuda() && x.is_contiguous(), name, " must be a contiguous GPU tensor");
@@ -306,7 +331,9 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
   auto dwb = at::empty({2, D}, x.options().dtype(param_dtype));
   if (rows == 0) return {dx, dwb[0].zero_(), dwb[1].zero_()};
   auto stream = at::hip::getCurrentHIPStream();
-  const int nb = ln_blocks(rows, 256);  // one block per CU: partial rows for dgamma/dbeta
+  // 4 blocks (16 waves) per CU: enough rows in flight to reach the HBM rate;
+  // each block writes one dgamma/dbeta partial row
+  const int nb = ln_blocks(rows, 1024);
   auto part = at::empty({nb, 2 * D}, x.options().dtype(at::kFloat));
   const bool pbf = hw && w->scalar_type() == at::kBFloat16;
 #define DMP_LN_BWD(T, P)                                                                        \
@@ -325,11 +352,9 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
 #undef DMP_LN_BWD
   const int n = (int)(2 * D);
   if (param_dtype == at::kBFloat16)
-    hipLaunchKernelGGL(ln_col_reduce_kernel<__bf16>, dim3((n + 31) / 32), dim3(256), 0, stream,
-                       part.data_ptr<float>(), nb, n, reinterpret_cast<__bf16*>(dwb.data_ptr()));
+    colreduce::launch(part.data_ptr<float>(), nb, n, reinterpret_cast<__bf16*>(dwb.data_ptr()), stream);
   else
-    hipLaunchKernelGGL(ln_col_reduce_kernel<float>, dim3((n + 31) / 32), dim3(256), 0, stream,
-                       part.data_ptr<float>(), nb, n, dwb.data_ptr<float>());
+    colreduce::launch(part.data_ptr<float>(), nb, n, dwb.data_ptr<float>(), stream);
   return {dx, dwb[0], dwb[1]};
 }
 

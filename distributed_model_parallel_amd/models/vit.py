@@ -20,17 +20,19 @@ import torch.nn.functional as F
 from ..ops.attention import self_attention_packed
 from ..ops.fused import GradSlot, grad_tap
 from ..ops.layernorm import LayerNorm
+from ..ops.linear import Linear, linear_gelu
 
 
 class MLP(nn.Module):
     def __init__(self, dim: int, hidden: int, dropout: float = 0.0):
         super().__init__()
-        self.fc1 = nn.Linear(dim, hidden)
-        self.fc2 = nn.Linear(hidden, dim)
+        self.fc1 = Linear(dim, hidden)
+        self.fc2 = Linear(hidden, dim)
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = F.gelu(self.fc1(x))
+        # fc1 + GELU: the backward fuses gelu'(h) with fc1's bias gradient (ops/linear.py)
+        x = linear_gelu(x, self.fc1.weight, self.fc1.bias)
         x = F.dropout(x, self.dropout, self.training)
         return F.dropout(self.fc2(x), self.dropout, self.training)
 
@@ -40,8 +42,8 @@ class SelfAttention(nn.Module):
         super().__init__()
         assert dim % heads == 0
         self.heads = heads
-        self.qkv = nn.Linear(dim, 3 * dim)
-        self.proj = nn.Linear(dim, dim)
+        self.qkv = Linear(dim, 3 * dim)
+        self.proj = Linear(dim, dim)
         self.dropout = dropout
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:

@@ -17,8 +17,11 @@ CATS = [
     ("dmp BN (ours)", ("bn_moments", "bn_apply", "bn_bwd", "bn_reduce")),
     ("dmp fused SGD (ours)", ("sgd_flat",)),
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
-    ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "split_reduce", "dw_fwd",
+    ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "split_reduce", "dw_fwd",
                               "dw_dgrad", "dw_wgrad", "column_reduce")),
+    ("dmp attention (ours)", ("attn_fwd_kernel", "attn_bwd_kernel")),
+    ("dmp LayerNorm (ours)", ("ln_fwd", "ln_bwd", "ln_col_reduce")),
+    ("dmp linear side passes (ours)", ("colsum_kernel", "partial_colsum")),
     ("MIOpen conv (igemm/ck)", ("igemm", "conv", "ck::", "naive_conv", "gridwise")),
     ("MIOpen tensor ops", ("SubTensorOp", "Op1dTensor", "Op2dTensor", "Op4dTensor")),
     ("hipBLASLt / rocBLAS GEMM", ("Cijk", "gemm", "Gemm")),
