@@ -41,7 +41,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from distributed_model_parallel_amd.comm.rccl import default_communicator  # noqa: E402
 from distributed_model_parallel_amd.models import INPUT_SHAPES  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
-from distributed_model_parallel_amd.utils import gemm_tuning  # noqa: E402
+from distributed_model_parallel_amd.utils import gemm_tuning, miopen_db  # noqa: E402
 from distributed_model_parallel_amd.utils.env import destroy_distributed, init_distributed  # noqa: E402
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
 
@@ -73,6 +73,10 @@ def main() -> int:
     ap.add_argument("--lr", type=float, default=None,
                     help="SGD learning rate (default 0.1 for CNNs, 0.005 for ViT: plain SGD at 0.1 "
                          "diverges on a transformer, which would make the reported loss meaningless)")
+    ap.add_argument("--miopen-db", default=os.environ.get("DMP_MIOPEN_DB", "use"),
+                    choices=["use", "refresh", "off"],
+                    help="seed MIOpen's find/perf db from profiles/miopen/ (use), also write new "
+                         "entries back (refresh), or start empty (off); see utils/miopen_db.py")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
     ap.add_argument("--gemm-tuning", default=os.environ.get("DMP_GEMM_TUNING", "use"),
@@ -88,6 +92,8 @@ def main() -> int:
     if env.world_size != args.gpus and env.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
+    if env.device.type == "cuda":
+        miopen_db.seed(args.miopen_db)  # before the first conv creates the MIOpen handle
     dev = env.device
     tuning_file = gemm_tuning.configure(args.gemm_tuning, args.model) if dev.type == "cuda" else None
     cfg = StepConfig(model=args.model, batch_size=args.batch_size, image_size=args.image_size,

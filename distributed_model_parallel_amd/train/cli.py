@@ -260,7 +260,10 @@ def _spawn_entry(rank: int, world: int, args) -> None:
 
 def main_worker(args) -> None:
     from ..utils.env import destroy_distributed, init_distributed, seed_everything
+    from ..utils import miopen_db
     env = init_distributed(backend=args.dist_backend, dist_url=args.dist_url)
+    if env.device.type == "cuda":
+        miopen_db.seed("use")  # committed MIOpen find db (skips the first-step solver search)
     seed_everything(args.seed + (env.rank if args.parallel == "ddp" else 0))
     try:
         if args.parallel == "pipe":

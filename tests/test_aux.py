@@ -144,3 +144,20 @@ dist.destroy_process_group()
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "resnet50" in r.stdout and "vit_b_16" in r.stdout
+
+
+def test_miopen_db_seed(tmp_path, monkeypatch):
+    """utils/miopen_db.py: the committed find db is copied to a private dir and
+    MIOPEN_USER_DB_PATH points at it; a user-set path is left alone."""
+    from distributed_model_parallel_amd.utils import miopen_db
+    monkeypatch.delenv("MIOPEN_USER_DB_PATH", raising=False)
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    d = miopen_db.seed("use")
+    assert d is not None and os.environ["MIOPEN_USER_DB_PATH"] == d
+    shipped = sorted(f.name for f in miopen_db.DB_DIR.glob("*.txt"))
+    assert shipped and sorted(os.listdir(d)) == shipped
+    assert any(n.endswith(".ufdb.txt") for n in shipped)
+    monkeypatch.setenv("MIOPEN_USER_DB_PATH", "/somewhere/else")
+    assert miopen_db.seed("use") is None
+    assert os.environ["MIOPEN_USER_DB_PATH"] == "/somewhere/else"
+    assert miopen_db.seed("off") is None
