@@ -7,6 +7,16 @@ spends ~50 s timing every solver for each problem (measured: warm-up step 0
 104.6 s with an empty user database vs 54.4 s with the database below; the
 kernel binary cache made no difference, ``profiles/README.md`` finding 9).
 
+Measured further (``tools/first_step.py`` with ``MIOPEN_LOG_LEVEL=5``): with
+the find db seeded, MIOpen's find still *times* every applicable solver, and
+~54 s of the remaining first step is the reference "naive" direct solvers
+(``ConvDirectNaive{Fwd,Bwd,Wrw}``: e.g. 2.37 s per timing run of the stem's
+weight gradient, 30-1000x slower than the implicit-GEMM solvers that always
+win).  :func:`seed` therefore also takes them out of find's candidate list
+(``MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_*=0``, unless the user set them): every
+conv of the bench models has two implicit-GEMM solvers applicable (checked
+against the db: ``tests/test_aux.py``).
+
 The databases are MIOpen's own text formats (``*.ufdb.txt``: find results,
 ``*.udb.txt``: tuned solver parameters), produced by a bench run on MI355X and
 kept under ``profiles/miopen/``.  :func:`seed` copies them into a per-rank
@@ -29,6 +39,7 @@ from typing import Optional
 ROOT = Path(__file__).resolve().parents[2]
 DB_DIR = ROOT / "profiles" / "miopen"
 _ENV = "MIOPEN_USER_DB_PATH"
+NAIVE_SOLVER_ENVS = tuple(f"MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_{d}" for d in ("FWD", "BWD", "WRW"))
 
 
 def _rank_dir() -> Path:
@@ -37,11 +48,17 @@ def _rank_dir() -> Path:
     return base / f"dmp_miopen_db_{tag}"
 
 
-def seed(mode: str = "use") -> Optional[str]:
+def seed(mode: str = "use", skip_naive: bool = True) -> Optional[str]:
     """mode "use": seed from the committed db; "refresh": seed, then copy the
     (possibly grown) db back at exit; "off": MIOpen defaults.  Returns the
-    directory MIOpen will use, or None when untouched."""
-    if mode == "off" or os.environ.get(_ENV):
+    directory MIOpen will use, or None when untouched.  skip_naive: drop the
+    naive reference solvers from find (module docstring)."""
+    if mode == "off":
+        return None
+    if skip_naive:
+        for k in NAIVE_SOLVER_ENVS:
+            os.environ.setdefault(k, "0")
+    if os.environ.get(_ENV):
         return None
     if mode not in ("use", "refresh"):
         raise ValueError(f"unknown miopen db mode {mode!r}")

@@ -161,3 +161,20 @@ def test_miopen_db_seed(tmp_path, monkeypatch):
     assert miopen_db.seed("use") is None
     assert os.environ["MIOPEN_USER_DB_PATH"] == "/somewhere/else"
     assert miopen_db.seed("off") is None
+    for k in miopen_db.NAIVE_SOLVER_ENVS:
+        assert os.environ[k] == "0"
+        monkeypatch.delenv(k)
+
+
+def test_miopen_db_entries_have_fast_solvers():
+    """Every committed find-db problem has an implicit-GEMM solver besides the
+    naive reference one, so dropping the naive solvers from find is safe for it."""
+    from distributed_model_parallel_amd.utils import miopen_db
+    n = 0
+    for f in miopen_db.DB_DIR.glob("*.ufdb.txt"):
+        for line in f.read_text().splitlines():
+            key, sols = line.split("=", 1)
+            names = [s.split(":")[0] for s in sols.split(";")]
+            assert any("ImplicitGemm" in s for s in names), key
+            n += 1
+    assert n > 0
