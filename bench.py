@@ -4,10 +4,11 @@
 BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP bf16 at 1/2/4/8
 MI355X".  One process per GPU (torchrun for N>1), synthetic 3x224x224 inputs
 and random-init weights (no datasets / checkpoints are available offline),
-fixed per-GPU batch (weak scaling; ResNet-50 default 512 images per GPU --
+fixed per-GPU batch (weak scaling; ResNet-50 default 1024 images per GPU --
 measured on 1x MI355X: 7607 img/s at 128, 8339 at 192, 8866 at 256, 9279 at
-384, 9454 at 512; the 288 GB of HBM hold it easily and a bigger per-GPU
-share also amortises the fixed gradient all-reduce).  Every timed step is a full training step:
+384, 9600-9744 at 512, 9948 at 768, 10300 at 1024 (40 GB peak), 10580 at
+2048 (80 GB); the 288 GB of HBM hold it easily and a bigger per-GPU share
+also amortises the fixed gradient all-reduce).  Every timed step is a full training step:
 forward, fp32 cross-entropy, backward with the native C++ reducer doing
 bucketed RCCL all-reduces (25 MB buckets, ncclAvg) overlapped with backward,
 one fused flat-SGD (momentum 0.9, wd 1e-4) launch per dtype group.
@@ -46,7 +47,7 @@ from distributed_model_parallel_amd.utils.env import destroy_distributed, init_d
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
 
 # per-GPU batch defaults (measured throughput curves: module docstring, README)
-DEFAULT_BATCH = {"resnet50": 512, "vit_b_16": 256, "mobilenetv2": 512}
+DEFAULT_BATCH = {"resnet50": 1024, "vit_b_16": 256, "mobilenetv2": 512}
 BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference images/sec figure exists
 
 
@@ -170,6 +171,8 @@ def main() -> int:
             "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
             if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,
             "final_loss": round(final_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
+            if dev.type == "cuda" else None,
         },
     }
     if env.is_main:
