@@ -67,13 +67,32 @@ __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// rows [0, S) of a [S, 64] strided matrix into a zero-padded [SP][LROW] LDS image
+// rows [0, S) of two [S, 64] strided matrices into zero-padded [SP][LROW] LDS
+// images.  Every global load of both images is issued before the first LDS
+// store (SP*16/256 16-B loads in flight per lane instead of one): the staging
+// is the latency-bound head of both kernels.
 template <int SP>
-__device__ __forceinline__ void stage(bf16* dst, const bf16* src, int64_t ld, int S) {
-  for (int v = threadIdx.x; v < SP * (DH / 8); v += kThreads) {
+__device__ __forceinline__ void stage2(bf16* dst0, const bf16* src0, int64_t ld0, bf16* dst1,
+                                       const bf16* src1, int64_t ld1, int S) {
+  constexpr int PER = SP * (DH / 8);
+  constexpr int IT = (PER + kThreads - 1) / kThreads;
+  bf16x8 r0[IT], r1[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int v = threadIdx.x + i * kThreads;
     const int r = v >> 3, c = (v & 7) * 8;
-    bf16x8 x = r < S ? *reinterpret_cast<const bf16x8*>(src + (int64_t)r * ld + c) : bf16x8{};
-    *reinterpret_cast<bf16x8*>(dst + r * LROW + c) = x;
+    const bool ok = v < PER && r < S;
+    r0[i] = ok ? *reinterpret_cast<const bf16x8*>(src0 + (int64_t)r * ld0 + c) : bf16x8{};
+    r1[i] = ok ? *reinterpret_cast<const bf16x8*>(src1 + (int64_t)r * ld1 + c) : bf16x8{};
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int v = threadIdx.x + i * kThreads;
+    if (v < PER) {
+      const int r = v >> 3, c = (v & 7) * 8;
+      *reinterpret_cast<bf16x8*>(dst0 + r * LROW + c) = r0[i];
+      *reinterpret_cast<bf16x8*>(dst1 + r * LROW + c) = r1[i];
+    }
   }
 }
 
@@ -94,8 +113,7 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const bf16* __restri
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int D = H * DH;
   const bf16* qb = qkv + (int64_t)b * S * ld + h * DH;
-  stage<SP>(Ks, qb + D, ld, S);
-  stage<SP>(Vs, qb + 2 * D, ld, S);
+  stage2<SP>(Ks, qb + D, ld, Vs, qb + 2 * D, ld, S);
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -174,8 +192,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_kernel(
   const int D = H * DH;
   const bf16* qb = qkv + (int64_t)b * S * ld + h * DH;
   const bf16* db = dout + (int64_t)b * S * ldd + h * DH;
-  stage<SP>(X0, qb, ld, S);    // Q
-  stage<SP>(X1, db, ldd, S);   // dO
+  stage2<SP>(X0, qb, ld, X1, db, ldd, S);  // Q, dO
   __syncthreads();
   // D_i = sum_d dO[i][d] * O[i][d]  (fp32): O from global, dO from LDS
   for (int r = threadIdx.x; r < SP; r += kThreads) {
@@ -256,8 +273,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_kernel(
 
   // ---- phase B: K and V replace Q and dO in LDS ----
   __syncthreads();
-  stage<SP>(X0, qb + D, ld, S);      // K
-  stage<SP>(X1, qb + 2 * D, ld, S);  // V
+  stage2<SP>(X0, qb + D, ld, X1, qb + 2 * D, ld, S);  // K, V
   __syncthreads();
   const bf16* Ks = X0;
   const bf16* Vs = X1;
