@@ -14,6 +14,9 @@
 //             argmax bytes compared with the pixel's tap id, matching dy
 //             summed -- every dx element written exactly once.
 // Tie-breaking matches PyTorch (first maximum in window order; NaN wins).
+#include <cstdlib>
+#include <type_traits>
+
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "../common.h"
@@ -21,23 +24,26 @@
 namespace dmp {
 namespace {
 
+// 128 lanes per block: a 112-wide bf16 row of 64 channels is 896 lanes = 7 blocks.
+constexpr int kPoolThreads = 128;
+
 struct PoolGeo {
   int N, C, H, W, Ho, Wo, k, s, p, cv;  // cv = C / VEC
 };
 
 template <typename T>
-__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+__global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeo g,
-                                                          int64_t total) {
+                                                          int row_len) {
   constexpr int VEC = Vec16<T>::N;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int cvi = (int)(i % g.cv);
-  const int64_t pix = i / g.cv;
-  const int ow = (int)(pix % g.Wo);
-  const int64_t t = pix / g.Wo;
-  const int oh = (int)(t % g.Ho);
-  const int n = (int)(t / g.Ho);
+  // blockIdx.x = one output row (n, oh), uniform per block: no per-lane 64-bit
+  // div/mod chain; lanes run over (ow, channel vector) of that row.
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= row_len) return;
+  const int row = blockIdx.x;
+  const int n = row / g.Ho, oh = row - n * g.Ho;
+  const int ow = j / g.cv, cvi = j - ow * g.cv;
+  const int64_t pix = (int64_t)row * g.Wo + ow;
   const int c0 = cvi * VEC;
   float m[VEC];
   uint8_t am[VEC];
@@ -65,19 +71,18 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
 }
 
 template <typename T>
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy,
+__global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx,
                                                           T* __restrict__ dx, PoolGeo g,
-                                                          int64_t total) {
+                                                          int row_len) {
   constexpr int VEC = Vec16<T>::N;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int cvi = (int)(i % g.cv);
-  const int64_t pix = i / g.cv;
-  const int iw = (int)(pix % g.W);
-  const int64_t t = pix / g.W;
-  const int ih = (int)(t % g.H);
-  const int n = (int)(t / g.H);
+  // blockIdx.x = one input row (n, ih): the window range in oh is uniform per block.
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= row_len) return;
+  const int row = blockIdx.x;
+  const int n = row / g.H, ih = row - n * g.H;
+  const int iw = j / g.cv, cvi = j - iw * g.cv;
+  const int64_t pix = (int64_t)row * g.W + iw;
   const int c0 = cvi * VEC;
   float acc[VEC];
 #pragma unroll
@@ -117,6 +122,122 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
   Vec16<T>::store(dx + pix * g.C + c0, acc);
 }
 
+// Fixed-geometry fast paths (the ResNet stem's k=3, s=2).  Every tap of the
+// forward window and every candidate window of the backward is loaded
+// unconditionally from a clamped address and masked afterwards, so all loads
+// of a lane are in flight together instead of one dependent round trip per
+// tap (the runtime-k kernels above branch around each load).
+template <typename T, int K, int S>
+__global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_fixed_kernel(const T* __restrict__ x,
+                                                                       T* __restrict__ y,
+                                                                       uint8_t* __restrict__ idx,
+                                                                       PoolGeo g, int row_len) {
+  constexpr int VEC = Vec16<T>::N;
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= row_len) return;
+  const int row = blockIdx.x;
+  const int n = row / g.Ho, oh = row - n * g.Ho;
+  const int ow = j / g.cv, cvi = j - ow * g.cv;
+  const int c0 = cvi * VEC;
+  const int h0 = oh * S - g.p, w0 = ow * S - g.p;
+  const T* xn = x + (int64_t)n * g.H * g.W * g.C + c0;
+  float v[K][K][VEC];
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const int ih = min(max(h0 + a, 0), g.H - 1);
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const int iw = min(max(w0 + b, 0), g.W - 1);
+      Vec16<T>::load(xn + ((int64_t)ih * g.W + iw) * g.C, v[a][b]);
+    }
+  }
+  float m[VEC];
+  uint8_t am[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) { m[c] = -INFINITY; am[c] = 0; }
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const bool ha = (unsigned)(h0 + a) < (unsigned)g.H;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const bool ok = ha && (unsigned)(w0 + b) < (unsigned)g.W;
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) {
+        const float t = v[a][b][c];
+        if (ok && (t > m[c] || (t != t && m[c] == m[c]))) { m[c] = t; am[c] = (uint8_t)(a * K + b); }
+      }
+    }
+  }
+  const int64_t pix = (int64_t)row * g.Wo + ow;
+  Vec16<T>::store(y + pix * g.C + c0, m);
+  uint8_t* ip = idx + pix * g.C + c0;
+  if constexpr (VEC == 8) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) w |= (uint64_t)am[c] << (8 * c);
+    *reinterpret_cast<uint64_t*>(ip) = w;
+  } else {
+    uint32_t w = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) w |= (uint32_t)am[c] << (8 * c);
+    *reinterpret_cast<uint32_t*>(ip) = w;
+  }
+}
+
+template <typename T, int K, int S>
+__global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_fixed_kernel(const T* __restrict__ dy,
+                                                                       const uint8_t* __restrict__ idx,
+                                                                       T* __restrict__ dx, PoolGeo g,
+                                                                       int row_len) {
+  constexpr int VEC = Vec16<T>::N;
+  constexpr int MW = (K + S - 1) / S;  // windows containing a pixel, per dim
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= row_len) return;
+  const int row = blockIdx.x;
+  const int n = row / g.H, ih = row - n * g.H;
+  const int iw = j / g.cv, cvi = j - iw * g.cv;
+  const int c0 = cvi * VEC;
+  const int oh_hi = (ih + g.p) / S, ow_hi = (iw + g.p) / S;
+  const int64_t nbase = (int64_t)n * g.Ho * g.Wo * g.C + c0;
+  using IdxW = typename std::conditional<VEC == 8, uint64_t, uint32_t>::type;
+  IdxW w[MW][MW];
+  float v[MW][MW][VEC];
+  bool ok[MW][MW];
+#pragma unroll
+  for (int t = 0; t < MW; ++t) {
+    const int oh = oh_hi - t;
+    const int a = ih - (oh * S - g.p);
+    const bool okh = oh >= 0 && oh < g.Ho && a >= 0 && a < K;
+    const int ohc = min(max(oh, 0), g.Ho - 1);
+#pragma unroll
+    for (int u = 0; u < MW; ++u) {
+      const int ow = ow_hi - u;
+      const int b = iw - (ow * S - g.p);
+      ok[t][u] = okh && ow >= 0 && ow < g.Wo && b >= 0 && b < K;
+      const int owc = min(max(ow, 0), g.Wo - 1);
+      const int64_t o = nbase + ((int64_t)ohc * g.Wo + owc) * g.C;
+      w[t][u] = *reinterpret_cast<const IdxW*>(idx + o);
+      Vec16<T>::load(dy + o, v[t][u]);
+    }
+  }
+  float acc[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+#pragma unroll
+  for (int t = 0; t < MW; ++t) {
+    const int a = ih - ((oh_hi - t) * S - g.p);
+#pragma unroll
+    for (int u = 0; u < MW; ++u) {
+      const int b = iw - ((ow_hi - u) * S - g.p);
+      const uint8_t tap = (uint8_t)(a * K + b);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c)
+        if (ok[t][u] && (uint8_t)(w[t][u] >> (8 * c)) == tap) acc[c] += v[t][u][c];
+    }
+  }
+  Vec16<T>::store(dx + ((int64_t)row * g.W + iw) * g.C + c0, acc);
+}
+
 PoolGeo make_geo(const at::Tensor& x, int64_t k, int64_t s, int64_t p, int vec) {
   PoolGeo g;
   g.N = (int)x.size(0); g.C = (int)x.size(1); g.H = (int)x.size(2); g.W = (int)x.size(3);
@@ -125,6 +246,16 @@ PoolGeo make_geo(const at::Tensor& x, int64_t k, int64_t s, int64_t p, int vec) 
   g.Wo = (g.W + 2 * g.p - g.k) / g.s + 1;
   g.cv = g.C / vec;
   return g;
+}
+
+// DMP_POOL_GENERIC=1 routes every geometry through the runtime-k kernels
+// (A/B timing, tools/pool_bench.py).
+bool fixed_geometry_disabled() {
+  static const bool off = [] {
+    const char* e = std::getenv("DMP_POOL_GENERIC");
+    return e != nullptr && e[0] == '1';
+  }();
+  return off;
 }
 
 void check_x(const at::Tensor& x, const char* name) {
@@ -147,17 +278,25 @@ std::vector<at::Tensor> maxpool2d_forward(const at::Tensor& x, int64_t k, int64_
   TORCH_CHECK(g.Ho > 0 && g.Wo > 0, "pool output is empty");
   auto y = at::empty({g.N, g.C, g.Ho, g.Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto idx = at::empty({(int64_t)g.N * g.Ho * g.Wo * g.C}, x.options().dtype(at::kByte));
-  const int64_t total = (int64_t)g.N * g.Ho * g.Wo * g.cv;
-  if (total == 0) return {y, idx};
+  const int row_len = g.Wo * g.cv;
+  if ((int64_t)g.N * g.Ho * row_len == 0) return {y, idx};
   auto stream = at::hip::getCurrentHIPStream();
-  const unsigned blocks = (unsigned)((total + 255) / 256);
-  if (x.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<__bf16>, dim3(blocks), dim3(256), 0, stream,
+  const dim3 blocks((unsigned)(g.N * g.Ho), (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads));
+  const bool fixed = k == 3 && s == 2 && !fixed_geometry_disabled();
+  if (fixed && x.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL((maxpool_fwd_fixed_kernel<__bf16, 3, 2>), blocks, dim3(kPoolThreads), 0, stream,
                        reinterpret_cast<const __bf16*>(x.data_ptr()), reinterpret_cast<__bf16*>(y.data_ptr()),
-                       idx.data_ptr<uint8_t>(), g, total);
+                       idx.data_ptr<uint8_t>(), g, row_len);
+  else if (fixed)
+    hipLaunchKernelGGL((maxpool_fwd_fixed_kernel<float, 3, 2>), blocks, dim3(kPoolThreads), 0, stream,
+                       x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(), g, row_len);
+  else if (x.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<__bf16>, blocks, dim3(kPoolThreads), 0, stream,
+                       reinterpret_cast<const __bf16*>(x.data_ptr()), reinterpret_cast<__bf16*>(y.data_ptr()),
+                       idx.data_ptr<uint8_t>(), g, row_len);
   else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(blocks), dim3(256), 0, stream,
-                       x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(), g, total);
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, blocks, dim3(kPoolThreads), 0, stream,
+                       x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(), g, row_len);
   return {y, idx};
 }
 
@@ -174,17 +313,25 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
               "dy does not match the pool geometry");
   TORCH_CHECK(idx.numel() == dy.numel() && idx.scalar_type() == at::kByte, "bad argmax tensor");
   auto dx = at::empty({g.N, g.C, g.H, g.W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int64_t total = (int64_t)g.N * g.H * g.W * g.cv;
-  if (total == 0) return dx;
+  const int row_len = g.W * g.cv;
+  if ((int64_t)g.N * g.H * row_len == 0) return dx;
   auto stream = at::hip::getCurrentHIPStream();
-  const unsigned blocks = (unsigned)((total + 255) / 256);
-  if (dy.scalar_type() == at::kBFloat16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<__bf16>, dim3(blocks), dim3(256), 0, stream,
+  const dim3 blocks((unsigned)(g.N * g.H), (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads));
+  const bool fixed = k == 3 && s == 2 && !fixed_geometry_disabled();
+  if (fixed && dy.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL((maxpool_bwd_fixed_kernel<__bf16, 3, 2>), blocks, dim3(kPoolThreads), 0, stream,
                        reinterpret_cast<const __bf16*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
-                       reinterpret_cast<__bf16*>(dx.data_ptr()), g, total);
+                       reinterpret_cast<__bf16*>(dx.data_ptr()), g, row_len);
+  else if (fixed)
+    hipLaunchKernelGGL((maxpool_bwd_fixed_kernel<float, 3, 2>), blocks, dim3(kPoolThreads), 0, stream,
+                       dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), g, row_len);
+  else if (dy.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<__bf16>, blocks, dim3(kPoolThreads), 0, stream,
+                       reinterpret_cast<const __bf16*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                       reinterpret_cast<__bf16*>(dx.data_ptr()), g, row_len);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(blocks), dim3(256), 0, stream,
-                       dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), g, total);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, blocks, dim3(kPoolThreads), 0, stream,
+                       dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), g, row_len);
   return dx;
 }
 

@@ -37,3 +37,22 @@ def test_maxpool_ties_first_wins():
     max_pool2d(xi, 2, 2, 0).sum().backward()
     F.max_pool2d(xr, 2, 2, 0).sum().backward()
     torch.testing.assert_close(xi.grad, xr.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_maxpool_k3s2_fixed_path_ties_and_borders(dtype):
+    """The k=3/s=2 fast path loads clamped taps unconditionally: all-equal
+    inputs (every window a tie) and odd sizes check the masking at the borders
+    and PyTorch's first-maximum tie-breaking."""
+    x = torch.zeros(2, 16, 7, 9, device="cuda", dtype=dtype).contiguous(memory_format=torch.channels_last)
+    x[1, :, 3:, :4] = 1.0
+    xi = x.detach().requires_grad_()
+    xr = x.detach().float().requires_grad_()
+    y = max_pool2d(xi, 3, 2, 1)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    torch.testing.assert_close(y.float(), yr)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-6
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol, rtol=tol)
