@@ -101,6 +101,7 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
 bool layernorm_supported(int64_t D);
 // maxpool.hip
 std::vector<at::Tensor> maxpool2d_forward(const at::Tensor& x, int64_t k, int64_t s, int64_t p);
+at::Tensor global_avgpool_backward(const at::Tensor& g, int64_t H, int64_t W);
 at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64_t H, int64_t W,
                               int64_t k, int64_t s, int64_t p);
 // coalesced.hip
@@ -187,6 +188,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // ---- NHWC max pooling with byte argmax ----
   m.def("maxpool2d_forward", &dmp::maxpool2d_forward);
   m.def("maxpool2d_backward", &dmp::maxpool2d_backward);
+  m.def("global_avgpool_backward", &dmp::global_avgpool_backward);
 
   // ---- depthwise 3x3 (NHWC) ----
   m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),

@@ -238,6 +238,26 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_fixed_kernel(const T
   Vec16<T>::store(dx + ((int64_t)row * g.W + iw) * g.C + c0, acc);
 }
 
+// Global average pool backward, channels-last: dx[n, hw, c] = g[n, c] / HW.
+// PyTorch returns an expanded gradient here that the next backward
+// materialises with a strided copy (~1.3 TB/s, profiles finding 13); this is
+// one 16-B vector store per lane, g read from L2.
+template <typename T>
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const T* __restrict__ g, T* __restrict__ dx,
+                                                      int HW, int cv, float inv, int64_t total) {
+  constexpr int VEC = Vec16<T>::N;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t row = i / cv;               // n * HW + hw
+  const int cvi = (int)(i - row * cv);
+  const int n = (int)(row / HW);
+  float v[VEC];
+  Vec16<T>::load(g + ((int64_t)n * cv + cvi) * VEC, v);
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) v[j] *= inv;
+  Vec16<T>::store(dx + i * VEC, v);
+}
+
 PoolGeo make_geo(const at::Tensor& x, int64_t k, int64_t s, int64_t p, int vec) {
   PoolGeo g;
   g.N = (int)x.size(0); g.C = (int)x.size(1); g.H = (int)x.size(2); g.W = (int)x.size(3);
@@ -332,6 +352,28 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<float>, blocks, dim3(kPoolThreads), 0, stream,
                        dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), g, row_len);
+  return dx;
+}
+
+at::Tensor global_avgpool_backward(const at::Tensor& g, int64_t H, int64_t W) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous(), "g must be a contiguous [N, C] GPU tensor");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat, "g must be bf16 or fp32");
+  const int vec = g.scalar_type() == at::kBFloat16 ? 8 : 4;
+  const int64_t N = g.size(0), C = g.size(1);
+  TORCH_CHECK(C % vec == 0 && H > 0 && W > 0, "channels must be a multiple of ", vec);
+  auto dx = at::empty({N, C, H, W}, g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t total = N * H * W * (C / vec);
+  if (total == 0) return dx;
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  const float inv = 1.f / (float)(H * W);
+  auto stream = at::hip::getCurrentHIPStream();
+  if (g.scalar_type() == at::kBFloat16)
+    hipLaunchKernelGGL(gap_bwd_kernel<__bf16>, dim3(blocks), dim3(256), 0, stream,
+                       reinterpret_cast<const __bf16*>(g.data_ptr()), reinterpret_cast<__bf16*>(dx.data_ptr()),
+                       (int)(H * W), (int)(C / vec), inv, total);
+  else
+    hipLaunchKernelGGL(gap_bwd_kernel<float>, dim3(blocks), dim3(256), 0, stream, g.data_ptr<float>(),
+                       dx.data_ptr<float>(), (int)(H * W), (int)(C / vec), inv, total);
   return dx;
 }
 

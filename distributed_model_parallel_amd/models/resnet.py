@@ -22,7 +22,7 @@ from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, grad_tap
-from ..ops.pool import MaxPool2d
+from ..ops.pool import MaxPool2d, global_avg_pool
 
 
 # bn2 -> conv3 prologue fusion (ops/fused.py bn_relu_conv1x1).  Off by default:
@@ -143,7 +143,7 @@ class ResNet(nn.Module):
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
         x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        return torch.flatten(self.avgpool(x), 1)
+        return global_avg_pool(x)  # channels-last broadcast backward (ops/pool.py)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return self.fc(self.forward_features(x))

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0}
+_STATS = {"native": 0, "torch": 0, "native_gap": 0}
 
 
 def _pair1(v) -> int:
@@ -53,6 +53,32 @@ def max_pool2d(x: torch.Tensor, kernel_size, stride=None, padding=0) -> torch.Te
         return _MaxPoolFn.apply(x, k, s, p)
     _STATS["torch"] += 1
     return F.max_pool2d(x, k, s, p)
+
+
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.hw = (x.shape[2], x.shape[3])
+        return x.mean((2, 3))
+
+    @staticmethod
+    def backward(ctx, g):
+        C = _native.require("global average pool backward")
+        return C.global_avgpool_backward(g.contiguous(), *ctx.hw)
+
+
+def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
+    """``adaptive_avg_pool2d(x, 1).flatten(1)`` for channels-last activations.
+
+    The backward writes the broadcast gradient channels-last in one vectorised
+    kernel instead of returning an expanded view that the preceding layer's
+    backward copies (profiles/README.md finding 13)."""
+    vec = 8 if x.dtype == torch.bfloat16 else 4
+    if (_native.gpu_path(x) and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)
+            and x.shape[1] % vec == 0 and x.is_contiguous(memory_format=torch.channels_last)):
+        _STATS["native_gap"] += 1
+        return _GlobalAvgPoolFn.apply(x)
+    return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
 
 
 class MaxPool2d(nn.MaxPool2d):

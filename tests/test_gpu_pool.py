@@ -56,3 +56,23 @@ def test_maxpool_k3s2_fixed_path_ties_and_borders(dtype):
     yr.backward(g.to(dtype).float())
     tol = 1e-2 if dtype == torch.bfloat16 else 1e-6
     torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_global_avg_pool_matches_torch(dtype):
+    from distributed_model_parallel_amd.ops.pool import global_avg_pool
+    torch.manual_seed(0)
+    x = torch.randn(4, 64, 7, 5, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    xi = x.detach().requires_grad_()
+    xr = x.detach().float().requires_grad_()
+    n0 = _STATS["native_gap"]
+    y = global_avg_pool(xi)
+    assert _STATS["native_gap"] == n0 + 1
+    yr = torch.flatten(F.adaptive_avg_pool2d(xr, 1), 1)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    assert xi.grad.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol, rtol=tol)
