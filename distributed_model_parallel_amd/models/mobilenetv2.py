@@ -28,6 +28,7 @@ from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.depthwise import DepthwiseConv2d
 from ..ops.fused import conv_bn
+from ..ops.pool import global_avg_pool
 
 # (expansion t, output channels c, repeats n, first stride s) -- CIFAR strides.
 CIFAR_SETTINGS: Tuple[Tuple[int, int, int, int], ...] = (
@@ -104,6 +105,8 @@ class HeadPool(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.apply_relu:
             x = F.relu(x)
+        if x.shape[2] == self.pool and x.shape[3] == self.pool:
+            return global_avg_pool(x)  # whole-map pool: channels-last broadcast backward
         return torch.flatten(F.avg_pool2d(x, self.pool), 1)
 
 
