@@ -96,14 +96,28 @@ class FlatSGD(torch.optim.Optimizer):
                 "layout": self.ddp.param_layout()}
 
     def load_state_dict(self, sd):
+        """Restore momentum / master weights parameter by parameter.
+
+        The saved flats follow the bucket layout of the run that wrote them
+        (usually the post-rebuild autograd-ready order), while a fresh DDP
+        starts in registration order -- so every parameter's slice is moved
+        from ``sd['layout']`` to the current layout, never copied flat-to-flat.
+        """
         self._ensure_state()
         self._steps = sd["steps"]
         for g, sg in zip(self.param_groups, sd["param_groups"]):
             g.update(sg)
-        for st, sst in zip(self._flat_state, sd["flat_state"]):
-            for k, v in sst.items():
-                if k in st:
-                    st[k].copy_(v)
+        dev = self._flat_state[0]["momentum"].device if self._flat_state else None
+        saved = [{k: v.to(dev) for k, v in sst.items()} for sst in sd["flat_state"]]
+        old_layout = [tuple(int(v) for v in e) for e in sd["layout"]]
+        if len(old_layout) != len(self.ddp._params):
+            raise ValueError("FlatSGD.load_state_dict: checkpoint has %d parameters, model has %d"
+                             % (len(old_layout), len(self.ddp._params)))
+        self._remap(saved, self._flat_state, old_layout, self.ddp.param_layout())
+        with torch.no_grad():
+            for st in self._flat_state:
+                if "master" in st:  # working weights follow the restored fp32 master
+                    st["param"].copy_(st["master"].to(st["param"].dtype))
 
 
 def _sgd_reference(master: Optional[torch.Tensor], mom: torch.Tensor, grad: torch.Tensor,

@@ -6,8 +6,9 @@ accuracy improves, resume with ``-r``; keys carry the DataParallel
 ``module.`` prefix; no optimizer/scheduler/RNG state; the pipeline script
 saves nothing.
 
-Here: rank-0 atomic save (temp file + rename) of the UNWRAPPED model state
-(no ``module.`` prefix; loading accepts either), optimizer, scheduler,
+Here: rank-0 atomic save (temp file + rename) of the model state
+(``module.``-prefixed when the model is wrapped, as in the reference; loading
+accepts either) with ``weights_only=True``-safe contents, optimizer, scheduler,
 epoch, best accuracy and RNG states; per-stage shards for pipeline runs;
 ``load_checkpoint`` maps onto the local device and (under DDP) re-broadcasts
 from rank 0 so every replica resumes bit-identical.
@@ -37,7 +38,13 @@ def _strip_prefix(sd: Dict[str, Any], prefix: str = "module.") -> Dict[str, Any]
 
 
 def rng_state() -> Dict[str, Any]:
-    st = {"python": random.getstate(), "numpy": np.random.get_state(), "torch": torch.get_rng_state()}
+    """RNG states as tensors / ints / tuples only, so the file loads with
+    ``torch.load(weights_only=True)`` (no pickled numpy objects)."""
+    name, keys, pos, has_gauss, gauss = np.random.get_state()
+    st = {"python": random.getstate(),
+          "numpy": [name, torch.from_numpy(np.asarray(keys, dtype=np.int64)), int(pos),
+                    int(has_gauss), float(gauss)],
+          "torch": torch.get_rng_state()}
     if torch.cuda.is_available():
         st["cuda"] = torch.cuda.get_rng_state_all()
     return st
@@ -45,7 +52,8 @@ def rng_state() -> Dict[str, Any]:
 
 def set_rng_state(st: Dict[str, Any]) -> None:
     random.setstate(st["python"])
-    np.random.set_state(st["numpy"])
+    name, keys, pos, has_gauss, gauss = st["numpy"]
+    np.random.set_state((name, keys.numpy().astype(np.uint32), pos, has_gauss, gauss))
     torch.set_rng_state(st["torch"])
     if "cuda" in st and torch.cuda.is_available():
         torch.cuda.set_rng_state_all(st["cuda"])
@@ -57,13 +65,24 @@ def _rank() -> int:
 
 def save_checkpoint(path: str, model: nn.Module, optimizer=None, scheduler=None, epoch: int = 0,
                     best_acc: float = 0.0, extra: Optional[Dict[str, Any]] = None,
-                    all_ranks: bool = False) -> Optional[str]:
-    """Write a checkpoint (rank 0 only unless `all_ranks`, e.g. pipeline shards)."""
+                    all_ranks: bool = False, module_prefix: Optional[bool] = None) -> Optional[str]:
+    """Write a checkpoint (rank 0 only unless `all_ranks`, e.g. pipeline shards).
+
+    ``module_prefix`` (default: whether `model` is a DP/DDP wrapper) writes the
+    ``net`` keys with the ``module.`` prefix the reference's DataParallel
+    checkpoints carry (``data_parallel.py:143-155``), so its
+    ``net.load_state_dict(checkpoint['net'])`` accepts our files too.
+    """
     if not all_ranks and _rank() != 0:
         return None
     os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+    net = unwrap(model).state_dict()
+    if module_prefix is None:
+        module_prefix = unwrap(model) is not model
+    if module_prefix:
+        net = {"module." + k: v for k, v in net.items()}
     state = {
-        "net": unwrap(model).state_dict(),
+        "net": net,
         "acc": best_acc,
         "epoch": epoch,
         "optimizer": optimizer.state_dict() if optimizer is not None else None,
@@ -83,8 +102,8 @@ def load_checkpoint(path: str, model: nn.Module, optimizer=None, scheduler=None,
     ``{'net','acc','epoch'}`` dict) into `model` / `optimizer` / `scheduler`."""
     if map_location is None:
         map_location = "cpu"
-    # our own files; weights_only=False is needed for RNG/optimizer state objects
-    state = torch.load(path, map_location=map_location, weights_only=False)
+    # tensors / containers / numbers only: nothing in the file is executed
+    state = torch.load(path, map_location=map_location, weights_only=True)
     target = unwrap(model)
     target.load_state_dict(_strip_prefix(state["net"]), strict=strict)
     if optimizer is not None and state.get("optimizer") is not None:

@@ -150,3 +150,61 @@ def test_bucket_assignment_caps_and_order():
     assert b[0] == [9]
     assert sorted(i for bb in b for i in bb) == list(range(10))
     assert all(len(bb) <= 3 for bb in b)
+
+
+class _HeadFirst(nn.Module):
+    """Registration order (head, body) differs from the autograd-ready order, so
+    the first-backward bucket rebuild really changes the flat layout."""
+
+    def __init__(self):
+        super().__init__()
+        self.head = nn.Linear(32, 5)
+        self.body = nn.Sequential(nn.Linear(12, 32), nn.ReLU(), nn.Linear(32, 32))
+
+    def forward(self, x):
+        return self.head(F.relu(self.body(x)))
+
+
+def _resume_worker(rank, world, path):
+    from distributed_model_parallel_amd.ops.optim import FlatSGD
+    from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
+
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(8, 12, generator=g) for _ in range(4)]
+    ys = [torch.randint(0, 5, (8,), generator=g) for _ in range(4)]
+
+    def make():
+        torch.manual_seed(0)
+        m = _HeadFirst()
+        ddp = DistributedDataParallel(m, bucket_cap_mb=0.002, first_bucket_mb=0.0005,
+                                      flat_parameters=True)
+        return m, ddp, FlatSGD(ddp, lr=0.1, momentum=0.9, weight_decay=1e-4)
+
+    def run(ddp, opt, idx):
+        for i in idx:
+            opt.zero_grad()
+            F.cross_entropy(ddp(xs[i]), ys[i]).backward()
+            opt.step()
+
+    m, ddp, opt = make()
+    run(ddp, opt, [0, 1])
+    layout_trained = list(ddp.param_layout())
+    torch.save({"net": m.state_dict(), "opt": opt.state_dict()}, path)
+    run(ddp, opt, [2, 3])
+    want = {k: v.clone() for k, v in m.state_dict().items()}
+
+    m2, ddp2, opt2 = make()
+    layout_fresh = list(ddp2.param_layout())
+    ck = torch.load(path, weights_only=True)
+    m2.load_state_dict(ck["net"])
+    opt2.load_state_dict(ck["opt"])
+    run(ddp2, opt2, [2, 3])
+    got = {k: v.clone() for k, v in m2.state_dict().items()}
+    return {"changed": layout_trained != layout_fresh, "want": want, "got": got}
+
+
+def test_flat_sgd_resume_across_bucket_rebuild(tmp_path):
+    res = run_world(_resume_worker, 1, str(tmp_path / "ck.pt"))[0]
+    assert res["changed"], "test must exercise a layout change between save and resume"
+    for k, v in res["want"].items():
+        torch.testing.assert_close(res["got"][k], v, atol=1e-6, rtol=1e-6, msg=k)

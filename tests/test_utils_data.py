@@ -99,6 +99,9 @@ def test_checkpoint_roundtrip(tmp_path):
     for a, b in zip(m.state_dict().values(), m2.state_dict().values()):
         torch.testing.assert_close(a, b)
     assert s2.epoch == 1
+    # safe loader reads it; wrapped models keep the reference's module. prefix
+    raw = torch.load(path, weights_only=True)
+    assert all(k.startswith("module.") for k in raw["net"])
     # reference-format dict with module. prefix loads too
     ref = {"net": {"module." + k: v for k, v in m.state_dict().items()}, "acc": 1.0, "epoch": 7}
     torch.save(ref, tmp_path / "ref.pth")
