@@ -239,7 +239,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<dmp::ReduceBackend, std::shared_ptr<dmp::ReduceBackend>>(m, "ReduceBackend");
   py::class_<dmp::RcclReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::RcclReduceBackend>>(
       m, "RcclReduceBackend")
-      .def(py::init<std::shared_ptr<dmp::RcclComm>>());
+      .def(py::init<std::shared_ptr<dmp::RcclComm>, double, int64_t>(), py::arg("comm"),
+           py::arg("postscale") = 1.0, py::arg("debug_delay_cycles") = 0);
   py::class_<dmp::NullReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::NullReduceBackend>>(
       m, "NullReduceBackend")
       .def(py::init<>());

@@ -1,5 +1,9 @@
 #include "reducer.h"
 
+#include <ATen/hip/Sleep.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/hip/HIPGuard.h>
+
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
 #include <torch/csrc/autograd/variable.h>
@@ -21,6 +25,17 @@ using torch::autograd::variable_list;
 // ---------------------------------------------------------------------------
 // Python comm-hook backend
 // ---------------------------------------------------------------------------
+void RcclReduceBackend::launch(int64_t, at::Tensor& flat) {
+  comm_->all_reduce(flat, "avg");
+  if (delay_ == 0 && postscale_ == 1.0) return;
+  // the tail runs on the stream the collective used, so wait_all() covers it
+  c10::hip::HIPStreamGuard guard(comm_->is_inline()
+                                     ? at::hip::getCurrentHIPStream(flat.device().index())
+                                     : comm_->torch_stream());
+  if (delay_ > 0) at::cuda::sleep(delay_);
+  if (postscale_ != 1.0) flat.mul_(postscale_);
+}
+
 PyReduceBackend::~PyReduceBackend() {
   py::gil_scoped_acquire gil;
   pending_.clear();

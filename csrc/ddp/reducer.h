@@ -46,12 +46,21 @@ class ReduceBackend {
 
 class RcclReduceBackend : public ReduceBackend {
  public:
-  explicit RcclReduceBackend(std::shared_ptr<RcclComm> comm) : comm_(std::move(comm)) {}
-  void launch(int64_t, at::Tensor& flat) override { comm_->all_reduce(flat, "avg"); }
+  // postscale: multiply the averaged bucket by this factor on the comm stream
+  // (folds a loss-scale / accumulation divisor into the collective's tail).
+  // debug_delay_cycles: spin the comm stream before the scale -- a test knob
+  // that widens any missing comm-stream -> compute-stream ordering into a
+  // visible wrong result (tests/test_gpu_ddp.py).
+  explicit RcclReduceBackend(std::shared_ptr<RcclComm> comm, double postscale = 1.0,
+                             int64_t debug_delay_cycles = 0)
+      : comm_(std::move(comm)), postscale_(postscale), delay_(debug_delay_cycles) {}
+  void launch(int64_t, at::Tensor& flat) override;
   void wait_all() override { comm_->wait(); }
 
  private:
   std::shared_ptr<RcclComm> comm_;
+  double postscale_;
+  int64_t delay_;
 };
 
 // world_size == 1: the average over one rank is the identity, nothing to move.

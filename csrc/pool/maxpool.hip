@@ -45,11 +45,14 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_kernel(const T* __re
   const int ow = j / g.cv, cvi = j - ow * g.cv;
   const int64_t pix = (int64_t)row * g.Wo + ow;
   const int c0 = cvi * VEC;
+  const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
+  // argmax starts at the first IN-BOUNDS tap (PyTorch semantics): an all -inf
+  // window at a border must still route its gradient to a real input pixel
+  const uint8_t tap0 = (uint8_t)(max(0, -h0) * g.k + max(0, -w0));
   float m[VEC];
   uint8_t am[VEC];
 #pragma unroll
-  for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; am[j] = 0; }
-  const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
+  for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; am[j] = tap0; }
   for (int a = 0; a < g.k; ++a) {
     const int ih = h0 + a;
     if (ih < 0 || ih >= g.H) continue;
@@ -151,10 +154,11 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_fwd_fixed_kernel(const T
       Vec16<T>::load(xn + ((int64_t)ih * g.W + iw) * g.C, v[a][b]);
     }
   }
+  const uint8_t tap0 = (uint8_t)(max(0, -h0) * K + max(0, -w0));  // first in-bounds tap
   float m[VEC];
   uint8_t am[VEC];
 #pragma unroll
-  for (int c = 0; c < VEC; ++c) { m[c] = -INFINITY; am[c] = 0; }
+  for (int c = 0; c < VEC; ++c) { m[c] = -INFINITY; am[c] = tap0; }
 #pragma unroll
   for (int a = 0; a < K; ++a) {
     const bool ha = (unsigned)(h0 + a) < (unsigned)g.H;

@@ -188,5 +188,8 @@ def default_communicator(device: Optional[torch.device] = None) -> Communicator:
 
 
 def reset_default_communicator() -> None:
+    """Forget the process-wide communicators (default + SyncBN's own)."""
     global _default
     _default = None
+    from ..parallel.sync_batchnorm import reset_syncbn_communicators
+    reset_syncbn_communicators()

@@ -120,6 +120,120 @@ class FlatSGD(torch.optim.Optimizer):
                     st["param"].copy_(st["master"].to(st["param"].dtype))
 
 
+class MasterSGD(torch.optim.Optimizer):
+    """torch.optim.SGD semantics with fp32 master weights for ANY parameter list.
+
+    Used where there is no DDP flat layout to borrow: single-process
+    DataParallel (its parameters live on ``device_ids[0]``), pipeline stages
+    and plain single-GPU training.  At construction the parameters of each
+    dtype/device group are moved into one flat buffer (parameters become
+    views, channels-last strides preserved) and their ``.grad`` is pre-set to
+    views of a flat gradient buffer, so autograd accumulates in place and the
+    update is ONE ``sgd_flat_step`` launch per group, fp32 master + fp32
+    momentum for bf16 groups (bf16 SGD would drop every update below one
+    bf16 ulp).  Same kernel and numerics as :class:`FlatSGD` under DDP, so DP,
+    pipeline and DDP train at equal precision.
+    """
+
+    def __init__(self, params, lr: float, momentum: float = 0.0, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, master_weights: bool = True):
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        params = [p for p in params if p.requires_grad]
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
+                        nesterov=nesterov)
+        super().__init__(params, defaults)
+        self.master_weights = master_weights
+        self._steps = 0
+        self._groups = []
+        by_key = {}
+        for p in params:
+            by_key.setdefault((p.dtype, p.device), []).append(p)
+        with torch.no_grad():
+            for (dt, dev), ps in by_key.items():
+                offs, o = [], 0
+                for p in ps:
+                    offs.append(o)
+                    o += (p.numel() + 7) // 8 * 8  # kernel works in 8-element vectors
+                pflat = torch.zeros(o, dtype=dt, device=dev)
+                gflat = torch.zeros(o, dtype=dt, device=dev)
+                gviews = []
+                for p, off in zip(ps, offs):
+                    view = pflat.as_strided(p.shape, p.stride(), off)
+                    view.copy_(p.detach())
+                    p.data = view
+                    gv = gflat.as_strided(p.shape, p.stride(), off)
+                    p.grad = gv
+                    gviews.append(gv)
+                st = {"params": ps, "offs": offs, "param": pflat, "grad": gflat, "gviews": gviews,
+                      "momentum": torch.zeros(o, dtype=torch.float32, device=dev)}
+                if dt != torch.float32 and master_weights:
+                    st["master"] = pflat.float()
+                self._groups.append(st)
+
+    @torch.no_grad()
+    def _adopt_grads(self, st) -> None:
+        """Grads replaced behind our back (set_to_none, a stolen tensor) go back into the flat."""
+        for p, gv in zip(st["params"], st["gviews"]):
+            g = p.grad
+            if g is gv or (g is not None and g.data_ptr() == gv.data_ptr() and g.stride() == gv.stride()):
+                continue
+            if g is None:
+                gv.zero_()
+            else:
+                gv.copy_(g)
+            p.grad = gv
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        g = self.param_groups[0]
+        first = self._steps == 0
+        for st in self._groups:
+            self._adopt_grads(st)
+            pflat, gflat, master = st["param"], st["grad"], st.get("master")
+            if pflat.is_cuda:
+                _native.require("MasterSGD").sgd_flat_step(
+                    master, st["momentum"], gflat, pflat, float(g["lr"]), float(g["weight_decay"]),
+                    float(g["momentum"]), float(g["dampening"]), bool(g["nesterov"]), 1.0, first)
+            else:
+                _sgd_reference(master, st["momentum"], gflat, pflat, g, first)
+        self._steps += 1
+        return loss
+
+    def zero_grad(self, set_to_none: bool = False):
+        """One fill per group; gradients stay flat views (``set_to_none`` is ignored)."""
+        for st in self._groups:
+            st["grad"].zero_()
+            for p, gv in zip(st["params"], st["gviews"]):
+                if p.grad is not gv:
+                    p.grad = gv
+
+    def state_dict(self):
+        return {"steps": self._steps,
+                "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
+                "numels": [[p.numel() for p in st["params"]] for st in self._groups],
+                "flat_state": [{k: st[k] for k in ("momentum", "master") if k in st}
+                               for st in self._groups]}
+
+    def load_state_dict(self, sd):
+        if sd["numels"] != [[p.numel() for p in st["params"]] for st in self._groups]:
+            raise ValueError("MasterSGD.load_state_dict: parameter layout differs from the checkpoint")
+        self._steps = sd["steps"]
+        for g, sg in zip(self.param_groups, sd["param_groups"]):
+            g.update(sg)
+        with torch.no_grad():
+            for st, sst in zip(self._groups, sd["flat_state"]):
+                for k, v in sst.items():
+                    if k in st:
+                        st[k].copy_(v)
+                if "master" in st:
+                    st["param"].copy_(st["master"].to(st["param"].dtype))
+
+
 def _sgd_reference(master: Optional[torch.Tensor], mom: torch.Tensor, grad: torch.Tensor,
                    param: torch.Tensor, g: dict, first: bool) -> None:
     """PyTorch implementation of the flat kernel (CPU path / test oracle)."""

@@ -18,8 +18,26 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..comm.rccl import Communicator, default_communicator
+from ..comm.rccl import Communicator
 from ..ops.batchnorm import BatchNormAct2d
+
+# One communicator per (device, group) shared by every SyncBatchNorm layer and
+# never by DDP: the moment all-reduces are enqueued on the COMPUTE stream, the
+# DDP bucket all-reduces on the reducer's side stream -- two streams driving one
+# ncclComm would serialise the ~100 tiny per-step SyncBN collectives behind
+# (and interleave them with) the 25 MB bucket collectives.
+_COMMS = {}
+
+
+def syncbn_communicator(device: torch.device, group: Optional[dist.ProcessGroup] = None) -> Communicator:
+    key = (str(device), id(group) if group is not None else None)
+    if key not in _COMMS:
+        _COMMS[key] = Communicator(device, group)
+    return _COMMS[key]
+
+
+def reset_syncbn_communicators() -> None:
+    _COMMS.clear()
 
 
 class SyncBatchNorm(BatchNormAct2d):
@@ -34,10 +52,7 @@ class SyncBatchNorm(BatchNormAct2d):
 
     def _communicator(self, device: torch.device) -> Communicator:
         if self._comm is None:
-            if self.process_group is None:
-                self._comm = default_communicator(device if device.type == "cuda" else None)
-            else:
-                self._comm = Communicator(device, self.process_group)
+            self._comm = syncbn_communicator(device, self.process_group)
         return self._comm
 
     def _moment_reducers(self):

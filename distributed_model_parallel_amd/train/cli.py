@@ -89,7 +89,7 @@ def _num_classes(args) -> int:
 def run_data_parallel(args, env) -> None:
     from ..data import prepare_dataloaders
     from ..models import build_model
-    from ..ops.optim import FlatSGD
+    from ..ops.optim import FlatSGD, MasterSGD
     from ..parallel.data_parallel import DataParallel
     from ..parallel.distributed import DistributedDataParallel
     from ..parallel.sync_batchnorm import SyncBatchNorm
@@ -113,9 +113,10 @@ def run_data_parallel(args, env) -> None:
         net = DistributedDataParallel(model, bucket_cap_mb=args.bucket_cap_mb, flat_parameters=True)
         opt = FlatSGD(net, lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
     else:
+        # fp32 master weights for bf16 models: same update as DDP's FlatSGD
+        opt = MasterSGD(model.parameters(), lr=args.lr, momentum=args.momentum,
+                        weight_decay=args.weight_decay)
         net = DataParallel(model) if args.parallel == "dp" else model
-        opt = torch.optim.SGD(model.parameters(), lr=args.lr, momentum=args.momentum,
-                              weight_decay=args.weight_decay)
     sched = build_schedule(opt, args.epochs, args.warmup_epochs)
     train_ds, val_ds = _datasets(args)
     sampler, train_loader, val_loader = prepare_dataloaders(
@@ -187,6 +188,7 @@ def run_pipeline(args, env) -> None:
     from ..comm.rccl import Communicator
     from ..data import prepare_dataloaders
     from ..models import INPUT_SHAPES, build_model
+    from ..ops.optim import MasterSGD
     from ..parallel.pipeline import Pipeline
     from ..utils.checkpoint import save_checkpoint, stage_checkpoint_path
     from ..utils.logging import MetricsLogger
@@ -200,8 +202,8 @@ def run_pipeline(args, env) -> None:
     pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=args.micro_batches,
                     schedule=args.schedule, dtype=parse_dtype(args.dtype),
                     channels_last=args.channels_last, partition=args.partition)
-    opt = torch.optim.SGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
-                          weight_decay=args.weight_decay)
+    opt = MasterSGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
+                    weight_decay=args.weight_decay)
     sched = build_schedule(opt, args.epochs, args.warmup_epochs)
     logger = MetricsLogger(args.log_dir, f"pipe_{args.arch}", env.rank, text_file=f"{args.batch_size}.txt")
     if env.rank == 0:
@@ -228,7 +230,7 @@ def run_pipeline(args, env) -> None:
             tot_d += time.perf_counter() - t
             r = pipe.train_step(x, y)
             opt.step()
-            opt.zero_grad(set_to_none=True)
+            opt.zero_grad()
             if r.loss is not None:
                 loss_s += r.loss
                 acc_s += r.top1

@@ -16,7 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..models import INPUT_SHAPES, build_model
-from ..ops.optim import FlatSGD
+from ..ops.optim import FlatSGD, MasterSGD
 from ..utils.precision import cast_model
 
 
@@ -121,28 +121,29 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
             return loss
     elif cfg.parallel == "dp":
         from ..parallel.data_parallel import DataParallel
+        # fp32 master weights + momentum, one launch per dtype group (same update as DDP's FlatSGD)
+        opt = MasterSGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
+                        weight_decay=cfg.weight_decay)
         wrapped = DataParallel(model, device_ids=list(range(ndp)) if device.type == "cuda" else None)
-        opt = torch.optim.SGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
-                              weight_decay=cfg.weight_decay, foreach=True)
 
         def step() -> torch.Tensor:
             out = wrapped(x)
             loss = F.cross_entropy(out.float(), y)
             loss.backward()
             opt.step()
-            opt.zero_grad(set_to_none=True)
+            opt.zero_grad()
             return loss
     else:
         wrapped = model
-        opt = torch.optim.SGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
-                              weight_decay=cfg.weight_decay, foreach=True)
+        opt = MasterSGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
+                        weight_decay=cfg.weight_decay)
 
         def step() -> torch.Tensor:
             out = model(x)
             loss = F.cross_entropy(out.float(), y)
             loss.backward()
             opt.step()
-            opt.zero_grad(set_to_none=True)
+            opt.zero_grad()
             return loss
 
     return TrainState(cfg, model, wrapped, opt, step, x, y)

@@ -71,3 +71,88 @@ def test_ddp_and_syncbn_rccl_backend_world1():
     assert r.returncode == 0, "subprocess failed (output above)"
     assert "ddp ok" in r.stdout and "syncbn ok" in r.stdout
     assert "rccl on-current-stream ok" in r.stdout
+
+
+ORDER_SCRIPT = r'''
+import os, sys, torch
+import torch.nn.functional as F
+sys.path.insert(0, os.environ["ROOT"])
+from distributed_model_parallel_amd import _native
+from distributed_model_parallel_amd.models import build_model
+from distributed_model_parallel_amd.ops.optim import FlatSGD, MasterSGD
+from distributed_model_parallel_amd.parallel.data_parallel import DataParallel
+from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
+from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed
+from distributed_model_parallel_amd.utils.precision import cast_model
+env = init_distributed()
+dev = env.device
+C = _native.require("test")
+g = torch.Generator().manual_seed(3)
+x = torch.randn(8, 3, 64, 64, generator=g).to(dev, torch.bfloat16).contiguous(memory_format=torch.channels_last)
+y = torch.randint(0, 1000, (8,), generator=g).to(dev)
+
+def model():
+    torch.manual_seed(0)
+    m = build_model("resnet18").to(dev).to(memory_format=torch.channels_last)
+    cast_model(m, torch.bfloat16)
+    return m
+
+def masters_ddp(m, ddp, opt):
+    flats = [st.get("master", st["param"]).float() for st in opt._flat_state]
+    return [flats[gi].narrow(0, off, p.numel()).clone() for p, (gi, off) in zip(ddp._params, ddp.param_layout())]
+
+def masters_sgd(opt):
+    out = {}
+    for st in opt._groups:
+        for p, off in zip(st["params"], st["offs"]):
+            out[id(p)] = st.get("master", st["param"]).float().narrow(0, off, p.numel()).clone()
+    return out
+
+def ddp_step(backend=None):
+    m = model()
+    ddp = DistributedDataParallel(m, flat_parameters=True)
+    if backend is not None:
+        ddp.reducer.set_backend(backend(ddp))
+    opt = FlatSGD(ddp, lr=1.0, momentum=0.0, weight_decay=0.0)
+    w0 = masters_ddp(m, ddp, opt)
+    F.cross_entropy(ddp(x).float(), y).backward()
+    opt.step()
+    torch.cuda.synchronize()
+    return [a - b for a, b in zip(masters_ddp(m, ddp, opt), w0)]
+
+# 1) ordering: the comm stream sleeps ~tens of ms, then doubles the averaged
+#    gradient; FlatSGD on the compute stream must see the doubled value.
+base = ddp_step()
+slow = ddp_step(lambda d: C.RcclReduceBackend(d.comm.native, 2.0, 200_000_000))
+worst = max(((s - 2 * b).abs().max() / (b.abs().max() + 1e-12)).item() for s, b in zip(slow, base))
+assert worst < 1e-2, ("optimizer read the gradient before the comm stream finished", worst)
+print("ordering ok", worst)
+
+# 2) precision parity: one bf16 DP step (device_ids=[0]) and one bf16 DDP step
+#    produce the same fp32 master update.
+m = model()
+opt = MasterSGD(m.parameters(), lr=1.0)
+dp = DataParallel(m, device_ids=[0])
+w0 = masters_sgd(opt)
+F.cross_entropy(dp(x).float(), y).backward()
+opt.step()
+torch.cuda.synchronize()
+w1 = masters_sgd(opt)
+dps = [w1[id(p)] - w0[id(p)] for p in m.parameters()]
+worst = max(((a - b).abs().max() / (b.abs().max() + 1e-12)).item() for a, b in zip(dps, base))
+assert worst < 1e-2, ("DP and DDP master updates differ", worst)
+print("dp-ddp parity ok", worst)
+destroy_distributed()
+'''
+
+
+def test_reducer_stream_ordering_and_dp_ddp_precision_parity():
+    env = dict(os.environ, ROOT=ROOT, RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, "-c", ORDER_SCRIPT], env=env, capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode != 0:
+        print(r.stdout[-3000:])
+        print(r.stderr[-6000:])
+    assert r.returncode == 0, "subprocess failed (output above)"
+    assert "ordering ok" in r.stdout and "dp-ddp parity ok" in r.stdout

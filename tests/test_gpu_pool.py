@@ -76,3 +76,15 @@ def test_global_avg_pool_matches_torch(dtype):
     yr.backward(g.to(dtype).float())
     assert xi.grad.is_contiguous(memory_format=torch.channels_last)
     torch.testing.assert_close(xi.grad.float(), xr.grad, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize("k,s,p", [(3, 2, 1), (3, 1, 1)])
+def test_maxpool_all_neg_inf_border_window(k, s, p):
+    # every value -inf: each window's gradient must land on its first in-bounds
+    # pixel (PyTorch), not on a padding tap that the backward can never match
+    x = torch.full((1, 8, 6, 6), float("-inf"), device="cuda").contiguous(memory_format=torch.channels_last)
+    xi = x.detach().requires_grad_()
+    xr = x.detach().requires_grad_()
+    max_pool2d(xi, k, s, p).sum().backward()
+    F.max_pool2d(xr, k, s, p).sum().backward()
+    torch.testing.assert_close(xi.grad, xr.grad)
