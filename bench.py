@@ -13,13 +13,15 @@ forward, fp32 cross-entropy, backward with the native C++ reducer doing
 bucketed RCCL all-reduces (25 MB buckets, ncclAvg) overlapped with backward,
 one fused flat-SGD (momentum 0.9, wd 1e-4) launch per dtype group.
 
-  python bench.py --gpus N --steps K --warmup W
+  python bench.py --gpus N --steps K --warmup W          (spawns N rank processes itself)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Other BASELINE.json configs:
   DP (scatter/replicate/gather, one process): python bench.py --parallel dp --gpus N
   DDP + SyncBatchNorm:                        ... bench.py --parallel syncbn --gpus N
   ViT-B/16 DDP:                               ... bench.py --model vit_b_16   (256 per GPU)
+  MobileNetV2 CIFAR pipeline (reference MP):  python bench.py --parallel pipe --model mobilenetv2
+                                              --gpus 4 --batch-size 512 [--schedule naive|gpipe|1f1b]
   ResNet-18 CPU/gloo plumbing (ws 2):         torchrun --nproc-per-node 2 bench.py --device cpu
                                               --model resnet18 --dtype fp32 --batch-size 8
                                               --steps 2 --warmup 1 --no-channels-last
@@ -32,6 +34,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -49,6 +53,45 @@ from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: 
 # per-GPU batch defaults (measured throughput curves: module docstring, README)
 DEFAULT_BATCH = {"resnet50": 1024, "vit_b_16": 256, "mobilenetv2": 512}
 BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference images/sec figure exists
+# The reference's only throughput numbers (Readme.md:283-292): MobileNetV2 CIFAR
+# time/batch -> images/sec, keyed (parallel, n_gpus, global batch).
+REFERENCE_MNV2 = {("pipe", 4, 512): 512 / 1.616, ("dp", 4, 512): 512 / 0.396,
+                  ("pipe", 2, 256): 256 / 0.772, ("dp", 2, 256): 256 / 0.363}
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Launch n rank processes of this script (one per GPU) like the reference's
+    ``mp.spawn(main_worker, nprocs=world_size)`` (model_parallel.py:160-162).
+
+    Runs BEFORE anything touches the GPU in this parent (it only counts
+    devices), children get the torchrun environment on 127.0.0.1; a failing
+    rank takes the others down.  Returns the worst exit code."""
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), DMP_BENCH_SPAWNED="1")
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # one rank died: the rest would hang in a collective
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main() -> int:
@@ -61,7 +104,12 @@ def main() -> int:
                     help="per-GPU batch (default: %s)" % DEFAULT_BATCH)
     ap.add_argument("--image-size", type=int, default=None, help="default: the model's native size")
     ap.add_argument("--dtype", default="bf16")
-    ap.add_argument("--parallel", default="ddp", choices=["ddp", "syncbn", "dp", "none"])
+    ap.add_argument("--parallel", default="ddp", choices=["ddp", "syncbn", "dp", "pipe", "none"])
+    ap.add_argument("--micro-batches", type=int, default=8, help="--parallel pipe")
+    ap.add_argument("--schedule", default="1f1b", choices=["naive", "gpipe", "1f1b"],
+                    help="--parallel pipe (naive = the reference's one-batch serial ring)")
+    ap.add_argument("--partition", default="balanced", choices=["balanced", "reference"],
+                    help="--parallel pipe stage cut")
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
     ap.add_argument("--no-channels-last", action="store_true")
@@ -88,10 +136,19 @@ def main() -> int:
     if args.batch_size is None:
         args.batch_size = DEFAULT_BATCH.get(args.model, 256)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.parallel != "dp":
+        # no launcher: become one (before any GPU call in this process)
+        if args.device != "cpu" and torch.cuda.device_count() < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but only {torch.cuda.device_count()} GPUs visible")
+        if args.device == "cpu":  # gloo plumbing run: do not oversubscribe the host
+            os.environ.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
+        return spawn_ranks(args.gpus, sys.argv[1:])
+
     use_gpu = None if args.device == "auto" else args.device == "cuda"
     env = init_distributed(use_gpu=use_gpu)
-    if env.world_size != args.gpus and env.is_main:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={env.world_size}", file=sys.stderr)
+    if args.parallel != "dp" and env.world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env.world_size}: the launcher and the "
+                         "flag disagree")
     torch.backends.cudnn.benchmark = bool(args.miopen_benchmark)
     if env.device.type == "cuda":
         miopen_db.seed(args.miopen_db)  # before the first conv creates the MIOpen handle
@@ -102,7 +159,8 @@ def main() -> int:
                      parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
                      first_bucket_mb=args.first_bucket_mb,
                      dp_devices=args.gpus if args.parallel == "dp" else 1, graph=args.graph,
-                     lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1))
+                     lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1),
+                     micro_batches=args.micro_batches, schedule=args.schedule, partition=args.partition)
     if args.parallel == "dp" and env.world_size > 1:
         raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
                          "--gpus N` without torchrun")
@@ -133,14 +191,19 @@ def main() -> int:
     elapsed = comm.max_scalar(elapsed)
     final_loss = float(loss.item())
 
-    n = env.world_size
+    import torch.distributed as dist
+    n = dist.get_world_size()
     if args.parallel == "dp" and dev.type == "cuda":
         n = args.gpus  # one process driving N GPUs
-    global_batch = args.batch_size * n
+    # pipe: the batch is the whole pipeline's batch; data parallel: per GPU
+    global_batch = args.batch_size if args.parallel == "pipe" else args.batch_size * n
     img_s = global_batch * args.steps / elapsed
-    par = {"ddp": "dp", "syncbn": "dp", "dp": "dp-single-process", "none": "none"}[args.parallel]
+    par = {"ddp": "dp", "syncbn": "dp", "dp": "dp-single-process", "pipe": "pipe",
+           "none": "none"}[args.parallel]
     metric = f"images/sec (whole node) {'ResNet-50' if args.model == 'resnet50' else args.model} " \
              f"{'DDP' if args.parallel in ('ddp', 'syncbn') else args.parallel.upper()} {args.dtype}"
+    ref = REFERENCE_MNV2.get((args.parallel, n, global_batch)) if args.model == "mobilenetv2" else None
+    ref = ref or BASELINE_VALUE
     result = {
         "metric": metric,
         "value": round(img_s, 2),
@@ -150,8 +213,8 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": (img_s / BASELINE_VALUE) if BASELINE_VALUE else None,
+        "scaling": "strong" if args.parallel == "pipe" else "weak",
+        "vs_baseline": round(img_s / ref, 3) if ref else None,
         "dtype": args.dtype,
         "data": "synthetic (random 3x%dx%d inputs, random labels, random-init weights)"
                 % (image_size, image_size),
@@ -163,10 +226,18 @@ def main() -> int:
             "seq_len": None,
             "image_size": image_size,
             "parallelism": f"{par}{n}",
+            "ranks": dist.get_world_size(),
+            "rccl_ranks": comm.size if comm.native is not None else None,
+            "launcher": "bench-spawn" if os.environ.get("DMP_BENCH_SPAWNED") else
+            ("torchrun" if "TORCHELASTIC_RUN_ID" in os.environ else "single"),
+            "optimizer": type(st.optimizer).__name__ + ("(fp32 master)" if args.dtype != "fp32" else ""),
             "sync_bn": args.parallel == "syncbn",
             "bucket_cap_mb": args.bucket_cap_mb,
             "channels_last": not args.no_channels_last,
             "grad_comm": getattr(st.wrapped, "comm_backend", None),
+            **({"micro_batches": args.micro_batches, "schedule": args.schedule,
+                "stage_partition": st.wrapped.partition} if args.parallel == "pipe" else {}),
+            **({"reference_images_per_sec": round(ref, 1)} if ref else {}),
             "hip_graph": args.graph,
             "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
             if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,

@@ -28,7 +28,7 @@ class StepConfig:
     num_classes: Optional[int] = None
     dtype: torch.dtype = torch.bfloat16
     channels_last: bool = True
-    parallel: str = "ddp"           # ddp | syncbn | dp | none
+    parallel: str = "ddp"           # ddp | syncbn | dp | pipe | none
     bucket_cap_mb: float = 25.0
     first_bucket_mb: float = 1.0
     dp_devices: int = 1             # parallel == "dp": GPUs driven by the single process
@@ -37,6 +37,9 @@ class StepConfig:
     momentum: float = 0.9
     weight_decay: float = 1e-4
     seed: int = 0
+    micro_batches: int = 8          # parallel == "pipe"
+    schedule: str = "1f1b"          # parallel == "pipe": naive | gpipe | 1f1b
+    partition: str = "balanced"     # parallel == "pipe": balanced | reference
     extra: dict = field(default_factory=dict)
 
 
@@ -67,6 +70,8 @@ def synthetic_batch(cfg: StepConfig, device: torch.device, generator_seed: int =
 
 
 def build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
+    if cfg.parallel == "pipe":
+        return build_pipeline_state(cfg, device)
     if cfg.graph:
         if device.type != "cuda":
             raise ValueError("graph capture needs a GPU")
@@ -147,3 +152,42 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
             return loss
 
     return TrainState(cfg, model, wrapped, opt, step, x, y)
+
+
+def build_pipeline_state(cfg: StepConfig, device: torch.device) -> TrainState:
+    """Pipeline model parallelism across the process group (one stage per rank).
+
+    ``cfg.batch_size`` is the WHOLE batch entering stage 0 (the reference's
+    model-parallel run feeds 512 images per step through 4 stages,
+    ``model_parallel.py:92``); it is cut into ``cfg.micro_batches`` micro-batches
+    scheduled naive / gpipe / 1f1b.  Every stage updates its own slice with the
+    same fp32-master SGD as the data-parallel paths.  ``step()`` returns the
+    loss on rank 0 (and a zero tensor elsewhere).
+    """
+    from ..comm.rccl import default_communicator
+    from ..parallel.pipeline import Pipeline
+
+    torch.manual_seed(cfg.seed)  # every rank builds the same full model, keeps its stage
+    kw = {"num_classes": cfg.num_classes} if cfg.num_classes else {}
+    model = build_model(cfg.model, **kw)
+    if not hasattr(model, "as_sequential"):
+        raise ValueError(f"--parallel pipe needs a model with as_sequential() (got {cfg.model})")
+    (c, h, w), _ = INPUT_SHAPES[cfg.model]
+    if cfg.image_size:
+        h = w = cfg.image_size
+    comm = default_communicator(device)
+    pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=cfg.micro_batches,
+                    schedule=cfg.schedule, device=device, dtype=cfg.dtype,
+                    channels_last=cfg.channels_last, partition=cfg.partition)
+    opt = MasterSGD(pipe.module.parameters(), lr=cfg.lr, momentum=cfg.momentum,
+                    weight_decay=cfg.weight_decay)
+    x, y = synthetic_batch(cfg, device) if pipe.is_first else (None, None)
+    zero = torch.zeros((), device=device)
+
+    def step() -> torch.Tensor:
+        r = pipe.train_step(x, y)
+        opt.step()
+        opt.zero_grad()
+        return torch.tensor(r.loss) if r.loss is not None else zero
+
+    return TrainState(cfg, pipe.module, pipe, opt, step, x, y)

@@ -1,0 +1,39 @@
+"""bench.py contract on CPU/gloo: `--gpus N` without a launcher spawns N rank
+processes itself (reference: mp.spawn, model_parallel.py:160-162) and rank 0
+prints ONE JSON line whose n_gpus is the real world size; `--parallel pipe`
+runs the pipeline across those ranks."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--device", "cpu", "--dtype", "fp32",
+                        "--no-channels-last", "--steps", "1", "--warmup", "1", *extra],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_ranks_ddp():
+    res = _run("--gpus", "2", "--model", "resnet18", "--batch-size", "2", "--image-size", "32")
+    assert res["n_gpus"] == 2 and res["config"]["ranks"] == 2
+    assert res["config"]["launcher"] == "bench-spawn"
+    assert res["config"]["global_batch"] == 4 and res["scaling"] == "weak"
+    assert res["config"]["grad_comm"] == "process_group"
+
+
+def test_bench_pipe_two_stages():
+    res = _run("--gpus", "2", "--parallel", "pipe", "--model", "mobilenetv2", "--batch-size", "8",
+               "--micro-batches", "2", "--schedule", "gpipe")
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "pipe2"
+    assert res["config"]["global_batch"] == 8 and res["scaling"] == "strong"
+    assert len(res["config"]["stage_partition"]) == 2
+    assert res["ms_per_step"] > 0
