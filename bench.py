@@ -45,7 +45,9 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from distributed_model_parallel_amd.comm.rccl import default_communicator  # noqa: E402
 from distributed_model_parallel_amd.models import INPUT_SHAPES  # noqa: E402
+from distributed_model_parallel_amd.train.cli import start_watchdog  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
+from distributed_model_parallel_amd.utils.profiling import trace_range  # noqa: E402
 from distributed_model_parallel_amd.utils import gemm_tuning, miopen_db  # noqa: E402
 from distributed_model_parallel_amd.utils.env import destroy_distributed, init_distributed  # noqa: E402
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
@@ -127,6 +129,9 @@ def main() -> int:
                     help="seed MIOpen's find/perf db from profiles/miopen/ (use), also write new "
                          "entries back (refresh), or start empty (off); see utils/miopen_db.py")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--watchdog", type=float, default=None, metavar="SECONDS",
+                    help="exit 1 when the collective stream is stuck this long (default 900 s for "
+                         "multi-rank GPU runs without --graph, 0 = off)")
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
     ap.add_argument("--gemm-tuning", default=os.environ.get("DMP_GEMM_TUNING", "use"),
                     choices=["use", "tune", "off"],
@@ -166,6 +171,9 @@ def main() -> int:
                          "--gpus N` without torchrun")
     st = build_train_state(cfg, dev)
     comm = default_communicator(dev)
+    wd = args.watchdog if args.watchdog is not None else (
+        900.0 if env.world_size > 1 and dev.type == "cuda" and not args.graph else 0.0)
+    dog = start_watchdog(wd, env)
 
     (_, img_h, _), _ = INPUT_SHAPES[args.model]
     image_size = args.image_size or img_h
@@ -183,7 +191,8 @@ def main() -> int:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        loss = st.step()
+        with trace_range("bench.step"):
+            loss = st.step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     comm.barrier()
@@ -239,6 +248,7 @@ def main() -> int:
                 "stage_partition": st.wrapped.partition} if args.parallel == "pipe" else {}),
             **({"reference_images_per_sec": round(ref, 1)} if ref else {}),
             "hip_graph": args.graph,
+            "watchdog_s": wd,
             "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
             if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,
             "final_loss": round(final_loss, 4),
@@ -252,6 +262,8 @@ def main() -> int:
         if args.json_out:
             with open(args.json_out, "w") as f:
                 f.write(line + "\n")
+    if dog is not None:
+        dog.stop()
     destroy_distributed()
     return 0
 

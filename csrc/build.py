@@ -8,7 +8,15 @@ linked against the HIP runtime and RCCL that PyTorch already loads (its own
 ``torch/lib`` copies, so one process never holds two RCCL/HIP runtimes).
 
 Incremental: an object is rebuilt when its source or any header under csrc/
-is newer.  Usage: ``python csrc/build.py [-j N] [--force]``.
+is newer.  Usage: ``python csrc/build.py [-j N] [--force] [--asan]``.
+
+``--asan`` (host code only -- GPU AddressSanitizer is not
+available here): every object is rebuilt with ``-fsanitize=address`` on the
+HOST side (``-Xarch_host`` for hipcc, device code untouched) into
+``build/native-asan/_C.so``; run the CPU suite against it with::
+
+    LD_PRELOAD=$(gcc -print-file-name=libasan.so) ASAN_OPTIONS=detect_leaks=0 \
+        DMP_NATIVE_SO=build/native-asan/_C.so python -m pytest tests -m "not gpu"
 """
 from __future__ import annotations
 
@@ -67,8 +75,16 @@ def _common_flags(inc, abi):
     return flags
 
 
+ASAN = False
+
+
+def _obj_for_build(src: Path) -> Path:
+    o = _obj_for(src)
+    return (ROOT / "build" / "native-asan" / o.name) if ASAN else o
+
+
 def compile_one(src: Path, inc, abi, force: bool, hdr_mtime: float) -> tuple[Path, str]:
-    obj = _obj_for(src)
+    obj = _obj_for_build(src)
     if not force and obj.exists():
         m = obj.stat().st_mtime
         if m >= src.stat().st_mtime and m >= hdr_mtime:
@@ -76,10 +92,12 @@ def compile_one(src: Path, inc, abi, force: bool, hdr_mtime: float) -> tuple[Pat
     obj.parent.mkdir(parents=True, exist_ok=True)
     common = _common_flags(inc, abi)
     if src.suffix == ".hip":
+        san = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"] if ASAN else []
         cmd = [str(ROCM / "bin" / "hipcc"), f"--offload-arch={ARCH}", "-x", "hip",
-               "-munsafe-fp-atomics", "-Wno-unused-result", *common, "-c", str(src), "-o", str(obj)]
+               "-munsafe-fp-atomics", "-Wno-unused-result", *san, *common, "-c", str(src), "-o", str(obj)]
     else:
-        cmd = ["g++", *common, "-Wno-unused-result", "-Wno-deprecated-declarations", "-c", str(src),
+        san = ["-fsanitize=address", "-fno-omit-frame-pointer", "-g"] if ASAN else []
+        cmd = ["g++", *common, *san, "-Wno-unused-result", "-Wno-deprecated-declarations", "-c", str(src),
                "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -87,9 +105,10 @@ def compile_one(src: Path, inc, abi, force: bool, hdr_mtime: float) -> tuple[Pat
     return obj, "built"
 
 
-def link(objs, tdir: Path):
+def link(objs, tdir: Path, out: Path = OUT):
     tlib = tdir / "lib"
-    cmd = ["g++", "-shared", "-o", str(OUT), *[str(o) for o in objs],
+    cmd = ["g++", "-shared", *(["-fsanitize=address"] if ASAN else []), "-o", str(out),
+           *[str(o) for o in objs],
            f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
            "-ltorch_python", "-lamdhip64", "-lrccl",
            f"-Wl,-rpath,{tlib}", f"-Wl,-rpath,{ROCM / 'lib'}"]
@@ -113,18 +132,21 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = True) -> Path:
             if verbose:
                 print(f"[dmp-build] {status:10s} {futs[f].relative_to(ROOT)}", flush=True)
     objs.sort()
-    if changed or force or not OUT.exists() or OUT.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        link(objs, tdir)
+    out = (ROOT / "build" / "native-asan" / "_C.so") if ASAN else OUT
+    if changed or force or not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        link(objs, tdir, out)
         if verbose:
-            print(f"[dmp-build] linked {OUT.relative_to(ROOT)}", flush=True)
-    return OUT
+            print(f"[dmp-build] linked {out.relative_to(ROOT)}", flush=True)
+    return out
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="host-side AddressSanitizer build (CPU tests)")
     a = ap.parse_args()
+    ASAN = a.asan
     try:
         build(a.jobs, a.force)
     except RuntimeError as e:

@@ -1,4 +1,5 @@
 #include "reducer.h"
+#include "../trace.h"
 
 #include <ATen/hip/Sleep.h>
 #include <ATen/hip/HIPContext.h>
@@ -9,6 +10,7 @@
 #include <torch/csrc/autograd/variable.h>
 #include <torch/csrc/autograd/grad_mode.h>
 
+#include <cstdio>
 #include <map>
 #include <unordered_set>
 
@@ -392,6 +394,9 @@ void Reducer::flush_bucket_locked(int64_t bi) {
 
 void Reducer::launch_ready_prefix_locked() {
   while (next_launch_ < (int64_t)buckets_.size() && buckets_[next_launch_].pending == 0) {
+    char name[48];
+    std::snprintf(name, sizeof(name), "ddp.bucket%lld.allreduce", (long long)next_launch_);
+    trace::Range r(name);
     backend_->launch(next_launch_, buckets_[next_launch_].flat);
     ++next_launch_;
   }
@@ -414,7 +419,10 @@ void Reducer::finalize() {
                 "gradient (indices: ", missing,
                 "...). Pass find_unused_parameters=True if parts of the model are unused.");
   }
-  backend_->wait_all();
+  {
+    trace::Range r("ddp.wait_all");
+    backend_->wait_all();
+  }
   if (record_order_ && !ready_order_.empty()) record_order_ = false;
 }
 

@@ -31,6 +31,15 @@ def _load() -> Optional[ModuleType]:
             _err = RuntimeError("DMP_DISABLE_NATIVE=1")
             return None
         try:
+            so = os.environ.get("DMP_NATIVE_SO")
+            if so:  # e.g. the host-ASan build (csrc/build.py --asan)
+                import importlib.util
+                import sys
+                spec = importlib.util.spec_from_file_location(f"{__package__}._C", so)
+                _mod = importlib.util.module_from_spec(spec)
+                spec.loader.exec_module(_mod)
+                sys.modules[f"{__package__}._C"] = _mod
+                return _mod
             from . import _C  # type: ignore[attr-defined]
             _mod = _C
         except ImportError as e:  # pragma: no cover - depends on build state

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
+from ..utils.profiling import trace_range
 from . import comm_ops
 
 
@@ -289,14 +290,21 @@ class DataParallel(nn.Module):
     def forward(self, *inputs, **kwargs):
         if not self.device_ids:
             return self.module(*inputs, **kwargs)
-        ins, kws = scatter_kwargs(inputs, kwargs, self.device_ids, self.dim)
+        # roctx ranges (rocprofv3 --marker-trace): the four phases upstream DP
+        # wraps in record_function("DataParallel.forward")
+        with trace_range("dp.scatter"):
+            ins, kws = scatter_kwargs(inputs, kwargs, self.device_ids, self.dim)
         if not ins and not kws:
             ins, kws = ((),), ({},)
         if len(self.device_ids) == 1:
-            return self.module(*ins[0], **kws[0])
-        replicas = self.replicate(self.module, self.device_ids[:len(ins)])
-        outs = self.parallel_apply(replicas, ins, kws)
-        return self.gather(outs, self.output_device)
+            with trace_range("dp.apply"):
+                return self.module(*ins[0], **kws[0])
+        with trace_range("dp.replicate"):
+            replicas = self.replicate(self.module, self.device_ids[:len(ins)])
+        with trace_range("dp.parallel_apply"):
+            outs = self.parallel_apply(replicas, ins, kws)
+        with trace_range("dp.gather"):
+            return self.gather(outs, self.output_device)
 
     def replicate(self, module, device_ids):
         return replicate(module, device_ids, not torch.is_grad_enabled())

@@ -34,6 +34,7 @@ import torch.nn as nn
 from .. import _native
 from ..comm.rccl import Communicator, default_communicator
 from ..ops import flat as flatops
+from ..utils.profiling import trace_range
 
 _MB = 1024 * 1024
 
@@ -320,10 +321,12 @@ class DistributedDataParallel(nn.Module):
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             self._maybe_rebuild_buckets()
         if self.broadcast_buffers and self.world_size > 1 and self._buffers_flat:
-            for f in self._buffers_flat:
-                self.comm.broadcast(f, 0)
-            self.comm.wait()
-        out = self.module(*inputs, **kwargs)
+            with trace_range("ddp.broadcast_buffers"):
+                for f in self._buffers_flat:
+                    self.comm.broadcast(f, 0)
+                self.comm.wait()
+        with trace_range("ddp.forward"):
+            out = self.module(*inputs, **kwargs)
         if torch.is_grad_enabled() and self.require_backward_grad_sync:
             outs = _tensors_in(out) if self.find_unused_parameters else []
             self.reducer.prepare_for_backward(outs)

@@ -40,6 +40,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..comm.rccl import Communicator
+from ..utils.profiling import trace_range
 
 
 # --------------------------------------------------------------------------- #
@@ -141,14 +142,16 @@ class SendForwardRecvBackward(torch.autograd.Function):
     def forward(ctx, x, comm: Communicator, peer: int):
         ctx.comm, ctx.peer = comm, peer
         ctx.shape, ctx.dtype, ctx.device = x.shape, x.dtype, x.device
-        comm.send(x.contiguous(), peer)
+        with trace_range("pipe.send_fwd"):
+            comm.send(x.contiguous(), peer)
         return x.view_as(x)
 
     @staticmethod
     def backward(ctx, g):
         buf = torch.empty(ctx.shape, dtype=ctx.dtype, device=ctx.device)
-        ctx.comm.recv(buf, ctx.peer)
-        ctx.comm.wait()
+        with trace_range("pipe.recv_bwd"):
+            ctx.comm.recv(buf, ctx.peer)
+            ctx.comm.wait()
         return buf, None, None
 
 
@@ -162,13 +165,15 @@ class RecvForwardSendBackward(torch.autograd.Function):
     def forward(ctx, anchor, shape, dtype, comm: Communicator, peer: int):
         ctx.comm, ctx.peer = comm, peer
         buf = torch.empty(shape, dtype=dtype, device=anchor.device)
-        comm.recv(buf, peer)
-        comm.wait()
+        with trace_range("pipe.recv_fwd"):
+            comm.recv(buf, peer)
+            comm.wait()
         return buf
 
     @staticmethod
     def backward(ctx, g):
-        ctx.comm.send(g.contiguous(), ctx.peer)
+        with trace_range("pipe.send_bwd"):
+            ctx.comm.send(g.contiguous(), ctx.peer)
         return None, None, None, None, None
 
 
@@ -416,8 +421,9 @@ class Pipeline:
             if self.is_first:
                 return self._prep_input(xs[m])
             buf = torch.empty(self._in_shape(sizes[m]), dtype=self.dtype, device=self.device)
-            self.comm.recv(buf, r - 1)
-            self.comm.wait()
+            with trace_range("pipe.recv_fwd"):
+                self.comm.recv(buf, r - 1)
+                self.comm.wait()
             return buf.requires_grad_()
 
         def bwd(x, y, g):
@@ -442,8 +448,9 @@ class Pipeline:
             g = None
             if not self.is_last:
                 g = torch.empty(self._out_shape(sizes[b_i]), dtype=self.dtype, device=self.device)
-                self.comm.batch_p2p([(y.detach().contiguous(), r + 1, True), (g, r + 1, False)])
-                self.comm.wait()
+                with trace_range("pipe.send_fwd+recv_bwd"):
+                    self.comm.batch_p2p([(y.detach().contiguous(), r + 1, True), (g, r + 1, False)])
+                    self.comm.wait()
             xo, yo = queue.pop(0)
             gx = bwd(xo, yo, g)
             b_i += 1
@@ -459,8 +466,9 @@ class Pipeline:
                 else:
                     buf = torch.empty(self._in_shape(sizes[m_next]), dtype=self.dtype,
                                       device=self.device)
-                    self.comm.batch_p2p([(gx.contiguous(), r - 1, True), (buf, r - 1, False)])
-                    self.comm.wait()
+                    with trace_range("pipe.send_bwd+recv_fwd"):
+                        self.comm.batch_p2p([(gx.contiguous(), r - 1, True), (buf, r - 1, False)])
+                        self.comm.wait()
                     x_next = buf.requires_grad_()
         for _ in range(warm):
             xo, yo = queue.pop(0)

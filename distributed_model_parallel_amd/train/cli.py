@@ -24,7 +24,6 @@ from __future__ import annotations
 import argparse
 import os
 import sys
-import time
 from typing import Optional
 
 import torch
@@ -64,6 +63,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--log-dir", default="./log")
     p.add_argument("--checkpoint", default="./checkpoint/ckpt.pth")
     p.add_argument("--seed", default=0, type=int)
+    p.add_argument("--watchdog", default=None, type=float, metavar="SECONDS",
+                   help="abort (exit 1, so torchrun can restart) when the collective stream makes "
+                        "no progress for SECONDS (default 1800 when distributed on GPU, 0 = off)")
     return p
 
 
@@ -97,7 +99,9 @@ def run_data_parallel(args, env) -> None:
     from ..utils.logging import MetricsLogger
     from ..utils.metrics import AverageMeter, accuracy
     from ..utils.precision import cast_model, parse_dtype
+    from ..utils.profiling import trace_range
     from ..utils.schedule import build_schedule
+    from ..utils.timers import StepTimer
 
     dev = env.device
     dtype = parse_dtype(args.dtype)
@@ -135,37 +139,42 @@ def run_data_parallel(args, env) -> None:
             x = x.contiguous(memory_format=torch.channels_last)
         return x, y.to(dev, non_blocking=True)
 
+    timer = StepTimer(dev)
     for epoch in range(start_epoch, args.epochs):
         if sampler is not None:
             sampler.set_epoch(epoch)
         net.train()
-        lm, am, bt, dt = AverageMeter(), AverageMeter(), AverageMeter(), AverageMeter()
-        t = time.perf_counter()
-        for i, (x, y) in enumerate(train_loader):
-            if args.steps_per_epoch and i >= args.steps_per_epoch:
-                break
-            x, y = to_dev(x, y)
-            dt.update(time.perf_counter() - t)
-            out = net(x)
-            loss = F.cross_entropy(out.float(), y)
-            loss.backward()
-            opt.step()
-            opt.zero_grad()
+        lm, am = AverageMeter(), AverageMeter()
+        it = iter(train_loader)
+        i = 0
+        while not (args.steps_per_epoch and i >= args.steps_per_epoch):
+            with timer.region("data"):  # reference data_time (utils.py:48): host wait + H2D
+                batch = next(it, None)
+                if batch is None:
+                    break
+                x, y = to_dev(*batch)
+            with timer.region("step"), trace_range("train.step"):
+                out = net(x)
+                loss = F.cross_entropy(out.float(), y)
+                loss.backward()
+                opt.step()
+                opt.zero_grad()
             lm.update(loss.detach(), y.shape[0])
             am.update(accuracy(out, y)[0], y.shape[0])
-            bt.update(time.perf_counter() - t)
-            t = time.perf_counter()
+            i += 1
         if dev.type == "cuda":
             torch.cuda.synchronize()
+        tm = timer.summary()  # device time of the step (HIP events), host time of the data wait
+        step_s, data_s = tm.get("step", 0.0) / 1e3, tm.get("data_host", 0.0) / 1e3
         vl, va = evaluate(net, val_loader, to_dev, args)
         sched.step()
         if env.is_main and va > best:
             best = va
             save_checkpoint(args.checkpoint, net, opt, sched, epoch, best)
         logger.log(epoch, loss_train=lm.avg, acc1_train=am.avg, loss_val=vl, acc1_val=va,
-                   time_per_batch=bt.avg, time_load_perbatch=dt.avg,
+                   time_per_batch=step_s + data_s, time_load_perbatch=data_s,
                    images_per_sec=(args.batch_size * max(1, env.world_size if args.parallel == "ddp" else 1))
-                   / max(bt.avg, 1e-9), lr=opt.param_groups[0]["lr"])
+                   / max(step_s + data_s, 1e-9), lr=opt.param_groups[0]["lr"])
 
 
 @torch.no_grad()
@@ -193,7 +202,9 @@ def run_pipeline(args, env) -> None:
     from ..utils.checkpoint import save_checkpoint, stage_checkpoint_path
     from ..utils.logging import MetricsLogger
     from ..utils.precision import parse_dtype
+    from ..utils.profiling import trace_range
     from ..utils.schedule import build_schedule
+    from ..utils.timers import StepTimer
 
     torch.manual_seed(args.seed)  # every rank builds the same full model (reference: unseeded)
     model = build_model(args.arch, num_classes=_num_classes(args))
@@ -221,21 +232,23 @@ def run_pipeline(args, env) -> None:
     n_train, n_val = (int(v) for v in counts.tolist())
     if args.steps_per_epoch:
         n_train, n_val = min(n_train, args.steps_per_epoch), min(n_val, args.steps_per_epoch)
+    timer = StepTimer(env.device)
     for epoch in range(args.epochs):
         it = iter(train_loader) if train_loader is not None else None
-        tot_t, tot_d, loss_s, acc_s = 0.0, 0.0, 0.0, 0.0
-        t = time.perf_counter()
+        loss_s, acc_s = 0.0, 0.0
         for i in range(n_train):
-            x, y = next(it) if it is not None else (None, None)
-            tot_d += time.perf_counter() - t
-            r = pipe.train_step(x, y)
-            opt.step()
-            opt.zero_grad()
+            with timer.region("data"):
+                x, y = next(it) if it is not None else (None, None)
+            with timer.region("step"), trace_range("pipe.train_step"):
+                r = pipe.train_step(x, y)
+                opt.step()
+                opt.zero_grad()
             if r.loss is not None:
                 loss_s += r.loss
                 acc_s += r.top1
-            tot_t += time.perf_counter() - t
-            t = time.perf_counter()
+        tm = timer.summary()
+        tot_t = (tm.get("step", 0.0) + tm.get("data_host", 0.0)) / 1e3 * max(n_train, 1)
+        tot_d = tm.get("data_host", 0.0) / 1e3 * max(n_train, 1)
         vit = iter(val_loader) if val_loader is not None else None
         vl, va = 0.0, 0.0
         for i in range(n_val):
@@ -267,13 +280,30 @@ def main_worker(args) -> None:
     if env.device.type == "cuda":
         miopen_db.seed("use")  # committed MIOpen find db (skips the first-step solver search)
     seed_everything(args.seed + (env.rank if args.parallel == "ddp" else 0))
+    dog = start_watchdog(args.watchdog, env)
     try:
         if args.parallel == "pipe":
             run_pipeline(args, env)
         else:
             run_data_parallel(args, env)
     finally:
+        if dog is not None:
+            dog.stop()
         destroy_distributed()
+
+
+def start_watchdog(seconds: Optional[float], env):
+    """Start a CommWatchdog on the process's communicator: a
+    collective stream stuck for `seconds` ends the process with exit code 1
+    (no re-exec), so torchrun --max-restarts can restart the job."""
+    if seconds is None:
+        seconds = 1800.0 if (env.distributed and env.device.type == "cuda") else 0.0
+    if seconds <= 0 or env.device.type != "cuda":
+        return None
+    from ..comm.rccl import default_communicator
+    from ..utils.debug import CommWatchdog
+    return CommWatchdog(default_communicator(env.device), timeout_s=seconds,
+                        interval_s=min(5.0, seconds / 4)).start()
 
 
 def main(argv: Optional[list] = None) -> int:

@@ -31,10 +31,14 @@ def _lib():
         cands.append(os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"))
     except Exception:  # noqa: BLE001
         pass
-    cands += ["libroctx64.so", "/opt/rocm/lib/libroctx64.so"]
+    # rocprofiler-sdk's roctx first (what rocprofv3 --marker-trace intercepts), then legacy
+    cands += ["librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+              "libroctx64.so", "/opt/rocm/lib/libroctx64.so"]
     for c in cands:
+        if os.path.isabs(c) and not os.path.exists(c):
+            continue
         try:
-            lib = ctypes.CDLL(c)
+            lib = ctypes.CDLL(c, mode=ctypes.RTLD_GLOBAL)
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
             lib.roctxRangePushA.restype = ctypes.c_int
             lib.roctxRangePop.restype = ctypes.c_int
@@ -54,6 +58,18 @@ def mark(msg: str) -> None:
     lib = _lib()
     if lib is not None:
         lib.roctxMarkA(msg.encode())
+
+
+def push(name: str) -> None:
+    lib = _lib()
+    if lib is not None:
+        lib.roctxRangePushA(name.encode())
+
+
+def pop() -> None:
+    lib = _lib()
+    if lib is not None:
+        lib.roctxRangePop()
 
 
 @contextlib.contextmanager
