@@ -15,8 +15,8 @@ available here): every object is rebuilt with ``-fsanitize=address`` on the
 HOST side (``-Xarch_host`` for hipcc, device code untouched) into
 ``build/native-asan/_C.so``; run the CPU suite against it with::
 
-    LD_PRELOAD=$(gcc -print-file-name=libasan.so) ASAN_OPTIONS=detect_leaks=0 \
-        DMP_NATIVE_SO=build/native-asan/_C.so python -m pytest tests -m "not gpu"
+    LD_PRELOAD="$(gcc -print-file-name=libasan.so) $(gcc -print-file-name=libstdc++.so)" \
+        ASAN_OPTIONS=detect_leaks=0 DMP_NATIVE_SO=build/native-asan/_C.so python -m pytest tests -m "not gpu"
 """
 from __future__ import annotations
 
