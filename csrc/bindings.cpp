@@ -3,6 +3,7 @@
 
 #include "comm/rccl_comm.h"
 #include "ddp/reducer.h"
+#include "dp/parallel_apply.h"
 
 namespace dmp {
 // batchnorm.hip
@@ -234,6 +235,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("synchronize", &dmp::RcclComm::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("stream_handle",
            [](const dmp::RcclComm& c) { return reinterpret_cast<uintptr_t>(c.stream()); });
+
+  // ---- DataParallel replica launcher ----
+  py::class_<dmp::ParallelApply, std::shared_ptr<dmp::ParallelApply>>(m, "ParallelApply")
+      .def(py::init<>())
+      .def("apply", &dmp::ParallelApply::apply, py::arg("modules"), py::arg("inputs"),
+           py::arg("kwargs"), py::arg("devices"))
+      .def("num_workers", &dmp::ParallelApply::num_workers);
 
   // ---- DDP reducer ----
   py::class_<dmp::ReduceBackend, std::shared_ptr<dmp::ReduceBackend>>(m, "ReduceBackend");

@@ -1,0 +1,150 @@
+#include "parallel_apply.h"
+
+#include <ATen/autocast_mode.h>
+#include <ATen/hip/HIPContext.h>
+#include <c10/core/GradMode.h>
+#include <c10/hip/HIPGuard.h>
+
+#include <string>
+
+#include "../trace.h"
+
+namespace py = pybind11;
+
+namespace dmp {
+
+ParallelApply::~ParallelApply() {
+  for (auto& w : workers_) {
+    {
+      std::lock_guard<std::mutex> lk(w->mu);
+      w->stop = true;
+    }
+    w->cv.notify_one();
+  }
+  // joining may wait for a replica that needs the GIL: release it if we hold it
+  const bool held = Py_IsInitialized() && PyGILState_Check();
+  PyThreadState* ts = held ? PyEval_SaveThread() : nullptr;
+  for (auto& w : workers_)
+    if (w->thread.joinable()) w->thread.join();
+  if (ts) PyEval_RestoreThread(ts);
+}
+
+void ParallelApply::ensure_workers(size_t n) {
+  while (workers_.size() < n) {
+    workers_.push_back(std::make_unique<Worker>());
+    Worker* w = workers_.back().get();
+    w->thread = std::thread([this, w] { worker_main(w); });
+  }
+}
+
+// Runs with the GIL NOT held; takes it only around the Python call.
+void ParallelApply::run_job(Job& job) {
+  char name[48];
+  std::snprintf(name, sizeof(name), "dp.replica%lld", (long long)job.index);
+  trace::Range range(name);
+  std::optional<c10::hip::HIPGuard> dev_guard;
+  if (job.device >= 0) {
+    dev_guard.emplace((c10::DeviceIndex)job.device);
+    if (job.stream) c10::hip::setCurrentHIPStream(*job.stream);
+  }
+  c10::AutoGradMode grad(job.grad_enabled);
+  const bool ac_prev = at::autocast::is_autocast_enabled(at::kCUDA);
+  const at::ScalarType ac_dtype_prev = at::autocast::get_autocast_dtype(at::kCUDA);
+  at::autocast::set_autocast_enabled(at::kCUDA, job.autocast);
+  at::autocast::set_autocast_dtype(at::kCUDA, job.autocast_dtype);
+  {
+    py::gil_scoped_acquire gil;
+    try {
+      py::object out = job.fn(*job.args, **job.kwargs);
+      job.result = py::make_tuple(true, out);
+    } catch (py::error_already_set& e) {
+      std::string tb;
+      try {
+        py::object lines = py::module_::import("traceback")
+                               .attr("format_exception")(e.type(), e.value(), e.trace());
+        tb = py::str("").attr("join")(lines).cast<std::string>();
+      } catch (...) {
+        tb = e.what();
+      }
+      std::string dev = job.device >= 0 ? "cuda:" + std::to_string(job.device) : "cpu";
+      std::string tname = py::str(e.type().attr("__name__")).cast<std::string>();
+      std::string msg = "Caught " + tname + " in replica " + std::to_string(job.index) +
+                        " on device " + dev + ".\nOriginal " + tb;
+      job.result = py::make_tuple(false, py::make_tuple(e.type(), msg));
+    }
+    job.fn = py::object();
+    job.args = py::object();
+    job.kwargs = py::object();
+  }
+  at::autocast::set_autocast_enabled(at::kCUDA, ac_prev);
+  at::autocast::set_autocast_dtype(at::kCUDA, ac_dtype_prev);
+}
+
+void ParallelApply::worker_main(Worker* w) {
+  for (;;) {
+    Job* job = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(w->mu);
+      w->cv.wait(lk, [w] { return w->stop || w->job != nullptr; });
+      if (w->stop) return;
+      job = w->job;
+      w->job = nullptr;
+    }
+    run_job(*job);
+    {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      --outstanding_;
+    }
+    done_cv_.notify_all();
+  }
+}
+
+py::list ParallelApply::apply(const py::list& modules, const py::list& inputs,
+                              const py::list& kwargs, const std::vector<int64_t>& devices) {
+  const size_t n = py::len(modules);
+  TORCH_CHECK(py::len(inputs) == n && py::len(kwargs) == n && devices.size() == n,
+              "parallel_apply: modules, inputs, kwargs and devices must have the same length");
+  if (n == 0) return py::list();
+  // caller's thread-local state, captured here (GIL held, calling thread)
+  const bool grad = c10::GradMode::is_enabled();
+  const bool ac = at::autocast::is_autocast_enabled(at::kCUDA);
+  const at::ScalarType ac_dtype = at::autocast::get_autocast_dtype(at::kCUDA);
+  std::vector<Job> jobs(n);
+  for (size_t i = 0; i < n; ++i) {
+    Job& j = jobs[i];
+    j.fn = modules[i];
+    py::object a = inputs[i];
+    j.args = py::isinstance<py::tuple>(a) ? a : (py::isinstance<py::list>(a) ? py::tuple(a) : py::make_tuple(a));
+    j.kwargs = kwargs[i].is_none() ? py::dict() : py::object(kwargs[i]);
+    j.index = (int64_t)i;
+    j.device = devices[i];
+    if (j.device >= 0) j.stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)j.device);
+    j.grad_enabled = grad;
+    j.autocast = ac;
+    j.autocast_dtype = ac_dtype;
+  }
+  ensure_workers(n - 1);
+  {
+    py::gil_scoped_release nogil;
+    {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      outstanding_ = (int64_t)n - 1;
+    }
+    for (size_t i = 1; i < n; ++i) {
+      Worker* w = workers_[i - 1].get();
+      {
+        std::lock_guard<std::mutex> lk(w->mu);
+        w->job = &jobs[i];
+      }
+      w->cv.notify_one();
+    }
+    run_job(jobs[0]);  // replica 0 on the calling thread
+    std::unique_lock<std::mutex> lk(done_mu_);
+    done_cv_.wait(lk, [this] { return outstanding_ == 0; });
+  }
+  py::list out;
+  for (auto& j : jobs) out.append(j.result);
+  return out;
+}
+
+}  // namespace dmp

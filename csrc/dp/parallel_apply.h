@@ -1,0 +1,70 @@
+// Native DataParallel replica launcher (reference Readme.md:70-107
+// studies upstream parallel_apply: one Python threading.Thread per replica,
+// created on every forward, results in a dict under a lock, exceptions wrapped
+// as ExceptionWrapper("in replica i on device d")).
+//
+// Here the replicas run on PERSISTENT C++ worker threads (one per extra
+// replica, created once, parked on a condition variable between steps), so a
+// forward costs no thread creation and no Python-level context managers.  The
+// caller's thread-local state is propagated in C++: the caller's current HIP
+// stream of each replica's device, grad mode and autocast (enabled + dtype).
+// Replica 0 runs inline on the calling thread (it already owns device 0's
+// stream); the caller releases the GIL while it waits for the others.  A
+// replica's exception comes back as (type, "Caught <T> in replica i on device
+// d.\nOriginal Traceback ...") for the Python layer to re-raise with the
+// original exception type (upstream ExceptionWrapper.reraise semantics).
+#pragma once
+
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <optional>
+#include <thread>
+#include <vector>
+
+namespace dmp {
+
+class ParallelApply {
+ public:
+  ParallelApply() = default;
+  ~ParallelApply();
+
+  // modules[i](*inputs[i], **kwargs[i]) on devices[i] (-1 = CPU).  Returns one
+  // (ok, value) tuple per replica; on failure value = (exc_type, message).
+  pybind11::list apply(const pybind11::list& modules, const pybind11::list& inputs,
+                       const pybind11::list& kwargs, const std::vector<int64_t>& devices);
+  int64_t num_workers() const { return (int64_t)workers_.size(); }
+
+ private:
+  struct Job {
+    pybind11::object fn, args, kwargs;
+    int64_t index = 0;
+    int64_t device = -1;
+    std::optional<c10::hip::HIPStream> stream;
+    bool grad_enabled = true;
+    bool autocast = false;
+    at::ScalarType autocast_dtype = at::kBFloat16;
+    pybind11::object result;  // (ok, value)
+  };
+  struct Worker {
+    std::thread thread;
+    std::mutex mu;
+    std::condition_variable cv;
+    Job* job = nullptr;
+    bool stop = false;
+  };
+
+  static void run_job(Job& job);
+  void worker_main(Worker* w);
+  void ensure_workers(size_t n);
+
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::mutex done_mu_;
+  std::condition_variable done_cv_;
+  int64_t outstanding_ = 0;
+};
+
+}  // namespace dmp

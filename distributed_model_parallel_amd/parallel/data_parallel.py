@@ -24,6 +24,7 @@ every peer pulls over its own xGMI link and the reduction is one kernel.
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -198,8 +199,66 @@ class ReplicaError(RuntimeError):
     pass
 
 
+_LAUNCHER = None
+
+
+def _native_launcher():
+    """Process-wide C++ replica launcher (csrc/dp/parallel_apply.cpp), or None."""
+    global _LAUNCHER
+    if _LAUNCHER is None and os.environ.get("DMP_DP_PY_APPLY", "0") != "1":
+        C = _native.native()
+        if C is not None and hasattr(C, "ParallelApply"):
+            _LAUNCHER = C.ParallelApply()
+    return _LAUNCHER
+
+
+def _reraise(i: int, payload) -> None:
+    """Upstream ExceptionWrapper.reraise: the original exception type with the
+    'Caught X in replica i on device d' message; ReplicaError if the type
+    cannot be rebuilt from a message."""
+    etype, msg = payload
+    try:
+        exc = etype(msg)
+    except Exception:  # noqa: BLE001
+        exc = ReplicaError(msg)
+    if not isinstance(exc, BaseException):
+        exc = ReplicaError(msg)
+    raise exc
+
+
 def parallel_apply(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=None,
                    devices: Optional[Sequence] = None) -> List[Any]:
+    """Run modules[i](*inputs[i], **kwargs_tup[i]) on devices[i] concurrently.
+
+    Native path: persistent C++ worker threads carry the caller's current
+    stream per device, grad mode and autocast (no thread creation per call).
+    ``DMP_DP_PY_APPLY=1`` selects the Python-thread version below (kept as the
+    upstream-shaped oracle for tests).
+    """
+    n = len(modules)
+    kwargs_tup = kwargs_tup or tuple({} for _ in range(n))
+    if devices is None:
+        devices = [next(m.parameters()).device if any(True for _ in m.parameters()) else None
+                   for m in modules]
+    launcher = _native_launcher() if n > 1 else None
+    if launcher is not None:
+        devs = []
+        for d in devices:
+            dd = comm_ops._dev(d) if d is not None else None
+            devs.append(dd.index if (dd is not None and dd.type == "cuda") else -1)
+        ins = [tuple(x) if isinstance(x, (list, tuple)) else (x,) for x in inputs]
+        res = launcher.apply(list(modules), ins, [dict(k) for k in kwargs_tup], devs)
+        outs = []
+        for i, (ok, val) in enumerate(res):
+            if not ok:
+                _reraise(i, val)
+            outs.append(val)
+        return outs
+    return _parallel_apply_threads(modules, inputs, kwargs_tup, devices)
+
+
+def _parallel_apply_threads(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=None,
+                            devices: Optional[Sequence] = None) -> List[Any]:
     n = len(modules)
     kwargs_tup = kwargs_tup or tuple({} for _ in range(n))
     if devices is None:

@@ -51,8 +51,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--parallel", default="ddp", choices=["ddp", "dp", "pipe", "none"])
     p.add_argument("--bucket-cap-mb", default=25.0, type=float)
     p.add_argument("--sync-bn", action="store_true")
-    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
-    p.add_argument("--channels-last", action="store_true")
+    p.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16"],
+                   help="auto: bf16 (fp32 master weights) on GPU -- the native MFMA path -- fp32 on CPU")
+    p.add_argument("--channels-last", dest="channels_last", action="store_true", default=None,
+                   help="NHWC activations (default on GPU: every native conv/BN kernel is NHWC)")
+    p.add_argument("--no-channels-last", dest="channels_last", action="store_false")
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--micro-batches", default=1, type=int)
     p.add_argument("--schedule", default="1f1b", choices=["naive", "gpipe", "1f1b"])
@@ -277,6 +280,11 @@ def main_worker(args) -> None:
     from ..utils.env import destroy_distributed, init_distributed, seed_everything
     from ..utils import miopen_db
     env = init_distributed(backend=args.dist_backend, dist_url=args.dist_url)
+    gpu = env.device.type == "cuda"
+    if args.dtype == "auto":
+        args.dtype = "bf16" if gpu else "fp32"
+    if args.channels_last is None:
+        args.channels_last = gpu
     if env.device.type == "cuda":
         miopen_db.seed("use")  # committed MIOpen find db (skips the first-step solver search)
     seed_everything(args.seed + (env.rank if args.parallel == "ddp" else 0))
