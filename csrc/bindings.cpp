@@ -54,6 +54,16 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& residual, bool relu,
                                 const std::vector<int64_t>& a_map,
                                 const std::vector<int64_t>& c_map);
+std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
+                                      const c10::optional<at::Tensor>& residual,
+                                      const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
+                                      const at::Tensor& mean, const c10::optional<at::Tensor>& scale,
+                                      const c10::optional<at::Tensor>& shift);
+// cross_entropy.hip
+std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& x, const at::Tensor& target,
+                                          int64_t ignore_index);
+at::Tensor cross_entropy_bwd(const at::Tensor& grad, const at::Tensor& x, const at::Tensor& target,
+                             const at::Tensor& lse, const at::Tensor& stats, int64_t ignore_index);
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
                    const c10::optional<at::Tensor>& pro_shift);
@@ -141,6 +151,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
         py::arg("residual") = py::none(), py::arg("relu") = false,
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{});
+
+  m.def("cross_entropy_fwd", &dmp::cross_entropy_fwd, py::arg("x"), py::arg("target"),
+        py::arg("ignore_index") = -100);
+  m.def("cross_entropy_bwd", &dmp::cross_entropy_bwd, py::arg("grad"), py::arg("x"), py::arg("target"),
+        py::arg("lse"), py::arg("stats"), py::arg("ignore_index") = -100);
+  m.def("gemm_nt_bnbwd", &dmp::gemm_nt_bnbwd, py::arg("A"), py::arg("B"), py::arg("residual"),
+        py::arg("bn_x"), py::arg("bn_y"), py::arg("mean"), py::arg("scale"), py::arg("shift"));
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),

@@ -19,6 +19,14 @@
 //                             (s, t null: C = acc + R -- a data gradient
 //                             summed with another branch's, see ops/fused.py)
 //                             conv + folded BN (+ residual) + ReLU in one kernel.
+//             EPI_BNBWD     : the data gradient G = bf16(acc (+ R)) of a layer
+//                             whose input is a training-mode BN+ReLU output:
+//                             C = dz = G * relu_mask (mask from the BN output y
+//                             when a residual was fused before the ReLU, else
+//                             re-derived from the BN input x as x*sc + sh > 0)
+//                             and per-column partial (sum dz, sum dz*(x-mean))
+//                             per M-tile -> the BN backward's reductions
+//                             without its separate read pass over dy and x.
 //
 // Structure (cdna_hip_programming.md §5): 256 threads = 4 waves in a
 // WAVES_M x WAVES_N grid, each wave owning a (BM/WAVES_M) x (BN/WAVES_N) tile
@@ -44,7 +52,7 @@ using bf16 = __bf16;
 constexpr int BK = 64;
 constexpr int kThreads = 256;
 
-enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2 };
+enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2, EPI_BNBWD = 3 };
 
 // Logical GEMM row -> physical activation row for strided 1x1 convs: logical
 // row (n, oh, ow) of an [N, Ho, Wo] output grid reads/writes physical row
@@ -92,6 +100,11 @@ struct NtArgs {
   double* zsums;                // EPI_MOMENTS: fp64 moments to zero (see common.h) or null
   RowMap amap, cmap;            // strided 1x1 row maps (non-CONV)
   ConvMap cv;                   // implicit-GEMM conv geometry (CONV)
+  // EPI_BNBWD: BN input x [M, N] and (optional) BN output y [M, N], per-column
+  // mean and the forward affine (sc, sh) for the mask when y is absent
+  const bf16* bx; int64_t ldbx;
+  const bf16* bny; int64_t ldby;
+  const float *bmean, *bsc, *bsh;
 };
 
 // NT = WAVES_M*WAVES_N*64 threads: 4 waves (2 blocks/CU) or 8 waves (256-row
@@ -116,7 +129,7 @@ void gemm_nt_kernel(const NtArgs p) {
   const RowMap& amap = p.amap;
   const RowMap& cmap = p.cmap;
   const ConvMap& cv = p.cv;
-  if constexpr (EPI == EPI_MOMENTS) zero_moments(p.zsums, 2 * N);
+  if constexpr (EPI == EPI_MOMENTS || EPI == EPI_BNBWD) zero_moments(p.zsums, 2 * N);
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int A_VECS = BM * BK / 8 / kThreads;  // 16-B vectors per thread per A tile
@@ -307,7 +320,8 @@ void gemm_nt_kernel(const NtArgs p) {
   // ---- store pass: each thread moves 8 contiguous columns of a row ----
   constexpr int CV = BN / 8;                  // 16-B vectors per row
   constexpr int RPP = kThreads / CV;          // rows per pass
-  static_assert(EPI != EPI_MOMENTS || 2 * RPP * BN * 4 <= LDS_BYTES, "moments scratch exceeds LDS");
+  constexpr bool kMom = EPI == EPI_MOMENTS || EPI == EPI_BNBWD;
+  static_assert(!kMom || 2 * RPP * BN * 4 <= LDS_BYTES, "moments scratch exceeds LDS");
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
   const bool col_ok = col < N;
@@ -323,6 +337,18 @@ void gemm_nt_kernel(const NtArgs p) {
   float msum[8], msq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; }
+  float bmu[8], bsc[8], bsh[8];
+  const bf16* __restrict__ bnx = p.bx;
+  const bf16* __restrict__ bny = p.bny;
+  const int64_t ldbx = p.ldbx, ldby = p.ldby;
+  if constexpr (EPI == EPI_BNBWD) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmu[j] = col_ok ? p.bmean[col + j] : 0.f;
+      bsc[j] = (col_ok && !p.bny) ? p.bsc[col + j] : 0.f;
+      bsh[j] = (col_ok && !p.bny) ? p.bsh[col + j] : 0.f;
+    }
+  }
 #pragma unroll
   for (int p = 0; p < BM / RPP; ++p) {
     const int lr = rr0 + p * RPP;
@@ -340,6 +366,28 @@ void gemm_nt_kernel(const NtArgs p) {
         }
         v = __builtin_convertvector(f, bf16x8);
       }
+      if constexpr (EPI == EPI_BNBWD) {
+        f32x8 g = __builtin_convertvector(v, f32x8);
+        if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
+          g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + (int64_t)row * ldr + col), f32x8);
+          v = __builtin_convertvector(g, bf16x8);
+          g = __builtin_convertvector(v, f32x8);
+        }
+        const f32x8 xv =
+            __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bnx + (int64_t)row * ldbx + col), f32x8);
+        f32x8 yv;
+        if (bny)
+          yv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bny + (int64_t)row * ldby + col), f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool on = bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);
+          const float dz = on ? g[j] : 0.f;
+          g[j] = dz;
+          msum[j] += dz;
+          msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+        }
+        v = __builtin_convertvector(g, bf16x8);  // exact: dz is G or 0
+      }
       *reinterpret_cast<bf16x8*>(C + map_row(cmap, row) * ldc + col) = v;
       if constexpr (EPI == EPI_MOMENTS) {
         f32x8 f = __builtin_convertvector(v, f32x8);
@@ -348,7 +396,7 @@ void gemm_nt_kernel(const NtArgs p) {
       }
     }
   }
-  if constexpr (EPI == EPI_MOMENTS) {
+  if constexpr (kMom) {
     // combine the RPP row-groups of each column through LDS, one partial per M-tile
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [2][RPP][BN]
@@ -797,6 +845,9 @@ void dispatch_mode(const NtArgs& a, bool pro, int epi, int bm, hipStream_t s) {
   } else if (epi == EPI_MOMENTS) {
     if (pro) dispatch_tile<true, EPI_MOMENTS, CONV>(a, bm, s);
     else dispatch_tile<false, EPI_MOMENTS, CONV>(a, bm, s);
+  } else if (epi == EPI_BNBWD) {
+    TORCH_CHECK(!pro, "bnbwd epilogue has no prologue variant");
+    dispatch_tile<false, EPI_BNBWD, CONV>(a, bm, s);
   } else {
     if (pro) dispatch_tile<true, EPI_AFFINE, CONV>(a, bm, s);
     else dispatch_tile<false, EPI_AFFINE, CONV>(a, bm, s);
@@ -832,8 +883,14 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   int epi = EPI_STORE;
   at::Tensor part;
   if (mode == "store") {
-  } else if (mode == "moments") {
-    epi = EPI_MOMENTS;
+  } else if (mode == "moments" || mode == "bnbwd") {
+    epi = mode == "moments" ? EPI_MOMENTS : EPI_BNBWD;
+    if (epi == EPI_BNBWD && residual.has_value() && residual->defined()) {
+      check_operand(*residual, "residual");
+      TORCH_CHECK(residual->size(0) == a.M && residual->size(1) == a.N, "residual shape");
+      a.R = reinterpret_cast<const bf16*>(residual->data_ptr());
+      a.ldr = residual->stride(0);
+    }
     const int mtiles = (a.M + tbm - 1) / tbm;
     part = at::empty({2, mtiles, a.N}, like.options().dtype(at::kFloat));
     a.part = part.data_ptr<float>();
@@ -860,7 +917,7 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   }
   if (conv) dispatch_mode<true>(a, pro, epi, bm, stream);
   else dispatch_mode<false>(a, pro, epi, bm, stream);
-  if (epi == EPI_MOMENTS)
+  if (epi == EPI_MOMENTS || epi == EPI_BNBWD)
     bn_reduce_partials_launch(a.part, (a.M + tbm - 1) / tbm, a.N, moments.data_ptr<double>(),
                               (double)a.M, stream);
   return {C, moments};
@@ -972,6 +1029,55 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
   a.C = reinterpret_cast<bf16*>(C.data_ptr());
   a.ldc = C.stride(0);
   return run_nt(a, true, x, pro_scale, pro_shift, mode, epi_scale, epi_shift, residual, relu, C);
+}
+
+// Data gradient of a 1x1 conv whose input is a training-mode BN(+residual)+ReLU
+// output, fused with that BN's backward reductions (EPI_BNBWD):
+//   G  = bf16(A @ B^T (+ residual))          A = dy [M, K], B = W^T [N, K]
+//   dz = G * mask,  mask = y > 0 (bn_y given) or x*scale + shift > 0
+//   returns (dz [M, N], fp64 [2N+1] = (sum dz, sum dz*(x - mean), M))
+std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
+                                      const c10::optional<at::Tensor>& residual,
+                                      const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
+                                      const at::Tensor& mean, const c10::optional<at::Tensor>& scale,
+                                      const c10::optional<at::Tensor>& shift) {
+  check_operand(A, "A");
+  check_operand(B, "B");
+  check_operand(bn_x, "bn_x");
+  NtArgs a{};
+  a.M = (int)A.size(0);
+  a.K = (int)A.size(1);
+  a.N = (int)B.size(0);
+  TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
+  TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
+  TORCH_CHECK(bn_x.size(0) == a.M && bn_x.size(1) == a.N, "bn_x must be [M, N]");
+  auto f32vec = [&](const at::Tensor& t, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == a.N,
+                name, " must be a contiguous fp32 [N] GPU tensor");
+    return t.data_ptr<float>();
+  };
+  a.bx = reinterpret_cast<const bf16*>(bn_x.data_ptr());
+  a.ldbx = bn_x.stride(0);
+  a.bmean = f32vec(mean, "mean");
+  if (bn_y.has_value() && bn_y->defined()) {
+    check_operand(*bn_y, "bn_y");
+    TORCH_CHECK(bn_y->size(0) == a.M && bn_y->size(1) == a.N, "bn_y must be [M, N]");
+    a.bny = reinterpret_cast<const bf16*>(bn_y->data_ptr());
+    a.ldby = bn_y->stride(0);
+  } else {
+    TORCH_CHECK(scale.has_value() && shift.has_value(), "mask from x needs the BN scale and shift");
+    a.bsc = f32vec(*scale, "scale");
+    a.bsh = f32vec(*shift, "shift");
+  }
+  auto C = at::empty({a.M, a.N}, A.options());
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr());
+  a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr());
+  a.ldb = B.stride(0);
+  a.C = reinterpret_cast<bf16*>(C.data_ptr());
+  a.ldc = C.stride(0);
+  return run_nt(a, false, A, c10::nullopt, c10::nullopt, "bnbwd", c10::nullopt, c10::nullopt, residual,
+                false, C);
 }
 
 void set_gemm_tile(int64_t t) { g_tile_override = (int)t; }

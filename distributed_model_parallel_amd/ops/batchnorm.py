@@ -32,6 +32,11 @@ GradReducer = Callable[[torch.Tensor], torch.Tensor]
 
 _STATS = {"native_fwd": 0, "torch_fwd": 0}
 
+# BN backward reductions fused into the consuming 1x1 conv's data-gradient
+# epilogue (BnBwdSlot); DMP_FUSE_BN_BWD=0 disables it for A/B runs.
+import os as _os  # noqa: E402
+_FUSE_BWD = _os.environ.get("DMP_FUSE_BN_BWD", "1") != "0"
+
 
 def stats() -> dict:
     return dict(_STATS)
@@ -180,12 +185,58 @@ def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, rel
 
 
 # --------------------------------------------------------------------------- #
+# Backward fusion handshake with the consuming 1x1 conv
+# --------------------------------------------------------------------------- #
+class BnBwdSlot:
+    """Mailbox between a training-mode BN+ReLU and the ONE native 1x1 conv that
+    consumes its output (attached to the output tensor as ``_dmp_bnbwd``).
+
+    The conv's data-gradient GEMM produces this BN's incoming gradient G; with
+    the slot it also applies the ReLU mask and reduces (sum dz, sum dz*(x-mean))
+    in its epilogue (``gemm_nt_bnbwd``) and parks the result here.  The BN
+    backward uses the parked sums -- skipping its own moments pass over dy and
+    x -- only if the gradient it receives IS the conv's output, unmodified
+    (same storage, same version): any other contribution summed in by autograd
+    makes it fall back to the full computation (still correct, since the mask
+    is idempotent)."""
+    __slots__ = ("x2", "y2", "mean", "invstd", "w32", "b32", "consumers", "sums", "dz_ptr", "dz_ver",
+                 "dz_shape")
+
+    def __init__(self):
+        self.consumers = 0
+        self.sums = None
+        self.dz_ptr = None
+        self.dz_ver = None
+        self.dz_shape = None
+        self.x2 = self.y2 = self.mean = self.invstd = self.w32 = self.b32 = None
+
+    def mask_affine(self):
+        sc = self.invstd * (self.w32 if self.w32 is not None else 1.0)
+        sh = (self.b32 if self.b32 is not None else 0.0) - self.mean * sc
+        return sc.contiguous(), sh.contiguous()
+
+    def park(self, dz: torch.Tensor, sums: torch.Tensor) -> None:
+        self.sums = sums
+        self.dz_ptr, self.dz_ver, self.dz_shape = dz.data_ptr(), dz._version, tuple(dz.shape)
+
+    def take(self, dy: torch.Tensor):
+        sums, self.sums = self.sums, None
+        if sums is None or dy.data_ptr() != self.dz_ptr or dy._version != self.dz_ver \
+                or tuple(dy.shape) != self.dz_shape:
+            return None
+        return sums
+
+
+_STATS["fused_bwd_moments"] = 0
+
+
+# --------------------------------------------------------------------------- #
 # Autograd function
 # --------------------------------------------------------------------------- #
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
-                relu, reduce_moments, reduce_grads, pre_sums=None, nbt=None):
+                relu, reduce_moments, reduce_grads, pre_sums=None, nbt=None, bwd_slot=None):
         x2, back = _as_rows(x)
         native = _native_ok(x2)
         _STATS["native_fwd" if native else "torch_fwd"] += 1
@@ -223,6 +274,12 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.meta = (native, training, relu, residual is not None, back,
                     weight is not None, bias is not None, reduce_grads,
                     weight.dtype if weight is not None else None, x.dim())
+        ctx.bwd_slot = None
+        if bwd_slot is not None and native and training and relu and x.dim() == 4:
+            bwd_slot.x2 = x2
+            bwd_slot.y2 = y2 if residual is not None else None
+            bwd_slot.mean, bwd_slot.invstd, bwd_slot.w32, bwd_slot.b32 = mean, invstd, w32, b32
+            ctx.bwd_slot = bwd_slot
         return back(y2)
 
     @staticmethod
@@ -231,13 +288,25 @@ class _BatchNormActFn(torch.autograd.Function):
         (native, training, relu, has_res, back, has_w, has_b, reduce_grads, wdtype,
          ndim) = ctx.meta
         dy2, _ = _as_rows(dy.to(x2.dtype))
-        sums = backward_moments(dy2, x2, y2, mean, relu, native, w32, b32, invstd)
+        slot = ctx.bwd_slot
+        fused = slot.take(dy) if slot is not None else None
+        ctx.bwd_slot = None
+        if fused is not None:
+            # the consumer's dgrad epilogue already masked dy (dz) and reduced the moments
+            _STATS["fused_bwd_moments"] += 1
+            sums = fused
+            relu_eff, y_eff, want_dres = False, None, False
+        else:
+            sums = backward_moments(dy2, x2, y2, mean, relu, native, w32, b32, invstd)
+            relu_eff, y_eff, want_dres = relu, y2, has_res
         local_sums = sums
         if training and reduce_grads is not None:
             local_sums = sums.clone()  # the reducer works in place
             sums = reduce_grads(sums)
-        dx2, dw, db, dres2 = backward_apply(dy2, x2, y2, sums, count, w32, mean, invstd, training,
-                                            relu, has_res, native, b32)
+        dx2, dw, db, dres2 = backward_apply(dy2, x2, y_eff, sums, count, w32, mean, invstd, training,
+                                            relu_eff, want_dres, native, b32)
+        if fused is not None and has_res:
+            dres2 = dy2  # d(residual) = dz, which is exactly the masked incoming gradient
         if reduce_grads is not None and training:
             # weight/bias grads are per-rank quantities (DDP averages them)
             c = x2.shape[1]
@@ -247,7 +316,7 @@ class _BatchNormActFn(torch.autograd.Function):
         gres = back(dres2) if has_res else None
         gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
         gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
-        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None, None
+        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
@@ -261,9 +330,15 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
     """Functional fused BN(+residual)(+ReLU).  `sums`: precomputed local moments
     [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode.
     `num_batches_tracked`: incremented once (training mode), in-kernel when native."""
-    return _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
-                                 momentum, eps, relu, reduce_moments, reduce_grads, sums,
-                                 num_batches_tracked if training else None)
+    slot = None
+    if training and relu and x.dim() == 4 and torch.is_grad_enabled() and _FUSE_BWD and x.is_cuda:
+        slot = BnBwdSlot()
+    out = _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
+                                momentum, eps, relu, reduce_moments, reduce_grads, sums,
+                                num_batches_tracked if training else None, slot)
+    if slot is not None and slot.x2 is not None:
+        out._dmp_bnbwd = slot  # a native 1x1 conv consuming `out` may fuse our backward reductions
+    return out
 
 
 class BatchNormAct2d(nn.BatchNorm2d):

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0}
+_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0}
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -59,7 +59,7 @@ def _geom(stride: int, hi: int, wi: int):
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, moments, slot):
+    def forward(ctx, x, weight, stride, moments, slot, bn_slot=None):
         C = _native.require("conv1x1")
         n, cin, h, w = x.shape
         geom = _geom(stride, h, w)
@@ -70,6 +70,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.geom = geom
         ctx.slot = slot
+        # x is a training-mode BN+ReLU output: our dgrad epilogue can also do
+        # that BN's backward reductions (ops/batchnorm.py BnBwdSlot)
+        ctx.bn_slot = bn_slot if (bn_slot is not None and not geom) else None
+        if ctx.bn_slot is not None:
+            bn_slot.consumers += 1
         if slot is not None and not geom:
             slot.consumer = True  # our dgrad epilogue will absorb the shortcut's gradient
         if mom is None:
@@ -83,7 +88,7 @@ class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dmom):
         if dy is None:
-            return (None,) * 5
+            return (None,) * 6
         x, weight = ctx.saved_tensors
         C = _native.require("conv1x1 backward")
         n, cin, h, w = x.shape
@@ -94,7 +99,24 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # strided: the GEMM scatters into the sampled rows of a zeroed full-size grad
             extra = ctx.slot.take() if (ctx.slot is not None and ctx.slot.consumer) else None
-            if extra is not None:  # dx = dy @ W + (the shortcut branch's gradient), one pass
+            bs = ctx.bn_slot
+            ctx.bn_slot = None
+            if bs is not None and bs.consumers == 1 and bs.x2 is not None:
+                # dz = relu_mask * (dy @ W (+ shortcut grad)) and the producer BN's
+                # (sum dz, sum dz*(x-mean)) in ONE epilogue pass
+                _STATS["fused_bn_bwd"] += 1
+                if extra is not None:
+                    _STATS["fused_dgrad"] += 1
+                    extra = _rows(extra.to(x.dtype).contiguous(memory_format=torch.channels_last))
+                sc = sh = None
+                if bs.y2 is None:
+                    sc, sh = bs.mask_affine()
+                dx2, sums = C.gemm_nt_bnbwd(dy2, w2.t().contiguous(), extra, bs.x2, bs.y2,
+                                            bs.mean.contiguous(), sc, sh)
+                dx = _unrows(dx2, n, h, w)
+                bs.park(dx, sums[: 2 * cin])
+                dx2 = None
+            elif extra is not None:  # dx = dy @ W + (the shortcut branch's gradient), one pass
                 _STATS["fused_dgrad"] += 1
                 extra = _rows(extra.to(x.dtype).contiguous(memory_format=torch.channels_last))
                 dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), mode="add", residual=extra)
@@ -102,14 +124,15 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dx2 = dy2 @ w2  # deep-K / short-M: hipBLASLt's stream-K tiles win here
             else:
                 dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), c_map=ctx.geom)
-            dx = _unrows(dx2, n, h, w)
+            if dx2 is not None:
+                dx = _unrows(dx2, n, h, w)
         if ctx.needs_input_grad[1]:
             # split-M MFMA GEMM with transposing LDS reads (hipBLASLt picks a 4-tile,
             # no-split kernel for this tiny-output / huge-reduction shape)
             dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
@@ -119,7 +142,8 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
     into this conv's data-gradient epilogue."""
     if _native_ok(x, weight):
         _STATS["native"] += 1
-        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments, grad_slot)
+        bn_slot = getattr(x, "_dmp_bnbwd", None) if torch.is_grad_enabled() else None
+        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments, grad_slot, bn_slot)
         return y, (mom if moments else None)
     _STATS["torch"] += 1
     return F.conv2d(x, weight, None, stride), None

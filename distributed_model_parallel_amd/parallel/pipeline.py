@@ -208,7 +208,7 @@ class Pipeline:
 
     def __init__(self, atoms: nn.Sequential, comm: Communicator, sample_shape: Sequence[int],
                  micro_batches: int = 1, schedule: str = "1f1b",
-                 loss_fn: Callable = F.cross_entropy, loss_on: str = "last",
+                 loss_fn: Optional[Callable] = None, loss_on: str = "last",
                  partition=None, balance: str = "flops",
                  device: Optional[torch.device] = None, dtype: torch.dtype = torch.float32,
                  channels_last: bool = False):
@@ -222,6 +222,8 @@ class Pipeline:
         self.rank, self.world = comm.rank, comm.size
         self.schedule = schedule
         self.micro_batches = 1 if schedule == "naive" else micro_batches
+        if loss_fn is None:
+            from ..ops.loss import cross_entropy as loss_fn  # fused HIP kernel on GPU
         self.loss_fn = loss_fn
         self.loss_on = loss_on if self.world > 1 else "last"
         self.device = torch.device(device) if device is not None else comm.device

@@ -102,6 +102,7 @@ def run_data_parallel(args, env) -> None:
     from ..utils.logging import MetricsLogger
     from ..utils.metrics import AverageMeter, accuracy
     from ..utils.precision import cast_model, parse_dtype
+    from ..ops.loss import cross_entropy
     from ..utils.profiling import trace_range
     from ..utils.schedule import build_schedule
     from ..utils.timers import StepTimer
@@ -158,7 +159,7 @@ def run_data_parallel(args, env) -> None:
                 x, y = to_dev(*batch)
             with timer.region("step"), trace_range("train.step"):
                 out = net(x)
-                loss = F.cross_entropy(out.float(), y)
+                loss = cross_entropy(out, y)
                 loss.backward()
                 opt.step()
                 opt.zero_grad()

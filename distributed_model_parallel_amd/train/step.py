@@ -16,6 +16,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..models import INPUT_SHAPES, build_model
+from ..ops.loss import cross_entropy
 from ..ops.optim import FlatSGD, MasterSGD
 from ..utils.precision import cast_model
 
@@ -119,7 +120,7 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
 
         def step() -> torch.Tensor:
             out = wrapped(x)
-            loss = F.cross_entropy(out.float(), y)
+            loss = cross_entropy(out, y)
             loss.backward()
             opt.step()
             opt.zero_grad()
@@ -133,7 +134,7 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
 
         def step() -> torch.Tensor:
             out = wrapped(x)
-            loss = F.cross_entropy(out.float(), y)
+            loss = cross_entropy(out, y)
             loss.backward()
             opt.step()
             opt.zero_grad()
@@ -145,7 +146,7 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
 
         def step() -> torch.Tensor:
             out = model(x)
-            loss = F.cross_entropy(out.float(), y)
+            loss = cross_entropy(out, y)
             loss.backward()
             opt.step()
             opt.zero_grad()

@@ -158,3 +158,29 @@ def test_native_launcher_propagates_current_stream_and_host_time():
     native, threads = host_us(parallel_apply), host_us(_parallel_apply_threads)
     print(f"parallel_apply host time, 4 replicas: native {native:.1f} us, python threads {threads:.1f} us")
     assert native < threads
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs two visible GPUs (peer access + cross-device event ordering)")
+def test_dp_distinct_devices_peer_path():
+    """Distinct device ids: DataParallel enables xGMI peer access, scatters /
+    replicates by peer pulls and reduces gradients on device 0 -- same result
+    as one device."""
+    ndev = min(torch.cuda.device_count(), 4)
+    torch.manual_seed(0)
+    m = Net().cuda()
+    ref = Net().cuda()
+    ref.load_state_dict(m.state_dict())
+    x = torch.randn(16, 3, 8, 8, device="cuda")
+    y = torch.randint(0, 5, (16,), device="cuda")
+    dp = DataParallel(m, device_ids=list(range(ndev)))
+    for _ in range(2):  # twice: the second step reuses peer state and cached streams
+        m.zero_grad()
+        out = dp(x)
+        F.cross_entropy(out, y).backward()
+    ref.zero_grad()
+    F.cross_entropy(ref(x), y).backward()
+    torch.testing.assert_close(out, ref(x), atol=1e-5, rtol=1e-5)
+    for (n, p), q in zip(m.named_parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, atol=1e-5, rtol=1e-4, msg=n)

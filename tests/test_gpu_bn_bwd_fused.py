@@ -1,0 +1,99 @@
+"""BN backward reductions fused into the consuming 1x1 conv's data-gradient
+GEMM (EPI_BNBWD, ops/batchnorm.py BnBwdSlot) against fp32/fp64 PyTorch
+references: the kernel on its own (mask from y or from the BN affine, with and
+without the shortcut-gradient add), then whole blocks fused vs unfused."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd import _native
+from distributed_model_parallel_amd.ops import batchnorm as bnops
+from distributed_model_parallel_amd.ops import conv1x1
+from distributed_model_parallel_amd.utils.precision import cast_model
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("M,N,K", [(4097, 64, 256), (1000, 256, 64), (333, 128, 512)])
+@pytest.mark.parametrize("mask_from_y", [False, True])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_gemm_nt_bnbwd_kernel(M, N, K, mask_from_y, with_res):
+    C = _native.require("bnbwd test")
+    torch.manual_seed(0)
+    dy = torch.randn(M, K, device=DEV).bfloat16()
+    wt = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()      # W^T as the NT "B" operand
+    x = torch.randn(M, N, device=DEV).bfloat16()               # BN input
+    mean = x.float().mean(0)
+    sc = torch.rand(N, device=DEV) + 0.5
+    sh = torch.randn(N, device=DEV) * 0.5
+    res = torch.randn(M, N, device=DEV).bfloat16() if with_res else None
+    y = torch.relu(x.float() * sc + sh + (res.float() if with_res else 0)).bfloat16() if mask_from_y else None
+    dz, sums = C.gemm_nt_bnbwd(dy, wt, res, x, y, mean, None if mask_from_y else sc,
+                               None if mask_from_y else sh)
+    g = dy.float() @ wt.float().t()
+    if with_res:
+        g = g.bfloat16().float() + res.float()
+    g = g.bfloat16().float()
+    mask = (y.float() > 0) if mask_from_y else (x.float() * sc + sh > 0)
+    ref = g * mask
+    torch.testing.assert_close(dz.float(), ref, atol=0.05 * K ** 0.5 * 0.1 + 0.02, rtol=2e-2)
+    # reductions are of the STORED dz (what the BN apply pass consumes)
+    dzd = dz.double()
+    torch.testing.assert_close(sums[:N], dzd.sum(0), atol=1e-2, rtol=1e-4)
+    torch.testing.assert_close(sums[N:2 * N], (dzd * (x.double() - mean.double())).sum(0), atol=1e-2, rtol=1e-4)
+    assert sums[2 * N].item() == M
+
+
+def _run(blk, x, g):
+    xi = x.detach().requires_grad_()
+    y = blk(xi)
+    y.backward(g)
+    return y.float(), xi.grad.float(), {n: p.grad.float().clone() for n, p in blk.named_parameters()}
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_bottleneck_fused_bn_backward_matches_unfused(stride):
+    """bn2 (mask from its affine, consumer conv3) and the previous block's bn3
+    (mask from y, residual, consumer conv1 with the shortcut gradient) fused vs
+    DMP_FUSE_BN_BWD off: same input / parameter gradients."""
+    from distributed_model_parallel_amd.models.resnet import Bottleneck
+    from distributed_model_parallel_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(0)
+    cin, planes = 256, 64
+    down = None
+    if stride != 1:
+        down = torch.nn.Sequential(conv1x1.Conv1x1(cin, planes * 4, stride), BatchNormAct2d(planes * 4))
+    b1 = Bottleneck(cin, planes, 1)              # its bn3 output feeds b2's conv1
+    b2 = Bottleneck(cin, planes, stride, down)
+    net = cast_model(torch.nn.Sequential(b1, b2).to(DEV).to(memory_format=torch.channels_last))
+    with torch.no_grad():
+        for b in (b1, b2):
+            b.bn3.weight.normal_(1.0, 0.1)
+    ref = copy.deepcopy(net)
+    net.train()
+    ref.train()
+    x = torch.randn(8, cin, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    gg = torch.randn(8, planes * 4, 16 // stride, 16 // stride, device=DEV).bfloat16() \
+        .contiguous(memory_format=torch.channels_last)
+    old = bnops._FUSE_BWD
+    try:
+        bnops._FUSE_BWD = False
+        net2 = copy.deepcopy(ref)
+        ya2, ga2, pa2 = _run(net2, x, gg)
+        bnops._FUSE_BWD = True
+        net3 = copy.deepcopy(ref)
+        n0 = bnops._STATS["fused_bwd_moments"]
+        ya3, ga3, pa3 = _run(net3, x, gg)
+        fused = bnops._STATS["fused_bwd_moments"] - n0
+    finally:
+        bnops._FUSE_BWD = old
+    assert fused >= 3, f"expected bn2 of both blocks and b1.bn3 fused, got {fused}"
+    torch.testing.assert_close(ya3, ya2)
+    cos = F.cosine_similarity(ga3.flatten(), ga2.flatten(), dim=0).item()
+    assert cos > 0.995, cos
+    for n in pa2:
+        c = F.cosine_similarity(pa3[n].flatten(), pa2[n].flatten(), dim=0).item()
+        assert c > 0.99, (n, c)

@@ -98,6 +98,7 @@ def model():
     return m
 
 def masters_ddp(m, ddp, opt):
+    opt._ensure_state()
     flats = [st.get("master", st["param"]).float() for st in opt._flat_state]
     return [flats[gi].narrow(0, off, p.numel()).clone() for p, (gi, off) in zip(ddp._params, ddp.param_layout())]
 

@@ -117,9 +117,8 @@ def main():
     t = time.time()
     for i in range(a.warmup):
         step()
-        if i == 0:
-            torch.cuda.synchronize()
-            print(f"first step {time.time()-t:.1f}s", file=sys.stderr)
+        torch.cuda.synchronize()  # MIOpen find runs in the first steps: report progress
+        print(f"warmup step {i} done at {time.time()-t:.1f}s", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
