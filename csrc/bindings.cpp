@@ -67,6 +67,8 @@ at::Tensor cross_entropy_bwd(const at::Tensor& grad, const at::Tensor& x, const 
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
                    const c10::optional<at::Tensor>& pro_shift);
+// stem.hip
+at::Tensor space_to_depth2(const at::Tensor& x, int64_t pad, int64_t out_channels);
 std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int64_t kh,
                                 int64_t kw, int64_t stride, int64_t pad, int64_t ho, int64_t wo,
                                 bool transposed, const c10::optional<at::Tensor>& pro_scale,
@@ -74,11 +76,13 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
                                 const std::string& mode,
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
-                                const c10::optional<at::Tensor>& residual, bool relu);
+                                const c10::optional<at::Tensor>& residual, bool relu,
+                                int64_t kc);
 void set_gemm_tile(int64_t t);
+void set_phase_dgrad(bool on);
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
-                      at::ScalarType out_dtype);
+                      at::ScalarType out_dtype, int64_t kc);
 // gemm_xl.hip
 at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
@@ -163,6 +167,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none());
 
+  m.def("set_phase_dgrad", &dmp::set_phase_dgrad, py::arg("on"),
+        "strided implicit-GEMM data gradients as stride-phase launches (default on)");
   m.def("set_gemm_tile", &dmp::set_gemm_tile,
         "debug: force the NT GEMM tile variant (-1 auto, 0 256x64, 1 128x64, 2 128x128, "
         "3 128x64/4x1, 4 64x128, 5 64x64)");
@@ -173,9 +179,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("transposed") = false, py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
-        py::arg("residual") = py::none(), py::arg("relu") = false);
+        py::arg("residual") = py::none(), py::arg("relu") = false, py::arg("kc") = 0);
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
-        py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"));
+        py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
+        py::arg("kc") = 0);
+  m.def("space_to_depth2", &dmp::space_to_depth2, py::arg("x"), py::arg("pad"), py::arg("out_channels") = 16);
 
   // ---- large-tile transformer GEMM with fused bias / GELU / residual epilogues ----
   m.def("gemm_xl", &dmp::gemm_xl, py::arg("A"), py::arg("B"), py::arg("mode") = "store",

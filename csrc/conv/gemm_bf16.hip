@@ -61,6 +61,7 @@ enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2, EPI_BNBWD = 3 };
 // scatter pass (dgrad).
 struct RowMap {
   int s = 1, ho = 1, wo = 1, hi = 1, wi = 1;
+  int oy = 0, ox = 0;  // phase offset: logical (oh, ow) -> physical (oh*s + oy, ow*s + ox)
 };
 
 __device__ __forceinline__ int64_t map_row(const RowMap& g, int64_t m) {
@@ -69,7 +70,7 @@ __device__ __forceinline__ int64_t map_row(const RowMap& g, int64_t m) {
   const int64_t n = m / hw;
   const int r = (int)(m - n * hw);
   const int oh = r / g.wo, ow = r - oh * g.wo;
-  return (n * g.hi + (int64_t)oh * g.s) * g.wi + (int64_t)ow * g.s;
+  return (n * g.hi + (int64_t)oh * g.s + g.oy) * g.wi + (int64_t)ow * g.s + g.ox;
 }
 
 __device__ __forceinline__ int swz(int row, int kvec) {
@@ -83,8 +84,16 @@ __device__ __forceinline__ int swz(int row, int kvec) {
 //   transposed : A pixel = ((oh + pad - r) / stride, ...) when divisible --
 //                the data gradient of a strided conv, no flipped weights.
 // kc = channels per tap (a multiple of BK so a K tile never straddles taps).
+// transposed == 2 is the STRIDE-PHASE data gradient: one launch per output
+// phase (py, px) of a stride-s conv; its rows are the phase's sub-grid pixels
+// (a, b) (physical (a*s + py, b*s + px), written through the C row map) and its
+// K runs over only the taps that reach that phase -- ptr/ptc[i] -- each a
+// dense dy pixel (a + (py + pad - tr)/s, ...): no multiply-by-zero taps (the
+// plain transposed gather wastes (s*s - 1)/(s*s) of its K on them).
 struct ConvMap {
   int kw = 1, stride = 1, pad = 0, hi = 1, wi = 1, ho = 1, wo = 1, kc = 0, transposed = 0;
+  int py = 0, px = 0;
+  int8_t ptr[16] = {}, ptc[16] = {};
 };
 
 struct NtArgs {
@@ -190,16 +199,29 @@ void gemm_nt_kernel(const NtArgs p) {
     const int k = kt * BK + kv * 8;
     const bool kin = k < K;
     int kch = k;  // channel index of this thread's 8-vector (prologue coefficients)
+    int bk = k;   // column of B this 8-vector multiplies (differs only for phase taps)
     if constexpr (CONV) {
       // K = taps * kc with kc % BK == 0: a K tile lies inside one tap
       const int tap = (kt * BK) / cv.kc;
       kch = k - tap * cv.kc;
-      const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
+      int tr, tc;
+      if (cv.transposed == 2) {
+        tr = cv.ptr[tap];
+        tc = cv.ptc[tap];
+        bk = (tr * cv.kw + tc) * cv.kc + kch;  // the phase's taps are a subset of the weight's
+      } else {
+        tr = tap / cv.kw;
+        tc = tap - tr * cv.kw;
+      }
 #pragma unroll
       for (int i = 0; i < A_VECS; ++i) {
         int ih, iw;
         bool ok = kin && pn[i] >= 0;
-        if (cv.transposed) {  // data gradient: input pixel (ph, pw) gathers dy at (ph+pad-r)/s
+        if (cv.transposed == 2) {  // exact by construction: (py + pad - tr) % stride == 0
+          ih = ph[i] + (cv.py + cv.pad - tr) / cv.stride;
+          iw = pw[i] + (cv.px + cv.pad - tc) / cv.stride;
+          ok = ok && ih >= 0 && iw >= 0;
+        } else if (cv.transposed) {  // data gradient: input pixel (ph, pw) gathers dy at (ph+pad-r)/s
           const int th = ph[i] + cv.pad - tr, tw = pw[i] + cv.pad - tc;
           ih = th / cv.stride;
           iw = tw / cv.stride;
@@ -228,7 +250,7 @@ void gemm_nt_kernel(const NtArgs p) {
 #pragma unroll
     for (int i = 0; i < B_VECS; ++i) {
       const int col = n0 + r0 + i * ROWS_PER_PASS;
-      if (kin && col < N) rb[i] = *reinterpret_cast<const bf16x8*>(B + (int64_t)col * ldb + k);
+      if (kin && col < N) rb[i] = *reinterpret_cast<const bf16x8*>(B + (int64_t)col * ldb + bk);
       else rb[i] = bf16x8{};
     }
     if constexpr (PRO_BN) {
@@ -437,6 +459,9 @@ void launch(const NtArgs& a, hipStream_t stream) {
 
 // Tile override for experiments (set_gemm_tile; -1 = automatic).
 int g_tile_override = -1;
+// Strided transposed convs (data gradients) as stride-phase launches (default)
+// or the plain zero-tap gather (set_phase_dgrad(false), for A/B runs).
+bool g_phase_dgrad = true;
 
 template <bool PRO, int EPI, bool CONV>
 void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {
@@ -523,8 +548,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wk = wave & 1;
   const int ntiles = (N + BNT - 1) / BNT, ktiles = (K + BKT - 1) / BKT;
-  const int tile = blockIdx.x % (ntiles * ktiles);
-  const int split = blockIdx.x / (ntiles * ktiles);
+  // XCD-aware order: the ntiles*ktiles output tiles of one M split are
+  // consecutive logical ids on ONE XCD and run together, so the dy rows they
+  // all stream (and, for a 3x3 wgrad, the neighbouring taps' x rows) come
+  // from that XCD's L2 instead of HBM once per tile.
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % (ntiles * ktiles);
+  const int split = bid / (ntiles * ktiles);
   const int n0 = (tile / ktiles) * BNT, k0 = (tile % ktiles) * BKT;
   const int64_t mb = (int64_t)split * rows_per_split;
   const int64_t me = min((int64_t)M, mb + rows_per_split);
@@ -816,23 +846,29 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
 // [N, Hi, Wi, Cin] -> dW [Cout, kh*kw*Cin] (channels_last weight memory).
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
-                      at::ScalarType out_dtype) {
+                      at::ScalarType out_dtype, int64_t kc) {
   check_operand(dy, "dy");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "x must be a channels_last bf16 GPU tensor");
   const int64_t nb = x.size(0), cin = x.size(1);
-  TORCH_CHECK(cin % 64 == 0, "conv_wgrad needs input channels % 64 == 0");
+  const int64_t kcv = kc > 0 ? kc : cin;  // > cin: row taps over kc/cin consecutive pixels (conv_nt)
+  if (kc > 0) {
+    TORCH_CHECK(kcv % cin == 0 && stride == 1 && pad == 0 && (wo - 1) + (kw - 1) + kcv / cin - 1 < x.size(3) &&
+                    (ho - 1) + (kh - 1) < x.size(2),
+                "row-tap conv_wgrad: kc must be a multiple of Cin, stride 1, pad 0, taps inside the input");
+  }
+  TORCH_CHECK(kcv % 64 == 0, "conv_wgrad needs channels per tap % 64 == 0");
   TORCH_CHECK(dy.size(0) == nb * ho * wo, "dy rows must be N*Ho*Wo");
   TORCH_CHECK(dy.size(1) % 8 == 0, "output channels must be a multiple of 8");
   ConvMap cm;
   cm.kw = (int)kw; cm.stride = (int)stride; cm.pad = (int)pad;
   cm.hi = (int)x.size(2); cm.wi = (int)x.size(3); cm.ho = (int)ho; cm.wo = (int)wo;
-  cm.kc = (int)cin;
-  const int M = (int)dy.size(0), N = (int)dy.size(1), K = (int)(kh * kw * cin);
-  // B rows are addressed through the map; ldb = Cin
+  cm.kc = (int)kcv;
+  const int M = (int)dy.size(0), N = (int)dy.size(1), K = (int)(kh * kw * kcv);
+  // B rows are addressed through the map; ldb = Cin (pixel stride)
   auto xv = x.permute({0, 2, 3, 1}).reshape({-1, cin});
-  return run_tn(dy, xv, M, N, K, out_dtype, cm, (int)(cin % 128 == 0 ? 128 : 64));
+  return run_tn(dy, xv, M, N, K, out_dtype, cm, (int)(kcv % 128 == 0 ? 128 : 64));
 }
 
 namespace {
@@ -995,18 +1031,70 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
                                 const std::string& mode,
                                 const c10::optional<at::Tensor>& epi_scale,
                                 const c10::optional<at::Tensor>& epi_shift,
-                                const c10::optional<at::Tensor>& residual, bool relu) {
+                                const c10::optional<at::Tensor>& residual, bool relu,
+                                int64_t kc) {
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4,
               "x must be a 4-D bf16 GPU tensor");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last");
   check_operand(wmat, "wmat");
   const int64_t nb = x.size(0), cin = x.size(1), hi = x.size(2), wi = x.size(3);
-  TORCH_CHECK(cin % BK == 0, "conv_nt needs input channels % 64 == 0");
-  TORCH_CHECK(wmat.size(1) == kh * kw * cin, "wmat must be [Cout, kh*kw*Cin]");
+  // kc > cin: ROW TAPS -- tap (r, c) reads kc / cin CONSECUTIVE pixels starting at
+  // (oh + r, ow + c) as one kc-channel operand (the pixels are adjacent in NHWC
+  // memory, overlapping between neighbouring outputs).  Lets a few-channel
+  // input (the ResNet stem after space-to-depth: 16 channels) run on the
+  // 64-deep K tiles: a 4x4 kernel becomes 4 row taps of 64.
+  const int64_t kcv = kc > 0 ? kc : cin;
+  if (kc > 0) {
+    TORCH_CHECK(!transposed && kcv % cin == 0 && stride == 1 && pad == 0 &&
+                    (wo - 1) + (kw - 1) + kcv / cin - 1 < wi && (ho - 1) + (kh - 1) < hi,
+                "row-tap conv_nt: kc must be a multiple of Cin, stride 1, pad 0, taps inside the input");
+  }
+  TORCH_CHECK(kcv % BK == 0, "conv_nt needs channels per tap % 64 == 0");
+  TORCH_CHECK(wmat.size(1) == kh * kw * kcv, "wmat must be [Cout, kh*kw*kc]");
   TORCH_CHECK(wmat.size(0) % 8 == 0, "output channels must be a multiple of 8");
   TORCH_CHECK(ho > 0 && wo > 0 && stride >= 1 && pad >= 0, "bad conv geometry");
   if (pro_scale.has_value() && pro_scale->defined())
     TORCH_CHECK(pro_scale->numel() == cin, "prologue coefficients must have Cin entries");
+  if (transposed && stride > 1 && g_phase_dgrad && mode == "store" &&
+      !(pro_scale.has_value() && pro_scale->defined())) {
+    TORCH_CHECK(kh * kw <= 16, "phase dgrad supports up to 16 taps");
+    // dx [N*ho*wo, Cout'] written phase by phase: every row exactly once
+    auto C = at::empty({nb * ho * wo, wmat.size(0)}, x.options());
+    for (int py = 0; py < stride; ++py)
+      for (int px = 0; px < stride; ++px) {
+        const int64_t ha = (ho - py + stride - 1) / stride, wa = (wo - px + stride - 1) / stride;
+        if (ha <= 0 || wa <= 0) continue;
+        NtArgs a{};
+        int nt = 0;
+        for (int r = 0; r < kh; ++r)
+          for (int c = 0; c < kw; ++c)
+            if ((py + pad - r) % stride == 0 && (px + pad - c) % stride == 0) {
+              a.cv.ptr[nt] = (int8_t)r;
+              a.cv.ptc[nt] = (int8_t)c;
+              ++nt;
+            }
+        if (nt == 0) {  // no tap reaches this phase: its dx rows are zero
+          C.view({nb, ho, wo, -1}).slice(1, py, ho, stride).slice(2, px, wo, stride).zero_();
+          continue;
+        }
+        a.cv.kw = (int)kw; a.cv.stride = (int)stride; a.cv.pad = (int)pad;
+        a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ha; a.cv.wo = (int)wa;
+        a.cv.kc = (int)cin; a.cv.transposed = 2; a.cv.py = py; a.cv.px = px;
+        a.cmap.s = (int)stride; a.cmap.ho = (int)ha; a.cmap.wo = (int)wa;
+        a.cmap.hi = (int)ho; a.cmap.wi = (int)wo; a.cmap.oy = py; a.cmap.ox = px;
+        a.M = (int)(nb * ha * wa);
+        a.N = (int)wmat.size(0);
+        a.K = nt * (int)cin;
+        a.A = reinterpret_cast<const bf16*>(x.data_ptr());
+        a.lda = cin;
+        a.B = reinterpret_cast<const bf16*>(wmat.data_ptr());
+        a.ldb = wmat.stride(0);
+        a.C = reinterpret_cast<bf16*>(C.data_ptr());
+        a.ldc = C.stride(0);
+        run_nt(a, true, x, pro_scale, pro_shift, mode, epi_scale, epi_shift, residual, relu, C);
+      }
+    return {C, at::Tensor()};
+  }
   NtArgs a{};
   a.cv.kw = (int)kw;
   a.cv.stride = (int)stride;
@@ -1015,12 +1103,12 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
   a.cv.wi = (int)wi;
   a.cv.ho = (int)ho;
   a.cv.wo = (int)wo;
-  a.cv.kc = (int)cin;
+  a.cv.kc = (int)kcv;
   a.cv.transposed = transposed;
   TORCH_CHECK(nb * ho * wo < (1LL << 31), "too many output pixels");
   a.M = (int)(nb * ho * wo);
   a.N = (int)wmat.size(0);
-  a.K = (int)(kh * kw * cin);
+  a.K = (int)(kh * kw * kcv);
   auto C = at::empty({a.M, a.N}, x.options());
   a.A = reinterpret_cast<const bf16*>(x.data_ptr());
   a.lda = cin;
@@ -1081,5 +1169,6 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
 }
 
 void set_gemm_tile(int64_t t) { g_tile_override = (int)t; }
+void set_phase_dgrad(bool on) { g_phase_dgrad = on; }
 
 }  // namespace dmp

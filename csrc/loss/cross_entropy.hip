@@ -123,7 +123,7 @@ std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& x, const at::Tensor&
   hipLaunchKernelGGL(ce_reduce_kernel, dim3(1), dim3(256), 0, stream, row_loss.data_ptr<float>(),
                      target.data_ptr<int64_t>(), B, ignore_index, stats.data_ptr<float>());
   DMP_HIP_CHECK(hipGetLastError());
-  return {stats.narrow(0, 0, 1).view({}), lse, stats};
+  return {stats.select(0, 0), lse, stats};  // 0-d view of the loss
 }
 
 at::Tensor cross_entropy_bwd(const at::Tensor& grad, const at::Tensor& x, const at::Tensor& target,

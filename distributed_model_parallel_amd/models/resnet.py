@@ -23,6 +23,7 @@ from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, grad_tap
 from ..ops.pool import MaxPool2d, global_avg_pool
+from ..ops.stem import StemConv2d
 
 
 # bn2 -> conv3 prologue fusion (ops/fused.py bn_relu_conv1x1).  Off by default:
@@ -105,7 +106,8 @@ class ResNet(nn.Module):
                  stem_channels: int = 64):
         super().__init__()
         self.inplanes = stem_channels
-        self.conv1 = nn.Conv2d(3, stem_channels, 7, stride=2, padding=3, bias=False)
+        # 7x7/s2 stem as a space-to-depth MFMA implicit GEMM with fused BN moments
+        self.conv1 = StemConv2d(3, stem_channels)
         self.bn1 = BatchNormAct2d(stem_channels, act="relu")
         self.maxpool = MaxPool2d(3, stride=2, padding=1)  # NHWC kernel, byte argmax
         self.layer1 = self._make_layer(block, 64, layers[0])
@@ -141,7 +143,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        x = self.maxpool(conv_bn(self.conv1, self.bn1, x))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return global_avg_pool(x)  # channels-last broadcast backward (ops/pool.py)
 

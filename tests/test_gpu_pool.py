@@ -81,10 +81,12 @@ def test_global_avg_pool_matches_torch(dtype):
 @pytest.mark.parametrize("k,s,p", [(3, 2, 1), (3, 1, 1)])
 def test_maxpool_all_neg_inf_border_window(k, s, p):
     # every value -inf: each window's gradient must land on its first in-bounds
-    # pixel (PyTorch), not on a padding tap that the backward can never match
+    # pixel -- PyTorch's CPU / NCHW semantics (its GPU NHWC kernel instead routes
+    # every such window to absolute index 0), not on a padding tap that the
+    # backward can never match (the gradient would be dropped)
     x = torch.full((1, 8, 6, 6), float("-inf"), device="cuda").contiguous(memory_format=torch.channels_last)
     xi = x.detach().requires_grad_()
-    xr = x.detach().requires_grad_()
+    xr = x.detach().cpu().contiguous().requires_grad_()
     max_pool2d(xi, k, s, p).sum().backward()
     F.max_pool2d(xr, k, s, p).sum().backward()
-    torch.testing.assert_close(xi.grad, xr.grad)
+    torch.testing.assert_close(xi.grad.cpu(), xr.grad)

@@ -115,10 +115,18 @@ def main():
         return loss
 
     t = time.time()
+    import threading
+    done = threading.Event()
+
+    def heartbeat():  # MIOpen find over every stock conv can take minutes in step 0
+        while not done.wait(30):
+            print(f"  ... still warming up at {time.time() - t:.0f}s", file=sys.stderr, flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     for i in range(a.warmup):
         step()
         torch.cuda.synchronize()  # MIOpen find runs in the first steps: report progress
         print(f"warmup step {i} done at {time.time()-t:.1f}s", file=sys.stderr, flush=True)
+    done.set()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):

@@ -99,7 +99,14 @@ def main():
             dy, x, w, None, (s, s), (pad, pad), (1, 1), False, (0, 0), 1, (True, False, False)))
         res["wgrad"]["miopen"] = timeit(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, (s, s), (pad, pad), (1, 1), False, (0, 0), 1, (False, True, False)))
-        if k == 1:
+        if name == "stem":
+            from distributed_model_parallel_amd.ops.stem import stem_wmat
+            wm = stem_wmat(w)
+            res["fwd"]["ours"] = timeit(lambda: C.conv_nt(C.space_to_depth2(x, 3), wm, 4, 1, 1, 0, ho, ho,
+                                                          mode="moments", kc=64))
+            s2d = C.space_to_depth2(x, 3)
+            res["wgrad"]["ours"] = timeit(lambda: C.conv_wgrad(dy2, s2d, 4, 1, 1, 0, ho, ho, dt, kc=64))
+        elif k == 1:
             w2 = w.view(cout, cin)
             wt = w2.t().contiguous()
             res["fwd"]["ours"] = timeit(lambda: C.gemm_nt(x2, w2, mode="moments", a_map=geom))
