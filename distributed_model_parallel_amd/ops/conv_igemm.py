@@ -4,11 +4,11 @@ emitting the BatchNorm moments of its output like the 1x1 path.
 
   forward   y[N*Ho*Wo, Cout] = im2col(x) @ W^T      tap gather in the A staging,
             K = kh*kw*Cin, W read in its channels_last memory [Cout][kh][kw][Cin]
-  (backward defaults to MIOpen -- see NATIVE_BWD -- our kernels below are
-   selectable and tested)
+  (backward: per-shape choice between ours and MIOpen -- see _use_native)
   dgrad     dx = "transposed" implicit GEMM over dy with W permuted to
             [Cin][kh][kw][Cout] (no flip; strided convs handled by the
-            divisibility test in the gather)
+            divisibility test in the gather; strided convs run as one launch per
+            stride phase over only the taps that reach it)
   wgrad     dW[Cout, kh*kw*Cin] = dy^T @ im2col(x)   split-M TN kernel with the
             tap gather in its B staging (channels_last weight memory directly)
 
@@ -32,12 +32,24 @@ from .. import _native
 _STATS = {"native": 0, "torch": 0}
 # DMP_IGEMM=0 routes these convs to MIOpen (A/B comparisons, debugging)
 ENABLED = os.environ.get("DMP_IGEMM", "1") != "0"
-# Backward on our kernels (DMP_IGEMM_BWD=1) or MIOpen (default).  Measured on
-# MI355X at the ResNet-50 bs256 shapes (profiles/conv3x3_igemm.md): our forward
-# beats MIOpen at every shape (and emits the BN moments for free); MIOpen's
-# data / weight gradients are still faster (stride-2 dgrad by ~3x: our
-# transposed gather multiplies zero taps).
-NATIVE_BWD = os.environ.get("DMP_IGEMM_BWD", "0") == "1"
+# Backward backend per pass: DMP_IGEMM_BWD=1 (ours everywhere), 0 (MIOpen
+# everywhere) or auto (default): ours where the per-shape table below measured
+# it at least as fast as MIOpen's tuned solution (tools/conv_roofline.py,
+# profiles/conv_roofline_r2.md), MIOpen elsewhere.
+_BWD_MODE = os.environ.get("DMP_IGEMM_BWD", "auto")
+NATIVE_BWD = _BWD_MODE == "1"
+
+# (pass, Cin, H_in, stride) of ResNet-50's 3x3 convs where our kernel won at
+# batch 1024 on MI355X; everything else goes to MIOpen in "auto" mode.
+_OURS_FASTER = set()
+
+
+def _use_native(pass_: str, cin: int, h: int, stride: int) -> bool:
+    if NATIVE_BWD:
+        return True
+    if _BWD_MODE == "0":
+        return False
+    return (pass_, cin, h, stride) in _OURS_FASTER
 
 
 def _out_size(h: int, k: int, s: int, p: int) -> int:
@@ -87,16 +99,19 @@ class _ConvIGFn(torch.autograd.Function):
         cout, _, kh, kw = weight.shape
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        if not NATIVE_BWD:
+        nat_d = ctx.needs_input_grad[0] and _use_native("dgrad", cin, h, stride)
+        nat_w = ctx.needs_input_grad[1] and _use_native("wgrad", cin, h, stride)
+        want_d = ctx.needs_input_grad[0] and not nat_d
+        want_w = ctx.needs_input_grad[1] and not nat_w
+        if want_d or want_w:
             dx, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
-                [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False])
-            return dx, dw, None, None, None
-        if ctx.needs_input_grad[0]:
+                [want_d, want_w, False])
+        if nat_d:
             wt = weight.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()  # [Cin][kh][kw][Cout]
             dx2, _ = C.conv_nt(dy, wt, kh, kw, stride, pad, h, w, transposed=True)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
+        if nat_w:
             dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
             g = C.conv_wgrad(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
             dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
