@@ -25,15 +25,16 @@ def _lib():
     _tried = True
     if os.environ.get("DMP_DISABLE_ROCTX") == "1":
         return None
-    cands = []
+    # rocprofiler-sdk's roctx first -- what rocprofv3 --marker-trace intercepts (the
+    # native reducer resolves the same library, csrc/trace.h) -- then the legacy
+    # roctracer one (torch's bundled copy last: rocprofv3 does not see it)
+    cands = ["librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+             "libroctx64.so", "/opt/rocm/lib/libroctx64.so"]
     try:
         import torch
         cands.append(os.path.join(os.path.dirname(torch.__file__), "lib", "libroctx64.so"))
     except Exception:  # noqa: BLE001
         pass
-    # rocprofiler-sdk's roctx first (what rocprofv3 --marker-trace intercepts), then legacy
-    cands += ["librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
-              "libroctx64.so", "/opt/rocm/lib/libroctx64.so"]
     for c in cands:
         if os.path.isabs(c) and not os.path.exists(c):
             continue
