@@ -88,6 +88,13 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out);
 void set_gemm_xl_bn(int bn, int pipe, int group_m);
+std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
+                                     const c10::optional<at::Tensor>& residual,
+                                     const c10::optional<at::Tensor>& bn_x,
+                                     const c10::optional<at::Tensor>& bn_y,
+                                     const c10::optional<at::Tensor>& mean,
+                                     const c10::optional<at::Tensor>& scale,
+                                     const c10::optional<at::Tensor>& shift);
 // attention.hip
 bool attention_supported(int64_t S, int64_t head_dim);
 std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale);
@@ -189,6 +196,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_xl", &dmp::gemm_xl, py::arg("A"), py::arg("B"), py::arg("mode") = "store",
         py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("residual") = py::none(), py::arg("out") = py::none());
+  m.def("gemm_xl_conv", &dmp::gemm_xl_conv, py::arg("A"), py::arg("B"), py::arg("mode"),
+        py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
+        py::arg("mean") = py::none(), py::arg("scale") = py::none(), py::arg("shift") = py::none());
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
 

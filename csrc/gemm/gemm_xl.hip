@@ -47,7 +47,10 @@ namespace {
 using bf16 = __bf16;
 constexpr int XBM = 256, XBK = 64, XTHREADS = 512;
 
-enum XlEpi { XL_STORE = 0, XL_BIAS = 1, XL_BIAS_GELU = 2, XL_DGELU = 3, XL_BIAS_RES = 4 };
+enum XlEpi { XL_STORE = 0, XL_BIAS = 1, XL_BIAS_GELU = 2, XL_DGELU = 3, XL_BIAS_RES = 4,
+             // conv epilogues (same semantics as gemm_bf16.hip's EPI_MOMENTS /
+             // EPI_AFFINE "add" / EPI_BNBWD), for the wide 1x1 conv GEMMs
+             XL_MOMENTS = 5, XL_ADD = 6, XL_BNBWD = 7 };
 
 using gptr_t = const __attribute__((address_space(1))) void*;
 using lptr_t = __attribute__((address_space(3))) void*;
@@ -106,8 +109,13 @@ struct XlArgs {
   int M, N, K;
   const bf16* bias;             // [N] (XL_BIAS*)
   bf16* aux; int64_t ldaux;     // XL_BIAS_GELU: pre-activation out; XL_DGELU: pre-activation in
-  const bf16* R; int64_t ldr;   // XL_BIAS_RES residual
+  const bf16* R; int64_t ldr;   // XL_BIAS_RES / XL_ADD / XL_BNBWD residual (optional for BNBWD)
   int group_m;                  // tile-order group height (M tiles)
+  float* part;                  // XL_MOMENTS / XL_BNBWD partials [2][mtiles][N]
+  double* zsums;                // moments target to zero (common.h) or null
+  const bf16* bx; int64_t ldbx; // XL_BNBWD: BN input x [M, N]
+  const bf16* bny; int64_t ldby;// XL_BNBWD: BN output y [M, N] (mask source) or null
+  const float *bmean, *bsc, *bsh;
 };
 
 template <int BN, int EPI, int PIPE>
@@ -123,6 +131,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   constexpr int W2 = 2 * (NA + NB);  // glds per wave per K tile
   static_assert(NA >= 1 && NB >= 1, "region smaller than one glds round");
   __shared__ __attribute__((aligned(16))) char smem[LDS];
+  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD;
+  if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
 
   const bf16* __restrict__ A = p.A;
   const bf16* __restrict__ B = p.B;
@@ -335,6 +345,18 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   constexpr int CV = BN / 8, RPP = XTHREADS / CV;
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
+  float msum[8], msq[8], bmu[8], bsc[8], bsh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = 0.f; }
+  if constexpr (EPI == XL_BNBWD) {
+    if (col < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bmu[j] = p.bmean[col + j];
+        if (!p.bny) { bsc[j] = p.bsc[col + j]; bsh[j] = p.bsh[col + j]; }
+      }
+    }
+  }
   if (col < N) {
 #pragma unroll 4
     for (int pr = 0; pr < XBM / RPP; ++pr) {
@@ -342,7 +364,36 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       const int row = m0 + lr;
       if (row >= M) break;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
-      if constexpr (EPI == XL_BIAS_GELU) {
+      if constexpr (EPI == XL_MOMENTS) {
+        const f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { msum[j] += f[j]; msq[j] = fmaf(f[j], f[j], msq[j]); }
+      } else if constexpr (EPI == XL_ADD) {
+        f32x8 f = __builtin_convertvector(v, f32x8);
+        f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+        v = __builtin_convertvector(f, bf16x8);
+      } else if constexpr (EPI == XL_BNBWD) {
+        f32x8 g = __builtin_convertvector(v, f32x8);
+        if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
+          g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+          v = __builtin_convertvector(g, bf16x8);
+          g = __builtin_convertvector(v, f32x8);
+        }
+        const f32x8 xv =
+            __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bx + (int64_t)row * p.ldbx + col), f32x8);
+        f32x8 yv{};
+        if (p.bny)
+          yv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bny + (int64_t)row * p.ldby + col), f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool on = p.bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);
+          const float dz = on ? g[j] : 0.f;
+          g[j] = dz;
+          msum[j] += dz;
+          msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+        }
+        v = __builtin_convertvector(g, bf16x8);
+      } else if constexpr (EPI == XL_BIAS_GELU) {
         *reinterpret_cast<bf16x8*>(p.aux + (int64_t)row * p.ldaux + col) = v;
         f32x8 f = __builtin_convertvector(v, f32x8);
 #pragma unroll
@@ -363,6 +414,29 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         v = __builtin_convertvector(f, bf16x8);
       }
       *reinterpret_cast<bf16x8*>(p.C + (int64_t)row * p.ldc + col) = v;
+    }
+  }
+  if constexpr (kMom) {
+    // fold the RPP row groups of each column through LDS: one partial per M tile
+    static_assert(2 * RPP * BN * 4 <= LDS, "moments scratch exceeds LDS");
+    __syncthreads();  // every thread finished reading the C tile
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(0 * RPP + rr0) * BN + cvi * 8 + j] = msum[j];
+      red[(1 * RPP + rr0) * BN + cvi * 8 + j] = msq[j];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += XTHREADS) {
+      float s0 = 0.f, q0 = 0.f;
+      for (int g = 0; g < RPP; ++g) {
+        s0 += red[(0 * RPP + g) * BN + c];
+        q0 += red[(1 * RPP + g) * BN + c];
+      }
+      if (n0 + c < N) {
+        p.part[(int64_t)mt * N + n0 + c] = s0;
+        p.part[(int64_t)(mtiles + mt) * N + n0 + c] = q0;
+      }
     }
   }
 }
@@ -611,6 +685,14 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
 
 template <int EPI>
 void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
+  if constexpr (EPI >= XL_MOMENTS) {  // conv epilogues: ring kernel only (no persistent form)
+    const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + bn - 1) / bn);
+    if (bn == 128)
+      hipLaunchKernelGGL((gemm_xl_nt_kernel<128, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    else
+      hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    return;
+  }
   if (bn == 128) launch_xl<128, EPI>(a, s);
   else launch_xl<256, EPI>(a, s);
 }
@@ -708,6 +790,86 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
   }
   DMP_HIP_CHECK(hipGetLastError());
   return C;
+}
+
+// bn_reduce_partials_launch: batchnorm.hip
+void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
+                               hipStream_t stream);
+
+// Wide 1x1-conv GEMMs with the conv epilogues on the glds-ring kernel:
+//   "moments": C = bf16(A @ B^T), returns fp64 [2N+1] (sum, sum^2, M) of C
+//   "add"    : C = bf16(bf16(A @ B^T) + residual)
+//   "bnbwd"  : C = dz = mask * bf16(A @ B^T (+ residual)), returns (sum dz, sum dz*(x-mean), M)
+//              (same contract as gemm_nt_bnbwd)
+std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
+                                     const c10::optional<at::Tensor>& residual,
+                                     const c10::optional<at::Tensor>& bn_x,
+                                     const c10::optional<at::Tensor>& bn_y,
+                                     const c10::optional<at::Tensor>& mean,
+                                     const c10::optional<at::Tensor>& scale,
+                                     const c10::optional<at::Tensor>& shift) {
+  check_bf16_2d(A, "A");
+  check_bf16_2d(B, "B");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && K % XBK == 0 && K >= XBK && N % 8 == 0, "gemm_xl_conv: bad shape");
+  TORCH_CHECK(M > 0 && M < (1LL << 31), "gemm_xl_conv: M out of range");
+  int epi;
+  if (mode == "moments") epi = XL_MOMENTS;
+  else if (mode == "add") epi = XL_ADD;
+  else if (mode == "bnbwd") epi = XL_BNBWD;
+  else TORCH_CHECK(false, "gemm_xl_conv: unknown mode ", mode);
+  auto C = at::empty({M, N}, A.options());
+  XlArgs a{};
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
+  a.C = reinterpret_cast<bf16*>(C.data_ptr()); a.ldc = C.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+  if (residual.has_value() && residual->defined()) {
+    check_bf16_2d(*residual, "residual");
+    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_xl_conv: residual shape");
+    a.R = reinterpret_cast<const bf16*>(residual->data_ptr());
+    a.ldr = residual->stride(0);
+  }
+  TORCH_CHECK(epi != XL_ADD || a.R, "gemm_xl_conv: add needs a residual");
+  auto f32vec = [&](const c10::optional<at::Tensor>& t, const char* name) {
+    TORCH_CHECK(t.has_value() && t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                    t->numel() == N, name, " must be a contiguous fp32 [N] GPU tensor");
+    return t->data_ptr<float>();
+  };
+  if (epi == XL_BNBWD) {
+    TORCH_CHECK(bn_x.has_value(), "bnbwd needs bn_x");
+    check_bf16_2d(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->size(0) == M && bn_x->size(1) == N, "bn_x shape");
+    a.bx = reinterpret_cast<const bf16*>(bn_x->data_ptr()); a.ldbx = bn_x->stride(0);
+    a.bmean = f32vec(mean, "mean");
+    if (bn_y.has_value() && bn_y->defined()) {
+      check_bf16_2d(*bn_y, "bn_y");
+      TORCH_CHECK(bn_y->size(0) == M && bn_y->size(1) == N, "bn_y shape");
+      a.bny = reinterpret_cast<const bf16*>(bn_y->data_ptr()); a.ldby = bn_y->stride(0);
+    } else {
+      a.bsc = f32vec(scale, "scale");
+      a.bsh = f32vec(shift, "shift");
+    }
+  }
+  const int bn = pick_bn((int)M, (int)N);
+  at::Tensor sums, part;
+  const int mtiles = (int)((M + XBM - 1) / XBM);
+  if (epi != XL_ADD) {
+    part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
+    sums = at::empty({2 * N + 1}, A.options().dtype(at::kDouble));
+    a.part = part.data_ptr<float>();
+    a.zsums = moments_zero_target(sums.data_ptr<double>(), mtiles);
+  }
+  hipStream_t s = at::hip::getCurrentHIPStream();
+  switch (epi) {
+    case XL_MOMENTS: dispatch_bn<XL_MOMENTS>(a, bn, s); break;
+    case XL_ADD: dispatch_bn<XL_ADD>(a, bn, s); break;
+    default: dispatch_bn<XL_BNBWD>(a, bn, s); break;
+  }
+  DMP_HIP_CHECK(hipGetLastError());
+  if (epi != XL_ADD) bn_reduce_partials_launch(a.part, mtiles, (int)N, sums.data_ptr<double>(), (double)M, s);
+  return {C, sums};
 }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0}
+_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0}
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -50,6 +50,14 @@ def _blaslt_dgrad(m: int, cin: int, cout: int) -> bool:
     return cout >= 1024 and m <= 65536
 
 
+def _xl(n: int, k: int) -> bool:
+    """Output width N, reduction K of a 1x1-conv GEMM where the 8-wave glds-ring
+    kernel (gemm_xl_conv) measured faster than the 4-wave NT kernel with the
+    same epilogue (profiles/conv1x1_xl.md, batch 1024): wide outputs with a
+    moderate K.  Narrow N (<= 128) and very short / very deep K stay on NT."""
+    return k >= 128 and k % 64 == 0 and (n >= 512 or (n >= 256 and k <= 512))
+
+
 def _geom(stride: int, hi: int, wi: int):
     """Row map [s, Ho, Wo, Hi, Wi] the kernels use to address a stride-s grid in place."""
     if stride == 1:
@@ -66,7 +74,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         ho, wo = (geom[1], geom[2]) if geom else (h, w)
         w2 = weight.reshape(weight.shape[0], cin)
         # strided convs read the sampled rows in place (no subsample copy)
-        y2, mom = C.gemm_nt(_rows(x), w2, mode="moments" if moments else "store", a_map=geom)
+        if moments and not geom and _xl(w2.shape[0], cin):
+            _STATS["xl"] += 1
+            y2, mom = C.gemm_xl_conv(_rows(x), w2, "moments")
+        else:
+            y2, mom = C.gemm_nt(_rows(x), w2, mode="moments" if moments else "store", a_map=geom)
         ctx.save_for_backward(x, weight)
         ctx.geom = geom
         ctx.slot = slot
@@ -111,8 +123,14 @@ class _Conv1x1Fn(torch.autograd.Function):
                 sc = sh = None
                 if bs.y2 is None:
                     sc, sh = bs.mask_affine()
-                dx2, sums = C.gemm_nt_bnbwd(dy2, w2.t().contiguous(), extra, bs.x2, bs.y2,
-                                            bs.mean.contiguous(), sc, sh)
+                if _xl(cin, cout):
+                    _STATS["xl"] += 1
+                    dx2, sums = C.gemm_xl_conv(dy2, w2.t().contiguous(), "bnbwd", residual=extra,
+                                               bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean.contiguous(),
+                                               scale=sc, shift=sh)
+                else:
+                    dx2, sums = C.gemm_nt_bnbwd(dy2, w2.t().contiguous(), extra, bs.x2, bs.y2,
+                                                bs.mean.contiguous(), sc, sh)
                 dx = _unrows(dx2, n, h, w)
                 bs.park(dx, sums[: 2 * cin])
                 dx2 = None

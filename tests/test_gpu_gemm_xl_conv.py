@@ -1,0 +1,61 @@
+"""gemm_xl conv epilogues (moments / add / bnbwd) on the glds-ring kernel must
+agree with the 4-wave NT kernel's (gemm_nt / gemm_nt_bnbwd) -- same math,
+same rounding points -- and with fp64 sums of what they store."""
+import pytest
+import torch
+
+from distributed_model_parallel_amd import _native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def C():
+    return _native.require("gemm_xl_conv tests")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 64), (3001, 512, 128), (50176, 1024, 256), (700, 128, 192)])
+def test_xl_moments_matches_nt(M, N, K):
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    c, mom = C().gemm_xl_conv(a, b, "moments")
+    c0, _ = C().gemm_nt(a, b)
+    torch.testing.assert_close(c.float(), c0.float(), atol=2e-2, rtol=1e-2)
+    cd = c.double()
+    torch.testing.assert_close(mom[:N], cd.sum(0), atol=1e-2, rtol=1e-4)
+    torch.testing.assert_close(mom[N:2 * N], (cd * cd).sum(0), atol=1e-2, rtol=1e-4)
+    assert mom[2 * N].item() == M
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 64), (1999, 512, 256)])
+def test_xl_add_matches_nt(M, N, K):
+    torch.manual_seed(1)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    r = torch.randn(M, N, device=DEV).bfloat16()
+    c, _ = C().gemm_xl_conv(a, b, "add", residual=r)
+    c0, _ = C().gemm_nt(a, b, mode="add", residual=r)
+    torch.testing.assert_close(c.float(), c0.float(), atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("mask_from_y", [False, True])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_xl_bnbwd_matches_nt(mask_from_y, with_res):
+    torch.manual_seed(2)
+    M, N, K = 5000, 256, 128
+    dy = torch.randn(M, K, device=DEV).bfloat16()
+    wt = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    x = torch.randn(M, N, device=DEV).bfloat16()
+    mean = x.float().mean(0)
+    sc = torch.rand(N, device=DEV) + 0.5
+    sh = torch.randn(N, device=DEV) * 0.5
+    res = torch.randn(M, N, device=DEV).bfloat16() if with_res else None
+    y = torch.relu(x.float() * sc + sh).bfloat16() if mask_from_y else None
+    s_, t_ = (None, None) if mask_from_y else (sc, sh)
+    dz, sums = C().gemm_xl_conv(dy, wt, "bnbwd", residual=res, bn_x=x, bn_y=y, mean=mean, scale=s_, shift=t_)
+    dz0, sums0 = C().gemm_nt_bnbwd(dy, wt, res, x, y, mean, s_, t_)
+    torch.testing.assert_close(dz.float(), dz0.float(), atol=2e-2, rtol=1e-2)
+    dzd = dz.double()
+    torch.testing.assert_close(sums[:N], dzd.sum(0), atol=1e-2, rtol=1e-4)
+    torch.testing.assert_close(sums[N:2 * N], (dzd * (x.double() - mean.double())).sum(0), atol=1e-2, rtol=1e-4)
