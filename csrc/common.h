@@ -81,6 +81,23 @@ __device__ __forceinline__ void zero_moments(double* z, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) z[i] = 0.0;
 }
 
+// A stride-s "compact" residual: it holds the values of the full-resolution
+// row m = (n*hi + h)*wi + w only at (h, w) = (s*a, s*b) -- the data gradient
+// of a stride-s 1x1 conv (a ResNet downsample), which is zero everywhere
+// else.  compact_row returns that row of the compact tensor, or -1 (zero).
+struct CompactMap {
+  int s = 1, ho = 1, wo = 1, hi = 1, wi = 1;
+};
+__device__ __forceinline__ int64_t compact_row(const CompactMap& c, int64_t m) {
+  if (c.s == 1) return m;
+  const int64_t hw = (int64_t)c.hi * c.wi;
+  const int64_t n = m / hw;
+  const int r = (int)(m - n * hw);
+  const int h = r / c.wi, w = r - h * c.wi;
+  if (h % c.s != 0 || w % c.s != 0) return -1;
+  return (n * c.ho + h / c.s) * c.wo + w / c.s;
+}
+
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5.5 T1):
 // consecutive logical tiles land on the same XCD (same L2).
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

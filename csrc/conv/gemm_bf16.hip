@@ -114,6 +114,7 @@ struct NtArgs {
   const bf16* bx; int64_t ldbx;
   const bf16* bny; int64_t ldby;
   const float *bmean, *bsc, *bsh;
+  CompactMap rmap;              // EPI_BNBWD residual R in compact stride-s form
 };
 
 // NT = WAVES_M*WAVES_N*64 threads: 4 waves (2 blocks/CU) or 8 waves (256-row
@@ -363,6 +364,7 @@ void gemm_nt_kernel(const NtArgs p) {
   const bf16* __restrict__ bnx = p.bx;
   const bf16* __restrict__ bny = p.bny;
   const int64_t ldbx = p.ldbx, ldby = p.ldby;
+  const CompactMap rmap = p.rmap;
   if constexpr (EPI == EPI_BNBWD) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -391,7 +393,9 @@ void gemm_nt_kernel(const NtArgs p) {
       if constexpr (EPI == EPI_BNBWD) {
         f32x8 g = __builtin_convertvector(v, f32x8);
         if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
-          g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + (int64_t)row * ldr + col), f32x8);
+          const int64_t rr = compact_row(rmap, row);
+          if (rr >= 0)
+            g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + rr * ldr + col), f32x8);
           v = __builtin_convertvector(g, bf16x8);
           g = __builtin_convertvector(v, f32x8);
         }
@@ -923,7 +927,9 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
     epi = mode == "moments" ? EPI_MOMENTS : EPI_BNBWD;
     if (epi == EPI_BNBWD && residual.has_value() && residual->defined()) {
       check_operand(*residual, "residual");
-      TORCH_CHECK(residual->size(0) == a.M && residual->size(1) == a.N, "residual shape");
+      const int64_t rrows = a.rmap.s == 1 ? a.M
+                                          : (int64_t)a.M / ((int64_t)a.rmap.hi * a.rmap.wi) * a.rmap.ho * a.rmap.wo;
+      TORCH_CHECK(residual->size(0) == rrows && residual->size(1) == a.N, "residual shape");
       a.R = reinterpret_cast<const bf16*>(residual->data_ptr());
       a.ldr = residual->stride(0);
     }
@@ -1124,15 +1130,28 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
 //   G  = bf16(A @ B^T (+ residual))          A = dy [M, K], B = W^T [N, K]
 //   dz = G * mask,  mask = y > 0 (bn_y given) or x*scale + shift > 0
 //   returns (dz [M, N], fp64 [2N+1] = (sum dz, sum dz*(x - mean), M))
+CompactMap parse_compact(const std::vector<int64_t>& g, int64_t M) {
+  CompactMap c;
+  if (g.empty()) return c;
+  TORCH_CHECK(g.size() == 5, "res_map must be [stride, Ho, Wo, Hi, Wi]");
+  c.s = (int)g[0]; c.ho = (int)g[1]; c.wo = (int)g[2]; c.hi = (int)g[3]; c.wi = (int)g[4];
+  TORCH_CHECK(c.s >= 1 && c.ho == (c.hi + c.s - 1) / c.s && c.wo == (c.wi + c.s - 1) / c.s &&
+                  M % ((int64_t)c.hi * c.wi) == 0,
+              "res_map does not describe a stride-s subsampling of the GEMM rows");
+  return c;
+}
+
 std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& residual,
                                       const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
                                       const at::Tensor& mean, const c10::optional<at::Tensor>& scale,
-                                      const c10::optional<at::Tensor>& shift) {
+                                      const c10::optional<at::Tensor>& shift,
+                                      const std::vector<int64_t>& res_map) {
   check_operand(A, "A");
   check_operand(B, "B");
   check_operand(bn_x, "bn_x");
   NtArgs a{};
+  a.rmap = parse_compact(res_map, A.size(0));
   a.M = (int)A.size(0);
   a.K = (int)A.size(1);
   a.N = (int)B.size(0);

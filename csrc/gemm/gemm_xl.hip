@@ -116,6 +116,7 @@ struct XlArgs {
   const bf16* bx; int64_t ldbx; // XL_BNBWD: BN input x [M, N]
   const bf16* bny; int64_t ldby;// XL_BNBWD: BN output y [M, N] (mask source) or null
   const float *bmean, *bsc, *bsh;
+  CompactMap rmap;              // XL_BNBWD residual in compact stride-s form
 };
 
 template <int BN, int EPI, int PIPE>
@@ -375,7 +376,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       } else if constexpr (EPI == XL_BNBWD) {
         f32x8 g = __builtin_convertvector(v, f32x8);
         if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
-          g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+          const int64_t rr = compact_row(p.rmap, row);
+          if (rr >= 0)
+            g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + rr * p.ldr + col), f32x8);
           v = __builtin_convertvector(g, bf16x8);
           g = __builtin_convertvector(v, f32x8);
         }
@@ -807,7 +810,8 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& bn_y,
                                      const c10::optional<at::Tensor>& mean,
                                      const c10::optional<at::Tensor>& scale,
-                                     const c10::optional<at::Tensor>& shift) {
+                                     const c10::optional<at::Tensor>& shift,
+                                     const std::vector<int64_t>& res_map) {
   check_bf16_2d(A, "A");
   check_bf16_2d(B, "B");
   const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
@@ -825,9 +829,18 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
   a.C = reinterpret_cast<bf16*>(C.data_ptr()); a.ldc = C.stride(0);
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+  if (!res_map.empty()) {
+    TORCH_CHECK(mode == "bnbwd" && res_map.size() == 5, "res_map: bnbwd only, [stride, Ho, Wo, Hi, Wi]");
+    a.rmap.s = (int)res_map[0]; a.rmap.ho = (int)res_map[1]; a.rmap.wo = (int)res_map[2];
+    a.rmap.hi = (int)res_map[3]; a.rmap.wi = (int)res_map[4];
+    TORCH_CHECK(a.rmap.ho == (a.rmap.hi + a.rmap.s - 1) / a.rmap.s &&
+                    a.rmap.wo == (a.rmap.wi + a.rmap.s - 1) / a.rmap.s && M % ((int64_t)a.rmap.hi * a.rmap.wi) == 0,
+                "res_map does not describe a stride-s subsampling of the GEMM rows");
+  }
   if (residual.has_value() && residual->defined()) {
     check_bf16_2d(*residual, "residual");
-    TORCH_CHECK(residual->size(0) == M && residual->size(1) == N, "gemm_xl_conv: residual shape");
+    const int64_t rrows = a.rmap.s == 1 ? M : M / ((int64_t)a.rmap.hi * a.rmap.wi) * a.rmap.ho * a.rmap.wo;
+    TORCH_CHECK(residual->size(0) == rrows && residual->size(1) == N, "gemm_xl_conv: residual shape");
     a.R = reinterpret_cast<const bf16*>(residual->data_ptr());
     a.ldr = residual->stride(0);
   }

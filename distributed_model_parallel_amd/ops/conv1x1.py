@@ -23,7 +23,8 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0}
+_STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0, "compact_dgrad": 0,
+          "compact_residual": 0}
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -67,7 +68,7 @@ def _geom(stride: int, hi: int, wi: int):
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, moments, slot, bn_slot=None):
+    def forward(ctx, x, weight, stride, moments, slot, bn_slot=None, park_slot=None):
         C = _native.require("conv1x1")
         n, cin, h, w = x.shape
         geom = _geom(stride, h, w)
@@ -85,6 +86,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         # x is a training-mode BN+ReLU output: our dgrad epilogue can also do
         # that BN's backward reductions (ops/batchnorm.py BnBwdSlot)
         ctx.bn_slot = bn_slot if (bn_slot is not None and not geom) else None
+        # strided conv on a grad_tap'ed branch: may park its dgrad compact (ops/fused.py)
+        ctx.park_slot = park_slot if geom else None
         if ctx.bn_slot is not None:
             bn_slot.consumers += 1
         if slot is not None and not geom:
@@ -100,7 +103,7 @@ class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dmom):
         if dy is None:
-            return (None,) * 6
+            return (None,) * 7
         x, weight = ctx.saved_tensors
         C = _native.require("conv1x1 backward")
         n, cin, h, w = x.shape
@@ -108,11 +111,26 @@ class _Conv1x1Fn(torch.autograd.Function):
         dy2 = _rows(dy.contiguous(memory_format=torch.channels_last).to(x.dtype))
         w2 = weight.reshape(cout, cin)
         dx = dw = None
-        if ctx.needs_input_grad[0]:
+        ps = ctx.park_slot
+        ctx.park_slot = None
+        if ctx.needs_input_grad[0] and ps is not None and ps.can_park_compact():
+            # the consumer adds the stride-grid rows itself: no zero-filled full-size dx
+            _STATS["compact_dgrad"] += 1
+            ps.compact, _ = C.gemm_nt(dy2, w2.t().contiguous())
+            ps.compact_geom = list(ctx.geom)
+        elif ctx.needs_input_grad[0]:
             # strided: the GEMM scatters into the sampled rows of a zeroed full-size grad
             extra = ctx.slot.take() if (ctx.slot is not None and ctx.slot.consumer) else None
+            cextra, cgeom = ctx.slot.take_compact() if ctx.slot is not None else (None, None)
             bs = ctx.bn_slot
             ctx.bn_slot = None
+            if cextra is not None and not (bs is not None and bs.consumers == 1 and bs.x2 is not None):
+                # no fused BN epilogue to read it compact: expand to full resolution
+                full = torch.zeros(n * h * w, cin, device=dy.device, dtype=x.dtype)
+                full.view(n, h, w, cin)[:, ::cgeom[0], ::cgeom[0]].copy_(cextra.view(n, cgeom[1], cgeom[2], cin))
+                extra = full.view(n, h, w, cin).permute(0, 3, 1, 2) if extra is None else extra + full.view(
+                    n, h, w, cin).permute(0, 3, 1, 2)
+                cextra = None
             if bs is not None and bs.consumers == 1 and bs.x2 is not None:
                 # dz = relu_mask * (dy @ W (+ shortcut grad)) and the producer BN's
                 # (sum dz, sum dz*(x-mean)) in ONE epilogue pass
@@ -123,14 +141,24 @@ class _Conv1x1Fn(torch.autograd.Function):
                 sc = sh = None
                 if bs.y2 is None:
                     sc, sh = bs.mask_affine()
+                rmap = []
+                if cextra is not None:
+                    if extra is not None:  # both a full and a compact parked gradient: expand
+                        full = torch.zeros(n * h * w, cin, device=dy.device, dtype=x.dtype)
+                        full.view(n, h, w, cin)[:, ::cgeom[0], ::cgeom[0]].copy_(
+                            cextra.view(n, cgeom[1], cgeom[2], cin))
+                        extra = extra + full
+                    else:
+                        extra, rmap = cextra, [cgeom[0], cgeom[1], cgeom[2], h, w]
+                        _STATS["compact_residual"] += 1
                 if _xl(cin, cout):
                     _STATS["xl"] += 1
                     dx2, sums = C.gemm_xl_conv(dy2, w2.t().contiguous(), "bnbwd", residual=extra,
                                                bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean.contiguous(),
-                                               scale=sc, shift=sh)
+                                               scale=sc, shift=sh, res_map=rmap)
                 else:
                     dx2, sums = C.gemm_nt_bnbwd(dy2, w2.t().contiguous(), extra, bs.x2, bs.y2,
-                                                bs.mean.contiguous(), sc, sh)
+                                                bs.mean.contiguous(), sc, sh, rmap)
                 dx = _unrows(dx2, n, h, w)
                 bs.park(dx, sums[: 2 * cin])
                 dx2 = None
@@ -150,7 +178,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
@@ -161,7 +189,8 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
     if _native_ok(x, weight):
         _STATS["native"] += 1
         bn_slot = getattr(x, "_dmp_bnbwd", None) if torch.is_grad_enabled() else None
-        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments, grad_slot, bn_slot)
+        park = getattr(x, "_dmp_gradslot", None) if (torch.is_grad_enabled() and stride != 1) else None
+        y, mom = _Conv1x1Fn.apply(x, weight, stride, moments, grad_slot, bn_slot, park)
         return y, (mom if moments else None)
     _STATS["torch"] += 1
     return F.conv2d(x, weight, None, stride), None

@@ -27,25 +27,42 @@ from .batchnorm import BatchNormAct2d
 
 
 class GradSlot:
-    """Per-forward-call mailbox between a grad_tap and one native consumer."""
-    __slots__ = ("consumer", "consumer_ran", "grad")
+    """Per-forward-call mailbox between a grad_tap and one native consumer.
+
+    A stride-s 1x1 conv on the tapped branch (the ResNet downsample) may park
+    its data gradient COMPACT -- [N*Ho*Wo, C] rows, the full-resolution
+    gradient being zero off the stride grid -- with its geometry: no zero-filled
+    full-size tensor, no scatter, and the consumer's epilogue reads 1/s^2 of the
+    bytes (``res_map`` of gemm_nt_bnbwd / gemm_xl_conv)."""
+    __slots__ = ("consumer", "consumer_ran", "grad", "compact", "compact_geom")
 
     def __init__(self):
         self.consumer = False      # a native conv registered to absorb the parked grad
         self.consumer_ran = False  # its backward already ran without a parked grad
         self.grad: Optional[torch.Tensor] = None
+        self.compact: Optional[torch.Tensor] = None
+        self.compact_geom = None
 
     def take(self) -> Optional[torch.Tensor]:
         g, self.grad = self.grad, None
-        if g is None:
+        if g is None and self.compact is None:
             self.consumer_ran = True
         return g
+
+    def take_compact(self):
+        c, geom = self.compact, self.compact_geom
+        self.compact = self.compact_geom = None
+        return c, geom
+
+    def can_park_compact(self) -> bool:
+        return self.consumer and not self.consumer_ran and self.grad is None and self.compact is None
 
 
 class _GradTap(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, slot):
         ctx.slot = slot
+        ctx.set_materialize_grads(False)  # a compact park leaves this output without a gradient
         return x.view_as(x)
 
     @staticmethod
@@ -60,7 +77,9 @@ class _GradTap(torch.autograd.Function):
 def grad_tap(x: torch.Tensor, slot: Optional[GradSlot]) -> torch.Tensor:
     if slot is None or not slot.consumer or not (torch.is_grad_enabled() and x.requires_grad):
         return x
-    return _GradTap.apply(x, slot)
+    out = _GradTap.apply(x, slot)
+    out._dmp_gradslot = slot  # a strided 1x1 conv consuming `out` may park a compact gradient
+    return out
 
 
 def conv_bn(conv: nn.Module, bn: nn.Module, x: torch.Tensor,

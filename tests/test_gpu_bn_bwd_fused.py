@@ -86,14 +86,48 @@ def test_bottleneck_fused_bn_backward_matches_unfused(stride):
         bnops._FUSE_BWD = True
         net3 = copy.deepcopy(ref)
         n0 = bnops._STATS["fused_bwd_moments"]
+        c0 = conv1x1._STATS["compact_residual"]
         ya3, ga3, pa3 = _run(net3, x, gg)
         fused = bnops._STATS["fused_bwd_moments"] - n0
+        compact = conv1x1._STATS["compact_residual"] - c0
     finally:
         bnops._FUSE_BWD = old
     assert fused >= 3, f"expected bn2 of both blocks and b1.bn3 fused, got {fused}"
+    if stride != 1:  # the strided shortcut's dgrad reached b2.conv1's epilogue compact
+        assert compact == 1, compact
     torch.testing.assert_close(ya3, ya2)
     cos = F.cosine_similarity(ga3.flatten(), ga2.flatten(), dim=0).item()
     assert cos > 0.995, cos
     for n in pa2:
         c = F.cosine_similarity(pa3[n].flatten(), pa2[n].flatten(), dim=0).item()
         assert c > 0.99, (n, c)
+
+
+@pytest.mark.parametrize("xl", [False, True])
+def test_bnbwd_compact_strided_residual(xl):
+    """A stride-2 compact residual (res_map) == the same residual zero-expanded
+    to full resolution, for both kernels."""
+    C = _native.require("bnbwd test")
+    torch.manual_seed(3)
+    n, h, w, s, N, K = 3, 10, 9, 2, 256, 128
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    M = n * h * w
+    dy = torch.randn(M, K, device=DEV).bfloat16()
+    wt = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
+    x = torch.randn(M, N, device=DEV).bfloat16()
+    mean = x.float().mean(0)
+    sc = torch.rand(N, device=DEV) + 0.5
+    sh = torch.randn(N, device=DEV) * 0.5
+    comp = torch.randn(n * ho * wo, N, device=DEV).bfloat16()
+    full = torch.zeros(n, h, w, N, device=DEV).bfloat16()
+    full[:, ::s, ::s] = comp.view(n, ho, wo, N)
+    full = full.view(M, N)
+    rmap = [s, ho, wo, h, w]
+    if xl:
+        a = C.gemm_xl_conv(dy, wt, "bnbwd", residual=comp, bn_x=x, mean=mean, scale=sc, shift=sh, res_map=rmap)
+        b = C.gemm_xl_conv(dy, wt, "bnbwd", residual=full, bn_x=x, mean=mean, scale=sc, shift=sh)
+    else:
+        a = C.gemm_nt_bnbwd(dy, wt, comp, x, None, mean, sc, sh, rmap)
+        b = C.gemm_nt_bnbwd(dy, wt, full, x, None, mean, sc, sh)
+    torch.testing.assert_close(a[0], b[0])
+    torch.testing.assert_close(a[1], b[1], atol=1e-6, rtol=1e-9)
