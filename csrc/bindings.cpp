@@ -70,6 +70,12 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
                    const c10::optional<at::Tensor>& pro_shift);
 // stem.hip
 at::Tensor space_to_depth2(const at::Tensor& x, int64_t pad, int64_t out_channels);
+// maxpool.hip (fused stem BN + pool)
+std::vector<at::Tensor> maxpool2d_bn_forward(const at::Tensor& x, const at::Tensor& scale,
+                                             const at::Tensor& shift, int64_t k, int64_t s, int64_t p);
+std::vector<at::Tensor> maxpool2d_bn_backward(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& x,
+                                              const at::Tensor& scale, const at::Tensor& shift,
+                                              const at::Tensor& mean, int64_t k, int64_t s, int64_t p);
 std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int64_t kh,
                                 int64_t kw, int64_t stride, int64_t pad, int64_t ho, int64_t wo,
                                 bool transposed, const c10::optional<at::Tensor>& pro_scale,
@@ -193,6 +199,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
         py::arg("kc") = 0);
+  m.def("maxpool2d_bn_forward", &dmp::maxpool2d_bn_forward, py::arg("x"), py::arg("scale"),
+        py::arg("shift"), py::arg("k"), py::arg("s"), py::arg("p"));
+  m.def("maxpool2d_bn_backward", &dmp::maxpool2d_bn_backward, py::arg("dy"), py::arg("idx"), py::arg("x"),
+        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("space_to_depth2", &dmp::space_to_depth2, py::arg("x"), py::arg("pad"), py::arg("out_channels") = 16);
 
   // ---- large-tile transformer GEMM with fused bias / GELU / residual epilogues ----

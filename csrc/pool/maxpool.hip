@@ -242,6 +242,167 @@ __global__ __launch_bounds__(kPoolThreads) void maxpool_bwd_fixed_kernel(const T
   Vec16<T>::store(dx + ((int64_t)row * g.W + iw) * g.C + c0, acc);
 }
 
+// ---------------------------------------------------------------------------
+// Stem fusion: training-mode BN + ReLU applied INSIDE the k3/s2 pool.
+// The pool's input is the raw conv output x; every tap is normalised on load
+// (relu(x * sc[c] + sh[c]), rounded to bf16 exactly as the unfused BN apply
+// would store it), so the BN output tensor is never written nor re-read.
+// The backward gathers the pool gradient per input pixel as usual, then does
+// the BN backward's reductions on the spot: ReLU mask from x through the same
+// affine, dz stored, (sum dz, sum dz*(x - mean)) accumulated per thread over a
+// grid-stride row loop and folded per block into [2][blocks][C] partials.
+// ---------------------------------------------------------------------------
+template <int K, int S>
+__global__ __launch_bounds__(kPoolThreads) void bnpool_fwd_kernel(
+    const __bf16* __restrict__ x, const float* __restrict__ sc, const float* __restrict__ sh,
+    __bf16* __restrict__ y, uint8_t* __restrict__ idx, PoolGeo g, int row_len) {
+  constexpr int VEC = 8;
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= row_len) return;
+  const int row = blockIdx.x;
+  const int n = row / g.Ho, oh = row - n * g.Ho;
+  const int ow = j / g.cv, cvi = j - ow * g.cv;
+  const int c0 = cvi * VEC;
+  const int h0 = oh * S - g.p, w0 = ow * S - g.p;
+  const __bf16* xn = x + (int64_t)n * g.H * g.W * g.C + c0;
+  float v[K][K][VEC];
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const int ih = min(max(h0 + a, 0), g.H - 1);
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const int iw = min(max(w0 + b, 0), g.W - 1);
+      Vec16<__bf16>::load(xn + ((int64_t)ih * g.W + iw) * g.C, v[a][b]);
+    }
+  }
+  float s8[VEC], t8[VEC];
+  {
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(sc + c0), s1 = *reinterpret_cast<const f32x4*>(sc + c0 + 4);
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(sh + c0), t1 = *reinterpret_cast<const f32x4*>(sh + c0 + 4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { s8[c] = s0[c]; s8[c + 4] = s1[c]; t8[c] = t0[c]; t8[c + 4] = t1[c]; }
+  }
+  const uint8_t tap0 = (uint8_t)(max(0, -h0) * K + max(0, -w0));
+  float m[VEC];
+  uint8_t am[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) { m[c] = -INFINITY; am[c] = tap0; }
+#pragma unroll
+  for (int a = 0; a < K; ++a) {
+    const bool ha = (unsigned)(h0 + a) < (unsigned)g.H;
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const bool ok = ha && (unsigned)(w0 + b) < (unsigned)g.W;
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) {
+        // the BN+ReLU output as the unfused apply pass would have stored it
+        const float t = (float)(__bf16)fmaxf(fmaf(v[a][b][c], s8[c], t8[c]), 0.f);
+        if (ok && (t > m[c] || (t != t && m[c] == m[c]))) { m[c] = t; am[c] = (uint8_t)(a * K + b); }
+      }
+    }
+  }
+  const int64_t pix = (int64_t)row * g.Wo + ow;
+  Vec16<__bf16>::store(y + pix * g.C + c0, m);
+  uint64_t w = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) w |= (uint64_t)am[c] << (8 * c);
+  *reinterpret_cast<uint64_t*>(idx + pix * g.C + c0) = w;
+}
+
+template <int K, int S>
+__global__ __launch_bounds__(kPoolThreads) void bnpool_bwd_kernel(
+    const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx, const __bf16* __restrict__ x,
+    const float* __restrict__ sc, const float* __restrict__ sh, const float* __restrict__ mean,
+    __bf16* __restrict__ dz, float* __restrict__ part, double* __restrict__ zsums, PoolGeo g, int row_len,
+    int rows) {
+  constexpr int VEC = 8;
+  constexpr int MW = (K + S - 1) / S;
+  zero_moments(zsums, 2 * g.C);
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  const bool active = j < row_len;
+  const int iw = active ? j / g.cv : 0, cvi = active ? j - (j / g.cv) * g.cv : 0;
+  const int c0 = cvi * VEC;
+  float s8[VEC], t8[VEC], mu[VEC], msum[VEC], msq[VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) {
+    s8[c] = sc[c0 + c]; t8[c] = sh[c0 + c]; mu[c] = mean[c0 + c];
+    msum[c] = 0.f; msq[c] = 0.f;
+  }
+  using IdxW = uint64_t;
+  for (int row = blockIdx.x; active && row < rows; row += gridDim.x) {
+    const int n = row / g.H, ih = row - n * g.H;
+    const int oh_hi = (ih + g.p) / S, ow_hi = (iw + g.p) / S;
+    const int64_t nbase = (int64_t)n * g.Ho * g.Wo * g.C + c0;
+    IdxW w[MW][MW];
+    float v[MW][MW][VEC];
+    bool ok[MW][MW];
+#pragma unroll
+    for (int t = 0; t < MW; ++t) {
+      const int oh = oh_hi - t;
+      const int a = ih - (oh * S - g.p);
+      const bool okh = oh >= 0 && oh < g.Ho && a >= 0 && a < K;
+      const int ohc = min(max(oh, 0), g.Ho - 1);
+#pragma unroll
+      for (int u = 0; u < MW; ++u) {
+        const int ow = ow_hi - u;
+        const int b = iw - (ow * S - g.p);
+        ok[t][u] = okh && ow >= 0 && ow < g.Wo && b >= 0 && b < K;
+        const int owc = min(max(ow, 0), g.Wo - 1);
+        const int64_t o = nbase + ((int64_t)ohc * g.Wo + owc) * g.C;
+        w[t][u] = *reinterpret_cast<const IdxW*>(idx + o);
+        Vec16<__bf16>::load(dy + o, v[t][u]);
+      }
+    }
+    const int64_t xo = ((int64_t)row * g.W + iw) * g.C + c0;
+    float xv[VEC];
+    Vec16<__bf16>::load(x + xo, xv);
+    float acc[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) acc[c] = 0.f;
+#pragma unroll
+    for (int t = 0; t < MW; ++t) {
+      const int a = ih - ((oh_hi - t) * S - g.p);
+#pragma unroll
+      for (int u = 0; u < MW; ++u) {
+        const int b = iw - ((ow_hi - u) * S - g.p);
+        const uint8_t tap = (uint8_t)(a * K + b);
+#pragma unroll
+        for (int c = 0; c < VEC; ++c)
+          if (ok[t][u] && (uint8_t)(w[t][u] >> (8 * c)) == tap) acc[c] += v[t][u][c];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) {
+      const float gq = (float)(__bf16)acc[c];  // the pool gradient as the unfused pass stores it
+      const float d = fmaf(xv[c], s8[c], t8[c]) > 0.f ? gq : 0.f;
+      acc[c] = d;
+      msum[c] += d;
+      msq[c] = fmaf(d, xv[c] - mu[c], msq[c]);
+    }
+    Vec16<__bf16>::store(dz + xo, acc);
+  }
+  // fold the threads of this block that share a channel vector (tid % cv, host
+  // guarantees kPoolThreads % cv == 0) into one [2][C] partial row
+  __shared__ float red[2][kPoolThreads][VEC];
+#pragma unroll
+  for (int c = 0; c < VEC; ++c) {
+    red[0][threadIdx.x][c] = active ? msum[c] : 0.f;
+    red[1][threadIdx.x][c] = active ? msq[c] : 0.f;
+  }
+  __syncthreads();
+  const int rb = gridDim.x * gridDim.y, prow = blockIdx.y * gridDim.x + blockIdx.x;
+  for (int c = threadIdx.x; c < g.C; c += kPoolThreads) {
+    const int cv = c / VEC, e = c - cv * VEC;
+    float a0 = 0.f, a1 = 0.f;
+    for (int t = cv; t < kPoolThreads; t += g.cv) {
+      a0 += red[0][t][e];
+      a1 += red[1][t][e];
+    }
+    part[(int64_t)prow * g.C + c] = a0;
+    part[(int64_t)(rb + prow) * g.C + c] = a1;
+  }
+}
+
 // Global average pool backward, channels-last: dx[n, hw, c] = g[n, c] / HW.
 // PyTorch returns an expanded gradient here that the next backward
 // materialises with a strided copy (~1.3 TB/s, profiles finding 13); this is
@@ -357,6 +518,71 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
     hipLaunchKernelGGL(maxpool_bwd_kernel<float>, blocks, dim3(kPoolThreads), 0, stream,
                        dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), g, row_len);
   return dx;
+}
+
+// batchnorm.hip
+void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
+                               hipStream_t stream);
+
+namespace {
+void check_bnpool(const at::Tensor& x, const at::Tensor& scale, const at::Tensor& shift, int64_t k,
+                  int64_t s, int64_t p) {
+  check_x(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && k == 3 && s == 2 && p <= 1,
+              "fused BN+pool covers bf16 3x3/s2 pools");
+  TORCH_CHECK(kPoolThreads % (x.size(1) / 8) == 0, "fused BN+pool: C/8 must divide ", kPoolThreads);
+  for (const auto* t : {&scale, &shift})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == x.size(1),
+                "BN coefficients must be contiguous fp32 [C]");
+}
+}  // namespace
+
+// y, argmax = maxpool(relu(x * scale + shift)) -- BN apply + ReLU fused into the pool.
+std::vector<at::Tensor> maxpool2d_bn_forward(const at::Tensor& x, const at::Tensor& scale,
+                                             const at::Tensor& shift, int64_t k, int64_t s, int64_t p) {
+  check_bnpool(x, scale, shift, k, s, p);
+  PoolGeo g = make_geo(x, k, s, p, 8);
+  TORCH_CHECK(g.Ho > 0 && g.Wo > 0, "pool output is empty");
+  auto y = at::empty({g.N, g.C, g.Ho, g.Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto idx = at::empty({(int64_t)g.N * g.Ho * g.Wo * g.C}, x.options().dtype(at::kByte));
+  const int row_len = g.Wo * g.cv;
+  if ((int64_t)g.N * g.Ho * row_len == 0) return {y, idx};
+  const dim3 blocks((unsigned)(g.N * g.Ho), (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads));
+  hipLaunchKernelGGL((bnpool_fwd_kernel<3, 2>), blocks, dim3(kPoolThreads), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const __bf16*>(x.data_ptr()), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                     reinterpret_cast<__bf16*>(y.data_ptr()), idx.data_ptr<uint8_t>(), g, row_len);
+  DMP_HIP_CHECK(hipGetLastError());
+  return {y, idx};
+}
+
+// dz = relu_mask(x) * maxpool_backward(dy), plus fp64 [2C+1] = (sum dz, sum dz*(x-mean), rows)
+std::vector<at::Tensor> maxpool2d_bn_backward(const at::Tensor& dy, const at::Tensor& idx, const at::Tensor& x,
+                                              const at::Tensor& scale, const at::Tensor& shift,
+                                              const at::Tensor& mean, int64_t k, int64_t s, int64_t p) {
+  check_bnpool(x, scale, shift, k, s, p);
+  check_x(dy, "dy");
+  TORCH_CHECK(mean.is_cuda() && mean.scalar_type() == at::kFloat && mean.is_contiguous() &&
+                  mean.numel() == x.size(1), "mean must be contiguous fp32 [C]");
+  PoolGeo g = make_geo(x, k, s, p, 8);
+  TORCH_CHECK(dy.size(0) == g.N && dy.size(1) == g.C && dy.size(2) == g.Ho && dy.size(3) == g.Wo,
+              "dy does not match the pool geometry");
+  TORCH_CHECK(idx.numel() == dy.numel() && idx.scalar_type() == at::kByte, "bad argmax tensor");
+  auto dz = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  auto sums = at::empty({2 * (int64_t)g.C + 1}, x.options().dtype(at::kDouble));
+  const int row_len = g.W * g.cv;
+  const int rows = g.N * g.H;
+  const unsigned gx = (unsigned)std::min(rows, 1024), gy = (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads);
+  const int rb = (int)(gx * gy);
+  auto part = at::empty({2, rb, (int64_t)g.C}, x.options().dtype(at::kFloat));
+  auto stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL((bnpool_bwd_kernel<3, 2>), dim3(gx, gy), dim3(kPoolThreads), 0, stream,
+                     reinterpret_cast<const __bf16*>(dy.data_ptr()), idx.data_ptr<uint8_t>(),
+                     reinterpret_cast<const __bf16*>(x.data_ptr()), scale.data_ptr<float>(),
+                     shift.data_ptr<float>(), mean.data_ptr<float>(), reinterpret_cast<__bf16*>(dz.data_ptr()),
+                     part.data_ptr<float>(), moments_zero_target(sums.data_ptr<double>(), rb), g, row_len, rows);
+  DMP_HIP_CHECK(hipGetLastError());
+  bn_reduce_partials_launch(part.data_ptr<float>(), rb, g.C, sums.data_ptr<double>(), (double)rows * g.W, stream);
+  return {dz, sums};
 }
 
 at::Tensor global_avgpool_backward(const at::Tensor& g, int64_t H, int64_t W) {

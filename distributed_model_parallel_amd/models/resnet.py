@@ -21,7 +21,7 @@ import torch.nn as nn
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
-from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, grad_tap
+from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, conv_bn_maxpool, grad_tap
 from ..ops.pool import MaxPool2d, global_avg_pool
 from ..ops.stem import StemConv2d
 
@@ -143,7 +143,8 @@ class ResNet(nn.Module):
         return nn.Sequential(*mods)
 
     def forward_features(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.maxpool(conv_bn(self.conv1, self.bn1, x))
+        # stem: BN + ReLU applied inside the max pool (ops/fused.py conv_bn_maxpool)
+        x = conv_bn_maxpool(self.conv1, self.bn1, self.maxpool, x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return global_avg_pool(x)  # channels-last broadcast backward (ops/pool.py)
 

@@ -21,6 +21,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import os
+
 from .. import _native
 
 _STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0, "compact_dgrad": 0,
@@ -51,12 +53,17 @@ def _blaslt_dgrad(m: int, cin: int, cout: int) -> bool:
     return cout >= 1024 and m <= 65536
 
 
+# A/B switches (measured per box): compact strided shortcut gradients, glds-ring GEMMs
+_COMPACT = os.environ.get("DMP_COMPACT_SHORTCUT", "1") != "0"
+_XL = os.environ.get("DMP_XL_CONV", "1") != "0"
+
+
 def _xl(n: int, k: int) -> bool:
     """Output width N, reduction K of a 1x1-conv GEMM where the 8-wave glds-ring
     kernel (gemm_xl_conv) measured faster than the 4-wave NT kernel with the
     same epilogue (profiles/conv1x1_xl.md, batch 1024): wide outputs with a
     moderate K.  Narrow N (<= 128) and very short / very deep K stay on NT."""
-    return k >= 128 and k % 64 == 0 and (n >= 512 or (n >= 256 and k <= 512))
+    return _XL and k >= 128 and k % 64 == 0 and (n >= 512 or (n >= 256 and k <= 512))
 
 
 def _geom(stride: int, hi: int, wi: int):
@@ -189,7 +196,8 @@ def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
     if _native_ok(x, weight):
         _STATS["native"] += 1
         bn_slot = getattr(x, "_dmp_bnbwd", None) if torch.is_grad_enabled() else None
-        park = getattr(x, "_dmp_gradslot", None) if (torch.is_grad_enabled() and stride != 1) else None
+        park = getattr(x, "_dmp_gradslot", None) if (_COMPACT and torch.is_grad_enabled() and stride != 1) \
+            else None
         y, mom = _Conv1x1Fn.apply(x, weight, stride, moments, grad_slot, bn_slot, park)
         return y, (mom if moments else None)
     _STATS["torch"] += 1

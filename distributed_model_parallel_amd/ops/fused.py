@@ -202,3 +202,99 @@ def bn_relu_conv1x1(bn: nn.Module, conv: nn.Module, x: torch.Tensor,
 
 
 _STATS_FUSED = {"bn_relu_conv1x1": 0}
+
+
+# --------------------------------------------------------------------------- #
+# Stem: BN(+ReLU) applied inside the 3x3/s2 max pool (training)
+# --------------------------------------------------------------------------- #
+class _BNReLUMaxPoolFn(torch.autograd.Function):
+    """pool(relu(bn(x))) with the BN output never materialised:
+
+    forward   bn_finalize (coefficients + running stats from the conv's fused
+              moments), then the pool normalises each tap on load
+              (``maxpool2d_bn_forward``);
+    backward  the pool's gather backward also masks with the ReLU (from x)
+              and reduces the BN backward's (sum dz, sum dz*(x-mean))
+              (``maxpool2d_bn_backward``); the BN apply pass then reads dz, x.
+    Saves the BN apply pass forward (write + re-read of the stem activation,
+    the largest tensor of the network) and the moments pass backward."""
+
+    @staticmethod
+    def forward(ctx, x, bn_w, bn_b, sums, running_mean, running_var, momentum, eps, nbt, reduce_moments,
+                reduce_grads, k, s, p):
+        from .. import _native
+        C = _native.require("bn_relu_maxpool")
+        c = x.shape[1]
+        if reduce_moments is not None:
+            sums = reduce_moments(sums)
+        w32 = bn_w.float() if bn_w is not None else None
+        b32 = bn_b.float() if bn_b is not None else None
+        coef = C.bn_finalize(sums, w32, b32, running_mean, running_var, float(momentum), float(eps), c, nbt)
+        y, idx = C.maxpool2d_bn_forward(x, coef[0].contiguous(), coef[1].contiguous(), k, s, p)
+        ctx.save_for_backward(x, idx, w32, b32, coef, sums[-1:])
+        ctx.meta = (reduce_grads, bn_w.dtype if bn_w is not None else None, bn_w is not None,
+                    bn_b is not None, k, s, p)
+        ctx.mark_non_differentiable(idx)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .. import _native
+        from .batchnorm import backward_apply
+        C = _native.require("bn_relu_maxpool backward")
+        x, idx, w32, b32, coef, count = ctx.saved_tensors
+        reduce_grads, wdtype, has_w, has_b, k, s, p = ctx.meta
+        c = x.shape[1]
+        scale, shift, mean, invstd = (coef[i].contiguous() for i in range(4))
+        dz, sums = C.maxpool2d_bn_backward(dy.contiguous(memory_format=torch.channels_last), idx, x,
+                                           scale, shift, mean, k, s, p)
+        sums = sums[: 2 * c]
+        local = sums
+        if reduce_grads is not None:
+            local = sums.clone()  # the reducer works in place
+            sums = reduce_grads(sums)
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, c)
+        dz2 = dz.permute(0, 2, 3, 1).reshape(-1, c)
+        dx2, dg, db, _ = backward_apply(dz2, x2, None, sums, count, w32, mean, invstd, True, False, False,
+                                        True, b32)
+        if reduce_grads is not None:
+            dg = (local[c:] * invstd.double()).float()
+            db = local[:c].float()
+        n, _, h, w = x.shape
+        gx = dx2.view(n, h, w, c).permute(0, 3, 1, 2)
+        gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[1] else None
+        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[2] else None
+        return gx, gw, gb, None, None, None, None, None, None, None, None, None, None, None
+
+
+_STATS_FUSED["bn_relu_maxpool"] = 0
+
+
+def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """pool(bn_relu(conv(x))) -- the ResNet stem.  BN apply + ReLU run inside the
+    pool (forward) and the BN backward's reductions inside the pool's backward
+    when training natively; otherwise the modules run one after another."""
+    from .. import _native
+    from ..utils.checkpointing import in_recompute
+    fusable = (isinstance(bn, BatchNormAct2d) and bn.act == "relu" and bn.training and bn.track_running_stats
+               and bn.momentum is not None and not in_recompute() and torch.is_grad_enabled()
+               and hasattr(conv, "forward_with_moments") and isinstance(pool, nn.MaxPool2d)
+               and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2))
+               and pool.padding in (0, 1, (1, 1), (0, 0)) and not pool.ceil_mode
+               and pool.dilation in (1, (1, 1)) and _FUSE_STEM_POOL)
+    if not fusable:
+        return pool(conv_bn(conv, bn, x))
+    y, sums = conv.forward_with_moments(x)
+    if (sums is None or not _native.gpu_path(y) or y.dtype != torch.bfloat16
+            or not y.is_contiguous(memory_format=torch.channels_last) or 128 % (y.shape[1] // 8) != 0
+            or y.shape[1] % 8 != 0 or bn.running_mean is None or bn.running_mean.dtype != torch.float32):
+        return pool(bn(y, sums=sums))
+    rmom, rgrad = bn._moment_reducers()
+    pad = pool.padding if isinstance(pool.padding, int) else pool.padding[0]
+    _STATS_FUSED["bn_relu_maxpool"] += 1
+    return _BNReLUMaxPoolFn.apply(y, bn.weight, bn.bias, sums, bn.running_mean, bn.running_var, bn.momentum,
+                                  bn.eps, bn.num_batches_tracked, rmom, rgrad, 3, 2, pad)
+
+
+import os as _os  # noqa: E402
+_FUSE_STEM_POOL = _os.environ.get("DMP_FUSE_STEM_POOL", "1") != "0"

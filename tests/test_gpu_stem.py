@@ -39,3 +39,42 @@ def test_stem_falls_back_when_input_needs_grad():
     n0 = _STATS["torch"]
     m(x).sum().backward()
     assert _STATS["torch"] == n0 + 1 and x.grad is not None
+
+
+def test_stem_bn_pool_fusion_matches_unfused():
+    """conv_bn_maxpool: BN+ReLU inside the pool (forward) and the BN backward's
+    reductions inside the pool's backward == the three modules run separately."""
+    import copy
+
+    from distributed_model_parallel_amd.ops import fused
+    from distributed_model_parallel_amd.ops.batchnorm import BatchNormAct2d
+    from distributed_model_parallel_amd.ops.pool import MaxPool2d
+    torch.manual_seed(0)
+    conv = StemConv2d(3, 64).cuda().bfloat16().to(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(64, act="relu").cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0.0, 0.2)
+    pool = MaxPool2d(3, 2, 1)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = torch.randn(4, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    n0 = fused._STATS_FUSED["bn_relu_maxpool"]
+    y = fused.conv_bn_maxpool(conv, bn, pool, x)
+    assert fused._STATS_FUSED["bn_relu_maxpool"] == n0 + 1, "fused stem did not run"
+    old = fused._FUSE_STEM_POOL
+    fused._FUSE_STEM_POOL = False
+    try:
+        yr = fused.conv_bn_maxpool(conv2, bn2, pool, x)
+    finally:
+        fused._FUSE_STEM_POOL = old
+    torch.testing.assert_close(y.float(), yr.float())
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for a, b, name in ((conv.weight.grad, conv2.weight.grad, "conv w"), (bn.weight.grad, bn2.weight.grad, "bn w"),
+                       (bn.bias.grad, bn2.bias.grad, "bn b")):
+        err = (a.float() - b.float()).norm() / b.float().norm()
+        assert err < 2e-2, (name, err.item())
+    torch.testing.assert_close(bn.running_mean, bn2.running_mean)
+    torch.testing.assert_close(bn.running_var, bn2.running_var)
+    assert int(bn.num_batches_tracked) == int(bn2.num_batches_tracked) == 1
