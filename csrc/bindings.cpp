@@ -70,6 +70,7 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
                    const c10::optional<at::Tensor>& pro_shift);
 // stem.hip
 at::Tensor space_to_depth2(const at::Tensor& x, int64_t pad, int64_t out_channels);
+at::Tensor pad_channels16(const at::Tensor& x, int64_t pad, int64_t extra_w);
 // maxpool.hip (fused stem BN + pool)
 std::vector<at::Tensor> maxpool2d_bn_forward(const at::Tensor& x, const at::Tensor& scale,
                                              const at::Tensor& shift, int64_t k, int64_t s, int64_t p);
@@ -203,6 +204,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("shift"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("maxpool2d_bn_backward", &dmp::maxpool2d_bn_backward, py::arg("dy"), py::arg("idx"), py::arg("x"),
         py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("k"), py::arg("s"), py::arg("p"));
+  m.def("pad_channels16", &dmp::pad_channels16, py::arg("x"), py::arg("pad"), py::arg("extra_w") = 0);
   m.def("space_to_depth2", &dmp::space_to_depth2, py::arg("x"), py::arg("pad"), py::arg("out_channels") = 16);
 
   // ---- large-tile transformer GEMM with fused bias / GELU / residual epilogues ----

@@ -48,7 +48,53 @@ __global__ __launch_bounds__(256) void s2d_kernel(const __bf16* __restrict__ x, 
   Vec16<__bf16>::store(o + 8, hi);
 }
 
+// one thread per output pixel: copy C <= 16 channels, zero the rest / the border
+__global__ __launch_bounds__(256) void pad16_kernel(const __bf16* __restrict__ x, int64_t N, int C, int H, int W,
+                                                    int Hp, int Wp, int pad, __bf16* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = N * Hp * Wp;
+  if (p >= total) return;
+  const int j = (int)(p % Wp);
+  const int64_t t = p / Wp;
+  const int i = (int)(t % Hp);
+  const int64_t n = t / Hp;
+  float v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = 0.f;
+  const int h = i - pad, w = j - pad;
+  if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+    const __bf16* px = x + ((n * H + h) * W + w) * C;
+    for (int c = 0; c < C; ++c) v[c] = (float)px[c];
+  }
+  __bf16* o = out + p * 16;
+  float lo[8], hi[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { lo[q] = v[q]; hi[q] = v[8 + q]; }
+  Vec16<__bf16>::store(o, lo);
+  Vec16<__bf16>::store(o + 8, hi);
+}
+
 }  // namespace
+
+// x: [N, C <= 16, H, W] bf16 channels_last -> [N, 16, H + 2 pad, W + 2 pad + extra_w]
+// zero-padded (channels and border): the input of a stride-1 few-channel conv run
+// as 64-channel row taps (conv_nt kc=64 reads 4 adjacent 16-channel pixels).
+at::Tensor pad_channels16(const at::Tensor& x, int64_t pad, int64_t extra_w) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.size(1) <= 16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "pad_channels16 expects a channels_last bf16 [N, C<=16, H, W] GPU tensor");
+  const int64_t N = x.size(0);
+  const int C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Hp = H + 2 * (int)pad, Wp = W + 2 * (int)pad + (int)extra_w;
+  auto out = at::empty({N, 16, Hp, Wp}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int64_t total = N * Hp * Wp;
+  if (total == 0) return out;
+  hipLaunchKernelGGL(pad16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     at::hip::getCurrentHIPStream(), reinterpret_cast<const __bf16*>(x.data_ptr()), N, C, H, W,
+                     Hp, Wp, (int)pad, reinterpret_cast<__bf16*>(out.data_ptr()));
+  DMP_HIP_CHECK(hipGetLastError());
+  return out;
+}
 
 // x: [N, 3, H, W] bf16 channels_last -> [N, 16, Hs, Ws] bf16 channels_last,
 // Hs = (H + 2 pad + 1) / 2 (the padded image is cut into 2x2 blocks).

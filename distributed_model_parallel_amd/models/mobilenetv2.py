@@ -29,6 +29,7 @@ from ..ops.conv1x1 import Conv1x1
 from ..ops.depthwise import DepthwiseConv2d
 from ..ops.fused import conv_bn
 from ..ops.pool import global_avg_pool
+from ..ops.stem import RowTapConv2d
 
 # (expansion t, output channels c, repeats n, first stride s) -- CIFAR strides.
 CIFAR_SETTINGS: Tuple[Tuple[int, int, int, int], ...] = (
@@ -118,7 +119,8 @@ class MobileNetV2(nn.Module):
                  nobn_shortcut_bn: bool = False):
         super().__init__()
         self.use_bn = use_bn
-        self.conv1 = nn.Conv2d(3, 32, 3, stride=1, padding=1, bias=False)
+        # 3x3 stem on the MFMA implicit GEMM (3 channels padded to 16, row taps)
+        self.conv1 = RowTapConv2d(3, 32, 3)
         self.bn1 = _norm(32, use_bn, act=True)
         blocks: List[nn.Module] = []
         cin = 32
@@ -135,7 +137,7 @@ class MobileNetV2(nn.Module):
         self.linear = nn.Linear(1280, num_classes)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.bn1(self.conv1(x))
+        x = conv_bn(self.conv1, self.bn1, x)  # stem BN moments from the conv epilogue
         x = self.layers(x)
         x = conv_bn(self.conv2, self.bn2, x)
         return self.linear(self.pool(x))

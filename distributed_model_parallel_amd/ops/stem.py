@@ -90,3 +90,77 @@ class StemConv2d(nn.Conv2d):
             return _StemFn.apply(x, stem_wmat(self.weight), False)[0]
         _STATS["torch"] += 1
         return super().forward(x)
+
+
+# --------------------------------------------------------------------------- #
+# Stride-1 few-channel conv (MobileNetV2 CIFAR stem: 3x3, pad 1, 3 -> 32)
+# --------------------------------------------------------------------------- #
+def rowtap_wmat(w: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin<=16, k, k] -> [Cout, k * 64]: row r holds 4 pixels x 16 channels;
+    pixels q >= k and channels >= Cin carry zero weights."""
+    co, ci, k, _ = w.shape
+    wp = w.contiguous().permute(0, 2, 3, 1)                         # co, r, q, c
+    wp = F.pad(wp, (0, 16 - ci, 0, 4 - k))                          # [co, k, 4, 16]
+    return wp.reshape(co, k * 64).contiguous()
+
+
+class _RowTapFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wmat, k, pad, moments):
+        C = _native.require("row-tap conv")
+        n, _, h, w = x.shape
+        xp = C.pad_channels16(x, pad, 4 - k)                         # [n, 16, h+2p, w+2p+4-k]
+        y2, mom = C.conv_nt(xp, wmat, k, 1, 1, 0, h, w, mode="moments" if moments else "store", kc=64)
+        ctx.save_for_backward(xp)
+        ctx.geo = (n, h, w, k, wmat.dtype)
+        if mom is None:
+            mom = torch.empty(0, device=x.device, dtype=torch.float64)
+        ctx.mark_non_differentiable(mom)
+        ctx.set_materialize_grads(False)
+        return y2.view(n, h, w, -1).permute(0, 3, 1, 2), mom
+
+    @staticmethod
+    def backward(ctx, dy, _dmom):
+        if dy is None:
+            return None, None, None, None, None
+        (xp,) = ctx.saved_tensors
+        n, h, w, k, wdt = ctx.geo
+        C = _native.require("row-tap conv backward")
+        dy2 = dy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(n * h * w, -1)
+        dw = C.conv_wgrad(dy2.to(xp.dtype), xp, k, 1, 1, 0, h, w, wdt, kc=64)
+        return None, dw, None, None, None
+
+
+def _rowtap_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
+    k = conv.kernel_size[0]
+    return (_native.gpu_path(x) and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+            and x.dim() == 4 and x.shape[1] <= 16 and x.is_contiguous(memory_format=torch.channels_last)
+            and not x.requires_grad and conv.kernel_size == (k, k) and k <= 4 and conv.stride == (1, 1)
+            and conv.padding == (k // 2, k // 2) and k % 2 == 1 and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.bias is None and conv.out_channels % 8 == 0)
+
+
+class RowTapConv2d(nn.Conv2d):
+    """Drop-in ``nn.Conv2d(cin <= 16, cout, k <= 3 odd, stride=1, padding=k//2, bias=False)``
+    on the MFMA implicit GEMM: the input is zero-padded to 16 channels and each
+    kernel row becomes one 64-channel row tap (4 adjacent pixels, the 4th with
+    zero weights)."""
+
+    def __init__(self, cin: int, cout: int, kernel_size: int = 3, device=None, dtype=None):
+        super().__init__(cin, cout, kernel_size, stride=1, padding=kernel_size // 2, bias=False,
+                         device=device, dtype=dtype)
+
+    def forward_with_moments(self, x: torch.Tensor):
+        if _rowtap_ok(self, x):
+            _STATS["native"] += 1
+            y, mom = _RowTapFn.apply(x, rowtap_wmat(self.weight), self.kernel_size[0], self.padding[0], True)
+            return y, mom
+        _STATS["torch"] += 1
+        return super().forward(x), None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _rowtap_ok(self, x):
+            _STATS["native"] += 1
+            return _RowTapFn.apply(x, rowtap_wmat(self.weight), self.kernel_size[0], self.padding[0], False)[0]
+        _STATS["torch"] += 1
+        return super().forward(x)

@@ -78,3 +78,25 @@ def test_stem_bn_pool_fusion_matches_unfused():
     torch.testing.assert_close(bn.running_mean, bn2.running_mean)
     torch.testing.assert_close(bn.running_var, bn2.running_var)
     assert int(bn.num_batches_tracked) == int(bn2.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("n,h,w,cout", [(8, 32, 32, 32), (3, 17, 13, 64)])
+def test_rowtap_stem_matches_conv2d(n, h, w, cout):
+    """MobileNetV2's 3x3/s1 stem on 3 channels as 64-channel row taps."""
+    from distributed_model_parallel_amd.ops.stem import RowTapConv2d
+    torch.manual_seed(1)
+    m = RowTapConv2d(3, cout, 3).cuda().bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(n, 3, h, w, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    n0 = _STATS["native"]
+    y, mom = m.forward_with_moments(x)
+    assert _STATS["native"] == n0 + 1
+    wr = m.weight.detach().float().requires_grad_()
+    yr = F.conv2d(x.float(), wr, None, 1, 1)
+    torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=2e-2)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, cout).double()
+    torch.testing.assert_close(mom[:cout], yf.sum(0), atol=1e-2 * yf.shape[0] ** 0.5, rtol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    err = (m.weight.grad.float() - wr.grad).norm() / wr.grad.norm()
+    assert err < 1e-2, err
