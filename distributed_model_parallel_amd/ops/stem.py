@@ -131,9 +131,12 @@ class _RowTapFn(torch.autograd.Function):
         return None, dw, None, None, None
 
 
+_ROWTAP = __import__("os").environ.get("DMP_ROWTAP_STEM", "1") != "0"
+
+
 def _rowtap_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:
     k = conv.kernel_size[0]
-    return (_native.gpu_path(x) and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
+    return (_ROWTAP and _native.gpu_path(x) and x.dtype == torch.bfloat16 and conv.weight.dtype == torch.bfloat16
             and x.dim() == 4 and x.shape[1] <= 16 and x.is_contiguous(memory_format=torch.channels_last)
             and not x.requires_grad and conv.kernel_size == (k, k) and k <= 4 and conv.stride == (1, 1)
             and conv.padding == (k // 2, k // 2) and k % 2 == 1 and conv.dilation == (1, 1)
