@@ -57,8 +57,9 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
 std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& residual,
                                       const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
-                                      const at::Tensor& mean, const c10::optional<at::Tensor>& scale,
-                                      const c10::optional<at::Tensor>& shift,
+                                      const at::Tensor& mean, const c10::optional<at::Tensor>& invstd,
+                                      const c10::optional<at::Tensor>& weight,
+                                      const c10::optional<at::Tensor>& bias,
                                       const std::vector<int64_t>& res_map);
 // cross_entropy.hip
 std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& x, const at::Tensor& target,
@@ -101,8 +102,9 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& bn_x,
                                      const c10::optional<at::Tensor>& bn_y,
                                      const c10::optional<at::Tensor>& mean,
-                                     const c10::optional<at::Tensor>& scale,
-                                     const c10::optional<at::Tensor>& shift,
+                                     const c10::optional<at::Tensor>& invstd,
+                                     const c10::optional<at::Tensor>& weight,
+                                     const c10::optional<at::Tensor>& bias,
                                      const std::vector<int64_t>& res_map);
 // attention.hip
 bool attention_supported(int64_t S, int64_t head_dim);
@@ -177,8 +179,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cross_entropy_bwd", &dmp::cross_entropy_bwd, py::arg("grad"), py::arg("x"), py::arg("target"),
         py::arg("lse"), py::arg("stats"), py::arg("ignore_index") = -100);
   m.def("gemm_nt_bnbwd", &dmp::gemm_nt_bnbwd, py::arg("A"), py::arg("B"), py::arg("residual"),
-        py::arg("bn_x"), py::arg("bn_y"), py::arg("mean"), py::arg("scale"), py::arg("shift"),
-        py::arg("res_map") = std::vector<int64_t>{});
+        py::arg("bn_x"), py::arg("bn_y"), py::arg("mean"), py::arg("invstd"), py::arg("weight"),
+        py::arg("bias"), py::arg("res_map") = std::vector<int64_t>{});
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
@@ -213,8 +215,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("residual") = py::none(), py::arg("out") = py::none());
   m.def("gemm_xl_conv", &dmp::gemm_xl_conv, py::arg("A"), py::arg("B"), py::arg("mode"),
         py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
-        py::arg("mean") = py::none(), py::arg("scale") = py::none(), py::arg("shift") = py::none(),
-        py::arg("res_map") = std::vector<int64_t>{});
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
+        py::arg("bias") = py::none(), py::arg("res_map") = std::vector<int64_t>{});
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
 

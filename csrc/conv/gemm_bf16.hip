@@ -113,7 +113,9 @@ struct NtArgs {
   // mean and the forward affine (sc, sh) for the mask when y is absent
   const bf16* bx; int64_t ldbx;
   const bf16* bny; int64_t ldby;
-  const float *bmean, *bsc, *bsh;
+  // mask affine x*sc + sh > 0 with sc = invstd * w, sh = b - mean * sc (w, b optional),
+  // computed per column in the epilogue (no coefficient kernels on the host side)
+  const float *bmean, *binv, *bw, *bb;
   CompactMap rmap;              // EPI_BNBWD residual R in compact stride-s form
 };
 
@@ -369,8 +371,8 @@ void gemm_nt_kernel(const NtArgs p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bmu[j] = col_ok ? p.bmean[col + j] : 0.f;
-      bsc[j] = (col_ok && !p.bny) ? p.bsc[col + j] : 0.f;
-      bsh[j] = (col_ok && !p.bny) ? p.bsh[col + j] : 0.f;
+      bsc[j] = (col_ok && !p.bny) ? p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f) : 0.f;
+      bsh[j] = (col_ok && !p.bny) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
     }
   }
 #pragma unroll
@@ -1128,7 +1130,8 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
 // Data gradient of a 1x1 conv whose input is a training-mode BN(+residual)+ReLU
 // output, fused with that BN's backward reductions (EPI_BNBWD):
 //   G  = bf16(A @ B^T (+ residual))          A = dy [M, K], B = W^T [N, K]
-//   dz = G * mask,  mask = y > 0 (bn_y given) or x*scale + shift > 0
+//   dz = G * mask,  mask = y > 0 (bn_y given) or x*sc + sh > 0 with
+//        sc = invstd * weight, sh = bias - mean * sc (weight / bias optional)
 //   returns (dz [M, N], fp64 [2N+1] = (sum dz, sum dz*(x - mean), M))
 CompactMap parse_compact(const std::vector<int64_t>& g, int64_t M) {
   CompactMap c;
@@ -1144,8 +1147,9 @@ CompactMap parse_compact(const std::vector<int64_t>& g, int64_t M) {
 std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& residual,
                                       const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
-                                      const at::Tensor& mean, const c10::optional<at::Tensor>& scale,
-                                      const c10::optional<at::Tensor>& shift,
+                                      const at::Tensor& mean, const c10::optional<at::Tensor>& invstd,
+                                      const c10::optional<at::Tensor>& weight,
+                                      const c10::optional<at::Tensor>& bias,
                                       const std::vector<int64_t>& res_map) {
   check_operand(A, "A");
   check_operand(B, "B");
@@ -1172,9 +1176,10 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
     a.bny = reinterpret_cast<const bf16*>(bn_y->data_ptr());
     a.ldby = bn_y->stride(0);
   } else {
-    TORCH_CHECK(scale.has_value() && shift.has_value(), "mask from x needs the BN scale and shift");
-    a.bsc = f32vec(*scale, "scale");
-    a.bsh = f32vec(*shift, "shift");
+    TORCH_CHECK(invstd.has_value() && invstd->defined(), "mask from x needs the BN invstd");
+    a.binv = f32vec(*invstd, "invstd");
+    if (weight.has_value() && weight->defined()) a.bw = f32vec(*weight, "weight");
+    if (bias.has_value() && bias->defined()) a.bb = f32vec(*bias, "bias");
   }
   auto C = at::empty({a.M, a.N}, A.options());
   a.A = reinterpret_cast<const bf16*>(A.data_ptr());

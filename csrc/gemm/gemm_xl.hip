@@ -115,7 +115,7 @@ struct XlArgs {
   double* zsums;                // moments target to zero (common.h) or null
   const bf16* bx; int64_t ldbx; // XL_BNBWD: BN input x [M, N]
   const bf16* bny; int64_t ldby;// XL_BNBWD: BN output y [M, N] (mask source) or null
-  const float *bmean, *bsc, *bsh;
+  const float *bmean, *binv, *bw, *bb;  // mask affine as in gemm_bf16.hip EPI_BNBWD
   CompactMap rmap;              // XL_BNBWD residual in compact stride-s form
 };
 
@@ -354,7 +354,10 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         bmu[j] = p.bmean[col + j];
-        if (!p.bny) { bsc[j] = p.bsc[col + j]; bsh[j] = p.bsh[col + j]; }
+        if (!p.bny) {
+          bsc[j] = p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f);
+          bsh[j] = (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j];
+        }
       }
     }
   }
@@ -809,8 +812,9 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& bn_x,
                                      const c10::optional<at::Tensor>& bn_y,
                                      const c10::optional<at::Tensor>& mean,
-                                     const c10::optional<at::Tensor>& scale,
-                                     const c10::optional<at::Tensor>& shift,
+                                     const c10::optional<at::Tensor>& invstd,
+                                     const c10::optional<at::Tensor>& weight,
+                                     const c10::optional<at::Tensor>& bias,
                                      const std::vector<int64_t>& res_map) {
   check_bf16_2d(A, "A");
   check_bf16_2d(B, "B");
@@ -861,8 +865,9 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
       TORCH_CHECK(bn_y->size(0) == M && bn_y->size(1) == N, "bn_y shape");
       a.bny = reinterpret_cast<const bf16*>(bn_y->data_ptr()); a.ldby = bn_y->stride(0);
     } else {
-      a.bsc = f32vec(scale, "scale");
-      a.bsh = f32vec(shift, "shift");
+      a.binv = f32vec(invstd, "invstd");
+      if (weight.has_value() && weight->defined()) a.bw = f32vec(weight, "weight");
+      if (bias.has_value() && bias->defined()) a.bb = f32vec(bias, "bias");
     }
   }
   const int bn = pick_bn((int)M, (int)N);

@@ -210,11 +210,6 @@ class BnBwdSlot:
         self.dz_shape = None
         self.x2 = self.y2 = self.mean = self.invstd = self.w32 = self.b32 = None
 
-    def mask_affine(self):
-        sc = self.invstd * (self.w32 if self.w32 is not None else 1.0)
-        sh = (self.b32 if self.b32 is not None else 0.0) - self.mean * sc
-        return sc.contiguous(), sh.contiguous()
-
     def park(self, dz: torch.Tensor, sums: torch.Tensor) -> None:
         self.sums = sums
         self.dz_ptr, self.dz_ver, self.dz_shape = dz.data_ptr(), dz._version, tuple(dz.shape)

@@ -145,9 +145,10 @@ class _Conv1x1Fn(torch.autograd.Function):
                 if extra is not None:
                     _STATS["fused_dgrad"] += 1
                     extra = _rows(extra.to(x.dtype).contiguous(memory_format=torch.channels_last))
-                sc = sh = None
-                if bs.y2 is None:
-                    sc, sh = bs.mask_affine()
+                # mask affine (x*invstd*w + b - mean*invstd*w > 0) is formed in the epilogue
+                inv = bs.invstd if bs.y2 is None else None
+                bw = bs.w32 if bs.y2 is None else None
+                bb = bs.b32 if bs.y2 is None else None
                 rmap = []
                 if cextra is not None:
                     if extra is not None:  # both a full and a compact parked gradient: expand
@@ -161,11 +162,11 @@ class _Conv1x1Fn(torch.autograd.Function):
                 if _xl(cin, cout):
                     _STATS["xl"] += 1
                     dx2, sums = C.gemm_xl_conv(dy2, w2.t().contiguous(), "bnbwd", residual=extra,
-                                               bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean.contiguous(),
-                                               scale=sc, shift=sh, res_map=rmap)
+                                               bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean, invstd=inv,
+                                               weight=bw, bias=bb, res_map=rmap)
                 else:
                     dx2, sums = C.gemm_nt_bnbwd(dy2, w2.t().contiguous(), extra, bs.x2, bs.y2,
-                                                bs.mean.contiguous(), sc, sh, rmap)
+                                                bs.mean, inv, bw, bb, rmap)
                 dx = _unrows(dx2, n, h, w)
                 bs.park(dx, sums[: 2 * cin])
                 dx2 = None

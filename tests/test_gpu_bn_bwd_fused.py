@@ -27,12 +27,15 @@ def test_gemm_nt_bnbwd_kernel(M, N, K, mask_from_y, with_res):
     wt = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()      # W^T as the NT "B" operand
     x = torch.randn(M, N, device=DEV).bfloat16()               # BN input
     mean = x.float().mean(0)
-    sc = torch.rand(N, device=DEV) + 0.5
-    sh = torch.randn(N, device=DEV) * 0.5
+    inv = torch.rand(N, device=DEV) + 0.5                       # BN invstd
+    bw = torch.rand(N, device=DEV) + 0.5                        # BN weight, bias
+    bb = torch.randn(N, device=DEV) * 0.5
+    sc = inv * bw
+    sh = bb - mean * sc
     res = torch.randn(M, N, device=DEV).bfloat16() if with_res else None
     y = torch.relu(x.float() * sc + sh + (res.float() if with_res else 0)).bfloat16() if mask_from_y else None
-    dz, sums = C.gemm_nt_bnbwd(dy, wt, res, x, y, mean, None if mask_from_y else sc,
-                               None if mask_from_y else sh)
+    dz, sums = C.gemm_nt_bnbwd(dy, wt, res, x, y, mean, None if mask_from_y else inv,
+                               None if mask_from_y else bw, None if mask_from_y else bb)
     g = dy.float() @ wt.float().t()
     if with_res:
         g = g.bfloat16().float() + res.float()
@@ -116,18 +119,18 @@ def test_bnbwd_compact_strided_residual(xl):
     wt = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
     x = torch.randn(M, N, device=DEV).bfloat16()
     mean = x.float().mean(0)
-    sc = torch.rand(N, device=DEV) + 0.5
-    sh = torch.randn(N, device=DEV) * 0.5
+    inv = torch.rand(N, device=DEV) + 0.5
+    bb = torch.randn(N, device=DEV) * 0.5
     comp = torch.randn(n * ho * wo, N, device=DEV).bfloat16()
     full = torch.zeros(n, h, w, N, device=DEV).bfloat16()
     full[:, ::s, ::s] = comp.view(n, ho, wo, N)
     full = full.view(M, N)
     rmap = [s, ho, wo, h, w]
     if xl:
-        a = C.gemm_xl_conv(dy, wt, "bnbwd", residual=comp, bn_x=x, mean=mean, scale=sc, shift=sh, res_map=rmap)
-        b = C.gemm_xl_conv(dy, wt, "bnbwd", residual=full, bn_x=x, mean=mean, scale=sc, shift=sh)
+        a = C.gemm_xl_conv(dy, wt, "bnbwd", residual=comp, bn_x=x, mean=mean, invstd=inv, bias=bb, res_map=rmap)
+        b = C.gemm_xl_conv(dy, wt, "bnbwd", residual=full, bn_x=x, mean=mean, invstd=inv, bias=bb)
     else:
-        a = C.gemm_nt_bnbwd(dy, wt, comp, x, None, mean, sc, sh, rmap)
-        b = C.gemm_nt_bnbwd(dy, wt, full, x, None, mean, sc, sh)
+        a = C.gemm_nt_bnbwd(dy, wt, comp, x, None, mean, inv, None, bb, rmap)
+        b = C.gemm_nt_bnbwd(dy, wt, full, x, None, mean, inv, None, bb)
     torch.testing.assert_close(a[0], b[0])
     torch.testing.assert_close(a[1], b[1], atol=1e-6, rtol=1e-9)

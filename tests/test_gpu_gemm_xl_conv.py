@@ -48,13 +48,15 @@ def test_xl_bnbwd_matches_nt(mask_from_y, with_res):
     wt = (torch.randn(N, K, device=DEV) * 0.1).bfloat16()
     x = torch.randn(M, N, device=DEV).bfloat16()
     mean = x.float().mean(0)
-    sc = torch.rand(N, device=DEV) + 0.5
-    sh = torch.randn(N, device=DEV) * 0.5
+    inv = torch.rand(N, device=DEV) + 0.5
+    bw = torch.rand(N, device=DEV) + 0.5
+    bb = torch.randn(N, device=DEV) * 0.5
     res = torch.randn(M, N, device=DEV).bfloat16() if with_res else None
-    y = torch.relu(x.float() * sc + sh).bfloat16() if mask_from_y else None
-    s_, t_ = (None, None) if mask_from_y else (sc, sh)
-    dz, sums = C().gemm_xl_conv(dy, wt, "bnbwd", residual=res, bn_x=x, bn_y=y, mean=mean, scale=s_, shift=t_)
-    dz0, sums0 = C().gemm_nt_bnbwd(dy, wt, res, x, y, mean, s_, t_)
+    y = torch.relu(x.float() * inv * bw + bb - mean * inv * bw).bfloat16() if mask_from_y else None
+    i_, w_, b_ = (None, None, None) if mask_from_y else (inv, bw, bb)
+    dz, sums = C().gemm_xl_conv(dy, wt, "bnbwd", residual=res, bn_x=x, bn_y=y, mean=mean, invstd=i_,
+                                weight=w_, bias=b_)
+    dz0, sums0 = C().gemm_nt_bnbwd(dy, wt, res, x, y, mean, i_, w_, b_)
     torch.testing.assert_close(dz.float(), dz0.float(), atol=2e-2, rtol=1e-2)
     dzd = dz.double()
     torch.testing.assert_close(sums[:N], dzd.sum(0), atol=1e-2, rtol=1e-4)

@@ -43,12 +43,11 @@ def main():
         dy = torch.randn(M, cout, device="cuda").bfloat16()
         wt = w.t().contiguous()
         mean = torch.zeros(cin, device="cuda")
-        sc = torch.ones(cin, device="cuda")
-        sh = torch.zeros(cin, device="cuda")
+        inv = torch.ones(cin, device="cuda")
         f_nt = timeit(lambda: C.gemm_nt(x, w, mode="moments"))
         f_xl = timeit(lambda: C.gemm_xl_conv(x, w, "moments")) if cout % 8 == 0 and cin % 64 == 0 else float("nan")
-        d_nt = timeit(lambda: C.gemm_nt_bnbwd(dy, wt, None, x, None, mean, sc, sh))
-        d_xl = timeit(lambda: C.gemm_xl_conv(dy, wt, "bnbwd", bn_x=x, mean=mean, scale=sc, shift=sh)) \
+        d_nt = timeit(lambda: C.gemm_nt_bnbwd(dy, wt, None, x, None, mean, inv, None, None))
+        d_xl = timeit(lambda: C.gemm_xl_conv(dy, wt, "bnbwd", bn_x=x, mean=mean, invstd=inv)) \
             if cout % 64 == 0 else float("nan")
         print(f"| {name} | {M} | {cin} | {cout} | {f_nt:.3f} | {f_xl:.3f} | {d_nt:.3f} | {d_xl:.3f} |", flush=True)
         del x, w, dy, wt
