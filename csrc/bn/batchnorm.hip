@@ -28,6 +28,8 @@
 //     row-slab-0 blocks write dweight/dbias.
 // Forward = moments + reduce + apply, backward = moments + reduce + apply (the
 // moments pass disappears when the producing GEMM/depthwise kernel emits them).
+#include <cstdlib>
+
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "../common.h"
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
 // also save mean/invstd and update running stats.  Otherwise eval mode --
 // coefficients from running stats.
 // -------------------------------------------------------------------------
-template <typename T, bool RELU, bool RES, bool FROM_SUMS>
+template <typename T, bool RELU, bool RES, bool FROM_SUMS, bool NT = false>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ res, const double* __restrict__ sums,
     const float* __restrict__ weight, const float* __restrict__ bias,
@@ -282,11 +284,11 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
   for (; r + L.rpi < r1; r += 2 * L.rpi) {
     const int64_t o = r * C + off0, o2 = o + (int64_t)L.rpi * C;
     float v[VEC], v2[VEC], rv[VEC], rv2[VEC];
-    Vec16<T>::load(x + o, v);
-    Vec16<T>::load(x + o2, v2);
+    ld16<NT>(x + o, v);
+    ld16<NT>(x + o2, v2);
     if (RES) {
-      Vec16<T>::load(res + o, rv);
-      Vec16<T>::load(res + o2, rv2);
+      ld16<NT>(res + o, rv);
+      ld16<NT>(res + o2, rv2);
     }
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
@@ -296,14 +298,14 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
       v[i] = t;
       v2[i] = t2;
     }
-    Vec16<T>::store(y + o, v);
-    Vec16<T>::store(y + o2, v2);
+    st16<NT>(y + o, v);
+    st16<NT>(y + o2, v2);
   }
   if (r < r1) {
     const int64_t o = r * C + off0;
     float v[VEC], rv[VEC];
-    Vec16<T>::load(x + o, v);
-    if (RES) Vec16<T>::load(res + o, rv);
+    ld16<NT>(x + o, v);
+    if (RES) ld16<NT>(res + o, rv);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) {
       float t = fmaf(v[i], sc[i], sh[i]);
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
       if (RELU) t = fmaxf(t, 0.f);
       v[i] = t;
     }
-    Vec16<T>::store(y + o, v);
+    st16<NT>(y + o, v);
   }
 }
 
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
 // Backward pass 2: dx = a*dz + b*x + c ; dres = dz (residual fused); the
 // row-slab-0 blocks write dweight = sum(dz*(x-mean))*invstd, dbias = sum(dz).
 // -------------------------------------------------------------------------
-template <typename T, int RELU, bool DRES>
+template <typename T, int RELU, bool DRES, bool NT = false>
 __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const double* __restrict__ sums, const double* __restrict__ count_ptr,
@@ -427,21 +429,21 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   for (int64_t r = r0 + lr; r < r1; r += L.rpi) {
     const int64_t o = r * C + off0;
     float g[VEC], xv[VEC];
-    Vec16<T>::load(dy + o, g);
-    Vec16<T>::load(x + o, xv);
+    ld16<NT>(dy + o, g);
+    ld16<NT>(x + o, xv);
     if (RELU == 1) {
       float yv[VEC];
-      Vec16<T>::load(y + o, yv);
+      ld16<NT>(y + o, yv);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
     } else if (RELU == 2) {
 #pragma unroll
       for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
     }
-    if (DRES) Vec16<T>::store(dres + o, g);
+    if (DRES) st16<NT>(dres + o, g);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) xv[i] = fmaf(a[i], g[i], fmaf(b[i], xv[i], c[i]));
-    Vec16<T>::store(dx + o, xv);
+    st16<NT>(dx + o, xv);
   }
 }
 
@@ -487,6 +489,16 @@ void dispatch_t(const at::Tensor& x, F&& f) {
 }
 
 template <typename T> T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+// Non-temporal streaming for the apply passes over tensors much larger than
+// the Infinity Cache (DMP_BN_NT=0 disables, for A/B runs).
+bool streaming(int64_t M, int64_t C) {
+  static const bool on = [] {
+    const char* e = std::getenv("DMP_BN_NT");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on && M * C * 2 >= (int64_t)256 << 20;
+}
 float* fptr(const c10::optional<at::Tensor>& t) {
   return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
 }
@@ -550,17 +562,20 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
     dispatch_t(x, [&](auto tag) {
       using T = decltype(tag);
       const T* r = has_res ? ptr<T>(*residual) : nullptr;
-#define DMP_BN_FWD(RELU, RES)                                                                    \
-  hipLaunchKernelGGL((bn_apply_kernel<T, RELU, RES, true>), g.grid, dim3(kThreads), 0, stream,   \
+#define DMP_BN_FWD1(RELU, RES, NT)                                                               \
+  hipLaunchKernelGGL((bn_apply_kernel<T, RELU, RES, true, NT>), g.grid, dim3(kThreads), 0, stream, \
                      ptr<T>(x), r, sums.data_ptr<double>(), fptr(weight), fptr(bias),            \
                      fptr(running_mean), fptr(running_var), (float)momentum, (float)eps, M,      \
                      (int)C, g.rows_per_block, ptr<T>(y), saved.data_ptr<float>(),               \
                      saved.data_ptr<float>() + C, nbt)
+#define DMP_BN_FWD(RELU, RES) \
+  do { if (streaming(M, C)) DMP_BN_FWD1(RELU, RES, true); else DMP_BN_FWD1(RELU, RES, false); } while (0)
       if (relu && has_res) DMP_BN_FWD(true, true);
       else if (relu) DMP_BN_FWD(true, false);
       else if (has_res) DMP_BN_FWD(false, true);
       else DMP_BN_FWD(false, false);
 #undef DMP_BN_FWD
+#undef DMP_BN_FWD1
     });
   }
   return {y, saved[0], saved[1]};
@@ -687,8 +702,10 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
       const bool from_y = relu && y.has_value() && y->defined();
       const T* yp = from_y ? ptr<T>(*y) : nullptr;
       T* dr = want_dres ? ptr<T>(dres) : nullptr;
-#define DMP_BN_BWD(RELU, DRES)                                                                    \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU, DRES>), g.grid, dim3(kThreads), 0, stream,     \
+#define DMP_BN_BWD(RELU, DRES) \
+  do { if (streaming(M, C)) DMP_BN_BWD1(RELU, DRES, true); else DMP_BN_BWD1(RELU, DRES, false); } while (0)
+#define DMP_BN_BWD1(RELU, DRES, NT)                                                               \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU, DRES, NT>), g.grid, dim3(kThreads), 0, stream, \
                      ptr<T>(dy), ptr<T>(x), yp, sums.data_ptr<double>(), count.data_ptr<double>(), \
                      fptr(weight), fptr(bias), mean.data_ptr<float>(), invstd.data_ptr<float>(),  \
                      (int)training, M, (int)C, g.rows_per_block, ptr<T>(dx), dr,                  \
@@ -701,6 +718,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
       else if (want_dres) DMP_BN_BWD(0, true);
       else DMP_BN_BWD(0, false);
 #undef DMP_BN_BWD
+#undef DMP_BN_BWD1
     });
   }
   return {dx, dwb[0], dwb[1], dres};

@@ -57,6 +57,47 @@ template <> struct Vec16<__bf16> {
   }
 };
 
+// Streaming (non-temporal) 16-B accesses for tensors touched exactly once per
+// pass and far larger than the 256 MB Infinity Cache (BN apply passes over
+// 0.4-1.6 GB activations): the nt policy keeps them from evicting reused lines.
+template <bool NT, typename T>
+__device__ __forceinline__ void ld16(const T* p, float (&v)[Vec16<T>::N]) {
+  if constexpr (NT) {
+    using R = typename Vec16<T>::raw;
+    const R r = __builtin_nontemporal_load(reinterpret_cast<const R*>(p));
+    if constexpr (Vec16<T>::N == 8) {
+      const f32x8 f = __builtin_convertvector(r, f32x8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = f[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = r[i];
+    }
+  } else {
+    Vec16<T>::load(p, v);
+  }
+}
+
+template <bool NT, typename T>
+__device__ __forceinline__ void st16(T* p, const float (&v)[Vec16<T>::N]) {
+  if constexpr (NT) {
+    using R = typename Vec16<T>::raw;
+    R r;
+    if constexpr (Vec16<T>::N == 8) {
+      f32x8 f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = v[i];
+      r = __builtin_convertvector(f, bf16x8);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = v[i];
+    }
+    __builtin_nontemporal_store(r, reinterpret_cast<R*>(p));
+  } else {
+    Vec16<T>::store(p, v);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
