@@ -36,6 +36,7 @@
 // K-tile's global loads are issued before the current tile's MFMAs.  The
 // epilogue restages the accumulator tile through LDS so C is written with
 // 16-byte row-contiguous stores.  Blocks are remapped XCD-aware (T1).
+#include <cstdlib>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "../common.h"
@@ -468,6 +469,11 @@ int g_tile_override = -1;
 // Strided transposed convs (data gradients) as stride-phase launches (default)
 // or the plain zero-tap gather (set_phase_dgrad(false), for A/B runs).
 bool g_phase_dgrad = true;
+// Wide (128 x 256) TN tiles for deep weight gradients; set_tn_wide for A/B runs.
+bool g_tn_wide = [] {
+  const char* e = std::getenv("DMP_TN_WIDE");
+  return !(e && e[0] == '0');
+}();
 
 template <bool PRO, int EPI, bool CONV>
 void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {
@@ -534,8 +540,8 @@ __device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
 // PRO_B: B' = relu(B * s[k] + t[k]) applied while staging B (the weight
 // gradient of a conv whose input is a BN+ReLU output that was never
 // materialised -- ops/fused.py bn_relu_conv1x1).
-template <int BNT, int BKT, bool PRO_B>
-__global__ __launch_bounds__(kThreads, 2) void gemm_tn_kernel(
+template <int BNT, int BKT, bool PRO_B, int MINB = 2>
+__global__ __launch_bounds__(kThreads, MINB) void gemm_tn_kernel(
     const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B, int64_t ldb, int M, int N,
     int K, int64_t rows_per_split, float* __restrict__ part, ConvMap bmap,
     const float* __restrict__ bps, const float* __restrict__ bpt) {
@@ -754,16 +760,25 @@ void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, fl
                int splits, int64_t rps, const ConvMap& bm, const float* bps, const float* bpt,
                hipStream_t s) {
   const int tiles = ((N + BNT - 1) / BNT) * ((K + BKT - 1) / BKT);
-  if (bps)
+  // the 128 x 256 tile holds 128 accumulator VGPRs per lane and 96 KB of LDS: 1 block/CU
+  constexpr int MINB = BKT * BNT > 128 * 128 ? 1 : 2;
+  if constexpr (MINB == 1) {
+    TORCH_CHECK(bps == nullptr, "wide TN tile has no B prologue variant");
+    hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT, false, 1>), dim3(tiles * splits), dim3(kThreads), 0, s,
+                       reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
+                       reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part,
+                       bm, nullptr, nullptr);
+  } else if (bps) {
     hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT, true>), dim3(tiles * splits), dim3(kThreads), 0, s,
                        reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
                        reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part,
                        bm, bps, bpt);
-  else
+  } else {
     hipLaunchKernelGGL((gemm_tn_kernel<BNT, BKT, false>), dim3(tiles * splits), dim3(kThreads), 0, s,
                        reinterpret_cast<const bf16*>(A.data_ptr()), A.stride(0),
                        reinterpret_cast<const bf16*>(B.data_ptr()), B.stride(0), M, N, K, rps, part,
                        bm, nullptr, nullptr);
+  }
 }
 
 }  // namespace
@@ -777,7 +792,10 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   auto stream = at::hip::getCurrentHIPStream();
   auto out = at::empty({N, K}, A.options().dtype(out_dtype));
   if (M == 0) return out.zero_();
-  const int bnt = N >= 128 ? 128 : 64, bkt = (K >= 128 && kgran % 128 == 0) ? 128 : 64;
+  // 128 x 256 output tiles (1 block/CU) halve the L2 re-reads of A (dy) for deep
+  // implicit-GEMM weight gradients (K = taps * Cin, Cin % 256 == 0): g_tn_wide
+  const bool wide = g_tn_wide && bps == nullptr && N >= 128 && K >= 256 && kgran % 256 == 0;
+  const int bnt = N >= 128 ? 128 : 64, bkt = wide ? 256 : ((K >= 128 && kgran % 128 == 0) ? 128 : 64);
   const int tiles = ((N + bnt - 1) / bnt) * ((K + bkt - 1) / bkt);
   // ~4 blocks per CU, but keep the fp32 partial traffic well under the operand
   // traffic (the GEMM streams (N+K)*M bf16; partials cost 2 * splits*N*K*4 B).
@@ -794,7 +812,8 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   splits = (int)(((int64_t)M + rps - 1) / rps);
   auto part = at::empty({splits, N, K}, A.options().dtype(at::kFloat));
   float* pp = part.data_ptr<float>();
-  if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
+  if (bkt == 256) launch_tn<128, 256>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
+  else if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
@@ -1194,5 +1213,6 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
 
 void set_gemm_tile(int64_t t) { g_tile_override = (int)t; }
 void set_phase_dgrad(bool on) { g_phase_dgrad = on; }
+void set_tn_wide(bool on) { g_tn_wide = on; }
 
 }  // namespace dmp

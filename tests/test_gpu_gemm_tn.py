@@ -110,3 +110,38 @@ def test_gemm_tn_b_prologue():
     got = C.gemm_tn(a, b, torch.float32, pro_scale=s, pro_shift=t)
     bp = torch.relu(b.float() * s + t).bfloat16().float()
     torch.testing.assert_close(got, a.float().t() @ bp, atol=1e-3 * M ** 0.5, rtol=1e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(5000, 200, 768), (131, 128, 256), (40000, 512, 2304)])
+def test_gemm_tn_wide_tile(M, N, K):
+    """128 x 256 tiles (deep weight gradients) vs the fp32 reference, ragged N edge."""
+    C = _native.require("gemm_tn")
+    torch.manual_seed(6)
+    a = torch.randn(M, N, device=DEV).bfloat16()
+    b = torch.randn(M, K, device=DEV).bfloat16()
+    ref = a.float().t() @ b.float()
+    C.set_tn_wide(True)
+    got = C.gemm_tn(a, b, torch.float32)
+    C.set_tn_wide(False)
+    try:
+        narrow = C.gemm_tn(a, b, torch.float32)
+    finally:
+        C.set_tn_wide(True)
+    tol = 1e-3 * M ** 0.5
+    torch.testing.assert_close(got, ref, atol=tol, rtol=1e-2)
+    torch.testing.assert_close(got, narrow, atol=tol, rtol=1e-2)
+
+
+def test_conv_wgrad_wide_tile_3x3():
+    """Implicit-GEMM 3x3 weight gradient with Cin % 256 == 0 (wide tile, one tap per K tile)."""
+    C = _native.require("conv_wgrad")
+    torch.manual_seed(7)
+    n, cin, cout, h = 4, 256, 192, 9
+    x = torch.randn(n, cin, h, h, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(n, cout, h, h, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+    got = C.conv_wgrad(dy2, x, 3, 3, 1, 1, h, h, torch.float32).view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    xr = x.float().requires_grad_()
+    wr = torch.zeros(cout, cin, 3, 3, device=DEV, requires_grad=True)
+    F.conv2d(xr, wr, None, 1, 1).backward(dy.float())
+    torch.testing.assert_close(got, wr.grad, atol=1e-3 * (n * h * h) ** 0.5, rtol=1e-2)

@@ -63,6 +63,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--only", default="", help="comma-separated name prefixes (e.g. l4,stem)")
+    ap.add_argument("--tn-ab", action="store_true", help="also time weight gradients with narrow TN tiles")
     a = ap.parse_args()
     only = [p for p in a.only.split(",") if p]
     C = _native.require("conv roofline")
@@ -121,6 +122,15 @@ def main():
             wtr = w.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
             res["dgrad"]["ours"] = timeit(lambda: C.conv_nt(dy, wtr, k, k, s, pad, h, h, transposed=True))
             res["wgrad"]["ours"] = timeit(lambda: C.conv_wgrad(dy2, x, k, k, s, pad, ho, ho, dt))
+        if a.tn_ab and "ours" in res["wgrad"] and name != "stem":
+            # A/B of the 128 x 256 TN tile: the narrow-tile time under its own column
+            C.set_tn_wide(False)
+            if k == 1:
+                res["wgrad"]["narrow"] = timeit(lambda: C.gemm_tn(dy2, x2, dt, b_map=geom))
+            else:
+                res["wgrad"]["narrow"] = timeit(lambda: C.conv_wgrad(dy2, x, k, k, s, pad, ho, ho, dt))
+            C.set_tn_wide(True)
+            print(f"  {name} wgrad: wide-enabled {res['wgrad']['ours']:.3f} narrow {res['wgrad']['narrow']:.3f}")
         for p in ("fwd", "dgrad", "wgrad"):
             if name == "stem" and p == "dgrad":
                 continue  # the input image needs no gradient
