@@ -98,6 +98,12 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out);
 void set_gemm_xl_bn(int bn, int pipe, int group_m);
+std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
+                                int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
+                                const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& bn_x,
+                                const c10::optional<at::Tensor>& bn_y, const c10::optional<at::Tensor>& mean,
+                                const c10::optional<at::Tensor>& invstd, const c10::optional<at::Tensor>& weight,
+                                const c10::optional<at::Tensor>& bias);
 std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
                                      const c10::optional<at::Tensor>& residual,
                                      const c10::optional<at::Tensor>& bn_x,
@@ -216,11 +222,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_xl", &dmp::gemm_xl, py::arg("A"), py::arg("B"), py::arg("mode") = "store",
         py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("residual") = py::none(), py::arg("out") = py::none());
+  m.def("conv_xl", &dmp::conv_xl, py::arg("x"), py::arg("wmat"), py::arg("kh"), py::arg("kw"),
+        py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("mode") = "moments",
+        py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
+        py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
+        py::arg("bias") = py::none(),
+        "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues");
   m.def("gemm_xl_conv", &dmp::gemm_xl_conv, py::arg("A"), py::arg("B"), py::arg("mode"),
         py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(), py::arg("res_map") = std::vector<int64_t>{});
-  m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 1, py::arg("group_m") = 0,
+  m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 7, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
 
   // ---- fused self-attention on packed qkv (ViT) ----

@@ -38,6 +38,7 @@
 //     adjacent (they share the A panel in L2);
 //   * epilogue restages the tile through LDS for 16-B row-contiguous stores.
 #include <torch/extension.h>
+#include <type_traits>
 #include <ATen/hip/HIPContext.h>
 #include "../common.h"
 
@@ -59,13 +60,32 @@ __device__ __forceinline__ void glds16(const void* g, char* l) {
   __builtin_amdgcn_global_load_lds((gptr_t)g, (lptr_t)l, 16, 0, 0);
 }
 
+// Exact-GELU pieces for the epilogues: Phi(x) via erf(|x|/sqrt2) from
+// Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, far below the bf16 output's
+// 2^-9 relative rounding) and phi(x) from the SAME exponential, since
+// exp(-z^2) with z = x/sqrt2 is exp(-x^2/2).  ~12 VALU ops against erff's
+// ~40: the epilogue runs after the MFMA loop at 1 block/CU, so its VALU time
+// is not hidden (libm erff made the fused fc1 epilogue cost more than the
+// separate GELU pass it replaces).
+__device__ __forceinline__ void gelu_parts(float x, float& cdf, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  const float e = __expf(-z * z);
+  const float poly =
+      fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t, 0.254829592f) * t;
+  const float erf_abs = fmaf(-poly, e, 1.f);
+  cdf = 0.5f + 0.5f * copysignf(erf_abs, x);
+  pdf = 0.39894228040143268f * e;
+}
 __device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+  float c, d;
+  gelu_parts(x, c, d);
+  return x * c;
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float c, d;
+  gelu_parts(x, c, d);
+  return fmaf(x, d, c);
 }
 
 // 16-B chunk swizzle of a k32 region (rows of 64 B = 4 chunks, 4 rows per
@@ -102,6 +122,16 @@ __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Implicit-GEMM convolution view of the A operand (PIPE 7 only): GEMM row m
+// is output pixel (n, oh, ow) of an NHWC input [N, Hi, Wi, cin]; K tile kt
+// is channels c0..c0+63 of tap (tr, tc), K = taps * cin.  cin == 0: plain GEMM.
+struct XlConv {
+  int cin = 0, hi = 0, wi = 0, ho = 0, wo = 0, stride = 1, pad = 0, kw = 1;
+};
+
+// 16-B reads of padding taps land here (LDS-DMA cannot write zeros itself).
+__device__ __attribute__((aligned(16))) bf16 g_zero_row[128] = {};
+
 struct XlArgs {
   const bf16* A; int64_t lda;
   const bf16* B; int64_t ldb;
@@ -117,6 +147,7 @@ struct XlArgs {
   const bf16* bny; int64_t ldby;// XL_BNBWD: BN output y [M, N] (mask source) or null
   const float *bmean, *binv, *bw, *bb;  // mask affine as in gemm_bf16.hip EPI_BNBWD
   CompactMap rmap;              // XL_BNBWD residual in compact stride-s form
+  XlConv cv;                    // implicit-GEMM conv gather of A (PIPE 7)
 };
 
 template <int BN, int EPI, int PIPE>
@@ -246,6 +277,151 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     if (has2) vmcnt<W2>(); else if (has1) vmcnt<NA + NB>(); else vmcnt<0>();
     barrier();
   }
+  } else if constexpr (PIPE == 7) {
+  // ---- PIPE 7: ping-pong quadrant schedule (cdna_hip_programming.md §5 "256²
+  // 8-phase template").  The two wave rows (wr) run one barrier apart: while
+  // one group's 4 waves run a phase's 16 MFMAs, the other group (one wave on
+  // each SIMD) issues that phase's ds_reads and LDS-DMA copies, so every SIMD
+  // alternates a MFMA wave and a memory wave between consecutive barriers.
+  // A K tile is 4 phases, one per quadrant (m half, n half) of the wave's
+  // 128 x 64 outputs, in the order (0,0) (0,1) (1,1) (1,0) so that each phase
+  // re-reads only one operand.  A tile's operands are staged as 4 units of
+  // 16 KB (2 glds per wave): U0 = A rows of m half 0, U3 = m half 1, U1 = B
+  // cols of n half 0, U2 = n half 1.  Phase r of tile t stages U3(t+1),
+  // U1(t+1), U0(t+2), U2(t+2) (r = 0..3): every unit is written >= 2 barrier
+  // slots after its previous contents were last read (WAR), and is retired by
+  // the vmcnt(4) of a phase >= 2 before its first reader (RAW: the counted
+  // wait -- never 0 in steady state -- then a barrier, then the ds_read).
+  static_assert(BN == 256, "ping-pong schedule is written for 256 x 256 tiles");
+  const int pks = wave >> 2;  // k32 half carried by this wave's two copies of a unit
+  const bf16* pa[2][2];
+  const bf16* pb[2][2];
+  int oa[2][2], ob[2][2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = (2 * wave + q) & 7;
+      const int ba = (j & 3) + 8 * (j >> 2) + 4 * v, bb = (j & 1) + 4 * (j >> 1) + 2 * v;
+      pa[v][q] = A + (int64_t)min(m0 + ba * 16 + srow, M - 1) * lda + schunk * 8 + pks * 32;
+      pb[v][q] = B + (int64_t)min(n0 + bb * 16 + srow, N - 1) * ldb + schunk * 8 + pks * 32;
+      oa[v][q] = ba * 1024;
+      ob[v][q] = bb * 1024;
+    }
+  // conv gather: per staged A row, its top-left input pixel and coordinates
+  const XlConv cv = p.cv;
+  const bool gather = cv.cin > 0;
+  const int loff = schunk * 8 + pks * 32;
+  int gpix[2][2], gih[2][2], giw[2][2];
+  if (gather) {
+    const int hw = cv.ho * cv.wo;
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = (2 * wave + q) & 7;
+        const int row = min(m0 + ((j & 3) + 8 * (j >> 2) + 4 * v) * 16 + srow, M - 1);
+        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+        gih[v][q] = oh * cv.stride - cv.pad;
+        giw[v][q] = ow * cv.stride - cv.pad;
+        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
+      }
+  }
+  auto stage_unit = [&](auto u, int kt) {
+    constexpr int U = decltype(u)::value;
+    const int buf = kt & 1, koff = kt * XBK;
+    if constexpr (U == 0 || U == 3) {
+      if (gather) {  // tap (tr, tc), channels c0.. of every staged output pixel, or zeros
+        const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
+        const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ih = gih[U == 3][q] + tr, iw = giw[U == 3][q] + tc;
+          const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
+          const bf16* src = ok ? A + (int64_t)(gpix[U == 3][q] + tr * cv.wi + tc) * lda + c0 + loff
+                               : g_zero_row + loff;
+          glds16(src, a_region(pks, buf) + oa[U == 3][q]);
+        }
+        return;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if constexpr (U == 0 || U == 3)
+        glds16(pa[U == 3][q] + koff, a_region(pks, buf) + oa[U == 3][q]);
+      else
+        glds16(pb[U == 2][q] + koff, b_region(pks, buf) + ob[U == 2][q]);
+    }
+  };
+  bf16x8 qa[2][4], qb[2][2];
+  auto read_a = [&](int mq, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        qa[ks][i] = *reinterpret_cast<const bf16x8*>(a_region(ks, buf) + (wr * WTM + mq * 64 + i * 16) * 64 + frag_off);
+  };
+  auto read_b = [&](int nq, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        qb[ks][j] = *reinterpret_cast<const bf16x8*>(b_region(ks, buf) + (wc * WTN + nq * 32 + j * 16) * 64 + frag_off);
+  };
+  auto quad = [&](auto mqc, auto nqc) {
+    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[MQ * 4 + i][NQ * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  stage_unit(I0{}, 0);
+  stage_unit(I2{}, 0);
+  stage_unit(I3{}, 0);
+  stage_unit(I1{}, 0);
+  if (ktiles > 1) {
+    stage_unit(I0{}, 1);
+    stage_unit(I2{}, 1);
+    vmcnt<4>();
+  } else {
+    vmcnt<0>();
+  }
+  barrier();
+  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    const bool n1 = kt + 1 < ktiles, n2 = kt + 2 < ktiles;
+    read_a(0, buf);
+    read_b(0, buf);
+    if (n1) { stage_unit(I3{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I0{}, I0{});
+    read_b(1, buf);
+    if (n1) { stage_unit(I1{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I0{}, I1{});
+    read_a(1, buf);
+    if (n2) { stage_unit(I0{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I1{}, I1{});
+    read_b(0, buf);
+    if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I1{}, I0{});
+  }
+  if (wr == 0) barrier();  // equal barrier counts before the epilogue
+  barrier();
   } else {
   // ---- PIPE 1: half-step ring.  Half-step s (K tile s/2, k32 half s%2) lives
   // in LDS region s%4.  During half-step s: stage region s%4 with the data of
@@ -659,7 +835,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_persistent_kernel(const X
 
 int g_num_cus = 0;
 
-int g_xl_pipe = 1;
+// main loop: 7 = ping-pong quadrant schedule (256-wide tiles; 128-wide tiles use the ring, 1)
+int g_xl_pipe = 7;
 
 template <int BN, int EPI>
 void launch_xl(const XlArgs& a, hipStream_t s) {
@@ -683,6 +860,12 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_xl_persistent_kernel<BN, EPI>), dim3(grid), dim3(XTHREADS), 0, s, a);
     return;
   }
+  if constexpr (BN == 256) {
+    if (g_xl_pipe == 7) {
+      hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+      return;
+    }
+  }
   if (g_xl_pipe == 0)
     hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 0>), dim3(blocks), dim3(XTHREADS), 0, s, a);
   else
@@ -695,6 +878,8 @@ void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
     const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + bn - 1) / bn);
     if (bn == 128)
       hipLaunchKernelGGL((gemm_xl_nt_kernel<128, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    else if (g_xl_pipe == 7)
+      hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     else
       hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     return;
@@ -714,8 +899,10 @@ int pick_bn(int M, int N) {
   auto eff = [&](int bn) {
     const double blocks = (double)((M + XBM - 1) / XBM) * ((N + bn - 1) / bn);
     const double rounds = std::ceil(blocks / cus);
-    // useful work / (rounds x tile work), with the smaller tile paying ~12%
-    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : 0.88);
+    // useful work / (rounds x tile work); the 128-wide tile runs the ring
+    // loop, ~12 % slower per FLOP than the 256-wide ring and ~25 % slower than
+    // the 256-wide ping-pong loop (profiles/vit_gemm_backends.md)
+    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : (g_xl_pipe == 7 ? 0.75 : 0.88));
   };
   return eff(128) > eff(256) ? 128 : 256;
 }
@@ -807,31 +994,29 @@ void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, d
 //   "add"    : C = bf16(bf16(A @ B^T) + residual)
 //   "bnbwd"  : C = dz = mask * bf16(A @ B^T (+ residual)), returns (sum dz, sum dz*(x-mean), M)
 //              (same contract as gemm_nt_bnbwd)
-std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
-                                     const c10::optional<at::Tensor>& residual,
-                                     const c10::optional<at::Tensor>& bn_x,
-                                     const c10::optional<at::Tensor>& bn_y,
-                                     const c10::optional<at::Tensor>& mean,
-                                     const c10::optional<at::Tensor>& invstd,
-                                     const c10::optional<at::Tensor>& weight,
-                                     const c10::optional<at::Tensor>& bias,
-                                     const std::vector<int64_t>& res_map) {
-  check_bf16_2d(A, "A");
-  check_bf16_2d(B, "B");
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-  TORCH_CHECK(B.size(1) == K && K % XBK == 0 && K >= XBK && N % 8 == 0, "gemm_xl_conv: bad shape");
-  TORCH_CHECK(M > 0 && M < (1LL << 31), "gemm_xl_conv: M out of range");
+namespace {
+
+// Shared tail of gemm_xl_conv / conv_xl: epilogue operands, launch, moments reduce.
+// `a` holds the operands and M, N, K; conv (a.cv.cin > 0) always runs the
+// 256-wide ping-pong kernel (the only main loop with the gather).
+std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::string& mode,
+                                    const c10::optional<at::Tensor>& residual,
+                                    const c10::optional<at::Tensor>& bn_x,
+                                    const c10::optional<at::Tensor>& bn_y,
+                                    const c10::optional<at::Tensor>& mean,
+                                    const c10::optional<at::Tensor>& invstd,
+                                    const c10::optional<at::Tensor>& weight,
+                                    const c10::optional<at::Tensor>& bias,
+                                    const std::vector<int64_t>& res_map) {
+  const int64_t M = a.M, N = a.N;
   int epi;
   if (mode == "moments") epi = XL_MOMENTS;
   else if (mode == "add") epi = XL_ADD;
   else if (mode == "bnbwd") epi = XL_BNBWD;
+  else if (mode == "store" && a.cv.cin > 0) epi = XL_STORE;
   else TORCH_CHECK(false, "gemm_xl_conv: unknown mode ", mode);
   auto C = at::empty({M, N}, A.options());
-  XlArgs a{};
-  a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
-  a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
   a.C = reinterpret_cast<bf16*>(C.data_ptr()); a.ldc = C.stride(0);
-  a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
   if (!res_map.empty()) {
     TORCH_CHECK(mode == "bnbwd" && res_map.size() == 5, "res_map: bnbwd only, [stride, Ho, Wo, Hi, Wi]");
@@ -870,31 +1055,101 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
       if (bias.has_value() && bias->defined()) a.bb = f32vec(bias, "bias");
     }
   }
-  const int bn = pick_bn((int)M, (int)N);
+  const bool conv = a.cv.cin > 0;
+  const int bn = conv ? 256 : pick_bn((int)M, (int)N);
   at::Tensor sums, part;
   const int mtiles = (int)((M + XBM - 1) / XBM);
-  if (epi != XL_ADD) {
+  const bool moments = epi == XL_MOMENTS || epi == XL_BNBWD;
+  if (moments) {
     part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
     sums = at::empty({2 * N + 1}, A.options().dtype(at::kDouble));
     a.part = part.data_ptr<float>();
     a.zsums = moments_zero_target(sums.data_ptr<double>(), mtiles);
   }
   hipStream_t s = at::hip::getCurrentHIPStream();
-  switch (epi) {
-    case XL_MOMENTS: dispatch_bn<XL_MOMENTS>(a, bn, s); break;
-    case XL_ADD: dispatch_bn<XL_ADD>(a, bn, s); break;
-    default: dispatch_bn<XL_BNBWD>(a, bn, s); break;
+  if (conv) {
+    const int blocks = mtiles * (int)((N + 255) / 256);
+    switch (epi) {
+      case XL_STORE: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_STORE, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+      case XL_MOMENTS: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_MOMENTS, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+      case XL_ADD: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_ADD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+      default: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_BNBWD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+    }
+  } else {
+    switch (epi) {
+      case XL_MOMENTS: dispatch_bn<XL_MOMENTS>(a, bn, s); break;
+      case XL_ADD: dispatch_bn<XL_ADD>(a, bn, s); break;
+      default: dispatch_bn<XL_BNBWD>(a, bn, s); break;
+    }
   }
   DMP_HIP_CHECK(hipGetLastError());
-  if (epi != XL_ADD) bn_reduce_partials_launch(a.part, mtiles, (int)N, sums.data_ptr<double>(), (double)M, s);
+  if (moments) bn_reduce_partials_launch(a.part, mtiles, (int)N, sums.data_ptr<double>(), (double)M, s);
   return {C, sums};
+}
+
+}  // namespace
+
+std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
+                                     const c10::optional<at::Tensor>& residual,
+                                     const c10::optional<at::Tensor>& bn_x,
+                                     const c10::optional<at::Tensor>& bn_y,
+                                     const c10::optional<at::Tensor>& mean,
+                                     const c10::optional<at::Tensor>& invstd,
+                                     const c10::optional<at::Tensor>& weight,
+                                     const c10::optional<at::Tensor>& bias,
+                                     const std::vector<int64_t>& res_map) {
+  check_bf16_2d(A, "A");
+  check_bf16_2d(B, "B");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && K % XBK == 0 && K >= XBK && N % 8 == 0, "gemm_xl_conv: bad shape");
+  TORCH_CHECK(M > 0 && M < (1LL << 31), "gemm_xl_conv: M out of range");
+  TORCH_CHECK(mode != "store", "gemm_xl_conv: use gemm_xl for a plain store");
+  XlArgs a{};
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  return xl_conv_run(a, A, mode, residual, bn_x, bn_y, mean, invstd, weight, bias, res_map);
+}
+
+// kh x kw convolution of an NHWC (channels-last) input as an implicit GEMM on
+// the ping-pong kernel: C[N*Ho*Wo, Cout] = gather(x) @ wmat^T with wmat
+// [Cout, kh*kw*Cin] (tap-major, channel-minor), padding taps read as zeros.
+// mode "store" | "moments" | "add" | "bnbwd" (epilogues as gemm_xl_conv; the
+// bnbwd / add operands are [N*Ho*Wo, Cout] row-major).  Returns (C, sums).
+std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
+                                int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
+                                const c10::optional<at::Tensor>& residual,
+                                const c10::optional<at::Tensor>& bn_x,
+                                const c10::optional<at::Tensor>& bn_y,
+                                const c10::optional<at::Tensor>& mean,
+                                const c10::optional<at::Tensor>& invstd,
+                                const c10::optional<at::Tensor>& weight,
+                                const c10::optional<at::Tensor>& bias) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4, "conv_xl: x must be 4-D bf16 GPU");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_xl: x must be channels_last");
+  check_bf16_2d(wmat, "wmat");
+  const int64_t nb = x.size(0), cin = x.size(1), hi = x.size(2), wi = x.size(3);
+  TORCH_CHECK(cin % 64 == 0, "conv_xl: Cin must be a multiple of 64");
+  TORCH_CHECK(wmat.size(1) == kh * kw * cin && wmat.size(0) % 8 == 0, "conv_xl: wmat must be [Cout, kh*kw*Cin]");
+  TORCH_CHECK(ho > 0 && wo > 0 && stride >= 1 && pad >= 0 && (ho - 1) * stride - pad + kh - 1 < hi + pad &&
+                  (wo - 1) * stride - pad + kw - 1 < wi + pad, "conv_xl: bad geometry");
+  TORCH_CHECK(nb * ho * wo < (1LL << 31) && nb * hi * wi < (1LL << 31), "conv_xl: too many pixels");
+  TORCH_CHECK(x.device() == wmat.device(), "conv_xl: device mismatch");
+  XlArgs a{};
+  a.A = reinterpret_cast<const bf16*>(x.data_ptr()); a.lda = cin;
+  a.B = reinterpret_cast<const bf16*>(wmat.data_ptr()); a.ldb = wmat.stride(0);
+  a.M = (int)(nb * ho * wo); a.N = (int)wmat.size(0); a.K = (int)(kh * kw * cin);
+  a.cv.cin = (int)cin; a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
+  a.cv.stride = (int)stride; a.cv.pad = (int)pad; a.cv.kw = (int)kw;
+  return xl_conv_run(a, x, mode, residual, bn_x, bn_y, mean, invstd, weight, bias, {});
 }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
   TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");
   g_xl_group_m = group_m;
   TORCH_CHECK(bn == 0 || bn == 128 || bn == 256, "bn must be 0 (auto), 128 or 256");
-  TORCH_CHECK(pipe >= 0 && pipe <= 6, "pipe must be 0..6 (2..5: timing-only ablations, 6: persistent)");
+  TORCH_CHECK(pipe >= 0 && pipe <= 7,
+              "pipe must be 0..7 (2..5: timing-only ablations, 6: persistent, 7: ping-pong 256x256)");
   g_xl_bn_override = bn;
   g_xl_pipe = pipe;
 }

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 from ..ops.attention import self_attention_packed
 from ..ops.fused import GradSlot, grad_tap
 from ..ops.layernorm import LayerNorm
-from ..ops.linear import Linear, linear_gelu
+from ..ops.linear import Linear, linear_gelu, linear_residual, mlp_residual
 
 
 class MLP(nn.Module):
@@ -36,6 +36,10 @@ class MLP(nn.Module):
         x = F.dropout(x, self.dropout, self.training)
         return F.dropout(self.fc2(x), self.dropout, self.training)
 
+    def forward_residual(self, x: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+        """res + forward(x) with the GELU and residual add inside the GEMM epilogues."""
+        return mlp_residual(x, res, self.fc1, self.fc2, self.dropout, self.training)
+
 
 class SelfAttention(nn.Module):
     def __init__(self, dim: int, heads: int, dropout: float = 0.0):
@@ -49,8 +53,14 @@ class SelfAttention(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         # packed-qkv attention (ops/attention.py): the fused HIP kernels read the
         # qkv GEMM output and write the proj GEMM input / the qkv gradient as is
-        o = self_attention_packed(self.qkv(x), self.heads, self.dropout if self.training else 0.0)
-        return self.proj(o)
+        return self.proj(self._core(x))
+
+    def _core(self, x: torch.Tensor) -> torch.Tensor:
+        return self_attention_packed(self.qkv(x), self.heads, self.dropout if self.training else 0.0)
+
+    def forward_residual(self, x: torch.Tensor, res: torch.Tensor) -> torch.Tensor:
+        """res + forward(x): bias and residual added in the proj GEMM's store."""
+        return linear_residual(self._core(x), res, self.proj.weight, self.proj.bias)
 
 
 class EncoderBlock(nn.Module):
@@ -68,10 +78,10 @@ class EncoderBlock(nn.Module):
         train = self.training and torch.is_grad_enabled()
         s1 = GradSlot() if train else None
         h = self.ln1(x, s1)
-        x = grad_tap(x, s1) + self.attn(h)
+        x = self.attn.forward_residual(h, grad_tap(x, s1))
         s2 = GradSlot() if train else None
         h = self.ln2(x, s2)
-        return grad_tap(x, s2) + self.mlp(h)
+        return self.mlp.forward_residual(h, grad_tap(x, s2))
 
 
 class VisionTransformer(nn.Module):

@@ -43,6 +43,26 @@ NATIVE_BWD = _BWD_MODE == "1"
 # batch 1024 on MI355X; everything else goes to MIOpen in "auto" mode.
 _OURS_FASTER = set()
 
+# 256x256 ping-pong implicit GEMM (csrc/gemm/gemm_xl.hip conv_xl), used where
+# its 256-wide output tile is full: forward (with the BN moments) when
+# Cout >= 256, stride-1 data gradient (a forward conv over flipped weights,
+# optionally fused with the producer BN's backward reductions) when
+# Cin >= 256.  ResNet-50 layers 3-4: forward 0.30-0.33 ms vs 0.46-0.49 (conv_nt)
+# and dgrad 0.30-0.31 vs MIOpen 0.38-0.41 (profiles/conv3x3_xl_r2.md).
+# DMP_XL_CONV3=0 disables it.
+_XL3 = os.environ.get("DMP_XL_CONV3", "1") != "0"
+_STATS["xl_fwd"] = 0
+_STATS["xl_dgrad"] = 0
+_STATS["xl_bnbwd"] = 0
+
+
+def _xl_fwd(cout: int, kh: int, kw: int) -> bool:
+    return _XL3 and cout >= 256 and kh == kw and kh > 1
+
+
+def _xl_dgrad(cin: int, kh: int, kw: int, stride: int) -> bool:
+    return _XL3 and cin >= 256 and stride == 1 and kh == kw and kh > 1
+
 
 def _use_native(pass_: str, cin: int, h: int, stride: int) -> bool:
     if NATIVE_BWD:
@@ -71,15 +91,26 @@ def _wmat(w: torch.Tensor) -> torch.Tensor:
 
 class _ConvIGFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, stride, pad, moments):
+    def forward(ctx, x, weight, stride, pad, moments, bn_slot=None):
         C = _native.require("conv_igemm")
         n, cin, h, w = x.shape
         cout, _, kh, kw = weight.shape
         ho, wo = _out_size(h, kh, stride, pad), _out_size(w, kw, stride, pad)
-        y2, mom = C.conv_nt(x, _wmat(weight), kh, kw, stride, pad, ho, wo,
-                            mode="moments" if moments else "store")
+        mode = "moments" if moments else "store"
+        if _xl_fwd(cout, kh, kw):
+            _STATS["xl_fwd"] += 1
+            y2, mom = C.conv_xl(x, _wmat(weight), kh, kw, stride, pad, ho, wo, mode)
+            if not moments:
+                mom = None
+        else:
+            y2, mom = C.conv_nt(x, _wmat(weight), kh, kw, stride, pad, ho, wo, mode=mode)
         ctx.save_for_backward(x, weight)
         ctx.geo = (stride, pad, ho, wo)
+        # x is a training-mode BN+ReLU output and our dgrad runs on conv_xl: its
+        # epilogue can also do that BN's backward reductions (BnBwdSlot)
+        ctx.bn_slot = bn_slot if (bn_slot is not None and _xl_dgrad(cin, kh, kw, stride)) else None
+        if ctx.bn_slot is not None:
+            bn_slot.consumers += 1
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
@@ -91,7 +122,7 @@ class _ConvIGFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dmom):
         if dy is None:
-            return (None,) * 5
+            return (None,) * 6
         x, weight = ctx.saved_tensors
         C = _native.require("conv_igemm backward")
         stride, pad, ho, wo = ctx.geo
@@ -99,14 +130,31 @@ class _ConvIGFn(torch.autograd.Function):
         cout, _, kh, kw = weight.shape
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx = dw = None
-        nat_d = ctx.needs_input_grad[0] and _use_native("dgrad", cin, h, stride)
+        bs, ctx.bn_slot = ctx.bn_slot, None
+        if ctx.needs_input_grad[0] and _xl_dgrad(cin, kh, kw, stride):
+            # dx = conv(dy, flip(W)^T, pad k-1-p) on the ping-pong implicit GEMM
+            wfl = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+            _STATS["xl_dgrad"] += 1
+            if bs is not None and bs.consumers == 1 and bs.x2 is not None:
+                _STATS["xl_bnbwd"] += 1
+                inv, bw, bb = (bs.invstd, bs.w32, bs.b32) if bs.y2 is None else (None, None, None)
+                dx2, sums = C.conv_xl(dy, wfl, kh, kw, 1, kh - 1 - pad, h, w, "bnbwd", bn_x=bs.x2, bn_y=bs.y2,
+                                      mean=bs.mean, invstd=inv, weight=bw, bias=bb)
+                dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+                bs.park(dx, sums[: 2 * cin])
+            else:
+                dx2, _ = C.conv_xl(dy, wfl, kh, kw, 1, kh - 1 - pad, h, w, "store")
+                dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        nat_d = ctx.needs_input_grad[0] and dx is None and _use_native("dgrad", cin, h, stride)
         nat_w = ctx.needs_input_grad[1] and _use_native("wgrad", cin, h, stride)
-        want_d = ctx.needs_input_grad[0] and not nat_d
+        want_d = ctx.needs_input_grad[0] and not nat_d and dx is None
         want_w = ctx.needs_input_grad[1] and not nat_w
         if want_d or want_w:
-            dx, dw, _ = torch.ops.aten.convolution_backward(
+            dx_l, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                 [want_d, want_w, False])
+            if want_d:
+                dx = dx_l
         if nat_d:
             wt = weight.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()  # [Cin][kh][kw][Cout]
             dx2, _ = C.conv_nt(dy, wt, kh, kw, stride, pad, h, w, transposed=True)
@@ -117,7 +165,7 @@ class _ConvIGFn(torch.autograd.Function):
             dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
             if not weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous()
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0,
@@ -126,7 +174,8 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
     """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
     if _native_ok(x, weight, groups, dilation):
         _STATS["native"] += 1
-        y, mom = _ConvIGFn.apply(x, weight, stride, padding, moments)
+        bn_slot = getattr(x, "_dmp_bnbwd", None) if torch.is_grad_enabled() else None
+        y, mom = _ConvIGFn.apply(x, weight, stride, padding, moments, bn_slot)
         return y, (mom if moments else None)
     _STATS["torch"] += 1
     return F.conv2d(x, weight, None, stride, padding, dilation, groups), None

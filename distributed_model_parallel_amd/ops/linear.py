@@ -9,10 +9,20 @@
 * ``linear_gelu``: fc1 + exact GELU; the backward fuses gelu'(h) with fc1's
   bias gradient in one pass over the pre-activation.
 
+* ``mlp_residual`` / ``linear_residual``: the ViT block's MLP and attention
+  output projection with the residual add, on our 256x256 ping-pong MFMA GEMM
+  (``csrc/gemm/gemm_xl.hip``, PIPE 7) and its fused epilogues: fc1 writes the
+  pre-activation and GELU(h) in one pass (no GELU kernel), fc2 / proj add bias
+  and residual in the store (no add kernel), and fc2's data gradient applies
+  gelu'(h) in its epilogue (no GELU-backward pass).  Weight gradients stay on
+  hipBLASLt (split-M shapes our tile grid cannot fill).  ``DMP_VIT_XL=0``
+  restores the library path for A/B runs.
+
 CPU tensors, non-bf16 dtypes and widths that are not a multiple of 256 use
 the plain PyTorch ops (same math)."""
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -21,7 +31,9 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0}
+_STATS = {"native": 0, "torch": 0, "xl": 0}
+_XL = os.environ.get("DMP_VIT_XL", "1") != "0"
+_XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> bool:
@@ -98,3 +110,95 @@ class Linear(nn.Linear):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return linear(x, self.weight, self.bias)
+
+
+# --------------------------------------------------------------------------- #
+# Fused-epilogue paths on the ping-pong GEMM (ViT encoder block)
+# --------------------------------------------------------------------------- #
+def _xl_ok(x: torch.Tensor, *ws: torch.Tensor) -> bool:
+    if not (_XL and _native.gpu_path(x)) or x.dtype != torch.bfloat16:
+        return False
+    C = _native.native()
+    rows = x.numel() // x.shape[-1]
+    return (rows >= _XL_MIN_ROWS and all(w.dtype == torch.bfloat16 and w.shape[1] % 64 == 0 and
+                                         w.shape[0] % 64 == 0 and C.colsum_supported(w.shape[0]) for w in ws))
+
+
+def _rows(t: torch.Tensor) -> torch.Tensor:
+    t2 = t.reshape(-1, t.shape[-1])
+    return t2 if t2.stride(-1) == 1 and t2.stride(0) % 8 == 0 else t2.contiguous()
+
+
+class _LinearResidualFn(torch.autograd.Function):
+    """y = res + (x @ W^T + b): bias and residual added in the GEMM's store."""
+
+    @staticmethod
+    def forward(ctx, x, res, w, b):
+        C = _native.require("linear_residual")
+        x2, r2 = _rows(x), _rows(res)
+        y = C.gemm_xl(x2, w, "bias_res", bias=b, residual=r2)
+        ctx.save_for_backward(x2, w)
+        ctx.xshape = x.shape
+        return y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        C = _native.require("linear_residual backward")
+        dy2 = _rows(dy)
+        dx = dy2.mm(w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dw = dy2.t().mm(x2) if ctx.needs_input_grad[2] else None
+        db = C.bias_grad(dy2, w.dtype) if ctx.needs_input_grad[3] else None
+        return dx, dy, dw, db
+
+
+class _MLPResidualFn(torch.autograd.Function):
+    """y = res + fc2(gelu(fc1(x))) on three fused-epilogue GEMMs:
+    fc1 -> (h, gelu(h)); fc2 -> bias + residual; fc2 dgrad -> * gelu'(h)."""
+
+    @staticmethod
+    def forward(ctx, x, res, w1, b1, w2, b2):
+        C = _native.require("mlp_residual")
+        x2, r2 = _rows(x), _rows(res)
+        h = torch.empty(x2.shape[0], w1.shape[0], dtype=x2.dtype, device=x2.device)
+        a = C.gemm_xl(x2, w1, "bias_gelu", bias=b1, aux=h)
+        y = C.gemm_xl(a, w2, "bias_res", bias=b2, residual=r2)
+        ctx.save_for_backward(x2, w1, h, a, w2)
+        ctx.xshape = x.shape
+        return y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, h, a, w2 = ctx.saved_tensors
+        C = _native.require("mlp_residual backward")
+        dy2 = _rows(dy)
+        db2 = C.bias_grad(dy2, w2.dtype)
+        dw2 = dy2.t().mm(a)
+        # dh = bf16(bf16(dy @ W2) * gelu'(h)): B operand is W2^T [hidden, dim]
+        dh = C.gemm_xl(dy2, w2.t().contiguous(), "dgelu", aux=h)
+        db1 = C.bias_grad(dh, w1.dtype)
+        dw1 = dh.t().mm(x2)
+        dx = dh.mm(w1)
+        return dx.view(ctx.xshape), dy, dw1, db1, dw2, db2
+
+
+def linear_residual(x: torch.Tensor, res: torch.Tensor, weight: torch.Tensor,
+                    bias: torch.Tensor) -> torch.Tensor:
+    """res + linear(x): one GEMM with the bias and residual in its epilogue."""
+    if (bias is not None and bias.dtype == torch.bfloat16 and _xl_ok(x, weight)
+            and res.dtype == torch.bfloat16 and res.shape[:-1] == x.shape[:-1]):
+        _STATS["xl"] += 1
+        return _LinearResidualFn.apply(x, res, weight, bias)
+    return res + linear(x, weight, bias)
+
+
+def mlp_residual(x: torch.Tensor, res: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear,
+                 dropout: float = 0.0, training: bool = False) -> torch.Tensor:
+    """res + fc2(gelu(fc1(x))) (exact erf GELU, as ``nn.GELU()``)."""
+    if ((dropout == 0.0 or not training) and fc1.bias is not None and fc2.bias is not None
+            and fc1.bias.dtype == torch.bfloat16 and fc2.bias.dtype == torch.bfloat16
+            and _xl_ok(x, fc1.weight, fc2.weight) and res.dtype == torch.bfloat16):
+        _STATS["xl"] += 1
+        return _MLPResidualFn.apply(x, res, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+    hdn = F.dropout(linear_gelu(x, fc1.weight, fc1.bias), dropout, training)
+    return res + F.dropout(linear(hdn, fc2.weight, fc2.bias), dropout, training)

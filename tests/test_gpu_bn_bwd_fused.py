@@ -134,3 +134,40 @@ def test_bnbwd_compact_strided_residual(xl):
         b = C.gemm_nt_bnbwd(dy, wt, full, x, None, mean, inv, None, bb)
     torch.testing.assert_close(a[0], b[0])
     torch.testing.assert_close(a[1], b[1], atol=1e-6, rtol=1e-9)
+
+
+def test_bottleneck_3x3_on_conv_xl_with_fused_bn1_backward():
+    """Layer-3-width block: conv2 (3x3, 256 -> 256) forward and data gradient on
+    conv_xl, its dgrad epilogue doing bn1's backward reductions -- vs conv_nt /
+    MIOpen with the unfused BN backward."""
+    from distributed_model_parallel_amd.models.resnet import Bottleneck
+    from distributed_model_parallel_amd.ops import conv_igemm
+    torch.manual_seed(4)
+    blk = Bottleneck(1024, 256, 1)
+    net = cast_model(blk.to(DEV).to(memory_format=torch.channels_last))
+    with torch.no_grad():
+        net.bn1.weight.normal_(1.0, 0.1)
+        net.bn1.bias.normal_(0.0, 0.1)
+    net.train()
+    x = torch.randn(4, 1024, 8, 8, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    gg = torch.randn(4, 1024, 8, 8, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    old = (bnops._FUSE_BWD, conv_igemm._XL3)
+    try:
+        bnops._FUSE_BWD, conv_igemm._XL3 = False, False
+        ya, ga, pa = _run(copy.deepcopy(net), x, gg)
+        bnops._FUSE_BWD, conv_igemm._XL3 = True, True
+        s0 = dict(conv_igemm._STATS)
+        n0 = bnops._STATS["fused_bwd_moments"]
+        yb, gb, pb = _run(copy.deepcopy(net), x, gg)
+        fused = bnops._STATS["fused_bwd_moments"] - n0
+    finally:
+        bnops._FUSE_BWD, conv_igemm._XL3 = old
+    assert conv_igemm._STATS["xl_fwd"] > s0["xl_fwd"] and conv_igemm._STATS["xl_dgrad"] > s0["xl_dgrad"]
+    assert conv_igemm._STATS["xl_bnbwd"] == s0["xl_bnbwd"] + 1
+    assert fused >= 2, fused  # bn1 (via conv2 = conv_xl) and bn2 (via conv3)
+    torch.testing.assert_close(yb, ya, atol=0.1, rtol=5e-2)
+    cos = F.cosine_similarity(gb.flatten(), ga.flatten(), dim=0).item()
+    assert cos > 0.995, cos
+    for n in pa:
+        c = F.cosine_similarity(pb[n].flatten(), pa[n].flatten(), dim=0).item()
+        assert c > 0.99, (n, c)

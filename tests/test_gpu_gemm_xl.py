@@ -20,8 +20,9 @@ def _tol(K):
     return dict(atol=0.03 * K ** 0.5, rtol=2e-2)
 
 
-@pytest.fixture(params=[(0, 1), (128, 1), (256, 1), (128, 0), (256, 0), (128, 6), (256, 6)],
-                ids=["auto", "bn128", "bn256", "bn128-pipe0", "bn256-pipe0", "bn128-persist", "bn256-persist"])
+@pytest.fixture(params=[(0, 1), (128, 1), (256, 1), (128, 0), (256, 0), (128, 6), (256, 6), (256, 7)],
+                ids=["auto", "bn128", "bn256", "bn128-pipe0", "bn256-pipe0", "bn128-persist", "bn256-persist",
+                     "bn256-pingpong"])
 def bn(request):
     C().set_gemm_xl_bn(*request.param)
     yield request.param

@@ -61,3 +61,26 @@ def test_xl_bnbwd_matches_nt(mask_from_y, with_res):
     dzd = dz.double()
     torch.testing.assert_close(sums[:N], dzd.sum(0), atol=1e-2, rtol=1e-4)
     torch.testing.assert_close(sums[N:2 * N], (dzd * (x.double() - mean.double())).sum(0), atol=1e-2, rtol=1e-4)
+
+
+@pytest.mark.parametrize("mode", ["moments", "bnbwd"])
+def test_xl_conv_pingpong_schedule(mode):
+    """The 256 x 256 ping-pong main loop (PIPE 7) under the conv epilogues equals the ring kernel."""
+    C = _native.require("gemm_xl_conv")
+    torch.manual_seed(11)
+    M, N, K = 5000, 512, 576
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    kw = {}
+    if mode == "bnbwd":
+        x = torch.randn(M, N, device=DEV).bfloat16()
+        kw = dict(bn_x=x, mean=torch.zeros(N, device=DEV), invstd=torch.ones(N, device=DEV))
+    C.set_gemm_xl_bn(256, 1)
+    try:
+        ref, rs = C.gemm_xl_conv(a, b, mode, **kw)
+        C.set_gemm_xl_bn(256, 7)
+        got, gs = C.gemm_xl_conv(a, b, mode, **kw)
+    finally:
+        C.set_gemm_xl_bn(0)
+    torch.testing.assert_close(got.float(), ref.float(), atol=0.02, rtol=1e-2)
+    torch.testing.assert_close(gs, rs, atol=1e-2 * M ** 0.5, rtol=1e-3)

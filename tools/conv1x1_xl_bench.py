@@ -35,8 +35,9 @@ def main():
              ("l4.conv1", B * 49, 2048, 512), ("l4.conv3", B * 49, 512, 2048),
              ("l2.b0.conv1", B * 3136, 256, 128), ("l3.b0.conv1", B * 784, 512, 256),
              ("l4.b0.conv1", B * 196, 1024, 512)]
-    print("| conv | M | Cin | Cout | fwd+mom nt | fwd+mom xl | dgrad bnbwd nt | dgrad bnbwd xl |")
-    print("|---|---|---|---|---|---|---|---|")
+    print("| conv | M | Cin | Cout | fwd+mom nt | fwd+mom xl ring | fwd+mom xl pp | dgrad bnbwd nt | "
+          "dgrad bnbwd xl ring | dgrad bnbwd xl pp |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for name, M, cin, cout in convs:
         x = torch.randn(M, cin, device="cuda").bfloat16()
         w = (torch.randn(cout, cin, device="cuda") * 0.05).bfloat16()
@@ -45,11 +46,17 @@ def main():
         mean = torch.zeros(cin, device="cuda")
         inv = torch.ones(cin, device="cuda")
         f_nt = timeit(lambda: C.gemm_nt(x, w, mode="moments"))
-        f_xl = timeit(lambda: C.gemm_xl_conv(x, w, "moments")) if cout % 8 == 0 and cin % 64 == 0 else float("nan")
         d_nt = timeit(lambda: C.gemm_nt_bnbwd(dy, wt, None, x, None, mean, inv, None, None))
-        d_xl = timeit(lambda: C.gemm_xl_conv(dy, wt, "bnbwd", bn_x=x, mean=mean, invstd=inv)) \
-            if cout % 64 == 0 else float("nan")
-        print(f"| {name} | {M} | {cin} | {cout} | {f_nt:.3f} | {f_xl:.3f} | {d_nt:.3f} | {d_xl:.3f} |", flush=True)
+        res = {}
+        for pipe in (1, 7):  # ring vs ping-pong main loop (auto tile width)
+            C.set_gemm_xl_bn(0, pipe)
+            res[pipe] = (
+                timeit(lambda: C.gemm_xl_conv(x, w, "moments")) if cout % 8 == 0 and cin % 64 == 0 else float("nan"),
+                timeit(lambda: C.gemm_xl_conv(dy, wt, "bnbwd", bn_x=x, mean=mean, invstd=inv))
+                if cout % 64 == 0 else float("nan"))
+        C.set_gemm_xl_bn(0)
+        print(f"| {name} | {M} | {cin} | {cout} | {f_nt:.3f} | {res[1][0]:.3f} | {res[7][0]:.3f} | {d_nt:.3f} | "
+              f"{res[1][1]:.3f} | {res[7][1]:.3f} |", flush=True)
         del x, w, dy, wt
         torch.cuda.empty_cache()
 

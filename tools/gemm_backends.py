@@ -6,7 +6,7 @@ our 4-wave NT kernel (csrc/conv/gemm_bf16.hip ``gemm_nt``), the 8-wave
 ViT-B/16 linears at batch 256 (197 tokens) and the ResNet-50 implicit-GEMM
 shapes at batch 1024 taken as plain GEMMs.  Markdown table on stdout.
 
-usage: python tools/gemm_backends.py
+usage: python tools/gemm_backends.py [comma-separated shape-name prefixes]
 """
 from __future__ import annotations
 
@@ -46,18 +46,31 @@ SHAPES = [
 def main():
     C = _native.require("gemm backends")
     dev, dt = "cuda", torch.bfloat16
-    print("| shape | M | N | K | gemm_nt ms | gemm_xl ms | hipBLASLt ms | best TF/s | xl / blaslt |")
-    print("|---|---|---|---|---|---|---|---|---|")
+    only = sys.argv[1].split(",") if len(sys.argv) > 1 else None
+    print("| shape | M | N | K | gemm_nt ms | gemm_xl ms | xl ping-pong ms | hipBLASLt ms | best TF/s | pp / blaslt |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for name, M, N, K in SHAPES:
+        if only and not any(name.startswith(o) for o in only):
+            continue
         a = torch.rand(M, K, device=dev, dtype=dt) * 2 - 1
         b = torch.rand(N, K, device=dev, dtype=dt) * 2 - 1
         t_nt = timeit(lambda: C.gemm_nt(a, b))
         t_xl = timeit(lambda: C.gemm_xl(a, b)) if (K % 64 == 0 and N % 8 == 0) else float("nan")
+        t_pp = float("nan")
+        if K % 64 == 0 and N % 8 == 0:
+            C.set_gemm_xl_bn(256, 7)  # 256 x 256 ping-pong schedule (PIPE 7)
+            try:
+                t_pp = timeit(lambda: C.gemm_xl(a, b))
+                err = (C.gemm_xl(a, b).float() - (a.float() @ b.float().t())).abs().max().item() if M * N <= 1 << 26 else 0.0
+            finally:
+                C.set_gemm_xl_bn(0)
+            if err > 0.05 * K ** 0.5:
+                print(f"  !! ping-pong max error {err:.3f}", flush=True)
         t_bl = timeit(lambda: a @ b.t())
         fl = 2.0 * M * N * K
-        best = min(t for t in (t_nt, t_xl, t_bl) if t == t)
-        print(f"| {name} | {M} | {N} | {K} | {t_nt:.3f} | {t_xl:.3f} | {t_bl:.3f} | {fl / best / 1e9:.0f} | "
-              f"{t_xl / t_bl:.2f} |", flush=True)
+        best = min(t for t in (t_nt, t_xl, t_pp, t_bl) if t == t)
+        print(f"| {name} | {M} | {N} | {K} | {t_nt:.3f} | {t_xl:.3f} | {t_pp:.3f} | {t_bl:.3f} | {fl / best / 1e9:.0f} | "
+              f"{t_pp / t_bl:.2f} |", flush=True)
         del a, b
         torch.cuda.empty_cache()
 
