@@ -15,8 +15,11 @@
   pre-activation and GELU(h) in one pass (no GELU kernel), fc2 / proj add bias
   and residual in the store (no add kernel), and fc2's data gradient applies
   gelu'(h) in its epilogue (no GELU-backward pass).  Weight gradients stay on
-  hipBLASLt (split-M shapes our tile grid cannot fill).  ``DMP_VIT_XL=0``
-  restores the library path for A/B runs.
+  hipBLASLt (split-M shapes our tile grid cannot fill).  Off by default
+  (``DMP_VIT_XL=1`` enables it): measured at batch 256 the fused path is
+  1.6 % slower per step than hipBLASLt + the separate GELU / add passes --
+  fc1+GELU and fc2-dgrad+GELU' break even, fc2 / proj + residual lose
+  (profiles/vit_xl_epilogues_r2.md).
 
 CPU tensors, non-bf16 dtypes and widths that are not a multiple of 256 use
 the plain PyTorch ops (same math)."""
@@ -32,7 +35,7 @@ import torch.nn.functional as F
 from .. import _native
 
 _STATS = {"native": 0, "torch": 0, "xl": 0}
-_XL = os.environ.get("DMP_VIT_XL", "1") != "0"
+_XL = os.environ.get("DMP_VIT_XL", "0") == "1"
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 
 

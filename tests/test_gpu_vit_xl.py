@@ -12,6 +12,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.fixture(autouse=True)
+def _xl_on(monkeypatch):
+    monkeypatch.setattr(L, "_XL", True)
+
+
 def _ref_mlp(x, res, w1, b1, w2, b2):
     return res + F.linear(F.gelu(F.linear(x, w1, b1)), w2, b2)
 
