@@ -538,11 +538,14 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     }
   }
   if (col < N) {
-#pragma unroll 4
+    // 8 row groups per unrolled batch, predicated rather than exited: the
+    // epilogue operand loads (BN input / residual / aux) of a batch are all in
+    // flight together -- with 1 block/CU the epilogue is memory-latency bound
+#pragma unroll 8
     for (int pr = 0; pr < XBM / RPP; ++pr) {
       const int lr = rr0 + pr * RPP;
       const int row = m0 + lr;
-      if (row >= M) break;
+      if (row >= M) continue;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
       if constexpr (EPI == XL_MOMENTS) {
         const f32x8 f = __builtin_convertvector(v, f32x8);
