@@ -104,6 +104,10 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
                                 const c10::optional<at::Tensor>& bn_y, const c10::optional<at::Tensor>& mean,
                                 const c10::optional<at::Tensor>& invstd, const c10::optional<at::Tensor>& weight,
                                 const c10::optional<at::Tensor>& bias);
+at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
+void set_tn_xl_rounds(int r);
+at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
+                         int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
 std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
                                      const c10::optional<at::Tensor>& residual,
                                      const c10::optional<at::Tensor>& bn_x,
@@ -228,6 +232,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(),
         "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues");
+  m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
+  m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
+        "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M");
+  m.def("conv_wgrad_xl", &dmp::conv_wgrad_xl, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
+        py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
+        "kh x kw conv weight gradient (tap gather) on the ping-pong TN kernel; Cin % 256 == 0");
   m.def("gemm_xl_conv", &dmp::gemm_xl_conv, py::arg("A"), py::arg("B"), py::arg("mode"),
         py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),

@@ -531,9 +531,15 @@ constexpr int TN_BM = 64;  // m rows per LDS stage (two MFMA k-steps)
 __device__ __forceinline__ int tn_off(int row, int col, int row_bytes) {
   // byte offset of element (row, col) [bf16] with the 32-B-chunk swizzle; the
   // XOR stays inside the row (row_bytes / 32 chunks: 8 for 256-B, 4 for 128-B rows)
+  // ds_read_b64_tr_b16 banks per 32-lane half: lanes l and l+16 read rows r
+  // and r+8, which must land on different banks (MI355X_MICROARCH.md §LDS).
+  // 256-/512-B rows: the +4*(row>>3) term moves rows 8-15 to the other half of
+  // the chunk range; 128-B rows (4 chunks, rows q and q+2 already share a bank
+  // half) need an XOR with bit 3 of the row instead.
   const int byte = col * 2;
   const int mask = (row_bytes >> 5) - 1;
-  const int chunk = (byte >> 5) ^ ((row + 4 * (row >> 3)) & mask);
+  const int f = mask == 3 ? ((row & 3) ^ ((row >> 3) & 1)) : ((row + 4 * (row >> 3)) & mask);
+  const int chunk = (byte >> 5) ^ f;
   return row * row_bytes + (chunk << 5) + (byte & 31);
 }
 
@@ -783,6 +789,8 @@ void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, fl
 
 }  // namespace
 
+void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream);
+
 namespace {
 
 // C[N, K] = sum_m A[m, :]^T Bmapped[m, :]  -> out [N, K] (bf16 or fp32)
@@ -817,20 +825,24 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
-  const int64_t n = (int64_t)N * K;
+  split_reduce_launch(pp, splits, (int64_t)N * K, out, stream);
+  return out;
+}
+
+}  // namespace
+
+// out[c] = sum over splits of part[s][c] (c < n, n % 4 == 0), bf16 or fp32 out.
+void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream) {
   int sl = 1;  // split lanes per column: grow until >= 512 blocks or lanes cover the splits
   while (sl < 64 && sl < splits && (n / 4 + 256 / sl - 1) / (256 / sl) < 512) sl *= 2;
   const unsigned blocks = (unsigned)((n / 4 + 256 / sl - 1) / (256 / sl));
-  if (out_dtype == at::kBFloat16)
+  if (out.scalar_type() == at::kBFloat16)
     hipLaunchKernelGGL((split_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
                        sl, reinterpret_cast<bf16*>(out.data_ptr()));
   else
     hipLaunchKernelGGL((split_reduce_kernel<float>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
                        sl, out.data_ptr<float>());
-  return out;
 }
-
-}  // namespace
 
 // Weight gradient of a 1x1 conv: C[N, K] = A^T B with A [M, N], B [M, K] (bf16,
 // row-major).  Output dtype bf16 or fp32.  b_map ([s, Ho, Wo, Hi, Wi]) reads

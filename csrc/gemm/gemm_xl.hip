@@ -836,6 +836,209 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_persistent_kernel(const X
   epilogue(cur_tile);
 }
 
+// ---------------------------------------------------------------------------
+// Weight-gradient GEMM on the ping-pong schedule:
+//   part[split][n][k] = sum_{m in split} A[m, n] * B[m, k]
+// (A = dy [M, N], B = x [M, K] or the implicit-GEMM tap gather of an NHWC
+// input).  The reduction runs over the huge M = batch*H*W, split across
+// blocks; a column reduce sums the fp32 partials.  256 (n) x 256 (k) output
+// tile, 8 waves as 2 x 4 (128 x 64 each), 64 m per K tile.  MFMA operands
+// need 8 consecutive m per lane: the LDS holds m-major tiles and fragments
+// come from ds_read_b64_tr_b16 (transposing read).  Each operand tile of a
+// stage is 8 planes of [64 m][32 cols] (64-B rows, 32-B chunk XOR row & 1),
+// so every 16 KB staging unit is 4 whole planes: U0 / U3 = the n columns of
+// the waves' m-halves 0 / 1, U1 / U2 = the k columns of their n-halves 0 / 1,
+// with the same phase order, unit schedule and vmcnt counts as PIPE 7 of
+// gemm_xl_nt_kernel.  LDS-DMA writes lane-linearly, so each lane fetches the
+// logical 16 B that its physical slot holds under the swizzle.
+// ---------------------------------------------------------------------------
+struct TnPPArgs {
+  const bf16* A; int64_t lda;
+  const bf16* B; int64_t ldb;
+  int M, N, K;
+  int64_t rps;   // rows per split, a multiple of 64
+  float* part;   // [splits][N][K]
+  XlConv cv;     // cin > 0: B row m of a K tile = input pixel of its tap (K tile inside one tap)
+};
+
+// 32-B chunk XOR: row & 1 separates rows q, q+1 (one 256-B bank row holds 4
+// rows); bit 3 separates rows r and r+8, which lanes l and l+16 of one
+// ds_read_b64_tr_b16 half-wave read (they would otherwise share banks: 2x).
+__device__ __forceinline__ int tn64_swz(int row) { return (row ^ (row >> 3)) & 1; }
+__device__ __forceinline__ int tn64_off(int row, int col) {
+  const int byte = col * 2;
+  return row * 64 + ((((byte >> 5) ^ tn64_swz(row))) << 5) + (byte & 31);
+}
+
+__global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs p) {
+  constexpr int PLANE = 64 * 64, OPER = 8 * PLANE;  // bytes
+  __shared__ __attribute__((aligned(16))) char smem[4 * OPER];
+  using v4i16 = short __attribute__((ext_vector_type(4)));
+  using lds_v4 = __attribute__((address_space(3))) v4i16;
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int ntiles = (N + 255) >> 8, ktiles = (K + 255) >> 8;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % (ntiles * ktiles), split = bid / (ntiles * ktiles);
+  const int n0 = (tile / ktiles) * 256, k0 = (tile % ktiles) * 256;
+  const int64_t mb = (int64_t)split * p.rps;
+  const int64_t me = min((int64_t)M, mb + p.rps);
+  const int KT = (int)((me - mb + 63) >> 6);
+  const XlConv cv = p.cv;
+  const bool gather = cv.cin > 0;
+  int tr = 0, tc = 0, kc0 = k0;
+  if (gather) {
+    const int tap = k0 / cv.cin;
+    tr = tap / cv.kw;
+    tc = tap - tr * cv.kw;
+    kc0 = k0 - tap * cv.cin;
+  }
+  auto a_plane = [&](int buf, int pl) { return smem + buf * 2 * OPER + pl * PLANE; };
+  auto b_plane = [&](int buf, int pl) { return smem + buf * 2 * OPER + OPER + pl * PLANE; };
+
+  // staging roles: wave w writes blocks b = 2 (w & 1) + q (q = 0, 1) of the
+  // unit's plane pi = w >> 1; lane -> physical row, 16-B slot
+  const int pi = wave >> 1;
+  int srow[2], scol[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int b = 2 * (wave & 1) + q;
+    srow[q] = 16 * b + (lane >> 2);
+    const int slot = lane & 3;
+    scol[q] = ((((slot >> 1) ^ tn64_swz(srow[q]))) << 4) + (slot & 1) * 8;
+  }
+  auto stage_unit = [&](auto u, int kt) {
+    constexpr int U = decltype(u)::value;
+    const int buf = kt & 1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t m = mb + (int64_t)kt * 64 + srow[q];
+      char* dst;
+      const bf16* src = g_zero_row;
+      if constexpr (U == 0 || U == 3) {
+        const int pl = (U == 0 ? 0 : 2) + (pi & 1) + (pi >> 1) * 4;  // {0,1,4,5} / {2,3,6,7}
+        const int col = n0 + pl * 32 + scol[q];
+        dst = a_plane(buf, pl) + ((2 * (wave & 1) + q) << 10);
+        if (m < me && col < N) src = p.A + m * p.lda + col;
+      } else {
+        const int pl = 2 * pi + (U == 2 ? 1 : 0);                     // {0,2,4,6} / {1,3,5,7}
+        const int col = pl * 32 + scol[q];
+        dst = b_plane(buf, pl) + ((2 * (wave & 1) + q) << 10);
+        if (m < me && k0 + col < K) {
+          if (!gather) {
+            src = p.B + m * p.ldb + k0 + col;
+          } else {
+            const int hw = cv.ho * cv.wo;
+            const int mi = (int)m, n = mi / hw, r = mi - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+            const int ih = oh * cv.stride - cv.pad + tr, iw = ow * cv.stride - cv.pad + tc;
+            if ((unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi)
+              src = p.B + ((int64_t)(n * cv.hi + ih) * cv.wi + iw) * p.ldb + kc0 + col;
+          }
+        }
+      }
+      glds16(src, dst);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // tr-read lane roles (as gemm_tn_kernel): group g = lane >> 4 covers m rows
+  // 8g..8g+7 of a k32 step; lane 4q+p of the group reads row q, cols 4p..4p+3
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  bf16x8 qa[2][4], qb[2][2];
+  auto tr_frag = [&](const char* plane, int ks, int col_in) {
+    const int rb = ks * 32 + 8 * g + q4;
+    v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(plane + tn64_off(rb, col_in)));
+    v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(plane + tn64_off(rb + 4, col_in)));
+    short __attribute__((ext_vector_type(8))) t8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, t8);
+  };
+  auto read_a = [&](int mq, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        qa[ks][i] = tr_frag(a_plane(buf, wr * 4 + mq * 2 + (i >> 1)), ks, (i & 1) * 16 + 4 * p4);
+  };
+  auto read_b = [&](int nq, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) qb[ks][j] = tr_frag(b_plane(buf, wc * 2 + nq), ks, j * 16 + 4 * p4);
+  };
+  auto quad = [&](auto mqc, auto nqc) {
+    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[MQ * 4 + i][NQ * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  if (KT > 0) {
+    stage_unit(I0{}, 0);
+    stage_unit(I2{}, 0);
+    stage_unit(I3{}, 0);
+    stage_unit(I1{}, 0);
+    if (KT > 1) {
+      stage_unit(I0{}, 1);
+      stage_unit(I2{}, 1);
+      vmcnt<4>();
+    } else {
+      vmcnt<0>();
+    }
+    barrier();
+    if (wr == 1) barrier();
+    for (int kt = 0; kt < KT; ++kt) {
+      const int buf = kt & 1;
+      const bool n1 = kt + 1 < KT, n2 = kt + 2 < KT;
+      read_a(0, buf);
+      read_b(0, buf);
+      if (n1) { stage_unit(I3{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
+      quad(I0{}, I0{});
+      read_b(1, buf);
+      if (n1) { stage_unit(I1{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
+      quad(I0{}, I1{});
+      read_a(1, buf);
+      if (n2) { stage_unit(I0{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
+      quad(I1{}, I1{});
+      read_b(0, buf);
+      if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
+      quad(I1{}, I0{});
+    }
+    if (wr == 0) barrier();
+  }
+  float* out = p.part + (int64_t)split * N * K;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wc * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wr * 128 + i * 16 + (lane >> 4) * 4 + e;
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[i][j][e];
+      }
+    }
+}
+
 int g_num_cus = 0;
 
 // main loop: 7 = ping-pong quadrant schedule (256-wide tiles; 128-wide tiles use the ring, 1)
@@ -1146,6 +1349,77 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
   a.cv.stride = (int)stride; a.cv.pad = (int)pad; a.cv.kw = (int)kw;
   return xl_conv_run(a, x, mode, residual, bn_x, bn_y, mean, invstd, weight, bias, {});
 }
+
+void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream);
+
+namespace {
+
+int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
+
+at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype) {
+  const int M = a.M, N = a.N, K = a.K;
+  auto out = at::empty({N, K}, like.options().dtype(out_dtype));
+  if (M == 0) return out.zero_();
+  const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
+  // one or two full rounds of 1-block/CU work; every split >= 16 K tiles
+  const int mtl = (M + 63) / 64;
+  int rounds = tiles >= 256 ? (tiles + 255) / 256 : (tiles * std::max(1, 256 / tiles) >= 192 ? 1 : 2);
+  if (g_tn_xl_rounds > 0) rounds = g_tn_xl_rounds;
+  int splits = std::max(1, std::min(256 * rounds / tiles, mtl / 16));
+  int64_t rps = ((int64_t)M + splits - 1) / splits;
+  rps = (rps + 63) / 64 * 64;
+  splits = (int)(((int64_t)M + rps - 1) / rps);
+  a.rps = rps;
+  auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
+  a.part = part.data_ptr<float>();
+  hipStream_t s = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(gemm_tn_pp_kernel, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  DMP_HIP_CHECK(hipGetLastError());
+  split_reduce_launch(a.part, splits, (int64_t)N * K, out, s);
+  return out;
+}
+
+}  // namespace
+
+// dW = A^T B on the ping-pong TN kernel: A [M, N], B [M, K] bf16 row-major.
+at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype) {
+  check_bf16_2d(A, "A");
+  check_bf16_2d(B, "B");
+  TORCH_CHECK(A.size(0) == B.size(0), "gemm_tn_xl: M mismatch");
+  TORCH_CHECK(A.size(1) % 8 == 0 && B.size(1) % 8 == 0, "gemm_tn_xl: N, K must be multiples of 8");
+  TORCH_CHECK(A.size(0) < (1LL << 31), "gemm_tn_xl: M out of range");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "gemm_tn_xl: fp32 or bf16 output");
+  TnPPArgs a{};
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
+  a.M = (int)A.size(0); a.N = (int)A.size(1); a.K = (int)B.size(1);
+  return run_tn_pp(a, A, out_dtype);
+}
+
+// Weight gradient of a kh x kw conv on the ping-pong TN kernel:
+// dW[Cout, kh*kw*Cin] (tap-major) = dy^T @ im2col(x); dy [N*Ho*Wo, Cout]
+// row-major, x NHWC (channels_last), Cin % 256 == 0 (a 256-wide K tile never
+// straddles a tap).
+at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
+                         int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype) {
+  check_bf16_2d(dy, "dy");
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_wgrad_xl: x must be channels_last bf16");
+  const int64_t nb = x.size(0), cin = x.size(1), hi = x.size(2), wi = x.size(3);
+  TORCH_CHECK(cin % 256 == 0, "conv_wgrad_xl: Cin must be a multiple of 256");
+  TORCH_CHECK(dy.size(0) == nb * ho * wo && dy.size(1) % 8 == 0, "conv_wgrad_xl: dy must be [N*Ho*Wo, Cout]");
+  TORCH_CHECK(nb * hi * wi < (1LL << 31) && dy.size(0) < (1LL << 31), "conv_wgrad_xl: too many pixels");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "conv_wgrad_xl: fp32 or bf16 output");
+  TnPPArgs a{};
+  a.A = reinterpret_cast<const bf16*>(dy.data_ptr()); a.lda = dy.stride(0);
+  a.B = reinterpret_cast<const bf16*>(x.data_ptr()); a.ldb = cin;
+  a.M = (int)dy.size(0); a.N = (int)dy.size(1); a.K = (int)(kh * kw * cin);
+  a.cv.cin = (int)cin; a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
+  a.cv.stride = (int)stride; a.cv.pad = (int)pad; a.cv.kw = (int)kw;
+  return run_tn_pp(a, dy, out_dtype);
+}
+
+void set_tn_xl_rounds(int r) { g_tn_xl_rounds = r; }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
   TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");

@@ -182,11 +182,27 @@ class _Conv1x1Fn(torch.autograd.Function):
                 dx = _unrows(dx2, n, h, w)
         if ctx.needs_input_grad[1]:
             # split-M MFMA GEMM with transposing LDS reads (hipBLASLt picks a 4-tile,
-            # no-split kernel for this tiny-output / huge-reduction shape)
-            dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
+            # no-split kernel for this tiny-output / huge-reduction shape); the
+            # ping-pong form where both output dims fill its 256x256 tile
+            if not ctx.geom and _tn_xl(dy2.shape[0], cout, cin):
+                _STATS["tn_xl"] += 1
+                dw = C.gemm_tn_xl(dy2, _rows(x), weight.dtype).view(cout, cin, 1, 1)
+            else:
+                dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)
         return dx, dw, None, None, None, None, None
+
+
+_TN_XL = os.environ.get("DMP_TN_XL", "1") != "0"
+_STATS["tn_xl"] = 0
+
+
+def _tn_xl(m: int, cout: int, cin: int) -> bool:
+    """Ping-pong TN weight gradient: layer-3-sized 1x1 convs (both output dims
+    >= 256, M >= 150k rows), where it measured 0.17 vs 0.20 ms
+    (tools/tn_xl_bench.py); deeper-K / shorter-M layer-4 shapes tie."""
+    return _TN_XL and cout >= 256 and cin >= 256 and m >= 150_000
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,

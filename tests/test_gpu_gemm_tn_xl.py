@@ -1,0 +1,51 @@
+"""Weight-gradient GEMM on the ping-pong schedule (csrc/gemm/gemm_xl.hip
+gemm_tn_pp_kernel: m-major LDS planes, transposing LDS reads, split over M)
+against fp32 torch: plain A^T B with ragged M / N / K, and the implicit-GEMM
+conv weight gradient (3x3, strided, 1x1 strided) against autograd."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd import _native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last
+
+
+@pytest.mark.parametrize("M,N,K", [(802816 // 4, 256, 1024), (5000, 200, 264), (100, 256, 256), (64, 512, 512),
+                                   (33, 64, 128), (50176, 2048, 512)])
+@pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])
+def test_gemm_tn_xl(M, N, K, out):
+    C = _native.require("gemm_tn_xl")
+    torch.manual_seed(0)
+    a = torch.randn(M, N, device=DEV).bfloat16()
+    b = torch.randn(M, K, device=DEV).bfloat16()
+    got = C.gemm_tn_xl(a, b, out)
+    ref = a.float().t() @ b.float()
+    tol = 1e-3 * M ** 0.5 + (0.02 * ref.abs().max().item() if out == torch.bfloat16 else 0)
+    torch.testing.assert_close(got.float(), ref, atol=tol, rtol=1e-2)
+
+
+def test_gemm_tn_xl_exact_pattern():
+    C = _native.require("gemm_tn_xl")
+    M, N, K = 640, 256, 512
+    a = (torch.arange(M * N, device=DEV).reshape(M, N) % 7 - 3).bfloat16()
+    b = (torch.arange(M * K, device=DEV).reshape(M, K) % 5 - 2).bfloat16()
+    assert torch.equal(C.gemm_tn_xl(a, b, torch.float32), a.float().t() @ b.float())
+
+
+@pytest.mark.parametrize("n,cin,cout,h,k,s", [(4, 256, 256, 9, 3, 1), (3, 256, 512, 15, 3, 2), (2, 512, 256, 7, 3, 1),
+                                              (4, 256, 128, 10, 1, 2)])
+def test_conv_wgrad_xl(n, cin, cout, h, k, s):
+    C = _native.require("conv_wgrad_xl")
+    torch.manual_seed(1)
+    p = k // 2
+    ho = (h + 2 * p - k) // s + 1
+    x = torch.randn(n, cin, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    dy = torch.randn(n, cout, ho, ho, device=DEV).bfloat16().contiguous(memory_format=CL)
+    dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+    got = C.conv_wgrad_xl(dy2, x, k, k, s, p, ho, ho, torch.float32).view(cout, k, k, cin).permute(0, 3, 1, 2)
+    wr = torch.zeros(cout, cin, k, k, device=DEV, requires_grad=True)
+    F.conv2d(x.float(), wr, None, s, p).backward(dy.float())
+    torch.testing.assert_close(got, wr.grad, atol=2e-3 * (n * ho * ho) ** 0.5, rtol=1e-2)

@@ -113,6 +113,8 @@ def main():
             res["fwd"]["ours"] = timeit(lambda: C.gemm_nt(x2, w2, mode="moments", a_map=geom))
             res["dgrad"]["ours"] = timeit(lambda: C.gemm_nt(dy2, wt, c_map=geom))
             res["wgrad"]["ours"] = timeit(lambda: C.gemm_tn(dy2, x2, dt, b_map=geom))
+            if hasattr(C, "gemm_tn_xl") and s == 1 and cout >= 128 and cin >= 256:
+                res["wgrad"]["xl"] = timeit(lambda: C.gemm_tn_xl(dy2, x2, dt))
             if s == 1:
                 res["fwd"]["blaslt"] = timeit(lambda: x2 @ w2.t())
                 res["dgrad"]["blaslt"] = timeit(lambda: dy2 @ w2)
@@ -122,6 +124,8 @@ def main():
             wtr = w.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
             res["dgrad"]["ours"] = timeit(lambda: C.conv_nt(dy, wtr, k, k, s, pad, h, h, transposed=True))
             res["wgrad"]["ours"] = timeit(lambda: C.conv_wgrad(dy2, x, k, k, s, pad, ho, ho, dt))
+            if hasattr(C, "conv_wgrad_xl") and cin % 256 == 0:
+                res["wgrad"]["xl"] = timeit(lambda: C.conv_wgrad_xl(dy2, x, k, k, s, pad, ho, ho, dt))
             if hasattr(C, "conv_xl") and k > 1:  # 256x256 ping-pong implicit GEMM
                 res["fwd"]["xl"] = timeit(lambda: C.conv_xl(x, _wmat(w), k, k, s, pad, ho, ho, "moments"))
                 if s == 1:
