@@ -56,6 +56,19 @@ _STATS["xl_dgrad"] = 0
 _STATS["xl_bnbwd"] = 0
 
 
+# Forward where neither of our kernels wins: for Cout < 256 (layers 1-2) the
+# 4-wave conv_nt with fused moments (0.47-0.70 ms) loses to MIOpen's forward
+# plus the separate BN moments pass (0.33-0.53 + 0.04-0.08 ms;
+# profiles/conv3x3_xl_r2.md), so those run F.conv2d and let the BN reduce.
+# DMP_IGEMM_FWD=1 keeps them on conv_nt.
+_FWD_MODE = os.environ.get("DMP_IGEMM_FWD", "auto")
+_STATS["miopen_fwd"] = 0
+
+
+def _miopen_fwd(cout: int, kh: int) -> bool:
+    return _FWD_MODE == "auto" and kh > 1 and not (_XL3 and cout >= 256)
+
+
 def _xl_fwd(cout: int, kh: int, kw: int) -> bool:
     return _XL3 and cout >= 256 and kh == kw and kh > 1
 
@@ -172,6 +185,9 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
                  moments: bool = False, groups: int = 1,
                  dilation=(1, 1)) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
+    if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]):
+        _STATS["miopen_fwd"] += 1
+        return F.conv2d(x, weight, None, stride, padding, dilation, groups), None
     if _native_ok(x, weight, groups, dilation):
         _STATS["native"] += 1
         bn_slot = getattr(x, "_dmp_bnbwd", None) if torch.is_grad_enabled() else None

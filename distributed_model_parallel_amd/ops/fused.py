@@ -184,6 +184,10 @@ def bn_relu_conv1x1(bn: nn.Module, conv: nn.Module, x: torch.Tensor,
     from .. import _native
     from ..utils.checkpointing import in_recompute
     from .conv1x1 import Conv1x1, _native_ok
+    if sums is None and isinstance(bn, BatchNormAct2d) and bn.training and _native_ok(x, conv.weight):
+        # the producing conv ran on a library kernel (no fused moments): reduce here
+        from .batchnorm import _as_rows, local_moments
+        sums = local_moments(_as_rows(x)[0], True)
     fusable = (sums is not None and isinstance(bn, BatchNormAct2d) and bn.act == "relu"
                and bn.training and bn.track_running_stats and bn.momentum is not None
                and not in_recompute() and isinstance(conv, Conv1x1) and conv.stride[0] == 1

@@ -21,6 +21,13 @@ SHAPES = [  # n, cin, cout, h, w, k, stride, pad
 ]
 
 
+@pytest.fixture(autouse=True)
+def _native_forward(monkeypatch):
+    """These tests exercise our kernels: keep layer-1/2-sized forwards off MIOpen."""
+    from distributed_model_parallel_amd.ops import conv_igemm
+    monkeypatch.setattr(conv_igemm, "_FWD_MODE", "1")
+
+
 def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
