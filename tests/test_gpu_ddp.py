@@ -34,9 +34,12 @@ for parallel in ("ddp", "syncbn"):
     a, b = out[(parallel, "0")], out[(parallel, "1")]
     assert "rccl" in str(b[2]).lower(), b[2]
     assert abs(a[0] - b[0]) < 1e-3 * max(1.0, abs(a[0])), (parallel, a[0], b[0])
-    cos = min(torch.nn.functional.cosine_similarity(x.flatten(), y.flatten(), dim=0).item()
-              for x, y in zip(a[1], b[1]) if y.norm() > 0)
-    assert cos > 0.98, (parallel, cos)
+    # whole-update cosine: MIOpen's weight gradients are not bit-deterministic
+    # (profiles/README.md finding 4), so single small tensors (a BN bias) can drift
+    # between two identical steps; an identity "average" must still keep the update
+    cos = torch.nn.functional.cosine_similarity(torch.cat([x.flatten() for x in a[1]]),
+                                                torch.cat([y.flatten() for y in b[1]]), dim=0).item()
+    assert cos > 0.99, (parallel, cos)
     print(parallel, "ok", a[0], b[0], b[2], cos)
 from distributed_model_parallel_amd.comm.rccl import default_communicator
 comm = default_communicator(env.device)
