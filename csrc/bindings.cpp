@@ -105,6 +105,8 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
                                 const c10::optional<at::Tensor>& invstd, const c10::optional<at::Tensor>& weight,
                                 const c10::optional<at::Tensor>& bias);
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
+// conv3x3_halo.hip
+std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 void set_tn_xl_rounds(int r);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
@@ -232,6 +234,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(),
         "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues");
+  m.def("conv3x3_c64", &dmp::conv3x3_c64, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
+        "3x3/s1/p1 64->64-channel conv (W = 56) on the persistent halo-tiled MFMA kernel; "
+        "returns (y [N*H*W, 64], fp64 moments [129] or empty)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M");

@@ -1,0 +1,298 @@
+// 3x3 / stride-1 / pad-1 convolution for 64 -> 64 channels (ResNet-50 layer 1:
+// 56x56, forward and data gradient) as a persistent, halo-tiled MFMA kernel.
+//
+// Why not the implicit GEMM: at Cin = Cout = 64 the tap-gather GEMMs
+// (conv_nt, MIOpen's igemm) re-read every input pixel 9 times through L2 and
+// run 3.7-4.6x over the conv's HBM floor (profiles/raw_r2/roofline_stem_l1.log:
+// l1 conv2 fwd 0.51 ms, dgrad 0.62 ms at batch 1024 vs a 0.137 ms floor).
+// Here each block keeps:
+//   * the whole weight tensor in VGPRs, as MFMA B fragments: wave (wm, wn)
+//     owns Cout [32 wn, 32 wn + 32) = 2 x 16 columns over the 18 k32 steps of
+//     K = 9 taps x 64 channels (144 VGPRs, loaded once per persistent block);
+//   * a (R+2) x (W+2)-pixel input halo in LDS (the zero padding included),
+//     staged by global_load_lds_dwordx4 (LDS DMA, no VGPR round trip) and
+//     double buffered: tile t+1's halo streams in while tile t multiplies;
+//   * the R x W output pixels of a tile as one flat M range (R = 4, W = 56:
+//     224 pixels = 14 row fragments of 16; wave row wm takes 7 of them), so
+//     no MFMA row is padding.
+// Every A fragment read is a ds_read_b128 of one halo pixel's 8 channels at
+// tap offset (kh, kw); the 16-B chunk of a pixel is XOR-swizzled by
+// (pixel >> 1) & 7 (applied to the DMA source address, undone on the read).
+// Tiles are R full output rows of one image, so a tile's output is one
+// contiguous 28 KB run of y: the epilogue restages it through LDS and writes
+// it with 16-B row-contiguous stores.  Blocks take contiguous tile ranges
+// (adjacent tiles share 2 halo rows in L2).  MOM: the block accumulates
+// per-channel (sum, sum^2) of the bf16-rounded outputs over all its tiles and
+// writes one partial row (gemm_bf16.hip's EPI_MOMENTS contract, reduced by
+// bn_reduce_partials_launch).
+//
+// The data gradient of the same conv is this kernel over dy with the weights
+// flipped and transposed (ops/conv_igemm.py), so one kernel serves both.
+// Reference: the convolutions it replaces are torchvision ResNet-50's
+// cuDNN/MIOpen 3x3s (reference model_parallel.py:61).
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include "../common.h"
+
+namespace dmp {
+
+void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
+                               hipStream_t stream);
+
+namespace {
+
+using bf16 = __bf16;
+using gptr_t = const __attribute__((address_space(1))) void*;
+using lptr_t = __attribute__((address_space(3))) void*;
+
+constexpr int C64 = 64;            // channels in and out
+constexpr int KSTEPS = 9 * C64 / 32;  // 18 k32 steps
+constexpr int HALO_THREADS = 256;
+
+// 16 zero bytes the DMA reads for padding / out-of-image halo pixels
+__device__ __attribute__((aligned(16))) uint32_t g_halo_zero[4];
+
+template <int W, int R>
+struct HaloGeo {
+  static constexpr int HW2 = W + 2;                       // halo row length (pixels)
+  static constexpr int PIX = (R + 2) * HW2;               // halo pixels
+  static constexpr int DMA_INSTR = (PIX * 8 + 63) / 64;   // 1 KB wave instructions per halo
+  static constexpr int DMA_PER_WAVE = (DMA_INSTR + 3) / 4;
+  static constexpr int BUF_BYTES = DMA_PER_WAVE * 4 * 1024;
+  static constexpr int OUT_PIX = R * W;
+  static constexpr int MFRAG = OUT_PIX / 16;              // row fragments per tile
+  static constexpr int MF_WAVE = MFRAG / 2;               // per wave row
+  static_assert(OUT_PIX % 32 == 0, "R*W must split into 2 x 16-row fragments");
+};
+
+__device__ __forceinline__ int halo_key(int q) { return (q >> 1) & 7; }
+
+template <int N>
+__device__ __forceinline__ void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Issue the LDS-DMA copies of tile `tile`'s halo into `buf` (this wave's share).
+template <int W, int R>
+__device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf, int tile, int H,
+                                           int tiles_per_img, int wave, int lane) {
+  using G = HaloGeo<W, R>;
+  const int n = tile / tiles_per_img;
+  const int r0 = (tile - n * tiles_per_img) * R;
+#pragma unroll
+  for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
+    const int ins = wave * G::DMA_PER_WAVE + i;
+    const int g = ins * 64 + lane;   // 16-B slot in the lane-linear LDS image
+    const int q = g >> 3;            // halo pixel
+    const int c = (g & 7) ^ halo_key(q);
+    const int hy = q / G::HW2, hx = q - hy * G::HW2;
+    const int iy = r0 - 1 + hy, ix = hx - 1;
+    const bool ok = q < G::PIX && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const void* src = ok ? (const void*)(x + (((int64_t)n * H + iy) * W + ix) * C64 + c * 8)
+                         : (const void*)g_halo_zero;
+    if (ins < G::DMA_INSTR)
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(buf + ins * 1024), 16, 0, 0);
+  }
+}
+
+template <int W, int R, bool MOM>
+__global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
+    const bf16* __restrict__ x, const bf16* __restrict__ wk, bf16* __restrict__ y, float* __restrict__ part,
+    double* zsums, int H, int tiles, int tiles_per_img) {
+  using G = HaloGeo<W, R>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  bf16* ostage = reinterpret_cast<bf16*>(smem + 2 * G::BUF_BYTES);  // [OUT_PIX][64]
+  float* mred = reinterpret_cast<float*>(smem + 2 * G::BUF_BYTES + G::OUT_PIX * C64 * 2);  // [2][64]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int l15 = lane & 15, lh = lane >> 4;
+  if constexpr (MOM) {
+    zero_moments(zsums, 2 * C64);
+    if (threadIdx.x < 2 * C64) mred[threadIdx.x] = 0.f;  // ordered by the first tile's barrier
+  }
+
+  // contiguous tile range of this block
+  const int t_begin = (int)((int64_t)tiles * blockIdx.x / gridDim.x);
+  const int t_end = (int)((int64_t)tiles * (blockIdx.x + 1) / gridDim.x);
+  if (t_begin < t_end) halo_issue<W, R>(x, smem, t_begin, H, tiles_per_img, wave, lane);
+
+  // weights -> B fragments: lane holds W[cout = 32 wn + 16 nf + l15][k = 32 s + 8 lh + j]
+  bf16x8 bw[2][KSTEPS];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf) {
+    const bf16* wrow = wk + (int64_t)(32 * wn + 16 * nf + l15) * (9 * C64) + 8 * lh;
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) bw[nf][s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
+  }
+  // flat output pixel of each of this lane's A rows -> halo pixel at tap (0, 0)
+  int q0[G::MF_WAVE];
+#pragma unroll
+  for (int f = 0; f < G::MF_WAVE; ++f) {
+    const int p = (wm * G::MF_WAVE + f) * 16 + l15;
+    const int oy = p / W, ox = p - oy * W;
+    q0[f] = oy * G::HW2 + ox;
+  }
+
+  int cur = 0;
+  for (int t = t_begin; t < t_end; ++t) {
+    vmcnt<0>();        // this tile's halo (and the previous tile's stores) landed
+    raw_barrier();     // ... for every wave; the other buffer is free again
+    if (t + 1 < t_end) halo_issue<W, R>(x, smem + (cur ^ 1) * G::BUF_BYTES, t + 1, H, tiles_per_img, wave, lane);
+    const char* hb = smem + cur * G::BUF_BYTES;
+
+    f32x4 acc[G::MF_WAVE][2];
+#pragma unroll
+    for (int f = 0; f < G::MF_WAVE; ++f)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) acc[f][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      const int tap = s >> 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
+      const int c = (s & 1) * 4 + lh;
+      bf16x8 a[G::MF_WAVE];
+#pragma unroll
+      for (int f = 0; f < G::MF_WAVE; ++f) {
+        const int q = q0[f] + kh * G::HW2 + kw;
+        a[f] = *reinterpret_cast<const bf16x8*>(hb + q * 128 + ((c ^ halo_key(q)) << 4));
+      }
+#pragma unroll
+      for (int f = 0; f < G::MF_WAVE; ++f)
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf)
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], bw[nf][s], acc[f][nf], 0, 0, 0);
+      // keep each k-step's 7 fragment reads next to its MFMAs: hoisting the
+      // reads of later steps (the default schedule) needs 28 VGPRs per step
+      // on top of the 144 weight registers and spills
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // epilogue: C/D row = 4 lh + i (pixel), col = l15 (channel) -> LDS stage
+#pragma unroll
+    for (int f = 0; f < G::MF_WAVE; ++f)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = (wm * G::MF_WAVE + f) * 16 + 4 * lh + i;
+          ostage[p * C64 + 32 * wn + 16 * nf + l15] = (bf16)acc[f][nf][i];
+        }
+    __syncthreads();
+    // the tile = R whole output rows of one image = one contiguous run of y;
+    // MOM: thread t always holds channels 8 (t % 8) .. +7 of its chunks
+    {
+      const int n = t / tiles_per_img;
+      const int r0 = (t - n * tiles_per_img) * R;
+      const int rows = min(R, H - r0);
+      const int chunks = rows * W * (C64 / 8);
+      bf16* dst = y + (((int64_t)n * H + r0) * W) * C64;
+      float s8[8], q8[8];
+      if constexpr (MOM)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s8[j] = q8[j] = 0.f;
+      for (int i = threadIdx.x; i < chunks; i += HALO_THREADS) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(ostage + i * 8);
+        *reinterpret_cast<bf16x8*>(dst + i * 8) = v;
+        if constexpr (MOM)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float fv = (float)v[j];
+            s8[j] += fv;
+            q8[j] = fmaf(fv, fv, q8[j]);
+          }
+      }
+      if constexpr (MOM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int off = 8; off < 64; off <<= 1) {
+            s8[j] += __shfl_xor(s8[j], off, 64);
+            q8[j] += __shfl_xor(q8[j], off, 64);
+          }
+        }
+        if (lane < 8)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            atomicAdd(&mred[8 * lane + j], s8[j]);        // LDS atomics
+            atomicAdd(&mred[C64 + 8 * lane + j], q8[j]);
+          }
+      }
+    }
+    cur ^= 1;
+    // the next iteration's barrier orders these LDS reads before the next tile's
+    // stage writes (which come after its MFMA loop)
+  }
+
+  if constexpr (MOM) {
+    // rows beyond H (a partial last tile) are never copied out, so they add
+    // nothing to either moment
+    __syncthreads();
+    if (threadIdx.x < 2 * C64) {
+      const int mo = threadIdx.x / C64, ch = threadIdx.x % C64;
+      part[((int64_t)mo * gridDim.x + blockIdx.x) * C64 + ch] = mred[mo * C64 + ch];
+    }
+  }
+}
+
+template <int W, int R, bool MOM>
+void launch(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* part, double* zs, int H,
+            int tiles, int tpi, int grid, hipStream_t stream) {
+  using G = HaloGeo<W, R>;
+  const int smem = 2 * G::BUF_BYTES + G::OUT_PIX * C64 * 2 + 2 * C64 * 4;
+  auto kern = conv3x3_c64_kernel<W, R, MOM>;
+  static bool attr = false;
+  if (!attr) {
+    DMP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
+    attr = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(HALO_THREADS), smem, stream,
+                     reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<const bf16*>(wk.data_ptr()),
+                     reinterpret_cast<bf16*>(y.data_ptr()), part, zs, H, tiles, tpi);
+}
+
+}  // namespace
+
+// y = conv3x3(x, W), stride 1, pad 1, x: [N, 64, H, 56] bf16 channels_last,
+// wmat: [64 cout][3][3][64 cin] flattened to [64, 576] bf16.  Returns
+// (y as [N*H*W, 64], moments fp64 [129] or empty).
+std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments) {
+  constexpr int W = 56, R = 4;
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4, "conv3x3_c64: bf16 NCHW-shaped x");
+  TORCH_CHECK(x.size(1) == C64 && x.size(3) == W && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_c64: x must be [N, 64, H, 56] channels_last");
+  TORCH_CHECK(wmat.scalar_type() == at::kBFloat16 && wmat.is_contiguous() && wmat.size(0) == C64 &&
+                  wmat.size(1) == 9 * C64, "conv3x3_c64: wmat must be contiguous [64, 576] bf16");
+  const int64_t n = x.size(0), H = x.size(2);
+  const int tpi = (int)((H + R - 1) / R);
+  const int64_t tiles64 = n * tpi;
+  TORCH_CHECK(tiles64 < (1 << 30), "conv3x3_c64: too many tiles");
+  const int tiles = (int)tiles64;
+  auto y = at::empty({n * H * W, C64}, x.options());
+  auto stream = at::hip::getCurrentHIPStream();
+  at::Tensor mom;
+  if (tiles == 0) return {y, at::zeros({moments ? 2 * C64 + 1 : 0}, x.options().dtype(at::kDouble))};
+  int dev = 0, cus = 256;
+  DMP_HIP_CHECK(hipGetDevice(&dev));
+  DMP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int grid = std::min(tiles, cus);
+  if (moments) {
+    mom = at::empty({2 * C64 + 1}, x.options().dtype(at::kDouble));
+    auto part = at::empty({2, grid, C64}, x.options().dtype(at::kFloat));
+    launch<W, R, true>(x, wmat, y, part.data_ptr<float>(), moments_zero_target(mom.data_ptr<double>(), grid),
+                       (int)H, tiles, tpi, grid, stream);
+    bn_reduce_partials_launch(part.data_ptr<float>(), grid, C64, mom.data_ptr<double>(),
+                              (double)(n * H * W), stream);
+  } else {
+    mom = at::empty({0}, x.options().dtype(at::kDouble));
+    launch<W, R, false>(x, wmat, y, nullptr, nullptr, (int)H, tiles, tpi, grid, stream);
+  }
+  DMP_HIP_CHECK(hipGetLastError());
+  return {y, mom};
+}
+
+}  // namespace dmp

@@ -65,6 +65,21 @@ _FWD_MODE = os.environ.get("DMP_IGEMM_FWD", "auto")
 _STATS["miopen_fwd"] = 0
 
 
+# 64 -> 64-channel 3x3/s1/p1 convs on 56-wide maps (ResNet-50 layer 1) run on
+# the persistent halo-tiled kernel (csrc/conv/conv3x3_halo.hip: weights in
+# VGPRs, input halo in LDS, read once from HBM), forward with the BN moments
+# fused and the data gradient as the same conv over flipped weights.
+# DMP_HALO3=0 sends them back to the policy below.
+_HALO3 = os.environ.get("DMP_HALO3", "1") != "0"
+_STATS["halo_fwd"] = 0
+_STATS["halo_dgrad"] = 0
+
+
+def _halo_ok(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, wdt: int) -> bool:
+    return _HALO3 and cin == 64 and cout == 64 and kh == 3 and kw == 3 and stride == 1 and pad == 1 \
+        and wdt == 56
+
+
 def _miopen_fwd(cout: int, kh: int) -> bool:
     return _FWD_MODE == "auto" and kh > 1 and not (_XL3 and cout >= 256)
 
@@ -110,7 +125,12 @@ class _ConvIGFn(torch.autograd.Function):
         cout, _, kh, kw = weight.shape
         ho, wo = _out_size(h, kh, stride, pad), _out_size(w, kw, stride, pad)
         mode = "moments" if moments else "store"
-        if _xl_fwd(cout, kh, kw):
+        if _halo_ok(cin, cout, kh, kw, stride, pad, w):
+            _STATS["halo_fwd"] += 1
+            y2, mom = C.conv3x3_c64(x, _wmat(weight).contiguous(), moments)
+            if not moments:
+                mom = None
+        elif _xl_fwd(cout, kh, kw):
             _STATS["xl_fwd"] += 1
             y2, mom = C.conv_xl(x, _wmat(weight), kh, kw, stride, pad, ho, wo, mode)
             if not moments:
@@ -144,7 +164,13 @@ class _ConvIGFn(torch.autograd.Function):
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         bs, ctx.bn_slot = ctx.bn_slot, None
-        if ctx.needs_input_grad[0] and _xl_dgrad(cin, kh, kw, stride):
+        if ctx.needs_input_grad[0] and _halo_ok(cin, cout, kh, kw, stride, pad, w):
+            # dx = conv(dy, flip(W)^T): the same 3x3/s1/p1 64->64 conv
+            wfl = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+            _STATS["halo_dgrad"] += 1
+            dx2, _ = C.conv3x3_c64(dy, wfl, False)
+            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        elif ctx.needs_input_grad[0] and _xl_dgrad(cin, kh, kw, stride):
             # dx = conv(dy, flip(W)^T, pad k-1-p) on the ping-pong implicit GEMM
             wfl = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
             _STATS["xl_dgrad"] += 1
@@ -185,7 +211,8 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
                  moments: bool = False, groups: int = 1,
                  dilation=(1, 1)) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
-    if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]):
+    if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]) and not \
+            _halo_ok(x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[3]):
         _STATS["miopen_fwd"] += 1
         return F.conv2d(x, weight, None, stride, padding, dilation, groups), None
     if _native_ok(x, weight, groups, dilation):

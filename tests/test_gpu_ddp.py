@@ -150,6 +150,9 @@ torch.cuda.synchronize()
 w1 = masters_sgd(opt)
 dps = [w1[id(p)] - w0[id(p)] for p in m.parameters()]
 errs = rel_errs(dps, base)
+pn = [n for n, _ in m.named_parameters()]
+print("dp-ddp worst", sorted(((((a - b).norm() / (b.norm() + 1e-12)).item(), n) for n, a, b in zip(pn, dps, base)), reverse=True)[:6])
+print("ddp-ddp noise", sorted(((((a - 2 * b).norm() / (2 * b.norm() + 1e-12)).item(), n) for n, a, b in zip(pn, slow, base)), reverse=True)[:6])
 assert errs[len(errs) // 2] < 0.02 and errs[-1] < 0.25, ("DP and DDP master updates differ", errs[len(errs) // 2], errs[-1])
 print("dp-ddp parity ok", errs[len(errs) // 2], errs[-1])
 destroy_distributed()
@@ -161,8 +164,8 @@ def test_reducer_stream_ordering_and_dp_ddp_precision_parity():
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     r = subprocess.run([sys.executable, "-c", ORDER_SCRIPT], env=env, capture_output=True, text=True,
                        timeout=600)
+    print(r.stdout[-3000:])
     if r.returncode != 0:
-        print(r.stdout[-3000:])
         print(r.stderr[-6000:])
     assert r.returncode == 0, "subprocess failed (output above)"
     assert "ordering ok" in r.stdout and "dp-ddp parity ok" in r.stdout
