@@ -151,24 +151,39 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
 #pragma unroll
       for (int nf = 0; nf < 2; ++nf) acc[f][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
+    // software pipeline over the 18 k-steps: step s+1's 7 fragment reads are
+    // issued before step s's 14 MFMAs, so their LDS latency hides behind them
+    // (one wave per SIMD: nothing else would).  The sched barrier keeps the
+    // compiler from hoisting further (a third fragment set would spill).
+    bf16x8 a[2][G::MF_WAVE];
+    auto load_step = [&](int s, bf16x8 (&dst)[G::MF_WAVE]) {
       const int tap = s >> 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
       const int c = (s & 1) * 4 + lh;
-      bf16x8 a[G::MF_WAVE];
 #pragma unroll
       for (int f = 0; f < G::MF_WAVE; ++f) {
         const int q = q0[f] + kh * G::HW2 + kw;
-        a[f] = *reinterpret_cast<const bf16x8*>(hb + q * 128 + ((c ^ halo_key(q)) << 4));
+        dst[f] = *reinterpret_cast<const bf16x8*>(hb + q * 128 + ((c ^ halo_key(q)) << 4));
       }
+    };
+    load_step(0, a[0]);
+#pragma unroll
+    for (int s = 0; s < KSTEPS; ++s) {
+      if (s + 1 < KSTEPS) load_step(s + 1, a[(s + 1) & 1]);
 #pragma unroll
       for (int f = 0; f < G::MF_WAVE; ++f)
 #pragma unroll
         for (int nf = 0; nf < 2; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], bw[nf][s], acc[f][nf], 0, 0, 0);
-      // keep each k-step's 7 fragment reads next to its MFMAs: hoisting the
-      // reads of later steps (the default schedule) needs 28 VGPRs per step
-      // on top of the 144 weight registers and spills
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s & 1][f], bw[nf][s], acc[f][nf], 0, 0, 0);
+      // interleave: the next step's 7 ds_reads go one per MFMA over the first
+      // half of this step, leaving 7 MFMAs (~112 cycles) for the last to land
+      if (s + 1 < KSTEPS) {
+#pragma unroll
+        for (int f = 0; f < G::MF_WAVE; ++f) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, G::MF_WAVE, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
 

@@ -4,9 +4,11 @@ per-GPU batch 2048): activations of 1.6 G elements / 3.3 GB per tensor, so any
 numerics tests.
 
 A batch made of the same 1024 images twice has exactly the training-mode BN
-statistics of the 1024 images alone, the same mean cross-entropy and the same
-(mean) gradients, so the 2048-image step must reproduce the 1024-image step up
-to reduction order.  The comparison runs in one subprocess (the model at this
+statistics of the 1024 images alone and the same mean cross-entropy, and its two
+halves must produce the same activations and input gradients; a wrapped offset
+breaks that symmetry.  (The parameter gradients are not compared exactly: a
+random-init ResNet-50 amplifies reduction-order differences chaotically,
+profiles/README.md finding 4.)  The comparison runs in one subprocess (the model at this
 size needs ~80 GB; nothing else is resident)."""
 import os
 import subprocess
@@ -46,30 +48,34 @@ def run(xb, yb):
 names = [n for n, _ in m.named_parameters()]
 l1, g1 = run(x, y)
 print("1024 done", file=sys.stderr, flush=True)
-l1b, g1b = run(x, y)                       # noise floor: the same step again
-l2, g2 = run(torch.cat([x, x]), torch.cat([y, y]))
-
-def cos_per_param(a, b):
-    out, off = [], 0
-    for p in m.parameters():
-        k = p.numel()
-        out.append(F.cosine_similarity(a[off:off + k], b[off:off + k], dim=0).item())
-        off += k
-    return out
-
-c_noise, c_big = cos_per_param(g1, g1b), cos_per_param(g1, g2)
-worst = sorted(range(len(names)), key=lambda i: c_big[i] - c_noise[i])[:8]
-for i in worst:
-    print(f"  {names[i]:40s} cos(1024,2048dup) {c_big[i]:.4f}  cos(1024,1024) {c_noise[i]:.4f}")
-print(f"loss 1024 {l1:.5f} / {l1b:.5f}  2048-dup {l2:.5f}  fc.weight cos {c_big[-2]:.5f}  "
-      f"finite {bool(torch.isfinite(g2).all())} bn {bn.stats()}", flush=True)
+# the duplicated batch: every per-sample path of the second half runs at
+# offsets past 2^31 bytes in the big activations (layer 1: 2048 x 56 x 56 x 256
+# bf16 = 3.3 GB), the first half below; with shared BN statistics the two halves
+# must agree -- forward activations and input gradients -- up to reduction order
+acts = []
+hooks = [mod.register_forward_hook(lambda _m, _i, o: acts.append(o.detach()))
+         for mod in m.modules() if type(mod).__name__ in ("Bottleneck", "BasicBlock")]
+xx = torch.cat([x, x]).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+for p in m.parameters():
+    p.grad = None
+loss2 = F.cross_entropy(m(xx).float(), torch.cat([y, y]))
+loss2.backward()
+torch.cuda.synchronize()
+for h in hooks:
+    h.remove()
+l2 = loss2.item()
+g2 = torch.cat([p.grad.float().flatten() for p in m.parameters()])
+worst_act = max(((a[:1024].float() - a[1024:].float()).norm() / a[:1024].float().norm()).item() for a in acts)
+d = xx.grad.float()
+dx_rel = ((d[:1024] - d[1024:]).norm() / d[:1024].norm()).item()
+cos = F.cosine_similarity(g1, g2, dim=0).item()
+print(f"loss 1024 {l1:.5f} 2048-dup {l2:.5f}; {len(acts)} block outputs, worst half-vs-half rel {worst_act:.2e}; "
+      f"input-grad half-vs-half rel {dx_rel:.2e}; param-grad cos vs 1024 {cos:.4f} (chaotic, not asserted); "
+      f"bn {bn.stats()}", flush=True)
 assert abs(l1 - l2) < 2e-3 * abs(l1), (l1, l2)
-assert bool(torch.isfinite(g2).all())
-# the head sees no backward chaos: its gradient must agree to bf16 precision;
-# deeper layers must agree as well as two identical 1024-image steps do
-assert c_big[-2] > 0.999 and c_big[-1] > 0.999, (c_big[-2], c_big[-1])
-bad = [names[i] for i in range(len(names)) if c_big[i] < min(0.99, c_noise[i] - 0.05)]
-assert not bad, bad
+assert bool(torch.isfinite(g2).all()) and bool(torch.isfinite(d).all())
+assert len(acts) == 16 and worst_act < 1e-2, worst_act
+assert dx_rel < 2e-2, dx_rel
 print("bigbatch ok")
 '''
 
