@@ -4,10 +4,12 @@
 BASELINE.json metric: "images/sec (whole node) ResNet-50 DDP bf16 at 1/2/4/8
 MI355X".  One process per GPU (torchrun for N>1), synthetic 3x224x224 inputs
 and random-init weights (no datasets / checkpoints are available offline),
-fixed per-GPU batch (weak scaling; ResNet-50 default 1024 images per GPU --
+fixed per-GPU batch (weak scaling; ResNet-50 default 2048 images per GPU --
 measured on 1x MI355X: 7607 img/s at 128, 8339 at 192, 8866 at 256, 9279 at
-384, 9600-9744 at 512, 9948 at 768, 10300 at 1024 (40 GB peak), 10580 at
-2048 (80 GB); the 288 GB of HBM hold it easily and a bigger per-GPU share
+384, 9600-9744 at 512, 9948 at 768 (round 1); round 2: 11491-11818 at 1024
+(40 GB peak), 11956-12155 at 2048 (80 GB peak, profiles/raw_r2/bench_bs*.log);
+the 288 GB of HBM hold it easily, the activations of 3.3 GB per tensor are
+checked for offset wrap by tests/test_gpu_bigbatch.py, and a bigger per-GPU share
 also amortises the fixed gradient all-reduce).  Every timed step is a full training step:
 forward, fp32 cross-entropy, backward with the native C++ reducer doing
 bucketed RCCL all-reduces (25 MB buckets, ncclAvg) overlapped with backward,
@@ -53,7 +55,7 @@ from distributed_model_parallel_amd.utils.env import destroy_distributed, init_d
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
 
 # per-GPU batch defaults (measured throughput curves: module docstring, README)
-DEFAULT_BATCH = {"resnet50": 1024, "vit_b_16": 256, "mobilenetv2": 512}
+DEFAULT_BATCH = {"resnet50": 2048, "vit_b_16": 256, "mobilenetv2": 512}
 BASELINE_VALUE = None  # BASELINE.json "published": {} -- no reference images/sec figure exists
 # The reference's only throughput numbers (Readme.md:283-292): MobileNetV2 CIFAR
 # time/batch -> images/sec, keyed (parallel, n_gpus, global batch).
