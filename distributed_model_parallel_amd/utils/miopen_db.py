@@ -27,6 +27,7 @@ full problem (batch, shape, layout, dtype) and MIOpen version: shapes that are
 not in the file are searched as usual and nothing else changes.
 
   python bench.py --miopen-db refresh   # search, then write the found entries back
+  DMP_MIOPEN_DB_OUT=gpurun_out/miopen python bench.py --miopen-db refresh   # ... elsewhere
 """
 from __future__ import annotations
 
@@ -76,7 +77,10 @@ def seed(mode: str = "use", skip_naive: bool = True) -> Optional[str]:
 
 
 def _write_back(d: Path) -> None:
-    DB_DIR.mkdir(parents=True, exist_ok=True)
+    # DMP_MIOPEN_DB_OUT: write somewhere else (e.g. gpurun_out/ on a remote box,
+    # to be copied into profiles/miopen/ afterwards)
+    out = Path(os.environ.get("DMP_MIOPEN_DB_OUT", str(DB_DIR)))
+    out.mkdir(parents=True, exist_ok=True)
     for f in d.glob("*.txt"):
-        shutil.copy2(f, DB_DIR / f.name)
+        shutil.copy2(f, out / f.name)
     shutil.rmtree(d, ignore_errors=True)
