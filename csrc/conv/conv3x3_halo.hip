@@ -62,6 +62,8 @@ struct HaloGeo {
   static constexpr int OUT_PIX = R * W;
   static constexpr int MFRAG = OUT_PIX / 16;              // row fragments per tile
   static constexpr int MF_WAVE = MFRAG / 2;               // per wave row
+  static constexpr int STORES_PER_THREAD = OUT_PIX * 8 / 256;  // 16-B output chunks, full tile
+  static_assert(OUT_PIX * 8 % 256 == 0, "full tiles must give every thread the same store count");
   static_assert(OUT_PIX % 32 == 0, "R*W must split into 2 x 16-row fragments");
 };
 
@@ -139,8 +141,14 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
   }
 
   int cur = 0;
+  bool full_prev = false;  // previous tile issued exactly STORES_PER_THREAD stores
   for (int t = t_begin; t < t_end; ++t) {
-    vmcnt<0>();        // this tile's halo (and the previous tile's stores) landed
+    // this tile's halo landed.  VMEM ops retire in issue order (one VM_CNT for
+    // loads, LDS-DMA and stores on CDNA), and the previous tile's stores were
+    // issued after this halo's DMA: leaving them in flight overlaps their
+    // write-back with this tile instead of draining it every tile
+    if (full_prev) vmcnt<G::STORES_PER_THREAD>();
+    else vmcnt<0>();
     raw_barrier();     // ... for every wave; the other buffer is free again
     if (t + 1 < t_end) halo_issue<W, R>(x, smem + (cur ^ 1) * G::BUF_BYTES, t + 1, H, tiles_per_img, wave, lane);
     const char* hb = smem + cur * G::BUF_BYTES;
@@ -205,6 +213,7 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
       const int r0 = (t - n * tiles_per_img) * R;
       const int rows = min(R, H - r0);
       const int chunks = rows * W * (C64 / 8);
+      full_prev = chunks == G::STORES_PER_THREAD * HALO_THREADS;
       bf16* dst = y + (((int64_t)n * H + r0) * W) * C64;
       float s8[8], q8[8];
       if constexpr (MOM)
