@@ -16,8 +16,8 @@
 //     224 pixels = 14 row fragments of 16; wave row wm takes 7 of them), so
 //     no MFMA row is padding.
 // Every A fragment read is a ds_read_b128 of one halo pixel's 8 channels at
-// tap offset (kh, kw); the 16-B chunk of a pixel is XOR-swizzled by
-// (pixel >> 1) & 7 (applied to the DMA source address, undone on the read).
+// tap offset (kh, kw); the 16-B chunk of a pixel is XOR-swizzled by a key of
+// the pixel index (halo_key; applied to the DMA source address, undone on the read).
 // Tiles are R full output rows of one image, so a tile's output is one
 // contiguous 28 KB run of y: the epilogue restages it through LDS and writes
 // it with 16-B row-contiguous stores.  Blocks take contiguous tile ranges
@@ -67,7 +67,15 @@ struct HaloGeo {
   static_assert(OUT_PIX % 32 == 0, "R*W must split into 2 x 16-row fragments");
 };
 
-__device__ __forceinline__ int halo_key(int q) { return (q >> 1) & 7; }
+// 16-B chunk swizzle of halo pixel q (128 B = 8 chunks).  A fragment read has
+// lane l on pixel q0 + (l & 15), chunk c0 + (l >> 4), and q0 takes every
+// residue (the tap offsets kh * 58 + kw); ds_read_b128 is serviced in 16-lane
+// groups {0-3,12-15,20-27}, {4-11,16-19,28-31} and their +32 images.  This
+// period-8 table keeps every group on 16 distinct 16-B bank slots for all 16
+// residues of q0 (exhaustive check; the (q >> 1) & 7 key of the GEMM tiles is
+// conflict-free only for 4-aligned q0 and measured 17 % of the kernel in
+// SQ_LDS_BANK_CONFLICT cycles).
+__device__ __forceinline__ int halo_key(int q) { return (0x31165572u >> (4 * (q & 7))) & 7; }
 
 template <int N>
 __device__ __forceinline__ void vmcnt() {
