@@ -77,6 +77,10 @@ struct HaloGeo {
 // SQ_LDS_BANK_CONFLICT cycles).
 __device__ __forceinline__ int halo_key(int q) { return (0x31165572u >> (4 * (q & 7))) & 7; }
 
+// output stage [pixel][64 ch]: 16-B chunk swizzle by pixel (even values, so a
+// channel pair of chunks stays adjacent)
+__device__ __forceinline__ int stage_key(int p) { return ((p >> 2) & 3) << 1; }
+
 template <int N>
 __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -87,24 +91,51 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// Issue the LDS-DMA copies of tile `tile`'s halo into `buf` (this wave's share).
+// The tile-invariant part of this lane's LDS-DMA slots: slot i of wave w is
+// 16-B piece g = (11 w + i) * 64 + lane of the lane-linear halo image, i.e.
+// halo pixel q = g / 8 and (swizzled) channel chunk c.  Packed per slot as
+// (element offset from the tile's first output row) << 3 | halo row, plus a
+// bitmask of the slots whose column is inside the image.
 template <int W, int R>
-__device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf, int tile, int H,
-                                           int tiles_per_img, int wave, int lane) {
+struct HaloSlots {
+  int pk[HaloGeo<W, R>::DMA_PER_WAVE];
+  uint32_t xok = 0;
+};
+
+template <int W, int R>
+__device__ __forceinline__ HaloSlots<W, R> halo_slots(int wave, int lane) {
   using G = HaloGeo<W, R>;
-  const int n = tile / tiles_per_img;
-  const int r0 = (tile - n * tiles_per_img) * R;
+  HaloSlots<W, R> hs;
 #pragma unroll
   for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
     const int ins = wave * G::DMA_PER_WAVE + i;
-    const int g = ins * 64 + lane;   // 16-B slot in the lane-linear LDS image
-    const int q = g >> 3;            // halo pixel
+    const int g = ins * 64 + lane;
+    const int q = g >> 3;
     const int c = (g & 7) ^ halo_key(q);
     const int hy = q / G::HW2, hx = q - hy * G::HW2;
-    const int iy = r0 - 1 + hy, ix = hx - 1;
-    const bool ok = q < G::PIX && iy >= 0 && iy < H && ix >= 0 && ix < W;
-    const void* src = ok ? (const void*)(x + (((int64_t)n * H + iy) * W + ix) * C64 + c * 8)
-                         : (const void*)g_halo_zero;
+    const int ix = hx - 1;
+    hs.pk[i] = (((hy - 1) * W + ix) * C64 + c * 8) * 8 + min(hy, 7);
+    if (q < G::PIX && ins < G::DMA_INSTR && ix >= 0 && ix < W) hs.xok |= 1u << i;
+  }
+  return hs;
+}
+
+// Issue the LDS-DMA copies of tile `tile`'s halo into `buf` (this wave's share).
+template <int W, int R>
+__device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf, int tile, int H,
+                                           int tiles_per_img, int wave, int lane,
+                                           const HaloSlots<W, R>& hs) {
+  using G = HaloGeo<W, R>;
+  const int n = tile / tiles_per_img;
+  const int r0 = (tile - n * tiles_per_img) * R;
+  const bf16* base = x + ((int64_t)n * H + r0) * W * C64;
+  const int rlo = 1 - r0, rhi = H - r0 + 1;  // valid halo rows: rlo <= hy < rhi
+#pragma unroll
+  for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
+    const int ins = wave * G::DMA_PER_WAVE + i;
+    const int hy = hs.pk[i] & 7;
+    const bool ok = ((hs.xok >> i) & 1u) && hy >= rlo && hy < rhi;
+    const void* src = ok ? (const void*)(base + (hs.pk[i] >> 3)) : (const void*)g_halo_zero;
     if (ins < G::DMA_INSTR)
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(buf + ins * 1024), 16, 0, 0);
   }
@@ -129,7 +160,8 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
   // contiguous tile range of this block
   const int t_begin = (int)((int64_t)tiles * blockIdx.x / gridDim.x);
   const int t_end = (int)((int64_t)tiles * (blockIdx.x + 1) / gridDim.x);
-  if (t_begin < t_end) halo_issue<W, R>(x, smem, t_begin, H, tiles_per_img, wave, lane);
+  const HaloSlots<W, R> hs = halo_slots<W, R>(wave, lane);
+  if (t_begin < t_end) halo_issue<W, R>(x, smem, t_begin, H, tiles_per_img, wave, lane, hs);
 
   // weights -> B fragments: lane holds W[cout = 32 wn + 16 nf + l15][k = 32 s + 8 lh + j]
   bf16x8 bw[2][KSTEPS];
@@ -164,7 +196,7 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
     if (full_prev) vmcnt<G::STORES_PER_THREAD>();
     else vmcnt<0>();
     raw_barrier();     // ... for every wave; the other buffer is free again
-    if (t + 1 < t_end) halo_issue<W, R>(x, smem + (cur ^ 1) * G::BUF_BYTES, t + 1, H, tiles_per_img, wave, lane);
+    if (t + 1 < t_end) halo_issue<W, R>(x, smem + (cur ^ 1) * G::BUF_BYTES, t + 1, H, tiles_per_img, wave, lane, hs);
     const char* hb = smem + cur * G::BUF_BYTES;
 
     f32x4 acc[G::MF_WAVE][2];
@@ -217,7 +249,10 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int p = (wm * G::MF_WAVE + f) * 16 + 4 * lh + i;
-          ostage[p * C64 + 32 * wn + 16 * nf + l15] = (bf16)acc[f][nf][i];
+          // chunk swizzle: the 4 rows a write touches (4 lh + i, stride 4) land
+          // on 4 different 32-B spans of their bank window
+          const int ch = (4 * wn + 2 * nf + (l15 >> 3)) ^ stage_key(p);
+          ostage[p * C64 + ch * 8 + (l15 & 7)] = (bf16)acc[f][nf][i];
         }
     __syncthreads();
     // the tile = R whole output rows of one image = one contiguous run of y
@@ -229,7 +264,8 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
       full_prev = chunks == G::STORES_PER_THREAD * HALO_THREADS;
       bf16* dst = y + (((int64_t)n * H + r0) * W) * C64;
       for (int i = threadIdx.x; i < chunks; i += HALO_THREADS) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(ostage + i * 8);
+        const int sp = i >> 3;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(ostage + sp * C64 + (((i & 7) ^ stage_key(sp)) << 3));
         *reinterpret_cast<bf16x8*>(dst + i * 8) = v;
         if constexpr (MOM)
 #pragma unroll
