@@ -30,6 +30,7 @@
 // flipped and transposed (ops/conv_igemm.py), so one kernel serves both.
 // Reference: the convolutions it replaces are torchvision ResNet-50's
 // cuDNN/MIOpen 3x3s (reference model_parallel.py:61).
+#include <cstdlib>
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
 #include "../common.h"
@@ -47,23 +48,25 @@ using lptr_t = __attribute__((address_space(3))) void*;
 
 constexpr int C64 = 64;            // channels in and out
 constexpr int KSTEPS = 9 * C64 / 32;  // 18 k32 steps
-constexpr int HALO_THREADS = 256;
 
 // 16 zero bytes the DMA reads for padding / out-of-image halo pixels
 __device__ __attribute__((aligned(16))) uint32_t g_halo_zero[4];
 
-template <int W, int R>
+template <int W, int R, int NW>
 struct HaloGeo {
+  static constexpr int NT = 64 * NW;                      // threads (NW waves: 2 M x NW/2 N)
+  static constexpr int NFW = 8 / NW;                      // 16-channel output fragments per wave
   static constexpr int HW2 = W + 2;                       // halo row length (pixels)
   static constexpr int PIX = (R + 2) * HW2;               // halo pixels
   static constexpr int DMA_INSTR = (PIX * 8 + 63) / 64;   // 1 KB wave instructions per halo
-  static constexpr int DMA_PER_WAVE = (DMA_INSTR + 3) / 4;
-  static constexpr int BUF_BYTES = DMA_PER_WAVE * 4 * 1024;
+  static constexpr int DMA_PER_WAVE = (DMA_INSTR + NW - 1) / NW;
+  static constexpr int BUF_BYTES = DMA_PER_WAVE * NW * 1024;
   static constexpr int OUT_PIX = R * W;
   static constexpr int MFRAG = OUT_PIX / 16;              // row fragments per tile
   static constexpr int MF_WAVE = MFRAG / 2;               // per wave row
-  static constexpr int STORES_PER_THREAD = OUT_PIX * 8 / 256;  // 16-B output chunks, full tile
-  static_assert(OUT_PIX * 8 % 256 == 0, "full tiles must give every thread the same store count");
+  static constexpr int STORES_PER_THREAD = OUT_PIX * 8 / NT;  // 16-B output chunks, full tile
+  static constexpr bool STORES_EXACT = OUT_PIX * 8 % NT == 0;
+  static_assert(NW == 4 || NW == 8, "4 waves (2 x 32 channels each) or 8 (1 x 16)");
   static_assert(OUT_PIX % 32 == 0, "R*W must split into 2 x 16-row fragments");
 };
 
@@ -75,6 +78,7 @@ struct HaloGeo {
 // residues of q0 (exhaustive check; the (q >> 1) & 7 key of the GEMM tiles is
 // conflict-free only for 4-aligned q0 and measured 17 % of the kernel in
 // SQ_LDS_BANK_CONFLICT cycles).
+constexpr uint32_t kHaloKeys = 0x31165572u;  // nibble i = key of residue i
 __device__ __forceinline__ int halo_key(int q) { return (0x31165572u >> (4 * (q & 7))) & 7; }
 
 // output stage [pixel][64 ch]: 16-B chunk swizzle by pixel (even values, so a
@@ -96,16 +100,16 @@ __device__ __forceinline__ void raw_barrier() {
 // halo pixel q = g / 8 and (swizzled) channel chunk c.  Packed per slot as
 // (element offset from the tile's first output row) << 3 | halo row, plus a
 // bitmask of the slots whose column is inside the image.
-template <int W, int R>
+template <int W, int R, int NW>
 struct HaloSlots {
-  int pk[HaloGeo<W, R>::DMA_PER_WAVE];
+  int pk[HaloGeo<W, R, NW>::DMA_PER_WAVE];
   uint32_t xok = 0;
 };
 
-template <int W, int R>
-__device__ __forceinline__ HaloSlots<W, R> halo_slots(int wave, int lane) {
-  using G = HaloGeo<W, R>;
-  HaloSlots<W, R> hs;
+template <int W, int R, int NW>
+__device__ __forceinline__ HaloSlots<W, R, NW> halo_slots(int wave, int lane) {
+  using G = HaloGeo<W, R, NW>;
+  HaloSlots<W, R, NW> hs;
 #pragma unroll
   for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
     const int ins = wave * G::DMA_PER_WAVE + i;
@@ -121,11 +125,11 @@ __device__ __forceinline__ HaloSlots<W, R> halo_slots(int wave, int lane) {
 }
 
 // Issue the LDS-DMA copies of tile `tile`'s halo into `buf` (this wave's share).
-template <int W, int R>
+template <int W, int R, int NW>
 __device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf, int tile, int H,
                                            int tiles_per_img, int wave, int lane,
-                                           const HaloSlots<W, R>& hs) {
-  using G = HaloGeo<W, R>;
+                                           const HaloSlots<W, R, NW>& hs) {
+  using G = HaloGeo<W, R, NW>;
   const int n = tile / tiles_per_img;
   const int r0 = (tile - n * tiles_per_img) * R;
   const bf16* base = x + ((int64_t)n * H + r0) * W * C64;
@@ -141,11 +145,12 @@ __device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf
   }
 }
 
-template <int W, int R, bool MOM>
-__global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
+template <int W, int R, int NW, bool MOM>
+__global__ __launch_bounds__(64 * NW, 1) void conv3x3_c64_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, bf16* __restrict__ y, float* __restrict__ part,
     double* zsums, int H, int tiles, int tiles_per_img) {
-  using G = HaloGeo<W, R>;
+  using G = HaloGeo<W, R, NW>;
+  constexpr int NFW = G::NFW;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   bf16* ostage = reinterpret_cast<bf16*>(smem + 2 * G::BUF_BYTES);  // [OUT_PIX][64]
   float* mred = reinterpret_cast<float*>(smem + 2 * G::BUF_BYTES + G::OUT_PIX * C64 * 2);  // [2][64]
@@ -160,24 +165,34 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
   // contiguous tile range of this block
   const int t_begin = (int)((int64_t)tiles * blockIdx.x / gridDim.x);
   const int t_end = (int)((int64_t)tiles * (blockIdx.x + 1) / gridDim.x);
-  const HaloSlots<W, R> hs = halo_slots<W, R>(wave, lane);
-  if (t_begin < t_end) halo_issue<W, R>(x, smem, t_begin, H, tiles_per_img, wave, lane, hs);
+  const HaloSlots<W, R, NW> hs = halo_slots<W, R, NW>(wave, lane);
+  if (t_begin < t_end) halo_issue<W, R, NW>(x, smem, t_begin, H, tiles_per_img, wave, lane, hs);
 
-  // weights -> B fragments: lane holds W[cout = 32 wn + 16 nf + l15][k = 32 s + 8 lh + j]
-  bf16x8 bw[2][KSTEPS];
+  // weights -> B fragments: lane holds W[cout = 16 (NFW wn + nf) + l15][k = 32 s + 8 lh + j]
+  bf16x8 bw[NFW][KSTEPS];
 #pragma unroll
-  for (int nf = 0; nf < 2; ++nf) {
-    const bf16* wrow = wk + (int64_t)(32 * wn + 16 * nf + l15) * (9 * C64) + 8 * lh;
+  for (int nf = 0; nf < NFW; ++nf) {
+    const bf16* wrow = wk + (int64_t)(16 * (NFW * wn + nf) + l15) * (9 * C64) + 8 * lh;
 #pragma unroll
     for (int s = 0; s < KSTEPS; ++s) bw[nf][s] = *reinterpret_cast<const bf16x8*>(wrow + 32 * s);
   }
   // flat output pixel of each of this lane's A rows -> halo pixel at tap (0, 0)
-  int q0[G::MF_WAVE];
+  // Per fragment: the byte address of its tap-(0,0) halo pixel, and the
+  // halo_key nibble table rotated to that pixel's residue with this lane's
+  // chunk (lh) folded in, so a read at tap offset o costs one bit-field
+  // extract (nibble o & 7) and one shift-add.  (Precomputing every (fragment,
+  // k-step) offset instead -- the compiler's own choice -- holds 126 registers.)
+  int qb[G::MF_WAVE];
+  uint32_t kt[G::MF_WAVE];
 #pragma unroll
   for (int f = 0; f < G::MF_WAVE; ++f) {
     const int p = (wm * G::MF_WAVE + f) * 16 + l15;
     const int oy = p / W, ox = p - oy * W;
-    q0[f] = oy * G::HW2 + ox;
+    const int q = oy * G::HW2 + ox;
+    qb[f] = q * 128;
+    const uint32_t r = 4u * (uint32_t)(q & 7);
+    const uint32_t rot = r == 0 ? kHaloKeys : (kHaloKeys >> r) | (kHaloKeys << (32u - r));
+    kt[f] = rot ^ (0x11111111u * (uint32_t)lh);
   }
 
   // MOM: thread t always holds channels 8 (t % 8) .. +7 of the chunks it
@@ -189,21 +204,29 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
   int cur = 0;
   bool full_prev = false;  // previous tile issued exactly STORES_PER_THREAD stores
   for (int t = t_begin; t < t_end; ++t) {
+    // opaque per tile: keeps the per-(fragment, tap) offsets from being
+    // hoisted out of the tile loop into 126 live registers
+#pragma unroll
+    for (int f = 0; f < G::MF_WAVE; ++f) asm volatile("" : "+v"(kt[f]), "+v"(qb[f]));
     // this tile's halo landed.  VMEM ops retire in issue order (one VM_CNT for
     // loads, LDS-DMA and stores on CDNA), and the previous tile's stores were
     // issued after this halo's DMA: leaving them in flight overlaps their
     // write-back with this tile instead of draining it every tile
-    if (full_prev) vmcnt<G::STORES_PER_THREAD>();
-    else vmcnt<0>();
+    if constexpr (G::STORES_EXACT) {
+      if (full_prev) vmcnt<G::STORES_PER_THREAD>();
+      else vmcnt<0>();
+    } else {
+      vmcnt<0>();
+    }
     raw_barrier();     // ... for every wave; the other buffer is free again
-    if (t + 1 < t_end) halo_issue<W, R>(x, smem + (cur ^ 1) * G::BUF_BYTES, t + 1, H, tiles_per_img, wave, lane, hs);
+    if (t + 1 < t_end) halo_issue<W, R, NW>(x, smem + (cur ^ 1) * G::BUF_BYTES, t + 1, H, tiles_per_img, wave, lane, hs);
     const char* hb = smem + cur * G::BUF_BYTES;
 
-    f32x4 acc[G::MF_WAVE][2];
+    f32x4 acc[G::MF_WAVE][NFW];
 #pragma unroll
     for (int f = 0; f < G::MF_WAVE; ++f)
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf) acc[f][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nf = 0; nf < NFW; ++nf) acc[f][nf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // software pipeline over the 18 k-steps: step s+1's 7 fragment reads are
     // issued before step s's 14 MFMAs, so their LDS latency hides behind them
@@ -212,11 +235,12 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
     bf16x8 a[2][G::MF_WAVE];
     auto load_step = [&](int s, bf16x8 (&dst)[G::MF_WAVE]) {
       const int tap = s >> 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
-      const int c = (s & 1) * 4 + lh;
+      const int o = kh * G::HW2 + kw;   // tap offset in halo pixels
 #pragma unroll
       for (int f = 0; f < G::MF_WAVE; ++f) {
-        const int q = q0[f] + kh * G::HW2 + kw;
-        dst[f] = *reinterpret_cast<const bf16x8*>(hb + q * 128 + ((c ^ halo_key(q)) << 4));
+        // chunk = ((s & 1) * 4 + lh) ^ halo_key(q0 + o)
+        const uint32_t ch = ((kt[f] >> (4 * (o & 7))) & 7u) ^ (uint32_t)((s & 1) * 4);
+        dst[f] = *reinterpret_cast<const bf16x8*>(hb + qb[f] + o * 128 + (ch << 4));
       }
     };
     load_step(0, a[0]);
@@ -226,7 +250,7 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
 #pragma unroll
       for (int f = 0; f < G::MF_WAVE; ++f)
 #pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
+        for (int nf = 0; nf < NFW; ++nf)
           acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s & 1][f], bw[nf][s], acc[f][nf], 0, 0, 0);
       // interleave: the next step's 7 ds_reads go one per MFMA over the first
       // half of this step, leaving 7 MFMAs (~112 cycles) for the last to land
@@ -236,7 +260,7 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, G::MF_WAVE, 0);
+        if constexpr (NFW > 1) __builtin_amdgcn_sched_group_barrier(0x008, G::MF_WAVE * (NFW - 1), 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -245,13 +269,13 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
 #pragma unroll
     for (int f = 0; f < G::MF_WAVE; ++f)
 #pragma unroll
-      for (int nf = 0; nf < 2; ++nf)
+      for (int nf = 0; nf < NFW; ++nf)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int p = (wm * G::MF_WAVE + f) * 16 + 4 * lh + i;
           // chunk swizzle: the 4 rows a write touches (4 lh + i, stride 4) land
           // on 4 different 32-B spans of their bank window
-          const int ch = (4 * wn + 2 * nf + (l15 >> 3)) ^ stage_key(p);
+          const int ch = (2 * (NFW * wn + nf) + (l15 >> 3)) ^ stage_key(p);
           ostage[p * C64 + ch * 8 + (l15 & 7)] = (bf16)acc[f][nf][i];
         }
     __syncthreads();
@@ -261,9 +285,9 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
       const int r0 = (t - n * tiles_per_img) * R;
       const int rows = min(R, H - r0);
       const int chunks = rows * W * (C64 / 8);
-      full_prev = chunks == G::STORES_PER_THREAD * HALO_THREADS;
+      full_prev = chunks == G::STORES_PER_THREAD * G::NT;
       bf16* dst = y + (((int64_t)n * H + r0) * W) * C64;
-      for (int i = threadIdx.x; i < chunks; i += HALO_THREADS) {
+      for (int i = threadIdx.x; i < chunks; i += G::NT) {
         const int sp = i >> 3;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(ostage + sp * C64 + (((i & 7) ^ stage_key(sp)) << 3));
         *reinterpret_cast<bf16x8*>(dst + i * 8) = v;
@@ -306,20 +330,37 @@ __global__ __launch_bounds__(HALO_THREADS, 1) void conv3x3_c64_kernel(
   }
 }
 
-template <int W, int R, bool MOM>
-void launch(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* part, double* zs, int H,
-            int tiles, int tpi, int grid, hipStream_t stream) {
-  using G = HaloGeo<W, R>;
+template <int W, int R, int NW, bool MOM>
+void launch_nw(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* part, double* zs, int H,
+               int tiles, int tpi, int grid, hipStream_t stream) {
+  using G = HaloGeo<W, R, NW>;
   const int smem = 2 * G::BUF_BYTES + G::OUT_PIX * C64 * 2 + 2 * C64 * 4;
-  auto kern = conv3x3_c64_kernel<W, R, MOM>;
+  auto kern = conv3x3_c64_kernel<W, R, NW, MOM>;
   static bool attr = false;
   if (!attr) {
     DMP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
     attr = true;
   }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(HALO_THREADS), smem, stream,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), smem, stream,
                      reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<const bf16*>(wk.data_ptr()),
                      reinterpret_cast<bf16*>(y.data_ptr()), part, zs, H, tiles, tpi);
+}
+
+// DMP_HALO_WAVES=8: 8 waves (2 per SIMD, 16 output channels and 72 weight
+// VGPRs each) instead of 4 (1 per SIMD, 32 channels, 144 VGPRs)
+int halo_waves() {
+  static const int nw = [] {
+    const char* e = std::getenv("DMP_HALO_WAVES");
+    return (e != nullptr && std::atoi(e) == 8) ? 8 : 4;
+  }();
+  return nw;
+}
+
+template <int W, int R, bool MOM>
+void launch(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* part, double* zs, int H,
+            int tiles, int tpi, int grid, hipStream_t stream) {
+  if (halo_waves() == 8) launch_nw<W, R, 8, MOM>(x, wk, y, part, zs, H, tiles, tpi, grid, stream);
+  else launch_nw<W, R, 4, MOM>(x, wk, y, part, zs, H, tiles, tpi, grid, stream);
 }
 
 }  // namespace

@@ -17,11 +17,29 @@ GROUPS += [[lane + 32 for lane in g] for g in GROUPS]
 
 
 def _halo_key_table():
-    m = re.search(r"halo_key\(int q\) \{ return \((0x[0-9a-fA-F]+)u >> \(4 \* \(q & 7\)\)\) & 7; \}",
-                  SRC.read_text())
-    assert m, "halo_key definition changed: update this test"
+    src = SRC.read_text()
+    m = re.search(r"halo_key\(int q\) \{ return \((0x[0-9a-fA-F]+)u >> \(4 \* \(q & 7\)\)\) & 7; \}", src)
+    k = re.search(r"constexpr uint32_t kHaloKeys = (0x[0-9a-fA-F]+)u;", src)
+    assert m and k, "halo_key / kHaloKeys definition changed: update this test"
+    # the DMA side (halo_key) and the fragment reads (kHaloKeys) must agree
+    assert int(m.group(1), 16) == int(k.group(1), 16)
     packed = int(m.group(1), 16)
     return [(packed >> (4 * i)) & 7 for i in range(8)]
+
+
+def test_rotated_table_addressing_matches_key():
+    # fragment reads: nibble (o & 7) of rotr(table, 4 * (q0 & 7)) ^ lh == key(q0 + o) ^ lh
+    key = _halo_key_table()
+    packed = sum(k << (4 * i) for i, k in enumerate(key))
+    for q0 in range(64):
+        r = 4 * (q0 & 7)
+        rot = packed if r == 0 else ((packed >> r) | (packed << (32 - r))) & 0xFFFFFFFF
+        for lh in range(4):
+            kt = rot ^ (0x11111111 * lh)
+            for o in range(3 * 58 + 3):
+                for odd in (0, 1):
+                    ch = ((kt >> (4 * (o & 7))) & 7) ^ (4 * odd)
+                    assert ch == ((4 * odd + lh) ^ key[(q0 + o) & 7])
 
 
 def test_halo_key_conflict_free_for_every_start_residue():
