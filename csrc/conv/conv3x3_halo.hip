@@ -62,6 +62,7 @@ struct HaloGeo {
   static constexpr int DMA_PER_WAVE = (DMA_INSTR + NW - 1) / NW;
   static constexpr int BUF_BYTES = DMA_PER_WAVE * NW * 1024;
   static constexpr int OUT_PIX = R * W;
+  static constexpr int SMEM_BYTES = 2 * BUF_BYTES + OUT_PIX * 64 * 2 + 2 * 64 * 4;  // halo x2, stage, moments
   static constexpr int MFRAG = OUT_PIX / 16;              // row fragments per tile
   static constexpr int MF_WAVE = MFRAG / 2;               // per wave row
   static constexpr int STORES_PER_THREAD = OUT_PIX * 8 / NT;  // 16-B output chunks, full tile
@@ -151,7 +152,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_c64_kernel(
     double* zsums, int H, int tiles, int tiles_per_img) {
   using G = HaloGeo<W, R, NW>;
   constexpr int NFW = G::NFW;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  // static LDS (no per-device hipFuncSetAttribute: one process may drive
+  // several GPUs in DataParallel mode)
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM_BYTES];
   bf16* ostage = reinterpret_cast<bf16*>(smem + 2 * G::BUF_BYTES);  // [OUT_PIX][64]
   float* mred = reinterpret_cast<float*>(smem + 2 * G::BUF_BYTES + G::OUT_PIX * C64 * 2);  // [2][64]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -334,14 +337,9 @@ template <int W, int R, int NW, bool MOM>
 void launch_nw(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* part, double* zs, int H,
                int tiles, int tpi, int grid, hipStream_t stream) {
   using G = HaloGeo<W, R, NW>;
-  const int smem = 2 * G::BUF_BYTES + G::OUT_PIX * C64 * 2 + 2 * C64 * 4;
+  static_assert(G::SMEM_BYTES <= 160 * 1024, "LDS budget");
   auto kern = conv3x3_c64_kernel<W, R, NW, MOM>;
-  static bool attr = false;
-  if (!attr) {
-    DMP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
-    attr = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), smem, stream,
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT), 0, stream,
                      reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<const bf16*>(wk.data_ptr()),
                      reinterpret_cast<bf16*>(y.data_ptr()), part, zs, H, tiles, tpi);
 }
