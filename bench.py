@@ -49,9 +49,11 @@ from distributed_model_parallel_amd.comm.rccl import default_communicator  # noq
 from distributed_model_parallel_amd.models import INPUT_SHAPES  # noqa: E402
 from distributed_model_parallel_amd.train.cli import start_watchdog  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
-from distributed_model_parallel_amd.utils.profiling import trace_range  # noqa: E402
+from distributed_model_parallel_amd.utils.profiling import (  # noqa: E402
+    enable_phase_timing, phase_summary, trace_range)
 from distributed_model_parallel_amd.utils import gemm_tuning, miopen_db  # noqa: E402
-from distributed_model_parallel_amd.utils.env import destroy_distributed, init_distributed  # noqa: E402
+from distributed_model_parallel_amd.utils.env import (  # noqa: E402
+    count_gpus_without_hip, destroy_distributed, init_distributed)
 from distributed_model_parallel_amd.utils.precision import parse_dtype  # noqa: E402
 
 # per-GPU batch defaults (measured throughput curves: module docstring, README)
@@ -130,6 +132,16 @@ def main() -> int:
                     choices=["use", "refresh", "off"],
                     help="seed MIOpen's find/perf db from profiles/miopen/ (use), also write new "
                          "entries back (refresh), or start empty (off); see utils/miopen_db.py")
+    ap.add_argument("--dp-replicas", type=int, default=1,
+                    help="--parallel dp: replicas per GPU; K>1 aliases K replicas onto each device so "
+                         "scatter / replicate / parallel_apply / gather / reduce-add all execute even "
+                         "on one GPU (the per-GPU batch is split K ways)")
+    ap.add_argument("--phase-times", action="store_true",
+                    help="record HIP events around the DataParallel phases and report their GPU "
+                         "ms per step in the JSON (config.phase_ms_per_step)")
+    ap.add_argument("--single-rank-comm", action="store_true",
+                    help="run the DDP bucket all-reduces and SyncBN moment all-reduces through RCCL "
+                         "even at world size 1 (measures their cost on one GPU)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--watchdog", type=float, default=None, metavar="SECONDS",
                     help="exit 1 when the collective stream is stuck this long (default 900 s for "
@@ -145,12 +157,16 @@ def main() -> int:
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.parallel != "dp":
         # no launcher: become one (before any GPU call in this process)
-        if args.device != "cpu" and torch.cuda.device_count() < args.gpus:
-            raise SystemExit(f"--gpus {args.gpus} but only {torch.cuda.device_count()} GPUs visible")
+        # counted from the environment / KFD topology: this launcher never touches HIP
+        seen = count_gpus_without_hip() if args.device != "cpu" else None
+        if seen is not None and seen < args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but only {seen} GPUs visible")
         if args.device == "cpu":  # gloo plumbing run: do not oversubscribe the host
             os.environ.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // args.gpus)))
         return spawn_ranks(args.gpus, sys.argv[1:])
 
+    if args.single_rank_comm:
+        os.environ["DMP_SINGLE_RANK_COMM"] = "1"
     use_gpu = None if args.device == "auto" else args.device == "cuda"
     env = init_distributed(use_gpu=use_gpu)
     if args.parallel != "dp" and env.world_size != args.gpus:
@@ -165,7 +181,8 @@ def main() -> int:
                      dtype=parse_dtype(args.dtype), channels_last=not args.no_channels_last,
                      parallel=args.parallel, bucket_cap_mb=args.bucket_cap_mb,
                      first_bucket_mb=args.first_bucket_mb,
-                     dp_devices=args.gpus if args.parallel == "dp" else 1, graph=args.graph,
+                     dp_devices=args.gpus if args.parallel == "dp" else 1,
+                     dp_replicas=args.dp_replicas, graph=args.graph,
                      lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1),
                      micro_batches=args.micro_batches, schedule=args.schedule, partition=args.partition)
     if args.parallel == "dp" and env.world_size > 1:
@@ -191,6 +208,8 @@ def main() -> int:
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    if args.phase_times:
+        enable_phase_timing()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         with trace_range("bench.step"):
@@ -201,6 +220,8 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     elapsed = comm.max_scalar(elapsed)
     final_loss = float(loss.item())
+    phases = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] / args.steps}
+              for k, v in phase_summary().items()} if args.phase_times else None
 
     import torch.distributed as dist
     n = dist.get_world_size()
@@ -209,7 +230,7 @@ def main() -> int:
     # pipe: the batch is the whole pipeline's batch; data parallel: per GPU
     global_batch = args.batch_size if args.parallel == "pipe" else args.batch_size * n
     img_s = global_batch * args.steps / elapsed
-    par = {"ddp": "dp", "syncbn": "dp", "dp": "dp-single-process", "pipe": "pipe",
+    par = {"ddp": "ddp", "syncbn": "ddp-syncbn", "dp": "dp-single-process", "pipe": "pipe",
            "none": "none"}[args.parallel]
     metric = f"images/sec (whole node) {'ResNet-50' if args.model == 'resnet50' else args.model} " \
              f"{'DDP' if args.parallel in ('ddp', 'syncbn') else args.parallel.upper()} {args.dtype}"
@@ -237,6 +258,10 @@ def main() -> int:
             "seq_len": None,
             "image_size": image_size,
             "parallelism": f"{par}{n}",
+            **({"dp_replicas_per_gpu": args.dp_replicas,
+                "dp_device_ids": getattr(st.wrapped, "device_ids", None)} if args.parallel == "dp" else {}),
+            **({"phase_ms_per_step": phases} if phases is not None else {}),
+            "single_rank_comm": bool(args.single_rank_comm),
             "ranks": dist.get_world_size(),
             "rccl_ranks": comm.size if comm.native is not None else None,
             "launcher": "bench-spawn" if os.environ.get("DMP_BENCH_SPAWNED") else

@@ -154,7 +154,7 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
 void gather_slabs(const std::vector<at::Tensor>& inputs, at::Tensor& out, bool along_inner);
-void enable_peer_access(int64_t num_devices);
+std::vector<std::vector<bool>> enable_peer_access(int64_t num_devices);
 }  // namespace dmp
 
 namespace py = pybind11;

@@ -298,11 +298,18 @@ void gather_slabs(const std::vector<at::Tensor>& inputs, at::Tensor& out, bool a
                      static_cast<uint8_t*>(out.data_ptr()), out_row_bytes);
 }
 
-void enable_peer_access(int64_t num_devices) {
+// Enables every possible peer mapping among devices [0, num_devices) and
+// returns direct[a][b] = "a kernel on device a may dereference device b's
+// memory" (a == b is always direct).  Pairs without peer access are reported,
+// not skipped silently: comm_ops routes them through a staged copy
+// (hipMemcpyPeerAsync via torch's copy_) instead of a peer-pointer kernel.
+std::vector<std::vector<bool>> enable_peer_access(int64_t num_devices) {
+  std::vector<std::vector<bool>> direct(num_devices, std::vector<bool>(num_devices, false));
   int cur = 0;
   DMP_HIP_CHECK(hipGetDevice(&cur));
   for (int a = 0; a < num_devices; ++a) {
     DMP_HIP_CHECK(hipSetDevice(a));
+    direct[a][a] = true;
     for (int b = 0; b < num_devices; ++b) {
       if (a == b) continue;
       int can = 0;
@@ -314,9 +321,11 @@ void enable_peer_access(int64_t num_devices) {
         TORCH_CHECK(false, "hipDeviceEnablePeerAccess(", a, "->", b, ") failed: ", hipGetErrorString(e));
       }
       (void)hipGetLastError();
+      direct[a][b] = true;
     }
   }
   DMP_HIP_CHECK(hipSetDevice(cur));
+  return direct;
 }
 
 }  // namespace dmp

@@ -37,8 +37,43 @@ void ParallelApply::ensure_workers(size_t n) {
   }
 }
 
-// Runs with the GIL NOT held; takes it only around the Python call.
+namespace {
+// restores the thread's autocast state however run_job_impl leaves
+struct AutocastRestore {
+  bool enabled = at::autocast::is_autocast_enabled(at::kCUDA);
+  at::ScalarType dtype = at::autocast::get_autocast_dtype(at::kCUDA);
+  ~AutocastRestore() {
+    at::autocast::set_autocast_enabled(at::kCUDA, enabled);
+    at::autocast::set_autocast_dtype(at::kCUDA, dtype);
+  }
+};
+}  // namespace
+
+// A C++ exception (c10::Error from the device guard, a pybind11 cast error)
+// must not unwind through a worker thread or past apply() while other workers
+// still read `jobs`: it becomes this replica's (False, (RuntimeError, msg)).
 void ParallelApply::run_job(Job& job) {
+  std::string err;
+  try {
+    run_job_impl(job);
+  } catch (const std::exception& e) {
+    err = e.what();
+  } catch (...) {
+    err = "unknown C++ exception";
+  }
+  if (err.empty()) return;
+  py::gil_scoped_acquire gil;
+  std::string dev = job.device >= 0 ? "cuda:" + std::to_string(job.device) : "cpu";
+  std::string msg = "Caught RuntimeError in replica " + std::to_string(job.index) + " on device " + dev +
+                    ".\n" + err;
+  job.result = py::make_tuple(false, py::make_tuple(py::module_::import("builtins").attr("RuntimeError"), msg));
+  job.fn = py::object();
+  job.args = py::object();
+  job.kwargs = py::object();
+}
+
+// Runs with the GIL NOT held; takes it only around the Python call.
+void ParallelApply::run_job_impl(Job& job) {
   char name[48];
   std::snprintf(name, sizeof(name), "dp.replica%lld", (long long)job.index);
   trace::Range range(name);
@@ -48,8 +83,7 @@ void ParallelApply::run_job(Job& job) {
     if (job.stream) c10::hip::setCurrentHIPStream(*job.stream);
   }
   c10::AutoGradMode grad(job.grad_enabled);
-  const bool ac_prev = at::autocast::is_autocast_enabled(at::kCUDA);
-  const at::ScalarType ac_dtype_prev = at::autocast::get_autocast_dtype(at::kCUDA);
+  AutocastRestore ac_restore;
   at::autocast::set_autocast_enabled(at::kCUDA, job.autocast);
   at::autocast::set_autocast_dtype(at::kCUDA, job.autocast_dtype);
   {
@@ -76,8 +110,6 @@ void ParallelApply::run_job(Job& job) {
     job.args = py::object();
     job.kwargs = py::object();
   }
-  at::autocast::set_autocast_enabled(at::kCUDA, ac_prev);
-  at::autocast::set_autocast_dtype(at::kCUDA, ac_dtype_prev);
 }
 
 void ParallelApply::worker_main(Worker* w) {
@@ -99,8 +131,10 @@ void ParallelApply::worker_main(Worker* w) {
   }
 }
 
-py::list ParallelApply::apply(const py::list& modules, const py::list& inputs,
-                              const py::list& kwargs, const std::vector<int64_t>& devices) {
+py::object ParallelApply::apply(const py::list& modules, const py::list& inputs,
+                                const py::list& kwargs, const std::vector<int64_t>& devices) {
+  std::unique_lock<std::mutex> busy(apply_mu_, std::try_to_lock);
+  if (!busy.owns_lock()) return py::none();  // re-entered: the caller uses its own threads
   const size_t n = py::len(modules);
   TORCH_CHECK(py::len(inputs) == n && py::len(kwargs) == n && devices.size() == n,
               "parallel_apply: modules, inputs, kwargs and devices must have the same length");

@@ -34,7 +34,10 @@ class ParallelApply {
 
   // modules[i](*inputs[i], **kwargs[i]) on devices[i] (-1 = CPU).  Returns one
   // (ok, value) tuple per replica; on failure value = (exc_type, message).
-  pybind11::list apply(const pybind11::list& modules, const pybind11::list& inputs,
+  // Not reentrant: a call made while another is in flight (a second Python
+  // thread, or a DataParallel nested inside a replica) returns None at once and
+  // the caller falls back to its own threads.
+  pybind11::object apply(const pybind11::list& modules, const pybind11::list& inputs,
                        const pybind11::list& kwargs, const std::vector<int64_t>& devices);
   int64_t num_workers() const { return (int64_t)workers_.size(); }
 
@@ -57,10 +60,12 @@ class ParallelApply {
     bool stop = false;
   };
 
-  static void run_job(Job& job);
+  static void run_job(Job& job);       // never throws: errors become (False, ...)
+  static void run_job_impl(Job& job);
   void worker_main(Worker* w);
   void ensure_workers(size_t n);
 
+  std::mutex apply_mu_;  // held for the whole of one apply()
   std::vector<std::unique_ptr<Worker>> workers_;
   std::mutex done_mu_;
   std::condition_variable done_cv_;

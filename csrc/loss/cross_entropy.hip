@@ -45,8 +45,13 @@ __global__ __launch_bounds__(64 * kRowsPerBlock) void ce_fwd_kernel(
     const float lse = m + __logf(s);
     const int64_t t = tgt[row];
     const bool valid = t != ignore_index;
-    row_loss[row] = valid ? lse - ld(xr + (valid ? t : 0)) : 0.f;
-    lse_out[row] = lse;
+    // a label outside [0, C) (class-count / dataset mismatch) must not read
+    // past the row: it poisons the loss and this row's gradient with NaN
+    // instead (F.cross_entropy raises; a device-side NaN is visible in the
+    // very next loss.item() without a host sync here)
+    const bool in_range = t >= 0 && t < C;
+    row_loss[row] = !valid ? 0.f : in_range ? lse - ld(xr + t) : NAN;
+    lse_out[row] = (valid && !in_range) ? NAN : lse;
   }
 }
 
@@ -86,7 +91,8 @@ __global__ __launch_bounds__(64 * kRowsPerBlock) void ce_bwd_kernel(
   T* dr = dx + (int64_t)row * C;
   const int64_t t = tgt[row];
   const float n = stats[1];
-  const float scale = (t == ignore_index || n == 0.f) ? 0.f : gout[0] / n;
+  const bool bad = t != ignore_index && (t < 0 || t >= C);  // NaN lse: gradient is NaN too
+  const float scale = (t == ignore_index || n == 0.f) ? 0.f : bad ? NAN : gout[0] / n;
   const float l = lse[row];
   for (int c = lane; c < C; c += 64) {
     const float p = __expf(ld(xr + c) - l);

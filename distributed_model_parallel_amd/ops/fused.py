@@ -290,8 +290,9 @@ def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Te
         return pool(conv_bn(conv, bn, x))
     y, sums = conv.forward_with_moments(x)
     if (sums is None or not _native.gpu_path(y) or y.dtype != torch.bfloat16
-            or not y.is_contiguous(memory_format=torch.channels_last) or 128 % (y.shape[1] // 8) != 0
-            or y.shape[1] % 8 != 0 or bn.running_mean is None or bn.running_mean.dtype != torch.float32):
+            or not y.is_contiguous(memory_format=torch.channels_last)
+            or y.shape[1] < 8 or y.shape[1] % 8 != 0 or 128 % (y.shape[1] // 8) != 0
+            or bn.running_mean is None or bn.running_mean.dtype != torch.float32):
         return pool(bn(y, sums=sums))
     rmom, rgrad = bn._moment_reducers()
     pad = pool.padding if isinstance(pool.padding, int) else pool.padding[0]

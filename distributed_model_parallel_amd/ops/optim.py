@@ -87,6 +87,15 @@ class FlatSGD(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.ddp.zero_grad()
 
+    @torch.no_grad()
+    def sync_from_params(self) -> None:
+        """Re-seed the fp32 masters from the current working weights (weights
+        loaded behind the optimizer's back, e.g. a checkpoint without optimizer
+        state); otherwise the next step would write the stale masters back."""
+        for st in self._flat_state:
+            if "master" in st:
+                st["master"].copy_(st["param"])
+
     def state_dict(self):
         self._ensure_state()
         return {"steps": self._steps, "param_groups": [{k: v for k, v in g.items() if k != "params"}
@@ -103,6 +112,9 @@ class FlatSGD(torch.optim.Optimizer):
         starts in registration order -- so every parameter's slice is moved
         from ``sd['layout']`` to the current layout, never copied flat-to-flat.
         """
+        if "layout" not in sd or "flat_state" not in sd:
+            raise ValueError("FlatSGD.load_state_dict: not a FlatSGD state (e.g. a torch.optim.SGD "
+                             "state dict)")
         self._ensure_state()
         self._steps = sd["steps"]
         for g, sg in zip(self.param_groups, sd["param_groups"]):
@@ -212,6 +224,17 @@ class MasterSGD(torch.optim.Optimizer):
                 if p.grad is not gv:
                     p.grad = gv
 
+    @torch.no_grad()
+    def sync_from_params(self) -> None:
+        """Re-seed the fp32 masters from the current working weights.  The masters
+        are snapshotted at construction, so weights loaded afterwards without
+        optimizer state (the reference's {'net','acc','epoch'} checkpoints, a
+        plain ``model.load_state_dict``) must be adopted here, or the first step
+        would overwrite them with the init weights."""
+        for st in self._groups:
+            if "master" in st:
+                st["master"].copy_(st["param"])
+
     def state_dict(self):
         return {"steps": self._steps,
                 "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups],
@@ -220,6 +243,9 @@ class MasterSGD(torch.optim.Optimizer):
                                for st in self._groups]}
 
     def load_state_dict(self, sd):
+        if "numels" not in sd or "flat_state" not in sd:
+            raise ValueError("MasterSGD.load_state_dict: not a MasterSGD state (e.g. a torch.optim.SGD "
+                             "state dict)")
         if sd["numels"] != [[p.numel() for p in st["params"]] for st in self._groups]:
             raise ValueError("MasterSGD.load_state_dict: parameter layout differs from the checkpoint")
         self._steps = sd["steps"]

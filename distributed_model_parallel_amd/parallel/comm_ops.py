@@ -35,6 +35,38 @@ def _dev(d) -> torch.device:
     return torch.device("cuda", int(d)) if not isinstance(d, str) else torch.device(d)
 
 
+# _PEER[a][b]: a kernel on GPU a may dereference GPU b's memory (filled by
+# set_peer_matrix from the native enable_peer_access result).  Unknown (None)
+# means "never": a peer-pointer kernel over a pair without peer access is a GPU
+# fault, a staged copy is merely slower.
+_PEER: Optional[List[List[bool]]] = None
+
+
+def set_peer_matrix(direct: Optional[Sequence[Sequence[bool]]]) -> None:
+    global _PEER
+    _PEER = [list(map(bool, row)) for row in direct] if direct is not None else None
+
+
+def peer_ok(reader: torch.device, owner: torch.device) -> bool:
+    """May a kernel running on `reader` read `owner`'s memory directly?"""
+    reader, owner = _dev(reader), _dev(owner)
+    if reader == owner:
+        return True
+    if reader.type != "cuda" or owner.type != "cuda" or _PEER is None:
+        return False
+    try:
+        return _PEER[reader.index][owner.index]
+    except (IndexError, TypeError):
+        return False
+
+
+def _local(ts: Sequence[torch.Tensor], dst: torch.device) -> List[torch.Tensor]:
+    """`ts` made readable by a kernel on `dst`: tensors on a device `dst` has no
+    peer mapping to are first copied over by the runtime (staged
+    hipMemcpyPeerAsync behind torch's copy_, ordered on both current streams)."""
+    return [t if peer_ok(dst, t.device) else t.to(dst, non_blocking=True) for t in ts]
+
+
 def _wait_for(src_dev: torch.device, dst_dev: torch.device) -> None:
     """Make dst's current stream wait for work already queued on src's current stream."""
     if src_dev.type != "cuda" or dst_dev.type != "cuda" or src_dev == dst_dev:
@@ -61,6 +93,15 @@ def pull_copy(srcs: Sequence[torch.Tensor], dsts: Sequence[torch.Tensor]) -> Non
     if not srcs:
         return
     dd = dsts[0].device
+    if dd.type == "cuda" and not all(peer_ok(dd, t.device) for t in srcs):
+        direct = [(a, b) for a, b in zip(srcs, dsts) if peer_ok(dd, a.device)]
+        with torch.no_grad():
+            for a, b in zip(srcs, dsts):
+                if not peer_ok(dd, a.device):
+                    b.copy_(a, non_blocking=True)  # staged: no peer mapping for this pair
+        if direct:
+            pull_copy([a for a, _ in direct], [b for _, b in direct])
+        return
     for s in {t.device for t in srcs}:
         _wait_for(s, dd)
     _keep_alive(srcs, dd)
@@ -140,6 +181,8 @@ def reduce_add_coalesced(grads_per_device: Sequence[Sequence[torch.Tensor]],
             flats.append(flatops.flatten(ts))
         total = flats[0].numel()
         res = torch.empty(total, dtype=flats[0].dtype, device=dst)
+        if dst.type == "cuda":
+            flats = _local(flats, dst)
         for f in flats:
             _wait_for(f.device, dst)
         _keep_alive(flats, dst)
@@ -206,6 +249,7 @@ def gather_tensors(ts: Sequence[torch.Tensor], destination, dim: int = 0) -> tor
     out = torch.empty(shape, dtype=ts[0].dtype, device=dst)
     if dst.type != "cuda":
         return torch.cat([t.to(dst) for t in ts], dim, out=out)
+    ts = _local(ts, dst)
     for t in ts:
         _wait_for(t.device, dst)
     srcs = [t.contiguous() for t in ts]

@@ -32,7 +32,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from ..utils.profiling import trace_range
+from ..utils.profiling import phase, trace_range
 from . import comm_ops
 
 
@@ -53,7 +53,8 @@ class Scatter(torch.autograd.Function):
         grads = [g if g is not None else None for g in grads]
         if any(g is None for g in grads):
             return None, None, None, None
-        return None, None, None, comm_ops.gather_tensors(grads, ctx.src, ctx.dim)
+        with phase("dp.scatter_bwd"):
+            return None, None, None, comm_ops.gather_tensors(grads, ctx.src, ctx.dim)
 
 
 class Gather(torch.autograd.Function):
@@ -67,7 +68,8 @@ class Gather(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        parts = comm_ops.scatter_tensor(g.contiguous(), ctx.devices, ctx.dim, ctx.sizes)
+        with phase("dp.gather_bwd"):
+            parts = comm_ops.scatter_tensor(g.contiguous(), ctx.devices, ctx.dim, ctx.sizes)
         if ctx.scalar:
             parts = [p.view(()) for p in parts]
         return (None, None) + tuple(parts)
@@ -102,6 +104,11 @@ class Replicate(torch.autograd.Function):
                     ref = next(l[j] for l in per_dev if l[j] is not None) if any(
                         l[j] is not None for l in per_dev) else None
                     lst[j] = torch.zeros_like(ref, device=dev) if ref is not None else None
+        with phase("dp.reduce_add"):
+            return Replicate._reduce(ctx, per_dev, n)
+
+    @staticmethod
+    def _reduce(ctx, per_dev, n):
         if any(g is None for g in per_dev[0]):
             # a parameter with no grad anywhere
             keep = [j for j in range(n) if per_dev[0][j] is not None]
@@ -248,6 +255,8 @@ def parallel_apply(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=No
             devs.append(dd.index if (dd is not None and dd.type == "cuda") else -1)
         ins = [tuple(x) if isinstance(x, (list, tuple)) else (x,) for x in inputs]
         res = launcher.apply(list(modules), ins, [dict(k) for k in kwargs_tup], devs)
+        if res is None:  # launcher busy (another thread / a nested DataParallel): own threads
+            return _parallel_apply_threads(modules, inputs, kwargs_tup, devices)
         outs = []
         for i, (ok, val) in enumerate(res):
             if not ok:
@@ -342,27 +351,31 @@ class DataParallel(nn.Module):
             if t.device != self.src_device_obj:
                 raise RuntimeError(f"module must have its parameters and buffers on device "
                                    f"{self.src_device_obj} (device_ids[0]) but found one on {t.device}")
+        self.peer_matrix = None
         if len(set(self.device_ids)) > 1:
-            _native.require("DataParallel peer access").enable_peer_access(
+            # which pairs got a direct mapping; the others are routed through
+            # staged copies by comm_ops (never a peer-pointer kernel)
+            self.peer_matrix = _native.require("DataParallel peer access").enable_peer_access(
                 max(self.device_ids) + 1)
+            comm_ops.set_peer_matrix(self.peer_matrix)
 
     def forward(self, *inputs, **kwargs):
         if not self.device_ids:
             return self.module(*inputs, **kwargs)
         # roctx ranges (rocprofv3 --marker-trace): the four phases upstream DP
         # wraps in record_function("DataParallel.forward")
-        with trace_range("dp.scatter"):
+        with phase("dp.scatter"):
             ins, kws = scatter_kwargs(inputs, kwargs, self.device_ids, self.dim)
         if not ins and not kws:
             ins, kws = ((),), ({},)
         if len(self.device_ids) == 1:
-            with trace_range("dp.apply"):
+            with phase("dp.apply"):
                 return self.module(*ins[0], **kws[0])
-        with trace_range("dp.replicate"):
+        with phase("dp.replicate"):
             replicas = self.replicate(self.module, self.device_ids[:len(ins)])
-        with trace_range("dp.parallel_apply"):
+        with phase("dp.parallel_apply"):
             outs = self.parallel_apply(replicas, ins, kws)
-        with trace_range("dp.gather"):
+        with phase("dp.gather"):
             return self.gather(outs, self.output_device)
 
     def replicate(self, module, device_ids):

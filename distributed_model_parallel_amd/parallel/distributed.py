@@ -31,6 +31,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..utils.env import single_rank_comm
 from .. import _native
 from ..comm.rccl import Communicator, default_communicator
 from ..ops import flat as flatops
@@ -172,7 +173,7 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------------ #
     def _make_backend(self):
         C = _native.native()
-        if self.world_size == 1 and os.environ.get("DMP_DDP_SINGLE_RANK_COMM", "0") != "1":
+        if self.world_size == 1 and not single_rank_comm():
             # averaging over one rank is the identity: no collective to launch
             self.comm_backend = "none(world_size=1)"
             return C.NullReduceBackend()

@@ -32,7 +32,6 @@ loops in ``utils.py:34-210``, partition at ``model_parallel.py:101-104,
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -185,11 +184,47 @@ def recv_activation(shape, dtype, device, comm: Communicator, peer: int) -> torc
 # --------------------------------------------------------------------------- #
 # Pipeline engine
 # --------------------------------------------------------------------------- #
-@dataclass
 class StepResult:
-    loss: Optional[float]
-    top1: Optional[float]
-    top5: Optional[float]
+    """Per-step [loss, top1 %, top5 %] of one pipeline step.
+
+    Holds the device tensor of the sums; the Python floats are materialised
+    on first access (one host sync then), so a training loop that does not
+    look at them every step never blocks on the pipeline (no
+    per-step host round-trips).  ``loss_tensor`` is the 0-d device loss.
+    """
+
+    def __init__(self, loss: Optional[float] = None, top1: Optional[float] = None,
+                 top5: Optional[float] = None, stats: Optional[torch.Tensor] = None,
+                 batch: Optional[int] = None):
+        self._vals = None if stats is not None else (loss, top1, top5)
+        self._stats, self._batch = stats, batch
+
+    def _get(self):
+        if self._vals is None:
+            s = self._stats.tolist()
+            self._vals = (s[0], 100.0 * s[1] / self._batch, 100.0 * s[2] / self._batch)
+        return self._vals
+
+    @property
+    def loss(self) -> Optional[float]:
+        return self._get()[0]
+
+    @property
+    def top1(self) -> Optional[float]:
+        return self._get()[1]
+
+    @property
+    def top5(self) -> Optional[float]:
+        return self._get()[2]
+
+    @property
+    def loss_tensor(self) -> Optional[torch.Tensor]:
+        return self._stats[0] if self._stats is not None else (
+            None if self._vals[0] is None else torch.tensor(self._vals[0]))
+
+    @property
+    def valid(self) -> bool:
+        return self._stats is not None or self._vals[0] is not None
 
 
 def _topk_correct(logits: torch.Tensor, target: torch.Tensor, ks=(1, 5)) -> List[torch.Tensor]:
@@ -211,7 +246,7 @@ class Pipeline:
                  loss_fn: Optional[Callable] = None, loss_on: str = "last",
                  partition=None, balance: str = "flops",
                  device: Optional[torch.device] = None, dtype: torch.dtype = torch.float32,
-                 channels_last: bool = False):
+                 channels_last: bool = False, static_batch: Optional[int] = None):
         if schedule not in ("naive", "gpipe", "1f1b"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if loss_on not in ("last", "first"):
@@ -219,6 +254,7 @@ class Pipeline:
         if loss_on == "first" and schedule == "1f1b":
             raise ValueError("loss_on='first' (reference ring) supports schedule naive/gpipe")
         self.comm = comm
+        self.static_batch = static_batch  # batch-size contract shared by every rank (or None)
         self.rank, self.world = comm.rank, comm.size
         self.schedule = schedule
         self.micro_batches = 1 if schedule == "naive" else micro_batches
@@ -286,8 +322,19 @@ class Pipeline:
             left -= sizes[-1]
         return sizes
 
-    def _batch_size(self, inputs: Optional[torch.Tensor]) -> int:
-        """Rank 0 knows the batch; broadcast it along the pipeline (one int)."""
+    def _batch_size(self, inputs: Optional[torch.Tensor], batch_size: Optional[int] = None) -> int:
+        """The step's batch.  Static contract (no message, no host sync): every
+        rank passes ``batch_size`` (or the Pipeline was built with
+        ``static_batch``); rank 0 checks its input against it.  Dynamic
+        fallback: rank 0 forwards one int along the pipeline, which costs each
+        later stage one host sync (the receive buffers are sized from it)."""
+        if batch_size is None:
+            batch_size = self.static_batch
+        if batch_size is not None:
+            if self.is_first and inputs is not None and inputs.shape[0] != batch_size:
+                raise ValueError(f"pipeline batch contract is {batch_size} but rank 0 got "
+                                 f"{inputs.shape[0]} (pass batch_size= for a ragged last batch)")
+            return int(batch_size)
         t = torch.zeros(1, dtype=torch.int64, device=self.device)
         if self.is_first:
             t[0] = inputs.shape[0]
@@ -313,11 +360,12 @@ class Pipeline:
 
     # ---- public API -----------------------------------------------------------------
     def train_step(self, inputs: Optional[torch.Tensor] = None,
-                   targets: Optional[torch.Tensor] = None) -> StepResult:
+                   targets: Optional[torch.Tensor] = None, batch_size: Optional[int] = None) -> StepResult:
         """Forward + backward of one batch (inputs/targets needed on rank 0 only).
-        Gradients accumulate in ``self.module``; step your stage optimizer after."""
+        Gradients accumulate in ``self.module``; step your stage optimizer after.
+        ``batch_size`` (same on every rank) skips the batch-size message."""
         self.module.train()
-        batch = self._batch_size(inputs)
+        batch = self._batch_size(inputs, batch_size)
         sizes = self._mb_sizes(batch)
         if self.is_first:
             xs = list(torch.split(inputs, sizes, 0))
@@ -352,10 +400,9 @@ class Pipeline:
                 self.comm.send(stats, 0)
             elif self.is_first:
                 self.comm.recv(stats, holder)
-                self.comm.synchronize()
+                self.comm.wait()  # stream dependency only: the host does not block here
         if self.is_first or self.world == 1 or (self.rank == holder):
-            s = stats.tolist()
-            return StepResult(s[0], 100.0 * s[1] / batch, 100.0 * s[2] / batch)
+            return StepResult(stats=stats, batch=batch)
         return StepResult(None, None, None)
 
     def _loss_and_stats(self, y: torch.Tensor, t: torch.Tensor, stats: torch.Tensor) -> torch.Tensor:
@@ -486,10 +533,10 @@ class Pipeline:
 
     @torch.no_grad()
     def eval_step(self, inputs: Optional[torch.Tensor] = None,
-                  targets: Optional[torch.Tensor] = None) -> StepResult:
+                  targets: Optional[torch.Tensor] = None, batch_size: Optional[int] = None) -> StepResult:
         """Forward-only pass over the pipeline (reference val_* loops)."""
         self.module.eval()
-        batch = self._batch_size(inputs)
+        batch = self._batch_size(inputs, batch_size)
         sizes = self._mb_sizes(batch)
         stats = torch.zeros(3, dtype=torch.float64, device=self.device)
         tgt = None
@@ -531,9 +578,8 @@ class Pipeline:
                 self.comm.send(stats, 0)
             elif self.is_first:
                 self.comm.recv(stats, self.world - 1)
-                self.comm.synchronize()
+                self.comm.wait()
         if self.is_first:
-            s = stats.tolist()
-            return StepResult(s[0], 100.0 * s[1] / batch, 100.0 * s[2] / batch)
+            return StepResult(stats=stats, batch=batch)
         return StepResult(None, None, None)
 

@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from ..comm.rccl import Communicator
 from ..ops.batchnorm import BatchNormAct2d
+from ..utils.env import single_rank_comm
 
 # One communicator per (device, group) shared by every SyncBatchNorm layer and
 # never by DDP: the moment all-reduces are enqueued on the COMPUTE stream, the
@@ -58,8 +59,8 @@ class SyncBatchNorm(BatchNormAct2d):
     def _moment_reducers(self):
         if not (dist.is_available() and dist.is_initialized()):
             return None, None
-        if dist.get_world_size(self.process_group) == 1:
-            return None, None
+        if dist.get_world_size(self.process_group) == 1 and not single_rank_comm():
+            return None, None  # the all-reduce of one rank's moments is the identity
         dev = self.weight.device if self.weight is not None else self.running_mean.device
         comm = self._communicator(dev)
 

@@ -226,30 +226,40 @@ def run_pipeline(args, env) -> None:
         _, train_loader, val_loader = prepare_dataloaders(train_ds, val_ds, args.batch_size, args.workers,
                                                           pin_memory=env.device.type == "cuda")
         n_train, n_val = len(train_loader), len(val_loader)
+        vbs = val_loader.batch_size or args.batch_size
+
+        def _last(n_items: int, bs: int, drop: bool) -> int:
+            return bs if (drop or n_items % bs == 0) else n_items % bs
+        last_t = _last(len(train_ds), args.batch_size, bool(getattr(train_loader, "drop_last", False)))
+        last_v = _last(len(val_ds), vbs, bool(getattr(val_loader, "drop_last", False)))
     else:
         train_loader = val_loader = None
-        n_train = n_val = 0
-    # only rank 0 loads data; the others learn the iteration counts (defect 6)
-    counts = torch.tensor([n_train, n_val], dtype=torch.int64, device=env.device)
+        n_train = n_val = last_t = last_v = vbs = 0
+    # only rank 0 loads data; the others learn the iteration counts and batch
+    # sizes once (defect 6), so no step needs a batch-size message or host sync
+    counts = torch.tensor([n_train, n_val, last_t, last_v, vbs], dtype=torch.int64, device=env.device)
     comm.broadcast(counts, 0)
     comm.synchronize()
-    n_train, n_val = (int(v) for v in counts.tolist())
+    n_train, n_val, last_t, last_v, vbs = (int(v) for v in counts.tolist())
+    n_train_all, n_val_all = n_train, n_val
     if args.steps_per_epoch:
         n_train, n_val = min(n_train, args.steps_per_epoch), min(n_val, args.steps_per_epoch)
     timer = StepTimer(env.device)
     for epoch in range(args.epochs):
         it = iter(train_loader) if train_loader is not None else None
-        loss_s, acc_s = 0.0, 0.0
+        sums = []  # per-step device stats, read once per epoch
         for i in range(n_train):
             with timer.region("data"):
                 x, y = next(it) if it is not None else (None, None)
+            bs = last_t if i == n_train_all - 1 else args.batch_size
             with timer.region("step"), trace_range("pipe.train_step"):
-                r = pipe.train_step(x, y)
+                r = pipe.train_step(x, y, batch_size=bs)
                 opt.step()
                 opt.zero_grad()
-            if r.loss is not None:
-                loss_s += r.loss
-                acc_s += r.top1
+            if r.valid:
+                sums.append(r)
+        loss_s = sum(r.loss for r in sums)
+        acc_s = sum(r.top1 for r in sums)
         tm = timer.summary()
         tot_t = (tm.get("step", 0.0) + tm.get("data_host", 0.0)) / 1e3 * max(n_train, 1)
         tot_d = tm.get("data_host", 0.0) / 1e3 * max(n_train, 1)
@@ -257,8 +267,8 @@ def run_pipeline(args, env) -> None:
         vl, va = 0.0, 0.0
         for i in range(n_val):
             x, y = next(vit) if vit is not None else (None, None)
-            r = pipe.eval_step(x, y)
-            if r.loss is not None:
+            r = pipe.eval_step(x, y, batch_size=last_v if i == n_val_all - 1 else vbs)
+            if r.valid:
                 vl += r.loss
                 va += r.top1
         sched.step()

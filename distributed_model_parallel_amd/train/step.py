@@ -33,6 +33,9 @@ class StepConfig:
     bucket_cap_mb: float = 25.0
     first_bucket_mb: float = 1.0
     dp_devices: int = 1             # parallel == "dp": GPUs driven by the single process
+    dp_replicas: int = 1            # parallel == "dp": replicas per GPU (>1 aliases several
+                                    # replicas onto one device, so scatter / replicate /
+                                    # parallel_apply / gather / reduce-add all run on 1 GPU)
     graph: bool = False             # capture the whole step in a hipGraph (constant LR, static data)
     lr: float = 0.1
     momentum: float = 0.9
@@ -130,7 +133,9 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
         # fp32 master weights + momentum, one launch per dtype group (same update as DDP's FlatSGD)
         opt = MasterSGD(model.parameters(), lr=cfg.lr, momentum=cfg.momentum,
                         weight_decay=cfg.weight_decay)
-        wrapped = DataParallel(model, device_ids=list(range(ndp)) if device.type == "cuda" else None)
+        reps = max(1, cfg.dp_replicas)
+        wrapped = DataParallel(model, device_ids=[d for d in range(ndp) for _ in range(reps)]
+                               if device.type == "cuda" else None)
 
         def step() -> torch.Tensor:
             out = wrapped(x)
@@ -179,7 +184,8 @@ def build_pipeline_state(cfg: StepConfig, device: torch.device) -> TrainState:
     comm = default_communicator(device)
     pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=cfg.micro_batches,
                     schedule=cfg.schedule, device=device, dtype=cfg.dtype,
-                    channels_last=cfg.channels_last, partition=cfg.partition)
+                    channels_last=cfg.channels_last, partition=cfg.partition,
+                    static_batch=cfg.batch_size)  # every rank knows it: no per-step size message
     opt = MasterSGD(pipe.module.parameters(), lr=cfg.lr, momentum=cfg.momentum,
                     weight_decay=cfg.weight_decay)
     x, y = synthetic_batch(cfg, device) if pipe.is_first else (None, None)
@@ -189,6 +195,7 @@ def build_pipeline_state(cfg: StepConfig, device: torch.device) -> TrainState:
         r = pipe.train_step(x, y)
         opt.step()
         opt.zero_grad()
-        return torch.tensor(r.loss) if r.loss is not None else zero
+        lt = r.loss_tensor if r.valid else None  # device tensor: no host sync per step
+        return lt if lt is not None else zero
 
     return TrainState(cfg, pipe.module, pipe, opt, step, x, y)

@@ -16,7 +16,9 @@ from rank 0 so every replica resumes bit-identical.
 from __future__ import annotations
 
 import os
+import pickle
 import random
+import warnings
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -53,7 +55,9 @@ def rng_state() -> Dict[str, Any]:
 def set_rng_state(st: Dict[str, Any]) -> None:
     random.setstate(st["python"])
     name, keys, pos, has_gauss, gauss = st["numpy"]
-    np.random.set_state((name, keys.numpy().astype(np.uint32), pos, has_gauss, gauss))
+    # current format: keys as an int64 tensor; legacy files: np.random.get_state()'s ndarray
+    keys = keys.numpy() if isinstance(keys, torch.Tensor) else np.asarray(keys)
+    np.random.set_state((name, keys.astype(np.uint32), int(pos), int(has_gauss), float(gauss)))
     torch.set_rng_state(st["torch"])
     if "cuda" in st and torch.cuda.is_available():
         torch.cuda.set_rng_state_all(st["cuda"])
@@ -102,12 +106,20 @@ def load_checkpoint(path: str, model: nn.Module, optimizer=None, scheduler=None,
     ``{'net','acc','epoch'}`` dict) into `model` / `optimizer` / `scheduler`."""
     if map_location is None:
         map_location = "cpu"
-    # tensors / containers / numbers only: nothing in the file is executed
-    state = torch.load(path, map_location=map_location, weights_only=True)
+    state = _load_weights_only(path, map_location)
     target = unwrap(model)
     target.load_state_dict(_strip_prefix(state["net"]), strict=strict)
+    restored = False
     if optimizer is not None and state.get("optimizer") is not None:
-        optimizer.load_state_dict(state["optimizer"])
+        try:
+            optimizer.load_state_dict(state["optimizer"])
+            restored = True
+        except (KeyError, ValueError) as e:  # e.g. a torch.optim.SGD state from an older DP run
+            warnings.warn(f"load_checkpoint: optimizer state not restored ({e}); starting it fresh "
+                          "from the loaded weights")
+    if optimizer is not None and not restored and hasattr(optimizer, "sync_from_params"):
+        # weights came without (usable) optimizer state: the fp32 masters must follow them
+        optimizer.sync_from_params()
     if scheduler is not None and state.get("scheduler") is not None:
         scheduler.load_state_dict(state["scheduler"])
     if restore_rng and state.get("rng") is not None:
@@ -119,6 +131,27 @@ def load_checkpoint(path: str, model: nn.Module, optimizer=None, scheduler=None,
     if ddp is not None and ddp.world_size > 1:
         ddp._sync_module_states()
     return {"epoch": state.get("epoch", 0), "acc": state.get("acc", 0.0), "extra": state.get("extra", {})}
+
+
+def _load_weights_only(path: str, map_location):
+    """``torch.load(weights_only=True)``: tensors / containers / numbers only,
+    nothing in the file is executed.  Files written before the RNG state became
+    tensor-only pickle ``np.random.get_state()``'s uint32 ndarray; for those the
+    numpy array *reconstructors* (plain data constructors, no code) are
+    allow-listed and the load retried, still weights-only."""
+    try:
+        return torch.load(path, map_location=map_location, weights_only=True)
+    except pickle.UnpicklingError:
+        allowed = [np.ndarray, np.dtype]
+        try:
+            from numpy.core.multiarray import _reconstruct  # numpy >= 2 keeps this alias
+            allowed.append(_reconstruct)
+        except ImportError:  # pragma: no cover
+            pass
+        allowed.extend(t for t in (getattr(np, "dtypes", None) and getattr(np.dtypes, "UInt32DType", None),)
+                       if t is not None)
+        with torch.serialization.safe_globals(allowed):
+            return torch.load(path, map_location=map_location, weights_only=True)
 
 
 def stage_checkpoint_path(path: str, stage: int) -> str:

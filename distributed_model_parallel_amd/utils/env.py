@@ -43,6 +43,38 @@ def env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
+def single_rank_comm() -> bool:
+    """Run the collectives even at world size 1 (measurement mode: the DDP
+    bucket all-reduces and the SyncBN moment all-reduces then really go through
+    RCCL instead of being skipped as identities).  ``DMP_SINGLE_RANK_COMM=1``;
+    the round-2 name ``DMP_DDP_SINGLE_RANK_COMM=1`` is still honoured."""
+    return os.environ.get("DMP_SINGLE_RANK_COMM", os.environ.get("DMP_DDP_SINGLE_RANK_COMM", "0")) == "1"
+
+
+def count_gpus_without_hip() -> Optional[int]:
+    """Number of visible GPUs, read WITHOUT initialising the HIP runtime (for
+    launcher processes that must stay GPU-free): the *_VISIBLE_DEVICES lists
+    when set, else the KFD topology nodes that have SIMDs.  None = unknown
+    (let the ranks validate)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() != ""])
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        n = 0
+        for node in os.listdir(root):
+            with open(os.path.join(root, node, "properties")) as f:
+                for line in f:
+                    k, _, val = line.partition(" ")
+                    if k == "simd_count" and int(val) > 0:
+                        n += 1
+                        break
+        return n
+    except (OSError, ValueError):
+        return None
+
+
 def read_env() -> DistEnv:
     rank = env_int("RANK", 0)
     ws = env_int("WORLD_SIZE", 1)

@@ -100,3 +100,53 @@ def torch_profile(path: Optional[str] = None, cuda: bool = True, row_limit: int 
     print(prof.key_averages().table(sort_by=key, row_limit=row_limit))
     if path:
         prof.export_chrome_trace(path)
+
+
+# --------------------------------------------------------------------------- #
+# Per-phase GPU time (bench.py --phase-times): HIP events recorded on the
+# current stream around each named phase, summed per name.  Off by default
+# (no events, no syncs); the roctx range is emitted either way.
+_PHASES = None  # name -> list of (start_event, end_event)
+
+
+def enable_phase_timing(on: bool = True) -> None:
+    global _PHASES
+    _PHASES = {} if on else None
+
+
+@contextlib.contextmanager
+def phase(name: str) -> Iterator[None]:
+    """roctx range + (when enabled) a start/end HIP event pair on the current stream."""
+    if _PHASES is None:
+        with trace_range(name):
+            yield
+        return
+    import torch
+    if not torch.cuda.is_available():
+        with trace_range(name):
+            yield
+        return
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    with trace_range(name):
+        a.record()
+        try:
+            yield
+        finally:
+            b.record()
+    _PHASES.setdefault(name, []).append((a, b))
+
+
+def phase_summary(reset: bool = True) -> dict:
+    """{name: {"ms": total GPU ms, "calls": n}} over everything since the last reset
+    (synchronises the device)."""
+    global _PHASES
+    if not _PHASES:
+        return {}
+    import torch
+    torch.cuda.synchronize()
+    out = {k: {"ms": round(sum(a.elapsed_time(b) for a, b in v), 3), "calls": len(v)}
+           for k, v in _PHASES.items()}
+    if reset:
+        _PHASES = {}
+    return out

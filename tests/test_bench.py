@@ -37,3 +37,30 @@ def test_bench_pipe_two_stages():
     assert res["config"]["global_batch"] == 8 and res["scaling"] == "strong"
     assert len(res["config"]["stage_partition"]) == 2
     assert res["ms_per_step"] > 0
+
+
+def test_bench_syncbn_four_ranks():
+    """DDP + SyncBatchNorm through bench.py on 4 gloo ranks: the moment
+    all-reduces run across ranks (rehearse more ranks on CPU)."""
+    res = _run("--gpus", "4", "--parallel", "syncbn", "--model", "resnet18", "--batch-size", "2",
+               "--image-size", "32")
+    assert res["n_gpus"] == 4 and res["config"]["ranks"] == 4
+    assert res["config"]["sync_bn"] is True and res["config"]["parallelism"] == "ddp-syncbn4"
+    assert res["config"]["global_batch"] == 8
+
+
+def test_bench_pipe_reference_four_way_naive():
+    """The reference's own experiment: MobileNetV2 cut 4 ways exactly as
+    model_parallel.py:103,129,144 does, naive (one batch, serial ring) schedule."""
+    res = _run("--gpus", "4", "--parallel", "pipe", "--model", "mobilenetv2", "--batch-size", "8",
+               "--micro-batches", "1", "--schedule", "naive", "--partition", "reference")
+    assert res["n_gpus"] == 4 and res["config"]["parallelism"] == "pipe4"
+    assert res["config"]["schedule"] == "naive" and len(res["config"]["stage_partition"]) == 4
+    assert res["ms_per_step"] > 0
+
+
+def test_bench_ddp_label_and_single_rank_comm_flag():
+    res = _run("--model", "resnet18", "--batch-size", "2", "--image-size", "32", "--single-rank-comm")
+    assert res["config"]["parallelism"] == "ddp1" and res["config"]["single_rank_comm"] is True
+    # at world size 1 the forced path goes through the process-group backend on CPU
+    assert res["config"]["grad_comm"] == "process_group"

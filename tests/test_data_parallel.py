@@ -184,3 +184,21 @@ def test_dp_distinct_devices_peer_path():
     torch.testing.assert_close(out, ref(x), atol=1e-5, rtol=1e-5)
     for (n, p), q in zip(m.named_parameters(), ref.parameters()):
         torch.testing.assert_close(p.grad, q.grad, atol=1e-5, rtol=1e-4, msg=n)
+
+
+def test_peer_routing_decision():
+    """pairs without hipDeviceCanAccessPeer must never get a
+    peer-pointer kernel; comm_ops routes them through a staged copy."""
+    from distributed_model_parallel_amd.parallel import comm_ops
+    d = [torch.device("cuda", i) for i in range(3)]
+    try:
+        comm_ops.set_peer_matrix(None)
+        assert comm_ops.peer_ok(d[0], d[0])            # same device: always direct
+        assert not comm_ops.peer_ok(d[0], d[1])        # unknown matrix: never assume peer access
+        comm_ops.set_peer_matrix([[True, True, False], [True, True, True], [False, True, True]])
+        assert comm_ops.peer_ok(d[0], d[1]) and comm_ops.peer_ok(d[1], d[2])
+        assert not comm_ops.peer_ok(d[0], d[2]) and not comm_ops.peer_ok(d[2], d[0])
+        assert not comm_ops.peer_ok(d[0], torch.device("cuda", 7))  # outside the matrix
+        assert not comm_ops.peer_ok(torch.device("cpu"), d[0])
+    finally:
+        comm_ops.set_peer_matrix(None)

@@ -208,3 +208,48 @@ def test_flat_sgd_resume_across_bucket_rebuild(tmp_path):
     assert res["changed"], "test must exercise a layout change between save and resume"
     for k, v in res["want"].items():
         torch.testing.assert_close(res["got"][k], v, atol=1e-6, rtol=1e-6, msg=k)
+
+
+class _Branches(nn.Module):
+    """Four parallel branches; the order they run in (hence the autograd
+    ready order of their parameters) depends on the rank."""
+
+    def __init__(self, rank):
+        super().__init__()
+        torch.manual_seed(0)
+        self.br = nn.ModuleList(nn.Linear(64, 64) for _ in range(4))
+        self.head = nn.Linear(64, 3)
+        self.perm = [(3 - i + rank) % 4 for i in range(4)]
+
+    def forward(self, x):
+        out = 0
+        for i in self.perm:
+            out = out + torch.tanh(self.br[i](x))
+        return self.head(out)
+
+
+def _rebuild_worker(rank, world):
+    from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
+    m = _Branches(rank)
+    # ~17 KB per branch: a 20 KB cap gives several buckets
+    ddp = DistributedDataParallel(m, bucket_cap_mb=0.02, first_bucket_mb=0.02)
+    g = torch.Generator().manual_seed(rank)
+    before = [list(b) for b in ddp.reducer.buckets()]
+    for _ in range(3):
+        x = torch.randn(4, 64, generator=g)
+        F.cross_entropy(ddp(x), torch.randint(0, 3, (4,), generator=g)).backward()
+        ddp.zero_grad()
+    return {"before": before, "after": [list(b) for b in ddp.reducer.buckets()],
+            "ready": list(ddp.reducer.ready_order())}
+
+
+def test_bucket_rebuild_identical_on_eight_ranks():
+    """after the first iteration every rank adopts rank 0's
+    autograd ready order, so the rebuilt buckets (and the order RCCL bucket
+    collectives are launched in) are identical on all 8 ranks even when the
+    ranks observe different ready orders."""
+    res = run_world(_rebuild_worker, 8)
+    after = [r["after"] for r in res]
+    assert all(a == after[0] for a in after), after
+    assert after[0] != res[0]["before"]                     # a rebuild happened
+    assert len({tuple(r["ready"]) for r in res}) > 1        # ranks really saw different orders

@@ -27,3 +27,16 @@ def test_cross_entropy_matches_torch(dtype, B, C):
     tol = 1e-6 if dtype == torch.float32 else 2e-3
     torch.testing.assert_close(xa.grad.float(), xr.grad, atol=tol, rtol=1e-2)
     assert xa.grad.dtype == dtype
+
+
+@pytest.mark.parametrize("bad", [10, 12345, -3])
+def test_cross_entropy_out_of_range_label_is_nan_not_oob(bad):
+    """a label outside [0, C) must not read past the row (the fused
+    kernel replaces F.cross_entropy, which raises); it poisons loss and grad."""
+    x = torch.randn(8, 10, device="cuda", requires_grad=True)
+    t = torch.randint(0, 10, (8,), device="cuda")
+    t[3] = bad
+    loss = cross_entropy(x, t)
+    assert torch.isnan(loss).item()
+    loss.backward()
+    assert torch.isnan(x.grad[3]).all().item()

@@ -62,3 +62,66 @@ def test_master_sgd_adopts_replaced_grads_and_state_roundtrip():
     o2.load_state_dict(sd)
     torch.testing.assert_close(o2._groups[0]["momentum"], o._groups[0]["momentum"])
     assert o2._steps == 1
+
+
+def test_master_sgd_follows_weights_loaded_without_optimizer_state(tmp_path):
+    """a checkpoint carrying only 'net' (the reference's
+    {'net','acc','epoch'} format) loaded after MasterSGD exists must not be
+    overwritten by the construction-time fp32 master on the first step."""
+    from distributed_model_parallel_amd.utils.checkpoint import load_checkpoint
+    src = _net().to(torch.bfloat16)
+    with torch.no_grad():
+        for p in src.parameters():
+            p.add_(1.0)  # clearly different from _net()'s init
+    path = str(tmp_path / "ckpt.pth")
+    torch.save({"net": src.state_dict(), "acc": 50.0, "epoch": 3}, path)
+    dst = _net().to(torch.bfloat16)
+    opt = MasterSGD(dst.parameters(), lr=0.1, momentum=0.9, weight_decay=0.0)
+    meta = load_checkpoint(path, dst, opt, restore_rng=False)
+    assert meta["epoch"] == 3
+    opt.zero_grad()
+    opt.step()  # zero gradient, no weight decay: weights must stay the loaded ones
+    for (k, a), b in zip(src.state_dict().items(), dst.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+def test_master_sgd_rejects_foreign_optimizer_state(tmp_path):
+    """An older checkpoint holding a torch.optim.SGD state: warn, start fresh
+    from the loaded weights instead of raising KeyError('numels')."""
+    import warnings
+    from distributed_model_parallel_amd.utils.checkpoint import load_checkpoint
+    src = _net().to(torch.bfloat16)
+    with torch.no_grad():
+        for p in src.parameters():
+            p.mul_(0.5)
+    sgd = torch.optim.SGD(src.parameters(), lr=0.1, momentum=0.9)
+    path = str(tmp_path / "ckpt.pth")
+    torch.save({"net": src.state_dict(), "optimizer": sgd.state_dict(), "acc": 1.0, "epoch": 1}, path)
+    dst = _net().to(torch.bfloat16)
+    opt = MasterSGD(dst.parameters(), lr=0.1, momentum=0.0, weight_decay=0.0)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        load_checkpoint(path, dst, opt, restore_rng=False)
+    assert any("optimizer state not restored" in str(x.message) for x in w)
+    opt.zero_grad()
+    opt.step()
+    for a, b in zip(src.state_dict().values(), dst.state_dict().values()):
+        assert torch.equal(a, b)
+
+
+def test_checkpoint_with_legacy_numpy_rng_state_loads(tmp_path):
+    """files whose RNG entry is np.random.get_state() (an
+    ndarray) still load weights-only, and the numpy RNG is restored."""
+    import numpy as np
+    from distributed_model_parallel_amd.utils.checkpoint import load_checkpoint
+    net = _net()
+    np.random.seed(7)
+    legacy = np.random.get_state()
+    expect = np.random.rand(3)
+    path = str(tmp_path / "legacy.pth")
+    import random
+    torch.save({"net": net.state_dict(), "acc": 0.0, "epoch": 0,
+                "rng": {"python": random.getstate(), "numpy": legacy, "torch": torch.get_rng_state()}}, path)
+    np.random.seed(99)
+    load_checkpoint(path, _net(), restore_rng=True)
+    assert np.allclose(np.random.rand(3), expect)

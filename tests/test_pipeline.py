@@ -145,3 +145,31 @@ def test_pipeline_dynamic_last_batch(world, partition):
         for i, gs in r["grads"].items():
             for g, rg in zip(gs, ref_grads[i]):
                 torch.testing.assert_close(g, rg, atol=1e-4, rtol=1e-3)
+
+
+def _static_batch_worker(rank, world):
+    from distributed_model_parallel_amd.comm.rccl import Communicator
+    from distributed_model_parallel_amd.parallel.pipeline import Pipeline
+    atoms = _mlp_atoms()
+    comm = Communicator(torch.device("cpu"))
+    pipe = Pipeline(atoms, comm, (3, 4, 4), micro_batches=2, schedule="1f1b", static_batch=6)
+    x, y = _data("mlp", 6)
+    r1 = pipe.train_step(x if rank == 0 else None, y if rank == 0 else None)  # static: no size message
+    # a ragged batch must be passed explicitly on every rank
+    r2 = pipe.train_step(x[:5] if rank == 0 else None, y[:5] if rank == 0 else None, batch_size=5)
+    err = None
+    if rank == 0:
+        try:
+            pipe._batch_size(x[:4])
+        except ValueError as e:
+            err = str(e)
+    return {"l1": r1.loss if r1.valid else None, "l2": r2.loss if r2.valid else None, "err": err}
+
+
+def test_pipeline_static_batch_contract():
+    """the batch size is part of the static contract (no
+    per-step message / host sync); rank 0 refuses a batch that breaks it."""
+    res = run_world(_static_batch_worker, 2)
+    assert res[0]["l1"] is not None and res[0]["l2"] is not None
+    assert abs(res[1]["l1"] - res[0]["l1"]) < 1e-6  # the last stage holds the same loss
+    assert "contract is 6" in res[0]["err"]
