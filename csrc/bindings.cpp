@@ -107,6 +107,9 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
+at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x);
+bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W);
+void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
@@ -234,6 +237,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(),
         "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues");
+  m.def("wgrad3x3", &dmp::wgrad3x3, py::arg("dy"), py::arg("x"),
+        "dW [C, C, 3, 3] (channels_last) of a 3x3/s1/p1 conv: persistent halo-tiled MFMA kernel");
+  m.def("wgrad3x3_supported", &dmp::wgrad3x3_supported);
+  m.def("set_wgrad3x3_waves", &dmp::set_wgrad3x3_waves);
   m.def("conv3x3_c64", &dmp::conv3x3_c64, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
         "3x3/s1/p1 64->64-channel conv (W = 56) on the persistent halo-tiled MFMA kernel; "
         "returns (y [N*H*W, 64], fp64 moments [129] or empty)");

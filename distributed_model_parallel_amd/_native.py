@@ -8,6 +8,7 @@ are used for the math, while the C++ Reducer still runs if ``_C`` imports.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 from types import ModuleType
@@ -68,11 +69,32 @@ def require(what: str = "this operation") -> ModuleType:
     return m
 
 
+_REFERENCE = False
+
+
+@contextlib.contextmanager
+def reference_mode():
+    """Test oracle only: inside this block every op takes its stock-PyTorch
+    path (F.conv2d / F.batch_norm / F.linear ...) even on GPU tensors, so the
+    SAME model object can be trained as a plain-PyTorch reference on the same
+    device (tests/test_gpu_convergence.py).  Not thread-safe; never used by
+    the framework itself."""
+    global _REFERENCE
+    prev, _REFERENCE = _REFERENCE, True
+    try:
+        yield
+    finally:
+        _REFERENCE = prev
+
+
 def gpu_path(t: torch.Tensor) -> bool:
     """True when `t` should take the HIP path: it lives on a GPU.
 
-    GPU tensors never fall back: if the extension is missing this raises.
+    GPU tensors never fall back: if the extension is missing this raises
+    (``reference_mode`` aside).
     """
+    if _REFERENCE:
+        return False
     if t.is_cuda:
         require(f"GPU op on {t.device}")
         return True

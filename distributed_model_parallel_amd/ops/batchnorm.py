@@ -326,7 +326,7 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
     [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode.
     `num_batches_tracked`: incremented once (training mode), in-kernel when native."""
     slot = None
-    if training and relu and x.dim() == 4 and torch.is_grad_enabled() and _FUSE_BWD and x.is_cuda:
+    if training and relu and x.dim() == 4 and torch.is_grad_enabled() and _FUSE_BWD and _native.gpu_path(x):
         slot = BnBwdSlot()
     out = _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
                                 momentum, eps, relu, reduce_moments, reduce_grads, sums,

@@ -80,6 +80,18 @@ def _halo_ok(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, wdt: 
         and wdt == 56
 
 
+# Weight gradients of the stride-1 3x3s (every ResNet-50 stage) on the
+# persistent halo-tiled kernel: dW in registers, dy / x halo tiles streamed
+# through LDS (csrc/conv/wgrad3x3.hip).  Batch 2048 on MI355X
+# (tools/wgrad_bench.py): 0.45-0.52 ms vs MIOpen's igemm_wrw 0.62-1.18 ms.
+_STATS["halo_wgrad"] = 0
+
+
+def _halo_wgrad_ok(C, cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, h: int, w: int) -> bool:
+    return (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin == cout and h == w
+            and C.wgrad3x3_supported(cin, h, w))
+
+
 def _miopen_fwd(cout: int, kh: int) -> bool:
     return _FWD_MODE == "auto" and kh > 1 and not (_XL3 and cout >= 256)
 
@@ -125,7 +137,14 @@ class _ConvIGFn(torch.autograd.Function):
         cout, _, kh, kw = weight.shape
         ho, wo = _out_size(h, kh, stride, pad), _out_size(w, kw, stride, pad)
         mode = "moments" if moments else "store"
-        if _halo_ok(cin, cout, kh, kw, stride, pad, w):
+        y4 = None
+        if moments is None:
+            # MIOpen forward (layers whose native forward loses, finding 27); the
+            # backward below still takes our kernels where they win (the halo
+            # weight gradient of every stride-1 3x3)
+            y4 = F.conv2d(x, weight, None, stride, pad)
+            y2, mom = None, None
+        elif _halo_ok(cin, cout, kh, kw, stride, pad, w):
             _STATS["halo_fwd"] += 1
             y2, mom = C.conv3x3_c64(x, _wmat(weight).contiguous(), moments)
             if not moments:
@@ -150,6 +169,8 @@ class _ConvIGFn(torch.autograd.Function):
         # the moments output never gets a gradient: do not let autograd build a
         # zero [2C+1] fp64 tensor for it every backward (one fill launch per layer)
         ctx.set_materialize_grads(False)
+        if y4 is not None:
+            return y4, mom
         return y2.view(n, ho, wo, cout).permute(0, 3, 1, 2), mom
 
     @staticmethod
@@ -184,10 +205,16 @@ class _ConvIGFn(torch.autograd.Function):
             else:
                 dx2, _ = C.conv_xl(dy, wfl, kh, kw, 1, kh - 1 - pad, h, w, "store")
                 dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1] and _halo_wgrad_ok(C, cin, cout, kh, kw, stride, pad, h, w):
+            # persistent halo-tiled MFMA weight gradient (csrc/conv/wgrad3x3.hip)
+            _STATS["halo_wgrad"] += 1
+            dw = C.wgrad3x3(dy, x)
+            if not weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous()
         nat_d = ctx.needs_input_grad[0] and dx is None and _use_native("dgrad", cin, h, stride)
-        nat_w = ctx.needs_input_grad[1] and _use_native("wgrad", cin, h, stride)
+        nat_w = ctx.needs_input_grad[1] and dw is None and _use_native("wgrad", cin, h, stride)
         want_d = ctx.needs_input_grad[0] and not nat_d and dx is None
-        want_w = ctx.needs_input_grad[1] and not nat_w
+        want_w = ctx.needs_input_grad[1] and not nat_w and dw is None
         if want_d or want_w:
             dx_l, dw, _ = torch.ops.aten.convolution_backward(
                 dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
@@ -214,6 +241,12 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
     if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]) and not \
             _halo_ok(x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[3]):
         _STATS["miopen_fwd"] += 1
+        if torch.is_grad_enabled() and weight.requires_grad and _halo_wgrad_ok(
+                _native.native(), x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding,
+                x.shape[2], x.shape[3]):
+            # MIOpen forward inside our Function so the backward can use the halo wgrad
+            y, _ = _ConvIGFn.apply(x, weight, stride, padding, None, None)
+            return y, None
         return F.conv2d(x, weight, None, stride, padding, dilation, groups), None
     if _native_ok(x, weight, groups, dilation):
         _STATS["native"] += 1

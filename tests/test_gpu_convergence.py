@@ -1,0 +1,145 @@
+"""Convergence regression of the whole native training path.
+
+The reference's only correctness claim is accuracy (MobileNetV2 CIFAR-10:
+MP 93.3 % / DP 93.8 %, reference Readme.md:283-286, loop in
+data_parallel.py:99-156).  CIFAR-10 is not available offline, so that number
+stays unpinned; what IS checked here, on a fixed learnable synthetic task
+(class-conditional templates + noise, CIFAR-shaped), is that the native stack
+-- bf16 weights/activations, channels-last, fused BN forward/backward
+(BnBwdSlot hand-offs, compact shortcut, stem-pool fusion), MFMA conv kernels,
+halo 3x3 kernels, fused cross-entropy, the C++ DDP reducer and FlatSGD with
+fp32 masters -- TRAINS like stock PyTorch: the same model object, the same
+initial weights and the same batches, trained once natively and once in
+``_native.reference_mode()`` (stock F.conv2d / F.batch_norm / torch SGD in
+fp32).  The loss curves must stay inside a band and both runs must learn the
+task.  Set DMP_CONVERGENCE_OUT=<file.json> to dump the curves.
+"""
+import copy
+import json
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd import _native
+from distributed_model_parallel_amd.models import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _task(n_cls, shape, n, seed=0, noise=2.0):
+    g = torch.Generator().manual_seed(seed)
+    c, h, w = shape
+    # low-frequency class templates (upsampled 8x8 noise): learnable, not trivial
+    t = torch.randn(n_cls, c, 8, 8, generator=g)
+    t = F.interpolate(t, size=(h, w), mode="bilinear", align_corners=False)
+    t = t / t.std(dim=(1, 2, 3), keepdim=True)
+    y = torch.randint(0, n_cls, (n,), generator=g)
+    x = t[y] + noise * torch.randn(n, c, h, w, generator=g)
+    return x, y
+
+
+def _ensure_pg():
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+
+
+def _train_native(model, xs, ys, steps, batch, lr):
+    from distributed_model_parallel_amd.ops.loss import cross_entropy
+    from distributed_model_parallel_amd.ops.optim import FlatSGD
+    from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
+    from distributed_model_parallel_amd.utils.precision import cast_model
+    _ensure_pg()
+    m = model.cuda().to(memory_format=torch.channels_last)
+    cast_model(m, torch.bfloat16)
+    ddp = DistributedDataParallel(m, flat_parameters=True)
+    opt = FlatSGD(ddp, lr=lr, momentum=0.9, weight_decay=5e-4)
+    losses = []
+    for i in range(steps):
+        sl = slice((i * batch) % xs.shape[0], (i * batch) % xs.shape[0] + batch)
+        x = xs[sl].cuda().bfloat16().contiguous(memory_format=torch.channels_last)
+        y = ys[sl].cuda()
+        loss = cross_entropy(ddp(x), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(loss.detach().float())
+    return m, [float(v) for v in torch.stack(losses).cpu()]
+
+
+def _train_reference(model, xs, ys, steps, batch, lr):
+    m = model.cuda()
+    opt = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    losses = []
+    with _native.reference_mode():
+        for i in range(steps):
+            sl = slice((i * batch) % xs.shape[0], (i * batch) % xs.shape[0] + batch)
+            loss = F.cross_entropy(m(xs[sl].cuda()), ys[sl].cuda())
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.detach())
+    return m, [float(v) for v in torch.stack(losses).cpu()]
+
+
+@torch.no_grad()
+def _accuracy(m, x, y, native, batch=256):
+    m.eval()
+    ok = 0
+    ctx = _native.reference_mode() if not native else torch.no_grad()
+    with ctx:
+        for i in range(0, x.shape[0], batch):
+            xb = x[i:i + batch].cuda()
+            if native:
+                xb = xb.bfloat16().contiguous(memory_format=torch.channels_last)
+            ok += (m(xb).float().argmax(1).cpu() == y[i:i + batch]).sum().item()
+    m.train()
+    return 100.0 * ok / x.shape[0]
+
+
+def _mean(v):
+    return sum(v) / len(v)
+
+
+@pytest.mark.parametrize("arch,shape,ncls,steps,batch,lr", [
+    ("mobilenetv2", (3, 32, 32), 10, 240, 128, 0.05),
+    ("resnet50", (3, 64, 64), 10, 120, 128, 0.05),
+])
+def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, lr):
+    torch.manual_seed(0)
+    xs, ys = _task(ncls, shape, 8192, seed=1)
+    gv = torch.Generator().manual_seed(7)
+    base = build_model(arch, num_classes=ncls)
+    ref0 = copy.deepcopy(base)
+    nat, l_nat = _train_native(base, xs, ys, steps, batch, lr)
+    ref, l_ref = _train_reference(ref0, xs, ys, steps, batch, lr)
+    # held-out samples: the same class templates (seed 1), labels and noise re-drawn
+    xh, yh = _task(ncls, shape, 9216, seed=1)
+    xh, yh = xh[8192:], yh[8192:]
+    xh = xh + 0.25 * torch.randn(xh.shape, generator=gv)
+    acc_nat, acc_ref = _accuracy(nat, xh, yh, True), _accuracy(ref, xh, yh, False)
+    out = os.environ.get("DMP_CONVERGENCE_OUT")
+    if out:
+        rec = {}
+        if os.path.exists(out):
+            with open(out) as f:
+                rec = json.load(f)
+        rec[arch] = {"native_bf16": l_nat, "stock_fp32": l_ref, "acc_native": acc_nat, "acc_stock": acc_ref,
+                     "steps": steps, "batch": batch, "lr": lr, "shape": list(shape)}
+        with open(out, "w") as f:
+            json.dump(rec, f)
+    k = max(10, steps // 6)
+    # both learn the task (chance = 10 %)
+    assert _mean(l_nat[-k:]) < 0.5 * _mean(l_nat[:k]), (l_nat[:5], l_nat[-5:])
+    assert acc_ref > 80.0 and acc_nat > 80.0, (acc_nat, acc_ref)
+    assert acc_nat > acc_ref - 10.0, (acc_nat, acc_ref)
+    # the curves stay in a band: windowed means within 25 % (+0.05 absolute) of the stock run
+    for w0 in range(0, steps - k + 1, k):
+        a, b = _mean(l_nat[w0:w0 + k]), _mean(l_ref[w0:w0 + k])
+        assert abs(a - b) <= 0.25 * b + 0.05, (w0, a, b)

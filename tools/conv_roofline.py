@@ -75,8 +75,8 @@ def main():
     tot = {"fwd": [0.0, 0.0], "dgrad": [0.0, 0.0], "wgrad": [0.0, 0.0]}  # best, floor
     print(f"ResNet-50 convolutions, batch {B}, ms per call (HIP events); floor = max(FLOP/{PEAK_FLOPS/1e15:.1f} PF/s, "
           f"bytes/{PEAK_BYTES/1e12:.0f} TB/s)\n")
-    print("| conv | x | pass | ours | xl | MIOpen | hipBLASLt | floor | best/floor | TF/s (best) |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
+    print("| conv | x | pass | ours | xl | halo | MIOpen | hipBLASLt | floor | best/floor | TF/s (best) |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|")
     for name, cin, cout, k, s, h, cnt in resnet50_convs():
         if only and not any(name.startswith(p) for p in only):
             continue
@@ -124,6 +124,8 @@ def main():
             wtr = w.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
             res["dgrad"]["ours"] = timeit(lambda: C.conv_nt(dy, wtr, k, k, s, pad, h, h, transposed=True))
             res["wgrad"]["ours"] = timeit(lambda: C.conv_wgrad(dy2, x, k, k, s, pad, ho, ho, dt))
+            if hasattr(C, "wgrad3x3") and k == 3 and s == 1 and cin == cout and C.wgrad3x3_supported(cin, ho, ho):
+                res["wgrad"]["halo"] = timeit(lambda: C.wgrad3x3(dy, x))
             if hasattr(C, "conv_wgrad_xl") and cin % 256 == 0:
                 res["wgrad"]["xl"] = timeit(lambda: C.conv_wgrad_xl(dy2, x, k, k, s, pad, ho, ho, dt))
             if hasattr(C, "conv_xl") and k > 1:  # 256x256 ping-pong implicit GEMM
@@ -148,7 +150,8 @@ def main():
             tot[p][0] += best * cnt
             tot[p][1] += floors[p] * cnt
             f = lambda k_: f"{r[k_]:.3f}" if k_ in r else "-"  # noqa: E731
-            print(f"| {name} | {cnt} | {p} | {f('ours')} | {f('xl')} | {f('miopen')} | {f('blaslt')} | {floors[p]:.3f} | "
+            print(f"| {name} | {cnt} | {p} | {f('ours')} | {f('xl')} | {f('halo')} | {f('miopen')} | {f('blaslt')} | "
+                  f"{floors[p]:.3f} | "
                   f"{best / floors[p]:.2f} | {flops / best / 1e9:.0f} |")
         del x, w, dy, x2, dy2
         torch.cuda.empty_cache()

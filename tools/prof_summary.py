@@ -18,7 +18,8 @@ CATS = [
     ("dmp fused SGD (ours)", ("sgd_flat",)),
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
     ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "split_reduce", "dw_fwd",
-                              "dw_dgrad", "dw_wgrad", "column_reduce", "conv3x3_c64", "gemm_tn_pp")),
+                              "dw_dgrad", "dw_wgrad", "column_reduce", "conv3x3_c64", "gemm_tn_pp",
+                              "wgrad3x3", "wgrad_reduce")),
     ("dmp attention (ours)", ("attn_fwd_kernel", "attn_bwd_kernel")),
     ("dmp LayerNorm (ours)", ("ln_fwd", "ln_bwd", "ln_col_reduce")),
     ("dmp linear side passes (ours)", ("colsum_kernel", "partial_colsum")),
