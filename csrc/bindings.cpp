@@ -108,6 +108,9 @@ at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType o
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x);
+bool stem_halo_supported(int64_t hs, int64_t ws, int64_t ho, int64_t wo);
+std::vector<at::Tensor> stem_halo_fwd(const at::Tensor& s, const at::Tensor& wm, int64_t ho, bool moments);
+at::Tensor stem_halo_wgrad(const at::Tensor& dy, const at::Tensor& s, int64_t ho, at::ScalarType out_dtype);
 bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
@@ -237,6 +240,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(),
         "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues");
+  m.def("stem_halo_supported", &dmp::stem_halo_supported);
+  m.def("stem_halo_fwd", &dmp::stem_halo_fwd, py::arg("s"), py::arg("wm"), py::arg("ho"), py::arg("moments") = false,
+        "ResNet stem (s2d 4x4 conv, 16 -> 64 ch, Wo = 112) forward: halo-tiled, weights in VGPRs");
+  m.def("stem_halo_wgrad", &dmp::stem_halo_wgrad, py::arg("dy"), py::arg("s"), py::arg("ho"), py::arg("out_dtype"),
+        "ResNet stem weight gradient [64, 256]: halo-tiled, dW in VGPRs");
   m.def("wgrad3x3", &dmp::wgrad3x3, py::arg("dy"), py::arg("x"),
         "dW [C, C, 3, 3] (channels_last) of a 3x3/s1/p1 conv: persistent halo-tiled MFMA kernel");
   m.def("wgrad3x3_supported", &dmp::wgrad3x3_supported);

@@ -86,6 +86,17 @@ __device__ __forceinline__ int halo_key(int q) { return (0x31165572u >> (4 * (q 
 // channel pair of chunks stays adjacent)
 __device__ __forceinline__ int stage_key(int p) { return ((p >> 2) & 3) << 1; }
 
+// LDS-DMA from inline asm (see wgrad3x3.hip): with the builtin, hipcc cannot
+// tell which LDS bytes a pending copy writes and drains it (vmcnt(0)) at the
+// next LDS access / __syncthreads -- here the epilogue's stage barrier waited
+// for the NEXT tile's halo every tile.  The explicit counted vmcnt + barrier
+// at the top of each tile is the only ordering the copies need.
+__device__ __forceinline__ void glds16(const void* g, char* lds) {
+  const uint32_t l = (uint32_t)(uintptr_t)(lptr_t)lds;
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+               :: "s"(__builtin_amdgcn_readfirstlane(l)), "v"(g) : "memory", "m0");
+}
+
 template <int N>
 __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -142,7 +153,7 @@ __device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf
     const bool ok = ((hs.xok >> i) & 1u) && hy >= rlo && hy < rhi;
     const void* src = ok ? (const void*)(base + (hs.pk[i] >> 3)) : (const void*)g_halo_zero;
     if (ins < G::DMA_INSTR)
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(buf + ins * 1024), 16, 0, 0);
+      glds16(src, buf + ins * 1024);
   }
 }
 

@@ -21,7 +21,11 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0}
+_STATS = {"native": 0, "torch": 0, "halo": 0}
+# 224-px inputs (Wo = 112): the persistent halo-tiled stem kernels
+# (csrc/conv/stem_halo.hip) instead of the generic row-tap implicit GEMM;
+# DMP_STEM_HALO=0 for A/B runs.
+_HALO = __import__("os").environ.get("DMP_STEM_HALO", "1") != "0"
 
 
 def stem_wmat(w: torch.Tensor) -> torch.Tensor:
@@ -41,9 +45,16 @@ class _StemFn(torch.autograd.Function):
         n, _, h, w = x.shape
         ho, wo = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1
         s = C.space_to_depth2(x, 3)                                # [n, 16, (h+7)//2, (w+7)//2]
-        y2, mom = C.conv_nt(s, wmat, 4, 1, 1, 0, ho, wo, mode="moments" if moments else "store", kc=64)
+        halo = _HALO and C.stem_halo_supported(s.shape[2], s.shape[3], ho, wo)
+        if halo:  # halo-tiled kernel, weights in VGPRs (csrc/conv/stem_halo.hip)
+            _STATS["halo"] += 1
+            y2, mom = C.stem_halo_fwd(s, wmat.contiguous(), ho, moments)
+            if not moments:
+                mom = None
+        else:
+            y2, mom = C.conv_nt(s, wmat, 4, 1, 1, 0, ho, wo, mode="moments" if moments else "store", kc=64)
         ctx.save_for_backward(s)
-        ctx.geo = (n, ho, wo, wmat.dtype)
+        ctx.geo = (n, ho, wo, wmat.dtype, halo)
         if mom is None:
             mom = torch.empty(0, device=x.device, dtype=torch.float64)
         ctx.mark_non_differentiable(mom)
@@ -55,10 +66,13 @@ class _StemFn(torch.autograd.Function):
         if dy is None:
             return None, None, None
         (s,) = ctx.saved_tensors
-        n, ho, wo, wdt = ctx.geo
+        n, ho, wo, wdt, halo = ctx.geo
         C = _native.require("stem conv backward")
         dy2 = dy.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(n * ho * wo, -1)
-        dw = C.conv_wgrad(dy2.to(s.dtype), s, 4, 1, 1, 0, ho, wo, wdt, kc=64)
+        if halo:
+            dw = C.stem_halo_wgrad(dy2.to(s.dtype), s, ho, wdt)
+        else:
+            dw = C.conv_wgrad(dy2.to(s.dtype), s, 4, 1, 1, 0, ho, wo, wdt, kc=64)
         return None, dw, None
 
 

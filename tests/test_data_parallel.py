@@ -202,3 +202,30 @@ def test_peer_routing_decision():
         assert not comm_ops.peer_ok(torch.device("cpu"), d[0])
     finally:
         comm_ops.set_peer_matrix(None)
+
+
+@pytest.mark.gpu
+def test_replica_skeletons_are_reused_and_follow_mode_and_structure():
+    """Replica module objects persist across forwards (only parameter/buffer
+    slots are rebound); .eval() reaches them; re-assigning a submodule rebuilds."""
+    m = Net().cuda()
+    dp = DataParallel(m, device_ids=[0, 0, 0])
+    x = torch.randn(6, 3, 8, 8, device="cuda")
+    r1 = dp.replicate(m, [0, 0, 0])
+    r2 = dp.replicate(m, [0, 0, 0])
+    assert r1[1] is r2[1] and r1[1].conv is r2[1].conv
+    assert all(torch.equal(a, b) for a, b in zip(r2[2].parameters(), m.parameters()))
+    for _ in range(2):  # two steps through the cached skeleton: grads still match one module
+        m.zero_grad()
+        F.cross_entropy(dp(x), torch.arange(6, device="cuda") % 5).backward()
+        g = [p.grad.clone() for p in m.parameters()]
+        m.zero_grad()
+        F.cross_entropy(m(x), torch.arange(6, device="cuda") % 5).backward()
+        for a, p in zip(g, m.parameters()):
+            torch.testing.assert_close(a, p.grad, atol=1e-5, rtol=1e-4)
+    m.eval()
+    assert not dp.replicate(m, [0, 0, 0])[1].training
+    m.train()
+    m.fc = nn.Linear(16, 5).cuda()
+    r3 = dp.replicate(m, [0, 0, 0])
+    assert r3[1].fc is not r2[1].fc and torch.equal(r3[1].fc.weight, m.fc.weight)

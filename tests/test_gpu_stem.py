@@ -100,3 +100,29 @@ def test_rowtap_stem_matches_conv2d(n, h, w, cout):
     yr.backward(g)
     err = (m.weight.grad.float() - wr.grad).norm() / wr.grad.norm()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("n", [1, 7, 40])
+def test_stem_halo_kernels_224(n):
+    """224-px stem on the halo-tiled kernels (csrc/conv/stem_halo.hip): forward +
+    moments and weight gradient vs fp32, several persistent tile ranges."""
+    torch.manual_seed(n)
+    m = StemConv2d(3, 64).cuda().bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(n, 3, 224, 224, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    h0 = _STATS["halo"]
+    y, mom = m.forward_with_moments(x)
+    assert _STATS["halo"] == h0 + 1, "halo stem did not run"
+    wr = m.weight.detach().float().requires_grad_()
+    yr = F.conv2d(x.float(), wr, None, 2, 3)
+    torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=2e-2)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, 64).double()
+    torch.testing.assert_close(mom[:64], yf.sum(0), atol=1e-2 * yf.shape[0] ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(mom[64:128], (yf * yf).sum(0), atol=1e-2 * yf.shape[0] ** 0.5, rtol=1e-3)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    err = (m.weight.grad.float() - wr.grad).norm() / wr.grad.norm()
+    assert err < 1e-2, err
+    # no-moments forward path too
+    y2 = m(x)
+    assert torch.equal(y2, y)
