@@ -107,11 +107,11 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
-at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x);
+at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride);
 bool stem_halo_supported(int64_t hs, int64_t ws, int64_t ho, int64_t wo);
 std::vector<at::Tensor> stem_halo_fwd(const at::Tensor& s, const at::Tensor& wm, int64_t ho, bool moments);
 at::Tensor stem_halo_wgrad(const at::Tensor& dy, const at::Tensor& s, int64_t ho, at::ScalarType out_dtype);
-bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W);
+bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
@@ -245,9 +245,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "ResNet stem (s2d 4x4 conv, 16 -> 64 ch, Wo = 112) forward: halo-tiled, weights in VGPRs");
   m.def("stem_halo_wgrad", &dmp::stem_halo_wgrad, py::arg("dy"), py::arg("s"), py::arg("ho"), py::arg("out_dtype"),
         "ResNet stem weight gradient [64, 256]: halo-tiled, dW in VGPRs");
-  m.def("wgrad3x3", &dmp::wgrad3x3, py::arg("dy"), py::arg("x"),
+  m.def("wgrad3x3", &dmp::wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("stride") = 1,
         "dW [C, C, 3, 3] (channels_last) of a 3x3/s1/p1 conv: persistent halo-tiled MFMA kernel");
-  m.def("wgrad3x3_supported", &dmp::wgrad3x3_supported);
+  m.def("wgrad3x3_supported", &dmp::wgrad3x3_supported, py::arg("C"), py::arg("Ho"), py::arg("Wo"),
+        py::arg("stride") = 1);
   m.def("set_wgrad3x3_waves", &dmp::set_wgrad3x3_waves);
   m.def("conv3x3_c64", &dmp::conv3x3_c64, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
         "3x3/s1/p1 64->64-channel conv (W = 56) on the persistent halo-tiled MFMA kernel; "

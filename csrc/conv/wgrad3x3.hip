@@ -53,8 +53,6 @@ using lds_v4 = __attribute__((address_space(3))) v4i16;
 using i16x8 = short __attribute__((ext_vector_type(8)));
 
 constexpr int kCh = 64;          // channels per slice (one 128-B LDS row per pixel)
-constexpr int kKSteps = 7;       // 32-pixel k-steps per tile (P_ALLOC = 224)
-constexpr int kPAlloc = 32 * kKSteps;
 constexpr int kWaves = 4;
 constexpr int kCols = 9 * kCh;   // 576 output columns (tap, ci) per slice
 constexpr int kWCols = kCols / kWaves;  // 144 per wave = 9 fragments of 16
@@ -63,24 +61,63 @@ constexpr int kMB = kCh / 16;           // 4 co fragments
 
 __device__ __attribute__((aligned(16))) uint32_t g_wg_zero[4];
 
-template <int W, int R, int IMGS, int NW>
+// Tile geometry for output width W, R output rows per tile, IMGS images per
+// tile (small maps), stride S (1 or 2; pad 1), KS 32-pixel k-steps per tile.
+// Halo of a tile = S*(R-1)+3 input rows x S*(W-1)+3 input columns per image;
+// for S = 2 each halo row stores its even columns first, then the odd ones,
+// so the pixels a tap reads for consecutive output columns stay consecutive
+// rows of the LDS image (stride-1 reads, same bank analysis as S = 1).
+template <int W, int R, int IMGS, int NW, int S, int KS>
 struct WgGeo {
-  static constexpr int HW2 = W + 2;
-  static constexpr int HIMG = (R + 2) * HW2;              // halo rows per image
+  static constexpr int HC = S * (W - 1) + 3;              // halo columns (LDS rows per halo row)
+  static constexpr int HR = S * (R - 1) + 3;              // halo rows per image
+  static constexpr int HIMG = HR * HC;                    // LDS rows per image
   static constexpr int HROWS = IMGS * HIMG;
   static constexpr int P = IMGS * R * W;                  // output pixels per full tile
+  static constexpr int PALLOC = 32 * KS;
   static constexpr int DY_INSTR = (P + 7) / 8;            // 1-KB DMA pieces = 8 rows of 128 B
   static constexpr int H_INSTR = (HROWS + 7) / 8;
   static constexpr int DY_PW = (DY_INSTR + NW - 1) / NW;  // pieces per wave
   static constexpr int H_PW = (H_INSTR + NW - 1) / NW;
-  static constexpr int DY_BYTES = kPAlloc * 128;          // rows >= P stay zero (set once)
+  static constexpr int DY_BYTES = PALLOC * 128;           // rows >= P stay zero (set once)
   static constexpr int BUF_BYTES = DY_BYTES + H_INSTR * 1024;
   static constexpr int SMEM = 2 * BUF_BYTES;
   static constexpr int MBW = kMB * kWaves / NW;           // co fragments per wave (4 or 2)
-  static_assert(P <= kPAlloc && P > kPAlloc - 32, "tile must fill 7 k-steps");
+  // chunk-swizzle key index: the skewed index (conflict-free at row / image
+  // crossings, see the hb / kt comment) where its parity matches the physical
+  // row's, else the physical row itself
+  static constexpr bool SKEW = S == 1 || (W % 2 == 0 && IMGS == 1);
+  static_assert(P <= PALLOC && P > PALLOC - 32, "tile must fill its k-steps");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(NW == 4 || NW == 8, "4 waves (64 co each) or 8 (32 co each, 2 per SIMD)");
+  static_assert(S == 1 || S == 2, "stride 1 or 2");
+  // LDS row of halo column hc inside a halo row
+  static constexpr __device__ __host__ int pos(int hc) { return S == 1 ? hc : ((hc & 1) ? (HC + 1) / 2 + (hc >> 1) : hc >> 1); }
+  // LDS row offset of tap (kh, kw) from the output pixel's tap-(0,0) row
+  static constexpr __device__ __host__ int tap_off(int kh, int kw) { return kh * HC + pos(kw); }
+  // key-index offset of tap (kh, kw) from the pixel's own key index
+  static constexpr __device__ __host__ int key_off(int kh, int kw) {
+    return !SKEW ? tap_off(kh, kw) : S == 1 ? kh * W + kw : (kh >> 1) * W + (kw >> 1) + (kh & 1) + (kw & 1);
+  }
+  // key index of halo row (img, hy, hc)
+  static constexpr __device__ __host__ int key_of(int img, int hy, int hc) {
+    return !SKEW ? img * HIMG + hy * HC + pos(hc)
+                 : S == 1 ? img * (R * W) + hy * W + hc : (hy >> 1) * W + (hc >> 1) + (hy & 1) + (hc & 1);
+  }
 };
+
+// step(integral_constant<int, 0>) ... step(integral_constant<int, N - 1>), in order
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_impl(F& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F& f) {
+  static_for_impl<0, N>(f);
+}
 
 __device__ __forceinline__ int wg_key(int row) { return ((row >> 1) & 3) << 1; }
 // nibble i = wg_key(i) for row residues i = 0..7
@@ -113,7 +150,8 @@ struct WgArgs {
   const bf16* dy;  // [N*H*W][C] (channels-last), C = co channel stride
   const bf16* x;   // [N*H*W][C]
   float* part;     // [S][NB][64][576]
-  int N, H, C;     // C = channels (in == out)
+  int N, H, C;     // H = output rows; C = channels (in == out)
+  int HI, WI;      // input rows / columns (stride 2: 2 H x 2 W)
   int S, NB;       // (co, ci) slice combos, blocks per combo
   int tiles, tiles_per_img;  // IMGS == 1: row tiles of R rows; IMGS > 1: image groups
 };
@@ -122,9 +160,9 @@ struct WgArgs {
 // NW = 8: two waves per SIMD (<= 256 registers each); wave w: co half (w >> 2),
 // the same 144 columns as wave (w & 3), so a SIMD's two waves can cover each
 // other's LDS-read, DMA-issue and barrier stalls.
-template <int W, int R, int IMGS, int NW>
+template <int W, int R, int IMGS, int NW, int S, int KS>
 __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
-  using G = WgGeo<W, R, IMGS, NW>;
+  using G = WgGeo<W, R, IMGS, NW, S, KS>;
   constexpr int MBW = G::MBW;
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -147,10 +185,11 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
   const int co0 = (combo / nsl) * kCh, ci0 = (combo % nsl) * kCh;
   const int t_begin = (int)((int64_t)a.tiles * range / a.NB);
   const int t_end = (int)((int64_t)a.tiles * (range + 1) / a.NB);
-  const int HWp = a.H * W;
+  const int HWp = a.H * W;              // output pixels per image
+  const int HWi = a.HI * a.WI;          // input pixels per image
 
   // rows >= P of both dy buffers are never DMA'd: zero them once
-  for (int i = G::P * 8 + threadIdx.x; i < kPAlloc * 8; i += 64 * NW) {
+  for (int i = G::P * 8 + threadIdx.x; i < G::PALLOC * 8; i += 64 * NW) {
     *reinterpret_cast<u32x4*>(smem + i * 16) = u32x4{0u, 0u, 0u, 0u};
     *reinterpret_cast<u32x4*>(smem + G::BUF_BYTES + i * 16) = u32x4{0u, 0u, 0u, 0u};
   }
@@ -178,10 +217,13 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
     const int row = piece * 8 + (lane >> 3);
     const int img = row / G::HIMG;
     const int rr = row - img * G::HIMG;
-    const int hy = rr / G::HW2, hx = rr - hy * G::HW2;
-    const int c = (lane & 7) ^ wg_key(img * (R * W) + hy * W + hx);  // skewed key (see hb / kt)
-    const bool xok = hx >= 1 && hx <= W && row < G::HROWS;
-    h_off[i] = (img * HWp + (hy - 1) * W + (hx - 1)) * a.C + c * 8;
+    const int hy = rr / G::HC, pr = rr - hy * G::HC;
+    // LDS position pr -> halo column hc (S = 2: evens first, then odds)
+    const int hc = S == 1 ? pr : (pr < (G::HC + 1) / 2 ? 2 * pr : 2 * (pr - (G::HC + 1) / 2) + 1);
+    const int c = (lane & 7) ^ wg_key(G::key_of(img, hy, hc));
+    const int ix = hc - 1;
+    const bool xok = ix >= 0 && ix < a.WI && row < G::HROWS;
+    h_off[i] = (img * HWi + (hy - 1) * a.WI + ix) * a.C + c * 8;
     h_pk[i] = (xok ? 1 : 0) | (hy << 1) | (img << 6);
   }
 
@@ -201,7 +243,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
     const int64_t pix0 = (int64_t)n0 * HWp + (int64_t)r0 * W;
     const int pvalid = IMGS == 1 ? valid_rows * W : valid_imgs * R * W;
     const bf16* dyb = a.dy + pix0 * a.C + co0;
-    const bf16* xb = a.x + pix0 * a.C + ci0;
+    // halo row hy of the tile = input row S*r0 - 1 + hy (h_off carries the -1)
+    const bf16* xb = a.x + ((int64_t)n0 * HWi + (int64_t)(S * r0) * a.WI) * a.C + ci0;
 #pragma unroll
     for (int i = 0; i < G::DY_PW; ++i) {
       const int piece = wave + NW * i;
@@ -217,8 +260,8 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
       if (piece < G::H_INSTR) {
         const int pk = h_pk[i];
         const int hy = (pk >> 1) & 31, img = pk >> 6;
-        const int iy = r0 - 1 + hy;
-        const bool ok = (pk & 1) && iy >= 0 && iy < a.H && img < valid_imgs;
+        const int iy = S * r0 - 1 + hy;
+        const bool ok = (pk & 1) && iy >= 0 && iy < a.HI && img < valid_imgs;
         const void* src = ok ? (const void*)(xb + h_off[i]) : (const void*)g_wg_zero;
         glds16(src, hbuf + piece * 1024);
       }
@@ -248,19 +291,21 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
   // (kh*(W+2) + kw)*128 rides in the instruction's offset field.
   // Pixels past the tile's P (zero dy rows) are clamped onto a real halo row so
   // nothing non-finite is read.
-  int hb[kKSteps][2];
-  uint32_t kt[kKSteps][2];
+  int hb[KS][2];
+  uint32_t kt[KS][2];
 #pragma unroll
-  for (int ks = 0; ks < kKSteps; ++ks)
+  for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int pp = min(32 * ks + 8 * r + pin, G::P - 1);
       const int img = pp / (R * W);
       const int rem = pp - img * (R * W);
       const int oy = rem / W, ox = rem - oy * W;
-      const int row = img * G::HIMG + oy * G::HW2 + ox;
+      const int row = img * G::HIMG + S * oy * G::HC + ox;  // tap (0, 0)
       hb[ks][r] = row * 128 + lofs + G::DY_BYTES;
-      const uint32_t sh = 4u * (uint32_t)(pp & 7);  // s = pp at tap (0, 0)
+      // key index at tap (0, 0): the skewed index is the pixel itself
+      const int kidx = G::SKEW ? (S == 1 ? pp : oy * W + ox) : row;
+      const uint32_t sh = 4u * (uint32_t)(kidx & 7);
       kt[ks][r] = sh == 0 ? kKeyTab : (kKeyTab >> sh) | (kKeyTab << (32u - sh));
     }
   // A (dy) reads: rows 32 ks + 8 r + pin have key(row) == key(pin) (the k-step
@@ -282,11 +327,11 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
     if (t_begin < t_end) issue(t_begin, smem);
     int cur = 0;
     for (int t = t_begin; t < t_end; ++t) {
-      int hbc[kKSteps][2], abc[MBW];
+      int hbc[KS][2], abc[MBW];
       // opaque per tile: the per-(k-step, fragment) addresses are rebuilt inside
       // the loop instead of hoisted into ~130 live registers (they would spill)
 #pragma unroll
-      for (int ks = 0; ks < kKSteps; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
         asm volatile("" : "+v"(hb[ks][0]), "+v"(hb[ks][1]), "+v"(kt[ks][0]), "+v"(kt[ks][1]));
         hbc[ks][0] = hb[ks][0] + cur * G::BUF_BYTES;
         hbc[ks][1] = hb[ks][1] + cur * G::BUF_BYTES;
@@ -317,7 +362,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
 #pragma unroll
           for (int u = 0; u < 3; ++u) {
             const int tap = min(tap0 + u, 8);
-            const int so = (tap / 3) * W + (tap % 3);  // skewed-index offset of the tap
+            const int so = G::key_off(tap / 3, tap % 3);
             const uint32_t key = (kt[ks][r] >> (4 * (so & 7))) & 7u;
             base[r][u] = hbc[ks][r] | (int)(key << 4);
           }
@@ -325,7 +370,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
         for (int j = 0; j < kNB; ++j) {
           const int col = kWCols * WV + 16 * j;
           const int tap = col >> 6, f = (col >> 4) & 3;
-          const int o = (tap / 3) * G::HW2 + (tap % 3);
+          const int o = G::tap_off(tap / 3, tap % 3);
           const v4i16 lo = rd((base[0][tap - tap0] ^ (f << 5)) + o * 128);
           const v4i16 hi = rd((base[1][tap - tap0] ^ (f << 5)) + o * 128);
           const i16x8 t8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -336,7 +381,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
       auto step = [&](auto ks_tag) {
         constexpr int ks = decltype(ks_tag)::value;
         constexpr int NRD = 2 * (MBW + kNB), NMF = MBW * kNB;
-        if constexpr (ks + 1 < kKSteps)
+        if constexpr (ks + 1 < KS)
           load_step(std::integral_constant<int, ks + 1>{}, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
         // fragment-j-major order: the first MFMAs need A and B0 only, so the
         // waits on the next step's reads can be counted, not lgkmcnt(0)
@@ -345,7 +390,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
 #pragma unroll
           for (int i = 0; i < MBW; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[ks & 1][i], fb[ks & 1][j], acc[i][j], 0, 0, 0);
-        if constexpr (ks + 1 < kKSteps) {
+        if constexpr (ks + 1 < KS) {
           // the next step's reads spread over this step's MFMAs
           // (NW 4: 26 reads over 36 MFMAs; NW 8: 22 reads over 18, two per MFMA first)
           constexpr int PAIRS = NRD < NMF ? NRD : NMF;
@@ -364,14 +409,7 @@ __global__ __launch_bounds__(64 * NW, 1) void wgrad3x3_kernel(WgArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       };
-      step(std::integral_constant<int, 0>{});
-      step(std::integral_constant<int, 1>{});
-      step(std::integral_constant<int, 2>{});
-      step(std::integral_constant<int, 3>{});
-      step(std::integral_constant<int, 4>{});
-      step(std::integral_constant<int, 5>{});
-      step(std::integral_constant<int, 6>{});
-      static_assert(kKSteps == 7, "unrolled k-steps");
+      static_for<KS>(step);
       cur ^= 1;
     }
   };
@@ -431,12 +469,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 
 int g_wgrad_waves = 8;  // set_wgrad3x3_waves (A/B runs)
 
-template <int W, int R, int IMGS>
+template <int W, int R, int IMGS, int S, int KS>
 void launch(const WgArgs& a, int grid, hipStream_t stream) {
-  if (g_wgrad_waves == 4)
-    hipLaunchKernelGGL((wgrad3x3_kernel<W, R, IMGS, 4>), dim3(grid), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL((wgrad3x3_kernel<W, R, IMGS, 8>), dim3(grid), dim3(512), 0, stream, a);
+  // the 4-wave variant (A/B runs, set_wgrad3x3_waves) exists for stride 1 only
+  if constexpr (S == 1) {
+    if (g_wgrad_waves == 4) {
+      hipLaunchKernelGGL((wgrad3x3_kernel<W, R, IMGS, 4, S, KS>), dim3(grid), dim3(256), 0, stream, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((wgrad3x3_kernel<W, R, IMGS, 8, S, KS>), dim3(grid), dim3(512), 0, stream, a);
 }
 
 }  // namespace
@@ -446,23 +488,31 @@ void set_wgrad3x3_waves(int64_t nw) {
   g_wgrad_waves = (int)nw;
 }
 
-bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W) {
-  return (C == 64 && W == 56) || (C == 128 && W == 28 && H % 7 == 0) || (C == 256 && W == 14 && H == 14) ||
-         (C == 512 && W == 7 && H == 7);
+// (C, output H, output W, stride) of the 3x3 / pad-1 convs with a tile geometry
+bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride) {
+  if (stride == 1)
+    return (C == 64 && W == 56) || (C == 128 && W == 28 && H % 7 == 0) || (C == 256 && W == 14 && H == 14) ||
+           (C == 512 && W == 7 && H == 7);
+  if (stride == 2)
+    return (C == 128 && W == 28 && H % 2 == 0) || (C == 256 && W == 14 && H == 14) ||
+           (C == 512 && W == 7 && H == 7);
+  return false;
 }
 
-// dW of y = conv3x3(x, W, stride 1, pad 1) for dy, x: [N, C, H, W] bf16
-// channels_last (C in = C out).  Returns [C, C, 3, 3] bf16 in channels_last
-// memory ([C][3][3][C]).
-at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x) {
+// dW of y = conv3x3(x, W, stride s, pad 1) for dy: [N, C, Ho, Wo], x: [N, C,
+// s*Ho, s*Wo] bf16 channels_last (C in = C out).  Returns [C, C, 3, 3] bf16 in
+// channels_last memory ([C][3][3][C]).
+at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride) {
   TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.scalar_type() == at::kBFloat16 &&
                   x.scalar_type() == at::kBFloat16 && dy.dim() == 4 && x.dim() == 4,
               "wgrad3x3: bf16 4-D GPU tensors");
-  TORCH_CHECK(dy.sizes() == x.sizes(), "wgrad3x3: stride-1 same-channel conv (dy and x shapes equal)");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "wgrad3x3: channels_last tensors");
-  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), Wd = x.size(3);
-  TORCH_CHECK(wgrad3x3_supported(C, H, Wd), "wgrad3x3: unsupported shape C=", C, " H=", H, " W=", Wd);
+  const int64_t N = dy.size(0), C = dy.size(1), H = dy.size(2), Wd = dy.size(3);
+  TORCH_CHECK(x.size(0) == N && x.size(1) == C && x.size(2) == stride * H && x.size(3) == stride * Wd,
+              "wgrad3x3: x must be [N, C, stride*Ho, stride*Wo] for dy [N, C, Ho, Wo]");
+  TORCH_CHECK(wgrad3x3_supported(C, H, Wd, stride), "wgrad3x3: unsupported shape C=", C, " Ho=", H, " Wo=", Wd,
+              " stride=", stride);
   auto out = at::empty({C, C, 3, 3}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto stream = at::hip::getCurrentHIPStream();
   const int S = (int)((C / kCh) * (C / kCh));
@@ -480,26 +530,30 @@ at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x) {
   a.N = (int)N;
   a.H = (int)H;
   a.C = (int)C;
+  a.HI = (int)x.size(2);
+  a.WI = (int)x.size(3);
   a.S = S;
   a.NB = NB;
   // per-slot offsets are int32 relative to a tile origin; the origin is int64
-  TORCH_CHECK(H * Wd * C * 4 < ((int64_t)1 << 31), "wgrad3x3: image too large");
-  if (C == 64) {
-    a.tiles_per_img = (int)((H + 3) / 4);
+  TORCH_CHECK(x.size(2) * x.size(3) * C * 4 < ((int64_t)1 << 31), "wgrad3x3: image too large");
+  auto rows = [&](int R) {
+    a.tiles_per_img = (int)((H + R - 1) / R);
     a.tiles = (int)(N * a.tiles_per_img);
-    launch<56, 4, 1>(a, grid, stream);
-  } else if (C == 128) {
-    a.tiles_per_img = (int)(H / 7);
-    a.tiles = (int)(N * a.tiles_per_img);
-    launch<28, 7, 1>(a, grid, stream);
-  } else if (C == 256) {
+  };
+  auto imgs = [&](int I) {
     a.tiles_per_img = 1;
-    a.tiles = (int)N;
-    launch<14, 14, 1>(a, grid, stream);
+    a.tiles = (int)((N + I - 1) / I);
+  };
+  if (stride == 1) {
+    if (C == 64) { rows(4); launch<56, 4, 1, 1, 7>(a, grid, stream); }
+    else if (C == 128) { rows(7); launch<28, 7, 1, 1, 7>(a, grid, stream); }
+    else if (C == 256) { rows(14); launch<14, 14, 1, 1, 7>(a, grid, stream); }
+    else { imgs(4); launch<7, 7, 4, 1, 7>(a, grid, stream); }
   } else {
-    a.tiles_per_img = 1;
-    a.tiles = (int)((N + 3) / 4);
-    launch<7, 7, 4>(a, grid, stream);
+    // stride 2: the halo is ~4x the output tile, so tiles are shorter
+    if (C == 128) { rows(2); launch<28, 2, 1, 2, 2>(a, grid, stream); }       // 56 px, 5 x 57 halo
+    else if (C == 256) { rows(7); launch<14, 7, 1, 2, 4>(a, grid, stream); }  // 98 px, 15 x 29 halo
+    else { imgs(1); launch<7, 7, 1, 2, 2>(a, grid, stream); }                 // 49 px, 15 x 15 halo
   }
   DMP_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(kCh * kCols / 256, S), dim3(256), 0, stream,

@@ -80,16 +80,17 @@ def _halo_ok(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, wdt: 
         and wdt == 56
 
 
-# Weight gradients of the stride-1 3x3s (every ResNet-50 stage) on the
-# persistent halo-tiled kernel: dW in registers, dy / x halo tiles streamed
-# through LDS (csrc/conv/wgrad3x3.hip).  Batch 2048 on MI355X
-# (tools/wgrad_bench.py): 0.45-0.52 ms vs MIOpen's igemm_wrw 0.62-1.18 ms.
+# Weight gradients of every ResNet-50 3x3 (stride 1 and the stride-2 first
+# blocks) on the persistent halo-tiled kernel: dW in registers, dy / x halo
+# tiles streamed through LDS (csrc/conv/wgrad3x3.hip).  Stride 1 at batch 2048
+# on MI355X (tools/wgrad_bench.py): 0.45-0.52 ms vs MIOpen's igemm_wrw 0.62-1.18 ms.
 _STATS["halo_wgrad"] = 0
 
 
 def _halo_wgrad_ok(C, cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, h: int, w: int) -> bool:
-    return (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin == cout and h == w
-            and C.wgrad3x3_supported(cin, h, w))
+    """h, w: INPUT size; the kernel covers stride 1 and 2 (even input sizes)."""
+    return (kh == 3 and kw == 3 and stride in (1, 2) and pad == 1 and cin == cout and h == w
+            and h % stride == 0 and C.wgrad3x3_supported(cin, h // stride, w // stride, stride))
 
 
 def _miopen_fwd(cout: int, kh: int) -> bool:
@@ -208,7 +209,7 @@ class _ConvIGFn(torch.autograd.Function):
         if ctx.needs_input_grad[1] and _halo_wgrad_ok(C, cin, cout, kh, kw, stride, pad, h, w):
             # persistent halo-tiled MFMA weight gradient (csrc/conv/wgrad3x3.hip)
             _STATS["halo_wgrad"] += 1
-            dw = C.wgrad3x3(dy, x)
+            dw = C.wgrad3x3(dy, x, stride)
             if not weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous()
         nat_d = ctx.needs_input_grad[0] and dx is None and _use_native("dgrad", cin, h, stride)
@@ -216,11 +217,13 @@ class _ConvIGFn(torch.autograd.Function):
         want_d = ctx.needs_input_grad[0] and not nat_d and dx is None
         want_w = ctx.needs_input_grad[1] and not nat_w and dw is None
         if want_d or want_w:
-            dx_l, dw, _ = torch.ops.aten.convolution_backward(
+            dx_l, dw_l, _ = torch.ops.aten.convolution_backward(
                 dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
                 [want_d, want_w, False])
             if want_d:
                 dx = dx_l
+            if want_w:
+                dw = dw_l
         if nat_d:
             wt = weight.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()  # [Cin][kh][kw][Cout]
             dx2, _ = C.conv_nt(dy, wt, kh, kw, stride, pad, h, w, transposed=True)

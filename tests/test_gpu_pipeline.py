@@ -64,8 +64,16 @@ def test_pipeline_world1_on_gpu_matches_sequential(schedule, micro):
         loss.backward()
         total += float(loss)
     assert abs(r.loss - total) < 1e-3 * max(1.0, abs(total))
+    # MIOpen's fp32 weight gradients accumulate in a run-dependent order, and the
+    # bias gradients of BNs feeding another BN cancel to ~0 (two identical stock
+    # runs differ O(1) there, relative): compare per tensor in norm with an
+    # absolute floor at the model's gradient scale.  An engine bug -- a lost or
+    # doubled micro-batch -- is O(1) of the tensor's own norm.
+    norms = sorted(float(p.grad.norm()) for p in pipe.module.parameters())
+    floor = 1e-3 * norms[len(norms) // 2]
     for a, p in zip(grads, pipe.module.parameters()):
-        torch.testing.assert_close(a, p.grad, atol=2e-4, rtol=2e-3)
+        err = float((a - p.grad).norm())
+        assert err <= 1e-2 * float(p.grad.norm()) + floor, (err, float(p.grad.norm()), floor)
 
 
 def test_pipeline_world1_bf16_trains():

@@ -124,8 +124,8 @@ def main():
             wtr = w.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
             res["dgrad"]["ours"] = timeit(lambda: C.conv_nt(dy, wtr, k, k, s, pad, h, h, transposed=True))
             res["wgrad"]["ours"] = timeit(lambda: C.conv_wgrad(dy2, x, k, k, s, pad, ho, ho, dt))
-            if hasattr(C, "wgrad3x3") and k == 3 and s == 1 and cin == cout and C.wgrad3x3_supported(cin, ho, ho):
-                res["wgrad"]["halo"] = timeit(lambda: C.wgrad3x3(dy, x))
+            if hasattr(C, "wgrad3x3") and k == 3 and cin == cout and C.wgrad3x3_supported(cin, ho, ho, s):
+                res["wgrad"]["halo"] = timeit(lambda: C.wgrad3x3(dy, x, s))
             if hasattr(C, "conv_wgrad_xl") and cin % 256 == 0:
                 res["wgrad"]["xl"] = timeit(lambda: C.conv_wgrad_xl(dy2, x, k, k, s, pad, ho, ho, dt))
             if hasattr(C, "conv_xl") and k > 1:  # 256x256 ping-pong implicit GEMM

@@ -4,6 +4,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3e; mkdir -p $O
 export PYTHONUNBUFFERED=1
 run() { local name=$1; shift; echo "== $name"; timeout -k 10 ${T:-300} "$@" > $O/$name.log 2>&1; local rc=$?; tail -2 $O/$name.log; return $rc; }
+
 T=400 run tests python -u -m pytest tests/test_gpu_pipeline.py tests/test_data_parallel.py tests/test_gpu_loss.py tests/test_gpu_conv_halo.py -x -q --timeout 120 --timeout-method thread &&
 T=500 DMP_CONVERGENCE_OUT=$O/convergence.json run conv python -u -m pytest tests/test_gpu_convergence.py -x -q --timeout 400 --timeout-method thread &&
 T=200 run halobench python tools/halo_bench.py --batch 2048 &&

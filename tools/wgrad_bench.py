@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_model_parallel_amd import _native  # noqa: E402
 from distributed_model_parallel_amd.utils import miopen_db  # noqa: E402
 
-SHAPES = [(64, 56), (128, 28), (256, 14), (512, 7)]
+SHAPES = [(64, 56, 1), (128, 28, 1), (256, 14, 1), (512, 7, 1), (128, 28, 2), (256, 14, 2), (512, 7, 2)]
 
 
 def timeit(fn, reps=20, warm=5):
@@ -43,26 +43,28 @@ def main():
     miopen_db.seed("use")
     C = _native.require("wgrad_bench")
     print(f"3x3/s1 weight gradient, batch {args.batch}, ms per call (median of 20)")
-    print("| C | HxW | halo 8 waves | halo 4 waves | MIOpen | best halo TF/s |\n|---|---|---|---|---|---|")
-    for c, h in SHAPES:
+    print("| C | out HxW | stride | halo 8 waves | halo 4 waves | MIOpen | best halo TF/s |\n|---|---|---|---|---|---|---|")
+    for c, h, st in SHAPES:
         if only and c not in only:
             continue
-        x = torch.randn(args.batch, c, h, h, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-        dy = torch.randn_like(x)
+        x = torch.randn(args.batch, c, h * st, h * st, device="cuda").bfloat16().contiguous(
+            memory_format=torch.channels_last)
+        dy = torch.randn(args.batch, c, h, h, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         w = torch.randn(c, c, 3, 3, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
         if args.loop:
             for _ in range(args.loop):
-                C.wgrad3x3(dy, x)
+                C.wgrad3x3(dy, x, st)
             torch.cuda.synchronize()
             continue
         C.set_wgrad3x3_waves(4)
-        t4 = timeit(lambda: C.wgrad3x3(dy, x))
+        t4 = timeit(lambda: C.wgrad3x3(dy, x, st)) if st == 1 else float("nan")
         C.set_wgrad3x3_waves(8)
-        th = timeit(lambda: C.wgrad3x3(dy, x))
+        th = timeit(lambda: C.wgrad3x3(dy, x, st))
         tm = timeit(lambda: torch.ops.aten.convolution_backward(
-            dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
+            dy, x, w, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
         fl = 2.0 * args.batch * h * h * c * c * 9
-        print(f"| {c} | {h}x{h} | {th:.3f} | {t4:.3f} | {tm:.3f} | {fl / min(th, t4) / 1e9:.0f} |", flush=True)
+        best = th if st != 1 else min(th, t4)
+        print(f"| {c} | {h}x{h} | {st} | {th:.3f} | {t4:.3f} | {tm:.3f} | {fl / best / 1e9:.0f} |", flush=True)
     print("done")
 
 
