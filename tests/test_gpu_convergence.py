@@ -107,20 +107,21 @@ def _mean(v):
     return sum(v) / len(v)
 
 
-@pytest.mark.parametrize("arch,shape,ncls,steps,batch,lr", [
-    ("mobilenetv2", (3, 32, 32), 10, 240, 128, 0.05),
-    ("resnet50", (3, 64, 64), 10, 120, 128, 0.05),
+@pytest.mark.parametrize("arch,shape,ncls,steps,batch,lr,noise", [
+    ("mobilenetv2", (3, 32, 32), 10, 240, 128, 0.05, 6.0),
+    # random-init ResNet-50 without warm-up diverges at lr 0.05 (stock and native alike)
+    ("resnet50", (3, 64, 64), 10, 150, 128, 0.01, 3.0),
 ])
-def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, lr):
+def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, lr, noise):
     torch.manual_seed(0)
-    xs, ys = _task(ncls, shape, 8192, seed=1)
+    xs, ys = _task(ncls, shape, 8192, seed=1, noise=noise)
     gv = torch.Generator().manual_seed(7)
     base = build_model(arch, num_classes=ncls)
     ref0 = copy.deepcopy(base)
     nat, l_nat = _train_native(base, xs, ys, steps, batch, lr)
     ref, l_ref = _train_reference(ref0, xs, ys, steps, batch, lr)
     # held-out samples: the same class templates (seed 1), labels and noise re-drawn
-    xh, yh = _task(ncls, shape, 9216, seed=1)
+    xh, yh = _task(ncls, shape, 9216, seed=1, noise=noise)
     xh, yh = xh[8192:], yh[8192:]
     xh = xh + 0.25 * torch.randn(xh.shape, generator=gv)
     acc_nat, acc_ref = _accuracy(nat, xh, yh, True), _accuracy(ref, xh, yh, False)
@@ -131,7 +132,7 @@ def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, l
             with open(out) as f:
                 rec = json.load(f)
         rec[arch] = {"native_bf16": l_nat, "stock_fp32": l_ref, "acc_native": acc_nat, "acc_stock": acc_ref,
-                     "steps": steps, "batch": batch, "lr": lr, "shape": list(shape)}
+                     "steps": steps, "batch": batch, "lr": lr, "noise": noise, "shape": list(shape)}
         with open(out, "w") as f:
             json.dump(rec, f)
     k = max(10, steps // 6)

@@ -71,9 +71,9 @@ def test_conv_module_backward_uses_halo_wgrad():
     assert err < 1e-2, err
 
 
-@pytest.mark.parametrize("n,c,ho", [(2, 128, 28), (3, 256, 14), (5, 512, 7)])
+@pytest.mark.parametrize("n,c,ho", [(2, 128, 28), (3, 256, 14)])
 def test_wgrad3x3_stride2_matches_fp32(n, c, ho):
-    """Stride-2 first blocks (column-deinterleaved halo): l2 / l3 / l4 shapes."""
+    """Stride-2 first blocks (column-deinterleaved halo): l2 / l3 shapes."""
     C = _native.require("wgrad3x3")
     assert C.wgrad3x3_supported(c, ho, ho, 2)
     g = torch.Generator(device="cuda").manual_seed(n * 7 + c)

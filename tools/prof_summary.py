@@ -19,7 +19,8 @@ CATS = [
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
     ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "split_reduce", "dw_fwd",
                               "dw_dgrad", "dw_wgrad", "column_reduce", "conv3x3_c64", "gemm_tn_pp",
-                              "wgrad3x3", "wgrad_reduce")),
+                              "wgrad3x3", "wgrad_reduce", "stem_fwd", "stem_wgrad", "partial_sum_kernel",
+                              "s2d_kernel")),
     ("dmp attention (ours)", ("attn_fwd_kernel", "attn_bwd_kernel")),
     ("dmp LayerNorm (ours)", ("ln_fwd", "ln_bwd", "ln_col_reduce")),
     ("dmp linear side passes (ours)", ("colsum_kernel", "partial_colsum")),

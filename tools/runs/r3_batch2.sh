@@ -5,7 +5,9 @@ O=gpurun_out/r3e; mkdir -p $O
 export PYTHONUNBUFFERED=1
 run() { local name=$1; shift; echo "== $name"; timeout -k 10 ${T:-300} "$@" > $O/$name.log 2>&1; local rc=$?; tail -2 $O/$name.log; return $rc; }
 
-T=400 run tests python -u -m pytest tests/test_gpu_pipeline.py tests/test_data_parallel.py tests/test_gpu_loss.py tests/test_gpu_conv_halo.py -x -q --timeout 120 --timeout-method thread &&
+T=300 run bench python bench.py --steps 20 --warmup 5 &&
+T=300 run prof rocprofv3 --kernel-trace --stats -d $O/prof -o prof --output-format csv -- python3 bench.py --steps 6 --warmup 2 &&
+T=400 run tests python -u -m pytest tests/test_gpu_wgrad3x3.py tests/test_gpu_pipeline.py tests/test_data_parallel.py tests/test_gpu_loss.py tests/test_gpu_conv_halo.py -x -q --timeout 120 --timeout-method thread &&
 T=500 DMP_CONVERGENCE_OUT=$O/convergence.json run conv python -u -m pytest tests/test_gpu_convergence.py -x -q --timeout 400 --timeout-method thread &&
 T=200 run halobench python tools/halo_bench.py --batch 2048 &&
 T=300 run dp4_256 python bench.py --parallel dp --dp-replicas 4 --batch-size 256 --steps 30 --warmup 10 --phase-times &&
