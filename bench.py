@@ -119,7 +119,7 @@ def main() -> int:
     ap.add_argument("--bucket-cap-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=1.0)
     ap.add_argument("--no-channels-last", action="store_true")
-    ap.add_argument("--miopen-benchmark", type=int, default=int(os.environ.get("DMP_MIOPEN_BENCHMARK", "1")),
+    ap.add_argument("--miopen-benchmark", type=int, default=1,
                     help="MIOpen find mode for the convs left on MIOpen (first step pays the search)")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
                     help="cpu: gloo plumbing run (BASELINE config 1), fp32 recommended")
@@ -128,7 +128,7 @@ def main() -> int:
     ap.add_argument("--lr", type=float, default=None,
                     help="SGD learning rate (default 0.1 for CNNs, 0.005 for ViT: plain SGD at 0.1 "
                          "diverges on a transformer, which would make the reported loss meaningless)")
-    ap.add_argument("--miopen-db", default=os.environ.get("DMP_MIOPEN_DB", "use"),
+    ap.add_argument("--miopen-db", default="use",
                     choices=["use", "refresh", "off"],
                     help="seed MIOpen's find/perf db from profiles/miopen/ (use), also write new "
                          "entries back (refresh), or start empty (off); see utils/miopen_db.py")
@@ -147,7 +147,7 @@ def main() -> int:
                     help="exit 1 when the collective stream is stuck this long (default 900 s for "
                          "multi-rank GPU runs without --graph, 0 = off)")
     ap.add_argument("--trace-steps", action="store_true", help="diagnostic: time each warmup step")
-    ap.add_argument("--gemm-tuning", default=os.environ.get("DMP_GEMM_TUNING", "use"),
+    ap.add_argument("--gemm-tuning", default="use",
                     choices=["use", "tune", "off"],
                     help="library-GEMM solutions from profiles/tunableop/<model>_gfx950.csv "
                          "(use), re-tune and write that file (tune), or library defaults (off)")

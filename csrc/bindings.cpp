@@ -107,6 +107,10 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
+std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat, bool moments);
+bool conv3x3_c128_supported(int64_t c, int64_t h, int64_t w);
+void set_bn_streaming(bool on);
+void set_pool_generic(bool on);
 at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride);
 bool stem_halo_supported(int64_t hs, int64_t ws, int64_t ho, int64_t wo);
 std::vector<at::Tensor> stem_halo_fwd(const at::Tensor& s, const at::Tensor& wm, int64_t ho, bool moments);
@@ -253,6 +257,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_c64", &dmp::conv3x3_c64, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
         "3x3/s1/p1 64->64-channel conv (W = 56) on the persistent halo-tiled MFMA kernel; "
         "returns (y [N*H*W, 64], fp64 moments [129] or empty)");
+  m.def("conv3x3_c128", &dmp::conv3x3_c128, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
+        "3x3/s1/p1 128->128-channel conv (W = 28, H % 4 == 0) on the persistent halo-tiled MFMA kernel "
+        "(Cout split over grid halves, K split over wave pairs); returns (y [N*H*W, 128], fp64 moments [257] or empty)");
+  m.def("conv3x3_c128_supported", &dmp::conv3x3_c128_supported, py::arg("C"), py::arg("H"), py::arg("W"));
+  m.def("set_bn_streaming", &dmp::set_bn_streaming, py::arg("on"),
+        "A/B: non-temporal streaming in the BN apply passes over > 256 MB tensors (default on)");
+  m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
+        "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M");

@@ -491,14 +491,9 @@ void dispatch_t(const at::Tensor& x, F&& f) {
 template <typename T> T* ptr(const at::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
 
 // Non-temporal streaming for the apply passes over tensors much larger than
-// the Infinity Cache (DMP_BN_NT=0 disables, for A/B runs).
-bool streaming(int64_t M, int64_t C) {
-  static const bool on = [] {
-    const char* e = std::getenv("DMP_BN_NT");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  return on && M * C * 2 >= (int64_t)256 << 20;
-}
+// the Infinity Cache (set_bn_streaming(false) disables it, for A/B runs).
+bool g_bn_streaming = true;
+bool streaming(int64_t M, int64_t C) { return g_bn_streaming && M * C * 2 >= (int64_t)256 << 20; }
 float* fptr(const c10::optional<at::Tensor>& t) {
   return (t.has_value() && t->defined()) ? t->data_ptr<float>() : nullptr;
 }
@@ -723,5 +718,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
   }
   return {dx, dwb[0], dwb[1], dres};
 }
+
+void set_bn_streaming(bool on) { g_bn_streaming = on; }
 
 }  // namespace dmp

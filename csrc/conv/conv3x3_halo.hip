@@ -355,21 +355,12 @@ void launch_nw(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* 
                      reinterpret_cast<bf16*>(y.data_ptr()), part, zs, H, tiles, tpi);
 }
 
-// DMP_HALO_WAVES=8: 8 waves (2 per SIMD, 16 output channels and 72 weight
-// VGPRs each) instead of 4 (1 per SIMD, 32 channels, 144 VGPRs)
-int halo_waves() {
-  static const int nw = [] {
-    const char* e = std::getenv("DMP_HALO_WAVES");
-    return (e != nullptr && std::atoi(e) == 8) ? 8 : 4;
-  }();
-  return nw;
-}
-
+// 4 waves (1 per SIMD, 32 output channels and 144 weight VGPRs each); the
+// 8-wave form (16 channels, 72 VGPRs) measured slower (profiles/README.md).
 template <int W, int R, bool MOM>
 void launch(const at::Tensor& x, const at::Tensor& wk, at::Tensor& y, float* part, double* zs, int H,
             int tiles, int tpi, int grid, hipStream_t stream) {
-  if (halo_waves() == 8) launch_nw<W, R, 8, MOM>(x, wk, y, part, zs, H, tiles, tpi, grid, stream);
-  else launch_nw<W, R, 4, MOM>(x, wk, y, part, zs, H, tiles, tpi, grid, stream);
+  launch_nw<W, R, 4, MOM>(x, wk, y, part, zs, H, tiles, tpi, grid, stream);
 }
 
 }  // namespace

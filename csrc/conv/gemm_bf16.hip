@@ -470,10 +470,7 @@ int g_tile_override = -1;
 // or the plain zero-tap gather (set_phase_dgrad(false), for A/B runs).
 bool g_phase_dgrad = true;
 // Wide (128 x 256) TN tiles for deep weight gradients; set_tn_wide for A/B runs.
-bool g_tn_wide = [] {
-  const char* e = std::getenv("DMP_TN_WIDE");
-  return !(e && e[0] == '0');
-}();
+bool g_tn_wide = true;
 
 template <bool PRO, int EPI, bool CONV>
 void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {

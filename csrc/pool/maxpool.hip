@@ -433,15 +433,10 @@ PoolGeo make_geo(const at::Tensor& x, int64_t k, int64_t s, int64_t p, int vec) 
   return g;
 }
 
-// DMP_POOL_GENERIC=1 routes every geometry through the runtime-k kernels
+// set_pool_generic(true) routes every geometry through the runtime-k kernels
 // (A/B timing, tools/pool_bench.py).
-bool fixed_geometry_disabled() {
-  static const bool off = [] {
-    const char* e = std::getenv("DMP_POOL_GENERIC");
-    return e != nullptr && e[0] == '1';
-  }();
-  return off;
-}
+bool g_pool_generic = false;
+bool fixed_geometry_disabled() { return g_pool_generic; }
 
 void check_x(const at::Tensor& x, const char* name) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4, name, " must be a 4-D GPU tensor");
@@ -606,5 +601,7 @@ at::Tensor global_avgpool_backward(const at::Tensor& g, int64_t H, int64_t W) {
                        dx.data_ptr<float>(), (int)(H * W), (int)(C / vec), inv, total);
   return dx;
 }
+
+void set_pool_generic(bool on) { g_pool_generic = on; }
 
 }  // namespace dmp

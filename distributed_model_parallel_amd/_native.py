@@ -69,6 +69,38 @@ def require(what: str = "this operation") -> ModuleType:
     return m
 
 
+# Native kernel paths / fusions that DMP_DISABLE=<name>[,<name>...] turns off
+# (A/B measurement and bisection; the fallback is the unfused native path or
+# the stock op).  The one kernel-selection switch of the framework.
+FEATURES = {
+    "igemm": "every native 3x3 conv (ops/conv_igemm.py) -> MIOpen",
+    "halo3": "halo-tiled 3x3 convs of layers 1-2 (conv3x3_halo.hip, conv3x3_c128.hip)",
+    "xl_conv3": "256x256 ping-pong implicit GEMM for layer-3/4 3x3 convs (gemm_xl.hip conv_xl)",
+    "xl_conv": "256x256 ping-pong GEMM for wide 1x1 convs (gemm_xl.hip)",
+    "tn_xl": "ping-pong TN weight gradients of wide 1x1 convs",
+    "compact_shortcut": "stride-2 shortcut gradient kept compact (no zero-filled tensor)",
+    "fuse_bn_bwd": "BN backward reductions in the consumer's data-gradient epilogue (BnBwdSlot)",
+    "fuse_stem_pool": "stem BN apply + ReLU inside the max-pool (forward and backward)",
+    "stem_halo": "halo-tiled stem kernels (stem_halo.hip) -> row-tap implicit GEMM",
+    "rowtap_stem": "row-tap stem implicit GEMM (stem.hip) -> MIOpen",
+}
+_disabled_cache: Optional[frozenset] = None
+
+
+def disabled(feature: str) -> bool:
+    """True when ``feature`` (a FEATURES key) is listed in DMP_DISABLE."""
+    global _disabled_cache
+    if _disabled_cache is None:
+        names = {f.strip() for f in os.environ.get("DMP_DISABLE", "").split(",") if f.strip()}
+        unknown = names - set(FEATURES)
+        if unknown:
+            raise ValueError(f"DMP_DISABLE: unknown feature(s) {sorted(unknown)}; known: {sorted(FEATURES)}")
+        _disabled_cache = frozenset(names)
+    if feature not in FEATURES:
+        raise KeyError(feature)
+    return feature in _disabled_cache
+
+
 _REFERENCE = False
 
 

@@ -12,7 +12,6 @@ MI355X-first choices:
 """
 from __future__ import annotations
 
-import os
 from typing import List, Optional, Sequence, Type, Union
 
 import torch
@@ -29,8 +28,14 @@ from ..ops.stem import StemConv2d
 # bn2 -> conv3 prologue fusion (ops/fused.py bn_relu_conv1x1).  Off by default:
 # measured on MI355X (profiles/README.md finding 6) the per-element BN+ReLU in
 # the GEMM operand staging costs more (+0.2 ms forward GEMM, +0.5 ms weight
-# gradient) than the removed BN apply pass saves (0.39 ms).
-_FUSE_BN2_CONV3 = os.environ.get("DMP_FUSE_BN_CONV", "0") == "1"
+# gradient) than the removed BN apply pass saves (0.39 ms).  Kept as an API
+# option (set_fuse_bn2_conv3; tests/test_gpu_models.py), not an env switch.
+_FUSE_BN2_CONV3 = False
+
+
+def set_fuse_bn2_conv3(on: bool) -> None:
+    global _FUSE_BN2_CONV3
+    _FUSE_BN2_CONV3 = bool(on)
 
 
 def _conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:

@@ -33,9 +33,8 @@ GradReducer = Callable[[torch.Tensor], torch.Tensor]
 _STATS = {"native_fwd": 0, "torch_fwd": 0}
 
 # BN backward reductions fused into the consuming 1x1 conv's data-gradient
-# epilogue (BnBwdSlot); DMP_FUSE_BN_BWD=0 disables it for A/B runs.
-import os as _os  # noqa: E402
-_FUSE_BWD = _os.environ.get("DMP_FUSE_BN_BWD", "1") != "0"
+# epilogue (BnBwdSlot); DMP_DISABLE=fuse_bn_bwd turns it off for A/B runs.
+_FUSE_BWD = not _native.disabled("fuse_bn_bwd")
 
 
 def stats() -> dict:

@@ -21,7 +21,6 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-import os
 
 from .. import _native
 
@@ -54,8 +53,8 @@ def _blaslt_dgrad(m: int, cin: int, cout: int) -> bool:
 
 
 # A/B switches (measured per box): compact strided shortcut gradients, glds-ring GEMMs
-_COMPACT = os.environ.get("DMP_COMPACT_SHORTCUT", "1") != "0"
-_XL = os.environ.get("DMP_XL_CONV", "1") != "0"
+_COMPACT = not _native.disabled("compact_shortcut")
+_XL = not _native.disabled("xl_conv")
 
 
 def _xl(n: int, k: int) -> bool:
@@ -194,7 +193,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, dw, None, None, None, None, None
 
 
-_TN_XL = os.environ.get("DMP_TN_XL", "1") != "0"
+_TN_XL = not _native.disabled("tn_xl")
 _STATS["tn_xl"] = 0
 
 

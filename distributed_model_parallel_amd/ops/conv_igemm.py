@@ -21,8 +21,6 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
-import os
-
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -30,18 +28,18 @@ import torch.nn.functional as F
 from .. import _native
 
 _STATS = {"native": 0, "torch": 0}
-# DMP_IGEMM=0 routes these convs to MIOpen (A/B comparisons, debugging)
-ENABLED = os.environ.get("DMP_IGEMM", "1") != "0"
-# Backward backend per pass: DMP_IGEMM_BWD=1 (ours everywhere), 0 (MIOpen
-# everywhere) or auto (default): ours where the per-shape table below measured
-# it at least as fast as MIOpen's tuned solution (tools/conv_roofline.py,
-# profiles/conv_roofline_r2.md), MIOpen elsewhere.
-_BWD_MODE = os.environ.get("DMP_IGEMM_BWD", "auto")
-NATIVE_BWD = _BWD_MODE == "1"
+# DMP_DISABLE=igemm routes these convs to MIOpen (A/B comparisons, debugging)
+ENABLED = not _native.disabled("igemm")
+# Backward passes that neither the halo kernels nor conv_xl cover run on
+# MIOpen: the generic implicit-GEMM backward (conv_nt transposed / conv_wgrad)
+# measured slower on every ResNet-50 shape (profiles/raw_r2/roofline_*.log).
+# set_generic_backward(True) routes them to it (any shape; tests).
+NATIVE_BWD = False
 
-# (pass, Cin, H_in, stride) of ResNet-50's 3x3 convs where our kernel won at
-# batch 1024 on MI355X; everything else goes to MIOpen in "auto" mode.
-_OURS_FASTER = set()
+
+def set_generic_backward(on: bool) -> None:
+    global NATIVE_BWD
+    NATIVE_BWD = bool(on)
 
 # 256x256 ping-pong implicit GEMM (csrc/gemm/gemm_xl.hip conv_xl), used where
 # its 256-wide output tile is full: forward (with the BN moments) when
@@ -49,35 +47,47 @@ _OURS_FASTER = set()
 # optionally fused with the producer BN's backward reductions) when
 # Cin >= 256.  ResNet-50 layers 3-4: forward 0.30-0.33 ms vs 0.46-0.49 (conv_nt)
 # and dgrad 0.30-0.31 vs MIOpen 0.38-0.41 (profiles/conv3x3_xl_r2.md).
-# DMP_XL_CONV3=0 disables it.
-_XL3 = os.environ.get("DMP_XL_CONV3", "1") != "0"
+# DMP_DISABLE=xl_conv3 turns it off.
+_XL3 = not _native.disabled("xl_conv3")
 _STATS["xl_fwd"] = 0
 _STATS["xl_dgrad"] = 0
 _STATS["xl_bnbwd"] = 0
 
 
-# Forward where neither of our kernels wins: for Cout < 256 (layers 1-2) the
-# 4-wave conv_nt with fused moments (0.47-0.70 ms) loses to MIOpen's forward
-# plus the separate BN moments pass (0.33-0.53 + 0.04-0.08 ms;
-# profiles/conv3x3_xl_r2.md), so those run F.conv2d and let the BN reduce.
-# DMP_IGEMM_FWD=1 keeps them on conv_nt.
-_FWD_MODE = os.environ.get("DMP_IGEMM_FWD", "auto")
+# Forward where none of our kernels wins (the layer-2 stride-2 3x3, other
+# Cout < 256 shapes outside the halo kernels): the 4-wave conv_nt with fused
+# moments (0.47-0.70 ms at batch 1024) loses to MIOpen's forward plus the
+# separate BN moments pass (0.33-0.53 + 0.04-0.08 ms; profiles/conv3x3_xl_r2.md),
+# so those run F.conv2d and let the BN reduce.  Tests set _MIOPEN_FWD = False
+# to exercise conv_nt's forward.
+_MIOPEN_FWD = True
 _STATS["miopen_fwd"] = 0
 
 
-# 64 -> 64-channel 3x3/s1/p1 convs on 56-wide maps (ResNet-50 layer 1) run on
-# the persistent halo-tiled kernel (csrc/conv/conv3x3_halo.hip: weights in
-# VGPRs, input halo in LDS, read once from HBM), forward with the BN moments
-# fused and the data gradient as the same conv over flipped weights.
-# DMP_HALO3=0 sends them back to the policy below.
-_HALO3 = os.environ.get("DMP_HALO3", "1") != "0"
+# 3x3/s1/p1 convs with Cin = Cout = 64 on 56-wide maps (ResNet-50 layer 1)
+# and 128 on 28-wide maps (layer 2) run on the persistent halo-tiled kernels
+# (csrc/conv/conv3x3_halo.hip, conv3x3_c128.hip: weights in VGPRs, input halo
+# in LDS, read once from HBM), forward with the BN moments fused and the data
+# gradient as the same conv over flipped weights.  DMP_DISABLE=halo3 sends
+# them back to the policy below.
+_HALO3 = not _native.disabled("halo3")
 _STATS["halo_fwd"] = 0
 _STATS["halo_dgrad"] = 0
 
 
-def _halo_ok(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, wdt: int) -> bool:
-    return _HALO3 and cin == 64 and cout == 64 and kh == 3 and kw == 3 and stride == 1 and pad == 1 \
-        and wdt == 56
+def _halo_kind(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, h: int, wdt: int) -> int:
+    """64 / 128: which halo conv kernel runs this 3x3/s1/p1 conv; 0: none."""
+    if not (_HALO3 and cin == cout and kh == 3 and kw == 3 and stride == 1 and pad == 1):
+        return 0
+    if cin == 64 and wdt == 56:
+        return 64
+    if cin == 128 and wdt == 28 and h % 4 == 0:
+        return 128
+    return 0
+
+
+def _halo_conv(C, kind: int):
+    return C.conv3x3_c64 if kind == 64 else C.conv3x3_c128
 
 
 # Weight gradients of every ResNet-50 3x3 (stride 1 and the stride-2 first
@@ -94,7 +104,7 @@ def _halo_wgrad_ok(C, cin: int, cout: int, kh: int, kw: int, stride: int, pad: i
 
 
 def _miopen_fwd(cout: int, kh: int) -> bool:
-    return _FWD_MODE == "auto" and kh > 1 and not (_XL3 and cout >= 256)
+    return _MIOPEN_FWD and kh > 1 and not (_XL3 and cout >= 256)
 
 
 def _xl_fwd(cout: int, kh: int, kw: int) -> bool:
@@ -103,14 +113,6 @@ def _xl_fwd(cout: int, kh: int, kw: int) -> bool:
 
 def _xl_dgrad(cin: int, kh: int, kw: int, stride: int) -> bool:
     return _XL3 and cin >= 256 and stride == 1 and kh == kw and kh > 1
-
-
-def _use_native(pass_: str, cin: int, h: int, stride: int) -> bool:
-    if NATIVE_BWD:
-        return True
-    if _BWD_MODE == "0":
-        return False
-    return (pass_, cin, h, stride) in _OURS_FASTER
 
 
 def _out_size(h: int, k: int, s: int, p: int) -> int:
@@ -145,9 +147,10 @@ class _ConvIGFn(torch.autograd.Function):
             # weight gradient of every stride-1 3x3)
             y4 = F.conv2d(x, weight, None, stride, pad)
             y2, mom = None, None
-        elif _halo_ok(cin, cout, kh, kw, stride, pad, w):
+        elif _halo_kind(cin, cout, kh, kw, stride, pad, h, w):
             _STATS["halo_fwd"] += 1
-            y2, mom = C.conv3x3_c64(x, _wmat(weight).contiguous(), moments)
+            y2, mom = _halo_conv(C, _halo_kind(cin, cout, kh, kw, stride, pad, h, w))(
+                x, _wmat(weight).contiguous(), moments)
             if not moments:
                 mom = None
         elif _xl_fwd(cout, kh, kw):
@@ -186,11 +189,12 @@ class _ConvIGFn(torch.autograd.Function):
         dy = dy.to(x.dtype).contiguous(memory_format=torch.channels_last)
         dx = dw = None
         bs, ctx.bn_slot = ctx.bn_slot, None
-        if ctx.needs_input_grad[0] and _halo_ok(cin, cout, kh, kw, stride, pad, w):
-            # dx = conv(dy, flip(W)^T): the same 3x3/s1/p1 64->64 conv
+        hk = _halo_kind(cin, cout, kh, kw, stride, pad, h, w)
+        if ctx.needs_input_grad[0] and hk:
+            # dx = conv(dy, flip(W)^T): the same 3x3/s1/p1 C->C conv
             wfl = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
             _STATS["halo_dgrad"] += 1
-            dx2, _ = C.conv3x3_c64(dy, wfl, False)
+            dx2, _ = _halo_conv(C, hk)(dy, wfl, False)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
         elif ctx.needs_input_grad[0] and _xl_dgrad(cin, kh, kw, stride):
             # dx = conv(dy, flip(W)^T, pad k-1-p) on the ping-pong implicit GEMM
@@ -212,8 +216,8 @@ class _ConvIGFn(torch.autograd.Function):
             dw = C.wgrad3x3(dy, x, stride)
             if not weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous()
-        nat_d = ctx.needs_input_grad[0] and dx is None and _use_native("dgrad", cin, h, stride)
-        nat_w = ctx.needs_input_grad[1] and dw is None and _use_native("wgrad", cin, h, stride)
+        nat_d = ctx.needs_input_grad[0] and dx is None and NATIVE_BWD
+        nat_w = ctx.needs_input_grad[1] and dw is None and NATIVE_BWD
         want_d = ctx.needs_input_grad[0] and not nat_d and dx is None
         want_w = ctx.needs_input_grad[1] and not nat_w and dw is None
         if want_d or want_w:
@@ -242,7 +246,8 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
                  dilation=(1, 1)) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
     if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]) and not \
-            _halo_ok(x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[3]):
+            _halo_kind(x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[2],
+                       x.shape[3]):
         _STATS["miopen_fwd"] += 1
         if torch.is_grad_enabled() and weight.requires_grad and _halo_wgrad_ok(
                 _native.native(), x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding,

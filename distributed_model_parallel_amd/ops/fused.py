@@ -301,5 +301,5 @@ def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Te
                                   bn.eps, bn.num_batches_tracked, rmom, rgrad, 3, 2, pad)
 
 
-import os as _os  # noqa: E402
-_FUSE_STEM_POOL = _os.environ.get("DMP_FUSE_STEM_POOL", "1") != "0"
+from .. import _native as _nat  # noqa: E402
+_FUSE_STEM_POOL = not _nat.disabled("fuse_stem_pool")

@@ -16,7 +16,7 @@
   and residual in the store (no add kernel), and fc2's data gradient applies
   gelu'(h) in its epilogue (no GELU-backward pass).  Weight gradients stay on
   hipBLASLt (split-M shapes our tile grid cannot fill).  Off by default
-  (``DMP_VIT_XL=1`` enables it): measured at batch 256 the fused path is
+  (``set_xl_linear(True)`` enables it): measured at batch 256 the fused path is
   1.6 % slower per step than hipBLASLt + the separate GELU / add passes --
   fc1+GELU and fc2-dgrad+GELU' break even, fc2 / proj + residual lose
   (profiles/vit_xl_epilogues_r2.md).
@@ -25,7 +25,6 @@ CPU tensors, non-bf16 dtypes and widths that are not a multiple of 256 use
 the plain PyTorch ops (same math)."""
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -35,7 +34,14 @@ import torch.nn.functional as F
 from .. import _native
 
 _STATS = {"native": 0, "torch": 0, "xl": 0}
-_XL = os.environ.get("DMP_VIT_XL", "0") == "1"
+_XL = False
+
+
+def set_xl_linear(on: bool) -> None:
+    """Route mlp_residual / linear_residual to the fused gemm_xl path."""
+    global _XL
+    _XL = bool(on)
+
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 
 

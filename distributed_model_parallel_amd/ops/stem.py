@@ -24,8 +24,8 @@ from .. import _native
 _STATS = {"native": 0, "torch": 0, "halo": 0}
 # 224-px inputs (Wo = 112): the persistent halo-tiled stem kernels
 # (csrc/conv/stem_halo.hip) instead of the generic row-tap implicit GEMM;
-# DMP_STEM_HALO=0 for A/B runs.
-_HALO = __import__("os").environ.get("DMP_STEM_HALO", "1") != "0"
+# DMP_DISABLE=stem_halo for A/B runs.
+_HALO = not _native.disabled("stem_halo")
 
 
 def stem_wmat(w: torch.Tensor) -> torch.Tensor:
@@ -145,7 +145,7 @@ class _RowTapFn(torch.autograd.Function):
         return None, dw, None, None, None
 
 
-_ROWTAP = __import__("os").environ.get("DMP_ROWTAP_STEM", "1") != "0"
+_ROWTAP = not _native.disabled("rowtap_stem")
 
 
 def _rowtap_ok(conv: nn.Conv2d, x: torch.Tensor) -> bool:

@@ -25,7 +25,7 @@ SHAPES = [  # n, cin, cout, h, w, k, stride, pad
 def _native_forward(monkeypatch):
     """These tests exercise our kernels: keep layer-1/2-sized forwards off MIOpen."""
     from distributed_model_parallel_amd.ops import conv_igemm
-    monkeypatch.setattr(conv_igemm, "_FWD_MODE", "1")
+    monkeypatch.setattr(conv_igemm, "_MIOPEN_FWD", False)
 
 
 def _cl(t):

@@ -83,10 +83,37 @@ def test_stage_write_rows_on_distinct_spans():
 
 
 def test_routing_predicate():
-    ok = conv_igemm._halo_ok
-    assert ok(64, 64, 3, 3, 1, 1, 56)
-    assert not ok(64, 64, 3, 3, 2, 1, 56)     # strided
-    assert not ok(128, 128, 3, 3, 1, 1, 28)   # layer 2
-    assert not ok(64, 64, 3, 3, 1, 1, 16)     # other widths (kernel is built for W = 56)
-    assert not ok(64, 128, 3, 3, 1, 1, 56)
-    assert not ok(64, 64, 1, 1, 1, 0, 56)
+    kind = conv_igemm._halo_kind
+    assert kind(64, 64, 3, 3, 1, 1, 56, 56) == 64
+    assert kind(64, 64, 3, 3, 2, 1, 56, 56) == 0      # strided
+    assert kind(128, 128, 3, 3, 1, 1, 28, 28) == 128  # layer 2 (conv3x3_c128.hip)
+    assert kind(128, 128, 3, 3, 1, 1, 30, 28) == 0    # c128 tiles are 4 whole rows
+    assert kind(128, 128, 3, 3, 2, 1, 56, 56) == 0
+    assert kind(64, 64, 3, 3, 1, 1, 16, 16) == 0      # other widths (kernels are built per W)
+    assert kind(64, 128, 3, 3, 1, 1, 56, 56) == 0
+    assert kind(64, 64, 1, 1, 1, 0, 56, 56) == 0
+    assert kind(256, 256, 3, 3, 1, 1, 14, 14) == 0
+
+
+C128 = Path(__file__).resolve().parents[1] / "csrc" / "conv" / "conv3x3_c128.hip"
+
+
+def test_c128_key_conflict_free_for_every_start_residue():
+    """conv3x3_c128.hip: 256-B halo pixels (one whole bank row each), key
+    2 (q & 7) XOR-ed into the 16 chunks of a pixel.  Every ds_read_b128 service
+    group hits 16 distinct 16-B slots for any fragment start and chunk base."""
+    src = C128.read_text()
+    assert "hkey(int q) { return (q & 7) << 1; }" in src, "hkey changed: update this test"
+
+    def key(q):
+        return (q & 7) << 1
+    for q0 in range(16):
+        for base in (0, 4, 8, 12):     # 8 wk + 4 (s & 1): the chunk base of a k-step
+            for g in GROUPS:
+                slots = {(base + (lane >> 4)) ^ key(q0 + (lane & 15)) for lane in g}
+                assert len(slots) == 16, (q0, base, g)
+    # the c64 period-8 table does not carry over to the 256-B pixel stride
+    old = _halo_key_table()
+    bad = sum(len({(lane >> 4) ^ old[(q0 + (lane & 15)) & 7] for lane in g}) < 16
+              for q0 in range(16) for g in GROUPS)
+    assert bad > 0
