@@ -109,7 +109,9 @@ at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType o
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 bool conv3x3_c128_supported(int64_t c, int64_t h, int64_t w);
+at::Tensor conv3x3_c128_dgrad_s2(const at::Tensor& dy, const at::Tensor& wt);
 void set_bn_streaming(bool on);
+at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>& wph, int64_t hi, int64_t wi);
 void set_pool_generic(bool on);
 at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride);
 bool stem_halo_supported(int64_t hs, int64_t ws, int64_t ho, int64_t wo);
@@ -260,7 +262,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_c128", &dmp::conv3x3_c128, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
         "3x3/s1/p1 128->128-channel conv (W = 28, H % 4 == 0) on the persistent halo-tiled MFMA kernel "
         "(Cout split over grid halves, K split over wave pairs); returns (y [N*H*W, 128], fp64 moments [257] or empty)");
+  m.def("conv3x3_c128_dgrad_s2", &dmp::conv3x3_c128_dgrad_s2, py::arg("dy"), py::arg("wt"),
+        "data gradient of a 3x3/s2/p1 128->128 conv (dy 28 wide) as its four stride phases on the halo kernel; "
+        "wt = W.permute(1, 2, 3, 0) as [128, 1152]; returns dx [N*2H*56, 128]");
   m.def("conv3x3_c128_supported", &dmp::conv3x3_c128_supported, py::arg("C"), py::arg("H"), py::arg("W"));
+  m.def("conv_xl_dgrad_s2", &dmp::conv_xl_dgrad_s2, py::arg("dy"), py::arg("wph"), py::arg("hi"), py::arg("wi"),
+        "data gradient of a 3x3/s2/p1 conv as four stride-phase implicit GEMMs on the ping-pong kernel; "
+        "returns dx [N*hi*wi, Cin]");
   m.def("set_bn_streaming", &dmp::set_bn_streaming, py::arg("on"),
         "A/B: non-temporal streaming in the BN apply passes over > 256 MB tensors (default on)");
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),

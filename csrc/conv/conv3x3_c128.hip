@@ -1,13 +1,22 @@
-// 3x3 / stride-1 / pad-1 convolution for 128 -> 128 channels on 28-wide maps
-// (ResNet-50 layer 2: forward, and the data gradient as the same conv over
-// flipped weights) as a persistent, halo-tiled MFMA kernel -- the C = 128
-// sibling of conv3x3_halo.hip, which it follows except where noted.
+// 3x3 convolutions with 128 -> 128 channels of ResNet-50 layer 2 as a
+// persistent, halo-tiled MFMA kernel -- the C = 128 sibling of
+// conv3x3_halo.hip, which it follows except where noted:
+//   * stride 1 / pad 1 on 28-wide maps: the forward (+ BN moments) and the
+//     data gradient (the same conv over flipped weights);
+//   * the data gradient of the stride-2 block-0 conv (dy 28x28 -> dx 56x56)
+//     as its four stride phases (PH): dx[2m + py, 2q + px] collects the taps
+//     (ky, kx) of phase (py, px) -- 1, 2, 2 or 4 of the 9 -- from dy[m + a(ky),
+//     q + a(kx)] (a(1) = 0 for the even phase, a(2) = 0 and a(0) = 1 for the
+//     odd one).  One dy halo tile of 4 rows serves all four phases; each phase
+//     is its own MFMA sweep and epilogue, written straight into its pixels of
+//     dx: no zero-filled dx, no zero taps (MIOpen zero-fills dx, then runs
+//     igemm_bwd).
 //
 // The weights of a 64 x 64 conv fit a 4-wave block's VGPRs (each wave 32 Cout
 // x 576 K = 144 VGPRs); a 128 -> 128 conv has 4x the weights.  So:
-//   * the grid is split in two halves, one per 64-channel Cout chunk: block
-//     b < G/2 holds Cout 0..63, block b + G/2 Cout 64..127, and both walk the
-//     same tile range at the same time on the same XCD (b and b + G/2 are
+//   * the grid is split in two halves, one per 64-channel output chunk: block
+//     b < G/2 holds outputs 0..63, block b + G/2 outputs 64..127, and both walk
+//     the same tile range at the same time on the same XCD (b and b + G/2 are
 //     congruent mod 8), so each input halo is read from HBM once and from L2
 //     once more;
 //   * the K = 9 x 128 reduction is split between the wave pairs instead of
@@ -20,11 +29,10 @@
 //     2 (q & 7): a ds_read_b128 16-lane service group holds the lanes of one
 //     lh parity at 8 consecutive pixels and of the other at the 8 after, and
 //     the even / odd keys of those two sets can never collide (exhaustive
-//     check over all 16 tap residues; the c64 table does not apply at this
-//     stride).
-// Tile = R = 4 full output rows of one image (112 px; 28 / 4 tiles per
-// image), so its output chunk is one contiguous run of rows.  MOM: per-block
-// (sum, sum^2) partials of the bf16 outputs, as conv3x3_halo.hip.
+//     check over all 16 tap residues in tests/test_halo_layout.py; the c64
+//     table does not apply at this stride).
+// Tile = R = 4 full rows of one image (112 px; 28 / 4 tiles per image).
+// MOM: per-block (sum, sum^2) partials of the bf16 outputs, as conv3x3_halo.hip.
 // Reference: these replace MIOpen's 3x3s of torchvision ResNet-50 layer 2
 // (reference model_parallel.py:61, data_parallel.py:78).
 #include <torch/extension.h>
@@ -44,20 +52,30 @@ using lptr_t = __attribute__((address_space(3))) void*;
 constexpr int CI = 128, CO = 128, CB = 64;   // channels in, out, out per block
 constexpr int W = 28, R = 4;
 constexpr int NT = 256;                      // 4 waves: wk = wave & 1, wn = wave >> 1
-constexpr int HW2 = W + 2, PIX = (R + 2) * HW2;
-constexpr int DMA_INSTR = PIX * (CI / 8) / 64;      // 1 KB wave instructions per halo (45)
-constexpr int DMA_PER_WAVE = (DMA_INSTR + 3) / 4;   // 12
-constexpr int BUF = DMA_PER_WAVE * 4 * 1024;
-constexpr int OUT_PIX = R * W;                      // 112
-constexpr int MF = OUT_PIX / 16;                    // 7 row fragments
-constexpr int MF_LO = 4;                            // fragments finalised by wk = 0
-constexpr int KSTEPS = 9 * 64 / 32;                 // k32 steps per K half
-constexpr int SCR_OFF = 2 * BUF;                    // K-half exchange [2 wn][7 f][2 nf][64 lanes] x f32x4
-constexpr int STAGE_OFF = SCR_OFF + 2 * MF * 2 * 1024;
-constexpr int MRED_OFF = STAGE_OFF + OUT_PIX * CB * 2;
-constexpr int SMEM = MRED_OFF + 2 * CB * 4;
-static_assert(PIX * (CI / 8) % 64 == 0, "halo is a whole number of 1 KB DMA rounds");
-static_assert(SMEM <= 160 * 1024, "LDS budget");
+constexpr int OUT_PIX = R * W;               // 112 pixels per tile (per phase)
+constexpr int MF = OUT_PIX / 16;             // 7 row fragments
+constexpr int MF_LO = 4;                     // fragments finalised by wk = 0
+constexpr int KSTEPS = 9 * 64 / 32;          // k32 steps per K half (all 9 taps)
+
+// PH = false: stride-1 conv, halo (R+2) x (W+2) starting one row / column
+// before the tile; PH = true: stride-2 data gradient, dy halo (R+1) x (W+1)
+// starting at the tile (the odd phases reach one row / column past it).
+template <bool PH>
+struct Geo {
+  static constexpr int HR = PH ? R + 1 : R + 2, HC = PH ? W + 1 : W + 2;
+  static constexpr int OFF = PH ? 0 : 1;  // halo (0, 0) = input (r0 - OFF, -OFF)
+  static constexpr int PIX = HR * HC;
+  static constexpr int DMA_INSTR = (PIX * (CI / 8) + 63) / 64;   // 1 KB wave instructions per halo
+  static constexpr int DMA_PER_WAVE = (DMA_INSTR + 3) / 4;
+  static constexpr int BUF = DMA_PER_WAVE * 4 * 1024;
+  static constexpr int SCR_OFF = 2 * BUF;          // K-half exchange [2 wn][7 f][2 nf][64 lanes] x f32x4
+  static constexpr int STAGE_OFF = SCR_OFF + 2 * MF * 2 * 1024;
+  static constexpr int MRED_OFF = STAGE_OFF + OUT_PIX * CB * 2;
+  static constexpr int SMEM = MRED_OFF + 2 * CB * 4;
+  // stores per thread per tile: >= 3 per epilogue (896 16-B chunks / 256 threads)
+  static constexpr int MIN_STORES = PH ? 12 : 3;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+};
 
 __device__ __attribute__((aligned(16))) uint32_t g_c128_zero[4];
 
@@ -82,58 +100,157 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// Per DMA slot of this lane: (element offset from the tile's first output row
+// Per DMA slot of this lane: (element offset from the tile's first input row
 // of the logical 16-B chunk it carries) << 3 | halo row, and a bitmask of the
 // slots whose column lies inside the image.
+template <bool PH>
 struct Slots {
-  int pk[DMA_PER_WAVE];
+  int pk[Geo<PH>::DMA_PER_WAVE];
   uint32_t xok = 0;
 };
 
-__device__ __forceinline__ Slots make_slots(int wave, int lane) {
-  Slots s;
+template <bool PH>
+__device__ __forceinline__ Slots<PH> make_slots(int wave, int lane) {
+  using G = Geo<PH>;
+  Slots<PH> s;
 #pragma unroll
-  for (int i = 0; i < DMA_PER_WAVE; ++i) {
-    const int ins = wave * DMA_PER_WAVE + i;
+  for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
+    const int ins = wave * G::DMA_PER_WAVE + i;
     const int g = ins * 64 + lane;
     const int q = g >> 4;
     const int c = (g & 15) ^ hkey(q);
-    const int hy = q / HW2, hx = q - hy * HW2, ix = hx - 1;
-    s.pk[i] = (((hy - 1) * W + ix) * CI + c * 8) * 8 + min(hy, 7);
-    if (q < PIX && ins < DMA_INSTR && ix >= 0 && ix < W) s.xok |= 1u << i;
+    const int hy = q / G::HC, hx = q - hy * G::HC, ix = hx - G::OFF;
+    s.pk[i] = (((hy - G::OFF) * W + ix) * CI + c * 8) * 8 + min(hy, 7);
+    if (q < G::PIX && ins < G::DMA_INSTR && ix >= 0 && ix < W) s.xok |= 1u << i;
   }
   return s;
 }
 
+// H: input height (x for the stride-1 conv, dy for PH); tiles of R input rows.
+template <bool PH>
 __device__ __forceinline__ void halo_issue(const bf16* __restrict__ x, char* buf, int tile, int H, int tpi,
-                                           int wave, const Slots& s) {
+                                           int wave, const Slots<PH>& s) {
+  using G = Geo<PH>;
   const int n = tile / tpi;
   const int r0 = (tile - n * tpi) * R;
   const bf16* base = x + ((int64_t)n * H + r0) * W * CI;
-  const int rlo = 1 - r0, rhi = H - r0 + 1;
+  const int rlo = G::OFF - r0, rhi = H - r0 + G::OFF;  // valid halo rows: rlo <= hy < rhi
 #pragma unroll
-  for (int i = 0; i < DMA_PER_WAVE; ++i) {
-    const int ins = wave * DMA_PER_WAVE + i;
+  for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
+    const int ins = wave * G::DMA_PER_WAVE + i;
     const int hy = s.pk[i] & 7;
     const bool ok = ((s.xok >> i) & 1u) && hy >= rlo && hy < rhi;
     const void* src = ok ? (const void*)(base + (s.pk[i] >> 3)) : (const void*)g_c128_zero;
-    if (ins < DMA_INSTR) glds16(src, buf + ins * 1024);
+    if (ins < G::DMA_INSTR) glds16(src, buf + ins * 1024);
   }
 }
 
-template <bool MOM>
+// stride-phase tap tables: phase parity p, tap i -> kernel index / dy offset
+__host__ __device__ constexpr int ph_k(int p, int i) { return p == 0 ? 1 : (i == 0 ? 2 : 0); }
+__host__ __device__ constexpr int ph_a(int p, int i) { return p == 0 ? 0 : i; }
+
+// One MFMA sweep over the k-steps of a phase (PH) or of the whole 3x3 (PY =
+// PX = -1): step s -> tap (ky, kx), halo offset o, weight fragment index.
+template <bool PH, int PY, int PX>
+__device__ __forceinline__ void sweep(f32x4 (&acc)[MF][2], const bf16x8 (&bw)[2][KSTEPS], const char* hb,
+                                      const int (&qb)[MF], const uint32_t (&kt)[MF], int lchunk) {
+  using G = Geo<PH>;
+  constexpr int NTY = PH ? (PY ? 2 : 1) : 3, NTX = PH ? (PX ? 2 : 1) : 3;
+  constexpr int KS = 2 * NTY * NTX;
+  bf16x8 a[2][MF];
+  auto load_step = [&](int s, bf16x8 (&dst)[MF]) __attribute__((always_inline)) {
+    const int t = s >> 1, ty = t / NTX, tx = t - ty * NTX;
+    const int oy = PH ? ph_a(PY, ty) : ty, ox = PH ? ph_a(PX, tx) : tx;
+    const int o = oy * G::HC + ox;
+#pragma unroll
+    for (int f = 0; f < MF; ++f) {
+      const int key = (int)((kt[f] >> (4 * (o & 7))) & 15u);
+      const int ch = (lchunk + 4 * (s & 1)) ^ key;
+      dst[f] = *reinterpret_cast<const bf16x8*>(hb + qb[f] + o * (CI * 2) + (ch << 4));
+    }
+  };
+  load_step(0, a[0]);
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) load_step(s + 1, a[(s + 1) & 1]);
+    const int t = s >> 1, ty = t / NTX, tx = t - ty * NTX;
+    const int ky = PH ? ph_k(PY, ty) : ty, kx = PH ? ph_k(PX, tx) : tx;
+    const int ws = (ky * 3 + kx) * 2 + (s & 1);
+#pragma unroll
+    for (int f = 0; f < MF; ++f)
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf)
+        acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s & 1][f], bw[nf][ws], acc[f][nf], 0, 0, 0);
+    if (s + 1 < KS) {
+#pragma unroll
+      for (int f = 0; f < MF; ++f) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// K-half exchange through LDS, bf16 rounding into the output stage; returns
+// after the barrier that publishes the stage.
+template <int F0, int F1>
+__device__ __forceinline__ void send_frags(const f32x4 (&acc)[MF][2], f32x4* scr, int wn, int lane) {
+#pragma unroll
+  for (int f = F0; f < F1; ++f)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) scr[((wn * MF + f) * 2 + nf) * 64 + lane] = acc[f][nf];
+}
+
+template <int F0, int F1>
+__device__ __forceinline__ void finish_frags(const f32x4 (&acc)[MF][2], const f32x4* scr, bf16* ostage, int wn,
+                                             int lane, int l15, int lh) {
+#pragma unroll
+  for (int f = F0; f < F1; ++f)
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      const f32x4 o = scr[((wn * MF + f) * 2 + nf) * 64 + lane];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int p = f * 16 + 4 * lh + i;
+        const int ch = (4 * wn + 2 * nf + (l15 >> 3)) ^ stage_key(p);
+        ostage[p * CB + ch * 8 + (l15 & 7)] = (bf16)(acc[f][nf][i] + o[i]);
+      }
+    }
+}
+
+// K-half exchange through LDS (wk = 0 finalises fragments 0..3, wk = 1
+// fragments 4..6; the split is a wave-uniform branch over two statically
+// indexed loops -- a runtime-selected fragment index would put acc in
+// scratch), bf16 rounding into the output stage; returns after the barrier
+// that publishes the stage.
+__device__ __forceinline__ void exchange_to_stage(const f32x4 (&acc)[MF][2], f32x4* scr, bf16* ostage, int wkh,
+                                                  int wn, int lane, int l15, int lh) {
+  if (wkh == 0) send_frags<MF_LO, MF>(acc, scr, wn, lane);
+  else send_frags<0, MF_LO>(acc, scr, wn, lane);
+  __syncthreads();
+  if (wkh == 0) finish_frags<0, MF_LO>(acc, scr, ostage, wn, lane, l15, lh);
+  else finish_frags<MF_LO, MF>(acc, scr, ostage, wn, lane, l15, lh);
+  __syncthreads();
+}
+
+// PH: x = dy [N, 28 (H), 28, 128], y = dx [N, 2H, 56, 128]; wk = W^T
+// [dx ch][ky][kx][dy ch] (unflipped).  Otherwise x [N, H, 28, 128] -> y same.
+template <bool MOM, bool PH>
 __global__ __launch_bounds__(NT, 1) void conv3x3_c128_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ wk, bf16* __restrict__ y, float* __restrict__ part,
     double* zsums, int H, int tiles) {
-  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
-  f32x4* scr = reinterpret_cast<f32x4*>(smem + SCR_OFF);
-  bf16* ostage = reinterpret_cast<bf16*>(smem + STAGE_OFF);
-  float* mred = reinterpret_cast<float*>(smem + MRED_OFF);
+  using G = Geo<PH>;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  f32x4* scr = reinterpret_cast<f32x4*>(smem + G::SCR_OFF);
+  bf16* ostage = reinterpret_cast<bf16*>(smem + G::STAGE_OFF);
+  float* mred = reinterpret_cast<float*>(smem + G::MRED_OFF);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wkh = wave & 1, wn = wave >> 1;
   const int l15 = lane & 15, lh = lane >> 4;
   const int half = (int)gridDim.x >> 1;
-  const int cb = (int)blockIdx.x >= half ? 1 : 0;      // Cout chunk
+  const int cb = (int)blockIdx.x >= half ? 1 : 0;      // output-channel chunk
   const int rb = (int)blockIdx.x - cb * half;          // block within the chunk's half-grid
   const int tpi = H / R;
   if constexpr (MOM) {
@@ -142,10 +259,10 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c128_kernel(
   }
   const int t_begin = (int)((int64_t)tiles * rb / half);
   const int t_end = (int)((int64_t)tiles * (rb + 1) / half);
-  const Slots sl = make_slots(wave, lane);
-  if (t_begin < t_end) halo_issue(x, smem, t_begin, H, tpi, wave, sl);
+  const Slots<PH> sl = make_slots<PH>(wave, lane);
+  if (t_begin < t_end) halo_issue<PH>(x, smem, t_begin, H, tpi, wave, sl);
 
-  // B fragments: lane holds W[cout = 64 cb + 32 wn + 16 nf + l15][tap][cin = 64 wkh + 32 (s & 1) + 8 lh + j]
+  // B fragments: lane holds W[out = 64 cb + 32 wn + 16 nf + l15][tap][in = 64 wkh + 32 (s & 1) + 8 lh + j]
   bf16x8 bw[2][KSTEPS];
 #pragma unroll
   for (int nf = 0; nf < 2; ++nf) {
@@ -158,12 +275,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c128_kernel(
   // pixels q .. q+7 as a nibble table (read at tap offset o: nibble o & 7)
   int qb[MF];
   uint32_t kt[MF];
-  const int lchunk = 8 * wkh + lh;  // logical 16-B chunk of k-step 0 (cin 64 wkh + 8 lh ..)
+  const int lchunk = 8 * wkh + lh;  // logical 16-B chunk of k-step 0 (channels 64 wk + 8 lh ..)
 #pragma unroll
   for (int f = 0; f < MF; ++f) {
     const int p = f * 16 + l15;
     const int oy = p / W, ox = p - oy * W;
-    const int q = oy * HW2 + ox;
+    const int q = oy * G::HC + ox;
     qb[f] = q * (CI * 2);
     uint32_t t = 0;
 #pragma unroll
@@ -179,83 +296,29 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c128_kernel(
   for (int t = t_begin; t < t_end; ++t) {
 #pragma unroll
     for (int f = 0; f < MF; ++f) asm volatile("" : "+v"(kt[f]), "+v"(qb[f]));
-    // this tile's halo landed: the previous tile's >= 3 stores per thread were
-    // issued after it, so they may stay in flight
-    if (stored_prev) vmcnt<3>();
+    // this tile's halo landed: the previous tile's >= MIN_STORES stores per
+    // thread were issued after it, so they may stay in flight
+    if (stored_prev) vmcnt<G::MIN_STORES>();
     else vmcnt<0>();
     raw_barrier();
-    if (t + 1 < t_end) halo_issue(x, smem + (cur ^ 1) * BUF, t + 1, H, tpi, wave, sl);
-    const char* hb = smem + cur * BUF;
+    if (t + 1 < t_end) halo_issue<PH>(x, smem + (cur ^ 1) * G::BUF, t + 1, H, tpi, wave, sl);
+    const char* hb = smem + cur * G::BUF;
+    const int n = t / tpi;
+    const int r0 = (t - n * tpi) * R;
 
-    f32x4 acc[MF][2];
-#pragma unroll
-    for (int f = 0; f < MF; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    bf16x8 a[2][MF];
-    auto load_step = [&](int s, bf16x8 (&dst)[MF]) {
-      const int tap = s >> 1, kh = tap / 3, kw = tap - 3 * (tap / 3);
-      const int o = kh * HW2 + kw;
-#pragma unroll
-      for (int f = 0; f < MF; ++f) {
-        // logical chunk 8 wkh + 4 (s & 1) + lh (folded into qb), XOR the pixel key
-        const int key = (int)((kt[f] >> (4 * (o & 7))) & 15u);
-        const int ch = (lchunk + 4 * (s & 1)) ^ key;
-        dst[f] = *reinterpret_cast<const bf16x8*>(hb + qb[f] + o * (CI * 2) + (ch << 4));
-      }
-    };
-    load_step(0, a[0]);
-#pragma unroll
-    for (int s = 0; s < KSTEPS; ++s) {
-      if (s + 1 < KSTEPS) load_step(s + 1, a[(s + 1) & 1]);
-#pragma unroll
-      for (int f = 0; f < MF; ++f)
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s & 1][f], bw[nf][s], acc[f][nf], 0, 0, 0);
-      if (s + 1 < KSTEPS) {
-#pragma unroll
-        for (int f = 0; f < MF; ++f) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, MF, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-
-    // K-half exchange: wk = 0 finalises fragments 0..3, wk = 1 fragments 4..6
-#pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      const bool mine = (f < MF_LO) == (wkh == 0);
-      if (!mine)
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf) scr[((wn * MF + f) * 2 + nf) * 64 + lane] = acc[f][nf];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int f = 0; f < MF; ++f) {
-      const bool mine = (f < MF_LO) == (wkh == 0);
-      if (mine)
-#pragma unroll
-        for (int nf = 0; nf < 2; ++nf) {
-          const f32x4 o = scr[((wn * MF + f) * 2 + nf) * 64 + lane];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int p = f * 16 + 4 * lh + i;
-            const int ch = (4 * wn + 2 * nf + (l15 >> 3)) ^ stage_key(p);
-            ostage[p * CB + ch * 8 + (l15 & 7)] = (bf16)(acc[f][nf][i] + o[i]);
-          }
-        }
-    }
-    __syncthreads();
-    {
-      const int n = t / tpi;
-      const int r0 = (t - n * tpi) * R;
-      bf16* dst = y + (((int64_t)n * H + r0) * W) * CO + CB * cb;
+    // one epilogue: stage -> 16-B stores of this block's 64 channels per pixel
+    auto store_stage = [&](int py, int px) __attribute__((always_inline)) {
       for (int i = threadIdx.x; i < OUT_PIX * 8; i += NT) {
         const int sp = i >> 3;
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(ostage + sp * CB + (((i & 7) ^ stage_key(sp)) << 3));
-        *reinterpret_cast<bf16x8*>(dst + (int64_t)sp * CO + (i & 7) * 8) = v;
+        int64_t pix;
+        if constexpr (PH) {
+          const int m = sp / W, q = sp - m * W;
+          pix = ((int64_t)n * (2 * H) + 2 * (r0 + m) + py) * (2 * W) + 2 * q + px;
+        } else {
+          pix = ((int64_t)n * H + r0) * W + sp;
+        }
+        *reinterpret_cast<bf16x8*>(y + pix * CO + CB * cb + (i & 7) * 8) = v;
         if constexpr (MOM)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -264,6 +327,29 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c128_kernel(
             q8[j] = fmaf(fv, fv, q8[j]);
           }
       }
+    };
+    auto phase = [&](auto pyc, auto pxc) __attribute__((always_inline)) {
+      constexpr int PY = decltype(pyc)::value, PX = decltype(pxc)::value;
+      f32x4 acc[MF][2];
+#pragma unroll
+      for (int f = 0; f < MF; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      sweep<PH, PY, PX>(acc, bw, hb, qb, kt, lchunk);
+      exchange_to_stage(acc, scr, ostage, wkh, wn, lane, l15, lh);
+      store_stage(PY < 0 ? 0 : PY, PX < 0 ? 0 : PX);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using IN = std::integral_constant<int, -1>;
+    if constexpr (PH) {
+      // the next phase's stage writes come after its MFMA sweep and the
+      // exchange barrier, which every thread reaches only after finishing the
+      // previous phase's store loop
+      phase(I0{}, I0{});
+      phase(I0{}, I1{});
+      phase(I1{}, I0{});
+      phase(I1{}, I1{});
+    } else {
+      phase(IN{}, IN{});
     }
     stored_prev = true;
     cur ^= 1;
@@ -291,6 +377,18 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_c128_kernel(
   }
 }
 
+int grid_half(int tiles) {
+  int dev = 0, cus = 256;
+  DMP_HIP_CHECK(hipGetDevice(&dev));
+  DMP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return std::max(1, std::min(tiles, cus / 2));
+}
+
+void check_wmat(const at::Tensor& wmat, const char* who) {
+  TORCH_CHECK(wmat.scalar_type() == at::kBFloat16 && wmat.is_contiguous() && wmat.dim() == 2 &&
+                  wmat.size(0) == CO && wmat.size(1) == 9 * CI, who, ": wmat must be contiguous [128, 1152] bf16");
+}
+
 }  // namespace
 
 bool conv3x3_c128_supported(int64_t c, int64_t h, int64_t w) {
@@ -305,8 +403,8 @@ std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat
   TORCH_CHECK(conv3x3_c128_supported(x.size(1), x.size(2), x.size(3)) &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv3x3_c128: x must be [N, 128, H % 4 == 0, 28] channels_last");
-  TORCH_CHECK(wmat.scalar_type() == at::kBFloat16 && wmat.is_contiguous() && wmat.size(0) == CO &&
-                  wmat.size(1) == 9 * CI, "conv3x3_c128: wmat must be contiguous [128, 1152] bf16");
+  check_wmat(wmat, "conv3x3_c128");
+  TORCH_CHECK(wmat.device() == x.device(), "conv3x3_c128: device mismatch");
   const int64_t n = x.size(0), H = x.size(2);
   const int64_t tiles64 = n * (H / R);
   TORCH_CHECK(tiles64 < (1 << 30), "conv3x3_c128: too many tiles");
@@ -314,16 +412,13 @@ std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat
   auto y = at::empty({n * H * W, CO}, x.options());
   if (tiles == 0) return {y, at::zeros({moments ? 2 * CO + 1 : 0}, x.options().dtype(at::kDouble))};
   auto stream = at::hip::getCurrentHIPStream();
-  int dev = 0, cus = 256;
-  DMP_HIP_CHECK(hipGetDevice(&dev));
-  DMP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int half = std::max(1, std::min(tiles, cus / 2));
+  const int half = grid_half(tiles);
   const int grid = 2 * half;
   at::Tensor mom;
   if (moments) {
     mom = at::empty({2 * CO + 1}, x.options().dtype(at::kDouble));
     auto part = at::empty({2, half, CO}, x.options().dtype(at::kFloat));
-    hipLaunchKernelGGL(conv3x3_c128_kernel<true>, dim3(grid), dim3(NT), 0, stream,
+    hipLaunchKernelGGL((conv3x3_c128_kernel<true, false>), dim3(grid), dim3(NT), 0, stream,
                        reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<const bf16*>(wmat.data_ptr()),
                        reinterpret_cast<bf16*>(y.data_ptr()), part.data_ptr<float>(),
                        moments_zero_target(mom.data_ptr<double>(), half), (int)H, tiles);
@@ -331,12 +426,39 @@ std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat
                               stream);
   } else {
     mom = at::empty({0}, x.options().dtype(at::kDouble));
-    hipLaunchKernelGGL(conv3x3_c128_kernel<false>, dim3(grid), dim3(NT), 0, stream,
+    hipLaunchKernelGGL((conv3x3_c128_kernel<false, false>), dim3(grid), dim3(NT), 0, stream,
                        reinterpret_cast<const bf16*>(x.data_ptr()), reinterpret_cast<const bf16*>(wmat.data_ptr()),
                        reinterpret_cast<bf16*>(y.data_ptr()), nullptr, nullptr, (int)H, tiles);
   }
   DMP_HIP_CHECK(hipGetLastError());
   return {y, mom};
+}
+
+// Data gradient of a 3x3 / stride-2 / pad-1 128 -> 128 conv on a 2H x 56 input:
+// dy [N, 128, H, 28] bf16 channels_last (H % 4 == 0), wt = W permuted to
+// [cin][ky][kx][cout] (unflipped) flattened to [128, 1152].  Returns dx as
+// [N*2H*56, 128].
+at::Tensor conv3x3_c128_dgrad_s2(const at::Tensor& dy, const at::Tensor& wt) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4,
+              "conv3x3_c128_dgrad_s2: bf16 NCHW-shaped dy");
+  TORCH_CHECK(conv3x3_c128_supported(dy.size(1), dy.size(2), dy.size(3)) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_c128_dgrad_s2: dy must be [N, 128, H % 4 == 0, 28] channels_last");
+  check_wmat(wt, "conv3x3_c128_dgrad_s2");
+  TORCH_CHECK(wt.device() == dy.device(), "conv3x3_c128_dgrad_s2: device mismatch");
+  const int64_t n = dy.size(0), H = dy.size(2);
+  const int64_t tiles64 = n * (H / R);
+  TORCH_CHECK(tiles64 < (1 << 30) && n * 4 * H * W < (1LL << 31), "conv3x3_c128_dgrad_s2: too large");
+  const int tiles = (int)tiles64;
+  auto dx = at::empty({n * 4 * H * W, CI}, dy.options());
+  if (tiles == 0) return dx;
+  auto stream = at::hip::getCurrentHIPStream();
+  const int half = grid_half(tiles);
+  hipLaunchKernelGGL((conv3x3_c128_kernel<false, true>), dim3(2 * half), dim3(NT), 0, stream,
+                     reinterpret_cast<const bf16*>(dy.data_ptr()), reinterpret_cast<const bf16*>(wt.data_ptr()),
+                     reinterpret_cast<bf16*>(dx.data_ptr()), nullptr, nullptr, (int)H, tiles);
+  DMP_HIP_CHECK(hipGetLastError());
+  return dx;
 }
 
 }  // namespace dmp

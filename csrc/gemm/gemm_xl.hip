@@ -129,6 +129,20 @@ struct XlConv {
   int cin = 0, hi = 0, wi = 0, ho = 0, wo = 0, stride = 1, pad = 0, kw = 1;
 };
 
+// Output row map (XL_STORE only): GEMM row m = (n, oh, ow) of an ho x wo grid
+// is written to row (n, s*oh + oy, s*ow + ox) of an hi x wi image -- one
+// stride phase of a strided conv's data gradient.  s == 1: identity.
+struct XlOutMap {
+  int s = 1, ho = 1, wo = 1, hi = 1, wi = 1, oy = 0, ox = 0;
+};
+__device__ __forceinline__ int64_t xl_out_row(const XlOutMap& g, int row) {
+  if (g.s == 1) return row;
+  const int hw = g.ho * g.wo;
+  const int n = row / hw, r = row - n * hw;
+  const int oh = r / g.wo, ow = r - oh * g.wo;
+  return ((int64_t)n * g.hi + oh * g.s + g.oy) * g.wi + ow * g.s + g.ox;
+}
+
 // 16-B reads of padding taps land here (LDS-DMA cannot write zeros itself).
 __device__ __attribute__((aligned(16))) bf16 g_zero_row[128] = {};
 
@@ -148,6 +162,7 @@ struct XlArgs {
   const float *bmean, *binv, *bw, *bb;  // mask affine as in gemm_bf16.hip EPI_BNBWD
   CompactMap rmap;              // XL_BNBWD residual in compact stride-s form
   XlConv cv;                    // implicit-GEMM conv gather of A (PIPE 7)
+  XlOutMap omap;                // C row map (XL_STORE)
 };
 
 template <int BN, int EPI, int PIPE>
@@ -598,7 +613,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         f += r;
         v = __builtin_convertvector(f, bf16x8);
       }
-      *reinterpret_cast<bf16x8*>(p.C + (int64_t)row * p.ldc + col) = v;
+      const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
+      *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
     }
   }
   if constexpr (kMom) {
@@ -1348,6 +1364,52 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
   a.cv.cin = (int)cin; a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
   a.cv.stride = (int)stride; a.cv.pad = (int)pad; a.cv.kw = (int)kw;
   return xl_conv_run(a, x, mode, residual, bn_x, bn_y, mean, invstd, weight, bias, {});
+}
+
+// Data gradient of a 3x3 / stride-2 / pad-1 conv as four stride-phase
+// implicit GEMMs on the ping-pong kernel (no zero-filled dx, no zero taps):
+// dx[n, 2m + py, 2q + px, :] = sum over the taps (ky, kx) of phase (py, px) of
+// dy[n, m + a(ky), q + a(kx), :] @ W[:, :, ky, kx], with a(1) = 0 for the even
+// phase and a(2) = 0, a(0) = 1 for the odd one.  Each phase is a stride-1,
+// pad-0 conv over dy with a 1x1 / 1x2 / 2x1 / 2x2 kernel (the gather's bounds
+// check supplies the zero row / column past the edge), written through an
+// output row map straight into its pixels of dx.  wph[2 py + px]:
+// [Cin][taps_y][taps_x][Cout] flattened to [Cin, taps * Cout].
+// dy: [N, Cout, Ho, Wo] channels_last; returns dx as [N*hi*wi, Cin].
+at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>& wph, int64_t hi, int64_t wi) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_xl_dgrad_s2: dy must be 4-D bf16 channels_last");
+  TORCH_CHECK(wph.size() == 4, "conv_xl_dgrad_s2: four phase weight matrices");
+  const int64_t nb = dy.size(0), cout = dy.size(1), ho = dy.size(2), wo = dy.size(3);
+  TORCH_CHECK(cout % 64 == 0 && hi % 2 == 0 && wi % 2 == 0 && ho == hi / 2 && wo == wi / 2,
+              "conv_xl_dgrad_s2: even input size, Ho = H / 2, Cout % 64 == 0");
+  const int64_t cin = wph[0].size(0);
+  TORCH_CHECK(cin % 256 == 0, "conv_xl_dgrad_s2: Cin must be a multiple of 256 (full 256-wide tiles)");
+  TORCH_CHECK(nb * hi * wi < (1LL << 31), "conv_xl_dgrad_s2: too many pixels");
+  auto dx = at::empty({nb * hi * wi, cin}, dy.options());
+  hipStream_t s = at::hip::getCurrentHIPStream();
+  for (int ph = 0; ph < 4; ++ph) {
+    const int py = ph >> 1, px = ph & 1;
+    const int ty = py ? 2 : 1, tx = px ? 2 : 1;
+    const at::Tensor& w = wph[ph];
+    check_bf16_2d(w, "wph");
+    TORCH_CHECK(w.size(0) == cin && w.size(1) == ty * tx * cout && w.device() == dy.device(),
+                "conv_xl_dgrad_s2: wph[", ph, "] must be [Cin, ", ty * tx, " * Cout]");
+    XlArgs a{};
+    a.A = reinterpret_cast<const bf16*>(dy.data_ptr()); a.lda = cout;
+    a.B = reinterpret_cast<const bf16*>(w.data_ptr()); a.ldb = w.stride(0);
+    a.C = reinterpret_cast<bf16*>(dx.data_ptr()); a.ldc = cin;
+    a.M = (int)(nb * ho * wo); a.N = (int)cin; a.K = (int)(ty * tx * cout);
+    a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+    a.cv.cin = (int)cout; a.cv.hi = (int)ho; a.cv.wi = (int)wo; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
+    a.cv.stride = 1; a.cv.pad = 0; a.cv.kw = tx;
+    a.omap.s = 2; a.omap.ho = (int)ho; a.omap.wo = (int)wo; a.omap.hi = (int)hi; a.omap.wi = (int)wi;
+    a.omap.oy = py; a.omap.ox = px;
+    const int blocks = (int)((a.M + XBM - 1) / XBM) * (int)(cin / 256);
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_STORE, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+  }
+  DMP_HIP_CHECK(hipGetLastError());
+  return dx;
 }
 
 void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream);

@@ -90,6 +90,16 @@ def _halo_conv(C, kind: int):
     return C.conv3x3_c64 if kind == 64 else C.conv3x3_c128
 
 
+# The stride-2 block-0 3x3 of layer 2 (128 -> 128, 56 -> 28): data gradient as
+# its four stride phases on the c128 halo kernel (conv3x3_c128.hip, PH).
+_STATS["halo_dgrad_s2"] = 0
+
+
+def _halo_dgrad_s2_ok(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, h: int, w: int) -> bool:
+    return (_HALO3 and cin == 128 and cout == 128 and kh == 3 and kw == 3 and stride == 2 and pad == 1
+            and w == 56 and h % 8 == 0)
+
+
 # Weight gradients of every ResNet-50 3x3 (stride 1 and the stride-2 first
 # blocks) on the persistent halo-tiled kernel: dW in registers, dy / x halo
 # tiles streamed through LDS (csrc/conv/wgrad3x3.hip).  Stride 1 at batch 2048
@@ -113,6 +123,31 @@ def _xl_fwd(cout: int, kh: int, kw: int) -> bool:
 
 def _xl_dgrad(cin: int, kh: int, kw: int, stride: int) -> bool:
     return _XL3 and cin >= 256 and stride == 1 and kh == kw and kh > 1
+
+
+# Data gradient of the stride-2 3x3s of layers 3-4 (Cin = 256 / 512): four
+# stride-phase implicit GEMMs on the ping-pong kernel writing straight into
+# their pixels of dx (gemm_xl.hip conv_xl_dgrad_s2) -- no zero-filled dx and
+# no zero taps, where MIOpen zero-fills dx and then runs its igemm_bwd.
+_STATS["xl_dgrad_s2"] = 0
+_PHASE_TAPS = ((1,), (2, 0))  # even / odd output phase: kernel taps, in offset order a = 0, 1
+
+
+def _xl_dgrad_s2(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, h: int, w: int) -> bool:
+    return (_XL3 and cin % 256 == 0 and cout % 64 == 0 and kh == 3 and kw == 3 and stride == 2 and pad == 1
+            and h % 2 == 0 and w % 2 == 0)
+
+
+def _phase_weights(weight: torch.Tensor):
+    """[Cout, Cin, 3, 3] -> the four [Cin, taps * Cout] phase matrices (py, px)."""
+    cout, cin = weight.shape[:2]
+    w9 = weight.permute(1, 2, 3, 0).reshape(cin, 9, cout)
+    out = []
+    for py in (0, 1):
+        for px in (0, 1):
+            idx = [ky * 3 + kx for ky in _PHASE_TAPS[py] for kx in _PHASE_TAPS[px]]
+            out.append(w9[:, idx].reshape(cin, -1).contiguous())
+    return out
 
 
 def _out_size(h: int, k: int, s: int, p: int) -> int:
@@ -210,6 +245,14 @@ class _ConvIGFn(torch.autograd.Function):
             else:
                 dx2, _ = C.conv_xl(dy, wfl, kh, kw, 1, kh - 1 - pad, h, w, "store")
                 dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        elif ctx.needs_input_grad[0] and _halo_dgrad_s2_ok(cin, cout, kh, kw, stride, pad, h, w):
+            _STATS["halo_dgrad_s2"] += 1
+            wt = weight.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+            dx = C.conv3x3_c128_dgrad_s2(dy, wt).view(n, h, w, cin).permute(0, 3, 1, 2)
+        elif ctx.needs_input_grad[0] and _xl_dgrad_s2(cin, cout, kh, kw, stride, pad, h, w):
+            _STATS["xl_dgrad_s2"] += 1
+            dx2 = C.conv_xl_dgrad_s2(dy, _phase_weights(weight), h, w)
+            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and _halo_wgrad_ok(C, cin, cout, kh, kw, stride, pad, h, w):
             # persistent halo-tiled MFMA weight gradient (csrc/conv/wgrad3x3.hip)
             _STATS["halo_wgrad"] += 1
@@ -249,10 +292,12 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
             _halo_kind(x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[2],
                        x.shape[3]):
         _STATS["miopen_fwd"] += 1
-        if torch.is_grad_enabled() and weight.requires_grad and _halo_wgrad_ok(
-                _native.native(), x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding,
-                x.shape[2], x.shape[3]):
-            # MIOpen forward inside our Function so the backward can use the halo wgrad
+        geo = (x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[2],
+               x.shape[3])
+        if torch.is_grad_enabled() and (weight.requires_grad or x.requires_grad) and (
+                _halo_wgrad_ok(_native.native(), *geo) or _halo_dgrad_s2_ok(*geo) or _xl_dgrad_s2(*geo)):
+            # MIOpen forward inside our Function so the backward can use the halo
+            # weight gradient / the stride-phase data gradients
             y, _ = _ConvIGFn.apply(x, weight, stride, padding, None, None)
             return y, None
         return F.conv2d(x, weight, None, stride, padding, dilation, groups), None

@@ -133,6 +133,19 @@ def main():
                 if s == 1:
                     wfl = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
                     res["dgrad"]["xl"] = timeit(lambda: C.conv_xl(dy, wfl, k, k, 1, pad, h, h, "store"))
+                elif k == 3 and s == 2 and cin % 256 == 0 and hasattr(C, "conv_xl_dgrad_s2"):
+                    from distributed_model_parallel_amd.ops.conv_igemm import _phase_weights
+                    wph = _phase_weights(w)
+                    res["dgrad"]["xl"] = timeit(lambda: C.conv_xl_dgrad_s2(dy, wph, h, h))
+            from distributed_model_parallel_amd.ops.conv_igemm import _halo_conv, _halo_dgrad_s2_ok, _halo_kind
+            hk = _halo_kind(cin, cout, k, k, s, pad, h, h)
+            if _halo_dgrad_s2_ok(cin, cout, k, k, s, pad, h, h):
+                wt_ = w.permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+                res["dgrad"]["halo"] = timeit(lambda: C.conv3x3_c128_dgrad_s2(dy, wt_))
+            if hk:  # halo-tiled 3x3 (layers 1-2): forward with moments, dgrad over flipped weights
+                wfl = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+                res["fwd"]["halo"] = timeit(lambda: _halo_conv(C, hk)(x, _wmat(w).contiguous(), True))
+                res["dgrad"]["halo"] = timeit(lambda: _halo_conv(C, hk)(dy, wfl, False))
         if a.tn_ab and "ours" in res["wgrad"] and name != "stem":
             # A/B of the 128 x 256 TN tile: the narrow-tile time under its own column
             C.set_tn_wide(False)

@@ -18,7 +18,7 @@ CATS = [
     ("dmp fused SGD (ours)", ("sgd_flat",)),
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
     ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "split_reduce", "dw_fwd",
-                              "dw_dgrad", "dw_wgrad", "column_reduce", "conv3x3_c64", "gemm_tn_pp",
+                              "dw_dgrad", "dw_wgrad", "column_reduce", "conv3x3_c64", "conv3x3_c128", "gemm_tn_pp",
                               "wgrad3x3", "wgrad_reduce", "stem_fwd", "stem_wgrad", "partial_sum_kernel",
                               "s2d_kernel")),
     ("dmp attention (ours)", ("attn_fwd_kernel", "attn_bwd_kernel")),
@@ -50,6 +50,12 @@ def main():
     trace = glob.glob(os.path.join(a.dir, "*kernel_trace.csv"))
     stats = glob.glob(os.path.join(a.dir, "*kernel_stats.csv"))
     rows = list(csv.DictReader(open(trace[0]))) if trace else []
+    dbs = glob.glob(os.path.join(a.dir, "*_results.db"))
+    if not rows and dbs:  # rocprofv3's default (rocpd sqlite) output
+        import sqlite3
+        con = sqlite3.connect(dbs[0])
+        rows = [{"Kernel_Name": n, "Start_Timestamp": str(st), "End_Timestamp": str(en)}
+                for n, st, en in con.execute("select name, start, end from kernels")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     out = sys.stdout
     if a.title:
