@@ -16,7 +16,8 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                                          double momentum, double eps,
                                          const c10::optional<at::Tensor>& residual, bool relu,
                                          int64_t C,
-                                         const c10::optional<at::Tensor>& num_batches_tracked);
+                                         const c10::optional<at::Tensor>& num_batches_tracked,
+                                         bool out_moments);
 std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& running_mean,
                                       const at::Tensor& running_var,
                                       const c10::optional<at::Tensor>& weight,
@@ -53,14 +54,19 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& epi_shift,
                                 const c10::optional<at::Tensor>& residual, bool relu,
                                 const std::vector<int64_t>& a_map,
-                                const std::vector<int64_t>& c_map);
+                                const std::vector<int64_t>& c_map,
+                                const c10::optional<at::Tensor>& a2);
 std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& residual,
-                                      const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
-                                      const at::Tensor& mean, const c10::optional<at::Tensor>& invstd,
+                                      const c10::optional<at::Tensor>& bn_x,
+                                      const c10::optional<at::Tensor>& bn_y,
+                                      const c10::optional<at::Tensor>& mean,
+                                      const c10::optional<at::Tensor>& invstd,
                                       const c10::optional<at::Tensor>& weight,
                                       const c10::optional<at::Tensor>& bias,
-                                      const std::vector<int64_t>& res_map);
+                                      const std::vector<int64_t>& res_map,
+                                      const c10::optional<at::Tensor>& a2,
+                                      const c10::optional<at::Tensor>& ebias);
 // cross_entropy.hip
 std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& x, const at::Tensor& target,
                                           int64_t ignore_index);
@@ -130,7 +136,11 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& invstd,
                                      const c10::optional<at::Tensor>& weight,
                                      const c10::optional<at::Tensor>& bias,
-                                     const std::vector<int64_t>& res_map);
+                                     const std::vector<int64_t>& res_map,
+                                     const c10::optional<at::Tensor>& a2,
+                                     const c10::optional<at::Tensor>& ebias,
+                                     const c10::optional<at::Tensor>& scale,
+                                     const c10::optional<at::Tensor>& shift, bool relu);
 // attention.hip
 bool attention_supported(int64_t S, int64_t head_dim);
 std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale);
@@ -179,7 +189,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_apply", &dmp::bn_forward_apply, py::arg("x"), py::arg("sums"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
         py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("C"),
-        py::arg("num_batches_tracked") = py::none());
+        py::arg("num_batches_tracked") = py::none(), py::arg("out_moments") = false);
   m.def("bn_eval_apply", &dmp::bn_eval_apply);
   m.def("bn_finalize", &dmp::bn_finalize, py::arg("sums"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
@@ -197,7 +207,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
         py::arg("residual") = py::none(), py::arg("relu") = false,
-        py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{});
+        py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},
+        py::arg("a2") = py::none());
 
   m.def("cross_entropy_fwd", &dmp::cross_entropy_fwd, py::arg("x"), py::arg("target"),
         py::arg("ignore_index") = -100);
@@ -205,7 +216,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lse"), py::arg("stats"), py::arg("ignore_index") = -100);
   m.def("gemm_nt_bnbwd", &dmp::gemm_nt_bnbwd, py::arg("A"), py::arg("B"), py::arg("residual"),
         py::arg("bn_x"), py::arg("bn_y"), py::arg("mean"), py::arg("invstd"), py::arg("weight"),
-        py::arg("bias"), py::arg("res_map") = std::vector<int64_t>{});
+        py::arg("bias"), py::arg("res_map") = std::vector<int64_t>{}, py::arg("a2") = py::none(),
+        py::arg("ebias") = py::none());
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
@@ -282,7 +294,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_xl_conv", &dmp::gemm_xl_conv, py::arg("A"), py::arg("B"), py::arg("mode"),
         py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
-        py::arg("bias") = py::none(), py::arg("res_map") = std::vector<int64_t>{});
+        py::arg("bias") = py::none(), py::arg("res_map") = std::vector<int64_t>{},
+        py::arg("a2") = py::none(), py::arg("ebias") = py::none(), py::arg("scale") = py::none(),
+        py::arg("shift") = py::none(), py::arg("relu") = false,
+        "wide 1x1-conv GEMM with conv epilogues: moments | add | bnbwd | affine (scale, shift, residual, relu); "
+        "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 7, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
 

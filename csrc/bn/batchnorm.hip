@@ -236,13 +236,26 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
 // also save mean/invstd and update running stats.  Otherwise eval mode --
 // coefficients from running stats.
 // -------------------------------------------------------------------------
-template <typename T, bool RELU, bool RES, bool FROM_SUMS, bool NT = false>
+template <typename T, bool RELU, bool RES, bool FROM_SUMS, bool NT, bool OSUM>
+__device__ __forceinline__ void bn_apply_rows(
+    const T* __restrict__ x, const T* __restrict__ res, const double* __restrict__ sums,
+    const float* __restrict__ weight, const float* __restrict__ bias,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
+    int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, const Layout& L, int lr, int cvec,
+    float (&os)[Vec16<T>::N], float (&oq)[Vec16<T>::N]);
+
+// OSUM: also reduce per-block partials of the column sums (and sums of
+// squares) of the STORED output -- the colsum a BN-folded consumer needs
+// (ops/bn_fold.py: the next BN's mean is W @ colsum(y) / M) without a pass.
+template <typename T, bool RELU, bool RES, bool FROM_SUMS, bool NT = false, bool OSUM = false>
 __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     const T* __restrict__ x, const T* __restrict__ res, const double* __restrict__ sums,
     const float* __restrict__ weight, const float* __restrict__ bias,
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
     int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
-    float* __restrict__ save_invstd, int64_t* __restrict__ num_batches_tracked) {
+    float* __restrict__ save_invstd, int64_t* __restrict__ num_batches_tracked,
+    float* __restrict__ opart = nullptr, double* __restrict__ ozsums = nullptr) {
   // BatchNorm's step counter rides along (one lane), instead of its own launch
   if (num_batches_tracked != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     *num_batches_tracked += 1;
@@ -251,7 +264,34 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
   const int tid = threadIdx.x;
   const int lc = tid % L.tc, lr = tid / L.tc;
   const int cvec = blockIdx.y * L.tc + lc;
+  if constexpr (OSUM) {
+    zero_moments(ozsums, 2 * C);
+    float os[VEC], oq[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) { os[i] = 0.f; oq[i] = 0.f; }
+    if (lr < L.rpi && cvec < L.cv)
+      bn_apply_rows<T, RELU, RES, FROM_SUMS, NT, true>(x, res, sums, weight, bias, running_mean, running_var,
+                                                       momentum, eps, M, C, rows_per_block, y, save_mean,
+                                                       save_invstd, L, lr, cvec, os, oq);
+    block_combine_store<VEC>(os, oq, L, C, opart);
+    return;
+  }
   if (lr >= L.rpi || cvec >= L.cv) return;
+  float os[VEC], oq[VEC];
+  bn_apply_rows<T, RELU, RES, FROM_SUMS, NT, false>(x, res, sums, weight, bias, running_mean, running_var,
+                                                    momentum, eps, M, C, rows_per_block, y, save_mean,
+                                                    save_invstd, L, lr, cvec, os, oq);
+}
+
+template <typename T, bool RELU, bool RES, bool FROM_SUMS, bool NT, bool OSUM>
+__device__ __forceinline__ void bn_apply_rows(
+    const T* __restrict__ x, const T* __restrict__ res, const double* __restrict__ sums,
+    const float* __restrict__ weight, const float* __restrict__ bias,
+    float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
+    int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
+    float* __restrict__ save_invstd, const Layout& L, int lr, int cvec,
+    float (&os)[Vec16<T>::N], float (&oq)[Vec16<T>::N]) {
+  constexpr int VEC = Vec16<T>::N;
   float sc[VEC], sh[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
@@ -295,6 +335,12 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
       float t = fmaf(v[i], sc[i], sh[i]), t2 = fmaf(v2[i], sc[i], sh[i]);
       if (RES) { t += rv[i]; t2 += rv2[i]; }
       if (RELU) { t = fmaxf(t, 0.f); t2 = fmaxf(t2, 0.f); }
+      if constexpr (OSUM) {  // moments of the values as stored
+        t = (float)(T)t;
+        t2 = (float)(T)t2;
+        os[i] += t + t2;
+        oq[i] = fmaf(t, t, fmaf(t2, t2, oq[i]));
+      }
       v[i] = t;
       v2[i] = t2;
     }
@@ -311,6 +357,11 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
       float t = fmaf(v[i], sc[i], sh[i]);
       if (RES) t += rv[i];
       if (RELU) t = fmaxf(t, 0.f);
+      if constexpr (OSUM) {
+        t = (float)(T)t;
+        os[i] += t;
+        oq[i] = fmaf(t, t, oq[i]);
+      }
       v[i] = t;
     }
     st16<NT>(y + o, v);
@@ -537,7 +588,8 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                                          double momentum, double eps,
                                          const c10::optional<at::Tensor>& residual, bool relu,
                                          int64_t C,
-                                         const c10::optional<at::Tensor>& num_batches_tracked) {
+                                         const c10::optional<at::Tensor>& num_batches_tracked,
+                                         bool out_moments) {
   check_input(x, C, "x");
   TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.numel() == 2 * C + 1, "bad moments");
   int64_t* nbt = nullptr;
@@ -552,7 +604,30 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
   auto stream = at::hip::getCurrentHIPStream();
   const bool has_res = residual.has_value() && residual->defined();
   if (has_res) check_input(*residual, C, "residual");
-  if (M > 0) {
+  at::Tensor osums;
+  if (out_moments) {
+    TORCH_CHECK(relu && !has_res && x.scalar_type() == at::kBFloat16,
+                "out_moments: bf16 BN + ReLU without residual only");
+    osums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
+    if (M == 0) osums.zero_();
+  }
+  if (M > 0 && out_moments) {
+    Grid g = plan(M, (int)C, vec_of(x));
+    auto part = at::empty({2, (int64_t)g.grid.x, C}, x.options().dtype(at::kFloat));
+    double* zt = moments_zero_target(osums.data_ptr<double>(), (int)g.grid.x);
+    using T = __bf16;
+#define DMP_BN_FWD_OS(NT)                                                                          \
+  hipLaunchKernelGGL((bn_apply_kernel<T, true, false, true, NT, true>), g.grid, dim3(kThreads), 0,   \
+                     stream, ptr<T>(x), nullptr, sums.data_ptr<double>(), fptr(weight), fptr(bias), \
+                     fptr(running_mean), fptr(running_var), (float)momentum, (float)eps, M, (int)C, \
+                     g.rows_per_block, ptr<T>(y), saved.data_ptr<float>(), saved.data_ptr<float>() + C, \
+                     nbt, part.data_ptr<float>(), zt)
+    if (streaming(M, C)) DMP_BN_FWD_OS(true);
+    else DMP_BN_FWD_OS(false);
+#undef DMP_BN_FWD_OS
+    bn_reduce_partials_launch(part.data_ptr<float>(), (int)g.grid.x, (int)C, osums.data_ptr<double>(),
+                              (double)M, stream);
+  } else if (M > 0) {
     Grid g = plan(M, (int)C, vec_of(x));
     dispatch_t(x, [&](auto tag) {
       using T = decltype(tag);
@@ -573,6 +648,7 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
 #undef DMP_BN_FWD1
     });
   }
+  if (out_moments) return {y, saved[0], saved[1], osums};
   return {y, saved[0], saved[1]};
 }
 

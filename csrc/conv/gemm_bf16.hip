@@ -118,6 +118,10 @@ struct NtArgs {
   // computed per column in the epilogue (no coefficient kernels on the host side)
   const float *bmean, *binv, *bw, *bb;
   CompactMap rmap;              // EPI_BNBWD residual R in compact stride-s form
+  // Second A source (non-CONV): K columns k >= K1 read A2[row, k - K1] -- the
+  // operand [dz | a] of a BN-folded data gradient (ops/bn_fold.py).  K1 % 8 == 0.
+  const bf16* A2; int64_t lda2; int K1;
+  const float* ebias;           // EPI_BNBWD: per-column bias added to the GEMM output
 };
 
 // NT = WAVES_M*WAVES_N*64 threads: 4 waves (2 blocks/CU) or 8 waves (256-row
@@ -179,6 +183,7 @@ void gemm_nt_kernel(const NtArgs p) {
   // one row pointer each.  Implicit-GEMM conv: the output pixel (n, oh, ow) of
   // each row; the tap of a K tile picks the input pixel (or zero padding).
   const bf16* arow[A_VECS];
+  const bf16* arow2[A_VECS];
   int pn[A_VECS], ph[A_VECS], pw[A_VECS];
 #pragma unroll
   for (int i = 0; i < A_VECS; ++i) {
@@ -195,6 +200,7 @@ void gemm_nt_kernel(const NtArgs p) {
       }
     } else {
       arow[i] = row < M ? A + map_row(amap, row) * lda : nullptr;
+      arow2[i] = (row < M && p.A2) ? p.A2 + map_row(amap, row) * p.lda2 - p.K1 : nullptr;
     }
   }
   bool aval[A_VECS];
@@ -244,10 +250,11 @@ void gemm_nt_kernel(const NtArgs p) {
           ra[i] = bf16x8{};
       }
     } else {
+      const bool second = p.A2 && k >= p.K1;  // [A | A2] K concatenation
 #pragma unroll
       for (int i = 0; i < A_VECS; ++i) {
         aval[i] = kin && arow[i];
-        if (aval[i]) ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + k);
+        if (aval[i]) ra[i] = *reinterpret_cast<const bf16x8*>((second ? arow2[i] : arow[i]) + k);
         else ra[i] = bf16x8{};
       }
     }
@@ -363,17 +370,19 @@ void gemm_nt_kernel(const NtArgs p) {
   float msum[8], msq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; }
-  float bmu[8], bsc[8], bsh[8];
+  float bmu[8], bsc[8], bsh[8], ebv[8];
   const bf16* __restrict__ bnx = p.bx;
   const bf16* __restrict__ bny = p.bny;
   const int64_t ldbx = p.ldbx, ldby = p.ldby;
   const CompactMap rmap = p.rmap;
+  const bool has_ebias = p.ebias != nullptr;
   if constexpr (EPI == EPI_BNBWD) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bmu[j] = col_ok ? p.bmean[col + j] : 0.f;
+      bmu[j] = (col_ok && p.bmean) ? p.bmean[col + j] : 0.f;
       bsc[j] = (col_ok && !p.bny) ? p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f) : 0.f;
       bsh[j] = (col_ok && !p.bny) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
+      ebv[j] = (col_ok && p.ebias) ? p.ebias[col + j] : 0.f;
     }
   }
 #pragma unroll
@@ -395,6 +404,11 @@ void gemm_nt_kernel(const NtArgs p) {
       }
       if constexpr (EPI == EPI_BNBWD) {
         f32x8 g = __builtin_convertvector(v, f32x8);
+        if (has_ebias) {  // BN-folded data gradient: the constant term of the folded BN backward
+          g += f32x8{ebv[0], ebv[1], ebv[2], ebv[3], ebv[4], ebv[5], ebv[6], ebv[7]};
+          v = __builtin_convertvector(g, bf16x8);
+          g = __builtin_convertvector(v, f32x8);
+        }
         if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
           const int64_t rr = compact_row(rmap, row);
           if (rr >= 0)
@@ -402,8 +416,11 @@ void gemm_nt_kernel(const NtArgs p) {
           v = __builtin_convertvector(g, bf16x8);
           g = __builtin_convertvector(v, f32x8);
         }
-        const f32x8 xv =
-            __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bnx + (int64_t)row * ldbx + col), f32x8);
+        // bnx null (the BN input was never materialised, ops/bn_fold.py): mask
+        // from y, only sum dz is reduced (sum dz*(x-mean) is formed from dz^T a)
+        f32x8 xv{};
+        if (bnx)
+          xv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bnx + (int64_t)row * ldbx + col), f32x8);
         f32x8 yv;
         if (bny)
           yv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bny + (int64_t)row * ldby + col), f32x8);
@@ -413,7 +430,7 @@ void gemm_nt_kernel(const NtArgs p) {
           const float dz = on ? g[j] : 0.f;
           g[j] = dz;
           msum[j] += dz;
-          msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+          if (bnx) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
         }
         v = __builtin_convertvector(g, bf16x8);  // exact: dz is G or 0
       }
@@ -971,9 +988,15 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   } else if (mode == "affine" || mode == "add") {
     epi = EPI_AFFINE;
     if (mode == "affine") {
-      TORCH_CHECK(epi_scale.has_value() && epi_shift.has_value(), "affine epilogue needs scale/shift");
-      a.epi_s = epi_scale->data_ptr<float>();
-      a.epi_t = epi_shift->data_ptr<float>();
+      const bool hs = epi_scale.has_value() && epi_scale->defined();
+      const bool ht = epi_shift.has_value() && epi_shift->defined();
+      TORCH_CHECK(hs || ht, "affine epilogue needs scale and/or shift (missing = 1 / 0)");
+      for (const auto* t : {&epi_scale, &epi_shift})
+        if (t->has_value() && (*t)->defined())
+          TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() == a.N,
+                      "affine coefficients must be contiguous fp32 [N]");
+      a.epi_s = hs ? epi_scale->data_ptr<float>() : nullptr;
+      a.epi_t = ht ? epi_shift->data_ptr<float>() : nullptr;
     } else {
       TORCH_CHECK(residual.has_value() && residual->defined(), "add epilogue needs a residual");
     }
@@ -997,6 +1020,19 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
 
 }  // namespace
 
+namespace {
+// [A | A2] along K: A2 [rows(A), K2] row-major; the GEMM's K becomes K(A) + K2.
+void set_second_source(NtArgs& a, const at::Tensor& A, const c10::optional<at::Tensor>& a2) {
+  if (!(a2.has_value() && a2->defined())) return;
+  check_operand(*a2, "a2");
+  TORCH_CHECK(a2->size(0) == A.size(0) && a2->size(1) % 8 == 0, "a2 must be [rows(A), K2], K2 % 8 == 0");
+  a.A2 = reinterpret_cast<const bf16*>(a2->data_ptr());
+  a.lda2 = a2->stride(0);
+  a.K1 = a.K;
+  a.K += (int)a2->size(1);
+}
+}  // namespace
+
 // C = prologue(A) @ B^T with an optional fused epilogue.  Returns (C, moments-or-undefined).
 //   A [M, K] bf16, B [N, K] bf16 (both K-contiguous), K % 8 == 0, N % 8 == 0.
 //   pro_scale/pro_shift [K] fp32: A' = relu(A*s + t)
@@ -1004,6 +1040,7 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
 //   (epi_scale/epi_shift [N], optional residual [M, N], relu flag) | "add"
 //   (C = acc + residual).
 //   a_map / c_map: [s, Ho, Wo, Hi, Wi] strided row maps for A reads / C writes.
+//   a2: optional second A source, [A | a2] concatenated along K (B is [N, K + K2]).
 std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& pro_scale,
                                 const c10::optional<at::Tensor>& pro_shift, const std::string& mode,
@@ -1011,7 +1048,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& epi_shift,
                                 const c10::optional<at::Tensor>& residual, bool relu,
                                 const std::vector<int64_t>& a_map,
-                                const std::vector<int64_t>& c_map) {
+                                const std::vector<int64_t>& c_map,
+                                const c10::optional<at::Tensor>& a2) {
   check_operand(A, "A");
   check_operand(B, "B");
   NtArgs a{};
@@ -1029,8 +1067,10 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
   a.M = (int)m64;
   a.K = (int)A.size(1);
   a.N = (int)B.size(0);
+  set_second_source(a, A, a2);
   TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
   TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
+  TORCH_CHECK(!a.A2 || !(pro_scale.has_value() && pro_scale->defined()), "a2 has no prologue variant");
   if (pro_scale.has_value() && pro_scale->defined())
     TORCH_CHECK(pro_scale->numel() == a.K, "prologue coefficients must have K entries");
   at::Tensor C;
@@ -1174,31 +1214,43 @@ CompactMap parse_compact(const std::vector<int64_t>& g, int64_t M) {
 
 std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& residual,
-                                      const at::Tensor& bn_x, const c10::optional<at::Tensor>& bn_y,
-                                      const at::Tensor& mean, const c10::optional<at::Tensor>& invstd,
+                                      const c10::optional<at::Tensor>& bn_x,
+                                      const c10::optional<at::Tensor>& bn_y,
+                                      const c10::optional<at::Tensor>& mean,
+                                      const c10::optional<at::Tensor>& invstd,
                                       const c10::optional<at::Tensor>& weight,
                                       const c10::optional<at::Tensor>& bias,
-                                      const std::vector<int64_t>& res_map) {
+                                      const std::vector<int64_t>& res_map,
+                                      const c10::optional<at::Tensor>& a2,
+                                      const c10::optional<at::Tensor>& ebias) {
   check_operand(A, "A");
   check_operand(B, "B");
-  check_operand(bn_x, "bn_x");
+  const bool has_x = bn_x.has_value() && bn_x->defined();
+  const bool has_y = bn_y.has_value() && bn_y->defined();
+  TORCH_CHECK(has_x || has_y, "bnbwd needs the BN input x and/or output y");
   NtArgs a{};
   a.rmap = parse_compact(res_map, A.size(0));
   a.M = (int)A.size(0);
   a.K = (int)A.size(1);
   a.N = (int)B.size(0);
+  set_second_source(a, A, a2);
   TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
   TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
-  TORCH_CHECK(bn_x.size(0) == a.M && bn_x.size(1) == a.N, "bn_x must be [M, N]");
   auto f32vec = [&](const at::Tensor& t, const char* name) {
     TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == a.N,
                 name, " must be a contiguous fp32 [N] GPU tensor");
     return t.data_ptr<float>();
   };
-  a.bx = reinterpret_cast<const bf16*>(bn_x.data_ptr());
-  a.ldbx = bn_x.stride(0);
-  a.bmean = f32vec(mean, "mean");
-  if (bn_y.has_value() && bn_y->defined()) {
+  if (has_x) {
+    check_operand(*bn_x, "bn_x");
+    TORCH_CHECK(bn_x->size(0) == a.M && bn_x->size(1) == a.N, "bn_x must be [M, N]");
+    a.bx = reinterpret_cast<const bf16*>(bn_x->data_ptr());
+    a.ldbx = bn_x->stride(0);
+    TORCH_CHECK(mean.has_value() && mean->defined(), "sum dz*(x-mean) needs the BN mean");
+    a.bmean = f32vec(*mean, "mean");
+  }
+  if (ebias.has_value() && ebias->defined()) a.ebias = f32vec(*ebias, "ebias");
+  if (has_y) {
     check_operand(*bn_y, "bn_y");
     TORCH_CHECK(bn_y->size(0) == a.M && bn_y->size(1) == a.N, "bn_y must be [M, N]");
     a.bny = reinterpret_cast<const bf16*>(bn_y->data_ptr());

@@ -51,7 +51,10 @@ constexpr int XBM = 256, XBK = 64, XTHREADS = 512;
 enum XlEpi { XL_STORE = 0, XL_BIAS = 1, XL_BIAS_GELU = 2, XL_DGELU = 3, XL_BIAS_RES = 4,
              // conv epilogues (same semantics as gemm_bf16.hip's EPI_MOMENTS /
              // EPI_AFFINE "add" / EPI_BNBWD), for the wide 1x1 conv GEMMs
-             XL_MOMENTS = 5, XL_ADD = 6, XL_BNBWD = 7 };
+             XL_MOMENTS = 5, XL_ADD = 6, XL_BNBWD = 7,
+             // C = act(acc * s[n] + t[n] (+ R)): conv + training-mode BN (+ residual)
+             // + ReLU when the BN statistics were formed before the GEMM (ops/bn_fold.py)
+             XL_AFFINE = 8 };
 
 using gptr_t = const __attribute__((address_space(1))) void*;
 using lptr_t = __attribute__((address_space(3))) void*;
@@ -163,6 +166,12 @@ struct XlArgs {
   CompactMap rmap;              // XL_BNBWD residual in compact stride-s form
   XlConv cv;                    // implicit-GEMM conv gather of A (PIPE 7)
   XlOutMap omap;                // C row map (XL_STORE)
+  // second A source (plain GEMM): K columns k >= K1 come from A2[row, k - K1]
+  // (the [dz | a] operand of a BN-folded data gradient); K1 % 64 == 0
+  const bf16* A2; int64_t lda2; int K1;
+  const float* ebias;           // XL_BNBWD: per-column constant added to the GEMM output
+  const float *esc, *esh;       // XL_AFFINE coefficients (null: 1 / 0)
+  int erelu;                    // XL_AFFINE ReLU
 };
 
 template <int BN, int EPI, int PIPE>
@@ -199,11 +208,13 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   const int srow = lane >> 2;
   const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
   const bf16* asrc[NA];
+  const bf16* asrc2[NA];
   const bf16* bsrc[NB];
 #pragma unroll
   for (int q = 0; q < NA; ++q) {
     const int r = (wave * NA + q) * 16 + srow;
     asrc[q] = A + (int64_t)min(m0 + r, M - 1) * lda + schunk * 8;
+    asrc2[q] = p.A2 ? p.A2 + (int64_t)min(m0 + r, M - 1) * p.lda2 + schunk * 8 - p.K1 : nullptr;
   }
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
@@ -215,8 +226,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   auto stage_a = [&](int ks, int kt, int buf) {
     char* dst = a_region(ks, buf) + wave * NA * 1024;
     const int koff = kt * XBK + ks * 32;
+    const bool second = p.A2 && koff >= p.K1;
 #pragma unroll
-    for (int q = 0; q < NA; ++q) glds16(asrc[q] + koff, dst + q * 1024);
+    for (int q = 0; q < NA; ++q) glds16((second ? asrc2[q] : asrc[q]) + koff, dst + q * 1024);
   };
   auto stage_b = [&](int ks, int kt, int buf) {
     char* dst = b_region(ks, buf) + wave * NB * 1024;
@@ -310,6 +322,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   static_assert(BN == 256, "ping-pong schedule is written for 256 x 256 tiles");
   const int pks = wave >> 2;  // k32 half carried by this wave's two copies of a unit
   const bf16* pa[2][2];
+  const bf16* pa2[2][2];
   const bf16* pb[2][2];
   int oa[2][2], ob[2][2];
 #pragma unroll
@@ -319,6 +332,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       const int j = (2 * wave + q) & 7;
       const int ba = (j & 3) + 8 * (j >> 2) + 4 * v, bb = (j & 1) + 4 * (j >> 1) + 2 * v;
       pa[v][q] = A + (int64_t)min(m0 + ba * 16 + srow, M - 1) * lda + schunk * 8 + pks * 32;
+      pa2[v][q] = p.A2 ? p.A2 + (int64_t)min(m0 + ba * 16 + srow, M - 1) * p.lda2 + schunk * 8 + pks * 32 - p.K1
+                       : nullptr;
       pb[v][q] = B + (int64_t)min(n0 + bb * 16 + srow, N - 1) * ldb + schunk * 8 + pks * 32;
       oa[v][q] = ba * 1024;
       ob[v][q] = bb * 1024;
@@ -360,10 +375,11 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         return;
       }
     }
+    const bool second = p.A2 && koff >= p.K1;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if constexpr (U == 0 || U == 3)
-        glds16(pa[U == 3][q] + koff, a_region(pks, buf) + oa[U == 3][q]);
+        glds16((second ? pa2[U == 3][q] : pa[U == 3][q]) + koff, a_region(pks, buf) + oa[U == 3][q]);
       else
         glds16(pb[U == 2][q] + koff, b_region(pks, buf) + ob[U == 2][q]);
     }
@@ -537,14 +553,24 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   constexpr int CV = BN / 8, RPP = XTHREADS / CV;
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
-  float msum[8], msq[8], bmu[8], bsc[8], bsh[8];
+  float msum[8], msq[8], bmu[8], bsc[8], bsh[8], ebv[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = 0.f; }
+  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = ebv[j] = 0.f; }
+  if constexpr (EPI == XL_AFFINE) {
+    if (col < N) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bsc[j] = p.esc ? p.esc[col + j] : 1.f;
+        bsh[j] = p.esh ? p.esh[col + j] : 0.f;
+      }
+    }
+  }
   if constexpr (EPI == XL_BNBWD) {
     if (col < N) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        bmu[j] = p.bmean[col + j];
+        bmu[j] = p.bmean ? p.bmean[col + j] : 0.f;
+        ebv[j] = p.ebias ? p.ebias[col + j] : 0.f;
         if (!p.bny) {
           bsc[j] = p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f);
           bsh[j] = (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j];
@@ -570,8 +596,23 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         f32x8 f = __builtin_convertvector(v, f32x8);
         f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
         v = __builtin_convertvector(f, bf16x8);
+      } else if constexpr (EPI == XL_AFFINE) {
+        f32x8 f = __builtin_convertvector(v, f32x8);
+        f32x8 r{};
+        if (p.R) r = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = fmaf(f[j], bsc[j], bsh[j]) + r[j];
+          f[j] = p.erelu ? fmaxf(t, 0.f) : t;
+        }
+        v = __builtin_convertvector(f, bf16x8);
       } else if constexpr (EPI == XL_BNBWD) {
         f32x8 g = __builtin_convertvector(v, f32x8);
+        if (p.ebias) {  // BN-folded data gradient: constant term of the folded BN backward
+          g += f32x8{ebv[0], ebv[1], ebv[2], ebv[3], ebv[4], ebv[5], ebv[6], ebv[7]};
+          v = __builtin_convertvector(g, bf16x8);
+          g = __builtin_convertvector(v, f32x8);
+        }
         if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
           const int64_t rr = compact_row(p.rmap, row);
           if (rr >= 0)
@@ -579,8 +620,10 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           v = __builtin_convertvector(g, bf16x8);
           g = __builtin_convertvector(v, f32x8);
         }
-        const f32x8 xv =
-            __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bx + (int64_t)row * p.ldbx + col), f32x8);
+        // bx null: BN input never materialised (ops/bn_fold.py) -- mask from y, sum dz only
+        f32x8 xv{};
+        if (p.bx)
+          xv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bx + (int64_t)row * p.ldbx + col), f32x8);
         f32x8 yv{};
         if (p.bny)
           yv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bny + (int64_t)row * p.ldby + col), f32x8);
@@ -590,7 +633,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           const float dz = on ? g[j] : 0.f;
           g[j] = dz;
           msum[j] += dz;
-          msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+          if (p.bx) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
         }
         v = __builtin_convertvector(g, bf16x8);
       } else if constexpr (EPI == XL_BIAS_GELU) {
@@ -1229,12 +1272,15 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
                                     const c10::optional<at::Tensor>& invstd,
                                     const c10::optional<at::Tensor>& weight,
                                     const c10::optional<at::Tensor>& bias,
-                                    const std::vector<int64_t>& res_map) {
+                                    const std::vector<int64_t>& res_map,
+                                    const c10::optional<at::Tensor>& ebias = c10::nullopt,
+                                    bool relu_flag = false) {
   const int64_t M = a.M, N = a.N;
   int epi;
   if (mode == "moments") epi = XL_MOMENTS;
   else if (mode == "add") epi = XL_ADD;
   else if (mode == "bnbwd") epi = XL_BNBWD;
+  else if (mode == "affine") epi = XL_AFFINE;
   else if (mode == "store" && a.cv.cin > 0) epi = XL_STORE;
   else TORCH_CHECK(false, "gemm_xl_conv: unknown mode ", mode);
   auto C = at::empty({M, N}, A.options());
@@ -1261,12 +1307,22 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
                     t->numel() == N, name, " must be a contiguous fp32 [N] GPU tensor");
     return t->data_ptr<float>();
   };
+  if (epi == XL_AFFINE) {
+    // mean / invstd carry the affine scale / shift (either may be absent: 1 / 0)
+    if (mean.has_value() && mean->defined()) a.esc = f32vec(mean, "scale");
+    if (invstd.has_value() && invstd->defined()) a.esh = f32vec(invstd, "shift");
+    a.erelu = relu_flag;
+  }
   if (epi == XL_BNBWD) {
-    TORCH_CHECK(bn_x.has_value(), "bnbwd needs bn_x");
-    check_bf16_2d(*bn_x, "bn_x");
-    TORCH_CHECK(bn_x->size(0) == M && bn_x->size(1) == N, "bn_x shape");
-    a.bx = reinterpret_cast<const bf16*>(bn_x->data_ptr()); a.ldbx = bn_x->stride(0);
-    a.bmean = f32vec(mean, "mean");
+    const bool has_x = bn_x.has_value() && bn_x->defined();
+    TORCH_CHECK(has_x || (bn_y.has_value() && bn_y->defined()), "bnbwd needs bn_x and/or bn_y");
+    if (has_x) {
+      check_bf16_2d(*bn_x, "bn_x");
+      TORCH_CHECK(bn_x->size(0) == M && bn_x->size(1) == N, "bn_x shape");
+      a.bx = reinterpret_cast<const bf16*>(bn_x->data_ptr()); a.ldbx = bn_x->stride(0);
+      a.bmean = f32vec(mean, "mean");
+    }
+    if (ebias.has_value() && ebias->defined()) a.ebias = f32vec(ebias, "ebias");
     if (bn_y.has_value() && bn_y->defined()) {
       check_bf16_2d(*bn_y, "bn_y");
       TORCH_CHECK(bn_y->size(0) == M && bn_y->size(1) == N, "bn_y shape");
@@ -1295,12 +1351,14 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
       case XL_STORE: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_STORE, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
       case XL_MOMENTS: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_MOMENTS, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
       case XL_ADD: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_ADD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
-      default: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_BNBWD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+      case XL_BNBWD: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_BNBWD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+      default: TORCH_CHECK(false, "conv_xl: mode ", mode, " has no implicit-GEMM variant");
     }
   } else {
     switch (epi) {
       case XL_MOMENTS: dispatch_bn<XL_MOMENTS>(a, bn, s); break;
       case XL_ADD: dispatch_bn<XL_ADD>(a, bn, s); break;
+      case XL_AFFINE: dispatch_bn<XL_AFFINE>(a, bn, s); break;
       default: dispatch_bn<XL_BNBWD>(a, bn, s); break;
     }
   }
@@ -1319,10 +1377,21 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& invstd,
                                      const c10::optional<at::Tensor>& weight,
                                      const c10::optional<at::Tensor>& bias,
-                                     const std::vector<int64_t>& res_map) {
+                                     const std::vector<int64_t>& res_map,
+                                     const c10::optional<at::Tensor>& a2,
+                                     const c10::optional<at::Tensor>& ebias,
+                                     const c10::optional<at::Tensor>& scale,
+                                     const c10::optional<at::Tensor>& shift, bool relu) {
   check_bf16_2d(A, "A");
   check_bf16_2d(B, "B");
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  const int64_t M = A.size(0), K1 = A.size(1), N = B.size(0);
+  int64_t K = K1;
+  const bool two = a2.has_value() && a2->defined();
+  if (two) {
+    check_bf16_2d(*a2, "a2");
+    TORCH_CHECK(a2->size(0) == M && K1 % XBK == 0, "gemm_xl_conv: a2 must be [M, K2] and K(A) % 64 == 0");
+    K += a2->size(1);
+  }
   TORCH_CHECK(B.size(1) == K && K % XBK == 0 && K >= XBK && N % 8 == 0, "gemm_xl_conv: bad shape");
   TORCH_CHECK(M > 0 && M < (1LL << 31), "gemm_xl_conv: M out of range");
   TORCH_CHECK(mode != "store", "gemm_xl_conv: use gemm_xl for a plain store");
@@ -1330,7 +1399,12 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
   a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
   a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
-  return xl_conv_run(a, A, mode, residual, bn_x, bn_y, mean, invstd, weight, bias, res_map);
+  if (two) {
+    a.A2 = reinterpret_cast<const bf16*>(a2->data_ptr()); a.lda2 = a2->stride(0); a.K1 = (int)K1;
+  }
+  if (mode == "affine")  // scale / shift travel in the mean / invstd slots of xl_conv_run
+    return xl_conv_run(a, A, mode, residual, bn_x, bn_y, scale, shift, weight, bias, res_map, ebias, relu);
+  return xl_conv_run(a, A, mode, residual, bn_x, bn_y, mean, invstd, weight, bias, res_map, ebias, relu);
 }
 
 // kh x kw convolution of an NHWC (channels-last) input as an implicit GEMM on

@@ -83,6 +83,7 @@ FEATURES = {
     "fuse_stem_pool": "stem BN apply + ReLU inside the max-pool (forward and backward)",
     "stem_halo": "halo-tiled stem kernels (stem_halo.hip) -> row-tap implicit GEMM",
     "rowtap_stem": "row-tap stem implicit GEMM (stem.hip) -> MIOpen",
+    "bn_fold": "bottleneck bn3 folded through conv3 (ops/bn_fold.py) -> conv + BN apply passes",
 }
 _disabled_cache: Optional[frozenset] = None
 

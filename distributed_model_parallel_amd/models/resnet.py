@@ -18,6 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.bn_fold import conv1x1_bn_fold, foldable
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, conv_bn_maxpool, grad_tap
@@ -101,6 +102,15 @@ class Bottleneck(nn.Module):
             raw, sums2 = self.conv2.forward_with_moments(out)
             out, sums3 = bn_relu_conv1x1(self.bn2, self.conv3, raw, sums2)
             return self.bn3(out, identity, sums=sums3)
+        if self.training and foldable(self.conv3, self.bn3, out) and isinstance(self.bn2, BatchNormAct2d):
+            # bn3 folded through conv3 (ops/bn_fold.py): conv3's 4x-wide output is
+            # never materialised; bn2's apply pass also reduces colsum(a2)
+            if hasattr(self.conv2, "forward_with_moments"):
+                raw, sums2 = self.conv2.forward_with_moments(out)
+            else:
+                raw, sums2 = self.conv2(out), None
+            a2, asums = self.bn2(raw, sums=sums2, out_moments=True)
+            return conv1x1_bn_fold(self.conv3, self.bn3, a2, asums, identity)
         out = conv_bn(self.conv2, self.bn2, out)
         return conv_bn(self.conv3, self.bn3, out, identity)
 

@@ -81,20 +81,25 @@ def local_moments(x2: torch.Tensor, native: bool) -> torch.Tensor:
     return torch.cat([xd.sum(0), (xd * xd).sum(0), xd.new_tensor([float(x2.shape[0])])])
 
 
-def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, native, nbt=None):
+def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, native, nbt=None,
+                  out_moments=False):
     """Training-mode normalise from (global) moments; updates running stats and
     increments `nbt` (num_batches_tracked) -- inside the kernel when native.
 
-    Returns (y, mean, invstd)."""
+    Returns (y, mean, invstd) [+ fp64 (colsum y, colsum y^2, rows) with out_moments]."""
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_forward_apply(x2, sums, weight, bias, rm, rv,
                                                        float(momentum), float(eps), res2, relu, c,
-                                                       nbt)
+                                                       nbt, out_moments)
     if nbt is not None:
         nbt.add_(1)
     mean, invstd, scale, shift = _finalize_torch(sums, weight, bias, rm, rv, momentum, eps)
-    return [_apply_torch(x2, scale, shift, res2, relu), mean, invstd]
+    y = _apply_torch(x2, scale, shift, res2, relu)
+    if out_moments:
+        yd = y.double()
+        return [y, mean, invstd, torch.cat([yd.sum(0), (yd * yd).sum(0), yd.new_tensor([float(y.shape[0])])])]
+    return [y, mean, invstd]
 
 
 def eval_apply(x2, rm, rv, weight, bias, eps, res2, relu, native):
@@ -209,6 +214,12 @@ class BnBwdSlot:
         self.dz_shape = None
         self.x2 = self.y2 = self.mean = self.invstd = self.w32 = self.b32 = None
 
+    def ready(self) -> bool:
+        """A producer filled the slot: x2 (BN input, with y2 when a residual was
+        fused), or y2 alone for a BN folded through its conv (ops/bn_fold.py):
+        the consumer then reduces only sum dz."""
+        return self.x2 is not None or self.y2 is not None
+
     def park(self, dz: torch.Tensor, sums: torch.Tensor) -> None:
         self.sums = sums
         self.dz_ptr, self.dz_ver, self.dz_shape = dz.data_ptr(), dz._version, tuple(dz.shape)
@@ -230,7 +241,8 @@ _STATS["fused_bwd_moments"] = 0
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
-                relu, reduce_moments, reduce_grads, pre_sums=None, nbt=None, bwd_slot=None):
+                relu, reduce_moments, reduce_grads, pre_sums=None, nbt=None, bwd_slot=None,
+                out_moments=False):
         x2, back = _as_rows(x)
         native = _native_ok(x2)
         _STATS["native_fwd" if native else "torch_fwd"] += 1
@@ -249,8 +261,10 @@ class _BatchNormActFn(torch.autograd.Function):
             count = sums[-1:]
             upd_rm = running_mean if (running_mean is not None and running_mean.dtype == torch.float32) else None
             upd_rv = running_var if upd_rm is not None else None
-            y2, mean, invstd = forward_apply(x2, sums, w32, b32, upd_rm, upd_rv, momentum, eps,
-                                             res2, relu, native, nbt)
+            res = forward_apply(x2, sums, w32, b32, upd_rm, upd_rv, momentum, eps, res2, relu, native, nbt,
+                                out_moments)
+            y2, mean, invstd = res[0], res[1], res[2]
+            osums = res[3] if out_moments else None
             if running_mean is not None and upd_rm is None:  # low-precision buffers
                 c = x2.shape[1]
                 n = sums[2 * c]
@@ -261,6 +275,7 @@ class _BatchNormActFn(torch.autograd.Function):
             count = torch.full((1,), float(x2.shape[0]), dtype=torch.float64, device=x2.device)
             y2, mean, invstd = eval_apply(x2, running_mean, running_var, w32, b32, eps, res2, relu,
                                           native)
+            osums = None
         # the ReLU mask needs the output only when a residual was added before the
         # ReLU; otherwise backward re-derives it from x (one tensor read fewer)
         ctx.save_for_backward(x2, y2 if (relu and residual is not None) else None, w32, b32, mean,
@@ -274,10 +289,16 @@ class _BatchNormActFn(torch.autograd.Function):
             bwd_slot.y2 = y2 if residual is not None else None
             bwd_slot.mean, bwd_slot.invstd, bwd_slot.w32, bwd_slot.b32 = mean, invstd, w32, b32
             ctx.bwd_slot = bwd_slot
+        if out_moments:
+            if osums is None:  # eval mode: moments of the output on request all the same
+                yd = y2.double()
+                osums = torch.cat([yd.sum(0), (yd * yd).sum(0), yd.new_tensor([float(y2.shape[0])])])
+            ctx.mark_non_differentiable(osums)
+            return back(y2), osums
         return back(y2)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, _dosums=None):
         x2, y2, w32, b32, mean, invstd, count = ctx.saved_tensors
         (native, training, relu, has_res, back, has_w, has_b, reduce_grads, wdtype,
          ndim) = ctx.meta
@@ -310,7 +331,7 @@ class _BatchNormActFn(torch.autograd.Function):
         gres = back(dres2) if has_res else None
         gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
         gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
-        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None, None, None
+        return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
@@ -320,19 +341,25 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
                    reduce_moments: Optional[MomentReducer] = None,
                    reduce_grads: Optional[GradReducer] = None,
                    sums: Optional[torch.Tensor] = None,
-                   num_batches_tracked: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   num_batches_tracked: Optional[torch.Tensor] = None,
+                   out_moments: bool = False):
     """Functional fused BN(+residual)(+ReLU).  `sums`: precomputed local moments
     [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode.
-    `num_batches_tracked`: incremented once (training mode), in-kernel when native."""
+    `num_batches_tracked`: incremented once (training mode), in-kernel when native.
+    `out_moments`: also return the fp64 [2C+1] (colsum, colsum of squares, rows)
+    of the OUTPUT, reduced inside the apply pass (ops/bn_fold.py needs colsum)."""
     slot = None
     if training and relu and x.dim() == 4 and torch.is_grad_enabled() and _FUSE_BWD and _native.gpu_path(x):
         slot = BnBwdSlot()
     out = _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
                                 momentum, eps, relu, reduce_moments, reduce_grads, sums,
-                                num_batches_tracked if training else None, slot)
+                                num_batches_tracked if training else None, slot, out_moments)
+    osums = None
+    if out_moments:
+        out, osums = out
     if slot is not None and slot.x2 is not None:
         out._dmp_bnbwd = slot  # a native 1x1 conv consuming `out` may fuse our backward reductions
-    return out
+    return (out, osums) if out_moments else out
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -362,7 +389,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return None, None
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                sums: Optional[torch.Tensor] = None) -> torch.Tensor:
+                sums: Optional[torch.Tensor] = None, out_moments: bool = False):
         self._check_input_dim(x)
         use_batch = self.training or not self.track_running_stats
         recompute = in_recompute()  # activation-checkpoint recompute: no second stat update
@@ -384,7 +411,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
                               use_batch, momentum, self.eps, relu=self.act == "relu",
                               residual=residual, reduce_moments=rmom, reduce_grads=rgrad,
                               sums=sums if use_batch else None,
-                              num_batches_tracked=nbt if use_batch else None)
+                              num_batches_tracked=nbt if use_batch else None,
+                              out_moments=out_moments)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (f", act={self.act}" if self.act else "")

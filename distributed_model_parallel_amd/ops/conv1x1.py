@@ -130,14 +130,14 @@ class _Conv1x1Fn(torch.autograd.Function):
             cextra, cgeom = ctx.slot.take_compact() if ctx.slot is not None else (None, None)
             bs = ctx.bn_slot
             ctx.bn_slot = None
-            if cextra is not None and not (bs is not None and bs.consumers == 1 and bs.x2 is not None):
+            if cextra is not None and not (bs is not None and bs.consumers == 1 and bs.ready()):
                 # no fused BN epilogue to read it compact: expand to full resolution
                 full = torch.zeros(n * h * w, cin, device=dy.device, dtype=x.dtype)
                 full.view(n, h, w, cin)[:, ::cgeom[0], ::cgeom[0]].copy_(cextra.view(n, cgeom[1], cgeom[2], cin))
                 extra = full.view(n, h, w, cin).permute(0, 3, 1, 2) if extra is None else extra + full.view(
                     n, h, w, cin).permute(0, 3, 1, 2)
                 cextra = None
-            if bs is not None and bs.consumers == 1 and bs.x2 is not None:
+            if bs is not None and bs.consumers == 1 and bs.ready():
                 # dz = relu_mask * (dy @ W (+ shortcut grad)) and the producer BN's
                 # (sum dz, sum dz*(x-mean)) in ONE epilogue pass
                 _STATS["fused_bn_bwd"] += 1

@@ -140,13 +140,15 @@ def _xl_dgrad_s2(cin: int, cout: int, kh: int, kw: int, stride: int, pad: int, h
 
 def _phase_weights(weight: torch.Tensor):
     """[Cout, Cin, 3, 3] -> the four [Cin, taps * Cout] phase matrices (py, px)."""
-    cout, cin = weight.shape[:2]
-    w9 = weight.permute(1, 2, 3, 0).reshape(cin, 9, cout)
+    cin = weight.shape[1]
+    w4 = weight.permute(1, 2, 3, 0)  # [Cin, 3, 3, Cout]
     out = []
     for py in (0, 1):
         for px in (0, 1):
-            idx = [ky * 3 + kx for ky in _PHASE_TAPS[py] for kx in _PHASE_TAPS[px]]
-            out.append(w9[:, idx].reshape(cin, -1).contiguous())
+            # stacked slices, not an index list: a list index is a host->device
+            # copy, which a hipGraph capture (train/graphed.py) refuses
+            taps = [w4[:, ky, kx] for ky in _PHASE_TAPS[py] for kx in _PHASE_TAPS[px]]
+            out.append(torch.stack(taps, 1).reshape(cin, -1))
     return out
 
 
