@@ -141,6 +141,15 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& ebias,
                                      const c10::optional<at::Tensor>& scale,
                                      const c10::optional<at::Tensor>& shift, bool relu);
+// bn_fold.hip
+bool bn_fold_supported(int64_t cout, int64_t cin);
+std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums);
+at::Tensor bn_fold_bwd_sums(const at::Tensor& D, const at::Tensor& W, const at::Tensor& sdz,
+                            const at::Tensor& mean);
+std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tensor& local, const at::Tensor& count,
+                                         const at::Tensor& invstd, const at::Tensor& mean,
+                                         const c10::optional<at::Tensor>& gamma, const at::Tensor& D,
+                                         const at::Tensor& WG, const at::Tensor& s, const at::Tensor& W);
 // attention.hip
 bool attention_supported(int64_t S, int64_t head_dim);
 std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale);
@@ -301,6 +310,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 7, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
+
+  // ---- BN folded through an expanding 1x1 conv (ops/bn_fold.py) ----
+  m.def("bn_fold_supported", &dmp::bn_fold_supported, py::arg("cout"), py::arg("cin"));
+  m.def("bn_fold_fwd", &dmp::bn_fold_fwd, py::arg("W"), py::arg("G"), py::arg("asums"),
+        "(sums fp64 [2Cout+1], WG fp32 [Cout, Cin]) of y = a W^T from G = a^T a and colsum(a)");
+  m.def("bn_fold_bwd_sums", &dmp::bn_fold_bwd_sums, py::arg("D"), py::arg("W"), py::arg("sdz"), py::arg("mean"),
+        "local fp64 [2Cout] = (sum dz, sum dz*(y - mean)) from D = dz^T a");
+  m.def("bn_fold_bwd_coef", &dmp::bn_fold_bwd_coef, py::arg("sums"), py::arg("local"), py::arg("count"),
+        py::arg("invstd"), py::arg("mean"), py::arg("gamma"), py::arg("D"), py::arg("WG"), py::arg("s"),
+        py::arg("W"), "(dW, dgamma, dbeta, Bm = [(al o W)^T | W^T diag(be) W], ebias = c^T W)");
 
   // ---- fused self-attention on packed qkv (ViT) ----
   m.def("attention_supported", &dmp::attention_supported);

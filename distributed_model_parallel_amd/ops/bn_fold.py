@@ -107,7 +107,10 @@ class _ConvBNFoldFn(torch.autograd.Function):
         else:
             ad = a2.double()
             G = ad.t() @ ad
-        sums, WG = _fold_stats(W2, G, s, count)
+        if native and C.bn_fold_supported(cout, cin):
+            sums, WG = C.bn_fold_fwd(W2, G, a_sums)   # one launch: W G and the row dots
+        else:
+            sums, WG = _fold_stats(W2, G, s, count)
         if reduce_moments is not None:
             sums = reduce_moments(sums)
         w32 = bn_w.float() if bn_w is not None else None
@@ -175,6 +178,20 @@ class _ConvBNFoldFn(torch.autograd.Function):
                 else C.gemm_tn(dz2, a2, torch.float32)
         else:
             D = dz2.double().t() @ a2.double()
+        if native and C.bn_fold_supported(cout, cin):
+            # two launches: the row dots, then every coefficient-level output
+            local = C.bn_fold_bwd_sums(D, W2, sdz.contiguous(), mean)
+            sums = reduce_grads(local.clone()) if reduce_grads is not None else local
+            dw2, dg, db, Bb, ebias = C.bn_fold_bwd_coef(sums, local, count, invstd, mean, w32, D,
+                                                        WG, s, W2)
+            dw = dw2.view(cout, cin, 1, 1)
+            if weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous(memory_format=torch.channels_last)
+            da = _FoldDgrad.run(ctx, C, dz2, a2, Bb, ebias, n, cin, h, w) if ctx.needs_input_grad[0] else None
+            gres = _unrows(dz2, n, h, w) if (has_res and ctx.needs_input_grad[5]) else None
+            gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[3] else None
+            gb = db.to(wdtype) if has_b and ctx.needs_input_grad[4] else None
+            return da, None, dw, gw, gb, gres, None, None, None, None, None, None, None, None, None, None
         Wd = W2.double()
         Dd = D.double()
         sdzx = (Dd * Wd).sum(1) - mean.double() * sdz
@@ -197,30 +214,7 @@ class _ConvBNFoldFn(torch.autograd.Function):
         da = None
         if ctx.needs_input_grad[0]:
             if native:
-                Bb = Bm.to(torch.bfloat16).contiguous()
-                bs = ctx.a_slot
-                ctx.a_slot = None
-                xl = _xl_fwd(cin, cout)
-                if bs is not None and bs.consumers == 1 and bs.x2 is not None:
-                    # a is a training-mode BN+ReLU output: its backward reductions in our epilogue
-                    _STATS["fold_bnbwd_epilogue"] += 1
-                    inv = bs.invstd if bs.y2 is None else None
-                    bw = bs.w32 if bs.y2 is None else None
-                    bb = bs.b32 if bs.y2 is None else None
-                    if xl:
-                        da2, asums = C.gemm_xl_conv(dz2, Bb, "bnbwd", bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean,
-                                                    invstd=inv, weight=bw, bias=bb, a2=a2, ebias=ebias)
-                    else:
-                        da2, asums = C.gemm_nt_bnbwd(dz2, Bb, None, bs.x2, bs.y2, bs.mean, inv, bw, bb,
-                                                     a2=a2, ebias=ebias)
-                    da = _unrows(da2, n, h, w)
-                    bs.park(da, asums[: 2 * cin])
-                else:
-                    if xl:
-                        da2, _ = C.gemm_xl_conv(dz2, Bb, "affine", a2=a2, shift=ebias)
-                    else:
-                        da2, _ = C.gemm_nt(dz2, Bb, mode="affine", epi_shift=ebias, a2=a2)
-                    da = _unrows(da2, n, h, w)
+                da = _FoldDgrad.run(ctx, C, dz2, a2, Bm.to(torch.bfloat16).contiguous(), ebias, n, cin, h, w)
             else:
                 da2 = (torch.cat([dz2.double(), a2.double()], 1) @ Bm.t() + ebias.double()).to(a.dtype)
                 da = _unrows(da2, n, h, w)
@@ -232,6 +226,37 @@ class _ConvBNFoldFn(torch.autograd.Function):
         gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[3] else None
         gb = db.to(wdtype) if has_b and ctx.needs_input_grad[4] else None
         return da, None, dw, gw, gb, gres, None, None, None, None, None, None, None, None, None, None
+
+
+class _FoldDgrad:
+    @staticmethod
+    def run(ctx, C, dz2, a2, Bb, ebias, n, cin, h, w):
+        """da = [dz | a] @ Bb^T + ebias on the MFMA GEMMs (two-source A operand);
+        when ``a`` is a training-mode BN+ReLU output its backward reductions
+        ride in the same epilogue (BnBwdSlot)."""
+        cout = dz2.shape[1]
+        bs = ctx.a_slot
+        ctx.a_slot = None
+        xl = _xl_fwd(cin, cout)
+        if bs is not None and bs.consumers == 1 and bs.x2 is not None:
+            _STATS["fold_bnbwd_epilogue"] += 1
+            inv = bs.invstd if bs.y2 is None else None
+            bw = bs.w32 if bs.y2 is None else None
+            bb = bs.b32 if bs.y2 is None else None
+            if xl:
+                da2, asums = C.gemm_xl_conv(dz2, Bb, "bnbwd", bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean,
+                                            invstd=inv, weight=bw, bias=bb, a2=a2, ebias=ebias)
+            else:
+                da2, asums = C.gemm_nt_bnbwd(dz2, Bb, None, bs.x2, bs.y2, bs.mean, inv, bw, bb,
+                                             a2=a2, ebias=ebias)
+            da = _unrows(da2, n, h, w)
+            bs.park(da, asums[: 2 * cin])
+            return da
+        if xl:
+            da2, _ = C.gemm_xl_conv(dz2, Bb, "affine", a2=a2, shift=ebias)
+        else:
+            da2, _ = C.gemm_nt(dz2, Bb, mode="affine", epi_shift=ebias, a2=a2)
+        return _unrows(da2, n, h, w)
 
 
 def foldable(conv: nn.Module, bn: nn.Module, a: torch.Tensor) -> bool:

@@ -191,3 +191,42 @@ def test_bottleneck_fold_matches_unfused_model():
     for (n1, b1), (_, b2) in zip(net.named_buffers(), ref.named_buffers()):
         if b1.dtype.is_floating_point:
             _check(b1, b2, 2e-2, n1)
+
+
+@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512)])
+def test_fold_coefficient_kernels_match_fp64(cout, cin):
+    """bn_fold_fwd / bn_fold_bwd_sums / bn_fold_bwd_coef against the same
+    algebra in fp64 torch ops (the framework's CPU path)."""
+    C = _native.require("fold kernels")
+    torch.manual_seed(5)
+    W = (torch.randn(cout, cin, device=DEV) * 0.05).bfloat16()
+    a = torch.relu(torch.randn(4096, cin, device=DEV)).bfloat16()
+    G = (a.double().t() @ a.double()).float()
+    ad = a.double()
+    asums = torch.cat([ad.sum(0), (ad * ad).sum(0), ad.new_tensor([4096.0])])
+    sums, WG = C.bn_fold_fwd(W, G, asums)
+    rs, rWG = bn_fold._fold_stats(W, G, asums[:cin], asums[2 * cin:])
+    torch.testing.assert_close(WG.double(), rWG, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(sums, rs, rtol=1e-6, atol=1e-6)
+    D = torch.randn(cout, cin, device=DEV)
+    sdz = torch.randn(cout, device=DEV, dtype=torch.float64)
+    mean = torch.randn(cout, device=DEV)
+    invstd = torch.rand(cout, device=DEV) + 0.5
+    gamma = torch.rand(cout, device=DEV) + 0.5
+    local = C.bn_fold_bwd_sums(D, W, sdz, mean)
+    Wd = W.double()
+    sdzx = (D.double() * Wd).sum(1) - mean.double() * sdz
+    torch.testing.assert_close(local, torch.cat([sdz, sdzx]), rtol=1e-9, atol=1e-9)
+    cnt = asums[2 * cin:]
+    dW, dg, db, Bm, eb = C.bn_fold_bwd_coef(local, local, cnt, invstd, mean, gamma, D, WG, asums[:cin], W)
+    istd = invstd.double()
+    al = istd * gamma.double()
+    be = -al * istd * istd * sdzx / cnt
+    cc = -al * sdz / cnt - be * mean.double()
+    rdW = al[:, None] * D.double() + be[:, None] * WG.double() + cc[:, None] * asums[:cin][None, :]
+    _check(dW, rdW, 1e-2)
+    torch.testing.assert_close(dg.double(), sdzx * istd, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(db.double(), sdz, rtol=1e-5, atol=1e-5)
+    _check(Bm[:, :cout], (al[:, None] * Wd).t(), 1e-2)
+    _check(Bm[:, cout:], Wd.t() @ (be[:, None] * Wd), 1e-2)
+    _check(eb, cc @ Wd, 1e-5)
