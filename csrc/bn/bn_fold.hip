@@ -6,11 +6,11 @@
 //
 //   forward   fold_fwd_kernel       WG = W G (fp32), sums = [W s, rowdot(WG, W), M] (fp64)
 //   backward  fold_bwd_sums_kernel  local = [sdz, rowdot(D, W) - mean * sdz] (fp64)
-//             fold_bwd_coef_kernel  al, be, c per channel from the (all-reduced) sums, then
-//                 role A  dW = al o D + be o WG + c (x) s,  Bm[:, :Cout] = (al o W)^T,  dgamma, dbeta
-//                 role B  Bm[:, Cout:] = W^T diag(be) W
-//                 role C  ebias = c^T W
-// W is bf16 [Cout, Cin] with Cin <= 512 (ResNet bottlenecks: 64..512); fp64
+//             fold_coef_kernel      al, be, c per channel from the (all-reduced) sums
+//             fold_bwd_coef_kernel  role A  dW = al o D + be o WG + c (x) s,  Bm[:, :Cout] = (al o W)^T,
+//                                           dgamma, dbeta
+//                                   role B  Bm[:, Cout:] = W^T diag(be) W, ebias = c^T W
+// W is bf16 [Cout, Cin] with Cin <= 1024 (ResNet: 64..1024); fp64
 // where sums over many rows or channels meet (row dots, coefficients).
 #include <torch/extension.h>
 #include <ATen/hip/HIPContext.h>
@@ -22,66 +22,86 @@ namespace {
 using bf16 = __bf16;
 constexpr int kFoldThreads = 256;
 constexpr int kFwdRows = 16;     // output channels per forward block
-constexpr int kMaxCin = 512;
+constexpr int kMaxCin = 1024;
 
-__device__ __forceinline__ double block_sum_d(double v, double* lds) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) lds[wave] = v;
-  __syncthreads();
-  double t = 0.0;
-  for (int w = 0; w < kFoldThreads / 64; ++w) t += lds[w];
-  return t;
-}
-
-// grid = Cout / kFwdRows.  Thread t owns columns j = t, t + 256 of WG rows k0..k0+15.
+// grid = Cout / kFwdRows.  Thread t owns columns j = t + 256 q (q < NQ) of WG rows
+// k0..k0+15; G streams through LDS in 8-row chunks (double buffered), so the
+// FMAs read LDS instead of waiting on L2 per row of G.
+template <int NQ>
 __global__ __launch_bounds__(kFoldThreads) void fold_fwd_kernel(const bf16* __restrict__ W,
                                                                 const float* __restrict__ G,
                                                                 const double* __restrict__ asums, int Cout,
                                                                 int Cin, float* __restrict__ WG,
                                                                 double* __restrict__ sums) {
-  __shared__ __attribute__((aligned(16))) float wl[kFwdRows][kMaxCin];
-  __shared__ double red[kFoldThreads / 64];
-  const int tid = threadIdx.x, k0 = blockIdx.x * kFwdRows;
+  constexpr int GR = 8;  // rows of G per LDS chunk
+  __shared__ __attribute__((aligned(16))) float wl[kFwdRows][NQ * kFoldThreads];
+  __shared__ __attribute__((aligned(16))) float gl[2][GR][NQ * kFoldThreads];
+  __shared__ double red[2][kFoldThreads / 64][kFwdRows];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, k0 = blockIdx.x * kFwdRows;
   for (int idx = tid; idx < kFwdRows * Cin; idx += kFoldThreads) {
     const int r = idx / Cin, i = idx - r * Cin;
     wl[r][i] = (float)W[(int64_t)(k0 + r) * Cin + i];
   }
-  __syncthreads();
-  const int j0 = tid, j1 = tid + kFoldThreads;
-  const bool v0 = j0 < Cin, v1 = j1 < Cin;
-  float acc0[kFwdRows], acc1[kFwdRows];
-#pragma unroll
-  for (int r = 0; r < kFwdRows; ++r) acc0[r] = acc1[r] = 0.f;
-  for (int i = 0; i < Cin; i += 4) {
-    float g0[4], g1[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      g0[u] = v0 ? G[(int64_t)(i + u) * Cin + j0] : 0.f;
-      g1[u] = v1 ? G[(int64_t)(i + u) * Cin + j1] : 0.f;
+  auto stage = [&](int i0, int buf) {  // G rows i0..i0+7 -> gl[buf] (16-B vectors)
+    const int nv = GR * Cin / 4;
+    for (int v = tid; v < nv; v += kFoldThreads) {
+      const int r = v / (Cin / 4), c = (v - r * (Cin / 4)) * 4;
+      *reinterpret_cast<f32x4*>(&gl[buf][r][c]) = *reinterpret_cast<const f32x4*>(G + (int64_t)(i0 + r) * Cin + c);
     }
+  };
+  float acc[kFwdRows][NQ];
 #pragma unroll
-    for (int r = 0; r < kFwdRows; ++r) {
-      const f32x4 w4 = *reinterpret_cast<const f32x4*>(&wl[r][i]);  // LDS broadcast
+  for (int r = 0; r < kFwdRows; ++r)
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc0[r] = fmaf(w4[u], g0[u], acc0[r]);
-        acc1[r] = fmaf(w4[u], g1[u], acc1[r]);
+    for (int q = 0; q < NQ; ++q) acc[r][q] = 0.f;
+  stage(0, 0);
+  __syncthreads();
+  for (int i0 = 0; i0 < Cin; i0 += GR) {
+    const int buf = (i0 / GR) & 1;
+    if (i0 + GR < Cin) stage(i0 + GR, buf ^ 1);
+#pragma unroll
+    for (int u = 0; u < GR; u += 4) {
+      float g[4][NQ];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) g[e][q] = gl[buf][u + e][tid + q * kFoldThreads];
+#pragma unroll
+      for (int r = 0; r < kFwdRows; ++r) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(&wl[r][i0 + u]);  // LDS broadcast
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) acc[r][q] = fmaf(w4[e], g[e][q], acc[r][q]);
       }
     }
+    __syncthreads();
   }
+  // WG and this thread's share of the two row dots, one wave reduction each,
+  // one LDS exchange for the whole block
+#pragma unroll
   for (int r = 0; r < kFwdRows; ++r) {
-    const int k = k0 + r;
-    double q = 0.0, m = 0.0;
-    if (v0) { WG[(int64_t)k * Cin + j0] = acc0[r]; q += (double)acc0[r] * wl[r][j0]; m += (double)wl[r][j0] * asums[j0]; }
-    if (v1) { WG[(int64_t)k * Cin + j1] = acc1[r]; q += (double)acc1[r] * wl[r][j1]; m += (double)wl[r][j1] * asums[j1]; }
-    m = block_sum_d(m, red);
-    q = block_sum_d(q, red);
-    if (tid == 0) {
-      sums[k] = m;         // sum_m y[m, k]
-      sums[Cout + k] = q;  // sum_m y[m, k]^2
+    double qd = 0.0, md = 0.0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int j = tid + q * kFoldThreads;
+      if (j < Cin) {
+        WG[(int64_t)(k0 + r) * Cin + j] = acc[r][q];
+        qd += (double)acc[r][q] * wl[r][j];
+        md += (double)wl[r][j] * asums[j];
+      }
     }
+    qd = wave_sum(qd);
+    md = wave_sum(md);
+    if (lane == 0) { red[0][wave][r] = md; red[1][wave][r] = qd; }
+  }
+  __syncthreads();
+  if (tid < 2 * kFwdRows) {
+    const int which = tid / kFwdRows, r = tid % kFwdRows;
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kFoldThreads / 64; ++w) t += red[which][w][r];
+    sums[which * Cout + k0 + r] = t;  // sum_m y[m, k] | sum_m y[m, k]^2
   }
   if (blockIdx.x == 0 && tid == 0) sums[2 * Cout] = asums[2 * Cin];  // rows
 }
@@ -104,36 +124,51 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_sums_kernel(const float
 }
 
 struct FoldBwdArgs {
-  const double* sums;   // [2Cout] (all-reduced) sdz, sdzx
-  const double* local;  // [2Cout] this rank's, for dgamma / dbeta
-  const double* count;  // [1] global rows
-  const float *invstd, *mean, *gamma;  // [Cout] (gamma may be null)
+  const double* local;  // [2Cout] this rank's sums, for dgamma / dbeta
+  const float* coef;    // [3, Cout] al, be, c (fold_coef_kernel)
+  const float* invstd;  // [Cout]
   const float *D, *WG;  // [Cout, Cin] fp32
-  const double* s;      // [Cin] colsum(a)
+  const double* s;      // [2Cin+1] (colsum a, colsum a^2, local rows) of a
   const bf16* W;        // [Cout, Cin]
   bf16* dW;             // [Cout, Cin]
   float *dgamma, *dbeta;
   bf16* Bm;             // [Cin, Cout + Cin]
   float* ebias;         // [Cin]
   int Cout, Cin;
-  int nA, nB;           // role A / B block counts (role C: the last block)
+  int nA;               // role A blocks; the rest are role B
 };
 
-__device__ __forceinline__ void fold_coef(const FoldBwdArgs& p, int k, double& al, double& be, double& c) {
-  const double istd = p.invstd[k];
-  const double cnt = p.count[0];
-  al = istd * (p.gamma ? (double)p.gamma[k] : 1.0);
-  be = -al * istd * istd * p.sums[p.Cout + k] / cnt;
-  c = -al * p.sums[k] / cnt - be * (double)p.mean[k];
+// al, be, c per output channel from the (all-reduced) backward sums -- once,
+// so the role kernels never repeat the fp64 divisions.
+__global__ __launch_bounds__(kFoldThreads) void fold_coef_kernel(const double* __restrict__ sums,
+                                                                 const double* __restrict__ count,
+                                                                 const float* __restrict__ invstd,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ gamma, int Cout,
+                                                                 float* __restrict__ coef) {
+  const int k = blockIdx.x * kFoldThreads + threadIdx.x;
+  if (k >= Cout) return;
+  const double rc = 1.0 / count[0];
+  const double istd = invstd[k];
+  const double al = istd * (gamma ? (double)gamma[k] : 1.0);
+  const double be = -al * istd * istd * sums[Cout + k] * rc;
+  const double c = -al * sums[k] * rc - be * (double)mean[k];
+  coef[k] = (float)al;
+  coef[Cout + k] = (float)be;
+  coef[2 * Cout + k] = (float)c;
 }
 
 constexpr int kTK = 16, kTI = 64;  // role A tile: 16 channels x 64 input columns
-constexpr int kTR = 8;             // role B: Bm rows (input channels i) per block
-constexpr int kKC = 64;            // role B: channels staged per LDS round
+constexpr int kTR = 8;             // role B: Bm rows (input channels i) per block (+1: ebias)
+constexpr int kKC = 32;            // role B: channels staged per LDS round
 
+template <int NQ>
 __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldBwdArgs p) {
   const int tid = threadIdx.x;
   const int Cout = p.Cout, Cin = p.Cin, LDB = Cout + Cin;
+  const float* al_ = p.coef;
+  const float* be_ = p.coef + Cout;
+  const float* c_ = p.coef + 2 * Cout;
   if ((int)blockIdx.x < p.nA) {
     // ---- role A: 16 x 64 tile of dW and of the transposed (al o W) block of Bm ----
     __shared__ float tr[kTI][kTK + 1];
@@ -143,12 +178,11 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
 #pragma unroll
     for (int rr = 0; rr < kTK / 4; ++rr) {
       const int r = rq + rr * 4, k = k0 + r, i = i0 + il;
-      double al, be, c;
-      fold_coef(p, k, al, be, c);
+      const float al = al_[k], be = be_[k], c = c_[k];
       const int64_t o = (int64_t)k * Cin + i;
-      const double dw = al * (double)p.D[o] + be * (double)p.WG[o] + c * p.s[i];
-      p.dW[o] = (bf16)(float)dw;
-      tr[il][r] = (float)(al * (double)(float)p.W[o]);
+      const float dw = fmaf(al, p.D[o], fmaf(be, p.WG[o], (float)((double)c * p.s[i])));
+      p.dW[o] = (bf16)dw;
+      tr[il][r] = al * (float)p.W[o];
       if (i0 == 0 && il == 0) {
         p.dgamma[k] = (float)(p.local[Cout + k] * (double)p.invstd[k]);
         p.dbeta[k] = (float)p.local[k];
@@ -163,50 +197,68 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
     }
     return;
   }
-  if ((int)blockIdx.x < p.nA + p.nB) {
-    // ---- role B: rows i0..i0+7 of W^T diag(be) W; thread t owns columns j = t, t + 256 ----
-    __shared__ float wb[kKC][kTR];
-    const int i0 = (blockIdx.x - p.nA) * kTR;
-    const int j0 = tid, j1 = tid + kFoldThreads;
-    const bool v0 = j0 < Cin, v1 = j1 < Cin;
-    float acc0[kTR], acc1[kTR];
+  // ---- role B: rows i0..i0+7 of B = W^T diag(be) W; thread t owns columns
+  // j = t + 256 q.  W rows of a channel chunk are staged in LDS as fp32 with
+  // the per-row factors applied.  ebias for the block's rows: c^T W[:, i].
+  __shared__ __attribute__((aligned(16))) float wj[kKC][NQ * kFoldThreads];
+  __shared__ float wb[kKC][kTR];
+  __shared__ float rsum[kFoldThreads / 64][kTR];
+  const int i0 = (blockIdx.x - p.nA) * kTR;
+  const int lane = tid & 63, wave = tid >> 6;
+  float acc[kTR][NQ];
 #pragma unroll
-    for (int r = 0; r < kTR; ++r) acc0[r] = acc1[r] = 0.f;
-    for (int kc = 0; kc < Cout; kc += kKC) {
-      __syncthreads();
-      for (int idx = tid; idx < kKC * kTR; idx += kFoldThreads) {
-        const int kk = idx / kTR, r = idx - kk * kTR, k = kc + kk;
-        double al, be, c;
-        fold_coef(p, k, al, be, c);
-        wb[kk][r] = (float)(be * (double)(float)p.W[(int64_t)k * Cin + i0 + r]);
-      }
-      __syncthreads();
-      for (int kk = 0; kk < kKC; ++kk) {
-        const int64_t row = (int64_t)(kc + kk) * Cin;
-        const float w0 = v0 ? (float)p.W[row + j0] : 0.f, w1 = v1 ? (float)p.W[row + j1] : 0.f;
+  for (int r = 0; r < kTR; ++r)
 #pragma unroll
-        for (int r = 0; r < kTR; ++r) {
-          acc0[r] = fmaf(wb[kk][r], w0, acc0[r]);
-          acc1[r] = fmaf(wb[kk][r], w1, acc1[r]);
-        }
-      }
+    for (int q = 0; q < NQ; ++q) acc[r][q] = 0.f;
+  for (int kc = 0; kc < Cout; kc += kKC) {
+    __syncthreads();
+    for (int v = tid; v < kKC * Cin / 8; v += kFoldThreads) {  // 16-B bf16 vectors
+      const int kk = v / (Cin / 8), c = (v - kk * (Cin / 8)) * 8;
+      const bf16x8 w8 = *reinterpret_cast<const bf16x8*>(p.W + (int64_t)(kc + kk) * Cin + c);
+      const f32x8 f = __builtin_convertvector(w8, f32x8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wj[kk][c + e] = f[e];
     }
-#pragma unroll
-    for (int r = 0; r < kTR; ++r) {
-      if (v0) p.Bm[(int64_t)(i0 + r) * LDB + Cout + j0] = (bf16)acc0[r];
-      if (v1) p.Bm[(int64_t)(i0 + r) * LDB + Cout + j1] = (bf16)acc1[r];
+    for (int idx = tid; idx < kKC * kTR; idx += kFoldThreads) {
+      const int kk = idx / kTR, r = idx - kk * kTR, k = kc + kk;
+      wb[kk][r] = be_[k] * (float)p.W[(int64_t)k * Cin + i0 + r];
     }
-    return;
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < kKC; ++kk) {
+      float w[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) w[q] = wj[kk][tid + q * kFoldThreads];
+#pragma unroll
+      for (int r = 0; r < kTR; ++r)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) acc[r][q] = fmaf(wb[kk][r], w[q], acc[r][q]);
+    }
   }
-  // ---- role C: ebias = c^T W ----
-  for (int i = tid; i < Cin; i += kFoldThreads) {
-    double e = 0.0;
-    for (int k = 0; k < Cout; ++k) {
-      double al, be, c;
-      fold_coef(p, k, al, be, c);
-      e += c * (double)(float)p.W[(int64_t)k * Cin + i];
+  // Bm rows, and this thread's share of ebias = c^T W[:, i] (channels k = t, t + 256, ..)
+  float part[kTR];
+#pragma unroll
+  for (int r = 0; r < kTR; ++r) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int j = tid + q * kFoldThreads;
+      if (j < Cin) p.Bm[(int64_t)(i0 + r) * LDB + Cout + j] = (bf16)acc[r][q];
     }
-    p.ebias[i] = (float)e;
+    float e = 0.f;
+    for (int k = tid; k < Cout; k += kFoldThreads) e = fmaf(c_[k], (float)p.W[(int64_t)k * Cin + i0 + r], e);
+    part[r] = e;
+  }
+#pragma unroll
+  for (int r = 0; r < kTR; ++r) {
+    const float v = wave_sum(part[r]);
+    if (lane == 0) rsum[wave][r] = v;
+  }
+  __syncthreads();
+  if (tid < kTR) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kFoldThreads / 64; ++w) t += rsum[w][tid];
+    p.ebias[i0 + tid] = t;
   }
 }
 
@@ -223,7 +275,7 @@ void check_w(const at::Tensor& W) {
               "W must be a contiguous bf16 [Cout, Cin] GPU tensor");
   TORCH_CHECK(W.size(1) % kTI == 0 && W.size(1) <= kMaxCin && W.size(0) % kFwdRows == 0 &&
                   W.size(0) % kKC == 0,
-              "bn fold: Cin % 64 == 0, Cin <= 512, Cout % 64 == 0");
+              "bn fold: Cin % 64 == 0, Cin <= 1024, Cout % 64 == 0");
 }
 
 }  // namespace
@@ -241,10 +293,15 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
   check_f64(asums, 2 * Cin + 1, "asums");
   auto sums = at::empty({2 * Cout + 1}, W.options().dtype(at::kDouble));
   auto WG = at::empty({Cout, Cin}, W.options().dtype(at::kFloat));
-  hipLaunchKernelGGL(fold_fwd_kernel, dim3((unsigned)(Cout / kFwdRows)), dim3(kFoldThreads), 0,
-                     at::hip::getCurrentHIPStream(), reinterpret_cast<const bf16*>(W.data_ptr()),
-                     G.data_ptr<float>(), asums.data_ptr<double>(), (int)Cout, (int)Cin, WG.data_ptr<float>(),
-                     sums.data_ptr<double>());
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)(Cout / kFwdRows)), dim3(kFoldThreads), 0,
+                       at::hip::getCurrentHIPStream(), reinterpret_cast<const bf16*>(W.data_ptr()),
+                       G.data_ptr<float>(), asums.data_ptr<double>(), (int)Cout, (int)Cin, WG.data_ptr<float>(),
+                       sums.data_ptr<double>());
+  };
+  if (Cin <= 256) go(fold_fwd_kernel<1>);
+  else if (Cin <= 512) go(fold_fwd_kernel<2>);
+  else go(fold_fwd_kernel<4>);
   DMP_HIP_CHECK(hipGetLastError());
   return {sums, WG};
 }
@@ -281,17 +338,23 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   check_f32(mean, Cout, "mean");
   check_f32(D, Cout * Cin, "D");
   check_f32(WG, Cout * Cin, "WG");
-  check_f64(s, Cin, "s");
+  check_f64(s, 2 * Cin + 1, "s (asums)");
   const bool hg = gamma.has_value() && gamma->defined();
   if (hg) check_f32(*gamma, Cout, "gamma");
   auto dW = at::empty({Cout, Cin}, W.options());
   auto dgb = at::empty({2, Cout}, W.options().dtype(at::kFloat));
   auto Bm = at::empty({Cin, Cout + Cin}, W.options());
   auto ebias = at::empty({Cin}, W.options().dtype(at::kFloat));
+  auto coef = at::empty({3, Cout}, W.options().dtype(at::kFloat));
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(fold_coef_kernel, dim3((unsigned)((Cout + kFoldThreads - 1) / kFoldThreads)),
+                     dim3(kFoldThreads), 0, stream, sums.data_ptr<double>(), count.data_ptr<double>(),
+                     invstd.data_ptr<float>(), mean.data_ptr<float>(), hg ? gamma->data_ptr<float>() : nullptr,
+                     (int)Cout, coef.data_ptr<float>());
   FoldBwdArgs p{};
-  p.sums = sums.data_ptr<double>(); p.local = local.data_ptr<double>(); p.count = count.data_ptr<double>();
-  p.invstd = invstd.data_ptr<float>(); p.mean = mean.data_ptr<float>();
-  p.gamma = hg ? gamma->data_ptr<float>() : nullptr;
+  p.local = local.data_ptr<double>();
+  p.coef = coef.data_ptr<float>();
+  p.invstd = invstd.data_ptr<float>();
   p.D = D.data_ptr<float>(); p.WG = WG.data_ptr<float>(); p.s = s.data_ptr<double>();
   p.W = reinterpret_cast<const bf16*>(W.data_ptr());
   p.dW = reinterpret_cast<bf16*>(dW.data_ptr());
@@ -300,9 +363,10 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   p.ebias = ebias.data_ptr<float>();
   p.Cout = (int)Cout; p.Cin = (int)Cin;
   p.nA = (int)((Cout / kTK) * (Cin / kTI));
-  p.nB = (int)(Cin / kTR);
-  hipLaunchKernelGGL(fold_bwd_coef_kernel, dim3((unsigned)(p.nA + p.nB + 1)), dim3(kFoldThreads), 0,
-                     at::hip::getCurrentHIPStream(), p);
+  const unsigned blocks = (unsigned)(p.nA + Cin / kTR);
+  if (Cin <= 256) hipLaunchKernelGGL(fold_bwd_coef_kernel<1>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
+  else if (Cin <= 512) hipLaunchKernelGGL(fold_bwd_coef_kernel<2>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
+  else hipLaunchKernelGGL(fold_bwd_coef_kernel<4>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
   DMP_HIP_CHECK(hipGetLastError());
   return {dW, dgb[0], dgb[1], Bm, ebias};
 }

@@ -336,6 +336,23 @@ void gemm_nt_kernel(const NtArgs p) {
   // ---- epilogue: accumulators -> bf16 tile in LDS (row-major [BM][BN]) ----
   bf16* ct = reinterpret_cast<bf16*>(smem);
   // (the last loop iteration ended with a barrier, staging buffers are free)
+  // Per-column affine on the fp32 accumulator before the bf16 staging
+  // (EPI_AFFINE scale/shift, EPI_BNBWD's folded-BN constant): a shift that
+  // nearly cancels acc must not meet a bf16-rounded acc (finding 33).
+  float cs[NI], cb[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int gc = n0 + wn * WTN + j * 16 + (lane & 15);
+    cs[j] = 1.f;
+    cb[j] = 0.f;
+    if constexpr (EPI == EPI_AFFINE) {
+      if (gc < N && epi_s) cs[j] = epi_s[gc];
+      if (gc < N && epi_t) cb[j] = epi_t[gc];
+    }
+    if constexpr (EPI == EPI_BNBWD) {
+      if (gc < N && p.ebias) cb[j] = p.ebias[gc];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -344,8 +361,8 @@ void gemm_nt_kernel(const NtArgs p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + e;
-        // affine / residual / activation are applied in the row-contiguous store pass
-        ct[row * CT_STRIDE + col] = (bf16)acc[i][j][e];
+        // residual / activation are applied in the row-contiguous store pass
+        ct[row * CT_STRIDE + col] = (bf16)fmaf(acc[i][j][e], cs[j], cb[j]);
       }
     }
   __syncthreads();
@@ -358,31 +375,20 @@ void gemm_nt_kernel(const NtArgs p) {
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
   const bool col_ok = col < N;
-  float es[8], et[8];
-  if constexpr (EPI == EPI_AFFINE) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      // null scale/shift = identity ("add" mode: C = acc + R)
-      es[j] = (col_ok && epi_s) ? epi_s[col + j] : 1.f;
-      et[j] = (col_ok && epi_t) ? epi_t[col + j] : 0.f;
-    }
-  }
   float msum[8], msq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; }
-  float bmu[8], bsc[8], bsh[8], ebv[8];
+  float bmu[8], bsc[8], bsh[8];
   const bf16* __restrict__ bnx = p.bx;
   const bf16* __restrict__ bny = p.bny;
   const int64_t ldbx = p.ldbx, ldby = p.ldby;
   const CompactMap rmap = p.rmap;
-  const bool has_ebias = p.ebias != nullptr;
   if constexpr (EPI == EPI_BNBWD) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bmu[j] = (col_ok && p.bmean) ? p.bmean[col + j] : 0.f;
       bsc[j] = (col_ok && !p.bny) ? p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f) : 0.f;
       bsh[j] = (col_ok && !p.bny) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
-      ebv[j] = (col_ok && p.ebias) ? p.ebias[col + j] : 0.f;
     }
   }
 #pragma unroll
@@ -391,24 +397,17 @@ void gemm_nt_kernel(const NtArgs p) {
     const int row = m0 + lr;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
     if (row < M && col_ok) {
-      if constexpr (EPI == EPI_AFFINE) {
+      if constexpr (EPI == EPI_AFFINE) {  // v = bf16(acc * s + t) (staged)
         f32x8 f = __builtin_convertvector(v, f32x8);
-        f32x8 r{};
-        if (R) r = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + (int64_t)row * ldr + col), f32x8);
+        if (R) f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + (int64_t)row * ldr + col), f32x8);
+        if (epi_relu) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float t = fmaf(f[j], es[j], et[j]) + r[j];
-          f[j] = epi_relu ? fmaxf(t, 0.f) : t;
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
         }
         v = __builtin_convertvector(f, bf16x8);
       }
       if constexpr (EPI == EPI_BNBWD) {
-        f32x8 g = __builtin_convertvector(v, f32x8);
-        if (has_ebias) {  // BN-folded data gradient: the constant term of the folded BN backward
-          g += f32x8{ebv[0], ebv[1], ebv[2], ebv[3], ebv[4], ebv[5], ebv[6], ebv[7]};
-          v = __builtin_convertvector(g, bf16x8);
-          g = __builtin_convertvector(v, f32x8);
-        }
+        f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
         if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
           const int64_t rr = compact_row(rmap, row);
           if (rr >= 0)

@@ -530,13 +530,23 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     return;
   }
   bf16* ct = reinterpret_cast<bf16*>(smem);
-  float bv[NI];
+  // per-column affine applied to the fp32 accumulator BEFORE the bf16 staging:
+  // a bias / BN shift that nearly cancels acc (XL_BNBWD's folded-BN constant,
+  // XL_AFFINE's -mean*scale) must not meet a bf16-rounded acc (finding 33)
+  float bv[NI], sv[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int col = n0 + wc * WTN + j * 16 + (lane & 15);
     bv[j] = 0.f;
+    sv[j] = 1.f;
     if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES)
       bv[j] = col < N ? (float)p.bias[col] : 0.f;
+    if constexpr (EPI == XL_BNBWD)
+      bv[j] = (col < N && p.ebias) ? p.ebias[col] : 0.f;
+    if constexpr (EPI == XL_AFFINE) {
+      sv[j] = (col < N && p.esc) ? p.esc[col] : 1.f;
+      bv[j] = (col < N && p.esh) ? p.esh[col] : 0.f;
+    }
   }
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -546,31 +556,21 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int row = wr * WTM + i * 16 + (lane >> 4) * 4 + e;
-        ct[row * CT_STRIDE + col] = (bf16)(acc[i][j][e] + bv[j]);
+        ct[row * CT_STRIDE + col] = (bf16)fmaf(acc[i][j][e], sv[j], bv[j]);
       }
     }
   __syncthreads();
   constexpr int CV = BN / 8, RPP = XTHREADS / CV;
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
-  float msum[8], msq[8], bmu[8], bsc[8], bsh[8], ebv[8];
+  float msum[8], msq[8], bmu[8], bsc[8], bsh[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = ebv[j] = 0.f; }
-  if constexpr (EPI == XL_AFFINE) {
-    if (col < N) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        bsc[j] = p.esc ? p.esc[col + j] : 1.f;
-        bsh[j] = p.esh ? p.esh[col + j] : 0.f;
-      }
-    }
-  }
+  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = 0.f; }
   if constexpr (EPI == XL_BNBWD) {
     if (col < N) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         bmu[j] = p.bmean ? p.bmean[col + j] : 0.f;
-        ebv[j] = p.ebias ? p.ebias[col + j] : 0.f;
         if (!p.bny) {
           bsc[j] = p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f);
           bsh[j] = (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j];
@@ -596,23 +596,16 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         f32x8 f = __builtin_convertvector(v, f32x8);
         f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
         v = __builtin_convertvector(f, bf16x8);
-      } else if constexpr (EPI == XL_AFFINE) {
+      } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
         f32x8 f = __builtin_convertvector(v, f32x8);
-        f32x8 r{};
-        if (p.R) r = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+        if (p.R) f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+        if (p.erelu) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float t = fmaf(f[j], bsc[j], bsh[j]) + r[j];
-          f[j] = p.erelu ? fmaxf(t, 0.f) : t;
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
         }
         v = __builtin_convertvector(f, bf16x8);
       } else if constexpr (EPI == XL_BNBWD) {
-        f32x8 g = __builtin_convertvector(v, f32x8);
-        if (p.ebias) {  // BN-folded data gradient: constant term of the folded BN backward
-          g += f32x8{ebv[0], ebv[1], ebv[2], ebv[3], ebv[4], ebv[5], ebv[6], ebv[7]};
-          v = __builtin_convertvector(g, bf16x8);
-          g = __builtin_convertvector(v, f32x8);
-        }
+        f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
         if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
           const int64_t rr = compact_row(p.rmap, row);
           if (rr >= 0)

@@ -133,7 +133,7 @@ class _ConvBNFoldFn(torch.autograd.Function):
             if res2 is not None:
                 t = t + res2.double()
             out2 = (t.clamp_min(0) if relu else t).to(a.dtype)
-        ctx.save_for_backward(a, weight, out2, WG.float(), s, mean, invstd, w32, sums[-1:])
+        ctx.save_for_backward(a, weight, out2, WG.float(), a_sums, mean, invstd, w32, sums[-1:])
         ctx.meta = (reduce_grads, relu, residual is not None, native, bn_w is not None, bn_b is not None,
                     bn_w.dtype if bn_w is not None else None)
         # a_slot: the producing BN's backward reductions can ride in our data-gradient epilogue
@@ -153,12 +153,13 @@ class _ConvBNFoldFn(torch.autograd.Function):
     def backward(ctx, dout):
         if dout is None:
             return (None,) * 16
-        a, weight, out2, WG, s, mean, invstd, w32, count = ctx.saved_tensors
+        a, weight, out2, WG, asums, mean, invstd, w32, count = ctx.saved_tensors
         reduce_grads, relu, has_res, native, has_w, has_b, wdtype = ctx.meta
         n, cin, h, w = a.shape
         cout = weight.shape[0]
         a2 = _rows(a)
         W2 = weight.reshape(cout, cin)
+        s = asums[:cin]
         slot = ctx.out_slot
         ctx.out_slot = None
         fused = slot.take(dout) if slot is not None else None
@@ -183,7 +184,7 @@ class _ConvBNFoldFn(torch.autograd.Function):
             local = C.bn_fold_bwd_sums(D, W2, sdz.contiguous(), mean)
             sums = reduce_grads(local.clone()) if reduce_grads is not None else local
             dw2, dg, db, Bb, ebias = C.bn_fold_bwd_coef(sums, local, count, invstd, mean, w32, D,
-                                                        WG, s, W2)
+                                                        WG, asums, W2)
             dw = dw2.view(cout, cin, 1, 1)
             if weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous(memory_format=torch.channels_last)

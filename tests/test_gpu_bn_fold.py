@@ -41,8 +41,7 @@ def test_two_source_gemm_bias_bnbwd(M, N, K1, K2, xl):
     B = (torch.randn(N, K1 + K2, device=DEV) * 0.05).bfloat16()
     bias = torch.randn(N, device=DEV)
     y = torch.relu(torch.randn(M, N, device=DEV)).bfloat16()          # mask source, no BN input
-    ref = (torch.cat([A, A2], 1).float() @ B.float().t()).bfloat16().float() + bias
-    ref = ref.bfloat16().float() * (y.float() > 0)
+    ref = (torch.cat([A, A2], 1).float() @ B.float().t() + bias).bfloat16().float() * (y.float() > 0)
     if xl:
         dz, sums = C.gemm_xl_conv(A, B, "bnbwd", bn_y=y, a2=A2, ebias=bias)
     else:
@@ -55,7 +54,7 @@ def test_two_source_gemm_bias_bnbwd(M, N, K1, K2, xl):
         c2, _ = C.gemm_xl_conv(A, B, "affine", a2=A2, shift=bias)
     else:
         c2, _ = C.gemm_nt(A, B, mode="affine", epi_shift=bias, a2=A2)
-    ref2 = (torch.cat([A, A2], 1).float() @ B.float().t()).bfloat16().float() + bias
+    ref2 = torch.cat([A, A2], 1).float() @ B.float().t() + bias
     _check(c2, ref2, 1e-2)
 
 
@@ -69,8 +68,8 @@ def test_xl_affine_residual_relu(M, N, K):
     sc = torch.rand(N, device=DEV) + 0.5
     sh = torch.randn(N, device=DEV)
     out, _ = C.gemm_xl_conv(A, B, "affine", residual=R, scale=sc, shift=sh, relu=True)
-    acc = (A.float() @ B.float().t()).bfloat16().float()
-    ref = torch.relu(acc * sc + sh + R.float())
+    acc = A.float() @ B.float().t()
+    ref = torch.relu((acc * sc + sh).bfloat16().float() + R.float())  # affine on fp32 acc, then + R
     _check(out, ref, 1e-2)
 
 
@@ -93,9 +92,13 @@ def test_bn_apply_out_moments():
         assert torch.equal(y, y0)
 
 
-def _chain(bn2, conv3, bn3, nxt, raw, res, up):
-    a2, asums = bn2(raw, out_moments=True)
-    out = bn_fold.conv1x1_bn_fold(conv3, bn3, a2, asums, res)
+def _chain(bn2, conv3, bn3, nxt, raw, res, up, fold=True):
+    from distributed_model_parallel_amd.ops.fused import conv_bn
+    if fold:
+        a2, asums = bn2(raw, out_moments=True)
+        out = bn_fold.conv1x1_bn_fold(conv3, bn3, a2, asums, res)
+    else:
+        out = conv_bn(conv3, bn3, bn2(raw), res)
     z = nxt(out)
     (z.float() * up).sum().backward()
     return out
@@ -103,6 +106,9 @@ def _chain(bn2, conv3, bn3, nxt, raw, res, up):
 
 @pytest.mark.parametrize("cin,hw,n", [(64, 56, 6), (128, 28, 16), (256, 14, 32), (512, 7, 64)])
 def test_fold_chain_matches_fp32_reference(cin, hw, n):
+    """Fold vs the unfused native bf16 chain, both measured against the fp32
+    stock chain: the fold may not be less accurate than what it replaces."""
+    import copy
     torch.manual_seed(3)
     cout = 4 * cin
     bn2 = BatchNormAct2d(cin, act="relu").to(DEV)
@@ -113,84 +119,94 @@ def test_fold_chain_matches_fp32_reference(cin, hw, n):
         for bn in (bn2, bn3):
             bn.weight.uniform_(0.5, 1.5)
             bn.bias.normal_(0, 0.2)
-    params32 = {k: v.detach().clone() for k, v in
-                [("w2", bn2.weight), ("b2", bn2.bias), ("w3", conv3.weight), ("g3", bn3.weight),
-                 ("be3", bn3.bias), ("wn", nxt.weight)]}
     for m in (conv3, nxt):
         m.weight.data = m.weight.data.bfloat16().contiguous(memory_format=torch.channels_last)
-    raw = (torch.randn(n, cin, hw, hw, device=DEV) * 2 + 0.5).bfloat16().contiguous(
-        memory_format=torch.channels_last).requires_grad_(True)
-    res = torch.randn(n, cout, hw, hw, device=DEV).bfloat16().contiguous(
-        memory_format=torch.channels_last).requires_grad_(True)
+    mods_u = copy.deepcopy((bn2, conv3, bn3, nxt))
+    raw0 = (torch.randn(n, cin, hw, hw, device=DEV) * 2 + 0.5).bfloat16().contiguous(memory_format=torch.channels_last)
+    res0 = torch.randn(n, cout, hw, hw, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
     up = torch.randn(n, cin, hw, hw, device=DEV).contiguous(memory_format=torch.channels_last)
-    before = bn_fold.stats()
-    out = _chain(bn2, conv3, bn3, nxt, raw, res, up)
-    after = bn_fold.stats()
-    assert after["fold"] == before["fold"] + 1
-    assert after["fold_fused_bwd"] == before["fold_fused_bwd"] + 1          # next conv masked dz
-    assert after["fold_bnbwd_epilogue"] == before["fold_bnbwd_epilogue"] + 1  # bn2 reductions fused
     # fp32 stock reference from the same bf16 inputs / weights
-    p = {k: v.float().requires_grad_(True) for k, v in params32.items()}
-    p["w3"].data = conv3.weight.detach().float().contiguous()
-    p["wn"].data = nxt.weight.detach().float().contiguous()
-    r_raw = raw.detach().float().requires_grad_(True)
-    r_res = res.detach().float().requires_grad_(True)
+    p = {"w2": bn2.weight, "b2": bn2.bias, "w3": conv3.weight, "g3": bn3.weight, "be3": bn3.bias, "wn": nxt.weight}
+    p = {k: v.detach().float().clone().requires_grad_(True) for k, v in p.items()}
+    r_raw = raw0.float().requires_grad_(True)
+    r_res = res0.float().requires_grad_(True)
     a = F.relu(F.batch_norm(r_raw, None, None, p["w2"], p["b2"], True, 0.1, 1e-5))
     y = F.batch_norm(F.conv2d(a, p["w3"]), None, None, p["g3"], p["be3"], True, 0.1, 1e-5)
     o = F.relu(y + r_res)
     (F.conv2d(o, p["wn"]) * up).sum().backward()
-    _check(out, o, 2e-2)
-    _check(res.grad, r_res.grad, 5e-2)
-    _check(raw.grad, r_raw.grad, 5e-2)
-    _check(conv3.weight.grad, p["w3"].grad, 3e-2)
-    _check(bn3.weight.grad, p["g3"].grad, 3e-2)
-    _check(bn3.bias.grad, p["be3"].grad, 3e-2)
-    _check(bn2.weight.grad, p["w2"].grad, 5e-2)
-    _check(bn2.bias.grad, p["b2"].grad, 5e-2)
+
+    def run(mods, fold):
+        raw = raw0.clone().requires_grad_(True)
+        res = res0.clone().requires_grad_(True)
+        out = _chain(*mods, raw, res, up, fold=fold)
+        b2, c3, b3, _ = mods
+        return {"out": (out, o), "res": (res.grad, r_res.grad), "raw": (raw.grad, r_raw.grad),
+                "w3": (c3.weight.grad, p["w3"].grad), "g3": (b3.weight.grad, p["g3"].grad),
+                "be3": (b3.bias.grad, p["be3"].grad), "w2": (b2.weight.grad, p["w2"].grad),
+                "b2": (b2.bias.grad, p["b2"].grad)}, b3
+
+    before = bn_fold.stats()
+    got, bn3f = run((bn2, conv3, bn3, nxt), True)
+    after = bn_fold.stats()
+    assert after["fold"] == before["fold"] + 1
+    assert after["fold_fused_bwd"] == before["fold_fused_bwd"] + 1          # next conv masked dz
+    assert after["fold_bnbwd_epilogue"] == before["fold_bnbwd_epilogue"] + 1  # bn2 reductions fused
+    ref, _ = run(mods_u, False)
+    assert bn_fold.stats()["fold"] == after["fold"]
+    errs = {k: (_rel(*got[k]), _rel(*ref[k])) for k in got}
+    print(f"\n[fold vs unfused rel. error, cin={cin}] " + " ".join(f"{k}={a:.4f}/{b:.4f}" for k, (a, b) in errs.items()))
+    for k, (e_fold, e_unf) in errs.items():
+        # bn2's dgamma/dbeta are sums of O(M) noisy terms whose true value is small:
+        # their relative errors are noise-dominated for both paths
+        slack = 2.0 if k in ("w2", "b2") else 1.3
+        assert e_fold < max(slack * e_unf, 1e-2), f"{k}: fold {e_fold:.4f} vs unfused {e_unf:.4f}"
     # running statistics of bn3 from the Gram algebra vs the stock moments of y
     yd = F.conv2d(a.detach(), p["w3"].detach()).double()
     mean = yd.mean((0, 2, 3))
     var = yd.var((0, 2, 3), unbiased=True)
-    torch.testing.assert_close(bn3.running_mean.double(), 0.1 * mean, rtol=2e-2, atol=2e-3)
-    torch.testing.assert_close(bn3.running_var.double(), 0.9 + 0.1 * var, rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(bn3f.running_mean.double(), 0.1 * mean, rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(bn3f.running_var.double(), 0.9 + 0.1 * var, rtol=2e-2, atol=2e-3)
 
 
 def test_bottleneck_fold_matches_unfused_model():
-    """Two ResNet-50 layer-1 bottlenecks in bf16: fold on vs DMP's unfused
-    native path (bn_fold.ENABLED off) -- outputs and every parameter gradient."""
+    """Two ResNet-50 layer-1 bottlenecks in bf16, fold on vs DMP's unfused
+    native path (bn_fold.ENABLED off), each measured against the same blocks
+    in fp32 stock PyTorch (reference_mode): the fold may not be less accurate."""
     import copy
     from distributed_model_parallel_amd.models.resnet import Bottleneck
     from distributed_model_parallel_amd.utils.precision import cast_model
     torch.manual_seed(4)
     down = torch.nn.Sequential(Conv1x1(64, 256), BatchNormAct2d(256))
-    net = cast_model(torch.nn.Sequential(Bottleneck(64, 64, 1, down), Bottleneck(256, 64))
-                     .to(DEV).to(memory_format=torch.channels_last))
+    base = torch.nn.Sequential(Bottleneck(64, 64, 1, down), Bottleneck(256, 64)).to(DEV)
+    net = cast_model(copy.deepcopy(base).to(memory_format=torch.channels_last))
     ref = copy.deepcopy(net)
-    net.train()
-    ref.train()
+    f32 = copy.deepcopy(net).float()
+    for m in (net, ref, f32):
+        m.train()
     x = torch.randn(8, 64, 56, 56, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
     g = torch.randn(8, 256, 56, 56, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+
+    def run(model, dtype):
+        xi = x.to(dtype).clone().requires_grad_(True)
+        y = model(xi)
+        y.backward(g.to(dtype))
+        return [y.float(), xi.grad.float()] + [p.grad.float() for p in model.parameters()]
+
     before = bn_fold.stats()["fold"]
-    x1 = x.clone().requires_grad_(True)
-    y1 = net(x1)
-    y1.backward(g)
+    got = run(net, torch.bfloat16)
     assert bn_fold.stats()["fold"] == before + 2
     old = bn_fold.ENABLED
     bn_fold.ENABLED = False
     try:
-        x2 = x.clone().requires_grad_(True)
-        y2 = ref(x2)
-        y2.backward(g)
+        unf = run(ref, torch.bfloat16)
     finally:
         bn_fold.ENABLED = old
-    assert bn_fold.stats()["fold"] == before + 2
-    _check(y1, y2, 2e-2)
-    _check(x1.grad, x2.grad, 5e-2)
-    for (n1, p1), (_, p2) in zip(net.named_parameters(), ref.named_parameters()):
-        _check(p1.grad, p2.grad, 6e-2, n1)
-    for (n1, b1), (_, b2) in zip(net.named_buffers(), ref.named_buffers()):
-        if b1.dtype.is_floating_point:
-            _check(b1, b2, 2e-2, n1)
+    with _native.reference_mode():
+        gold = run(f32, torch.float32)
+    names = ["out", "x.grad"] + [n for n, _ in net.named_parameters()]
+    for n, a, b, r in zip(names, got, unf, gold):
+        e_f, e_u = _rel(a, r), _rel(b, r)
+        assert e_f < max(1.3 * e_u, 1e-2), f"{n}: fold {e_f:.4f} vs unfused {e_u:.4f} (fp32 reference)"
 
 
 @pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512)])
@@ -206,7 +222,7 @@ def test_fold_coefficient_kernels_match_fp64(cout, cin):
     asums = torch.cat([ad.sum(0), (ad * ad).sum(0), ad.new_tensor([4096.0])])
     sums, WG = C.bn_fold_fwd(W, G, asums)
     rs, rWG = bn_fold._fold_stats(W, G, asums[:cin], asums[2 * cin:])
-    torch.testing.assert_close(WG.double(), rWG, rtol=1e-5, atol=1e-4)
+    _check(WG, rWG, 1e-5)  # fp32 accumulation: relative to the matrix norm
     torch.testing.assert_close(sums, rs, rtol=1e-6, atol=1e-6)
     D = torch.randn(cout, cin, device=DEV)
     sdz = torch.randn(cout, device=DEV, dtype=torch.float64)
@@ -218,7 +234,7 @@ def test_fold_coefficient_kernels_match_fp64(cout, cin):
     sdzx = (D.double() * Wd).sum(1) - mean.double() * sdz
     torch.testing.assert_close(local, torch.cat([sdz, sdzx]), rtol=1e-9, atol=1e-9)
     cnt = asums[2 * cin:]
-    dW, dg, db, Bm, eb = C.bn_fold_bwd_coef(local, local, cnt, invstd, mean, gamma, D, WG, asums[:cin], W)
+    dW, dg, db, Bm, eb = C.bn_fold_bwd_coef(local, local, cnt, invstd, mean, gamma, D, WG, asums, W)
     istd = invstd.double()
     al = istd * gamma.double()
     be = -al * istd * istd * sdzx / cnt

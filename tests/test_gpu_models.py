@@ -109,11 +109,19 @@ def test_bottleneck_fused_shortcut_grad(stride, ds):
     x = torch.randn(8, cin, 16, 16, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
     g = None
     outs = []
+    from distributed_model_parallel_amd.ops import bn_fold
+    fold_was = bn_fold.ENABLED
     for fused in (True, False):
         xi = x.detach().requires_grad_()
         n0 = conv1x1._STATS["fused_dgrad"]
         if fused:
-            y = blk(xi)
+            # isolate the shortcut fusion: bn3 unfolded (the fold has its own
+            # fp32-referenced tests, tests/test_gpu_bn_fold.py)
+            bn_fold.ENABLED = False
+            try:
+                y = blk(xi)
+            finally:
+                bn_fold.ENABLED = fold_was
         else:
             idn = xi if down is None else down[1](down[0](xi))
             out = blk.bn1(blk.conv1(xi))

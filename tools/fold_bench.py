@@ -65,7 +65,7 @@ def main():
         local = C.bn_fold_bwd_sums(D, w, sdz, sh)
         cnt = asums[2 * cin:]
         c_b = timeit(lambda: (C.bn_fold_bwd_sums(D, w, sdz, sh),
-                              C.bn_fold_bwd_coef(local, local, cnt, sc, sh, sc, D, WG, asums[:cin], w)))
+                              C.bn_fold_bwd_coef(local, local, cnt, sc, sh, sc, D, WG, asums, w)))
         print(f"| {name} | {M} | {cin} | {cout} | {f_nt:.3f} | {f_xl:.3f} | {gbs:.0f} | {d_nt:.3f} | {d_xl:.3f} | "
               f"{g_tn:.3f} | {g_xl:.3f} | {c_f:.3f} | {c_b:.3f} |", flush=True)
         del a, w, res, dz, bm, x2

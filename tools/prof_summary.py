@@ -14,7 +14,8 @@ import os
 import sys
 
 CATS = [
-    ("dmp BN (ours)", ("bn_moments", "bn_apply", "bn_bwd", "bn_reduce")),
+    ("dmp BN (ours)", ("bn_moments", "bn_apply", "bn_bwd", "bn_reduce", "bn_finalize")),
+    ("dmp BN fold coefficients (ours)", ("fold_fwd", "fold_bwd", "fold_coef")),
     ("dmp fused SGD (ours)", ("sgd_flat",)),
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
     ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "split_reduce", "dw_fwd",
