@@ -55,7 +55,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& residual, bool relu,
                                 const std::vector<int64_t>& a_map,
                                 const std::vector<int64_t>& c_map,
-                                const c10::optional<at::Tensor>& a2);
+                                const c10::optional<at::Tensor>& a2,
+                                const std::vector<int64_t>& a2_map);
 std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& residual,
                                       const c10::optional<at::Tensor>& bn_x,
@@ -66,7 +67,8 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& bias,
                                       const std::vector<int64_t>& res_map,
                                       const c10::optional<at::Tensor>& a2,
-                                      const c10::optional<at::Tensor>& ebias);
+                                      const c10::optional<at::Tensor>& ebias,
+                                      const std::vector<int64_t>& a2_map);
 // cross_entropy.hip
 std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& x, const at::Tensor& target,
                                           int64_t ignore_index);
@@ -74,7 +76,7 @@ at::Tensor cross_entropy_bwd(const at::Tensor& grad, const at::Tensor& x, const 
                              const at::Tensor& lse, const at::Tensor& stats, int64_t ignore_index);
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
-                   const c10::optional<at::Tensor>& pro_shift);
+                   const c10::optional<at::Tensor>& pro_shift, bool a_mapped);
 // stem.hip
 at::Tensor space_to_depth2(const at::Tensor& x, int64_t pad, int64_t out_channels);
 at::Tensor pad_channels16(const at::Tensor& x, int64_t pad, int64_t extra_w);
@@ -140,7 +142,8 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& a2,
                                      const c10::optional<at::Tensor>& ebias,
                                      const c10::optional<at::Tensor>& scale,
-                                     const c10::optional<at::Tensor>& shift, bool relu);
+                                     const c10::optional<at::Tensor>& shift, bool relu,
+                                     const std::vector<int64_t>& a2_map);
 // bn_fold.hip
 bool bn_fold_supported(int64_t cout, int64_t cin);
 std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums);
@@ -150,6 +153,9 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
                                          const at::Tensor& invstd, const at::Tensor& mean,
                                          const c10::optional<at::Tensor>& gamma, const at::Tensor& D,
                                          const at::Tensor& WG, const at::Tensor& s, const at::Tensor& W);
+at::Tensor bn_fold_colsum(const at::Tensor& x, const std::vector<int64_t>& map);
+std::vector<at::Tensor> bn_fold_scale_concat(const at::Tensor& W3, const at::Tensor& s3, const at::Tensor& t3,
+                                             const at::Tensor& Wd, const at::Tensor& sd, const at::Tensor& td);
 // attention.hip
 bool attention_supported(int64_t S, int64_t head_dim);
 std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale);
@@ -217,7 +223,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
         py::arg("residual") = py::none(), py::arg("relu") = false,
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},
-        py::arg("a2") = py::none());
+        py::arg("a2") = py::none(), py::arg("a2_map") = std::vector<int64_t>{});
 
   m.def("cross_entropy_fwd", &dmp::cross_entropy_fwd, py::arg("x"), py::arg("target"),
         py::arg("ignore_index") = -100);
@@ -226,11 +232,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_nt_bnbwd", &dmp::gemm_nt_bnbwd, py::arg("A"), py::arg("B"), py::arg("residual"),
         py::arg("bn_x"), py::arg("bn_y"), py::arg("mean"), py::arg("invstd"), py::arg("weight"),
         py::arg("bias"), py::arg("res_map") = std::vector<int64_t>{}, py::arg("a2") = py::none(),
-        py::arg("ebias") = py::none());
+        py::arg("ebias") = py::none(), py::arg("a2_map") = std::vector<int64_t>{});
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
-        py::arg("pro_shift") = py::none());
+        py::arg("pro_shift") = py::none(), py::arg("a_mapped") = false,
+        "C = A^T B (weight gradient); b_map reads B's rows through a strided map, a_mapped A's too (Gram of a sample)");
 
   m.def("set_tn_wide", &dmp::set_tn_wide, py::arg("on"),
         "128 x 256 TN tiles for deep weight gradients (default on)");
@@ -305,7 +312,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(), py::arg("res_map") = std::vector<int64_t>{},
         py::arg("a2") = py::none(), py::arg("ebias") = py::none(), py::arg("scale") = py::none(),
-        py::arg("shift") = py::none(), py::arg("relu") = false,
+        py::arg("shift") = py::none(), py::arg("relu") = false, py::arg("a2_map") = std::vector<int64_t>{},
         "wide 1x1-conv GEMM with conv epilogues: moments | add | bnbwd | affine (scale, shift, residual, relu); "
         "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 7, py::arg("group_m") = 0,
@@ -320,6 +327,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fold_bwd_coef", &dmp::bn_fold_bwd_coef, py::arg("sums"), py::arg("local"), py::arg("count"),
         py::arg("invstd"), py::arg("mean"), py::arg("gamma"), py::arg("D"), py::arg("WG"), py::arg("s"),
         py::arg("W"), "(dW, dgamma, dbeta, Bm = [(al o W)^T | W^T diag(be) W], ebias = c^T W)");
+
+  m.def("bn_fold_colsum", &dmp::bn_fold_colsum, py::arg("x"), py::arg("map") = std::vector<int64_t>{},
+        "fp64 [2C+1] (colsum, colsum of squares, rows) of x's rows sampled through a strided map");
+  m.def("bn_fold_scale_concat", &dmp::bn_fold_scale_concat, py::arg("W3"), py::arg("s3"), py::arg("t3"),
+        py::arg("Wd"), py::arg("sd"), py::arg("td"), "([s3 o W3 | sd o Wd] bf16, t3 + td)");
 
   // ---- fused self-attention on packed qkv (ViT) ----
   m.def("attention_supported", &dmp::attention_supported);

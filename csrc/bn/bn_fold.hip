@@ -17,6 +17,10 @@
 #include "../common.h"
 
 namespace dmp {
+
+void bn_reduce_partials_launch(const float* part, int rb, int C, double* sums, double count,
+                               hipStream_t stream);
+
 namespace {
 
 using bf16 = __bf16;
@@ -262,6 +266,69 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
   }
 }
 
+// Column sums and sums of squares of the rows of x [N*Hi*Wi, C] sampled at
+// stride s ((n, oh*s, ow*s) for the N*Ho*Wo logical rows; s = 1: every row):
+// the colsum a folded downsample's BN statistics need, per-block partials
+// [2][blocks][C] reduced deterministically by bn_reduce_partials_launch.
+// grid = (row blocks); 256 threads = (256 / cv) row lanes x cv channel vectors.
+__global__ __launch_bounds__(kFoldThreads) void fold_colsum_kernel(const bf16* __restrict__ x, int C, int64_t M,
+                                                                   int s, int ho, int wo, int hi, int wi,
+                                                                   int64_t rows_per_block, float* __restrict__ part,
+                                                                   double* __restrict__ zsums) {
+  zero_moments(zsums, 2 * C);
+  __shared__ float ls[kFoldThreads * 8], lq[kFoldThreads * 8];
+  const int cv = C / 8, rpi = kFoldThreads / cv;
+  const int tid = threadIdx.x, lc = tid % cv, lr = tid / cv;
+  float su[8], sq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) su[e] = sq[e] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (lr < rpi) {
+    for (int64_t m = r0 + lr; m < r1; m += rpi) {
+      int64_t pm = m;
+      if (s != 1) {
+        const int64_t hw = (int64_t)ho * wo;
+        const int64_t n = m / hw;
+        const int r = (int)(m - n * hw), oh = r / wo, ow = r - oh * wo;
+        pm = (n * hi + (int64_t)oh * s) * wi + (int64_t)ow * s;
+      }
+      const f32x8 f = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(x + pm * C + lc * 8), f32x8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { su[e] += f[e]; sq[e] = fmaf(f[e], f[e], sq[e]); }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { ls[e * kFoldThreads + tid] = su[e]; lq[e * kFoldThreads + tid] = sq[e]; }
+  __syncthreads();
+  for (int o = tid; o < C; o += kFoldThreads) {
+    const int c_l = o / 8, e = o % 8;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rpi; ++r) {
+      a += ls[e * kFoldThreads + r * cv + c_l];
+      b += lq[e * kFoldThreads + r * cv + c_l];
+    }
+    part[(int64_t)blockIdx.x * C + o] = a;
+    part[(int64_t)(gridDim.x + blockIdx.x) * C + o] = b;
+  }
+}
+
+// Bf = [s3 o W3 | sd o Wd] (bf16 [Cout, C3 + Cd]) and shift = t3 + td: the
+// operand and epilogue constant of a bottleneck whose bn3 and downsample BN
+// are both folded into one GEMM over [a | x_s].
+__global__ __launch_bounds__(kFoldThreads) void fold_scale_concat_kernel(
+    const bf16* __restrict__ W3, const float* __restrict__ s3, const float* __restrict__ t3, int C3,
+    const bf16* __restrict__ Wd, const float* __restrict__ sd, const float* __restrict__ td, int Cd, int Cout,
+    bf16* __restrict__ Bf, float* __restrict__ shift) {
+  const int ld = C3 + Cd;
+  const int64_t n = (int64_t)Cout * ld;
+  for (int64_t v = (int64_t)blockIdx.x * kFoldThreads + threadIdx.x; v < n; v += (int64_t)gridDim.x * kFoldThreads) {
+    const int k = (int)(v / ld), c = (int)(v - (int64_t)k * ld);
+    const float w = c < C3 ? s3[k] * (float)W3[(int64_t)k * C3 + c] : sd[k] * (float)Wd[(int64_t)k * Cd + c - C3];
+    Bf[v] = (bf16)w;
+    if (c == 0) shift[k] = t3[k] + td[k];
+  }
+}
+
 void check_f32(const at::Tensor& t, int64_t n, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n, name,
               " must be a contiguous fp32 GPU tensor of ", n, " elements");
@@ -369,6 +436,58 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   else hipLaunchKernelGGL(fold_bwd_coef_kernel<4>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
   DMP_HIP_CHECK(hipGetLastError());
   return {dW, dgb[0], dgb[1], Bm, ebias};
+}
+
+// fp64 [2C+1] = (colsum, colsum of squares, rows) of x's rows sampled through
+// map [s, Ho, Wo, Hi, Wi] (empty: all rows).
+at::Tensor bn_fold_colsum(const at::Tensor& x, const std::vector<int64_t>& map) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
+              "x must be a contiguous bf16 [rows, C] GPU tensor");
+  const int64_t C = x.size(1);
+  TORCH_CHECK(C % 8 == 0 && C <= 8 * kFoldThreads, "C % 8 == 0, C <= 2048");
+  int s = 1, ho = 1, wo = 1, hi = 1, wi = 1;
+  int64_t M = x.size(0);
+  if (!map.empty()) {
+    TORCH_CHECK(map.size() == 5, "map must be [stride, Ho, Wo, Hi, Wi]");
+    s = (int)map[0]; ho = (int)map[1]; wo = (int)map[2]; hi = (int)map[3]; wi = (int)map[4];
+    TORCH_CHECK(x.size(0) % ((int64_t)hi * wi) == 0 && (ho - 1) * s < hi && (wo - 1) * s < wi, "bad map");
+    M = x.size(0) / ((int64_t)hi * wi) * ho * wo;
+  }
+  auto sums = at::empty({2 * C + 1}, x.options().dtype(at::kDouble));
+  if (M == 0) return sums.zero_();
+  const int rpi = kFoldThreads / (int)(C / 8);
+  int64_t blocks = std::min<int64_t>(1024, (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16));
+  const int64_t rpb = (M + blocks - 1) / blocks;
+  blocks = (M + rpb - 1) / rpb;
+  auto part = at::empty({2, blocks, C}, x.options().dtype(at::kFloat));
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(fold_colsum_kernel, dim3((unsigned)blocks), dim3(kFoldThreads), 0, stream,
+                     reinterpret_cast<const bf16*>(x.data_ptr()), (int)C, M, s, ho, wo, hi, wi, rpb,
+                     part.data_ptr<float>(), moments_zero_target(sums.data_ptr<double>(), (int)blocks));
+  bn_reduce_partials_launch(part.data_ptr<float>(), (int)blocks, (int)C, sums.data_ptr<double>(), (double)M, stream);
+  DMP_HIP_CHECK(hipGetLastError());
+  return sums;
+}
+
+// (Bf bf16 [Cout, C3 + Cd] = [s3 o W3 | sd o Wd], shift fp32 [Cout] = t3 + td).
+std::vector<at::Tensor> bn_fold_scale_concat(const at::Tensor& W3, const at::Tensor& s3, const at::Tensor& t3,
+                                             const at::Tensor& Wd, const at::Tensor& sd, const at::Tensor& td) {
+  for (const at::Tensor* w : {&W3, &Wd})
+    TORCH_CHECK(w->is_cuda() && w->scalar_type() == at::kBFloat16 && w->dim() == 2 && w->is_contiguous(),
+                "weights must be contiguous bf16 [Cout, C] GPU tensors");
+  const int64_t Cout = W3.size(0), C3 = W3.size(1), Cd = Wd.size(1);
+  TORCH_CHECK(Wd.size(0) == Cout, "W3 / Wd Cout mismatch");
+  check_f32(s3, Cout, "s3"); check_f32(t3, Cout, "t3"); check_f32(sd, Cout, "sd"); check_f32(td, Cout, "td");
+  auto Bf = at::empty({Cout, C3 + Cd}, W3.options());
+  auto shift = at::empty({Cout}, W3.options().dtype(at::kFloat));
+  const int64_t n = Cout * (C3 + Cd);
+  const unsigned blocks = (unsigned)std::min<int64_t>(2048, (n + kFoldThreads - 1) / kFoldThreads);
+  hipLaunchKernelGGL(fold_scale_concat_kernel, dim3(blocks), dim3(kFoldThreads), 0, at::hip::getCurrentHIPStream(),
+                     reinterpret_cast<const bf16*>(W3.data_ptr()), s3.data_ptr<float>(), t3.data_ptr<float>(), (int)C3,
+                     reinterpret_cast<const bf16*>(Wd.data_ptr()), sd.data_ptr<float>(), td.data_ptr<float>(), (int)Cd,
+                     (int)Cout, reinterpret_cast<bf16*>(Bf.data_ptr()), shift.data_ptr<float>());
+  DMP_HIP_CHECK(hipGetLastError());
+  return {Bf, shift};
 }
 
 }  // namespace dmp

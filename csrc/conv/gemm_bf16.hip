@@ -95,6 +95,7 @@ struct ConvMap {
   int kw = 1, stride = 1, pad = 0, hi = 1, wi = 1, ho = 1, wo = 1, kc = 0, transposed = 0;
   int py = 0, px = 0;
   int8_t ptr[16] = {}, ptc[16] = {};
+  int amap = 0;  // TN only: A rows mapped like B's tap (0, 0) -- the Gram x_s^T x_s of a strided sample
 };
 
 struct NtArgs {
@@ -121,6 +122,7 @@ struct NtArgs {
   // Second A source (non-CONV): K columns k >= K1 read A2[row, k - K1] -- the
   // operand [dz | a] of a BN-folded data gradient (ops/bn_fold.py).  K1 % 8 == 0.
   const bf16* A2; int64_t lda2; int K1;
+  RowMap a2map;                 // A2 rows through a strided map (the x_s of a folded downsample)
   const float* ebias;           // EPI_BNBWD: per-column bias added to the GEMM output
 };
 
@@ -200,7 +202,7 @@ void gemm_nt_kernel(const NtArgs p) {
       }
     } else {
       arow[i] = row < M ? A + map_row(amap, row) * lda : nullptr;
-      arow2[i] = (row < M && p.A2) ? p.A2 + map_row(amap, row) * p.lda2 - p.K1 : nullptr;
+      arow2[i] = (row < M && p.A2) ? p.A2 + map_row(p.a2map, row) * p.lda2 - p.K1 : nullptr;
     }
   }
   bool aval[A_VECS];
@@ -616,7 +618,15 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm_tn_kernel(
     for (int i = 0; i < A_VECS; ++i) {
       const int v = tid + i * kThreads, r = v / A_VPR, c = (v % A_VPR) * 8;
       const int64_t m = m0 + r;
-      ra[i] = (m < me && n0 + c < N) ? *reinterpret_cast<const bf16x8*>(A + m * lda + n0 + c) : bf16x8{};
+      int64_t am = m;
+      if (bmap.amap) {  // physical pixel (n, oh*s, ow*s)
+        const int hw = bmap.ho * bmap.wo;
+        const int n = (int)(m / hw);
+        const int rr = (int)(m - (int64_t)n * hw);
+        const int oh = rr / bmap.wo, ow = rr - oh * bmap.wo;
+        am = ((int64_t)n * bmap.hi + oh * bmap.stride) * bmap.wi + ow * bmap.stride;
+      }
+      ra[i] = (m < me && n0 + c < N) ? *reinterpret_cast<const bf16x8*>(A + am * lda + n0 + c) : bf16x8{};
     }
 #pragma unroll
     for (int i = 0; i < B_VECS; ++i) {
@@ -862,13 +872,21 @@ void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out
 // B's logical row m from the strided physical row (stride-s 1x1 conv input).
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
-                   const c10::optional<at::Tensor>& pro_shift) {
+                   const c10::optional<at::Tensor>& pro_shift, bool a_mapped) {
   check_operand(A, "A");
   check_operand(B, "B");
   const RowMap rm = parse_map(b_map, "b_map");
   ConvMap cm;  // kc == 0: identity rows
+  TORCH_CHECK(!a_mapped || rm.s != 1, "a_mapped needs a strided b_map");
   if (rm.s == 1) {
     TORCH_CHECK(A.size(0) == B.size(0), "A/B M mismatch");
+  } else if (a_mapped) {  // Gram of a strided sample: A and B rows both through the map
+    TORCH_CHECK(A.size(0) == B.size(0) && B.size(0) % ((int64_t)rm.hi * rm.wi) == 0,
+                "a_mapped: A and B are the same physical rows");
+    cm.kw = 1; cm.stride = rm.s; cm.pad = 0;
+    cm.hi = rm.hi; cm.wi = rm.wi; cm.ho = rm.ho; cm.wo = rm.wo;
+    cm.kc = (int)B.size(1);
+    cm.amap = 1;
   } else {
     TORCH_CHECK(B.size(0) % ((int64_t)rm.hi * rm.wi) == 0 &&
                     A.size(0) == B.size(0) / ((int64_t)rm.hi * rm.wi) * rm.ho * rm.wo,
@@ -877,7 +895,8 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
     cm.hi = rm.hi; cm.wi = rm.wi; cm.ho = rm.ho; cm.wo = rm.wo;
     cm.kc = (int)B.size(1);
   }
-  const int M = (int)A.size(0), N = (int)A.size(1), K = (int)B.size(1);
+  const int M = cm.amap ? (int)(B.size(0) / ((int64_t)rm.hi * rm.wi) * rm.ho * rm.wo) : (int)A.size(0);
+  const int N = (int)A.size(1), K = (int)B.size(1);
   TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "N and K must be multiples of 8");
   const float* bps = nullptr;
   const float* bpt = nullptr;
@@ -1021,10 +1040,15 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
 
 namespace {
 // [A | A2] along K: A2 [rows(A), K2] row-major; the GEMM's K becomes K(A) + K2.
-void set_second_source(NtArgs& a, const at::Tensor& A, const c10::optional<at::Tensor>& a2) {
+void set_second_source(NtArgs& a, const at::Tensor& A, const c10::optional<at::Tensor>& a2,
+                       const std::vector<int64_t>& a2_map) {
   if (!(a2.has_value() && a2->defined())) return;
   check_operand(*a2, "a2");
-  TORCH_CHECK(a2->size(0) == A.size(0) && a2->size(1) % 8 == 0, "a2 must be [rows(A), K2], K2 % 8 == 0");
+  a.a2map = parse_map(a2_map, "a2_map");
+  const RowMap& m = a.a2map;
+  const int64_t rows = m.s == 1 ? a2->size(0) : a2->size(0) / ((int64_t)m.hi * m.wi) * m.ho * m.wo;
+  TORCH_CHECK(m.s == 1 || a2->size(0) % ((int64_t)m.hi * m.wi) == 0, "a2_map does not match a2's rows");
+  TORCH_CHECK(rows == a.M && a2->size(1) % 8 == 0, "a2 must be [GEMM rows (through a2_map), K2], K2 % 8 == 0");
   a.A2 = reinterpret_cast<const bf16*>(a2->data_ptr());
   a.lda2 = a2->stride(0);
   a.K1 = a.K;
@@ -1048,7 +1072,8 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
                                 const c10::optional<at::Tensor>& residual, bool relu,
                                 const std::vector<int64_t>& a_map,
                                 const std::vector<int64_t>& c_map,
-                                const c10::optional<at::Tensor>& a2) {
+                                const c10::optional<at::Tensor>& a2,
+                                const std::vector<int64_t>& a2_map) {
   check_operand(A, "A");
   check_operand(B, "B");
   NtArgs a{};
@@ -1066,7 +1091,7 @@ std::vector<at::Tensor> gemm_nt(const at::Tensor& A, const at::Tensor& B,
   a.M = (int)m64;
   a.K = (int)A.size(1);
   a.N = (int)B.size(0);
-  set_second_source(a, A, a2);
+  set_second_source(a, A, a2, a2_map);
   TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
   TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
   TORCH_CHECK(!a.A2 || !(pro_scale.has_value() && pro_scale->defined()), "a2 has no prologue variant");
@@ -1221,7 +1246,8 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const c10::optional<at::Tensor>& bias,
                                       const std::vector<int64_t>& res_map,
                                       const c10::optional<at::Tensor>& a2,
-                                      const c10::optional<at::Tensor>& ebias) {
+                                      const c10::optional<at::Tensor>& ebias,
+                                      const std::vector<int64_t>& a2_map) {
   check_operand(A, "A");
   check_operand(B, "B");
   const bool has_x = bn_x.has_value() && bn_x->defined();
@@ -1232,7 +1258,7 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
   a.M = (int)A.size(0);
   a.K = (int)A.size(1);
   a.N = (int)B.size(0);
-  set_second_source(a, A, a2);
+  set_second_source(a, A, a2, a2_map);
   TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
   TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
   auto f32vec = [&](const at::Tensor& t, const char* name) {

@@ -169,6 +169,7 @@ struct XlArgs {
   // second A source (plain GEMM): K columns k >= K1 come from A2[row, k - K1]
   // (the [dz | a] operand of a BN-folded data gradient); K1 % 64 == 0
   const bf16* A2; int64_t lda2; int K1;
+  XlOutMap a2m;                 // A2 rows through a strided map (x_s of a folded downsample)
   const float* ebias;           // XL_BNBWD: per-column constant added to the GEMM output
   const float *esc, *esh;       // XL_AFFINE coefficients (null: 1 / 0)
   int erelu;                    // XL_AFFINE ReLU
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   for (int q = 0; q < NA; ++q) {
     const int r = (wave * NA + q) * 16 + srow;
     asrc[q] = A + (int64_t)min(m0 + r, M - 1) * lda + schunk * 8;
-    asrc2[q] = p.A2 ? p.A2 + (int64_t)min(m0 + r, M - 1) * p.lda2 + schunk * 8 - p.K1 : nullptr;
+    asrc2[q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + r, M - 1)) * p.lda2 + schunk * 8 - p.K1 : nullptr;
   }
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
@@ -332,7 +333,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       const int j = (2 * wave + q) & 7;
       const int ba = (j & 3) + 8 * (j >> 2) + 4 * v, bb = (j & 1) + 4 * (j >> 1) + 2 * v;
       pa[v][q] = A + (int64_t)min(m0 + ba * 16 + srow, M - 1) * lda + schunk * 8 + pks * 32;
-      pa2[v][q] = p.A2 ? p.A2 + (int64_t)min(m0 + ba * 16 + srow, M - 1) * p.lda2 + schunk * 8 + pks * 32 - p.K1
+      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ba * 16 + srow, M - 1)) * p.lda2 + schunk * 8 + pks * 32 -
+                             p.K1
                        : nullptr;
       pb[v][q] = B + (int64_t)min(n0 + bb * 16 + srow, N - 1) * ldb + schunk * 8 + pks * 32;
       oa[v][q] = ba * 1024;
@@ -1374,15 +1376,25 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const c10::optional<at::Tensor>& a2,
                                      const c10::optional<at::Tensor>& ebias,
                                      const c10::optional<at::Tensor>& scale,
-                                     const c10::optional<at::Tensor>& shift, bool relu) {
+                                     const c10::optional<at::Tensor>& shift, bool relu,
+                                     const std::vector<int64_t>& a2_map) {
   check_bf16_2d(A, "A");
   check_bf16_2d(B, "B");
   const int64_t M = A.size(0), K1 = A.size(1), N = B.size(0);
   int64_t K = K1;
   const bool two = a2.has_value() && a2->defined();
+  XlOutMap a2m;
   if (two) {
     check_bf16_2d(*a2, "a2");
-    TORCH_CHECK(a2->size(0) == M && K1 % XBK == 0, "gemm_xl_conv: a2 must be [M, K2] and K(A) % 64 == 0");
+    int64_t rows = a2->size(0);
+    if (!a2_map.empty()) {
+      TORCH_CHECK(a2_map.size() == 5, "a2_map must be [stride, Ho, Wo, Hi, Wi]");
+      a2m.s = (int)a2_map[0]; a2m.ho = (int)a2_map[1]; a2m.wo = (int)a2_map[2];
+      a2m.hi = (int)a2_map[3]; a2m.wi = (int)a2_map[4];
+      TORCH_CHECK(rows % ((int64_t)a2m.hi * a2m.wi) == 0, "a2_map does not match a2's rows");
+      rows = rows / ((int64_t)a2m.hi * a2m.wi) * a2m.ho * a2m.wo;
+    }
+    TORCH_CHECK(rows == M && K1 % XBK == 0, "gemm_xl_conv: a2 must be [M (through a2_map), K2], K(A) % 64 == 0");
     K += a2->size(1);
   }
   TORCH_CHECK(B.size(1) == K && K % XBK == 0 && K >= XBK && N % 8 == 0, "gemm_xl_conv: bad shape");
@@ -1394,6 +1406,7 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
   if (two) {
     a.A2 = reinterpret_cast<const bf16*>(a2->data_ptr()); a.lda2 = a2->stride(0); a.K1 = (int)K1;
+    a.a2m = a2m;
   }
   if (mode == "affine")  // scale / shift travel in the mean / invstd slots of xl_conv_run
     return xl_conv_run(a, A, mode, residual, bn_x, bn_y, scale, shift, weight, bias, res_map, ebias, relu);

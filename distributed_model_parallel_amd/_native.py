@@ -84,6 +84,7 @@ FEATURES = {
     "stem_halo": "halo-tiled stem kernels (stem_halo.hip) -> row-tap implicit GEMM",
     "rowtap_stem": "row-tap stem implicit GEMM (stem.hip) -> MIOpen",
     "bn_fold": "bottleneck bn3 folded through conv3 (ops/bn_fold.py) -> conv + BN apply passes",
+    "bn_fold_ds": "downsample conv + BN folded into the same GEMM as bn3 (ops/bn_fold.py) -> separate shortcut",
 }
 _disabled_cache: Optional[frozenset] = None
 

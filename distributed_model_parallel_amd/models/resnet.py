@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.bn_fold import conv1x1_bn_fold, foldable
+from ..ops.bn_fold import conv1x1_bn_fold, foldable, foldable_downsample
 from ..ops.conv1x1 import Conv1x1
 from ..ops.conv_igemm import ConvIG2d
 from ..ops.fused import GradSlot, bn_relu_conv1x1, conv_bn, conv_bn_maxpool, grad_tap
@@ -95,14 +95,21 @@ class Bottleneck(nn.Module):
         # The shortcut is built AFTER conv1 so its backward nodes run first.
         slot = GradSlot() if (self.training and torch.is_grad_enabled()) else None
         out = conv_bn(self.conv1, self.bn1, x, grad_slot=slot)
-        identity = _shortcut(self.downsample, grad_tap(x, slot))
+        xt = grad_tap(x, slot)
+        fold = (self.training and not _FUSE_BN2_CONV3 and foldable(self.conv3, self.bn3, out)
+                and isinstance(self.bn2, BatchNormAct2d))
+        # the downsample conv + BN join the same folded GEMM (ops/bn_fold.py): its
+        # output and the residual tensor are never materialised either
+        fold_ds = fold and self.downsample is not None and foldable_downsample(
+            self.downsample, xt, self.conv3.weight.shape[0])
+        identity = None if fold_ds else _shortcut(self.downsample, xt)
         if _FUSE_BN2_CONV3 and self.training and isinstance(self.bn3, BatchNormAct2d) \
                 and hasattr(self.conv2, "forward_with_moments"):
             # bn2's apply + ReLU runs inside conv3's GEMM (never materialised)
             raw, sums2 = self.conv2.forward_with_moments(out)
             out, sums3 = bn_relu_conv1x1(self.bn2, self.conv3, raw, sums2)
             return self.bn3(out, identity, sums=sums3)
-        if self.training and foldable(self.conv3, self.bn3, out) and isinstance(self.bn2, BatchNormAct2d):
+        if fold:
             # bn3 folded through conv3 (ops/bn_fold.py): conv3's 4x-wide output is
             # never materialised; bn2's apply pass also reduces colsum(a2)
             if hasattr(self.conv2, "forward_with_moments"):
@@ -110,6 +117,8 @@ class Bottleneck(nn.Module):
             else:
                 raw, sums2 = self.conv2(out), None
             a2, asums = self.bn2(raw, sums=sums2, out_moments=True)
+            if fold_ds:
+                return conv1x1_bn_fold(self.conv3, self.bn3, a2, asums, downsample=self.downsample, x=xt)
             return conv1x1_bn_fold(self.conv3, self.bn3, a2, asums, identity)
         out = conv_bn(self.conv2, self.bn2, out)
         return conv_bn(self.conv3, self.bn3, out, identity)

@@ -86,82 +86,118 @@ def _xl_fwd(cout: int, cin: int) -> bool:
     return _xl(cout, cin)
 
 
+def _map_rows(x2: torch.Tensor, geom, n: int):
+    """The rows of x2 [N*Hi*Wi, C] a stride-s 1x1 conv reads (CPU path)."""
+    if not geom:
+        return x2
+    s, ho, wo, hi, wi = geom
+    return x2.view(n, hi, wi, -1)[:, ::s, ::s].reshape(n * ho * wo, -1)
+
+
+class _FoldMeta:
+    """Non-tensor configuration of one folded call: per BN (running_mean,
+    running_var, momentum, eps, num_batches_tracked, reduce_moments,
+    reduce_grads), the downsample stride, the BnBwdSlots and the GradSlot
+    that may take the shortcut's gradient compact."""
+    __slots__ = ("bn", "relu", "stride", "a_slot", "out_slot", "x_park")
+
+    def __init__(self, bn, relu, stride=1, a_slot=None, out_slot=None, x_park=None):
+        self.bn, self.relu, self.stride = bn, relu, stride
+        self.a_slot, self.out_slot, self.x_park = a_slot, out_slot, x_park
+
+
+def _bn_spec(bn: nn.Module):
+    rmom, rgrad = bn._moment_reducers()
+    return (bn.running_mean, bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked, rmom, rgrad)
+
+
 class _ConvBNFoldFn(torch.autograd.Function):
-    """out = relu(bn(conv1x1(a)) + residual), BN folded (module docstring)."""
+    """out = relu(bn3(conv3(a)) + residual)              (one branch), or
+    out = relu(bn3(conv3(a)) + bn_d(conv_d(x_s)))        (two: the downsample
+    folded too -- one GEMM over [a | x_s], x_s = x sampled at the stride),
+    BNs folded (module docstring)."""
 
     @staticmethod
-    def forward(ctx, a, a_sums, weight, bn_w, bn_b, residual, running_mean, running_var, momentum, eps,
-                nbt, reduce_moments, reduce_grads, relu, a_slot, out_slot):
+    def forward(ctx, meta, a, a_sums, w3, g3, b3, x, wd, gd, bd, residual):
         native = _native.gpu_path(a)
+        C = _native.require("bn_fold") if native else None
         n, cin, h, w = a.shape
-        cout = weight.shape[0]
+        cout = w3.shape[0]
         a2 = _rows(a)
-        W2 = weight.reshape(cout, cin)
-        count = a_sums[2 * cin:2 * cin + 1]
-        s = a_sums[:cin]
+        br = [dict(inp=a2, asums=a_sums, W=w3.reshape(cout, cin), g=g3, b=b3, spec=meta.bn[0], geom=[])]
+        if x is not None:
+            cx, hi, wi = x.shape[1], x.shape[2], x.shape[3]
+            from .conv1x1 import _geom
+            geom = _geom(meta.stride, hi, wi)
+            x2 = _rows(x)
+            xs = C.bn_fold_colsum(x2, geom) if native else _cpu_moments(_map_rows(x2, geom, n))
+            br.append(dict(inp=x2, asums=xs, W=wd.reshape(cout, cx), g=gd, b=bd, spec=meta.bn[1], geom=geom))
+        for b in br:
+            b.update(_fold_branch_forward(C, b, n, native))
         if native:
-            from .conv1x1 import _tn_xl
-            C = _native.require("bn_fold")
-            G = C.gemm_tn_xl(a2, a2, torch.float32) if _tn_xl(a2.shape[0], cin, cin) \
-                else C.gemm_tn(a2, a2, torch.float32)
-        else:
-            ad = a2.double()
-            G = ad.t() @ ad
-        if native and C.bn_fold_supported(cout, cin):
-            sums, WG = C.bn_fold_fwd(W2, G, a_sums)   # one launch: W G and the row dots
-        else:
-            sums, WG = _fold_stats(W2, G, s, count)
-        if reduce_moments is not None:
-            sums = reduce_moments(sums)
-        w32 = bn_w.float() if bn_w is not None else None
-        b32 = bn_b.float() if bn_b is not None else None
-        rm = running_mean if (running_mean is not None and running_mean.dtype == torch.float32) else None
-        rv = running_var if rm is not None else None
-        scale, shift, mean, invstd = _finalize(sums, w32, b32, rm, rv, momentum, eps, cout, nbt, native)
-        res2 = _rows(residual.to(a.dtype).contiguous(memory_format=torch.channels_last)) \
-            if residual is not None else None
-        if native:
-            if _xl_fwd(cout, cin):
-                out2, _ = C.gemm_xl_conv(a2, W2, "affine", residual=res2, scale=scale.contiguous(),
-                                         shift=shift.contiguous(), relu=relu)
+            xl = _xl_fwd(cout, cin)
+            if len(br) == 1:
+                res2 = _rows(residual.to(a.dtype).contiguous(memory_format=torch.channels_last)) \
+                    if residual is not None else None
+                if xl:
+                    out2, _ = C.gemm_xl_conv(a2, br[0]["W"], "affine", residual=res2, scale=br[0]["scale"],
+                                             shift=br[0]["shift"], relu=meta.relu)
+                else:
+                    out2, _ = C.gemm_nt(a2, br[0]["W"], mode="affine", epi_scale=br[0]["scale"],
+                                        epi_shift=br[0]["shift"], residual=res2, relu=meta.relu)
             else:
-                out2, _ = C.gemm_nt(a2, W2, mode="affine", epi_scale=scale.contiguous(),
-                                    epi_shift=shift.contiguous(), residual=res2, relu=relu)
+                # both BN scales folded into the operand, the shifts summed: one GEMM over [a | x_s]
+                Bf, shift = C.bn_fold_scale_concat(br[0]["W"], br[0]["scale"], br[0]["shift"], br[1]["W"],
+                                                   br[1]["scale"], br[1]["shift"])
+                if xl:
+                    out2, _ = C.gemm_xl_conv(a2, Bf, "affine", shift=shift, relu=meta.relu, a2=br[1]["inp"],
+                                             a2_map=br[1]["geom"])
+                else:
+                    out2, _ = C.gemm_nt(a2, Bf, mode="affine", epi_shift=shift, relu=meta.relu, a2=br[1]["inp"],
+                                        a2_map=br[1]["geom"])
         else:
-            y = (a2.double() @ W2.double().t()).to(a.dtype).double()
-            t = y * scale.double() + shift.double()
-            if res2 is not None:
-                t = t + res2.double()
-            out2 = (t.clamp_min(0) if relu else t).to(a.dtype)
-        ctx.save_for_backward(a, weight, out2, WG.float(), a_sums, mean, invstd, w32, sums[-1:])
-        ctx.meta = (reduce_grads, relu, residual is not None, native, bn_w is not None, bn_b is not None,
-                    bn_w.dtype if bn_w is not None else None)
-        # a_slot: the producing BN's backward reductions can ride in our data-gradient epilogue
-        ctx.a_slot = a_slot if native else None
-        if ctx.a_slot is not None:
-            a_slot.consumers += 1
-        ctx.out_slot = None
-        if out_slot is not None and native and relu:
-            out_slot.y2 = out2     # mask source; x2 stays None: the consumer reduces sum dz only
-            out_slot.mean = mean
-            ctx.out_slot = out_slot
+            t = 0.0
+            for b in br:
+                y = (_map_rows(b["inp"], b["geom"], n).double() @ b["W"].double().t()).to(a.dtype).double()
+                t = t + y * b["scale"].double() + b["shift"].double()
+            if residual is not None:
+                t = t + _rows(residual).double()
+            out2 = (t.clamp_min(0) if meta.relu else t).to(a.dtype)
+        saved = [a, x, w3, wd, out2]
+        for b in br:
+            saved += [b["WG"], b["asums"], b["mean"], b["invstd"], b["w32"], b["count"]]
+        ctx.save_for_backward(*saved)
+        ctx.nbr = len(br)
+        ctx.geoms = [b["geom"] for b in br]
+        ctx.meta = meta
+        ctx.native = native
+        ctx.has_res = residual is not None
+        ctx.wdtypes = (g3.dtype if g3 is not None else None, gd.dtype if gd is not None else None)
+        if native and meta.a_slot is not None:
+            meta.a_slot.consumers += 1  # the producing BN's reductions can ride in our dgrad epilogue
+        if native and meta.out_slot is not None and meta.relu:
+            meta.out_slot.y2 = out2     # mask source; x2 stays None: the consumer reduces sum dz only
+            meta.out_slot.mean = br[0]["mean"]
+        else:
+            meta.out_slot = None
         ctx.set_materialize_grads(False)
-        _STATS["fold"] += 1
+        _STATS["fold" if len(br) == 1 else "fold_ds"] += 1
         return _unrows(out2, n, h, w)
 
     @staticmethod
     def backward(ctx, dout):
+        nret = 11
         if dout is None:
-            return (None,) * 16
-        a, weight, out2, WG, asums, mean, invstd, w32, count = ctx.saved_tensors
-        reduce_grads, relu, has_res, native, has_w, has_b, wdtype = ctx.meta
+            return (None,) * nret
+        a, x, w3, wd, out2 = ctx.saved_tensors[:5]
+        rest = ctx.saved_tensors[5:]
+        meta, native = ctx.meta, ctx.native
+        C = _native.require("bn_fold backward") if native else None
         n, cin, h, w = a.shape
-        cout = weight.shape[0]
+        cout = w3.shape[0]
         a2 = _rows(a)
-        W2 = weight.reshape(cout, cin)
-        s = asums[:cin]
-        slot = ctx.out_slot
-        ctx.out_slot = None
+        slot = meta.out_slot
+        meta.out_slot = None
         fused = slot.take(dout) if slot is not None else None
         dz2 = _rows(dout.contiguous(memory_format=torch.channels_last).to(a.dtype))
         if fused is not None:
@@ -169,75 +205,161 @@ class _ConvBNFoldFn(torch.autograd.Function):
             _STATS["fold_fused_bwd"] += 1
             sdz = fused[:cout]
         else:
-            if relu:
+            if meta.relu:
                 dz2 = torch.where(out2 > 0, dz2, torch.zeros((), dtype=dz2.dtype, device=dz2.device))
             sdz = dz2.sum(0, dtype=torch.float64)
-        if native:
-            from .conv1x1 import _tn_xl
-            C = _native.require("bn_fold backward")
-            D = C.gemm_tn_xl(dz2, a2, torch.float32) if _tn_xl(a2.shape[0], cout, cin) \
-                else C.gemm_tn(dz2, a2, torch.float32)
-        else:
-            D = dz2.double().t() @ a2.double()
-        if native and C.bn_fold_supported(cout, cin):
-            # two launches: the row dots, then every coefficient-level output
-            local = C.bn_fold_bwd_sums(D, W2, sdz.contiguous(), mean)
-            sums = reduce_grads(local.clone()) if reduce_grads is not None else local
-            dw2, dg, db, Bb, ebias = C.bn_fold_bwd_coef(sums, local, count, invstd, mean, w32, D,
-                                                        WG, asums, W2)
-            dw = dw2.view(cout, cin, 1, 1)
-            if weight.is_contiguous(memory_format=torch.channels_last):
-                dw = dw.contiguous(memory_format=torch.channels_last)
-            da = _FoldDgrad.run(ctx, C, dz2, a2, Bb, ebias, n, cin, h, w) if ctx.needs_input_grad[0] else None
-            gres = _unrows(dz2, n, h, w) if (has_res and ctx.needs_input_grad[5]) else None
-            gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[3] else None
-            gb = db.to(wdtype) if has_b and ctx.needs_input_grad[4] else None
-            return da, None, dw, gw, gb, gres, None, None, None, None, None, None, None, None, None, None
-        Wd = W2.double()
-        Dd = D.double()
-        sdzx = (Dd * Wd).sum(1) - mean.double() * sdz
-        local = torch.cat([sdz, sdzx])
-        sums = local
-        if reduce_grads is not None:
-            sums = reduce_grads(local.clone())  # the reducer works in place
-        cnt = count.reshape(()).double()
-        istd = invstd.double()
-        al = istd * (w32.double() if w32 is not None else 1.0)
-        be = -al * istd * istd * sums[cout:] / cnt
-        cc = -al * sums[:cout] / cnt - be * mean.double()
-        dW = al[:, None] * Dd + be[:, None] * WG.double() + cc[:, None] * s[None, :]
-        dw = dW.to(weight.dtype).view(cout, cin, 1, 1)
-        if weight.is_contiguous(memory_format=torch.channels_last):
-            dw = dw.contiguous(memory_format=torch.channels_last)
-        # da = [dz | a] @ [al o W ; W^T diag(be) W] + c^T W
-        Bm = torch.cat([(al[:, None] * Wd).t(), Wd.t() @ (be[:, None] * Wd)], 1)
-        ebias = (cc @ Wd).float().contiguous()
+        inputs = [(a2, w3.reshape(cout, cin))]
+        if x is not None:
+            inputs.append((_rows(x), wd.reshape(cout, x.shape[1])))
+        grads = []
+        for i, (inp, W) in enumerate(inputs):
+            WG, asums, mean, invstd, w32, count = rest[6 * i:6 * i + 6]
+            grads.append(_fold_branch_backward(C, dz2, sdz, inp, ctx.geoms[i], n, W, WG, asums, mean, invstd, w32,
+                                               count, meta.bn[i][6], native))
+        wdt3, wdtd = ctx.wdtypes
+        # a: the data gradient of conv3 ([dz | a] @ Bm^T + c^T W), with the producing BN's reductions
         da = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[1]:
+            Bm, eb = grads[0]["Bm"], grads[0]["ebias"]
             if native:
-                da = _FoldDgrad.run(ctx, C, dz2, a2, Bm.to(torch.bfloat16).contiguous(), ebias, n, cin, h, w)
+                da = _FoldDgrad.run(meta, C, dz2, a2, Bm, eb, n, cin, h, w)
             else:
-                da2 = (torch.cat([dz2.double(), a2.double()], 1) @ Bm.t() + ebias.double()).to(a.dtype)
+                da2 = (torch.cat([dz2.double(), a2.double()], 1) @ Bm.double().t() + eb.double()).to(a.dtype)
                 da = _unrows(da2, n, h, w)
-        gres = _unrows(dz2, n, h, w) if (has_res and ctx.needs_input_grad[5]) else None
-        if reduce_grads is not None:
-            dg, db = local[cout:] * istd, local[:cout]
+        dw3 = _wgrad_view(grads[0]["dW"], w3)
+        gg3 = grads[0]["dg"].to(wdt3) if wdt3 is not None and ctx.needs_input_grad[4] else None
+        gb3 = grads[0]["db"].to(wdt3) if wdt3 is not None and ctx.needs_input_grad[5] else None
+        dx = dwd = ggd = gbd = None
+        if x is not None:
+            gd_ = grads[1]
+            dwd = _wgrad_view(gd_["dW"], wd)
+            ggd = gd_["dg"].to(wdtd) if wdtd is not None and ctx.needs_input_grad[8] else None
+            gbd = gd_["db"].to(wdtd) if wdtd is not None and ctx.needs_input_grad[9] else None
+            if ctx.needs_input_grad[6]:
+                dx = _fold_shortcut_dgrad(meta, C, dz2, _rows(x), x.shape, gd_, ctx.geoms[1], native, n)
+        gres = _unrows(dz2, n, h, w) if (ctx.has_res and ctx.needs_input_grad[10]) else None
+        return None, da, None, dw3, gg3, gb3, dx, dwd, ggd, gbd, gres
+
+
+def _cpu_moments(x2: torch.Tensor) -> torch.Tensor:
+    xd = x2.double()
+    return torch.cat([xd.sum(0), (xd * xd).sum(0), xd.new_tensor([float(x2.shape[0])])])
+
+
+def _gram(C, inp, geom, native, n):
+    if not native:
+        xd = _map_rows(inp, geom, n).double()
+        return xd.t() @ xd
+    from .conv1x1 import _tn_xl
+    if geom:
+        return C.gemm_tn(inp, inp, torch.float32, b_map=geom, a_mapped=True)
+    c = inp.shape[1]
+    return C.gemm_tn_xl(inp, inp, torch.float32) if _tn_xl(inp.shape[0], c, c) else C.gemm_tn(inp, inp, torch.float32)
+
+
+def _fold_branch_forward(C, b, n, native):
+    """Gram, folded moments, (cross-rank reduce), finalize of one branch."""
+    W, asums, geom = b["W"], b["asums"], b["geom"]
+    cout, cin = W.shape
+    rm, rv, momentum, eps, nbt, rmom, _ = b["spec"]
+    G = _gram(C, b["inp"], geom, native, n)
+    if native and C.bn_fold_supported(cout, cin):
+        sums, WG = C.bn_fold_fwd(W, G, asums)   # one launch: W G and the row dots
+    else:
+        sums, WG = _fold_stats(W, G, asums[:cin], asums[2 * cin:2 * cin + 1])
+    if rmom is not None:
+        sums = rmom(sums)
+    w32 = b["g"].float() if b["g"] is not None else None
+    b32 = b["b"].float() if b["b"] is not None else None
+    rm = rm if (rm is not None and rm.dtype == torch.float32) else None
+    rv = rv if rm is not None else None
+    scale, shift, mean, invstd = _finalize(sums, w32, b32, rm, rv, momentum, eps, cout, nbt, native)
+    return dict(WG=WG.float(), scale=scale.contiguous(), shift=shift.contiguous(), mean=mean, invstd=invstd,
+                w32=w32, count=sums[-1:])
+
+
+def _fold_branch_backward(C, dz2, sdz, inp, geom, n, W, WG, asums, mean, invstd, w32, count, reduce_grads, native):
+    """dW, dgamma, dbeta, the dgrad operand Bm = [(al o W)^T | W^T diag(be) W] and c^T W of one branch."""
+    cout, cin = W.shape
+    if native:
+        from .conv1x1 import _tn_xl
+        if geom:
+            D = C.gemm_tn(dz2, inp, torch.float32, b_map=geom)
         else:
-            dg, db = sdzx * istd, sdz
-        gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[3] else None
-        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[4] else None
-        return da, None, dw, gw, gb, gres, None, None, None, None, None, None, None, None, None, None
+            D = C.gemm_tn_xl(dz2, inp, torch.float32) if _tn_xl(inp.shape[0], cout, cin) \
+                else C.gemm_tn(dz2, inp, torch.float32)
+    else:
+        D = dz2.double().t() @ _map_rows(inp, geom, n).double()
+    if native and C.bn_fold_supported(cout, cin):
+        # two launches: the row dots, then every coefficient-level output
+        local = C.bn_fold_bwd_sums(D, W, sdz.contiguous(), mean)
+        sums = reduce_grads(local.clone()) if reduce_grads is not None else local
+        dW, dg, db, Bm, eb = C.bn_fold_bwd_coef(sums, local, count, invstd, mean, w32, D, WG, asums, W)
+        return dict(dW=dW, dg=dg, db=db, Bm=Bm, ebias=eb)
+    Wd = W.double()
+    Dd = D.double()
+    sdzx = (Dd * Wd).sum(1) - mean.double() * sdz
+    local = torch.cat([sdz, sdzx])
+    sums = reduce_grads(local.clone()) if reduce_grads is not None else local  # the reducer works in place
+    cnt = count.reshape(()).double()
+    istd = invstd.double()
+    al = istd * (w32.double() if w32 is not None else 1.0)
+    be = -al * istd * istd * sums[cout:] / cnt
+    cc = -al * sums[:cout] / cnt - be * mean.double()
+    dW = al[:, None] * Dd + be[:, None] * WG.double() + cc[:, None] * asums[:cin][None, :]
+    Bm = torch.cat([(al[:, None] * Wd).t(), Wd.t() @ (be[:, None] * Wd)], 1)
+    if native:
+        Bm = Bm.to(torch.bfloat16).contiguous()
+    return dict(dW=dW.to(W.dtype), dg=(local[cout:] * istd).float(), db=local[:cout].float(), Bm=Bm,
+                ebias=(cc @ Wd).float().contiguous())
+
+
+def _wgrad_view(dW, weight):
+    dw = dW.to(weight.dtype).view(weight.shape)
+    if weight.is_contiguous(memory_format=torch.channels_last):
+        dw = dw.contiguous(memory_format=torch.channels_last)
+    return dw
+
+
+def _fold_shortcut_dgrad(meta, C, dz2, x2, xshape, g, geom, native, n):
+    """Gradient of the folded downsample branch w.r.t. the block input x:
+    dx_s = [dz | x_s] @ Bm_d^T + c_d^T W_d on the stride grid.  A strided
+    branch parks it COMPACT in the GradSlot of conv1's data gradient (which
+    adds it in its epilogue, ops/fused.py); stride 1 returns it through
+    autograd (the grad_tap parks it)."""
+    nx, cx, hi, wi = xshape
+    cout = dz2.shape[1]
+    if native:
+        if _xl_fwd(cx, cout):
+            dxs, _ = C.gemm_xl_conv(dz2, g["Bm"], "affine", a2=x2, a2_map=geom, shift=g["ebias"])
+        else:
+            dxs, _ = C.gemm_nt(dz2, g["Bm"], mode="affine", epi_shift=g["ebias"], a2=x2, a2_map=geom)
+    else:
+        xs = _map_rows(x2, geom, n).double()
+        dxs = (torch.cat([dz2.double(), xs], 1) @ g["Bm"].double().t() + g["ebias"].double()).to(x2.dtype)
+    if not geom:
+        return _unrows(dxs, nx, hi, wi)
+    ps = meta.x_park
+    meta.x_park = None
+    if ps is not None and ps.can_park_compact():
+        _STATS["fold_ds_compact"] += 1
+        ps.compact, ps.compact_geom = dxs, list(geom)
+        return None
+    s, ho, wo = geom[0], geom[1], geom[2]
+    full = torch.zeros(nx * hi * wi, cx, device=dxs.device, dtype=dxs.dtype)
+    full.view(nx, hi, wi, cx)[:, ::s, ::s].copy_(dxs.view(nx, ho, wo, cx))
+    return _unrows(full, nx, hi, wi)
 
 
 class _FoldDgrad:
     @staticmethod
-    def run(ctx, C, dz2, a2, Bb, ebias, n, cin, h, w):
+    def run(meta, C, dz2, a2, Bb, ebias, n, cin, h, w):
         """da = [dz | a] @ Bb^T + ebias on the MFMA GEMMs (two-source A operand);
         when ``a`` is a training-mode BN+ReLU output its backward reductions
         ride in the same epilogue (BnBwdSlot)."""
         cout = dz2.shape[1]
-        bs = ctx.a_slot
-        ctx.a_slot = None
+        bs = meta.a_slot
+        meta.a_slot = None
         xl = _xl_fwd(cin, cout)
         if bs is not None and bs.consumers == 1 and bs.x2 is not None:
             _STATS["fold_bnbwd_epilogue"] += 1
@@ -273,8 +395,12 @@ def foldable(conv: nn.Module, bn: nn.Module, a: torch.Tensor) -> bool:
 
 
 def conv1x1_bn_fold(conv: nn.Module, bn: nn.Module, a: torch.Tensor, a_sums: torch.Tensor,
-                    residual: Optional[torch.Tensor] = None, force: bool = False) -> torch.Tensor:
-    """relu(bn(conv(a)) + residual) with the BN folded through the GEMM.
+                    residual: Optional[torch.Tensor] = None, force: bool = False,
+                    downsample: Optional[nn.Module] = None, x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """relu(bn(conv(a)) + residual) with the BN folded through the GEMM, or --
+    with ``downsample`` (Sequential(Conv1x1(stride s), BatchNormAct2d)) and the
+    block input ``x`` instead of ``residual`` -- relu(bn(conv(a)) +
+    bn_d(conv_d(x))) with both BNs folded into one GEMM over [a | x_s].
 
     ``a_sums``: fp64 [2Cin+1] (colsum a, colsum a^2, rows) -- from the producing
     BN apply (``BatchNormAct2d(..., out_moments=True)``).  ``force`` runs the
@@ -282,12 +408,43 @@ def conv1x1_bn_fold(conv: nn.Module, bn: nn.Module, a: torch.Tensor, a_sums: tor
     if not (force or foldable(conv, bn, a)):
         raise RuntimeError("conv1x1_bn_fold: configuration not covered (check foldable())")
     from .batchnorm import BnBwdSlot
-    rmom, rgrad = bn._moment_reducers()
-    a_slot = getattr(a, "_dmp_bnbwd", None)
-    out_slot = BnBwdSlot() if _native.gpu_path(a) else None
-    out = _ConvBNFoldFn.apply(a, a_sums, conv.weight, bn.weight, bn.bias, residual, bn.running_mean,
-                              bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked, rmom, rgrad,
-                              bn.act == "relu", a_slot, out_slot)
-    if out_slot is not None and out_slot.ready():
-        out._dmp_bnbwd = out_slot  # the next 1x1 conv's dgrad epilogue masks dz and reduces sum dz
+    native = _native.gpu_path(a)
+    two = downsample is not None
+    if two and residual is not None:
+        raise ValueError("conv1x1_bn_fold: residual and downsample are exclusive")
+    specs = [_bn_spec(bn)]
+    cd = bd = None
+    if two:
+        cd, bd = downsample[0], downsample[1]
+        specs.append(_bn_spec(bd))
+    meta = _FoldMeta(specs, bn.act == "relu", stride=cd.stride[0] if two else 1,
+                     a_slot=getattr(a, "_dmp_bnbwd", None) if native else None,
+                     out_slot=BnBwdSlot() if native else None,
+                     x_park=getattr(x, "_dmp_gradslot", None) if two else None)
+    out = _ConvBNFoldFn.apply(meta, a, a_sums, conv.weight, bn.weight, bn.bias, x if two else None,
+                              cd.weight if two else None, bd.weight if two else None, bd.bias if two else None,
+                              residual)
+    if meta.out_slot is not None and meta.out_slot.ready():
+        out._dmp_bnbwd = meta.out_slot  # the next 1x1 conv's dgrad epilogue masks dz and reduces sum dz
     return out
+
+
+def foldable_downsample(ds: Optional[nn.Module], x: torch.Tensor, cout: int) -> bool:
+    """A ResNet downsample (Sequential(Conv1x1, BatchNormAct2d without ReLU))
+    that can join the bn3 fold: the same checks as foldable() on its BN, the
+    block input as its conv's native operand, Cin <= 1024 for the coefficient kernels."""
+    from ..utils.checkpointing import in_recompute
+    from .batchnorm import BatchNormAct2d
+    from .conv1x1 import Conv1x1, _native_ok
+    if not (ENABLED and _FOLD_DS and isinstance(ds, nn.Sequential) and len(ds) == 2):
+        return False
+    conv, bn = ds[0], ds[1]
+    return (isinstance(conv, Conv1x1) and isinstance(bn, BatchNormAct2d) and bn.act is None and bn.training
+            and bn.track_running_stats and bn.momentum is not None and bn.running_mean is not None
+            and bn.running_mean.dtype == torch.float32 and torch.is_grad_enabled() and not in_recompute()
+            and _native_ok(x, conv.weight) and conv.weight.shape[0] == cout and x.shape[1] % 64 == 0
+            and x.shape[1] <= 1024)
+
+
+_FOLD_DS = not _native.disabled("bn_fold_ds")
+_STATS.update({"fold_ds": 0, "fold_ds_compact": 0})

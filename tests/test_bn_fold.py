@@ -94,3 +94,51 @@ def test_fold_after_bn_out_moments_chain():
     (o * up).sum().backward()
     a_.backward(a_2.grad)
     torch.testing.assert_close(raw.grad, raw_.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_downsample_fold_matches_stock_composition():
+    """bn3 and the downsample BN folded into one GEMM over [a | x_s]:
+    relu(bn3(conv3(a)) + bn_d(conv_d(x, stride s))) against F.conv2d /
+    F.batch_norm for stride 1 and 2 (fp64, CPU path of the same algebra)."""
+    import torch.nn as nn
+    for seed, stride in ((0, 1), (1, 2)):
+        g = torch.Generator().manual_seed(seed)
+        n, cin, cx, cout, hi = 2, 8, 16, 32, 6
+        ho = (hi - 1) // stride + 1
+        conv3, bn3, a, _, up = _setup(seed, n=n, cin=cin, cout=cout, h=ho, w=ho, residual=False)
+        cd = Conv1x1(cx, cout, stride).double()
+        bd = BatchNormAct2d(cout, act=None).double()
+        with torch.no_grad():
+            cd.weight.copy_(torch.randn(cout, cx, 1, 1, generator=g, dtype=torch.float64) * 0.4)
+            bd.weight.copy_(torch.rand(cout, generator=g, dtype=torch.float64) + 0.5)
+            bd.bias.copy_(torch.randn(cout, generator=g, dtype=torch.float64) * 0.3)
+        bd.running_mean = bd.running_mean.float()
+        bd.running_var = bd.running_var.float()
+        ds = nn.Sequential(cd, bd)
+        x = torch.randn(n, cx, hi, hi, generator=g, dtype=torch.float64).contiguous(
+            memory_format=torch.channels_last).requires_grad_(True)
+        # stock composition on clones
+        a_ = a.detach().clone().requires_grad_(True)
+        x_ = x.detach().clone().requires_grad_(True)
+        w3 = conv3.weight.detach().clone().requires_grad_(True)
+        wd = cd.weight.detach().clone().requires_grad_(True)
+        p = [t.detach().clone().requires_grad_(True) for t in (bn3.weight, bn3.bias, bd.weight, bd.bias)]
+        rm3, rv3 = bn3.running_mean.double().clone(), bn3.running_var.double().clone()
+        rmd, rvd = bd.running_mean.double().clone(), bd.running_var.double().clone()
+        y = F.batch_norm(F.conv2d(a_, w3), rm3, rv3, p[0], p[1], True, 0.1, 1e-5)
+        r = F.batch_norm(F.conv2d(x_, wd, stride=stride), rmd, rvd, p[2], p[3], True, 0.1, 1e-5)
+        o = F.relu(y + r)
+        (o * up).sum().backward()
+        out = conv1x1_bn_fold(conv3, bn3, a, _colsum_moments(a), force=True, downsample=ds, x=x)
+        (out * up).sum().backward()
+        tol = dict(rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(out, o, **tol)
+        torch.testing.assert_close(a.grad, a_.grad, **tol)
+        torch.testing.assert_close(x.grad, x_.grad, **tol)
+        torch.testing.assert_close(conv3.weight.grad, w3.grad, **tol)
+        torch.testing.assert_close(cd.weight.grad, wd.grad, **tol)
+        for mine, ref in zip((bn3.weight, bn3.bias, bd.weight, bd.bias), p):
+            torch.testing.assert_close(mine.grad, ref.grad, **tol)
+        torch.testing.assert_close(bd.running_mean.double(), rmd, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(bd.running_var.double(), rvd, rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(bn3.running_var.double(), rv3, rtol=1e-6, atol=1e-6)

@@ -168,23 +168,34 @@ def test_fold_chain_matches_fp32_reference(cin, hw, n):
     torch.testing.assert_close(bn3f.running_var.double(), 0.9 + 0.1 * var, rtol=2e-2, atol=2e-3)
 
 
-def test_bottleneck_fold_matches_unfused_model():
-    """Two ResNet-50 layer-1 bottlenecks in bf16, fold on vs DMP's unfused
-    native path (bn_fold.ENABLED off), each measured against the same blocks
-    in fp32 stock PyTorch (reference_mode): the fold may not be less accurate."""
+@pytest.mark.parametrize("cin,planes,stride,hw", [(64, 64, 1, 56), (256, 128, 2, 56), (512, 256, 2, 28),
+                                                   (1024, 512, 2, 14), (1024, 512, 2, 4)])
+def test_bottleneck_fold_matches_unfused_model(cin, planes, stride, hw):
+    """A downsampling bottleneck + a plain one in bf16, fold on (bn3 folded; the
+    first block's downsample conv + BN folded into the same GEMM) vs DMP's
+    unfused native path (bn_fold.ENABLED off), each measured against the same
+    blocks in fp32 stock PyTorch (reference_mode): the fold may not be less accurate."""
     import copy
     from distributed_model_parallel_amd.models.resnet import Bottleneck
     from distributed_model_parallel_amd.utils.precision import cast_model
     torch.manual_seed(4)
-    down = torch.nn.Sequential(Conv1x1(64, 256), BatchNormAct2d(256))
-    base = torch.nn.Sequential(Bottleneck(64, 64, 1, down), Bottleneck(256, 64)).to(DEV)
+    cout = planes * 4
+    down = torch.nn.Sequential(Conv1x1(cin, cout, stride), BatchNormAct2d(cout))
+    base = torch.nn.Sequential(Bottleneck(cin, planes, stride, down), Bottleneck(cout, planes)).to(DEV)
     net = cast_model(copy.deepcopy(base).to(memory_format=torch.channels_last))
+    with torch.no_grad():
+        for m in net.modules():
+            if isinstance(m, BatchNormAct2d):
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.normal_(0, 0.2)
     ref = copy.deepcopy(net)
     f32 = copy.deepcopy(net).float()
     for m in (net, ref, f32):
         m.train()
-    x = torch.randn(8, 64, 56, 56, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
-    g = torch.randn(8, 256, 56, 56, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    nb = {56: 8, 28: 16, 14: 32, 4: 128}[hw]
+    x = torch.relu(torch.randn(nb, cin, hw, hw, device=DEV)).bfloat16().contiguous(memory_format=torch.channels_last)
+    ho = hw // stride
+    g = torch.randn(nb, cout, ho, ho, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
 
     def run(model, dtype):
         xi = x.to(dtype).clone().requires_grad_(True)
@@ -192,9 +203,12 @@ def test_bottleneck_fold_matches_unfused_model():
         y.backward(g.to(dtype))
         return [y.float(), xi.grad.float()] + [p.grad.float() for p in model.parameters()]
 
-    before = bn_fold.stats()["fold"]
+    st0 = bn_fold.stats()
     got = run(net, torch.bfloat16)
-    assert bn_fold.stats()["fold"] == before + 2
+    st1 = bn_fold.stats()
+    assert st1["fold"] == st0["fold"] + 1 and st1["fold_ds"] == st0["fold_ds"] + 1
+    if stride != 1:
+        assert st1["fold_ds_compact"] == st0["fold_ds_compact"] + 1  # shortcut grad parked compact
     old = bn_fold.ENABLED
     bn_fold.ENABLED = False
     try:
@@ -207,9 +221,45 @@ def test_bottleneck_fold_matches_unfused_model():
     for n, a, b, r in zip(names, got, unf, gold):
         e_f, e_u = _rel(a, r), _rel(b, r)
         assert e_f < max(1.3 * e_u, 1e-2), f"{n}: fold {e_f:.4f} vs unfused {e_u:.4f} (fp32 reference)"
+    for (n, b1), (_, b2) in zip(net.named_buffers(), ref.named_buffers()):
+        if b1.dtype.is_floating_point:
+            _check(b1, b2, 2e-2, n)
 
 
-@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512)])
+def test_fold_ds_kernels():
+    """Strided colsum, Gram of a strided sample (gemm_tn a_mapped), the
+    scale-concat operand and the two-source GEMMs with a mapped second source."""
+    C = _native.require("fold kernels")
+    torch.manual_seed(6)
+    n, hi, cx, cin, cout, s = 4, 14, 256, 128, 512, 2
+    ho = hi // s
+    geom = [s, ho, ho, hi, hi]
+    x = torch.relu(torch.randn(n, hi, hi, cx, device=DEV)).bfloat16()
+    x2 = x.view(-1, cx)
+    xs = x[:, ::s, ::s].reshape(-1, cx)
+    for mp, rows in ((geom, xs), ([], x2)):
+        m = C.bn_fold_colsum(x2, mp)
+        rd = rows.double()
+        torch.testing.assert_close(m[:cx], rd.sum(0), rtol=1e-5, atol=1e-2)
+        torch.testing.assert_close(m[cx:2 * cx], (rd * rd).sum(0), rtol=1e-5, atol=1e-2)
+        assert m[2 * cx].item() == rows.shape[0]
+    G = C.gemm_tn(x2, x2, torch.float32, b_map=geom, a_mapped=True)
+    _check(G, xs.double().t() @ xs.double(), 1e-5)
+    W3 = (torch.randn(cout, cin, device=DEV) * 0.05).bfloat16()
+    Wd = (torch.randn(cout, cx, device=DEV) * 0.05).bfloat16()
+    s3, t3, sd, td = (torch.randn(cout, device=DEV) for _ in range(4))
+    Bf, sh = C.bn_fold_scale_concat(W3, s3, t3, Wd, sd, td)
+    torch.testing.assert_close(Bf.float(), torch.cat([s3[:, None] * W3.float(), sd[:, None] * Wd.float()], 1).bfloat16().float())
+    torch.testing.assert_close(sh, t3 + td)
+    a = torch.relu(torch.randn(n * ho * ho, cin, device=DEV)).bfloat16()
+    ref = torch.relu(torch.cat([a, xs], 1).float() @ Bf.float().t() + sh)
+    out_nt, _ = C.gemm_nt(a, Bf, mode="affine", epi_shift=sh, relu=True, a2=x2, a2_map=geom)
+    out_xl, _ = C.gemm_xl_conv(a, Bf, "affine", shift=sh, relu=True, a2=x2, a2_map=geom)
+    _check(out_nt, ref, 1e-2)
+    _check(out_xl, ref, 1e-2)
+
+
+@pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512), (2048, 1024), (512, 256)])
 def test_fold_coefficient_kernels_match_fp64(cout, cin):
     """bn_fold_fwd / bn_fold_bwd_sums / bn_fold_bwd_coef against the same
     algebra in fp64 torch ops (the framework's CPU path)."""

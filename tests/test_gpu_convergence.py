@@ -40,6 +40,17 @@ def _task(n_cls, shape, n, seed=0, noise=2.0):
     return x, y
 
 
+WARMUP = 30
+
+
+def _lr(lr, i):
+    """Linear warm-up (the reference recipe's) for both runs: without
+    it a random-init ResNet-50's first ~20 steps are chaotic -- measured, loss
+    excursions to 5-9 whose size differs run to run even for two stock fp32
+    runs -- and windowed comparisons in that phase test the chaos, not the kernels."""
+    return lr * min(1.0, (i + 1) / WARMUP)
+
+
 def _ensure_pg():
     import torch.distributed as dist
     if not dist.is_initialized():
@@ -62,6 +73,8 @@ def _train_native(model, xs, ys, steps, batch, lr):
     opt = FlatSGD(ddp, lr=lr, momentum=0.9, weight_decay=5e-4)
     losses = []
     for i in range(steps):
+        for g in opt.param_groups:
+            g["lr"] = _lr(lr, i)
         sl = slice((i * batch) % xs.shape[0], (i * batch) % xs.shape[0] + batch)
         x = xs[sl].cuda().bfloat16().contiguous(memory_format=torch.channels_last)
         y = ys[sl].cuda()
@@ -79,6 +92,8 @@ def _train_reference(model, xs, ys, steps, batch, lr):
     losses = []
     with _native.reference_mode():
         for i in range(steps):
+            for g in opt.param_groups:
+                g["lr"] = _lr(lr, i)
             sl = slice((i * batch) % xs.shape[0], (i * batch) % xs.shape[0] + batch)
             loss = F.cross_entropy(m(xs[sl].cuda()), ys[sl].cuda())
             opt.zero_grad()
