@@ -25,19 +25,19 @@ namespace {
 
 using bf16 = __bf16;
 constexpr int kFoldThreads = 256;
-constexpr int kFwdRows = 16;     // output channels per forward block
+constexpr int kFwdRows = 8;      // output channels per forward block (2 blocks / CU)
 constexpr int kMaxCin = 1024;
 
 // grid = Cout / kFwdRows.  Thread t owns columns j = t + 256 q (q < NQ) of WG rows
-// k0..k0+15; G streams through LDS in 8-row chunks (double buffered), so the
+// k0..k0+7; G streams through LDS in 4-row chunks (double buffered), so the
 // FMAs read LDS instead of waiting on L2 per row of G.
 template <int NQ>
-__global__ __launch_bounds__(kFoldThreads) void fold_fwd_kernel(const bf16* __restrict__ W,
+__global__ __launch_bounds__(kFoldThreads, 2) void fold_fwd_kernel(const bf16* __restrict__ W,
                                                                 const float* __restrict__ G,
                                                                 const double* __restrict__ asums, int Cout,
                                                                 int Cin, float* __restrict__ WG,
                                                                 double* __restrict__ sums) {
-  constexpr int GR = 8;  // rows of G per LDS chunk
+  constexpr int GR = 4;  // rows of G per LDS chunk
   __shared__ __attribute__((aligned(16))) float wl[kFwdRows][NQ * kFoldThreads];
   __shared__ __attribute__((aligned(16))) float gl[2][GR][NQ * kFoldThreads];
   __shared__ double red[2][kFoldThreads / 64][kFwdRows];
@@ -140,6 +140,9 @@ struct FoldBwdArgs {
   float* ebias;         // [Cin]
   int Cout, Cin;
   int nA;               // role A blocks; the rest are role B
+  int ksplit;           // role B: channel (K) range split over this many blocks per row group
+  float* bpart;         // role B partials [ksplit][Cin][Cin]
+  float* epart;         // role B ebias partials [ksplit][Cin]
 };
 
 // al, be, c per output channel from the (all-reduced) backward sums -- once,
@@ -207,14 +210,16 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
   __shared__ __attribute__((aligned(16))) float wj[kKC][NQ * kFoldThreads];
   __shared__ float wb[kKC][kTR];
   __shared__ float rsum[kFoldThreads / 64][kTR];
-  const int i0 = (blockIdx.x - p.nA) * kTR;
+  const int rb = blockIdx.x - p.nA, rgroups = Cin / kTR;
+  const int i0 = (rb % rgroups) * kTR, ks = rb / rgroups;
+  const int kchunk = Cout / p.ksplit, kbeg = ks * kchunk, kend = kbeg + kchunk;
   const int lane = tid & 63, wave = tid >> 6;
   float acc[kTR][NQ];
 #pragma unroll
   for (int r = 0; r < kTR; ++r)
 #pragma unroll
     for (int q = 0; q < NQ; ++q) acc[r][q] = 0.f;
-  for (int kc = 0; kc < Cout; kc += kKC) {
+  for (int kc = kbeg; kc < kend; kc += kKC) {
     __syncthreads();
     for (int v = tid; v < kKC * Cin / 8; v += kFoldThreads) {  // 16-B bf16 vectors
       const int kk = v / (Cin / 8), c = (v - kk * (Cin / 8)) * 8;
@@ -239,17 +244,18 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
         for (int q = 0; q < NQ; ++q) acc[r][q] = fmaf(wb[kk][r], w[q], acc[r][q]);
     }
   }
-  // Bm rows, and this thread's share of ebias = c^T W[:, i] (channels k = t, t + 256, ..)
+  // this channel range's partial rows of B, and its share of ebias = c^T W[:, i]
+  float* bp = p.bpart + (int64_t)ks * Cin * Cin;
   float part[kTR];
 #pragma unroll
   for (int r = 0; r < kTR; ++r) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int j = tid + q * kFoldThreads;
-      if (j < Cin) p.Bm[(int64_t)(i0 + r) * LDB + Cout + j] = (bf16)acc[r][q];
+      if (j < Cin) bp[(int64_t)(i0 + r) * Cin + j] = acc[r][q];
     }
     float e = 0.f;
-    for (int k = tid; k < Cout; k += kFoldThreads) e = fmaf(c_[k], (float)p.W[(int64_t)k * Cin + i0 + r], e);
+    for (int k = kbeg + tid; k < kend; k += kFoldThreads) e = fmaf(c_[k], (float)p.W[(int64_t)k * Cin + i0 + r], e);
     part[r] = e;
   }
 #pragma unroll
@@ -262,7 +268,29 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kFoldThreads / 64; ++w) t += rsum[w][tid];
-    p.ebias[i0 + tid] = t;
+    p.epart[(int64_t)ks * Cin + i0 + tid] = t;
+  }
+}
+
+// Sum role B's channel-split partials: Bm[:, Cout:] = bf16(sum_s part[s]), ebias = sum_s epart[s].
+__global__ __launch_bounds__(kFoldThreads) void fold_bwd_reduce_kernel(const float* __restrict__ bpart,
+                                                                       const float* __restrict__ epart, int ksplit,
+                                                                       int Cout, int Cin, bf16* __restrict__ Bm,
+                                                                       float* __restrict__ ebias) {
+  const int64_t n = (int64_t)Cin * Cin;
+  for (int64_t v = (int64_t)blockIdx.x * kFoldThreads + threadIdx.x; v < n + Cin;
+       v += (int64_t)gridDim.x * kFoldThreads) {
+    if (v < n) {
+      float t = 0.f;
+      for (int s = 0; s < ksplit; ++s) t += bpart[(int64_t)s * n + v];
+      const int i = (int)(v / Cin), j = (int)(v - (int64_t)i * Cin);
+      Bm[(int64_t)i * (Cout + Cin) + Cout + j] = (bf16)t;
+    } else {
+      const int i = (int)(v - n);
+      float t = 0.f;
+      for (int s = 0; s < ksplit; ++s) t += epart[(int64_t)s * Cin + i];
+      ebias[i] = t;
+    }
   }
 }
 
@@ -430,10 +458,22 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   p.ebias = ebias.data_ptr<float>();
   p.Cout = (int)Cout; p.Cin = (int)Cin;
   p.nA = (int)((Cout / kTK) * (Cin / kTI));
-  const unsigned blocks = (unsigned)(p.nA + Cin / kTR);
+  // split the channel range until role B has >= 256 blocks (one per CU), chunks of kKC channels
+  int ksplit = 1;
+  while ((Cin / kTR) * ksplit < 256 && Cout % (2 * ksplit * kKC) == 0) ksplit *= 2;
+  p.ksplit = ksplit;
+  auto bpart = at::empty({ksplit, Cin, Cin}, W.options().dtype(at::kFloat));
+  auto epart = at::empty({ksplit, Cin}, W.options().dtype(at::kFloat));
+  p.bpart = bpart.data_ptr<float>();
+  p.epart = epart.data_ptr<float>();
+  const unsigned blocks = (unsigned)(p.nA + (Cin / kTR) * ksplit);
   if (Cin <= 256) hipLaunchKernelGGL(fold_bwd_coef_kernel<1>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
   else if (Cin <= 512) hipLaunchKernelGGL(fold_bwd_coef_kernel<2>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
   else hipLaunchKernelGGL(fold_bwd_coef_kernel<4>, dim3(blocks), dim3(kFoldThreads), 0, stream, p);
+  const int64_t nred = Cin * Cin + Cin;
+  hipLaunchKernelGGL(fold_bwd_reduce_kernel, dim3((unsigned)std::min<int64_t>(1024, (nred + kFoldThreads - 1) / kFoldThreads)),
+                     dim3(kFoldThreads), 0, stream, p.bpart, p.epart, ksplit, (int)Cout, (int)Cin,
+                     p.Bm, p.ebias);
   DMP_HIP_CHECK(hipGetLastError());
   return {dW, dgb[0], dgb[1], Bm, ebias};
 }

@@ -393,9 +393,35 @@ void gemm_nt_kernel(const NtArgs p) {
       bsh[j] = (col_ok && !p.bny) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
     }
   }
+  // Phase 1 issues every global operand load of the tile's row passes
+  // (residual / BN input / BN output), phase 2 computes and stores: loads that
+  // sit behind possibly-aliasing stores would keep ~2 per lane in flight
+  // (tools/epi_bench.py; same structure as gemm_xl.hip's conv epilogues).
+  // (batched loads measured: bnbwd l2 1.83 -> 1.44 ms; the affine forward
+  // epilogue no better, so only EPI_BNBWD prefetches)
+  constexpr int NP = BM / RPP;
+  constexpr bool kLR = EPI == EPI_BNBWD;
+  bf16x8 l0[NP], l1[NP], l2[NP];
 #pragma unroll
-  for (int p = 0; p < BM / RPP; ++p) {
-    const int lr = rr0 + p * RPP;
+  for (int i = 0; i < NP; ++i) {
+    const int row = m0 + rr0 + i * RPP;
+    const bool ok = row < M && col_ok;
+    l0[i] = bf16x8{};
+    l1[i] = bf16x8{};
+    l2[i] = bf16x8{};
+    if constexpr (kLR) {
+      int64_t rr = -1;
+      if (ok && R) rr = EPI == EPI_BNBWD ? compact_row(rmap, row) : (int64_t)row;
+      if (rr >= 0) l0[i] = *reinterpret_cast<const bf16x8*>(R + rr * ldr + col);
+    }
+    if constexpr (EPI == EPI_BNBWD) {
+      if (ok && bnx) l1[i] = *reinterpret_cast<const bf16x8*>(bnx + (int64_t)row * ldbx + col);
+      if (ok && bny) l2[i] = *reinterpret_cast<const bf16x8*>(bny + (int64_t)row * ldby + col);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int lr = rr0 + i * RPP;
     const int row = m0 + lr;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
     if (row < M && col_ok) {
@@ -411,20 +437,14 @@ void gemm_nt_kernel(const NtArgs p) {
       if constexpr (EPI == EPI_BNBWD) {
         f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
         if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
-          const int64_t rr = compact_row(rmap, row);
-          if (rr >= 0)
-            g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + rr * ldr + col), f32x8);
+          g += __builtin_convertvector(l0[i], f32x8);
           v = __builtin_convertvector(g, bf16x8);
           g = __builtin_convertvector(v, f32x8);
         }
         // bnx null (the BN input was never materialised, ops/bn_fold.py): mask
         // from y, only sum dz is reduced (sum dz*(x-mean) is formed from dz^T a)
-        f32x8 xv{};
-        if (bnx)
-          xv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bnx + (int64_t)row * ldbx + col), f32x8);
-        f32x8 yv;
-        if (bny)
-          yv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(bny + (int64_t)row * ldby + col), f32x8);
+        const f32x8 xv = __builtin_convertvector(l1[i], f32x8);
+        const f32x8 yv = __builtin_convertvector(l2[i], f32x8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool on = bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);

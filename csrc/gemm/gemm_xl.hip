@@ -581,78 +581,145 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     }
   }
   if (col < N) {
-    // 8 row groups per unrolled batch, predicated rather than exited: the
-    // epilogue operand loads (BN input / residual / aux) of a batch are all in
-    // flight together -- with 1 block/CU the epilogue is memory-latency bound
-#pragma unroll 8
-    for (int pr = 0; pr < XBM / RPP; ++pr) {
-      const int lr = rr0 + pr * RPP;
-      const int row = m0 + lr;
-      if (row >= M) continue;
-      bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
-      if constexpr (EPI == XL_MOMENTS) {
-        const f32x8 f = __builtin_convertvector(v, f32x8);
+    // Epilogue in batches of PB row passes: phase 1 issues every global operand
+    // load of the batch (residual / BN input / BN output / aux), phase 2
+    // computes and stores.  The loads must not sit behind the batch's stores:
+    // C may alias them for all the compiler knows, so a load-compute-store loop
+    // keeps ~2 loads per lane in flight -- measured 2.2-3.1 TB/s on the
+    // short-K conv epilogues at 1 block/CU (tools/epi_bench.py).
+    // Batched for the gradient epilogues (XL_BNBWD 1.72 -> 1.24 ms at l2 shapes);
+    // the forward epilogues measured no better batched (one load per pass) and
+    // keep the row-at-a-time loop below.
+    constexpr bool kBatch = EPI == XL_BNBWD || EPI == XL_ADD;
+    constexpr int NP = kBatch ? XBM / RPP : 0, PB = 8;
+    constexpr bool kL0 = EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BNBWD || EPI == XL_DGELU ||
+                         EPI == XL_BIAS_RES;
+    constexpr bool kL12 = EPI == XL_BNBWD;
+#pragma unroll 1
+    for (int pb = 0; pb < NP; pb += PB) {
+      bf16x8 l0[PB], l1[PB], l2[PB];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { msum[j] += f[j]; msq[j] = fmaf(f[j], f[j], msq[j]); }
-      } else if constexpr (EPI == XL_ADD) {
-        f32x8 f = __builtin_convertvector(v, f32x8);
-        f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
-        v = __builtin_convertvector(f, bf16x8);
-      } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
-        f32x8 f = __builtin_convertvector(v, f32x8);
-        if (p.R) f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
-        if (p.erelu) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+      for (int i = 0; i < PB; ++i) {
+        const int row = m0 + rr0 + (pb + i) * RPP;
+        const bool ok = row < M;
+        l0[i] = bf16x8{};
+        l1[i] = bf16x8{};
+        l2[i] = bf16x8{};
+        if constexpr (kL0) {
+          const bf16* src = nullptr;
+          if constexpr (EPI == XL_DGELU) {
+            src = ok ? p.aux + (int64_t)row * p.ldaux + col : nullptr;
+          } else if constexpr (EPI == XL_BNBWD) {
+            const int64_t rr = (ok && p.R) ? compact_row(p.rmap, row) : -1;
+            src = rr >= 0 ? p.R + rr * p.ldr + col : nullptr;
+          } else {
+            src = (ok && p.R) ? p.R + (int64_t)row * p.ldr + col : nullptr;
+          }
+          if (src) l0[i] = *reinterpret_cast<const bf16x8*>(src);
         }
-        v = __builtin_convertvector(f, bf16x8);
-      } else if constexpr (EPI == XL_BNBWD) {
-        f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
-        if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
-          const int64_t rr = compact_row(p.rmap, row);
-          if (rr >= 0)
-            g += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + rr * p.ldr + col), f32x8);
-          v = __builtin_convertvector(g, bf16x8);
-          g = __builtin_convertvector(v, f32x8);
+        if constexpr (kL12) {
+          if (ok && p.bx) l1[i] = *reinterpret_cast<const bf16x8*>(p.bx + (int64_t)row * p.ldbx + col);
+          if (ok && p.bny) l2[i] = *reinterpret_cast<const bf16x8*>(p.bny + (int64_t)row * p.ldby + col);
         }
-        // bx null: BN input never materialised (ops/bn_fold.py) -- mask from y, sum dz only
-        f32x8 xv{};
-        if (p.bx)
-          xv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bx + (int64_t)row * p.ldbx + col), f32x8);
-        f32x8 yv{};
-        if (p.bny)
-          yv = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.bny + (int64_t)row * p.ldby + col), f32x8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const bool on = p.bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);
-          const float dz = on ? g[j] : 0.f;
-          g[j] = dz;
-          msum[j] += dz;
-          if (p.bx) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
-        }
-        v = __builtin_convertvector(g, bf16x8);
-      } else if constexpr (EPI == XL_BIAS_GELU) {
-        *reinterpret_cast<bf16x8*>(p.aux + (int64_t)row * p.ldaux + col) = v;
-        f32x8 f = __builtin_convertvector(v, f32x8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-        v = __builtin_convertvector(f, bf16x8);
-      } else if constexpr (EPI == XL_DGELU) {
-        f32x8 f = __builtin_convertvector(v, f32x8);
-        const f32x8 x = __builtin_convertvector(
-            *reinterpret_cast<const bf16x8*>(p.aux + (int64_t)row * p.ldaux + col), f32x8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
-        v = __builtin_convertvector(f, bf16x8);
-      } else if constexpr (EPI == XL_BIAS_RES) {
-        f32x8 f = __builtin_convertvector(v, f32x8);
-        const f32x8 r = __builtin_convertvector(
-            *reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
-        f += r;
-        v = __builtin_convertvector(f, bf16x8);
       }
-      const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
-      *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
+#pragma unroll
+      for (int i = 0; i < PB; ++i) {
+        const int lr = rr0 + (pb + i) * RPP;
+        const int row = m0 + lr;
+        if (row >= M) continue;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
+        if constexpr (EPI == XL_MOMENTS) {
+          const f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { msum[j] += f[j]; msq[j] = fmaf(f[j], f[j], msq[j]); }
+        } else if constexpr (EPI == XL_ADD || EPI == XL_BIAS_RES) {
+          f32x8 f = __builtin_convertvector(v, f32x8);
+          f += __builtin_convertvector(l0[i], f32x8);
+          v = __builtin_convertvector(f, bf16x8);
+        } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
+          f32x8 f = __builtin_convertvector(v, f32x8);
+          if (p.R) f += __builtin_convertvector(l0[i], f32x8);
+          if (p.erelu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+          }
+          v = __builtin_convertvector(f, bf16x8);
+        } else if constexpr (EPI == XL_BNBWD) {
+          f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
+          if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
+            g += __builtin_convertvector(l0[i], f32x8);
+            v = __builtin_convertvector(g, bf16x8);
+            g = __builtin_convertvector(v, f32x8);
+          }
+          // bx null: BN input never materialised (ops/bn_fold.py) -- mask from y, sum dz only
+          const f32x8 xv = __builtin_convertvector(l1[i], f32x8);
+          const f32x8 yv = __builtin_convertvector(l2[i], f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const bool on = p.bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);
+            const float dz = on ? g[j] : 0.f;
+            g[j] = dz;
+            msum[j] += dz;
+            if (p.bx) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+          }
+          v = __builtin_convertvector(g, bf16x8);
+        } else if constexpr (EPI == XL_BIAS_GELU) {
+          *reinterpret_cast<bf16x8*>(p.aux + (int64_t)row * p.ldaux + col) = v;
+          f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+          v = __builtin_convertvector(f, bf16x8);
+        } else if constexpr (EPI == XL_DGELU) {
+          f32x8 f = __builtin_convertvector(v, f32x8);
+          const f32x8 x = __builtin_convertvector(l0[i], f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
+          v = __builtin_convertvector(f, bf16x8);
+        }
+        const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
+        *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
+      }
+    }
+    if constexpr (!kBatch) {
+#pragma unroll 8
+      for (int pr = 0; pr < XBM / RPP; ++pr) {
+        const int lr = rr0 + pr * RPP;
+        const int row = m0 + lr;
+        if (row >= M) continue;
+        bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
+        if constexpr (EPI == XL_MOMENTS) {
+          const f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { msum[j] += f[j]; msq[j] = fmaf(f[j], f[j], msq[j]); }
+        } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
+          f32x8 f = __builtin_convertvector(v, f32x8);
+          if (p.R) f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+          if (p.erelu) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+          }
+          v = __builtin_convertvector(f, bf16x8);
+        } else if constexpr (EPI == XL_BIAS_GELU) {
+          *reinterpret_cast<bf16x8*>(p.aux + (int64_t)row * p.ldaux + col) = v;
+          f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
+          v = __builtin_convertvector(f, bf16x8);
+        } else if constexpr (EPI == XL_DGELU) {
+          f32x8 f = __builtin_convertvector(v, f32x8);
+          const f32x8 x = __builtin_convertvector(
+              *reinterpret_cast<const bf16x8*>(p.aux + (int64_t)row * p.ldaux + col), f32x8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
+          v = __builtin_convertvector(f, bf16x8);
+        } else if constexpr (EPI == XL_BIAS_RES) {
+          f32x8 f = __builtin_convertvector(v, f32x8);
+          f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
+          v = __builtin_convertvector(f, bf16x8);
+        }
+        const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
+        *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
+      }
     }
   }
   if constexpr (kMom) {
