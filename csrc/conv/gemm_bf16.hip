@@ -397,26 +397,33 @@ void gemm_nt_kernel(const NtArgs p) {
   // (residual / BN input / BN output), phase 2 computes and stores: loads that
   // sit behind possibly-aliasing stores would keep ~2 per lane in flight
   // (tools/epi_bench.py; same structure as gemm_xl.hip's conv epilogues).
-  // (batched loads measured: bnbwd l2 1.83 -> 1.44 ms; the affine forward
-  // epilogue no better, so only EPI_BNBWD prefetches)
   constexpr int NP = BM / RPP;
-  constexpr bool kLR = EPI == EPI_BNBWD;
+  constexpr bool kLR = EPI == EPI_BNBWD || EPI == EPI_AFFINE;
+  // branch-free operand loads (dummy row 0 of C when an operand is absent; see gemm_xl.hip)
+  const bf16* rbase = R ? R : C;
+  const int64_t rld = R ? ldr : 0;
+  const bf16* xbase = bnx ? bnx : C;
+  const int64_t xld = bnx ? ldbx : 0;
+  const bf16* ybase = bny ? bny : C;
+  const int64_t yld = bny ? ldby : 0;
   bf16x8 l0[NP], l1[NP], l2[NP];
+  unsigned rok = 0;
+  const int colc = col_ok ? col : 0;
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
-    const int row = m0 + rr0 + i * RPP;
-    const bool ok = row < M && col_ok;
-    l0[i] = bf16x8{};
-    l1[i] = bf16x8{};
-    l2[i] = bf16x8{};
+    const int row = min(m0 + rr0 + i * RPP, M - 1);
     if constexpr (kLR) {
-      int64_t rr = -1;
-      if (ok && R) rr = EPI == EPI_BNBWD ? compact_row(rmap, row) : (int64_t)row;
-      if (rr >= 0) l0[i] = *reinterpret_cast<const bf16x8*>(R + rr * ldr + col);
+      int64_t rr = row;
+      if constexpr (EPI == EPI_BNBWD) {
+        rr = R ? compact_row(rmap, row) : -1;
+        rok |= (rr >= 0 ? 1u : 0u) << i;
+        rr = rr >= 0 ? rr : 0;
+      }
+      l0[i] = *reinterpret_cast<const bf16x8*>(rbase + rr * rld + colc);
     }
     if constexpr (EPI == EPI_BNBWD) {
-      if (ok && bnx) l1[i] = *reinterpret_cast<const bf16x8*>(bnx + (int64_t)row * ldbx + col);
-      if (ok && bny) l2[i] = *reinterpret_cast<const bf16x8*>(bny + (int64_t)row * ldby + col);
+      l1[i] = *reinterpret_cast<const bf16x8*>(xbase + (int64_t)row * xld + colc);
+      l2[i] = *reinterpret_cast<const bf16x8*>(ybase + (int64_t)row * yld + colc);
     }
   }
 #pragma unroll
@@ -427,7 +434,7 @@ void gemm_nt_kernel(const NtArgs p) {
     if (row < M && col_ok) {
       if constexpr (EPI == EPI_AFFINE) {  // v = bf16(acc * s + t) (staged)
         f32x8 f = __builtin_convertvector(v, f32x8);
-        if (R) f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(R + (int64_t)row * ldr + col), f32x8);
+        if (R) f += __builtin_convertvector(l0[i], f32x8);
         if (epi_relu) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
@@ -437,7 +444,7 @@ void gemm_nt_kernel(const NtArgs p) {
       if constexpr (EPI == EPI_BNBWD) {
         f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
         if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
-          g += __builtin_convertvector(l0[i], f32x8);
+          if ((rok >> i) & 1u) g += __builtin_convertvector(l0[i], f32x8);
           v = __builtin_convertvector(g, bf16x8);
           g = __builtin_convertvector(v, f32x8);
         }

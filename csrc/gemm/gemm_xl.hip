@@ -587,39 +587,44 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     // C may alias them for all the compiler knows, so a load-compute-store loop
     // keeps ~2 loads per lane in flight -- measured 2.2-3.1 TB/s on the
     // short-K conv epilogues at 1 block/CU (tools/epi_bench.py).
-    // Batched for the gradient epilogues (XL_BNBWD 1.72 -> 1.24 ms at l2 shapes);
-    // the forward epilogues measured no better batched (one load per pass) and
-    // keep the row-at-a-time loop below.
-    constexpr bool kBatch = EPI == XL_BNBWD || EPI == XL_ADD;
+    // Batched for every epilogue with operand loads (XL_BNBWD 1.72 -> 1.24 ms
+    // at l2 shapes); the load-free ones keep the row-at-a-time loop below.
+    constexpr bool kBatch = EPI == XL_BNBWD || EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BIAS_RES ||
+                            EPI == XL_DGELU;
     constexpr int NP = kBatch ? XBM / RPP : 0, PB = 8;
-    constexpr bool kL0 = EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BNBWD || EPI == XL_DGELU ||
-                         EPI == XL_BIAS_RES;
+    constexpr bool kL0 = kBatch;
     constexpr bool kL12 = EPI == XL_BNBWD;
+    // operand bases for branch-free loads: a missing operand reads a valid
+    // dummy row (row 0 of C / of itself), its value is never used -- a
+    // per-load branch would split every load into its own block, and the
+    // compiler then waits for each one before the next (measured: the
+    // forward affine epilogue kept exactly one load per lane in flight)
+    const bf16* rsrc = EPI == XL_DGELU ? p.aux : p.R;  // GELU' reads the pre-activation
+    const bf16* rbase = rsrc ? rsrc : p.C;
+    const int64_t rld = rsrc ? (EPI == XL_DGELU ? p.ldaux : p.ldr) : 0;
+    const bf16* xbase = p.bx ? p.bx : p.C;
+    const int64_t xld = p.bx ? p.ldbx : 0;
+    const bf16* ybase = p.bny ? p.bny : p.C;
+    const int64_t yld = p.bny ? p.ldby : 0;
 #pragma unroll 1
     for (int pb = 0; pb < NP; pb += PB) {
       bf16x8 l0[PB], l1[PB], l2[PB];
+      unsigned rok = 0;  // bit i: row pass i has a residual row (compact map)
 #pragma unroll
       for (int i = 0; i < PB; ++i) {
-        const int row = m0 + rr0 + (pb + i) * RPP;
-        const bool ok = row < M;
-        l0[i] = bf16x8{};
-        l1[i] = bf16x8{};
-        l2[i] = bf16x8{};
+        const int row = min(m0 + rr0 + (pb + i) * RPP, M - 1);
         if constexpr (kL0) {
-          const bf16* src = nullptr;
-          if constexpr (EPI == XL_DGELU) {
-            src = ok ? p.aux + (int64_t)row * p.ldaux + col : nullptr;
-          } else if constexpr (EPI == XL_BNBWD) {
-            const int64_t rr = (ok && p.R) ? compact_row(p.rmap, row) : -1;
-            src = rr >= 0 ? p.R + rr * p.ldr + col : nullptr;
-          } else {
-            src = (ok && p.R) ? p.R + (int64_t)row * p.ldr + col : nullptr;
+          int64_t rr = row;
+          if constexpr (EPI == XL_BNBWD) {
+            rr = p.R ? compact_row(p.rmap, row) : -1;
+            rok |= (rr >= 0 ? 1u : 0u) << i;
+            rr = rr >= 0 ? rr : 0;
           }
-          if (src) l0[i] = *reinterpret_cast<const bf16x8*>(src);
+          l0[i] = *reinterpret_cast<const bf16x8*>(rbase + rr * rld + col);
         }
         if constexpr (kL12) {
-          if (ok && p.bx) l1[i] = *reinterpret_cast<const bf16x8*>(p.bx + (int64_t)row * p.ldbx + col);
-          if (ok && p.bny) l2[i] = *reinterpret_cast<const bf16x8*>(p.bny + (int64_t)row * p.ldby + col);
+          l1[i] = *reinterpret_cast<const bf16x8*>(xbase + (int64_t)row * xld + col);
+          l2[i] = *reinterpret_cast<const bf16x8*>(ybase + (int64_t)row * yld + col);
         }
       }
 #pragma unroll
@@ -647,7 +652,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         } else if constexpr (EPI == XL_BNBWD) {
           f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
           if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
-            g += __builtin_convertvector(l0[i], f32x8);
+            if ((rok >> i) & 1u) g += __builtin_convertvector(l0[i], f32x8);
             v = __builtin_convertvector(g, bf16x8);
             g = __builtin_convertvector(v, f32x8);
           }
@@ -691,30 +696,11 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           const f32x8 f = __builtin_convertvector(v, f32x8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) { msum[j] += f[j]; msq[j] = fmaf(f[j], f[j], msq[j]); }
-        } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
-          f32x8 f = __builtin_convertvector(v, f32x8);
-          if (p.R) f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
-          if (p.erelu) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-          }
-          v = __builtin_convertvector(f, bf16x8);
         } else if constexpr (EPI == XL_BIAS_GELU) {
           *reinterpret_cast<bf16x8*>(p.aux + (int64_t)row * p.ldaux + col) = v;
           f32x8 f = __builtin_convertvector(v, f32x8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-          v = __builtin_convertvector(f, bf16x8);
-        } else if constexpr (EPI == XL_DGELU) {
-          f32x8 f = __builtin_convertvector(v, f32x8);
-          const f32x8 x = __builtin_convertvector(
-              *reinterpret_cast<const bf16x8*>(p.aux + (int64_t)row * p.ldaux + col), f32x8);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
-          v = __builtin_convertvector(f, bf16x8);
-        } else if constexpr (EPI == XL_BIAS_RES) {
-          f32x8 f = __builtin_convertvector(v, f32x8);
-          f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + (int64_t)row * p.ldr + col), f32x8);
           v = __builtin_convertvector(f, bf16x8);
         }
         const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;

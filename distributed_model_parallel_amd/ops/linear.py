@@ -3,7 +3,8 @@
 
 * ``Linear``: drop-in ``nn.Linear``.  Forward is one library GEMM with the bias
   in its epilogue (``addmm`` -> hipBLASLt ``Bias`` kernels).  Backward runs the
-  two library GEMMs (dx, dW) and takes the bias gradient with our column-sum
+  data-gradient library GEMM, the weight gradient on our ping-pong TN kernel
+  (``_wgrad``) and takes the bias gradient with our column-sum
   kernel instead of PyTorch's generic reduce (1.77 ms -> see
   ``profiles/vit_b16_bs128_1gpu_v3.md``).
 * ``linear_gelu``: fc1 + exact GELU; the backward fuses gelu'(h) with fc1's
@@ -14,8 +15,7 @@
   (``csrc/gemm/gemm_xl.hip``, PIPE 7) and its fused epilogues: fc1 writes the
   pre-activation and GELU(h) in one pass (no GELU kernel), fc2 / proj add bias
   and residual in the store (no add kernel), and fc2's data gradient applies
-  gelu'(h) in its epilogue (no GELU-backward pass).  Weight gradients stay on
-  hipBLASLt (split-M shapes our tile grid cannot fill).  Off by default
+  gelu'(h) in its epilogue (no GELU-backward pass).  Off by default
   (``set_xl_linear(True)`` enables it): measured at batch 256 the fused path is
   1.6 % slower per step than hipBLASLt + the separate GELU / add passes --
   fc1+GELU and fc2-dgrad+GELU' break even, fc2 / proj + residual lose
@@ -33,7 +33,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0, "xl": 0}
+_STATS = {"native": 0, "torch": 0, "xl": 0, "tn_wgrad": 0}
 _XL = False
 
 
@@ -53,9 +53,26 @@ def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> b
             and b.dtype == torch.bfloat16 and C.colsum_supported(w.shape[0]))
 
 
+# Weight gradients dW = dy^T x on the ping-pong TN kernel (gemm_tn_xl: 256x256
+# tiles, split over the token rows, one reduce): the ViT shapes have a tiny
+# output (<= 3072 x 768) over a 50k-row reduction, where hipBLASLt's picks run at
+# 340-650 TF/s (profiles/vit_b16_bs256_1gpu_lib_r2.md) -- tools/vit_wgrad_bench.py
+_TN_WGRAD = not _native.disabled("tn_xl")
+_TN_MIN_ROWS = 16384
+
+
+def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    if (_TN_WGRAD and dy2.shape[0] >= _TN_MIN_ROWS and dy2.shape[1] >= 256 and x2.shape[1] >= 256
+            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1
+            and w.dtype == torch.bfloat16):
+        _STATS["tn_wgrad"] += 1
+        return _native.native().gemm_tn_xl(dy2, x2, w.dtype)
+    return dy2.t().mm(x2)
+
+
 def _weight_grads(ctx, dy2, x2, w):
     dx = dy2.mm(w) if ctx.needs_input_grad[0] else None
-    dw = dy2.t().mm(x2) if ctx.needs_input_grad[1] else None
+    dw = _wgrad(dy2, x2, w) if ctx.needs_input_grad[1] else None
     return dx, dw
 
 
@@ -156,7 +173,7 @@ class _LinearResidualFn(torch.autograd.Function):
         C = _native.require("linear_residual backward")
         dy2 = _rows(dy)
         dx = dy2.mm(w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dw = dy2.t().mm(x2) if ctx.needs_input_grad[2] else None
+        dw = _wgrad(dy2, x2, w) if ctx.needs_input_grad[2] else None
         db = C.bias_grad(dy2, w.dtype) if ctx.needs_input_grad[3] else None
         return dx, dy, dw, db
 
@@ -182,11 +199,11 @@ class _MLPResidualFn(torch.autograd.Function):
         C = _native.require("mlp_residual backward")
         dy2 = _rows(dy)
         db2 = C.bias_grad(dy2, w2.dtype)
-        dw2 = dy2.t().mm(a)
+        dw2 = _wgrad(dy2, a, w2)
         # dh = bf16(bf16(dy @ W2) * gelu'(h)): B operand is W2^T [hidden, dim]
         dh = C.gemm_xl(dy2, w2.t().contiguous(), "dgelu", aux=h)
         db1 = C.bias_grad(dh, w1.dtype)
-        dw1 = dh.t().mm(x2)
+        dw1 = _wgrad(dh, x2, w1)
         dx = dh.mm(w1)
         return dx.view(ctx.xshape), dy, dw1, db1, dw2, db2
 

@@ -20,27 +20,38 @@ from distributed_model_parallel_amd.utils.env import init_distributed, destroy_d
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state
 env = init_distributed()
 out = {}
-for parallel in ("ddp", "syncbn"):
+# resnet50: the BN fold (ops/bn_fold.py) routes its folded moments and backward
+# sums through SyncBN's reducers -- RCCL all-reduces when forced
+CASES = [("resnet18", "ddp"), ("resnet18", "syncbn"), ("resnet50", "syncbn")]
+# one throwaway step per model first: MIOpen's find mode may pick another
+# algorithm on a shape's first use (same as the ordering test below), and a
+# random-init ResNet-50 with batch-statistics BN at batch 8 turns that rounding
+# difference into ~0.5 % of the first loss
+for model in sorted({m for m, _ in CASES}):
+    build_train_state(StepConfig(model=model, batch_size=8, image_size=64, parallel="ddp"), env.device).step()
+for model, parallel in CASES:
     for forced in ("0", "1"):
         os.environ["DMP_DDP_SINGLE_RANK_COMM"] = forced
-        cfg = StepConfig(model="resnet18", batch_size=8, image_size=64, parallel=parallel)
+        cfg = StepConfig(model=model, batch_size=8, image_size=64, parallel=parallel)
         st = build_train_state(cfg, env.device)
         before = [p.detach().float().clone() for p in st.model.parameters()]
         loss = st.step()          # one step: the update carries the (averaged) gradient
         torch.cuda.synchronize()
         delta = [p.detach().float() - b for p, b in zip(st.model.parameters(), before)]
-        out[(parallel, forced)] = (loss.item(), delta, getattr(st.wrapped, "comm_backend", None))
-for parallel in ("ddp", "syncbn"):
-    a, b = out[(parallel, "0")], out[(parallel, "1")]
+        out[(model, parallel, forced)] = (loss.item(), delta, getattr(st.wrapped, "comm_backend", None))
+for model, parallel in CASES:
+    a, b = out[(model, parallel, "0")], out[(model, parallel, "1")]
     assert "rccl" in str(b[2]).lower(), b[2]
-    assert abs(a[0] - b[0]) < 1e-3 * max(1.0, abs(a[0])), (parallel, a[0], b[0])
+    # a broken identity all-reduce (doubled or unreduced moments, a read racing
+    # the collective) moves the loss by far more than this
+    assert abs(a[0] - b[0]) < 1e-2 * max(1.0, abs(a[0])), (model, parallel, a[0], b[0])
     # whole-update cosine: MIOpen's weight gradients are not bit-deterministic
     # (profiles/README.md finding 4), so single small tensors (a BN bias) can drift
     # between two identical steps; an identity "average" must still keep the update
     cos = torch.nn.functional.cosine_similarity(torch.cat([x.flatten() for x in a[1]]),
                                                 torch.cat([y.flatten() for y in b[1]]), dim=0).item()
-    assert cos > 0.99, (parallel, cos)
-    print(parallel, "ok", a[0], b[0], b[2], cos)
+    assert cos > 0.99, (model, parallel, cos)
+    print(model, parallel, "ok", a[0], b[0], b[2], cos)
 from distributed_model_parallel_amd.comm.rccl import default_communicator
 comm = default_communicator(env.device)
 t = torch.arange(10, dtype=torch.float64, device=env.device)
@@ -72,7 +83,7 @@ def test_ddp_and_syncbn_rccl_backend_world1():
         print(r.stdout[-3000:])
         print(r.stderr[-6000:])
     assert r.returncode == 0, "subprocess failed (output above)"
-    assert "ddp ok" in r.stdout and "syncbn ok" in r.stdout
+    assert "resnet18 ddp ok" in r.stdout and "resnet18 syncbn ok" in r.stdout and "resnet50 syncbn ok" in r.stdout
     assert "rccl on-current-stream ok" in r.stdout
 
 

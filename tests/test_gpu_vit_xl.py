@@ -79,3 +79,28 @@ def test_small_token_count_uses_library_path():
     y = L.mlp_residual(x, x, fc1, fc2)
     assert L._STATS["xl"] == n0
     torch.testing.assert_close(y.float(), (x + fc2(F.gelu(fc1(x)))).float(), atol=0.05, rtol=2e-2)
+
+
+@pytest.mark.parametrize("xl", [False, True])
+def test_weight_grads_on_tn_kernel_match_fp32(monkeypatch, xl):
+    """Token counts past _TN_MIN_ROWS: every weight gradient of the MLP runs on
+    gemm_tn_xl (split over tokens), on the library forward (linear_gelu +
+    Linear) and on the fused-epilogue forward alike."""
+    monkeypatch.setattr(L, "_XL", xl)
+    torch.manual_seed(2)
+    T, D, H = 20000, 768, 3072
+    fc1, fc2 = L.Linear(D, H).to(DEV).bfloat16(), L.Linear(H, D).to(DEV).bfloat16()
+    x = torch.randn(T, D, device=DEV).bfloat16()
+    res = torch.randn(T, D, device=DEV).bfloat16()
+    xb, rb = _leaves(x, res)
+    n0 = L._STATS["tn_wgrad"]
+    y = L.mlp_residual(xb, rb, fc1, fc2)
+    g = torch.randn(T, D, device=DEV)
+    y.backward(g.bfloat16())
+    assert L._STATS["tn_wgrad"] == n0 + 2, "weight gradients did not run on gemm_tn_xl"
+    xf, rf, w1, b1, w2, b2 = _leaves(x.float(), res.float(), fc1.weight.float(), fc1.bias.float(),
+                                     fc2.weight.float(), fc2.bias.float())
+    _ref_mlp(xf, rf, w1, b1, w2, b2).backward(g)
+    for got, ref in ((fc1.weight.grad, w1.grad), (fc2.weight.grad, w2.grad)):
+        err = ((got.float() - ref).norm() / ref.norm()).item()
+        assert err < 2e-2, err
