@@ -77,7 +77,8 @@ FEATURES = {
     "halo3": "halo-tiled 3x3 convs of layers 1-2 (conv3x3_halo.hip, conv3x3_c128.hip)",
     "xl_conv3": "256x256 ping-pong implicit GEMM for layer-3/4 3x3 convs (gemm_xl.hip conv_xl)",
     "xl_conv": "256x256 ping-pong GEMM for wide 1x1 convs (gemm_xl.hip)",
-    "tn_xl": "ping-pong TN weight gradients of wide 1x1 convs",
+    "tn_xl": "ping-pong TN weight gradients of wide 1x1 convs and of the ViT linears",
+    "xl_linear": "ViT MLP / attention projection on the fused-epilogue ping-pong GEMM -> hipBLASLt + GELU / add passes",
     "compact_shortcut": "stride-2 shortcut gradient kept compact (no zero-filled tensor)",
     "fuse_bn_bwd": "BN backward reductions in the consumer's data-gradient epilogue (BnBwdSlot)",
     "fuse_stem_pool": "stem BN apply + ReLU inside the max-pool (forward and backward)",

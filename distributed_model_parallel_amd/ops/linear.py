@@ -15,11 +15,12 @@
   (``csrc/gemm/gemm_xl.hip``, PIPE 7) and its fused epilogues: fc1 writes the
   pre-activation and GELU(h) in one pass (no GELU kernel), fc2 / proj add bias
   and residual in the store (no add kernel), and fc2's data gradient applies
-  gelu'(h) in its epilogue (no GELU-backward pass).  Off by default
-  (``set_xl_linear(True)`` enables it): measured at batch 256 the fused path is
-  1.6 % slower per step than hipBLASLt + the separate GELU / add passes --
-  fc1+GELU and fc2-dgrad+GELU' break even, fc2 / proj + residual lose
-  (profiles/vit_xl_epilogues_r2.md).
+  gelu'(h) in its epilogue (no GELU-backward pass).  On by default since the
+  weight gradients moved to the TN kernel: ViT-B/16 batch 256, 43.6 vs 43.7 ms
+  per step in round 3 (tools/vit_step_ab.py, profiles/raw_r3/vit_step_ab.log;
+  round 2 measured it 1.6 % slower with the library weight gradients,
+  profiles/vit_xl_epilogues_r2.md).  ``DMP_DISABLE=xl_linear`` or
+  ``set_xl_linear(False)`` selects hipBLASLt + the separate passes.
 
 CPU tensors, non-bf16 dtypes and widths that are not a multiple of 256 use
 the plain PyTorch ops (same math)."""
@@ -34,7 +35,7 @@ import torch.nn.functional as F
 from .. import _native
 
 _STATS = {"native": 0, "torch": 0, "xl": 0, "tn_wgrad": 0}
-_XL = False
+_XL = not _native.disabled("xl_linear")
 
 
 def set_xl_linear(on: bool) -> None:

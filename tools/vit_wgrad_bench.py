@@ -39,6 +39,12 @@ def main():
         xl = timeit(lambda: C.gemm_tn_xl(dy, x, torch.bfloat16))
         tn = timeit(lambda: C.gemm_tn(dy, x, torch.bfloat16))
         ref = (dy.t() @ x).float()
+        sweep = []
+        for r in (2, 3, 4):  # split count: r rounds of 256 blocks (0 = the default rule)
+            C.set_tn_xl_rounds(r)
+            sweep.append(f"r{r} {timeit(lambda: C.gemm_tn_xl(dy, x, torch.bfloat16)):.3f}")
+        C.set_tn_xl_rounds(0)
+        print("   tn_xl rounds sweep:", ", ".join(sweep))
         err = ((C.gemm_tn_xl(dy, x, torch.bfloat16).float() - ref).abs().max() / ref.abs().max()).item()
         fl = 2.0 * T * fin * fout
         print(f"| {name} | {fin} | {fout} | {lib:.3f} | {xl:.3f} | {tn:.3f} | {fl / lib / 1e9:.0f} | "
