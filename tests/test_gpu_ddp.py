@@ -48,10 +48,13 @@ for model, parallel in CASES:
     # whole-update cosine: MIOpen's weight gradients are not bit-deterministic
     # (profiles/README.md finding 4), so single small tensors (a BN bias) can drift
     # between two identical steps; an identity "average" must still keep the update
-    cos = torch.nn.functional.cosine_similarity(torch.cat([x.flatten() for x in a[1]]),
-                                                torch.cat([y.flatten() for y in b[1]]), dim=0).item()
-    assert cos > 0.99, (model, parallel, cos)
-    print(model, parallel, "ok", a[0], b[0], b[2], cos)
+    # (0.988-0.991 measured between two identical resnet18 steps at batch 8);
+    # the norm ratio catches a scaled "average" (sum instead of mean: 2x at ws 2)
+    ua, ub = torch.cat([x.flatten() for x in a[1]]), torch.cat([y.flatten() for y in b[1]])
+    cos = torch.nn.functional.cosine_similarity(ua, ub, dim=0).item()
+    nrm = (ub.norm() / ua.norm()).item()
+    assert cos > 0.97 and abs(nrm - 1) < 0.05, (model, parallel, cos, nrm)
+    print(model, parallel, "ok", a[0], b[0], b[2], cos, nrm)
 from distributed_model_parallel_amd.comm.rccl import default_communicator
 comm = default_communicator(env.device)
 t = torch.arange(10, dtype=torch.float64, device=env.device)
