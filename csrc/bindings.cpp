@@ -128,6 +128,7 @@ at::Tensor stem_halo_wgrad(const at::Tensor& dy, const at::Tensor& s, int64_t ho
 bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
+void set_tn_xl_ablation(int a);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
 std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
@@ -153,6 +154,7 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
                                          const at::Tensor& invstd, const at::Tensor& mean,
                                          const c10::optional<at::Tensor>& gamma, const at::Tensor& D,
                                          const at::Tensor& WG, const at::Tensor& s, const at::Tensor& W);
+std::vector<at::Tensor> bn_fold_relu_mask(const at::Tensor& dy, const at::Tensor& y);
 at::Tensor bn_fold_colsum(const at::Tensor& x, const std::vector<int64_t>& map);
 std::vector<at::Tensor> bn_fold_scale_concat(const at::Tensor& W3, const at::Tensor& s3, const at::Tensor& t3,
                                              const at::Tensor& Wd, const at::Tensor& sd, const at::Tensor& td);
@@ -302,6 +304,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
         "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
+  m.def("set_tn_xl_ablation", &dmp::set_tn_xl_ablation, py::arg("mode"));
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M");
   m.def("conv_wgrad_xl", &dmp::conv_wgrad_xl, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
@@ -328,6 +331,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("invstd"), py::arg("mean"), py::arg("gamma"), py::arg("D"), py::arg("WG"), py::arg("s"),
         py::arg("W"), "(dW, dgamma, dbeta, Bm = [(al o W)^T | W^T diag(be) W], ebias = c^T W)");
 
+  m.def("bn_fold_relu_mask", &dmp::bn_fold_relu_mask, py::arg("dy"), py::arg("y"));
   m.def("bn_fold_colsum", &dmp::bn_fold_colsum, py::arg("x"), py::arg("map") = std::vector<int64_t>{},
         "fp64 [2C+1] (colsum, colsum of squares, rows) of x's rows sampled through a strided map");
   m.def("bn_fold_scale_concat", &dmp::bn_fold_scale_concat, py::arg("W3"), py::arg("s3"), py::arg("t3"),

@@ -299,10 +299,15 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_reduce_kernel(const flo
 // the colsum a folded downsample's BN statistics need, per-block partials
 // [2][blocks][C] reduced deterministically by bn_reduce_partials_launch.
 // grid = (row blocks); 256 threads = (256 / cv) row lanes x cv channel vectors.
+// MASK: x is dL/dout of a ReLU output y; the pass writes dz = [y > 0] dL/dout
+// to out and reduces dz (the fold's backward when no consumer epilogue did it).
+template <bool MASK>
 __global__ __launch_bounds__(kFoldThreads) void fold_colsum_kernel(const bf16* __restrict__ x, int C, int64_t M,
                                                                    int s, int ho, int wo, int hi, int wi,
                                                                    int64_t rows_per_block, float* __restrict__ part,
-                                                                   double* __restrict__ zsums) {
+                                                                   double* __restrict__ zsums,
+                                                                   const bf16* __restrict__ y = nullptr,
+                                                                   bf16* __restrict__ out = nullptr) {
   zero_moments(zsums, 2 * C);
   __shared__ float ls[kFoldThreads * 8], lq[kFoldThreads * 8];
   const int cv = C / 8, rpi = kFoldThreads / cv;
@@ -320,7 +325,13 @@ __global__ __launch_bounds__(kFoldThreads) void fold_colsum_kernel(const bf16* _
         const int r = (int)(m - n * hw), oh = r / wo, ow = r - oh * wo;
         pm = (n * hi + (int64_t)oh * s) * wi + (int64_t)ow * s;
       }
-      const f32x8 f = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(x + pm * C + lc * 8), f32x8);
+      f32x8 f = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(x + pm * C + lc * 8), f32x8);
+      if constexpr (MASK) {
+        const bf16x8 yv = *reinterpret_cast<const bf16x8*>(y + pm * C + lc * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = (float)yv[e] > 0.f ? f[e] : 0.f;
+        *reinterpret_cast<bf16x8*>(out + pm * C + lc * 8) = __builtin_convertvector(f, bf16x8);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) { su[e] += f[e]; sq[e] = fmaf(f[e], f[e], sq[e]); }
     }
@@ -501,12 +512,41 @@ at::Tensor bn_fold_colsum(const at::Tensor& x, const std::vector<int64_t>& map) 
   blocks = (M + rpb - 1) / rpb;
   auto part = at::empty({2, blocks, C}, x.options().dtype(at::kFloat));
   hipStream_t stream = at::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(fold_colsum_kernel, dim3((unsigned)blocks), dim3(kFoldThreads), 0, stream,
+  hipLaunchKernelGGL(fold_colsum_kernel<false>, dim3((unsigned)blocks), dim3(kFoldThreads), 0, stream,
                      reinterpret_cast<const bf16*>(x.data_ptr()), (int)C, M, s, ho, wo, hi, wi, rpb,
-                     part.data_ptr<float>(), moments_zero_target(sums.data_ptr<double>(), (int)blocks));
+                     part.data_ptr<float>(), moments_zero_target(sums.data_ptr<double>(), (int)blocks),
+                     nullptr, nullptr);
   bn_reduce_partials_launch(part.data_ptr<float>(), (int)blocks, (int)C, sums.data_ptr<double>(), (double)M, stream);
   DMP_HIP_CHECK(hipGetLastError());
   return sums;
+}
+
+// (dz = [y > 0] dy bf16 [rows, C], fp64 [2C+1] = (sum dz, sum dz^2, rows)):
+// the ReLU mask and dz column sum of the folded bn3's backward in one pass
+// (ops/bn_fold.py, when no consumer data-gradient epilogue applied them).
+std::vector<at::Tensor> bn_fold_relu_mask(const at::Tensor& dy, const at::Tensor& y) {
+  for (const at::Tensor* t : {&dy, &y})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16 && t->dim() == 2 && t->is_contiguous(),
+                "dy / y must be contiguous bf16 [rows, C] GPU tensors");
+  TORCH_CHECK(dy.sizes() == y.sizes(), "dy / y shape mismatch");
+  const int64_t C = dy.size(1), M = dy.size(0);
+  TORCH_CHECK(C % 8 == 0 && C <= 8 * kFoldThreads, "C % 8 == 0, C <= 2048");
+  auto dz = at::empty_like(dy);
+  auto sums = at::empty({2 * C + 1}, dy.options().dtype(at::kDouble));
+  if (M == 0) return {dz, sums.zero_()};
+  const int rpi = kFoldThreads / (int)(C / 8);
+  int64_t blocks = std::min<int64_t>(1024, (M + (int64_t)rpi * 16 - 1) / ((int64_t)rpi * 16));
+  const int64_t rpb = (M + blocks - 1) / blocks;
+  blocks = (M + rpb - 1) / rpb;
+  auto part = at::empty({2, blocks, C}, dy.options().dtype(at::kFloat));
+  hipStream_t stream = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(fold_colsum_kernel<true>, dim3((unsigned)blocks), dim3(kFoldThreads), 0, stream,
+                     reinterpret_cast<const bf16*>(dy.data_ptr()), (int)C, M, 1, 1, 1, 1, 1, rpb,
+                     part.data_ptr<float>(), moments_zero_target(sums.data_ptr<double>(), (int)blocks),
+                     reinterpret_cast<const bf16*>(y.data_ptr()), reinterpret_cast<bf16*>(dz.data_ptr()));
+  bn_reduce_partials_launch(part.data_ptr<float>(), (int)blocks, (int)C, sums.data_ptr<double>(), (double)M, stream);
+  DMP_HIP_CHECK(hipGetLastError());
+  return {dz, sums};
 }
 
 // (Bf bf16 [Cout, C3 + Cd] = [s3 o W3 | sd o Wd], shift fp32 [Cout] = t3 + td).

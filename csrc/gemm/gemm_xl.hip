@@ -977,6 +977,10 @@ __device__ __forceinline__ int tn64_off(int row, int col) {
   return row * 64 + ((((byte >> 5) ^ tn64_swz(row))) << 5) + (byte & 31);
 }
 
+// ABL (timing-only ablations, tools/tn_vit_pmc.py --ablate): 1 = no global
+// staging after the prologue (the LDS tiles go stale: schedule + LDS + MFMA
+// bound), 2 = staging kept but no barriers inside the main loop.
+template <int ABL>
 __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs p) {
   constexpr int PLANE = 64 * 64, OPER = 8 * PLANE;  // bytes
   __shared__ __attribute__((aligned(16))) char smem[4 * OPER];
@@ -1017,6 +1021,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
   }
   auto stage_unit = [&](auto u, int kt) {
     constexpr int U = decltype(u)::value;
+    if (ABL == 1 && kt > 1) return;
     const int buf = kt & 1;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1079,7 +1084,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
   };
   auto quad = [&](auto mqc, auto nqc) {
     constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
-    barrier();
+    if (ABL != 2) barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -1093,7 +1098,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    barrier();
+    if (ABL != 2) barrier();
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -1112,7 +1117,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
       vmcnt<0>();
     }
     barrier();
-    if (wr == 1) barrier();
+    if (ABL != 2 && wr == 1) barrier();
     for (int kt = 0; kt < KT; ++kt) {
       const int buf = kt & 1;
       const bool n1 = kt + 1 < KT, n2 = kt + 2 < KT;
@@ -1130,7 +1135,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
       if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
       quad(I1{}, I0{});
     }
-    if (wr == 0) barrier();
+    if (ABL != 2 && wr == 0) barrier();
   }
   float* out = p.part + (int64_t)split * N * K;
 #pragma unroll
@@ -1549,6 +1554,7 @@ void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out
 
 namespace {
 
+int g_tn_xl_ablate = 0;  // timing-only ablations of the TN main loop (see gemm_tn_pp_kernel)
 int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
 
 at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype) {
@@ -1568,7 +1574,12 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
   a.part = part.data_ptr<float>();
   hipStream_t s = at::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(gemm_tn_pp_kernel, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  if (g_tn_xl_ablate == 1)
+    hipLaunchKernelGGL(gemm_tn_pp_kernel<1>, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  else if (g_tn_xl_ablate == 2)
+    hipLaunchKernelGGL(gemm_tn_pp_kernel<2>, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL(gemm_tn_pp_kernel<0>, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   DMP_HIP_CHECK(hipGetLastError());
   split_reduce_launch(a.part, splits, (int64_t)N * K, out, s);
   return out;
@@ -1615,6 +1626,10 @@ at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, 
 }
 
 void set_tn_xl_rounds(int r) { g_tn_xl_rounds = r; }
+void set_tn_xl_ablation(int a) {
+  TORCH_CHECK(a >= 0 && a <= 2, "tn ablation must be 0 (off), 1 (no staging) or 2 (no barriers)");
+  g_tn_xl_ablate = a;
+}
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
   TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");

@@ -204,6 +204,15 @@ class _ConvBNFoldFn(torch.autograd.Function):
             # the consumer's data-gradient epilogue applied the ReLU mask and reduced sum dz
             _STATS["fold_fused_bwd"] += 1
             sdz = fused[:cout]
+        elif native and dz2.shape[1] <= 2048:
+            # one pass: mask, store dz and reduce sum dz (the network's last block,
+            # whose gradient comes from the pooling: 1.3 ms of torch where / cast /
+            # fp64 sum at batch 2048 before, profiles/README.md finding 41)
+            if meta.relu:
+                dz2, s = C.bn_fold_relu_mask(dz2.contiguous(), out2.contiguous())
+            else:
+                s = C.bn_fold_colsum(dz2.contiguous())
+            sdz = s[:cout]
         else:
             if meta.relu:
                 dz2 = torch.where(out2 > 0, dz2, torch.zeros((), dtype=dz2.dtype, device=dz2.device))

@@ -296,3 +296,19 @@ def test_fold_coefficient_kernels_match_fp64(cout, cin):
     _check(Bm[:, :cout], (al[:, None] * Wd).t(), 1e-2)
     _check(Bm[:, cout:], Wd.t() @ (be[:, None] * Wd), 1e-2)
     _check(eb, cc @ Wd, 1e-5)
+
+
+@pytest.mark.parametrize("rows,c", [(100352, 2048), (1000, 256), (37, 64)])
+def test_relu_mask_colsum_kernel(rows, c):
+    """bn_fold_relu_mask: dz = [y > 0] dy and its fp64 column sums in one pass."""
+    C = _native.require("test")
+    torch.manual_seed(0)
+    dy = torch.randn(rows, c, device="cuda").bfloat16()
+    y = torch.relu(torch.randn(rows, c, device="cuda")).bfloat16()
+    dz, s = C.bn_fold_relu_mask(dy, y)
+    ref = torch.where(y > 0, dy, torch.zeros((), dtype=dy.dtype, device=dy.device))
+    assert torch.equal(dz, ref)
+    rd = ref.double()
+    torch.testing.assert_close(s[:c], rd.sum(0), atol=1e-3 * rows ** 0.5, rtol=1e-5)
+    torch.testing.assert_close(s[c:2 * c], (rd * rd).sum(0), atol=1e-3 * rows ** 0.5, rtol=1e-5)
+    assert s[2 * c].item() == rows

@@ -122,6 +122,14 @@ def _mean(v):
     return sum(v) / len(v)
 
 
+def _steps_to(v, thr, k=5):
+    """First step whose k-step mean is below thr (None if never)."""
+    for i in range(len(v) - k + 1):
+        if _mean(v[i:i + k]) < thr:
+            return i
+    return None
+
+
 @pytest.mark.parametrize("arch,shape,ncls,steps,batch,lr,noise", [
     ("mobilenetv2", (3, 32, 32), 10, 240, 128, 0.05, 6.0),
     # random-init ResNet-50 without warm-up diverges at lr 0.05 (stock and native alike)
@@ -155,14 +163,17 @@ def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, l
     assert _mean(l_nat[-k:]) < 0.5 * _mean(l_nat[:k]), (l_nat[:5], l_nat[-5:])
     assert acc_ref > 80.0 and acc_nat > 80.0, (acc_nat, acc_ref)
     assert acc_nat > acc_ref - 10.0, (acc_nat, acc_ref)
-    # the native curve never lags the stock one: windowed means at most 25 % (+0.05
-    # absolute) above it.  One-sided: in the steep part of the curve a run that is
-    # a few steps ahead differs by 2x in a window (measured: ResNet-50 native 0.49
-    # vs stock 1.11 at steps 25-49, same plateau after), and being ahead is not a
-    # native-path bug -- a lost/scaled gradient or a broken kernel makes it lag.
-    for w0 in range(0, steps - k + 1, k):
-        a, b = _mean(l_nat[w0:w0 + k]), _mean(l_ref[w0:w0 + k])
-        assert a <= 1.25 * b + 0.05, (w0, a, b)
+    # the native curve never lags the stock one: the step at which the 5-step
+    # mean first falls below 50 / 25 / 10 % of the initial loss is at most 25 %
+    # (+8 steps) later than stock's.  Steps-to-threshold, not windowed means: in
+    # the steep part of the curve a run that is a few steps ahead differs by
+    # 1.5-2x in a window (measured, full-suite runs: MobileNetV2 steps 40-79
+    # native 0.49 vs stock 0.34 one run, 0.49 vs 0.48 another), while a
+    # lost / scaled gradient or a broken kernel needs ~2x the steps.
+    l0 = _mean(l_ref[:5])
+    for frac in (0.5, 0.25, 0.1):
+        sn, sr = _steps_to(l_nat, frac * l0), _steps_to(l_ref, frac * l0)
+        assert sr is not None and sn is not None and sn <= 1.25 * sr + 8, (frac, sn, sr)
     # and both end on the same plateau
     a, b = _mean(l_nat[-k:]), _mean(l_ref[-k:])
     assert abs(a - b) <= 0.25 * max(a, b) + 0.05, (a, b)
