@@ -62,7 +62,7 @@ def test_pipeline_world1_on_gpu_matches_sequential(schedule, micro):
     for xs, ys in zip(torch.chunk(x.cuda(), micro), torch.chunk(y.cuda(), micro)):
         loss = F.cross_entropy(pipe.module(xs).float(), ys) / micro
         loss.backward()
-        total += float(loss)
+        total += float(loss.detach())
     assert abs(r.loss - total) < 1e-3 * max(1.0, abs(total))
     # MIOpen's fp32 weight gradients accumulate in a run-dependent order, and the
     # bias gradients of BNs feeding another BN cancel to ~0 (two identical stock
