@@ -106,6 +106,8 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out);
 void set_gemm_xl_bn(int bn, int pipe, int group_m);
+int get_gemm_xl_pipe();
+int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
                                 int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
                                 const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& bn_x,
@@ -129,6 +131,7 @@ bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
 void set_tn_xl_ablation(int a);
+void set_tn_xl_ring(int r);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
 std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
@@ -305,6 +308,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
   m.def("set_tn_xl_ablation", &dmp::set_tn_xl_ablation, py::arg("mode"));
+  m.def("set_tn_xl_ring", &dmp::set_tn_xl_ring, py::arg("ring"),
+        "gemm_tn_xl main loop: 0 = two tile buffers, 1 = the 10-slot LDS unit ring");
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M");
   m.def("conv_wgrad_xl", &dmp::conv_wgrad_xl, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
@@ -318,7 +323,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("shift") = py::none(), py::arg("relu") = false, py::arg("a2_map") = std::vector<int64_t>{},
         "wide 1x1-conv GEMM with conv epilogues: moments | add | bnbwd | affine (scale, shift, residual, relu); "
         "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
-  m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = 7, py::arg("group_m") = 0,
+  m.def("get_gemm_xl_pipe", &dmp::get_gemm_xl_pipe);
+  m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
+  m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
 
   // ---- BN folded through an expanding 1x1 conv (ops/bn_fold.py) ----

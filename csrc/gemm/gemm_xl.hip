@@ -119,6 +119,20 @@ template <int N>
 __device__ __forceinline__ void vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n in {0, 2, .., MAX} (the
+// immediate must be a constant): a chain of scalar compares, steady state first
+template <int MAX>
+__device__ __forceinline__ void vmcnt_upto(int n) {
+  if constexpr (MAX <= 0) {
+    vmcnt<0>();
+  } else {
+    if (n >= MAX) vmcnt<MAX>();
+    else vmcnt_upto<MAX - 2>(n);
+  }
+}
+
+// LDS ring depth of the PIPE 8 main loops, in 16 KB units (160 KB max)
+constexpr int XL_RING_SLOTS = 10;
 __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   constexpr int MI = WTM / 16, NI = WTN / 16;       // 8 x (4 | 2) accumulators
   constexpr int RA = XBM * 64, RB = BN * 64;        // bytes of one k32 region
   constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;  // glds per wave per region
-  constexpr int STAGE_LDS = 4 * RA + 4 * RB;
+  constexpr int STAGE_LDS = PIPE == 8 ? XL_RING_SLOTS * 16384 : 4 * RA + 4 * RB;
   constexpr int CT_STRIDE = BN + 8;
   constexpr int EPI_LDS = XBM * CT_STRIDE * 2;
   constexpr int LDS = STAGE_LDS > EPI_LDS ? STAGE_LDS : EPI_LDS;
@@ -452,6 +466,169 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     read_b(0, buf);
     if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
     quad(I1{}, I0{});
+  }
+  if (wr == 0) barrier();  // equal barrier counts before the epilogue
+  barrier();
+  } else if constexpr (PIPE == 8) {
+  // ---- PIPE 8: the ping-pong quadrant schedule of PIPE 7 on a ring of NS
+  // 16 KB unit slots instead of two fixed tile buffers (finding 42: PIPE 7
+  // keeps only two units = 32 KB in flight per CU, ~650-700 TF/s; the same
+  // schedule without the operand stream runs 1.2 PF/s).  Units are numbered
+  // in issue order i = 4 t + k, k = 0..3 <-> U0 (A m half 0), U2 (B n half 1),
+  // U3 (A m half 1), U1 (B n half 0) of K tile t; with the quadrant order
+  // (0,0) (0,1) (1,1) (1,0) unit i is last read in phase i (phase g = 4 t + r).
+  // Unit i lives in slot i % NS and is issued in phase i - D, D = NS - 1, so
+  // it overwrites unit i - NS, last read in phase i - NS = (issue phase) - 1
+  // (WAR: >= 2 barriers, as PIPE 7).  Phase g may read up to unit g + 4 (U1 of
+  // the next tile), so the phase-g wait retires every unit <= g + 4 and leaves
+  // V = D - 4 = NS - 5 units in flight: 80 KB at NS = 10 (vmcnt 10).
+  // Slot layout: [k32 half 2][8 blocks][16 rows x 64 B] (the 1 KB block is
+  // PIPE 7's 16-row swizzled image); block bj holds rows (bj >> 2) * 128 +
+  // mq * 64 + (bj & 3) * 16 of an A unit, cols (bj >> 1) * 64 + nq * 32 +
+  // (bj & 1) * 16 of a B unit -- the same rows PIPE 7's staging lanes fetch.
+  static_assert(BN == 256, "ring schedule is written for 256 x 256 tiles");
+  constexpr int NS = XL_RING_SLOTS, D = NS - 1, V = NS - 5, SLOT = 16384;
+  static_assert(NS * SLOT <= 160 * 1024, "ring exceeds LDS");
+  const int pks = wave >> 2;
+  const int bj0 = (2 * wave) & 7;  // block of copy q is bj0 + q
+  const bf16* pa[2][2];
+  const bf16* pa2[2][2];
+  const bf16* pb[2][2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = bj0 + q;
+      const int ra = (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow;
+      const int rb = (j >> 1) * 64 + v * 32 + (j & 1) * 16 + srow;
+      pa[v][q] = A + (int64_t)min(m0 + ra, M - 1) * lda + schunk * 8 + pks * 32;
+      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ra, M - 1)) * p.lda2 + schunk * 8 + pks * 32 - p.K1
+                       : nullptr;
+      pb[v][q] = B + (int64_t)min(n0 + rb, N - 1) * ldb + schunk * 8 + pks * 32;
+    }
+  const XlConv cv = p.cv;
+  const bool gather = cv.cin > 0;
+  const int loff = schunk * 8 + pks * 32;
+  int gpix[2][2], gih[2][2], giw[2][2];
+  if (gather) {
+    const int hw = cv.ho * cv.wo;
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = bj0 + q;
+        const int row = min(m0 + (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow, M - 1);
+        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+        gih[v][q] = oh * cv.stride - cv.pad;
+        giw[v][q] = ow * cv.stride - cv.pad;
+        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
+      }
+  }
+  const int U = 4 * ktiles;
+  // issue unit i (kind k = i & 3) into its slot; the per-kind operand tables
+  // are indexed by compile-time constants only (a runtime index would put
+  // them in scratch, cdna_hip_programming.md rule 20)
+  auto stage_a8 = [&](auto vc, int kt, char* dst) {
+    constexpr int VV = decltype(vc)::value;  // U0: m half 0, U3: m half 1
+    const int koff = kt * XBK;
+    if (gather) {
+      const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
+      const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ih = gih[VV][q] + tr, iw = giw[VV][q] + tc;
+        const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
+        const bf16* src = ok ? A + (int64_t)(gpix[VV][q] + tr * cv.wi + tc) * lda + c0 + loff : g_zero_row + loff;
+        glds16(src, dst + q * 1024);
+      }
+      return;
+    }
+    const bool second = p.A2 && koff >= p.K1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) glds16((second ? pa2[VV][q] : pa[VV][q]) + koff, dst + q * 1024);
+  };
+  auto stage_b8 = [&](auto vc, int kt, char* dst) {
+    constexpr int VV = decltype(vc)::value;  // U1: n half 0, U2: n half 1
+#pragma unroll
+    for (int q = 0; q < 2; ++q) glds16(pb[VV][q] + kt * XBK, dst + q * 1024);
+  };
+  auto stage_i = [&](int i) {
+    const int kt = i >> 2, k = i & 3;
+    char* dst = smem + (i % NS) * SLOT + pks * 8192 + bj0 * 1024;
+    if (k == 0) stage_a8(std::integral_constant<int, 0>{}, kt, dst);
+    else if (k == 1) stage_b8(std::integral_constant<int, 1>{}, kt, dst);
+    else if (k == 2) stage_a8(std::integral_constant<int, 1>{}, kt, dst);
+    else stage_b8(std::integral_constant<int, 0>{}, kt, dst);
+  };
+  // retire every unit <= g + 4 given units < issued are in flight or done
+  auto wait_for = [&](int g, int issued) {
+    const int n = min(V, issued - 1 - (g + 4));
+    vmcnt_upto<2 * V>(n > 0 ? 2 * n : 0);
+  };
+  bf16x8 qa[2][4], qb[2][2];
+  auto read_a = [&](int slot) {
+    const char* base = smem + slot * SLOT + (wr * 4) * 1024 + frag_off;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qa[ks][i] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + i * 1024);
+  };
+  auto read_b = [&](int slot) {
+    const char* base = smem + slot * SLOT + (wc * 2) * 1024 + frag_off;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) qb[ks][j] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + j * 1024);
+  };
+  auto quad = [&](auto mqc, auto nqc) {
+    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[MQ * 4 + i][NQ * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  const int pro = min(D, U);
+  for (int i = 0; i < pro; ++i) stage_i(i);
+  wait_for(-1, pro);  // units 0..3 (tile 0) landed
+  barrier();
+  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
+  int issued = pro;
+  int s0 = 0;  // slot of unit 4 kt
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int g = 4 * kt;
+    const int sU0 = s0, sU2 = s0 + 1 >= NS ? s0 + 1 - NS : s0 + 1;
+    const int sU3 = s0 + 2 >= NS ? s0 + 2 - NS : s0 + 2, sU1 = s0 + 3 >= NS ? s0 + 3 - NS : s0 + 3;
+    read_a(sU0);
+    read_b(sU1);
+    if (issued < U) stage_i(issued++);
+    wait_for(g, issued);
+    quad(I0{}, I0{});
+    read_b(sU2);
+    if (issued < U) stage_i(issued++);
+    wait_for(g + 1, issued);
+    quad(I0{}, I1{});
+    read_a(sU3);
+    if (issued < U) stage_i(issued++);
+    wait_for(g + 2, issued);
+    quad(I1{}, I1{});
+    read_b(sU1);
+    if (issued < U) stage_i(issued++);
+    wait_for(g + 3, issued);
+    quad(I1{}, I0{});
+    s0 = s0 + 4 >= NS ? s0 + 4 - NS : s0 + 4;
   }
   if (wr == 0) barrier();  // equal barrier counts before the epilogue
   barrier();
@@ -980,10 +1157,15 @@ __device__ __forceinline__ int tn64_off(int row, int col) {
 // ABL (timing-only ablations, tools/tn_vit_pmc.py --ablate): 1 = no global
 // staging after the prologue (the LDS tiles go stale: schedule + LDS + MFMA
 // bound), 2 = staging kept but no barriers inside the main loop.
-template <int ABL>
+// ABL (timing-only ablations, tools/tn_vit_pmc.py --ablate): 1 = no global
+// staging after the prologue (the LDS tiles go stale: schedule + LDS + MFMA
+// bound), 2 = staging kept but no barriers inside the main loop.  RING: the
+// LDS unit ring of gemm_xl_nt_kernel PIPE 8 instead of two tile buffers.
+template <int ABL, int RING>
 __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs p) {
   constexpr int PLANE = 64 * 64, OPER = 8 * PLANE;  // bytes
-  __shared__ __attribute__((aligned(16))) char smem[4 * OPER];
+  constexpr int NS = XL_RING_SLOTS, SLOT = 4 * PLANE;
+  __shared__ __attribute__((aligned(16))) char smem[RING ? NS * SLOT : 4 * OPER];
   using v4i16 = short __attribute__((ext_vector_type(4)));
   using lds_v4 = __attribute__((address_space(3))) v4i16;
   const int M = p.M, N = p.N, K = p.K;
@@ -1104,7 +1286,94 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  if (KT > 0) {
+  if constexpr (RING) {
+    // the unit ring of gemm_xl_nt_kernel PIPE 8 (same issue order, slot rule
+    // and counted waits); a unit slot holds 4 planes: A units U0 / U3 planes
+    // {0,1,4,5} / {2,3,6,7} as 2 wr + (plane & 1), B units U1 / U2 planes
+    // {0,2,4,6} / {1,3,5,7} as plane >> 1 (= wc of the reading wave)
+    constexpr int D = NS - 1, V = NS - 5;
+    const int U = 4 * KT;
+    auto stage_i = [&](int i) {
+      const int kt = i >> 2, k = i & 3;
+      char* slot = smem + (i % NS) * SLOT + pi * PLANE;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int64_t m = mb + (int64_t)kt * 64 + srow[q];
+        char* dst = slot + ((2 * (wave & 1) + q) << 10);
+        const bf16* src = g_zero_row;
+        if (k == 0 || k == 2) {
+          const int pl = k + (pi & 1) + (pi >> 1) * 4;
+          const int col = n0 + pl * 32 + scol[q];
+          if (m < me && col < N) src = p.A + m * p.lda + col;
+        } else {
+          const int pl = 2 * pi + (k == 1 ? 1 : 0);
+          const int col = pl * 32 + scol[q];
+          if (m < me && k0 + col < K) {
+            if (!gather) {
+              src = p.B + m * p.ldb + k0 + col;
+            } else {
+              const int hw = cv.ho * cv.wo;
+              const int mi = (int)m, n = mi / hw, r = mi - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+              const int ih = oh * cv.stride - cv.pad + tr, iw = ow * cv.stride - cv.pad + tc;
+              if ((unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi)
+                src = p.B + ((int64_t)(n * cv.hi + ih) * cv.wi + iw) * p.ldb + kc0 + col;
+            }
+          }
+        }
+        glds16(src, dst);
+      }
+    };
+    auto wait_for = [&](int g, int issued) {
+      const int n = min(V, issued - 1 - (g + 4));
+      vmcnt_upto<2 * V>(n > 0 ? 2 * n : 0);
+    };
+    auto ring_a = [&](int slot) {
+      const char* base = smem + slot * SLOT + wr * 2 * PLANE;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) qa[ks][i] = tr_frag(base + (i >> 1) * PLANE, ks, (i & 1) * 16 + 4 * p4);
+    };
+    auto ring_b = [&](int slot) {
+      const char* base = smem + slot * SLOT + wc * PLANE;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) qb[ks][j] = tr_frag(base, ks, j * 16 + 4 * p4);
+    };
+    if (U > 0) {
+      const int pro = min(D, U);
+      for (int i = 0; i < pro; ++i) stage_i(i);
+      wait_for(-1, pro);
+      barrier();
+      if (wr == 1) barrier();
+      int issued = pro, s0 = 0;
+      for (int kt = 0; kt < KT; ++kt) {
+        const int g = 4 * kt;
+        const int sU0 = s0, sU2 = s0 + 1 >= NS ? s0 + 1 - NS : s0 + 1;
+        const int sU3 = s0 + 2 >= NS ? s0 + 2 - NS : s0 + 2, sU1 = s0 + 3 >= NS ? s0 + 3 - NS : s0 + 3;
+        ring_a(sU0);
+        ring_b(sU1);
+        if (issued < U) stage_i(issued++);
+        wait_for(g, issued);
+        quad(I0{}, I0{});
+        ring_b(sU2);
+        if (issued < U) stage_i(issued++);
+        wait_for(g + 1, issued);
+        quad(I0{}, I1{});
+        ring_a(sU3);
+        if (issued < U) stage_i(issued++);
+        wait_for(g + 2, issued);
+        quad(I1{}, I1{});
+        ring_b(sU1);
+        if (issued < U) stage_i(issued++);
+        wait_for(g + 3, issued);
+        quad(I1{}, I0{});
+        s0 = s0 + 4 >= NS ? s0 + 4 - NS : s0 + 4;
+      }
+      if (wr == 0) barrier();
+    }
+  } else if (KT > 0) {
     stage_unit(I0{}, 0);
     stage_unit(I2{}, 0);
     stage_unit(I3{}, 0);
@@ -1153,8 +1422,20 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
 
 int g_num_cus = 0;
 
-// main loop: 7 = ping-pong quadrant schedule (256-wide tiles; 128-wide tiles use the ring, 1)
-int g_xl_pipe = 7;
+// main loop: 7 = ping-pong quadrant schedule on two tile buffers, 8 = the same
+// schedule on the 10-slot unit ring (256-wide tiles; 128-wide tiles use the
+// half-step ring, 1)
+constexpr int kXlPipeDefault = 7;
+int g_xl_pipe = kXlPipeDefault;
+
+// 256 x 256 ping-pong launch (PIPE 7 or its ring form, PIPE 8)
+template <int EPI>
+void launch_pp256(const XlArgs& a, int blocks, hipStream_t s) {
+  if (g_xl_pipe == 8)
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 8>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+}
 
 template <int BN, int EPI>
 void launch_xl(const XlArgs& a, hipStream_t s) {
@@ -1179,8 +1460,8 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
     return;
   }
   if constexpr (BN == 256) {
-    if (g_xl_pipe == 7) {
-      hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    if (g_xl_pipe >= 7) {
+      launch_pp256<EPI>(a, blocks, s);
       return;
     }
   }
@@ -1196,8 +1477,8 @@ void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
     const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + bn - 1) / bn);
     if (bn == 128)
       hipLaunchKernelGGL((gemm_xl_nt_kernel<128, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
-    else if (g_xl_pipe == 7)
-      hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    else if (g_xl_pipe >= 7)
+      launch_pp256<EPI>(a, blocks, s);
     else
       hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     return;
@@ -1220,7 +1501,7 @@ int pick_bn(int M, int N) {
     // useful work / (rounds x tile work); the 128-wide tile runs the ring
     // loop, ~12 % slower per FLOP than the 256-wide ring and ~25 % slower than
     // the 256-wide ping-pong loop (profiles/vit_gemm_backends.md)
-    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : (g_xl_pipe == 7 ? 0.75 : 0.88));
+    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : (g_xl_pipe >= 7 ? 0.75 : 0.88));
   };
   return eff(128) > eff(256) ? 128 : 256;
 }
@@ -1401,10 +1682,10 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   if (conv) {
     const int blocks = mtiles * (int)((N + 255) / 256);
     switch (epi) {
-      case XL_STORE: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_STORE, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
-      case XL_MOMENTS: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_MOMENTS, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
-      case XL_ADD: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_ADD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
-      case XL_BNBWD: hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_BNBWD, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a); break;
+      case XL_STORE: launch_pp256<XL_STORE>(a, blocks, s); break;
+      case XL_MOMENTS: launch_pp256<XL_MOMENTS>(a, blocks, s); break;
+      case XL_ADD: launch_pp256<XL_ADD>(a, blocks, s); break;
+      case XL_BNBWD: launch_pp256<XL_BNBWD>(a, blocks, s); break;
       default: TORCH_CHECK(false, "conv_xl: mode ", mode, " has no implicit-GEMM variant");
     }
   } else {
@@ -1544,7 +1825,7 @@ at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>&
     a.omap.s = 2; a.omap.ho = (int)ho; a.omap.wo = (int)wo; a.omap.hi = (int)hi; a.omap.wi = (int)wi;
     a.omap.oy = py; a.omap.ox = px;
     const int blocks = (int)((a.M + XBM - 1) / XBM) * (int)(cin / 256);
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, XL_STORE, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    launch_pp256<XL_STORE>(a, blocks, s);
   }
   DMP_HIP_CHECK(hipGetLastError());
   return dx;
@@ -1556,6 +1837,7 @@ namespace {
 
 int g_tn_xl_ablate = 0;  // timing-only ablations of the TN main loop (see gemm_tn_pp_kernel)
 int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
+int g_tn_xl_ring = 0;    // 1: main loop on the LDS unit ring (PIPE 8 schedule)
 
 at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype) {
   const int M = a.M, N = a.N, K = a.K;
@@ -1575,11 +1857,13 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   a.part = part.data_ptr<float>();
   hipStream_t s = at::hip::getCurrentHIPStream();
   if (g_tn_xl_ablate == 1)
-    hipLaunchKernelGGL(gemm_tn_pp_kernel<1>, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+    hipLaunchKernelGGL((gemm_tn_pp_kernel<1, 0>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   else if (g_tn_xl_ablate == 2)
-    hipLaunchKernelGGL(gemm_tn_pp_kernel<2>, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+    hipLaunchKernelGGL((gemm_tn_pp_kernel<2, 0>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  else if (g_tn_xl_ring)
+    hipLaunchKernelGGL((gemm_tn_pp_kernel<0, 1>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   else
-    hipLaunchKernelGGL(gemm_tn_pp_kernel<0>, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+    hipLaunchKernelGGL((gemm_tn_pp_kernel<0, 0>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   DMP_HIP_CHECK(hipGetLastError());
   split_reduce_launch(a.part, splits, (int64_t)N * K, out, s);
   return out;
@@ -1630,13 +1914,19 @@ void set_tn_xl_ablation(int a) {
   TORCH_CHECK(a >= 0 && a <= 2, "tn ablation must be 0 (off), 1 (no staging) or 2 (no barriers)");
   g_tn_xl_ablate = a;
 }
+void set_tn_xl_ring(int r) { g_tn_xl_ring = r != 0; }
+
+int get_gemm_xl_pipe() { return g_xl_pipe; }
+int get_tn_xl_ring() { return g_tn_xl_ring; }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
+  if (pipe < 0) pipe = kXlPipeDefault;
   TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");
   g_xl_group_m = group_m;
   TORCH_CHECK(bn == 0 || bn == 128 || bn == 256, "bn must be 0 (auto), 128 or 256");
-  TORCH_CHECK(pipe >= 0 && pipe <= 7,
-              "pipe must be 0..7 (2..5: timing-only ablations, 6: persistent, 7: ping-pong 256x256)");
+  TORCH_CHECK(pipe >= 0 && pipe <= 8,
+              "pipe must be 0..8 (2..5: timing-only ablations, 6: persistent, 7: ping-pong 256x256, "
+              "8: ping-pong on the LDS unit ring)");
   g_xl_bn_override = bn;
   g_xl_pipe = pipe;
 }

@@ -20,6 +20,13 @@ import torch
 from .. import _native
 
 
+
+class ForeignOptimizerState(ValueError):
+    """The state dict was written by another optimizer class (e.g. a
+    torch.optim.SGD state from an older DataParallel run): nothing in it maps
+    onto this optimizer.  ``load_checkpoint`` tolerates only this case; a
+    layout mismatch of our own format stays a hard error."""
+
 class FlatSGD(torch.optim.Optimizer):
     def __init__(self, ddp, lr: float, momentum: float = 0.0, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, master_weights: bool = True):
@@ -113,8 +120,8 @@ class FlatSGD(torch.optim.Optimizer):
         from ``sd['layout']`` to the current layout, never copied flat-to-flat.
         """
         if "layout" not in sd or "flat_state" not in sd:
-            raise ValueError("FlatSGD.load_state_dict: not a FlatSGD state (e.g. a torch.optim.SGD "
-                             "state dict)")
+            raise ForeignOptimizerState("FlatSGD.load_state_dict: not a FlatSGD state (e.g. a "
+                                        "torch.optim.SGD state dict)")
         self._ensure_state()
         self._steps = sd["steps"]
         for g, sg in zip(self.param_groups, sd["param_groups"]):
@@ -244,8 +251,8 @@ class MasterSGD(torch.optim.Optimizer):
 
     def load_state_dict(self, sd):
         if "numels" not in sd or "flat_state" not in sd:
-            raise ValueError("MasterSGD.load_state_dict: not a MasterSGD state (e.g. a torch.optim.SGD "
-                             "state dict)")
+            raise ForeignOptimizerState("MasterSGD.load_state_dict: not a MasterSGD state (e.g. a "
+                                        "torch.optim.SGD state dict)")
         if sd["numels"] != [[p.numel() for p in st["params"]] for st in self._groups]:
             raise ValueError("MasterSGD.load_state_dict: parameter layout differs from the checkpoint")
         self._steps = sd["steps"]

@@ -153,7 +153,8 @@ def scatter_kwargs(inputs: Tuple, kwargs: Optional[Dict], target_gpus: Sequence,
     return tuple(tuple(i) for i in ins), tuple(kws)
 
 
-_REPLICA_CACHE: Dict[Tuple[int, Tuple[str, ...]], "_Skeleton"] = {}
+_SLOTS = frozenset(("_parameters", "_buffers", "_modules", "_is_replica"))
+_MISSING = object()
 
 
 class _Skeleton:
@@ -164,11 +165,22 @@ class _Skeleton:
     on a host-bound step that is most of DP's replicate cost (measured: 15 ms
     of a 72 ms ResNet-50 step at 4 x 64 images, profiles/raw_r3/bench_dp4_256.log).
     Here the objects persist and each forward only rebinds their parameter and
-    buffer slots (and mirrors the mode flag / attributes); the structure is
-    re-validated every call, so a module added, removed or re-assigned rebuilds
-    the skeleton."""
+    buffer slots and re-mirrors every plain attribute whose object changed
+    (``training``, ``momentum``, ``p``, flags: upstream's per-call ``__dict__``
+    copy, at the cost of an identity compare per entry); the structure is
+    re-validated every call, so a module added, removed or re-assigned
+    rebuilds the skeleton.
+
+    A skeleton belongs to ONE DataParallel instance (``DataParallel._replicas``,
+    freed with it: no process-wide cache keeps a wrapped network alive) and
+    is held by one forward at a time (``lock``): a concurrent forward of the
+    same instance on another thread gets a fresh, uncached skeleton.  After
+    ``parallel_apply`` the replica slots are cleared (``release``), so the
+    broadcast parameter / buffer copies live only as long as the autograd
+    graph that needs them."""
 
     def __init__(self, network: nn.Module, ndev: int):
+        self.lock = threading.Lock()
         self.modules = list(network.modules())
         self.sig = self.signature(network, self.modules)
         midx = {id(m): i for i, m in enumerate(self.modules)}
@@ -197,21 +209,64 @@ class _Skeleton:
                      for m in modules)
 
     def refresh_attrs(self) -> None:
-        """The mode flag follows the source module every call (``.train()`` /
-        ``.eval()``); other attributes are shared shallowly as in upstream (a
-        re-bound attribute is picked up by a rebuild: ``invalidate_replicas``)."""
+        """Mirror every non-slot attribute of the source modules into the
+        replicas (re-bound or added ones included; removed ones removed)."""
         for i, m in enumerate(self.modules):
-            t = m.training
+            src = m.__dict__
             for mods in self.replicas:
-                mods[i].training = t
+                rd = mods[i].__dict__
+                for k, v in src.items():
+                    if k not in _SLOTS and rd.get(k, _MISSING) is not v:
+                        rd[k] = v
+                if len(rd) != len(src) + (0 if "_is_replica" in src else 1):
+                    for k in [k for k in rd if k not in src and k not in _SLOTS]:
+                        del rd[k]
+
+    def bind(self, per_dev, pidx, per_dev_b, bidx) -> None:
+        for i, m in enumerate(self.modules):
+            for d, mods in enumerate(self.replicas):
+                r = mods[i]
+                for k, p in m._parameters.items():
+                    r._parameters[k] = None if p is None else per_dev[d][pidx[id(p)]]
+                for k, b in m._buffers.items():
+                    if b is None:
+                        r._buffers[k] = None
+                    elif d == 0:
+                        r._buffers[k] = b  # device 0 shares the real buffers (running stats)
+                    else:
+                        r._buffers[k] = per_dev_b[d][bidx[id(b)]]
+
+    def release(self) -> None:
+        """Drop the per-call tensors from the replica slots and free the skeleton."""
+        for mods in self.replicas:
+            for r in mods:
+                for k in r._parameters:
+                    r._parameters[k] = None
+                for k in r._buffers:
+                    r._buffers[k] = None
+        if self.lock.locked():
+            self.lock.release()
 
 
-def invalidate_replicas() -> None:
-    """Drop the cached replica skeletons (after re-binding module attributes)."""
-    _REPLICA_CACHE.clear()
+class _Replicas(list):
+    """The replica roots of one forward; ``release()`` after parallel_apply."""
+
+    skeleton: Optional[_Skeleton] = None
+
+    def release(self) -> None:
+        if self.skeleton is not None:
+            self.skeleton.release()
+            self.skeleton = None
 
 
-def replicate(network: nn.Module, devices: Sequence, detach: bool = False) -> List[nn.Module]:
+def replicate(network: nn.Module, devices: Sequence, detach: bool = False,
+              cache: Optional[Dict] = None) -> List[nn.Module]:
+    """Replicas of ``network`` on ``devices`` (upstream ``replicate``).
+
+    ``cache``: a dict owned by the caller (DataParallel keeps one per
+    instance) in which the replica module objects persist between calls; the
+    returned list's ``release()`` must then be called once the replicas have
+    run.  Without a cache every call builds fresh module objects."""
     devices = [comm_ops._dev(d) for d in devices]
     params = list(network.parameters())
     pidx = {id(p): i for i, p in enumerate(params)}
@@ -229,25 +284,27 @@ def replicate(network: nn.Module, devices: Sequence, detach: bool = False) -> Li
     per_dev_b = comm_ops.broadcast_coalesced([b.detach() for b in bufs], devices) if bufs else \
         [[] for _ in devices]
 
-    key = (id(network), tuple(str(d) for d in devices))
-    sk = _REPLICA_CACHE.get(key)
-    if sk is None or sk.signature(network) != sk.sig:
-        sk = _REPLICA_CACHE[key] = _Skeleton(network, len(devices))
-    else:
-        sk.refresh_attrs()
-    for i, m in enumerate(sk.modules):
-        for d in range(len(devices)):
-            r = sk.replicas[d][i]
-            for k, p in m._parameters.items():
-                r._parameters[k] = None if p is None else per_dev[d][pidx[id(p)]]
-            for k, b in m._buffers.items():
-                if b is None:
-                    r._buffers[k] = None
-                elif d == 0:
-                    r._buffers[k] = b  # device 0 shares the real buffers (running stats)
-                else:
-                    r._buffers[k] = per_dev_b[d][bidx[id(b)]]
-    return [sk.replicas[d][0] for d in range(len(devices))]
+    sk = None
+    if cache is not None:
+        key = tuple(str(d) for d in devices)
+        sk = cache.get(key)
+        if sk is not None and sk.signature(network) != sk.sig:
+            sk = None
+        if sk is None:
+            sk = cache[key] = _Skeleton(network, len(devices))
+            sk.lock.acquire()
+        elif sk.lock.acquire(blocking=False):
+            sk.refresh_attrs()
+        else:  # this instance is mid-forward on another thread: do not share its replicas
+            sk = None
+    owned = sk is not None
+    if sk is None:
+        sk = _Skeleton(network, len(devices))
+    sk.bind(per_dev, pidx, per_dev_b, bidx)
+    out = _Replicas(sk.replicas[d][0] for d in range(len(devices)))
+    if owned:
+        out.skeleton = sk
+    return out
 
 
 class ReplicaError(RuntimeError):
@@ -386,6 +443,7 @@ class DataParallel(nn.Module):
         super().__init__()
         self.module = module
         self.dim = dim
+        self._replicas: Dict = {}  # per-instance replica skeletons (see _Skeleton)
         if not torch.cuda.is_available():
             self.device_ids: List[int] = []
             self.output_device = None
@@ -421,13 +479,22 @@ class DataParallel(nn.Module):
                 return self.module(*ins[0], **kws[0])
         with phase("dp.replicate"):
             replicas = self.replicate(self.module, self.device_ids[:len(ins)])
-        with phase("dp.parallel_apply"):
-            outs = self.parallel_apply(replicas, ins, kws)
+        try:
+            with phase("dp.parallel_apply"):
+                outs = self.parallel_apply(replicas, ins, kws)
+        finally:
+            release = getattr(replicas, "release", None)
+            if release is not None:
+                release()
         with phase("dp.gather"):
             return self.gather(outs, self.output_device)
 
     def replicate(self, module, device_ids):
-        return replicate(module, device_ids, not torch.is_grad_enabled())
+        return replicate(module, device_ids, not torch.is_grad_enabled(), cache=self._replicas)
+
+    def invalidate_replicas(self) -> None:
+        """Drop the cached replica skeletons (they are rebuilt on the next forward)."""
+        self._replicas.clear()
 
     def scatter(self, inputs, kwargs, device_ids):
         return scatter_kwargs(inputs, kwargs, device_ids, self.dim)

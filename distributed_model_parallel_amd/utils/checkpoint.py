@@ -111,12 +111,20 @@ def load_checkpoint(path: str, model: nn.Module, optimizer=None, scheduler=None,
     target.load_state_dict(_strip_prefix(state["net"]), strict=strict)
     restored = False
     if optimizer is not None and state.get("optimizer") is not None:
-        try:
-            optimizer.load_state_dict(state["optimizer"])
+        from ..ops.optim import ForeignOptimizerState
+        sd = state["optimizer"]
+        ours = hasattr(optimizer, "sync_from_params")  # FlatSGD / MasterSGD
+        if ours:
+            try:
+                optimizer.load_state_dict(sd)
+                restored = True
+            except ForeignOptimizerState as e:  # e.g. a torch.optim.SGD state from an older DP run
+                warnings.warn(f"load_checkpoint: optimizer state not restored ({e}); starting it "
+                              "fresh from the loaded weights")
+            # any other error (a layout that differs from the checkpoint) propagates
+        else:
+            optimizer.load_state_dict(sd)
             restored = True
-        except (KeyError, ValueError) as e:  # e.g. a torch.optim.SGD state from an older DP run
-            warnings.warn(f"load_checkpoint: optimizer state not restored ({e}); starting it fresh "
-                          "from the loaded weights")
     if optimizer is not None and not restored and hasattr(optimizer, "sync_from_params"):
         # weights came without (usable) optimizer state: the fp32 masters must follow them
         optimizer.sync_from_params()

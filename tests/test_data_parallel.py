@@ -212,9 +212,11 @@ def test_replica_skeletons_are_reused_and_follow_mode_and_structure():
     dp = DataParallel(m, device_ids=[0, 0, 0])
     x = torch.randn(6, 3, 8, 8, device="cuda")
     r1 = dp.replicate(m, [0, 0, 0])
+    r1.release()
     r2 = dp.replicate(m, [0, 0, 0])
     assert r1[1] is r2[1] and r1[1].conv is r2[1].conv
     assert all(torch.equal(a, b) for a, b in zip(r2[2].parameters(), m.parameters()))
+    r2.release()
     for _ in range(2):  # two steps through the cached skeleton: grads still match one module
         m.zero_grad()
         F.cross_entropy(dp(x), torch.arange(6, device="cuda") % 5).backward()
@@ -224,8 +226,57 @@ def test_replica_skeletons_are_reused_and_follow_mode_and_structure():
         for a, p in zip(g, m.parameters()):
             torch.testing.assert_close(a, p.grad, atol=1e-5, rtol=1e-4)
     m.eval()
-    assert not dp.replicate(m, [0, 0, 0])[1].training
+    r = dp.replicate(m, [0, 0, 0])
+    assert not r[1].training
+    r.release()
     m.train()
     m.fc = nn.Linear(16, 5).cuda()
     r3 = dp.replicate(m, [0, 0, 0])
     assert r3[1].fc is not r2[1].fc and torch.equal(r3[1].fc.weight, m.fc.weight)
+    r3.release()
+
+
+class BNNet(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(4, 4)
+        self.bn = nn.BatchNorm1d(4)
+        self.drop = nn.Dropout(0.0)
+
+    def forward(self, x):
+        return self.drop(self.bn(self.fc(x)))
+
+
+def test_replica_cache_attrs_concurrency_and_lifetime():
+    """The skeleton cache (advisor r3): re-bound plain attributes reach the
+    replicas, a forward holding the skeleton forces a concurrent one onto fresh
+    replicas, release() drops the per-call tensors, and the cache lives on the
+    caller (no process-wide dict keeps a network alive)."""
+    import gc
+    import weakref
+    m = BNNet()
+    cache = {}
+    devs = ["cpu", "cpu"]
+    r1 = replicate(m, devs, cache=cache)
+    assert r1[1].bn.momentum == 0.1
+    held = replicate(m, devs, cache=cache)  # r1 not released: must not share its objects
+    assert held[1] is not r1[1] and held.skeleton is None
+    r1.release()
+    assert r1[1].fc._parameters["weight"] is None and r1[1].bn._buffers["running_mean"] is None
+    m.bn.momentum = 0.5
+    m.drop.p = 0.25
+    m.extra_flag = True
+    r2 = replicate(m, devs, cache=cache)
+    assert r2[1] is r1[1], "released skeleton is reused"
+    assert r2[1].bn.momentum == 0.5 and r2[1].drop.p == 0.25 and r2[1].extra_flag
+    assert torch.equal(r2[1].fc.weight, m.fc.weight)
+    r2.release()
+    del m.extra_flag
+    r3 = replicate(m, devs, cache=cache)
+    assert not hasattr(r3[1], "extra_flag")
+    r3.release()
+    # a DataParallel-style owner: dropping it and the network frees both
+    ref = weakref.ref(m)
+    del m, r1, r2, r3, held, cache
+    gc.collect()
+    assert ref() is None, "the replica cache kept the network alive"

@@ -13,6 +13,16 @@ DEV = "cuda"
 CL = torch.channels_last
 
 
+@pytest.fixture(autouse=True, params=[0, 1], ids=["tilebuf", "ring"])
+def ring(request):
+    """Every case on both main loops: two tile buffers and the LDS unit ring."""
+    C = _native.require("gemm_tn_xl")
+    old = C.get_tn_xl_ring()
+    C.set_tn_xl_ring(request.param)
+    yield request.param
+    C.set_tn_xl_ring(old)
+
+
 @pytest.mark.parametrize("M,N,K", [(802816 // 4, 256, 1024), (5000, 200, 264), (100, 256, 256), (64, 512, 512),
                                    (33, 64, 128), (50176, 2048, 512)])
 @pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])
@@ -27,9 +37,12 @@ def test_gemm_tn_xl(M, N, K, out):
     torch.testing.assert_close(got.float(), ref, atol=tol, rtol=1e-2)
 
 
-def test_gemm_tn_xl_exact_pattern():
+@pytest.mark.parametrize("M", [640, 64, 192, 320, 576])
+def test_gemm_tn_xl_exact_pattern(M):
+    """Exact small-integer products; M = 64..576 covers 1..9 K tiles per split
+    (fewer than the ring's 9-unit prologue and the tail of the counted waits)."""
     C = _native.require("gemm_tn_xl")
-    M, N, K = 640, 256, 512
+    N, K = 256, 512
     a = (torch.arange(M * N, device=DEV).reshape(M, N) % 7 - 3).bfloat16()
     b = (torch.arange(M * K, device=DEV).reshape(M, K) % 5 - 2).bfloat16()
     assert torch.equal(C.gemm_tn_xl(a, b, torch.float32), a.float().t() @ b.float())

@@ -20,16 +20,18 @@ def _tol(K):
     return dict(atol=0.03 * K ** 0.5, rtol=2e-2)
 
 
-@pytest.fixture(params=[(0, 1), (128, 1), (256, 1), (128, 0), (256, 0), (128, 6), (256, 6), (256, 7)],
+@pytest.fixture(params=[(0, 1), (128, 1), (256, 1), (128, 0), (256, 0), (128, 6), (256, 6), (256, 7), (256, 8)],
                 ids=["auto", "bn128", "bn256", "bn128-pipe0", "bn256-pipe0", "bn128-persist", "bn256-persist",
-                     "bn256-pingpong"])
+                     "bn256-pingpong", "bn256-ring"])
 def bn(request):
+    old = C().get_gemm_xl_pipe()
     C().set_gemm_xl_bn(*request.param)
     yield request.param
-    C().set_gemm_xl_bn(0)
+    C().set_gemm_xl_bn(0, old)
 
 
-@pytest.mark.parametrize("M,N,K", [(25216, 768, 768), (300, 2304, 64), (513, 136, 192), (4096, 1024, 3072)])
+@pytest.mark.parametrize("M,N,K", [(25216, 768, 768), (300, 2304, 64), (513, 136, 192), (4096, 1024, 3072),
+                                   (700, 512, 128), (1100, 768, 576)])
 def test_xl_store(M, N, K, bn):
     torch.manual_seed(0)
     a = torch.randn(M, K, device=DEV).bfloat16()

@@ -63,9 +63,11 @@ def test_xl_bnbwd_matches_nt(mask_from_y, with_res):
     torch.testing.assert_close(sums[N:2 * N], (dzd * (x.double() - mean.double())).sum(0), atol=1e-2, rtol=1e-4)
 
 
+@pytest.mark.parametrize("pipe", [7, 8])
 @pytest.mark.parametrize("mode", ["moments", "bnbwd"])
-def test_xl_conv_pingpong_schedule(mode):
-    """The 256 x 256 ping-pong main loop (PIPE 7) under the conv epilogues equals the ring kernel."""
+def test_xl_conv_pingpong_schedule(mode, pipe):
+    """The 256 x 256 ping-pong main loop (PIPE 7: two tile buffers, PIPE 8: the
+    LDS unit ring) under the conv epilogues equals the half-step ring kernel."""
     C = _native.require("gemm_xl_conv")
     torch.manual_seed(11)
     M, N, K = 5000, 512, 576
@@ -78,7 +80,7 @@ def test_xl_conv_pingpong_schedule(mode):
     C.set_gemm_xl_bn(256, 1)
     try:
         ref, rs = C.gemm_xl_conv(a, b, mode, **kw)
-        C.set_gemm_xl_bn(256, 7)
+        C.set_gemm_xl_bn(256, pipe)
         got, gs = C.gemm_xl_conv(a, b, mode, **kw)
     finally:
         C.set_gemm_xl_bn(0)

@@ -109,6 +109,21 @@ def test_master_sgd_rejects_foreign_optimizer_state(tmp_path):
         assert torch.equal(a, b)
 
 
+def test_master_sgd_layout_mismatch_is_an_error(tmp_path):
+    """only a FOREIGN optimizer state is tolerated; a MasterSGD
+    state whose parameter layout differs from the model must not be skipped
+    silently (the resume would continue with fresh momentum)."""
+    import pytest
+    from distributed_model_parallel_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+    src = _net()
+    opt_src = MasterSGD(src.parameters(), lr=0.1, momentum=0.9)
+    path = save_checkpoint(str(tmp_path / "ck.pth"), src, opt_src, epoch=1)
+    dst = _net()
+    opt = MasterSGD(list(dst.parameters())[:-1], lr=0.1, momentum=0.9)  # one parameter short
+    with pytest.raises(ValueError, match="layout differs"):
+        load_checkpoint(path, dst, opt, restore_rng=False)
+
+
 def test_checkpoint_with_legacy_numpy_rng_state_loads(tmp_path):
     """files whose RNG entry is np.random.get_state() (an
     ndarray) still load weights-only, and the numpy RNG is restored."""
