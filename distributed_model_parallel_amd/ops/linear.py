@@ -62,10 +62,19 @@ _TN_WGRAD = not _native.disabled("tn_xl")
 _TN_MIN_ROWS = 16384
 
 
+def _gemm_operand_ok(t: torch.Tensor) -> bool:
+    """What csrc/gemm/gemm_xl.hip check_bf16_2d demands of a GEMM operand:
+    2-D bf16, unit column stride, 16-B aligned rows and base (a column-sliced
+    or offset view fails here and takes the library path instead of raising
+    in the kernel's TORCH_CHECK)."""
+    return (t.dim() == 2 and t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.data_ptr() % 16 == 0)
+
+
 def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if (_TN_WGRAD and dy2.shape[0] >= _TN_MIN_ROWS and dy2.shape[1] >= 256 and x2.shape[1] >= 256
-            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1
-            and w.dtype == torch.bfloat16):
+            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and _gemm_operand_ok(dy2)
+            and _gemm_operand_ok(x2) and w.dtype == torch.bfloat16):
         _STATS["tn_wgrad"] += 1
         return _native.native().gemm_tn_xl(dy2, x2, w.dtype)
     return dy2.t().mm(x2)

@@ -187,7 +187,9 @@ class DistributedDataParallel(nn.Module):
         """hook(state, bucket_tensor) -> torch.futures.Future (result ignored; the
         hook must leave the reduced gradient in the bucket tensor)."""
         def adapter(index, bucket):
-            fut = hook(state, _Bucket(index, bucket))
+            # buckets are launched in index order (csrc/ddp/reducer.cpp
+            # in-order launch): the last one reduced has the highest index
+            fut = hook(state, _Bucket(index, bucket, len(self.reducer.buckets())))
 
             class _H:
                 def wait(self_inner):
@@ -343,11 +345,18 @@ class DistributedDataParallel(nn.Module):
 
 
 class _Bucket:
-    """Object handed to comm hooks (mirrors upstream GradBucket's essentials)."""
+    """Object handed to comm hooks (mirrors upstream GradBucket's essentials).
 
-    def __init__(self, index: int, buffer: torch.Tensor):
+    ``index()`` is the launch position: bucket 0 (the parameters whose
+    gradients are ready first in backward) is reduced first, and ``is_last()``
+    is true for the bucket reduced last in the iteration -- upstream's meaning
+    (a hook that flushes per-iteration state on the last bucket sees every
+    other bucket first)."""
+
+    def __init__(self, index: int, buffer: torch.Tensor, num_buckets: int):
         self._index = index
         self._buffer = buffer
+        self._num = num_buckets
 
     def index(self) -> int:
         return self._index
@@ -356,7 +365,7 @@ class _Bucket:
         return self._buffer
 
     def is_last(self) -> bool:
-        return self._index == 0
+        return self._index == self._num - 1
 
 
 def allreduce_hook(group):

@@ -27,6 +27,23 @@ from ..utils.env import single_rank_comm
 # DDP bucket all-reduces on the reducer's side stream -- two streams driving one
 # ncclComm would serialise the ~100 tiny per-step SyncBN collectives behind
 # (and interleave them with) the 25 MB bucket collectives.
+#
+# Ordering (why two communicators on two streams cannot deadlock across ranks):
+# an RCCL kernel blocks its stream -- and, when GPU_MAX_HW_QUEUES (4 here) makes
+# two streams share a hardware queue, everything queued behind it -- until
+# every peer has launched the matching kernel.  A cross-communicator deadlock
+# needs two ranks to submit the SyncBN and bucket collectives in DIFFERENT
+# interleavings.  They cannot: (1) each communicator's own sequence is the same
+# on every rank (SyncBN: layer order of the shared module; DDP: buckets
+# launched strictly in index order, reducer.cpp launch_ready_prefix_locked);
+# (2) both are enqueued from ONE host thread per rank -- the forward thread
+# for the forward moments, the autograd device thread for the SyncBN backward
+# nodes and for the post-accumulate hooks that launch buckets -- in an order
+# fixed by the autograd graph, which is identical on every rank (bucket
+# rebuilds follow rank 0's recorded order).  So the merged submission order is
+# rank-independent and every blocking kernel waits only for kernels its peers
+# submitted before theirs.  tests/test_comm_ordering.py records the merged
+# order on every rank of a DDP + SyncBN ResNet-18 and requires it identical.
 _COMMS = {}
 
 

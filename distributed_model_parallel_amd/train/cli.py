@@ -197,6 +197,30 @@ def evaluate(net, loader, to_dev, args):
 
 
 # --------------------------------------------------------------------------- #
+def batch_schedule(loader, batch_size: int):
+    """(number of batches, size of the last) of `loader`, read from its batch
+    sampler without loading data; ValueError unless every batch but the last
+    has `batch_size` samples (the pipeline's static shape contract)."""
+    bsamp = getattr(loader, "batch_sampler", None)
+    sampler = getattr(bsamp, "sampler", None)
+    if bsamp is not None and type(bsamp) is torch.utils.data.BatchSampler and sampler is not None:
+        n_items, bs, drop = len(sampler), bsamp.batch_size, bsamp.drop_last
+        if bs != batch_size:
+            raise ValueError(f"loader batch size {bs} != contract {batch_size}")
+        n = n_items // bs if drop else -(-n_items // bs)
+        last = bs if (drop or n_items % bs == 0) else n_items % bs
+    else:  # a custom batch sampler: walk its index lists (no data is loaded)
+        sizes = [len(b) for b in (bsamp if bsamp is not None else [])]
+        if not sizes:
+            raise ValueError("loader has no inspectable batch sampler")
+        if any(s != batch_size for s in sizes[:-1]) or sizes[-1] > batch_size:
+            raise ValueError(f"batch sizes {sorted(set(sizes))} do not follow the contract {batch_size}")
+        n, last = len(sizes), sizes[-1]
+    if n != len(loader):
+        raise ValueError(f"batch sampler yields {n} batches, len(loader) = {len(loader)}")
+    return n, last
+
+
 def run_pipeline(args, env) -> None:
     from ..comm.rccl import Communicator
     from ..data import prepare_dataloaders
@@ -225,13 +249,17 @@ def run_pipeline(args, env) -> None:
         train_ds, val_ds = _datasets(args)
         _, train_loader, val_loader = prepare_dataloaders(train_ds, val_ds, args.batch_size, args.workers,
                                                           pin_memory=env.device.type == "cuda")
-        n_train, n_val = len(train_loader), len(val_loader)
         vbs = val_loader.batch_size or args.batch_size
-
-        def _last(n_items: int, bs: int, drop: bool) -> int:
-            return bs if (drop or n_items % bs == 0) else n_items % bs
-        last_t = _last(len(train_ds), args.batch_size, bool(getattr(train_loader, "drop_last", False)))
-        last_v = _last(len(val_ds), vbs, bool(getattr(val_loader, "drop_last", False)))
+        # the static batch contract of every step, checked against the loaders'
+        # batch samplers BEFORE the loop: a mismatch found later would raise on
+        # rank 0 only while the other stages wait in a receive
+        bad = ""
+        try:
+            n_train, last_t = batch_schedule(train_loader, args.batch_size)
+            n_val, last_v = batch_schedule(val_loader, vbs)
+        except ValueError as e:
+            bad, n_train = str(e), -1
+            n_val = last_t = last_v = 0
     else:
         train_loader = val_loader = None
         n_train = n_val = last_t = last_v = vbs = 0
@@ -241,6 +269,9 @@ def run_pipeline(args, env) -> None:
     comm.broadcast(counts, 0)
     comm.synchronize()
     n_train, n_val, last_t, last_v, vbs = (int(v) for v in counts.tolist())
+    if n_train < 0:  # every rank stops here, together
+        raise ValueError("pipeline: the data loader's batches do not follow the static batch contract"
+                         + (f" ({bad})" if env.rank == 0 else " (see rank 0)"))
     n_train_all, n_val_all = n_train, n_val
     if args.steps_per_epoch:
         n_train, n_val = min(n_train, args.steps_per_epoch), min(n_val, args.steps_per_epoch)

@@ -173,3 +173,28 @@ def test_pipeline_static_batch_contract():
     assert res[0]["l1"] is not None and res[0]["l2"] is not None
     assert abs(res[1]["l1"] - res[0]["l1"]) < 1e-6  # the last stage holds the same loss
     assert "contract is 6" in res[0]["err"]
+
+
+def test_batch_schedule_matches_loader_and_rejects_ragged_batches():
+    """the CLI checks the static batch contract against the
+    loader's batch sampler before the loop (every rank then stops together)."""
+    import pytest
+    from torch.utils.data import BatchSampler, DataLoader, SequentialSampler, TensorDataset
+    from distributed_model_parallel_amd.train.cli import batch_schedule
+    ds = TensorDataset(torch.zeros(50, 2))
+    assert batch_schedule(DataLoader(ds, batch_size=16), 16) == (4, 2)
+    assert batch_schedule(DataLoader(ds, batch_size=16, drop_last=True), 16) == (3, 16)
+    assert batch_schedule(DataLoader(ds, batch_size=10), 10) == (5, 10)
+    with pytest.raises(ValueError):
+        batch_schedule(DataLoader(ds, batch_size=8), 16)
+
+    class Ragged:  # a custom batch sampler that breaks the contract mid-epoch
+        def __iter__(self):
+            return iter([list(range(16)), list(range(16, 28)), list(range(28, 44))])
+
+        def __len__(self):
+            return 3
+    with pytest.raises(ValueError):
+        batch_schedule(DataLoader(ds, batch_sampler=Ragged()), 16)
+    ok = BatchSampler(SequentialSampler(range(40)), 16, False)
+    assert batch_schedule(DataLoader(ds, batch_sampler=list(ok)), 16) == (3, 8)
