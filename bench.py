@@ -142,6 +142,9 @@ def main() -> int:
     ap.add_argument("--single-rank-comm", action="store_true",
                     help="run the DDP bucket all-reduces and SyncBN moment all-reduces through RCCL "
                          "even at world size 1 (measures their cost on one GPU)")
+    ap.add_argument("--checkpoint-segments", type=int, default=0, metavar="K",
+                    help="activation checkpointing: recompute the block trunk in K segments in "
+                         "backward (the reference's '2048(checkpoint)' runs, Readme.md:168,192)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--watchdog", type=float, default=None, metavar="SECONDS",
                     help="exit 1 when the collective stream is stuck this long (default 900 s for "
@@ -184,7 +187,8 @@ def main() -> int:
                      dp_devices=args.gpus if args.parallel == "dp" else 1,
                      dp_replicas=args.dp_replicas, graph=args.graph,
                      lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1),
-                     micro_batches=args.micro_batches, schedule=args.schedule, partition=args.partition)
+                     micro_batches=args.micro_batches, schedule=args.schedule, partition=args.partition,
+                     checkpoint_segments=args.checkpoint_segments)
     if args.parallel == "dp" and env.world_size > 1:
         raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
                          "--gpus N` without torchrun")
@@ -275,6 +279,7 @@ def main() -> int:
                 "stage_partition": st.wrapped.partition} if args.parallel == "pipe" else {}),
             **({"reference_images_per_sec": round(ref, 1)} if ref else {}),
             "hip_graph": args.graph,
+            "checkpoint_segments": args.checkpoint_segments,
             "watchdog_s": wd,
             "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
             if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,

@@ -5,13 +5,15 @@ from typing import Callable, Dict
 
 import torch.nn as nn
 
-from .mobilenetv2 import HeadPool, InvertedResidual, MobileNetV2, mobilenet_v2, mobilenet_v2_nobn
+from .mobilenetv2 import (HeadPool, InvertedResidual, MobileNetV2, mobilenet_v2, mobilenet_v2_224,
+                          mobilenet_v2_nobn)
 from .resnet import BasicBlock, Bottleneck, ResNet, resnet18, resnet34, resnet50, resnet101, resnet152
 from .vit import VisionTransformer, vit_b_16, vit_tiny
 
 MODELS: Dict[str, Callable[..., nn.Module]] = {
     "mobilenetv2": mobilenet_v2,
     "mobilenetv2_nobn": mobilenet_v2_nobn,
+    "mobilenetv2_224": mobilenet_v2_224,
     "resnet18": resnet18,
     "resnet34": resnet34,
     "resnet50": resnet50,
@@ -25,6 +27,7 @@ MODELS: Dict[str, Callable[..., nn.Module]] = {
 INPUT_SHAPES = {
     "mobilenetv2": ((3, 32, 32), 10),
     "mobilenetv2_nobn": ((3, 32, 32), 10),
+    "mobilenetv2_224": ((3, 224, 224), 1000),
     "resnet18": ((3, 224, 224), 1000),
     "resnet34": ((3, 224, 224), 1000),
     "resnet50": ((3, 224, 224), 1000),
@@ -43,6 +46,6 @@ def build_model(name: str, **kw) -> nn.Module:
 
 
 __all__ = ["MODELS", "INPUT_SHAPES", "build_model", "MobileNetV2", "InvertedResidual", "HeadPool",
-           "mobilenet_v2", "mobilenet_v2_nobn", "ResNet", "BasicBlock", "Bottleneck", "resnet18",
+           "mobilenet_v2", "mobilenet_v2_nobn", "mobilenet_v2_224", "ResNet", "BasicBlock", "Bottleneck", "resnet18",
            "resnet34", "resnet50", "resnet101", "resnet152", "VisionTransformer", "vit_b_16",
            "vit_tiny"]

@@ -42,6 +42,18 @@ CIFAR_SETTINGS: Tuple[Tuple[int, int, int, int], ...] = (
     (6, 320, 1, 1),
 )
 
+# ImageNet strides (torchvision's ``inverted_residual_setting``): the 224-px
+# model of the reference's batch-size / finetune study (Readme.md:185-196).
+IMAGENET_SETTINGS: Tuple[Tuple[int, int, int, int], ...] = (
+    (1, 16, 1, 1),
+    (6, 24, 2, 2),
+    (6, 32, 3, 2),
+    (6, 64, 4, 2),
+    (6, 96, 3, 1),
+    (6, 160, 3, 2),
+    (6, 320, 1, 1),
+)
+
 
 def _norm(ch: int, use_bn: bool, act: bool) -> nn.Module:
     if use_bn:
@@ -58,21 +70,23 @@ class InvertedResidual(nn.Module):
     """
 
     def __init__(self, cin: int, cout: int, expansion: int, stride: int,
-                 use_bn: bool = True, shortcut_bn: bool | None = None):
+                 use_bn: bool = True, shortcut_bn: bool | None = None, imagenet: bool = False):
         super().__init__()
         hidden = cin * expansion
         self.stride = stride
         # 1x1 convs run as the MFMA GEMM and the depthwise as the NHWC kernel on
-        # MI355X, each emitting the following BN's statistics from its epilogue
-        self.conv1 = Conv1x1(cin, hidden)
-        self.bn1 = _norm(hidden, use_bn, act=True)
+        # MI355X, each emitting the following BN's statistics from its epilogue.
+        # ImageNet form (torchvision): no expand conv at expansion 1, identity
+        # residual only (no projection shortcut).
+        self.conv1 = Conv1x1(cin, hidden) if not (imagenet and expansion == 1) else None
+        self.bn1 = _norm(hidden, use_bn, act=True) if self.conv1 is not None else None
         self.conv2 = DepthwiseConv2d(hidden, stride=stride)
         self.bn2 = _norm(hidden, use_bn, act=True)
         self.conv3 = Conv1x1(hidden, cout)
         self.bn3 = _norm(cout, use_bn, act=False)
-        self.has_residual = stride == 1
+        self.has_residual = stride == 1 and (cin == cout or not imagenet)
         sc_bn = use_bn if shortcut_bn is None else shortcut_bn
-        if stride == 1 and cin != cout:
+        if stride == 1 and cin != cout and not imagenet:
             mods: List[nn.Module] = [Conv1x1(cin, cout)]
             if sc_bn:
                 mods.append(BatchNormAct2d(cout, act=None))
@@ -81,7 +95,7 @@ class InvertedResidual(nn.Module):
             self.shortcut = nn.Sequential()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = conv_bn(self.conv1, self.bn1, x)
+        y = conv_bn(self.conv1, self.bn1, x) if self.conv1 is not None else x
         y = conv_bn(self.conv2, self.bn2, y)
         res = None
         if self.has_residual:
@@ -96,9 +110,10 @@ class InvertedResidual(nn.Module):
 
 
 class HeadPool(nn.Module):
-    """ReLU -> 4x4 average pool -> flatten (reference ``Reshape1``)."""
+    """ReLU -> 4x4 average pool -> flatten (reference ``Reshape1``);
+    ``pool=None``: global average pool (the 224-px ImageNet head)."""
 
-    def __init__(self, apply_relu: bool = True, pool: int = 4):
+    def __init__(self, apply_relu: bool = True, pool: int | None = 4):
         super().__init__()
         self.apply_relu = apply_relu
         self.pool = pool
@@ -106,7 +121,7 @@ class HeadPool(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.apply_relu:
             x = F.relu(x)
-        if x.shape[2] == self.pool and x.shape[3] == self.pool:
+        if self.pool is None or (x.shape[2] == self.pool and x.shape[3] == self.pool):
             return global_avg_pool(x)  # whole-map pool: channels-last broadcast backward
         return torch.flatten(F.avg_pool2d(x, self.pool), 1)
 
@@ -116,11 +131,15 @@ class MobileNetV2(nn.Module):
 
     def __init__(self, num_classes: int = 10, use_bn: bool = True,
                  settings: Sequence[Tuple[int, int, int, int]] = CIFAR_SETTINGS,
-                 nobn_shortcut_bn: bool = False):
+                 nobn_shortcut_bn: bool = False, imagenet: bool = False, dropout: float = 0.0):
         super().__init__()
         self.use_bn = use_bn
-        # 3x3 stem on the MFMA implicit GEMM (3 channels padded to 16, row taps)
-        self.conv1 = RowTapConv2d(3, 32, 3)
+        if imagenet:
+            # 224-px stem: 3x3 / stride 2 (the library conv; 3 input channels)
+            self.conv1 = nn.Conv2d(3, 32, 3, stride=2, padding=1, bias=False)
+        else:
+            # 3x3 stem on the MFMA implicit GEMM (3 channels padded to 16, row taps)
+            self.conv1 = RowTapConv2d(3, 32, 3)
         self.bn1 = _norm(32, use_bn, act=True)
         blocks: List[nn.Module] = []
         cin = 32
@@ -128,19 +147,24 @@ class MobileNetV2(nn.Module):
         for t, c, n, s in settings:
             for i in range(n):
                 blocks.append(InvertedResidual(cin, c, t, s if i == 0 else 1,
-                                               use_bn=use_bn, shortcut_bn=sc_bn))
+                                               use_bn=use_bn, shortcut_bn=sc_bn, imagenet=imagenet))
                 cin = c
         self.layers = nn.Sequential(*blocks)
         self.conv2 = Conv1x1(cin, 1280)
         self.bn2 = _norm(1280, use_bn, act=True)
-        self.pool = HeadPool(apply_relu=False)
+        # CIFAR: the reference's 4x4 pool of the 4x4 map; ImageNet: global pool of 7x7
+        self.pool = HeadPool(apply_relu=False, pool=None if imagenet else 4)
+        self.dropout = dropout
         self.linear = nn.Linear(1280, num_classes)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = conv_bn(self.conv1, self.bn1, x)  # stem BN moments from the conv epilogue
         x = self.layers(x)
         x = conv_bn(self.conv2, self.bn2, x)
-        return self.linear(self.pool(x))
+        x = self.pool(x)
+        if self.dropout:
+            x = F.dropout(x, self.dropout, self.training)
+        return self.linear(x)
 
     # ------------------------------------------------------------------ #
     def as_sequential(self) -> nn.Sequential:
@@ -165,6 +189,16 @@ def mobilenet_v2(num_classes: int = 10, **kw) -> MobileNetV2:
 
 def mobilenet_v2_nobn(num_classes: int = 10, **kw) -> MobileNetV2:
     return MobileNetV2(num_classes=num_classes, use_bn=False, **kw)
+
+
+def mobilenet_v2_224(num_classes: int = 1000, **kw) -> MobileNetV2:
+    """MobileNetV2 at 224 px, ImageNet strides (torchvision's architecture:
+    3,504,872 parameters at 1000 classes, 2,236,682 at 10), the model of the
+    reference's batch-size finetune study (Readme.md:185-196).  Activations
+    are ReLU, not ReLU6 (the fused BN kernels implement ReLU); with no
+    pretrained weights offline the study's accuracy parity is unpinned."""
+    kw.setdefault("dropout", 0.2)
+    return MobileNetV2(num_classes=num_classes, settings=IMAGENET_SETTINGS, imagenet=True, **kw)
 
 
 def sample_forward(batch: int = 2) -> torch.Size:

@@ -393,13 +393,13 @@ class _FoldDgrad:
 
 def foldable(conv: nn.Module, bn: nn.Module, a: torch.Tensor) -> bool:
     """Training-mode conv1x1 -> BN(+residual)+ReLU that the fold covers natively."""
-    from ..utils.checkpointing import in_recompute
+    from ..utils.checkpointing import in_checkpoint
     from .batchnorm import BatchNormAct2d
     from .conv1x1 import Conv1x1, _native_ok
     return (ENABLED and isinstance(bn, BatchNormAct2d) and bn.act == "relu" and bn.training
             and bn.track_running_stats and bn.momentum is not None and bn.running_mean is not None
             and bn.running_mean.dtype == torch.float32 and isinstance(conv, Conv1x1)
-            and conv.stride[0] == 1 and torch.is_grad_enabled() and not in_recompute()
+            and conv.stride[0] == 1 and torch.is_grad_enabled() and not in_checkpoint()
             and _native_ok(a, conv.weight) and conv.weight.shape[0] % 64 == 0 and a.shape[1] % 64 == 0)
 
 
@@ -442,7 +442,7 @@ def foldable_downsample(ds: Optional[nn.Module], x: torch.Tensor, cout: int) -> 
     """A ResNet downsample (Sequential(Conv1x1, BatchNormAct2d without ReLU))
     that can join the bn3 fold: the same checks as foldable() on its BN, the
     block input as its conv's native operand, Cin <= 1024 for the coefficient kernels."""
-    from ..utils.checkpointing import in_recompute
+    from ..utils.checkpointing import in_checkpoint
     from .batchnorm import BatchNormAct2d
     from .conv1x1 import Conv1x1, _native_ok
     if not (ENABLED and _FOLD_DS and isinstance(ds, nn.Sequential) and len(ds) == 2):
@@ -450,7 +450,7 @@ def foldable_downsample(ds: Optional[nn.Module], x: torch.Tensor, cout: int) -> 
     conv, bn = ds[0], ds[1]
     return (isinstance(conv, Conv1x1) and isinstance(bn, BatchNormAct2d) and bn.act is None and bn.training
             and bn.track_running_stats and bn.momentum is not None and bn.running_mean is not None
-            and bn.running_mean.dtype == torch.float32 and torch.is_grad_enabled() and not in_recompute()
+            and bn.running_mean.dtype == torch.float32 and torch.is_grad_enabled() and not in_checkpoint()
             and _native_ok(x, conv.weight) and conv.weight.shape[0] == cout and x.shape[1] % 64 == 0
             and x.shape[1] <= 1024)
 

@@ -182,7 +182,7 @@ def bn_relu_conv1x1(bn: nn.Module, conv: nn.Module, x: torch.Tensor,
     the GEMM's operand staging) when training natively with fused input moments;
     otherwise the two modules run as usual."""
     from .. import _native
-    from ..utils.checkpointing import in_recompute
+    from ..utils.checkpointing import in_checkpoint
     from .conv1x1 import Conv1x1, _native_ok
     if sums is None and isinstance(bn, BatchNormAct2d) and bn.training and _native_ok(x, conv.weight):
         # the producing conv ran on a library kernel (no fused moments): reduce here
@@ -190,7 +190,7 @@ def bn_relu_conv1x1(bn: nn.Module, conv: nn.Module, x: torch.Tensor,
         sums = local_moments(_as_rows(x)[0], True)
     fusable = (sums is not None and isinstance(bn, BatchNormAct2d) and bn.act == "relu"
                and bn.training and bn.track_running_stats and bn.momentum is not None
-               and not in_recompute() and isinstance(conv, Conv1x1) and conv.stride[0] == 1
+               and not in_checkpoint() and isinstance(conv, Conv1x1) and conv.stride[0] == 1
                and bn.running_mean is not None and bn.running_mean.dtype == torch.float32
                and _native_ok(x, conv.weight) and torch.is_grad_enabled())
     if not fusable:
@@ -279,9 +279,9 @@ def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Te
     pool (forward) and the BN backward's reductions inside the pool's backward
     when training natively; otherwise the modules run one after another."""
     from .. import _native
-    from ..utils.checkpointing import in_recompute
+    from ..utils.checkpointing import in_checkpoint
     fusable = (isinstance(bn, BatchNormAct2d) and bn.act == "relu" and bn.training and bn.track_running_stats
-               and bn.momentum is not None and not in_recompute() and torch.is_grad_enabled()
+               and bn.momentum is not None and not in_checkpoint() and torch.is_grad_enabled()
                and hasattr(conv, "forward_with_moments") and isinstance(pool, nn.MaxPool2d)
                and pool.kernel_size in (3, (3, 3)) and pool.stride in (2, (2, 2))
                and pool.padding in (0, 1, (1, 1), (0, 0)) and not pool.ceil_mode

@@ -61,7 +61,13 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--schedule", default="1f1b", choices=["naive", "gpipe", "1f1b"])
     p.add_argument("--partition", default="balanced", choices=["balanced", "reference"],
                    help="pipeline stage cut: FLOP-balanced (any ws) or the reference's MobileNetV2 cut")
-    p.add_argument("--warmup-epochs", default=10, type=int)
+    p.add_argument("--warmup-epochs", default=10, type=int, help="linear lr warm-up (0 = none)")
+    p.add_argument("--lr-steps", default="", metavar="E1,E2,...",
+                   help="step decay at these epochs instead of cosine (reference no-BN study: 30,60)")
+    p.add_argument("--lr-gamma", default=0.1, type=float, help="decay factor of --lr-steps")
+    p.add_argument("--checkpoint-segments", default=0, type=int, metavar="K",
+                   help="activation checkpointing: recompute the model in K segments in backward "
+                        "(reference large-batch runs '2048(checkpoint)', Readme.md:168,192; 0 = off)")
     p.add_argument("--steps-per-epoch", default=0, type=int, help="cap iterations per epoch (0 = all)")
     p.add_argument("--log-dir", default="./log")
     p.add_argument("--checkpoint", default="./checkpoint/ckpt.pth")
@@ -83,6 +89,10 @@ def _datasets(args):
     else:
         tr, va = T.imagenet_train_transform(), T.imagenet_val_transform()
     return DatasetCollection(args.dataset_type, args.data, tr, va).init()
+
+
+def _lr_steps(args):
+    return [int(v) for v in args.lr_steps.split(",") if v.strip()] if args.lr_steps else None
 
 
 def _num_classes(args) -> int:
@@ -110,6 +120,9 @@ def run_data_parallel(args, env) -> None:
     dev = env.device
     dtype = parse_dtype(args.dtype)
     model = build_model(args.arch, num_classes=_num_classes(args))
+    if args.checkpoint_segments > 1:
+        from ..utils.checkpointing import enable_activation_checkpointing
+        enable_activation_checkpointing(model, args.checkpoint_segments)
     if args.sync_bn and args.parallel == "ddp":
         model = SyncBatchNorm.convert_sync_batchnorm(model)
     model = model.to(dev)
@@ -125,8 +138,10 @@ def run_data_parallel(args, env) -> None:
         opt = MasterSGD(model.parameters(), lr=args.lr, momentum=args.momentum,
                         weight_decay=args.weight_decay)
         net = DataParallel(model) if args.parallel == "dp" else model
-    sched = build_schedule(opt, args.epochs, args.warmup_epochs)
-    train_ds, val_ds = _datasets(args)
+    sched = build_schedule(opt, args.epochs, args.warmup_epochs, _lr_steps(args), args.lr_gamma)
+    from ..utils.debug import rank0_first
+    with rank0_first():  # defect 6: rank 0 prepares / indexes the dataset before the others read it
+        train_ds, val_ds = _datasets(args)
     sampler, train_loader, val_loader = prepare_dataloaders(
         train_ds, val_ds, args.batch_size, args.workers, distributed=args.parallel == "ddp" and env.distributed,
         pin_memory=dev.type == "cuda", seed=args.seed)
@@ -243,7 +258,7 @@ def run_pipeline(args, env) -> None:
                     channels_last=args.channels_last, partition=args.partition)
     opt = MasterSGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
                     weight_decay=args.weight_decay)
-    sched = build_schedule(opt, args.epochs, args.warmup_epochs)
+    sched = build_schedule(opt, args.epochs, args.warmup_epochs, _lr_steps(args), args.lr_gamma)
     logger = MetricsLogger(args.log_dir, f"pipe_{args.arch}", env.rank, text_file=f"{args.batch_size}.txt")
     if env.rank == 0:
         train_ds, val_ds = _datasets(args)

@@ -44,6 +44,7 @@ class StepConfig:
     micro_batches: int = 8          # parallel == "pipe"
     schedule: str = "1f1b"          # parallel == "pipe": naive | gpipe | 1f1b
     partition: str = "balanced"     # parallel == "pipe": balanced | reference
+    checkpoint_segments: int = 0    # activation checkpointing of the block trunk (0 = off)
     extra: dict = field(default_factory=dict)
 
 
@@ -103,6 +104,9 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
     if cfg.image_size and cfg.model.startswith("vit"):
         kw["image_size"] = cfg.image_size
     model = build_model(cfg.model, **kw)
+    if cfg.checkpoint_segments > 1:
+        from ..utils.checkpointing import enable_activation_checkpointing
+        enable_activation_checkpointing(model, cfg.checkpoint_segments)
     if cfg.parallel == "syncbn":
         model = SyncBatchNorm.convert_sync_batchnorm(model)
     model = model.to(device)

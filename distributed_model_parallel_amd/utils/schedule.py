@@ -110,6 +110,39 @@ class WarmupCosine:
         self._apply()
 
 
-def build_schedule(optimizer: torch.optim.Optimizer, epochs: int, warmup_epochs: int = 10):
-    """Cosine over `epochs` (not a mismatched T_max, defect 11) + linear warm-up."""
+class WarmupMultiStep(WarmupCosine):
+    """Step decay: lr(e) = base * gamma^(number of milestones <= e) * min(1, (e+1)/warmup).
+
+    The reference's no-BN large-batch study trains with "Linear decay (at
+    30,60)" (Readme.md:170): the lr drops by ``gamma`` at epochs 30 and 60
+    (torch ``MultiStepLR`` semantics, stepped per epoch)."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer, milestones, gamma: float = 0.1,
+                 warmup_epochs: int = 0, epochs: int = 90):
+        self.milestones = sorted(int(m) for m in milestones)
+        self.gamma = float(gamma)
+        super().__init__(optimizer, epochs, warmup_epochs)
+
+    def _apply(self) -> None:
+        w = min(1.0, (self.epoch + 1) / self.warmup)
+        k = sum(1 for m in self.milestones if m <= self.epoch)
+        for g, b in zip(self.optimizer.param_groups, self.base):
+            g["lr"] = b * self.gamma ** k * w
+
+    def state_dict(self):
+        sd = super().state_dict()
+        sd.update(milestones=self.milestones, gamma=self.gamma)
+        return sd
+
+    def load_state_dict(self, sd):
+        self.milestones, self.gamma = list(sd["milestones"]), sd["gamma"]
+        super().load_state_dict(sd)
+
+
+def build_schedule(optimizer: torch.optim.Optimizer, epochs: int, warmup_epochs: int = 10,
+                   lr_steps: Optional[List[int]] = None, gamma: float = 0.1):
+    """Cosine over `epochs` (not a mismatched T_max, defect 11) + linear warm-up,
+    or step decay at ``lr_steps`` (epochs) by ``gamma`` + the same warm-up."""
+    if lr_steps:
+        return WarmupMultiStep(optimizer, lr_steps, gamma, warmup_epochs, epochs)
     return WarmupCosine(optimizer, epochs, warmup_epochs)

@@ -178,3 +178,23 @@ def test_miopen_db_entries_have_fast_solvers():
             assert any("ImplicitGemm" in s for s in names), key
             n += 1
     assert n > 0
+
+
+def _rank0_first_worker(rank, world):
+    import time
+    from distributed_model_parallel_amd.utils.debug import rank0_first
+    with rank0_first():
+        t_in = time.monotonic()
+        if rank == 0:
+            time.sleep(0.5)  # slow "preparation" on rank 0
+        t_out = time.monotonic()
+    return (t_in, t_out)
+
+
+def test_rank0_first_orders_dataset_preparation():
+    """SURVEY defect 6 (all ranks preparing ./data at once): the CLI builds its
+    datasets under rank0_first -- every other rank enters only after rank 0 left."""
+    from tests.dist_utils import run_world
+    res = run_world(_rank0_first_worker, 3)
+    r0_out = res[0][1]
+    assert all(t_in >= r0_out - 1e-3 for t_in, _ in res[1:]), res

@@ -1,0 +1,98 @@
+"""The reference's large-batch / finetune study paths:
+step LR decay at 30/60 (Readme.md:170), activation checkpointing exposed as
+--checkpoint-segments (Readme.md:168,192), and the 224-px ImageNet-stride
+MobileNetV2 of the finetune study (Readme.md:185-196)."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_model_parallel_amd.models import build_model
+from distributed_model_parallel_amd.utils.schedule import WarmupMultiStep, build_schedule
+
+
+def test_multistep_decay_at_30_60():
+    p = torch.nn.Parameter(torch.zeros(1))
+    opt = torch.optim.SGD([p], lr=0.8)
+    s = build_schedule(opt, 90, 0, lr_steps=[30, 60], gamma=0.1)
+    assert isinstance(s, WarmupMultiStep)
+    lrs = []
+    for e in range(90):
+        lrs.append(opt.param_groups[0]["lr"])
+        s.step()
+    assert lrs[0] == pytest.approx(0.8) and lrs[29] == pytest.approx(0.8)
+    assert lrs[30] == pytest.approx(0.08) and lrs[59] == pytest.approx(0.08)
+    assert lrs[60] == pytest.approx(0.008) and lrs[89] == pytest.approx(0.008)
+    # torch's MultiStepLR gives the same sequence
+    opt2 = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=0.8)
+    ref = torch.optim.lr_scheduler.MultiStepLR(opt2, [30, 60], 0.1)
+    for e in range(90):
+        assert lrs[e] == pytest.approx(opt2.param_groups[0]["lr"])
+        opt2.step()
+        ref.step()
+    # state round trip
+    sd = s.state_dict()
+    opt3 = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=0.8)
+    s3 = build_schedule(opt3, 90, 0, lr_steps=[10], gamma=0.5)
+    s3.load_state_dict(sd)
+    assert s3.milestones == [30, 60] and opt3.param_groups[0]["lr"] == pytest.approx(0.008)
+
+
+def test_multistep_with_warmup():
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=1.0)
+    s = build_schedule(opt, 90, 5, lr_steps=[3])
+    assert opt.param_groups[0]["lr"] == pytest.approx(0.2)   # epoch 0: warm-up 1/5
+    for _ in range(3):
+        s.step()
+    assert opt.param_groups[0]["lr"] == pytest.approx(0.1 * 4 / 5)  # epoch 3: decayed, warm-up 4/5
+
+
+def test_cli_parses_study_flags():
+    from distributed_model_parallel_amd.train.cli import _lr_steps, build_parser
+    a = build_parser().parse_args(["--lr-steps", "30,60", "--checkpoint-segments", "4", "--arch",
+                                   "mobilenetv2_224"])
+    assert _lr_steps(a) == [30, 60] and a.checkpoint_segments == 4 and a.lr_gamma == 0.1
+
+
+@pytest.mark.parametrize("arch,shape", [("resnet18", (2, 3, 64, 64)), ("mobilenetv2", (2, 3, 32, 32)),
+                                        ("vit_tiny", (2, 3, 32, 32))])
+def test_activation_checkpointing_matches_plain(arch, shape):
+    from distributed_model_parallel_amd.utils.checkpointing import (CheckpointedSequential,
+                                                                    enable_activation_checkpointing)
+    torch.manual_seed(0)
+    m = build_model(arch, num_classes=10).double()
+    m2 = copy.deepcopy(m)
+    assert enable_activation_checkpointing(m2, 4) >= 1
+    assert any(isinstance(x, CheckpointedSequential) for x in m2.modules())
+    x = torch.randn(*shape, dtype=torch.float64)
+    y = torch.arange(shape[0]) % 10
+    F.cross_entropy(m(x), y).backward()
+    F.cross_entropy(m2(x), y).backward()
+    for (n, a), b in zip(m.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-7, atol=1e-9, msg=n)
+    for (n, a), b in zip(m.named_buffers(), m2.buffers()):  # running stats updated once, not twice
+        torch.testing.assert_close(a, b, msg=n)
+
+
+def test_mobilenet_v2_224_architecture():
+    m = build_model("mobilenetv2_224")
+    assert sum(p.numel() for p in m.parameters()) == 3504872  # torchvision mobilenet_v2
+    m10 = build_model("mobilenetv2_224", num_classes=10)
+    m10.eval()
+    x = torch.randn(2, 3, 224, 224)
+    out = m10(x)
+    assert out.shape == (2, 10)
+    torch.testing.assert_close(m10.as_sequential()(x), out)
+    # the head pools the 7x7 map globally (the CIFAR HeadPool would crash here)
+    feats = m10.layers(torch.nn.Sequential(m10.conv1, m10.bn1)(x))
+    assert feats.shape[-2:] == (7, 7)
+
+
+def test_mobilenet_v2_224_pipeline_partition():
+    """The 224-px model cuts into pipeline stages like the CIFAR one."""
+    from distributed_model_parallel_amd.parallel.pipeline import atom_costs, balanced_partition
+    seq = build_model("mobilenetv2_224", num_classes=10).as_sequential()
+    costs = atom_costs(seq, torch.zeros(1, 3, 224, 224))
+    parts = balanced_partition(costs, 4)
+    assert len(parts) == 4 and parts[0][0] == 0 and parts[-1][1] == len(seq)
