@@ -214,6 +214,8 @@ def main() -> int:
         torch.cuda.synchronize()
     if args.phase_times:
         enable_phase_timing()
+    from distributed_model_parallel_amd.utils import routes
+    routes0 = routes.route_counts()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         with trace_range("bench.step"):
@@ -224,6 +226,8 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     elapsed = comm.max_scalar(elapsed)
     final_loss = float(loss.item())
+    step_routes = {k: round(v / args.steps, 2) for k, v in
+                   sorted(routes.diff(routes.route_counts(), routes0).items())}
     phases = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] / args.steps}
               for k, v in phase_summary().items()} if args.phase_times else None
 
@@ -284,6 +288,7 @@ def main() -> int:
             "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
             if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,
             "final_loss": round(final_loss, 4),
+            "routes_per_step": step_routes,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
             if dev.type == "cuda" else None,
         },

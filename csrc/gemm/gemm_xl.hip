@@ -202,7 +202,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   constexpr int W2 = 2 * (NA + NB);  // glds per wave per K tile
   static_assert(NA >= 1 && NB >= 1, "region smaller than one glds round");
   __shared__ __attribute__((aligned(16))) char smem[LDS];
-  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD;
+  // XL_DGELU: column sums of the output (fc1's bias gradient) when p.part is set
+  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD || EPI == XL_DGELU;
   if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
 
   const bf16* __restrict__ A = p.A;
@@ -857,6 +858,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
           v = __builtin_convertvector(f, bf16x8);
+          const f32x8 fv = __builtin_convertvector(v, f32x8);  // the stored dh, as a column sum reads it
+#pragma unroll
+          for (int j = 0; j < 8; ++j) msum[j] += fv[j];
         }
         const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
         *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
@@ -885,7 +889,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       }
     }
   }
-  if constexpr (kMom) {
+  if (kMom && (EPI != XL_DGELU || p.part)) {
     // fold the RPP row groups of each column through LDS: one partial per M tile
     static_assert(2 * RPP * BN * 4 <= LDS, "moments scratch exceeds LDS");
     __syncthreads();  // every thread finished reading the C tile
@@ -1582,6 +1586,39 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
   }
   DMP_HIP_CHECK(hipGetLastError());
   return C;
+}
+
+// dh = bf16(bf16(A @ B^T) * gelu'(aux)) (fc2's data gradient through the GELU)
+// and fc1's bias gradient sum_rows dh (fp32 [N]) from the same epilogue: the
+// column sums leave as per-M-tile partials, no separate pass over dh.
+std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tensor& B, const at::Tensor& aux) {
+  check_bf16_2d(A, "A");
+  check_bf16_2d(B, "B");
+  check_bf16_2d(aux, "aux");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && K % XBK == 0 && K >= XBK && N % 8 == 0, "gemm_xl_dgelu_bgrad: shapes");
+  TORCH_CHECK(M > 0 && M < (1LL << 31), "gemm_xl_dgelu_bgrad: M out of range");
+  TORCH_CHECK(aux.size(0) == M && aux.size(1) == N, "gemm_xl_dgelu_bgrad: aux shape");
+  auto C = at::empty({M, N}, A.options());
+  XlArgs a{};
+  a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
+  a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
+  a.C = reinterpret_cast<bf16*>(C.data_ptr()); a.ldc = C.stride(0);
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.aux = const_cast<bf16*>(reinterpret_cast<const bf16*>(aux.data_ptr())); a.ldaux = aux.stride(0);
+  a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+  const int mtiles = (int)((M + XBM - 1) / XBM);
+  const bool fused = g_xl_pipe != 6;  // the persistent ablation kernel has no column sums
+  at::Tensor part;
+  if (fused) {
+    part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
+    a.part = part.data_ptr<float>();
+  }
+  hipStream_t s = at::hip::getCurrentHIPStream();
+  dispatch_bn<XL_DGELU>(a, pick_bn((int)M, (int)N), s);
+  DMP_HIP_CHECK(hipGetLastError());
+  auto bgrad = fused ? part[0].sum(0) : C.to(at::kFloat).sum(0);
+  return {C, bgrad};
 }
 
 // bn_reduce_partials_launch: batchnorm.hip

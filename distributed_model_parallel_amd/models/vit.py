@@ -4,7 +4,8 @@ embedding, 12 pre-LN encoder blocks, LayerNorm + linear head).
 
 BASELINE.json config 5 ("ViT-B/16 DDP bf16 ... large-grad bucket fusion, MFMA
 GEMM path").  The encoder is written so that all matmuls are plain GEMMs on
-[B*T, D] activations (qkv, proj, fc1, fc2 land on hipBLASLt/MFMA) and
+[B*T, D] activations (patch embedding, qkv, proj, fc1, fc2 and every data /
+weight gradient run on the hand-written MFMA GEMMs of csrc/gemm/gemm_xl.hip) and
 attention runs on the packed-qkv HIP kernels (ops/attention.py) with no
 head split / merge copies; no per-head Python loops.
 """
@@ -21,6 +22,7 @@ from ..ops.attention import self_attention_packed
 from ..ops.fused import GradSlot, grad_tap
 from ..ops.layernorm import LayerNorm
 from ..ops.linear import Linear, linear_gelu, linear_residual, mlp_residual
+from ..ops.patch_embed import PatchEmbed
 
 
 class MLP(nn.Module):
@@ -92,7 +94,8 @@ class VisionTransformer(nn.Module):
         assert image_size % patch_size == 0
         self.patch_size = patch_size
         self.hidden_dim = hidden_dim
-        self.patch_embed = nn.Conv2d(3, hidden_dim, patch_size, stride=patch_size)
+        # 16x16 / s16 conv as one MFMA GEMM over the patches (ops/patch_embed.py)
+        self.patch_embed = PatchEmbed(3, hidden_dim, patch_size)
         n_tokens = (image_size // patch_size) ** 2 + 1
         self.cls_token = nn.Parameter(torch.zeros(1, 1, hidden_dim))
         self.pos_embedding = nn.Parameter(torch.empty(1, n_tokens, hidden_dim).normal_(std=0.02))
@@ -114,7 +117,7 @@ class VisionTransformer(nn.Module):
         nn.init.zeros_(self.head.bias)
 
     def tokens(self, x: torch.Tensor) -> torch.Tensor:
-        x = self.patch_embed(x).flatten(2).transpose(1, 2)  # [B, T, D]
+        x = self.patch_embed(x)  # [B, T, D]
         cls = self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype)
         return torch.cat([cls, x], 1) + self.pos_embedding.to(x.dtype)
 

@@ -34,7 +34,7 @@ import torch.nn.functional as F
 
 from .. import _native
 
-_STATS = {"native": 0, "torch": 0, "xl": 0, "tn_wgrad": 0}
+_STATS = {"native": 0, "torch": 0, "xl": 0, "tn_wgrad": 0, "xl_dgrad": 0, "xl_fwd": 0}
 _XL = not _native.disabled("xl_linear")
 
 
@@ -80,8 +80,25 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor
     return dy2.t().mm(x2)
 
 
+def _xl_gemm_ok(a: torch.Tensor, n: int) -> bool:
+    """C[M, n] = a @ B^T on gemm_xl: bf16 operand contract, K % 64, n % 64,
+    and enough rows to fill the 256-row tile grid."""
+    return (_XL and a.is_cuda and _native.native() is not None and a.shape[0] >= _XL_MIN_ROWS
+            and a.shape[1] % 64 == 0 and n % 64 == 0 and _gemm_operand_ok(a))
+
+
+def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy @ W on the ping-pong MFMA GEMM (B operand = W^T [in, out], a
+    transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16) instead of
+    hipBLASLt (the data gradients were 17 % of the ViT step)."""
+    if w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
+        _STATS["xl_dgrad"] += 1
+        return _native.native().gemm_xl(dy2, w.t().contiguous())
+    return dy2.mm(w)
+
+
 def _weight_grads(ctx, dy2, x2, w):
-    dx = dy2.mm(w) if ctx.needs_input_grad[0] else None
+    dx = _dgrad(dy2, w) if ctx.needs_input_grad[0] else None
     dw = _wgrad(dy2, x2, w) if ctx.needs_input_grad[1] else None
     return dx, dw
 
@@ -90,7 +107,11 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t())
+        if _xl_gemm_ok(x2, w.shape[0]):  # the qkv projection: bias in the MFMA GEMM's store
+            _STATS["xl_fwd"] += 1
+            y = _native.native().gemm_xl(x2, w, "bias", bias=b)
+        else:
+            y = torch.addmm(b, x2, w.t())
         ctx.save_for_backward(x2, w)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -182,7 +203,7 @@ class _LinearResidualFn(torch.autograd.Function):
         x2, w = ctx.saved_tensors
         C = _native.require("linear_residual backward")
         dy2 = _rows(dy)
-        dx = dy2.mm(w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = _dgrad(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         dw = _wgrad(dy2, x2, w) if ctx.needs_input_grad[2] else None
         db = C.bias_grad(dy2, w.dtype) if ctx.needs_input_grad[3] else None
         return dx, dy, dw, db
@@ -211,10 +232,11 @@ class _MLPResidualFn(torch.autograd.Function):
         db2 = C.bias_grad(dy2, w2.dtype)
         dw2 = _wgrad(dy2, a, w2)
         # dh = bf16(bf16(dy @ W2) * gelu'(h)): B operand is W2^T [hidden, dim]
-        dh = C.gemm_xl(dy2, w2.t().contiguous(), "dgelu", aux=h)
-        db1 = C.bias_grad(dh, w1.dtype)
+        # and fc1's bias gradient (column sums of dh) from the same epilogue
+        dh, db1 = C.gemm_xl_dgelu_bgrad(dy2, w2.t().contiguous(), h)
+        db1 = db1.to(w1.dtype)
         dw1 = _wgrad(dh, x2, w1)
-        dx = dh.mm(w1)
+        dx = _dgrad(dh, w1)
         return dx.view(ctx.xshape), dy, dw1, db1, dw2, db2
 
 

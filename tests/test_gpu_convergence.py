@@ -177,3 +177,125 @@ def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, l
     # and both end on the same plateau
     a, b = _mean(l_nat[-k:]), _mean(l_ref[-k:])
     assert abs(a - b) <= 0.25 * max(a, b) + 0.05, (a, b)
+
+
+class _Templates:
+    """A harder, 224-px task: ``ncls`` low-frequency class templates plus heavy
+    noise, batches drawn deterministically per step (both runs see the same
+    data), so the loss plateaus well above zero within the run and a subtly
+    wrong gradient shows as a slower / higher curve."""
+
+    def __init__(self, ncls, size, noise, seed=3):
+        g = torch.Generator().manual_seed(seed)
+        t = torch.randn(ncls, 3, 8, 8, generator=g)
+        t = F.interpolate(t, size=(size, size), mode="bilinear", align_corners=False)
+        self.t = t / t.std(dim=(1, 2, 3), keepdim=True)
+        self.ncls, self.noise, self.seed = ncls, noise, seed
+
+    def batch(self, i, n):
+        g = torch.Generator().manual_seed(self.seed * 100003 + i)
+        y = torch.randint(0, self.ncls, (n,), generator=g)
+        return self.t[y] + self.noise * torch.randn(n, *self.t.shape[1:], generator=g), y
+
+
+def _train_native_fn(model, data, steps, batch, lr):
+    from distributed_model_parallel_amd.ops.loss import cross_entropy
+    from distributed_model_parallel_amd.ops.optim import FlatSGD
+    from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
+    from distributed_model_parallel_amd.utils.precision import cast_model
+    _ensure_pg()
+    m = model.cuda().to(memory_format=torch.channels_last)
+    cast_model(m, torch.bfloat16)
+    ddp = DistributedDataParallel(m, flat_parameters=True)
+    opt = FlatSGD(ddp, lr=lr, momentum=0.9, weight_decay=5e-4)
+    losses = []
+    for i in range(steps):
+        for g in opt.param_groups:
+            g["lr"] = _lr(lr, i)
+        x, y = data.batch(i, batch)
+        loss = cross_entropy(ddp(x.cuda().bfloat16().contiguous(memory_format=torch.channels_last)), y.cuda())
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        losses.append(loss.detach().float())
+    return [float(v) for v in torch.stack(losses).cpu()]
+
+
+def _train_reference_fn(model, data, steps, batch, lr):
+    m = model.cuda()
+    opt = torch.optim.SGD(m.parameters(), lr=lr, momentum=0.9, weight_decay=5e-4)
+    losses = []
+    with _native.reference_mode():
+        for i in range(steps):
+            for g in opt.param_groups:
+                g["lr"] = _lr(lr, i)
+            x, y = data.batch(i, batch)
+            loss = F.cross_entropy(m(x.cuda()), y.cuda())
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.detach())
+    return [float(v) for v in torch.stack(losses).cpu()]
+
+
+def _bench_routes(steps=2):
+    """The kernel routes of the headline bench step (bench.py defaults:
+    ResNet-50, DDP, bf16, channels-last, 2048 images, 224 px)."""
+    from distributed_model_parallel_amd.train.step import StepConfig, build_train_state
+    from distributed_model_parallel_amd.utils import routes
+    st = build_train_state(StepConfig(model="resnet50", batch_size=2048), torch.device("cuda", 0))
+    st.step()
+    r0 = routes.route_counts()
+    for _ in range(steps):
+        st.step()
+    torch.cuda.synchronize()
+    out = routes.active(routes.diff(routes.route_counts(), r0))
+    del st
+    torch.cuda.empty_cache()
+    return out
+
+
+def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
+    """ResNet-50 at 224 px (the bench's kernel routing:
+    stem_halo, halo c64/c128 forward / dgrad / wgrad, stride-phase dgrads,
+    the BN fold with and without the downsample), on a task that does not
+    saturate.  Every route the bench's timed steps take must also have run in
+    this training run, and the native bf16 curve must track stock fp32."""
+    from distributed_model_parallel_amd.utils import routes
+    steps, batch, lr, ncls = 160, 64, 0.02, 100
+    data = _Templates(ncls, 224, noise=4.0)
+    torch.manual_seed(0)
+    base = build_model("resnet50", num_classes=ncls)
+    ref0 = copy.deepcopy(base)
+    r0 = routes.route_counts()
+    l_nat = _train_native_fn(base, data, steps, batch, lr)
+    trained = routes.active(routes.diff(routes.route_counts(), r0))
+    del base
+    torch.cuda.empty_cache()
+    l_ref = _train_reference_fn(ref0, data, steps, batch, lr)
+    del ref0
+    torch.cuda.empty_cache()
+    bench = _bench_routes()
+    out = os.environ.get("DMP_CONVERGENCE_OUT")
+    if out:
+        rec = {}
+        if os.path.exists(out):
+            with open(out) as f:
+                rec = json.load(f)
+        rec["resnet50_224"] = {"native_bf16": l_nat, "stock_fp32": l_ref, "steps": steps, "batch": batch, "lr": lr,
+                               "classes": ncls, "noise": 4.0, "routes_trained": trained, "routes_bench": bench}
+        with open(out, "w") as f:
+            json.dump(rec, f)
+    miss = routes.missing(bench, trained)
+    assert not miss, f"bench kernel routes never trained here: {miss}"
+    k = 20
+    l0 = _mean(l_ref[:5])
+    a, b = _mean(l_nat[-k:]), _mean(l_ref[-k:])
+    # the task is learned but not saturated: the plateau stays well above zero
+    assert b < 0.9 * l0 and b > 0.1 * l0, (l0, b)
+    # native tracks stock: same plateau, and no lag in reaching 95 / 90 % of the start
+    assert abs(a - b) <= 0.1 * b + 0.05, (a, b)
+    for frac in (0.95, 0.9):
+        sn, sr = _steps_to(l_nat, frac * l0), _steps_to(l_ref, frac * l0)
+        if sr is not None:
+            assert sn is not None and sn <= 1.25 * sr + 8, (frac, sn, sr)

@@ -104,3 +104,70 @@ def test_weight_grads_on_tn_kernel_match_fp32(monkeypatch, xl):
     for got, ref in ((fc1.weight.grad, w1.grad), (fc2.weight.grad, w2.grad)):
         err = ((got.float() - ref).norm() / ref.norm()).item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("T", [50432, 1000])
+def test_dgelu_epilogue_bias_grad(T):
+    """fc1's bias gradient as column sums from fc2's data-gradient epilogue
+    (gemm_xl_dgelu_bgrad) vs an fp32 reference of the same math."""
+    from distributed_model_parallel_amd import _native
+    C = _native.require("test")
+    torch.manual_seed(3)
+    D, H = 768, 3072
+    dy = torch.randn(T, D, device=DEV).bfloat16()
+    w2t = (torch.randn(H, D, device=DEV) * 0.05).bfloat16()
+    h = torch.randn(T, H, device=DEV).bfloat16()
+    dh, db = C.gemm_xl_dgelu_bgrad(dy, w2t, h)
+    assert torch.equal(dh, C.gemm_xl(dy, w2t, "dgelu", aux=h))
+    torch.testing.assert_close(db, dh.float().sum(0), atol=1e-2 * T ** 0.5, rtol=1e-4)
+    hf = h.float()
+    ref = (dy.float() @ w2t.float().t()) * (0.5 * (1 + torch.erf(hf / 2 ** 0.5)) +
+                                             hf * torch.exp(-0.5 * hf * hf) / (2 * torch.pi) ** 0.5)
+    assert ((db - ref.sum(0)).norm() / ref.sum(0).norm()).item() < 1e-2
+
+
+def test_qkv_linear_forward_and_dgrad_on_xl():
+    """The qkv projection (ops.linear.linear -> _LinearFn): forward with the
+    bias in gemm_xl's store and the data gradient on gemm_xl (no hipBLASLt)."""
+    torch.manual_seed(4)
+    T, D = 8192, 768
+    qkv = nn.Linear(D, 3 * D).to(DEV).bfloat16()
+    x = torch.randn(T, D, device=DEV).bfloat16()
+    (xb,) = _leaves(x)
+    f0, d0 = L._STATS["xl_fwd"], L._STATS["xl_dgrad"]
+    y = L.linear(xb, qkv.weight, qkv.bias)
+    assert L._STATS["xl_fwd"] == f0 + 1
+    xf, w, b = _leaves(x.float(), qkv.weight.float(), qkv.bias.float())
+    yr = F.linear(xf, w, b)
+    torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    assert L._STATS["xl_dgrad"] == d0 + 1
+    torch.testing.assert_close(xb.grad.float(), xf.grad, atol=0.05 * (3 * D) ** 0.5 / 8, rtol=3e-2)
+    err = ((qkv.weight.grad.float() - w.grad).norm() / w.grad.norm()).item()
+    assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("B", [32, 3])
+def test_patch_embed_gemm_matches_conv(B):
+    """16x16/s16 patch embedding as one GEMM (ops/patch_embed.py) vs the fp32
+    convolution: tokens, weight and bias gradients (B = 3: 588 rows -> torch path)."""
+    from distributed_model_parallel_amd.ops import patch_embed as P
+    torch.manual_seed(5)
+    pe = P.PatchEmbed(3, 768, 16).to(DEV).bfloat16().to(memory_format=torch.channels_last)
+    x = torch.randn(B, 3, 224, 224, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    n0 = P._STATS["native"]
+    y = pe(x)
+    assert y.shape == (B, 196, 768)
+    if B * 196 >= L._XL_MIN_ROWS:
+        assert P._STATS["native"] == n0 + 1
+    w, b = _leaves(pe.weight.float(), pe.bias.float())
+    yr = F.conv2d(x.float(), w, b, stride=16).flatten(2).transpose(1, 2)
+    torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=2e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    yr.backward(g)
+    err = ((pe.weight.grad.float() - w.grad).norm() / w.grad.norm()).item()
+    assert err < 2e-2, err
+    torch.testing.assert_close(pe.bias.grad.float(), b.grad, atol=0.02 * (B * 196) ** 0.5, rtol=3e-2)
