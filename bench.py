@@ -136,6 +136,9 @@ def main() -> int:
                     help="--parallel dp: replicas per GPU; K>1 aliases K replicas onto each device so "
                          "scatter / replicate / parallel_apply / gather / reduce-add all execute even "
                          "on one GPU (the per-GPU batch is split K ways)")
+    ap.add_argument("--dp-graphs", action="store_true",
+                    help="--parallel dp: run every replica's forward / backward as captured hipGraphs "
+                         "(parallel/dp_graphs.py) instead of Python threads")
     ap.add_argument("--phase-times", action="store_true",
                     help="record HIP events around the DataParallel phases and report their GPU "
                          "ms per step in the JSON (config.phase_ms_per_step)")
@@ -188,7 +191,7 @@ def main() -> int:
                      dp_replicas=args.dp_replicas, graph=args.graph,
                      lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1),
                      micro_batches=args.micro_batches, schedule=args.schedule, partition=args.partition,
-                     checkpoint_segments=args.checkpoint_segments)
+                     checkpoint_segments=args.checkpoint_segments, dp_graphs=args.dp_graphs)
     if args.parallel == "dp" and env.world_size > 1:
         raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
                          "--gpus N` without torchrun")
@@ -266,7 +269,7 @@ def main() -> int:
             "seq_len": None,
             "image_size": image_size,
             "parallelism": f"{par}{n}",
-            **({"dp_replicas_per_gpu": args.dp_replicas,
+            **({"dp_replicas_per_gpu": args.dp_replicas, "dp_graphs": args.dp_graphs,
                 "dp_device_ids": getattr(st.wrapped, "device_ids", None)} if args.parallel == "dp" else {}),
             **({"phase_ms_per_step": phases} if phases is not None else {}),
             "single_rank_comm": bool(args.single_rank_comm),

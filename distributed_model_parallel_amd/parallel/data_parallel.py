@@ -439,11 +439,16 @@ class DataParallel(nn.Module):
     """Drop-in ``nn.DataParallel`` over the native scatter/replicate/gather kernels."""
 
     def __init__(self, module: nn.Module, device_ids: Optional[Sequence[int]] = None,
-                 output_device: Optional[int] = None, dim: int = 0):
+                 output_device: Optional[int] = None, dim: int = 0, graphs: bool = False):
         super().__init__()
         self.module = module
         self.dim = dim
         self._replicas: Dict = {}  # per-instance replica skeletons (see _Skeleton)
+        # graphs=True: replicas as captured hipGraphs (parallel/dp_graphs.py) for
+        # training steps with one tensor input of a fixed per-replica shape
+        self.graphs = bool(graphs)
+        self._graphed = None
+        self._graphed_sig = None
         if not torch.cuda.is_available():
             self.device_ids: List[int] = []
             self.output_device = None
@@ -468,6 +473,8 @@ class DataParallel(nn.Module):
     def forward(self, *inputs, **kwargs):
         if not self.device_ids:
             return self.module(*inputs, **kwargs)
+        if len(self.device_ids) > 1 and self._graph_ok(inputs, kwargs):
+            return self._graphed_forward(inputs[0])
         # roctx ranges (rocprofv3 --marker-trace): the four phases upstream DP
         # wraps in record_function("DataParallel.forward")
         with phase("dp.scatter"):
@@ -491,6 +498,26 @@ class DataParallel(nn.Module):
 
     def replicate(self, module, device_ids):
         return replicate(module, device_ids, not torch.is_grad_enabled(), cache=self._replicas)
+
+    # ---- graphed replicas ------------------------------------------------------
+    def _graph_ok(self, inputs, kwargs) -> bool:
+        return (self.graphs and self.training and torch.is_grad_enabled() and not kwargs
+                and len(inputs) == 1 and isinstance(inputs[0], torch.Tensor) and inputs[0].is_cuda
+                and self.dim == 0 and inputs[0].shape[0] % len(self.device_ids) == 0)
+
+    def _graphed_forward(self, x: torch.Tensor) -> torch.Tensor:
+        from .dp_graphs import GraphedReplicas, graphed_forward
+        with phase("dp.scatter"):
+            chunks = comm_ops.scatter_tensor(x.detach(), self.device_ids, 0)
+        sig = (_Skeleton.signature(self.module), tuple(tuple(c.shape) for c in chunks))
+        if self._graphed is None or self._graphed_sig != sig or not self._graphed.matches(chunks):
+            self._graphed = None
+            torch.cuda.synchronize()
+            self._graphed = GraphedReplicas(self.module, [torch.device("cuda", d) for d in
+                                                          self.device_ids[:len(chunks)]], chunks[0])
+            self._graphed_sig = sig
+        with phase("dp.graph_replay"):
+            return graphed_forward(self._graphed, chunks, self.output_device)
 
     def invalidate_replicas(self) -> None:
         """Drop the cached replica skeletons (they are rebuilt on the next forward)."""

@@ -50,6 +50,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--arch", default="mobilenetv2")
     p.add_argument("--parallel", default="ddp", choices=["ddp", "dp", "pipe", "none"])
     p.add_argument("--bucket-cap-mb", default=25.0, type=float)
+    p.add_argument("--dp-graphs", action="store_true",
+                   help="--parallel dp: replicas' forward/backward as captured hipGraphs (no replica threads)")
     p.add_argument("--sync-bn", action="store_true")
     p.add_argument("--dtype", default="auto", choices=["auto", "fp32", "bf16"],
                    help="auto: bf16 (fp32 master weights) on GPU -- the native MFMA path -- fp32 on CPU")
@@ -137,7 +139,7 @@ def run_data_parallel(args, env) -> None:
         # fp32 master weights for bf16 models: same update as DDP's FlatSGD
         opt = MasterSGD(model.parameters(), lr=args.lr, momentum=args.momentum,
                         weight_decay=args.weight_decay)
-        net = DataParallel(model) if args.parallel == "dp" else model
+        net = DataParallel(model, graphs=args.dp_graphs) if args.parallel == "dp" else model
     sched = build_schedule(opt, args.epochs, args.warmup_epochs, _lr_steps(args), args.lr_gamma)
     from ..utils.debug import rank0_first
     with rank0_first():  # defect 6: rank 0 prepares / indexes the dataset before the others read it

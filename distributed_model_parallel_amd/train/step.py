@@ -45,6 +45,7 @@ class StepConfig:
     schedule: str = "1f1b"          # parallel == "pipe": naive | gpipe | 1f1b
     partition: str = "balanced"     # parallel == "pipe": balanced | reference
     checkpoint_segments: int = 0    # activation checkpointing of the block trunk (0 = off)
+    dp_graphs: bool = False         # parallel == "dp": replicas as captured hipGraphs (dp_graphs.py)
     extra: dict = field(default_factory=dict)
 
 
@@ -139,7 +140,7 @@ def _build_train_state(cfg: StepConfig, device: torch.device) -> TrainState:
                         weight_decay=cfg.weight_decay)
         reps = max(1, cfg.dp_replicas)
         wrapped = DataParallel(model, device_ids=[d for d in range(ndp) for _ in range(reps)]
-                               if device.type == "cuda" else None)
+                               if device.type == "cuda" else None, graphs=cfg.dp_graphs)
 
         def step() -> torch.Tensor:
             out = wrapped(x)

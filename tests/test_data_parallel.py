@@ -280,3 +280,48 @@ def test_replica_cache_attrs_concurrency_and_lifetime():
     del m, r1, r2, r3, held, cache
     gc.collect()
     assert ref() is None, "the replica cache kept the network alive"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_dp_graphed_replicas_match_eager(arch):
+    """DataParallel(graphs=True) (parallel/dp_graphs.py: static replicas whose
+    forward / backward are captured hipGraphs) against the eager thread path:
+    outputs, parameter gradients and running statistics over three steps with
+    optimizer updates between them (the replicas must re-read the updated
+    weights every step)."""
+    import copy as _copy
+    from distributed_model_parallel_amd.models import build_model
+    from distributed_model_parallel_amd.ops.loss import cross_entropy
+    from distributed_model_parallel_amd.utils.precision import cast_model
+    torch.manual_seed(0)
+    base = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
+    cast_model(base, torch.bfloat16)
+    m_e, m_g = base, _copy.deepcopy(base)
+    dp_e = DataParallel(m_e, device_ids=[0, 0, 0, 0])
+    dp_g = DataParallel(m_g, device_ids=[0, 0, 0, 0], graphs=True)
+    opt_e = torch.optim.SGD(m_e.parameters(), lr=0.05)
+    opt_g = torch.optim.SGD(m_g.parameters(), lr=0.05)
+    for step in range(3):
+        x = torch.randn(16, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        y = torch.arange(16, device="cuda") % 10
+        outs = []
+        for dp, opt in ((dp_e, opt_e), (dp_g, opt_g)):
+            out = dp(x)
+            cross_entropy(out, y).backward()
+            outs.append(out.float())
+        torch.testing.assert_close(outs[1], outs[0], atol=3e-2, rtol=3e-2)
+        num = den = 0.0
+        for a, b in zip(m_e.parameters(), m_g.parameters()):
+            num += (a.grad.float() - b.grad.float()).pow(2).sum().item()
+            den += a.grad.float().pow(2).sum().item()
+        assert (num / den) ** 0.5 < 3e-2, (step, (num / den) ** 0.5)
+        for opt in (opt_e, opt_g):
+            opt.step()
+            opt.zero_grad()
+    assert dp_g._graphed is not None, "graphed path not taken"
+    for (n, a), b in zip(m_e.named_buffers(), m_g.buffers()):
+        if a.dtype.is_floating_point:
+            torch.testing.assert_close(b.float(), a.float(), atol=3e-2, rtol=3e-2, msg=n)
+        else:
+            assert torch.equal(a, b), n
