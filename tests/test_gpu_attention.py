@@ -61,3 +61,22 @@ def test_attention_matches_sdpa_path_in_vit_block():
     got = blk.attn(h)
     torch.testing.assert_close(got.float(), ref.float(), atol=3e-2, rtol=3e-2)
     assert torch.isfinite(y).all()
+
+
+def test_persistent_forward_equals_per_head_forward():
+    """The persistent forward (next-head K / V / Q prefetch) computes exactly
+    what the one-workgroup-per-head kernel computes (same MFMA order)."""
+    from distributed_model_parallel_amd import _native
+    C = _native.require("attention")
+    torch.manual_seed(9)
+    B, S, H = 40, 197, 12  # 480 heads: fewer and more than 2 x CUs per wave of the grid
+    qkv = torch.randn(B * S, 3 * H * 64, device="cuda").bfloat16()
+    try:
+        C.set_attention_variant(0)
+        o0, l0 = C.attention_forward(qkv, B, S, H, 0.125)
+        C.set_attention_variant(1)
+        o1, l1 = C.attention_forward(qkv, B, S, H, 0.125)
+    finally:
+        C.set_attention_variant(1)
+    assert torch.equal(o0, o1)
+    assert torch.equal(l0[:, :S], l1[:, :S])

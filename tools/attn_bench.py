@@ -37,7 +37,16 @@ def main():
     B, S, H = int(os.environ.get("B", 128)), 197, 12
     qkv = torch.randn(B, S, 3 * H * 64, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     go = torch.randn(B, S, H * 64, device="cuda", dtype=torch.bfloat16)
-    for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("packed hip", lambda: A.self_attention_packed(qkv, H))):
+    from distributed_model_parallel_amd import _native
+    C = _native.require("attn bench")
+
+    def variant(v):
+        def f():
+            C.set_attention_variant(v)
+            return A.self_attention_packed(qkv, H)
+        return f
+    for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("hip per-head", variant(0)),
+                     ("hip persistent", variant(1))):
         tf = timeit(lambda: fn())
         o = fn()
         tb = timeit(lambda: torch.autograd.grad(o, qkv, go, retain_graph=True))
