@@ -71,15 +71,15 @@ __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
 // images.  Every global load of both images is issued before the first LDS
 // store (SP*16/256 16-B loads in flight per lane instead of one): the staging
 // is the latency-bound head of both kernels.
-template <int SP>
+template <int SP, int NT = kThreads>
 __device__ __forceinline__ void stage2(bf16* dst0, const bf16* src0, int64_t ld0, bf16* dst1,
                                        const bf16* src1, int64_t ld1, int S) {
   constexpr int PER = SP * (DH / 8);
-  constexpr int IT = (PER + kThreads - 1) / kThreads;
+  constexpr int IT = (PER + NT - 1) / NT;
   bf16x8 r0[IT], r1[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int v = threadIdx.x + i * kThreads;
+    const int v = threadIdx.x + i * NT;
     const int r = v >> 3, c = (v & 7) * 8;
     const bool ok = v < PER && r < S;
     r0[i] = ok ? *reinterpret_cast<const bf16x8*>(src0 + (int64_t)r * ld0 + c) : bf16x8{};
@@ -87,7 +87,7 @@ __device__ __forceinline__ void stage2(bf16* dst0, const bf16* src0, int64_t ld0
   }
 #pragma unroll
   for (int i = 0; i < IT; ++i) {
-    const int v = threadIdx.x + i * kThreads;
+    const int v = threadIdx.x + i * NT;
     if (v < PER) {
       const int r = v >> 3, c = (v & 7) * 8;
       *reinterpret_cast<bf16x8*>(dst0 + r * LROW + c) = r0[i];
@@ -101,8 +101,8 @@ __device__ __forceinline__ void store4(bf16* p, const f32x4& v, float s) {
   *reinterpret_cast<bf16x4*>(p) = o;
 }
 
-template <int SP>
-__global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, int64_t ld,
+template <int SP, int NW = 4>
+__global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, int64_t ld,
                                                             int S, int H, float scale,
                                                             bf16* __restrict__ o, int64_t ldo,
                                                             float* __restrict__ lse) {
@@ -116,24 +116,23 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_kernel(const bf16* __res
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int nqt = (S + 15) / 16;
-  // This wave's query tiles are wave, wave + 4, ...: their Q fragments are
+  // This wave's query tiles are wave, wave + NW, ...: their Q fragments are
   // loaded up front, in flight together with the K / V staging, instead of one
-  // dependent global load at the head of every tile (the tile loop was bound
-  // by those round trips, ~10 % of MFMA peak in round 3).
-  constexpr int MAXT = (SP / 16 + 3) / 4;
+  // dependent global load at the head of every tile.
+  constexpr int MAXT = (SP / 16 + NW - 1) / NW;
   bf16x8 qf[MAXT][2];
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) {
-    const int qc = min((wave + 4 * i) * 16 + li, S - 1);
+    const int qc = min((wave + NW * i) * 16 + li, S - 1);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) qf[i][ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)qc * ld + ks * 32 + g * 8);
   }
-  stage2<SP>(Ks, qb + D, ld, Vs, qb + 2 * D, ld, S);
+  stage2<SP, NW * 64>(Ks, qb + D, ld, Vs, qb + 2 * D, ld, S);
   __syncthreads();
   const float sl2 = scale * kLog2e;
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) {
-    const int qt = wave + 4 * i;
+    const int qt = wave + NW * i;
     if (qt >= nqt) break;
     const int q = qt * 16 + li;
     f32x4 st[NKT];
@@ -494,12 +493,13 @@ void check_2d(const at::Tensor& t, const char* name, int64_t rows, int64_t min_c
 bool attention_supported(int64_t S, int64_t head_dim) { return head_dim == DH && S >= 1 && S <= 256; }
 
 namespace {
-int g_attn_fwd_variant = 1;  // 0: one workgroup per (batch, head); 1: persistent with next-head prefetch
+int g_attn_fwd_variant = 1;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
+                             // next-head prefetch; 2: one 8-wave workgroup per (batch, head)
 int g_num_cus_attn = 0;
 }  // namespace
 
 void set_attention_variant(int fwd) {
-  TORCH_CHECK(fwd == 0 || fwd == 1, "attention forward variant: 0 (per head) or 1 (persistent)");
+  TORCH_CHECK(fwd >= 0 && fwd <= 2, "attention forward variant: 0 (per head), 1 (persistent), 2 (per head, 8 waves)");
   g_attn_fwd_variant = fwd;
 }
 
@@ -523,6 +523,11 @@ std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int6
                                              (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,
                                              (float)scale, (bf16*)o.data_ptr(), o.stride(0),
                                              lse.data_ptr<float>(), nbh));
+  } else if (g_attn_fwd_variant == 2) {
+    DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_fwd_kernel<SPC, 8>), dim3(B * H), dim3(512), 0, st,
+                                             (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,
+                                             (float)scale, (bf16*)o.data_ptr(), o.stride(0),
+                                             lse.data_ptr<float>()));
   } else {
     DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_fwd_kernel<SPC>), dim3(B * H), dim3(kThreads), 0, st,
                                              (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,

@@ -76,7 +76,9 @@ def test_persistent_forward_equals_per_head_forward():
         o0, l0 = C.attention_forward(qkv, B, S, H, 0.125)
         C.set_attention_variant(1)
         o1, l1 = C.attention_forward(qkv, B, S, H, 0.125)
+        C.set_attention_variant(2)
+        o2, l2 = C.attention_forward(qkv, B, S, H, 0.125)
     finally:
         C.set_attention_variant(1)
-    assert torch.equal(o0, o1)
-    assert torch.equal(l0[:, :S], l1[:, :S])
+    assert torch.equal(o0, o1) and torch.equal(o0, o2)
+    assert torch.equal(l0[:, :S], l1[:, :S]) and torch.equal(l0[:, :S], l2[:, :S])

@@ -46,7 +46,7 @@ def main():
             return A.self_attention_packed(qkv, H)
         return f
     for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("hip per-head", variant(0)),
-                     ("hip persistent", variant(1))):
+                     ("hip persistent", variant(1)), ("hip 8-wave", variant(2))):
         tf = timeit(lambda: fn())
         o = fn()
         tb = timeit(lambda: torch.autograd.grad(o, qkv, go, retain_graph=True))
