@@ -312,3 +312,59 @@ def test_relu_mask_colsum_kernel(rows, c):
     torch.testing.assert_close(s[:c], rd.sum(0), atol=1e-3 * rows ** 0.5, rtol=1e-5)
     torch.testing.assert_close(s[c:2 * c], (rd * rd).sum(0), atol=1e-3 * rows ** 0.5, rtol=1e-5)
     assert s[2 * c].item() == rows
+
+
+@pytest.mark.parametrize("positive_w", [False, True], ids=["randn_w", "positive_w"])
+def test_fold_statistics_at_headline_rows(positive_w):
+    """the fold's BN3 statistics come from E[y^2] - E[y]^2
+    over an fp32 Gram matrix accumulated across M = 2048 * 56 * 56 = 6.4 M rows
+    (layer 1 of the batch-2048 bench).  Post-ReLU inputs (large mean / std)
+    and -- the adversarial case -- all-positive weights give y a mean far
+    above its spread, where the subtraction amplifies the Gram's fp32 error.
+    The running statistics the fold writes must match an fp64 reference over
+    the same bf16 operands."""
+    torch.manual_seed(11)
+    n, cin, cout, h = 2048, 64, 256, 56
+    conv = Conv1x1(cin, cout).to(DEV).bfloat16()
+    with torch.no_grad():
+        w = torch.randn(cout, cin, 1, 1, device=DEV) * 0.2
+        conv.weight.copy_(w.abs() if positive_w else w)
+    conv = conv.to(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(cout, act="relu").to(DEV)  # fp32 running stats, bf16-free affine
+    bn.weight.data = bn.weight.data.bfloat16()
+    bn.bias.data = bn.bias.data.bfloat16()
+    a = torch.relu(torch.randn(n, cin, h, h, device=DEV, dtype=torch.bfloat16) + 0.5)
+    a = a.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    a2 = a.detach().permute(0, 2, 3, 1).reshape(-1, cin)
+    # fp64 reference moments of the bf16 operands, chunked (6.4 M x 256 doubles would be 13 GB)
+    W = conv.weight.detach().reshape(cout, cin).double()
+    s1 = torch.zeros(cout, dtype=torch.float64, device=DEV)
+    s2 = torch.zeros(cout, dtype=torch.float64, device=DEV)
+    asum = torch.zeros(cin, dtype=torch.float64, device=DEV)
+    asq = torch.zeros(cin, dtype=torch.float64, device=DEV)
+    for r in range(0, a2.shape[0], 1 << 20):
+        blk = a2[r:r + (1 << 20)].double()
+        asum += blk.sum(0)
+        asq += (blk * blk).sum(0)
+        y = blk @ W.t()
+        s1 += y.sum(0)
+        s2 += (y * y).sum(0)
+    m_rows = a2.shape[0]
+    mean = s1 / m_rows
+    var = s2 / m_rows - mean * mean
+    a_sums = torch.cat([asum, asq, asum.new_tensor([float(m_rows)])])
+    f0 = bn_fold.stats()["fold"]
+    out = bn_fold.conv1x1_bn_fold(conv, bn, a, a_sums)
+    assert bn_fold.stats()["fold"] == f0 + 1, "fold did not run"
+    rm_ref = 0.1 * mean
+    rv_ref = 0.9 + 0.1 * var * m_rows / (m_rows - 1)
+    torch.testing.assert_close(bn.running_mean.double(), rm_ref, rtol=1e-4, atol=1e-5)
+    rel_var = ((bn.running_var.double() - 0.9) / (rv_ref - 0.9) - 1).abs().max().item()
+    ratio = (mean * mean / var).max().item()
+    assert rel_var < 2e-3, f"variance relative error {rel_var:.2e} (max mean^2/var {ratio:.0f})"
+    # and the normalised output of a sample of rows matches the fp64 statistics
+    rows = torch.arange(0, m_rows, 9973, device=DEV)
+    y = (a2[rows].double() @ W.t())
+    ref = torch.relu((y - mean) / torch.sqrt(var + bn.eps) * bn.weight.double() + bn.bias.double())
+    got = out.permute(0, 2, 3, 1).reshape(-1, cout)[rows].double()
+    assert ((got - ref).norm() / ref.norm()).item() < 1e-2
