@@ -205,13 +205,18 @@ def main() -> int:
     image_size = args.image_size or img_h
 
     t_warm0 = time.time()
+    first_step_ms = None
     for i in range(args.warmup):
         ts = time.perf_counter()
         loss = st.step()
-        if (i == 0 or args.trace_steps) and env.is_main:
+        if i == 0 or (args.trace_steps and env.is_main):
             torch.cuda.synchronize() if dev.type == "cuda" else None
-            print(f"[bench] warmup step {i} {1e3 * (time.perf_counter() - ts):.1f} ms "
-                  f"(t={time.time() - t_warm0:.1f}s) loss={loss.item():.4f}", file=sys.stderr, flush=True)
+            ms = 1e3 * (time.perf_counter() - ts)
+            if i == 0:
+                first_step_ms = ms
+            if env.is_main:
+                print(f"[bench] warmup step {i} {ms:.1f} ms (t={time.time() - t_warm0:.1f}s) "
+                      f"loss={loss.item():.4f}", file=sys.stderr, flush=True)
     comm.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -290,6 +295,10 @@ def main() -> int:
             "watchdog_s": wd,
             "gemm_tuning": os.path.relpath(tuning_file, os.path.dirname(os.path.abspath(__file__)))
             if tuning_file else args.gemm_tuning if args.gemm_tuning != "use" else None,
+            # the untimed first step pays MIOpen's solver search for the convs still on
+            # MIOpen unless its find db is seeded from profiles/miopen/ (utils/miopen_db.py)
+            "miopen_db": args.miopen_db if dev.type == "cuda" else None,
+            "first_step_ms": round(first_step_ms, 1) if first_step_ms is not None else None,
             "final_loss": round(final_loss, 4),
             "routes_per_step": step_routes,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
