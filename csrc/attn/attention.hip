@@ -302,6 +302,179 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_pp_kernel(const bf16* __
   }
 }
 
+// ---- backward building blocks (shared by the per-head and persistent kernels) ----
+template <int SP>
+struct BwdCtx {
+  static constexpr int MAXT = (SP / 16 + 3) / 4;
+  int S, D, lane, wave, g, li, nt;
+  float scale, sl2;
+};
+
+// D_i = sum_d dO[i][d] * O[i][d] (fp32, O from global, dO from the LDS image)
+// and the saved base-2 logsumexp, into LDS
+template <int SP>
+__device__ __forceinline__ void bwd_rowstats(const BwdCtx<SP>& c, const bf16* dOs, const bf16* o, int64_t ldo,
+                                             const float* lse, int b, int h, int bh, float* lse_s, float* dd_s) {
+  for (int r = threadIdx.x; r < SP; r += kThreads) {
+    float acc = 0.f;
+    if (r < c.S) {
+      const bf16* orow = o + ((int64_t)b * c.S + r) * ldo + h * DH;
+#pragma unroll
+      for (int cc = 0; cc < DH; cc += 8) {
+        const f32x8 x = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(orow + cc), f32x8);
+        const f32x8 y = __builtin_convertvector(lds8(dOs, r, cc), f32x8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc = fmaf(x[j], y[j], acc);
+      }
+    }
+    dd_s[r] = acc;
+    lse_s[r] = r < c.S ? lse[(int64_t)bh * SP + r] : INFINITY;
+  }
+}
+
+// phase A: per 16-key block, dV^T = dO^T P and dK^T = Q^T dS over all queries
+template <int SP>
+__device__ __forceinline__ void bwd_phase_a(const BwdCtx<SP>& c, const bf16* Qs, const bf16* dOs,
+                                            const float* lse_s, const float* dd_s,
+                                            const bf16* kg, const bf16* vg, int64_t ld, bf16* dq_base,
+                                            int64_t lddq) {
+  // K / V fragments of this wave's key blocks (wave, wave + 4, ...): block
+  // i + 1's are loaded while block i computes (rolling one-ahead prefetch)
+  bf16x8 kf[2], vf[2], kn[2], vn[2];
+  auto frag = [&](int kb, bf16x8 (&f0)[2], bf16x8 (&f1)[2]) {
+    const int r = min(kb * 16 + c.li, c.S - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f0[ks] = *reinterpret_cast<const bf16x8*>(kg + (int64_t)r * ld + ks * 32 + c.g * 8);
+      f1[ks] = *reinterpret_cast<const bf16x8*>(vg + (int64_t)r * ld + ks * 32 + c.g * 8);
+    }
+  };
+  frag(c.wave, kf, vf);
+#pragma unroll
+  for (int i = 0; i < BwdCtx<SP>::MAXT; ++i) {
+    const int kb = c.wave + 4 * i;
+    if (kb >= c.nt) break;
+    if (kb + 4 < c.nt) frag(kb + 4, kn, vn);
+    const int key = kb * 16 + c.li;
+    const bool kin = key < c.S;
+    f32x4 dv[4], dk[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
+#pragma unroll 1
+    for (int qc = 0; qc < SP / 32; ++qc) {
+      float pp[2][4], dss[2][4];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int q0 = qc * 32 + hf * 16;
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          sv = mfma(lds8(Qs, q0 + c.li, ks * 32 + c.g * 8), kf[ks], sv);
+          dp = mfma(lds8(dOs, q0 + c.li, ks * 32 + c.g * 8), vf[ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int q = q0 + 4 * c.g + e;
+          const float pv = kin ? exp2f(sv[e] * c.sl2 - lse_s[q]) : 0.f;
+          pp[hf][e] = pv;
+          dss[hf][e] = pv * (dp[e] - dd_s[q]);
+        }
+      }
+      const bf16x8 pb = pack_pi(pp[0], pp[1]);
+      const bf16x8 dsb = pack_pi(dss[0], dss[1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        dv[t] = mfma(lds_tr8(dOs, qc * 32, t * 16, c.lane), pb, dv[t]);
+        dk[t] = mfma(lds_tr8(Qs, qc * 32, t * 16, c.lane), dsb, dk[t]);
+      }
+    }
+    if (kin) {
+      bf16* row = dq_base + (int64_t)key * lddq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        store4(row + c.D + t * 16 + 4 * c.g, dk[t], c.scale);
+        store4(row + 2 * c.D + t * 16 + 4 * c.g, dv[t], 1.f);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) { kf[ks] = kn[ks]; vf[ks] = vn[ks]; }
+  }
+}
+
+// phase B: per 16-query tile, dQ^T = K^T dS^T over all keys
+template <int SP>
+__device__ __forceinline__ void bwd_phase_b(const BwdCtx<SP>& c, const bf16* Ks, const bf16* Vs,
+                                            const float* lse_s, const float* dd_s,
+                                            const bf16* qg, int64_t ldq, const bf16* dg, int64_t ldd,
+                                            bf16* dq_base, int64_t lddq) {
+  bf16x8 qf[2], dof[2], qn[2], dn[2];
+  auto frag = [&](int qt, bf16x8 (&f0)[2], bf16x8 (&f1)[2]) {
+    const int r = min(qt * 16 + c.li, c.S - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      f0[ks] = *reinterpret_cast<const bf16x8*>(qg + (int64_t)r * ldq + ks * 32 + c.g * 8);
+      f1[ks] = *reinterpret_cast<const bf16x8*>(dg + (int64_t)r * ldd + ks * 32 + c.g * 8);
+    }
+  };
+  frag(c.wave, qf, dof);
+#pragma unroll
+  for (int i = 0; i < BwdCtx<SP>::MAXT; ++i) {
+    const int qt = c.wave + 4 * i;
+    if (qt >= c.nt) break;
+    if (qt + 4 < c.nt) frag(qt + 4, qn, dn);
+    const int q = qt * 16 + c.li;
+    const float lq = lse_s[q], dq_d = dd_s[q];
+    f32x4 dq[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kc = 0; kc < SP / 32; ++kc) {
+      float dss[2][4];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int k0 = kc * 32 + hf * 16;
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = sv;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          sv = mfma(lds8(Ks, k0 + c.li, ks * 32 + c.g * 8), qf[ks], sv);
+          dp = mfma(lds8(Vs, k0 + c.li, ks * 32 + c.g * 8), dof[ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int key = k0 + 4 * c.g + e;
+          const float pv = key < c.S ? exp2f(sv[e] * c.sl2 - lq) : 0.f;
+          dss[hf][e] = pv * (dp[e] - dq_d);
+        }
+      }
+      const bf16x8 dsb = pack_pi(dss[0], dss[1]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) dq[t] = mfma(lds_tr8(Ks, kc * 32, t * 16, c.lane), dsb, dq[t]);
+    }
+    if (q < c.S) {
+      bf16* row = dq_base + (int64_t)q * lddq;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) store4(row + t * 16 + 4 * c.g, dq[t], c.scale);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) { qf[ks] = qn[ks]; dof[ks] = dn[ks]; }
+  }
+}
+
+template <int SP>
+__device__ __forceinline__ BwdCtx<SP> bwd_ctx(int S, int H, float scale) {
+  BwdCtx<SP> c;
+  c.S = S;
+  c.D = H * DH;
+  c.lane = threadIdx.x & 63;
+  c.wave = threadIdx.x >> 6;
+  c.g = c.lane >> 4;
+  c.li = c.lane & 15;
+  c.nt = (S + 15) / 16;
+  c.scale = scale;
+  c.sl2 = scale * kLog2e;
+  return c;
+}
+
 template <int SP>
 __global__ __launch_bounds__(kThreads, 2) void attn_bwd_kernel(
     const bf16* __restrict__ qkv, int64_t ld, const bf16* __restrict__ dout, int64_t ldd,
@@ -315,153 +488,89 @@ __global__ __launch_bounds__(kThreads, 2) void attn_bwd_kernel(
   bf16* X1 = X0 + SP * LROW;
   float* lse_s = reinterpret_cast<float*>(X1 + SP * LROW);
   float* dd_s = lse_s + SP;
+  const BwdCtx<SP> c = bwd_ctx<SP>(S, H, scale);
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int D = H * DH;
   const bf16* qb = qkv + (int64_t)b * S * ld + h * DH;
   const bf16* db = dout + (int64_t)b * S * ldd + h * DH;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int nt = (S + 15) / 16;
-  // this wave's key blocks (phase A) are wave, wave + 4, ...: their K / V
-  // fragments are loaded up front, in flight with the Q / dO staging
-  constexpr int MAXT = (SP / 16 + 3) / 4;
-  bf16x8 kf[MAXT][2], vf[MAXT][2];
-#pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
-    const int kr = min((wave + 4 * i) * 16 + li, S - 1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      kf[i][ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)kr * ld + D + ks * 32 + g * 8);
-      vf[i][ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)kr * ld + 2 * D + ks * 32 + g * 8);
-    }
-  }
+  bf16* dq_base = dqkv + (int64_t)b * S * lddq + h * DH;
   stage2<SP>(X0, qb, ld, X1, db, ldd, S);  // Q, dO
   __syncthreads();
-  // D_i = sum_d dO[i][d] * O[i][d]  (fp32): O from global, dO from LDS
-  for (int r = threadIdx.x; r < SP; r += kThreads) {
-    float acc = 0.f;
-    if (r < S) {
-      const bf16* orow = o + ((int64_t)b * S + r) * ldo + h * DH;
-#pragma unroll
-      for (int c = 0; c < DH; c += 8) {
-        const f32x8 x = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(orow + c), f32x8);
-        const f32x8 y = __builtin_convertvector(lds8(X1, r, c), f32x8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc = fmaf(x[j], y[j], acc);
-      }
-    }
-    dd_s[r] = acc;
-    lse_s[r] = r < S ? lse[(int64_t)bh * SP + r] : INFINITY;
-  }
+  bwd_rowstats<SP>(c, X1, o, ldo, lse, b, h, bh, lse_s, dd_s);
   __syncthreads();
-  const float sl2 = scale * kLog2e;
-  bf16* dq_base = dqkv + (int64_t)b * S * lddq + h * DH;
-  const bf16* Qs = X0;
-  const bf16* dOs = X1;
+  bwd_phase_a<SP>(c, X0, X1, lse_s, dd_s, qb + c.D, qb + 2 * c.D, ld, dq_base, lddq);
+  // phase B: K and V replace Q and dO in LDS
+  __syncthreads();
+  stage2<SP>(X0, qb + c.D, ld, X1, qb + 2 * c.D, ld, S);  // K, V
+  __syncthreads();
+  bwd_phase_b<SP>(c, X0, X1, lse_s, dd_s, qb, ld, db, ldd, dq_base, lddq);
+}
 
-  // ---- phase A: per 16-key block, dV^T = dO^T P and dK^T = Q^T dS over all queries ----
+// Persistent backward: 2 workgroups per CU walk the (batch, head) pairs; each
+// phase's LDS image is loaded into registers during the previous phase (K / V
+// of head i during its phase A, Q / dO of head i + grid during phase B of i),
+// so no phase waits on an HBM round trip for its operands.
+template <int SP>
+__global__ __launch_bounds__(kThreads, 2) void attn_bwd_pp_kernel(
+    const bf16* __restrict__ qkv, int64_t ld, const bf16* __restrict__ dout, int64_t ldd,
+    const bf16* __restrict__ o, int64_t ldo, const float* __restrict__ lse, int S, int H, float scale,
+    bf16* __restrict__ dqkv, int64_t lddq, int nbh) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * SP * LROW * 2 + 2 * SP * 4];
+  bf16* X0 = reinterpret_cast<bf16*>(smem);
+  bf16* X1 = X0 + SP * LROW;
+  float* lse_s = reinterpret_cast<float*>(X1 + SP * LROW);
+  float* dd_s = lse_s + SP;
+  const BwdCtx<SP> c = bwd_ctx<SP>(S, H, scale);
+  constexpr int PER = SP * (DH / 8);
+  constexpr int IT = (PER + kThreads - 1) / kThreads;
+  bf16x8 rA[IT], rB[IT];
+  auto gload = [&](const bf16* s0, int64_t l0, const bf16* s1, int64_t l1) {
 #pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
-    const int kb = wave + 4 * i;
-    if (kb >= nt) break;
-    const int key = kb * 16 + li;
-    const bool kin = key < S;
-    f32x4 dv[4], dk[4];
+    for (int i = 0; i < IT; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      const int r = v >> 3, cc = (v & 7) * 8;
+      const bool ok = v < PER && r < S;
+      rA[i] = ok ? *reinterpret_cast<const bf16x8*>(s0 + (int64_t)r * l0 + cc) : bf16x8{};
+      rB[i] = ok ? *reinterpret_cast<const bf16x8*>(s1 + (int64_t)r * l1 + cc) : bf16x8{};
+    }
+  };
+  auto lstore = [&] {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
-#pragma unroll 1
-    for (int qc = 0; qc < SP / 32; ++qc) {
-      float pp[2][4], dss[2][4];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int q0 = qc * 32 + hf * 16;
-        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          s = mfma(lds8(Qs, q0 + li, ks * 32 + g * 8), kf[i][ks], s);
-          dp = mfma(lds8(dOs, q0 + li, ks * 32 + g * 8), vf[i][ks], dp);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = q0 + 4 * g + e;
-          const float p = kin ? exp2f(s[e] * sl2 - lse_s[q]) : 0.f;
-          pp[hf][e] = p;
-          dss[hf][e] = p * (dp[e] - dd_s[q]);
-        }
-      }
-      const bf16x8 pb = pack_pi(pp[0], pp[1]);
-      const bf16x8 dsb = pack_pi(dss[0], dss[1]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        dv[t] = mfma(lds_tr8(dOs, qc * 32, t * 16, lane), pb, dv[t]);
-        dk[t] = mfma(lds_tr8(Qs, qc * 32, t * 16, lane), dsb, dk[t]);
+    for (int i = 0; i < IT; ++i) {
+      const int v = threadIdx.x + i * kThreads;
+      if (v < PER) {
+        const int r = v >> 3, cc = (v & 7) * 8;
+        *reinterpret_cast<bf16x8*>(X0 + r * LROW + cc) = rA[i];
+        *reinterpret_cast<bf16x8*>(X1 + r * LROW + cc) = rB[i];
       }
     }
-    if (kin) {
-      bf16* row = dq_base + (int64_t)key * lddq;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        store4(row + D + t * 16 + 4 * g, dk[t], scale);
-        store4(row + 2 * D + t * 16 + 4 * g, dv[t], 1.f);
-      }
-    }
+  };
+  int bh = blockIdx.x;
+  if (bh >= nbh) return;
+  {
+    const int b = bh / H, h = bh - b * H;
+    gload(qkv + (int64_t)b * S * ld + h * DH, ld, dout + (int64_t)b * S * ldd + h * DH, ldd);  // Q, dO
   }
-
-  // ---- phase B: K and V replace Q and dO in LDS ----
-  // this wave's query tiles' Q / dO fragments, in flight with the K / V staging
-  bf16x8 qf[MAXT][2], dof[MAXT][2];
-#pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
-    const int qr = min((wave + 4 * i) * 16 + li, S - 1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      qf[i][ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)qr * ld + ks * 32 + g * 8);
-      dof[i][ks] = *reinterpret_cast<const bf16x8*>(db + (int64_t)qr * ldd + ks * 32 + g * 8);
+  for (; bh < nbh; bh += gridDim.x) {
+    const int b = bh / H, h = bh - b * H;
+    const bf16* qb = qkv + (int64_t)b * S * ld + h * DH;
+    const bf16* db = dout + (int64_t)b * S * ldd + h * DH;
+    bf16* dq_base = dqkv + (int64_t)b * S * lddq + h * DH;
+    __syncthreads();  // the previous head's phase B is done with X0 / X1 / lse_s / dd_s
+    lstore();         // Q, dO
+    __syncthreads();
+    gload(qb + c.D, ld, qb + 2 * c.D, ld);  // K, V: in flight during phase A
+    bwd_rowstats<SP>(c, X1, o, ldo, lse, b, h, bh, lse_s, dd_s);
+    __syncthreads();
+    bwd_phase_a<SP>(c, X0, X1, lse_s, dd_s, qb + c.D, qb + 2 * c.D, ld, dq_base, lddq);
+    __syncthreads();  // phase A is done with Q / dO
+    lstore();         // K, V
+    __syncthreads();
+    const int nb = bh + gridDim.x;
+    if (nb < nbh) {  // the next head's Q, dO: in flight during phase B
+      const int b2 = nb / H, h2 = nb - b2 * H;
+      gload(qkv + (int64_t)b2 * S * ld + h2 * DH, ld, dout + (int64_t)b2 * S * ldd + h2 * DH, ldd);
     }
-  }
-  __syncthreads();
-  stage2<SP>(X0, qb + D, ld, X1, qb + 2 * D, ld, S);  // K, V
-  __syncthreads();
-  const bf16* Ks = X0;
-  const bf16* Vs = X1;
-  // per 16-query tile, dQ^T = K^T dS^T over all keys
-#pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
-    const int qt = wave + 4 * i;
-    if (qt >= nt) break;
-    const int q = qt * 16 + li;
-    const float lq = lse_s[q], dq_d = dd_s[q];
-    f32x4 dq[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) dq[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int kc = 0; kc < SP / 32; ++kc) {
-      float dss[2][4];
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int k0 = kc * 32 + hf * 16;
-        f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = s;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          s = mfma(lds8(Ks, k0 + li, ks * 32 + g * 8), qf[i][ks], s);
-          dp = mfma(lds8(Vs, k0 + li, ks * 32 + g * 8), dof[i][ks], dp);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int key = k0 + 4 * g + e;
-          const float p = key < S ? exp2f(s[e] * sl2 - lq) : 0.f;
-          dss[hf][e] = p * (dp[e] - dq_d);
-        }
-      }
-      const bf16x8 dsb = pack_pi(dss[0], dss[1]);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) dq[t] = mfma(lds_tr8(Ks, kc * 32, t * 16, lane), dsb, dq[t]);
-    }
-    if (q < S) {
-      bf16* row = dq_base + (int64_t)q * lddq;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) store4(row + t * 16 + 4 * g, dq[t], scale);
-    }
+    bwd_phase_b<SP>(c, X0, X1, lse_s, dd_s, qb, ld, db, ldd, dq_base, lddq);
   }
 }
 
@@ -493,14 +602,17 @@ void check_2d(const at::Tensor& t, const char* name, int64_t rows, int64_t min_c
 bool attention_supported(int64_t S, int64_t head_dim) { return head_dim == DH && S >= 1 && S <= 256; }
 
 namespace {
+int g_attn_bwd_variant = 1;  // 0: one workgroup per (batch, head); 1: persistent with prefetch
 int g_attn_fwd_variant = 1;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
                              // next-head prefetch; 2: one 8-wave workgroup per (batch, head)
 int g_num_cus_attn = 0;
 }  // namespace
 
-void set_attention_variant(int fwd) {
+void set_attention_variant(int fwd, int bwd) {
   TORCH_CHECK(fwd >= 0 && fwd <= 2, "attention forward variant: 0 (per head), 1 (persistent), 2 (per head, 8 waves)");
+  TORCH_CHECK(bwd >= 0 && bwd <= 1, "attention backward variant: 0 (per head), 1 (persistent)");
   g_attn_fwd_variant = fwd;
+  g_attn_bwd_variant = bwd;
 }
 
 // qkv [B*S, >= 3*H*64] -> (o [B*S, H*64], lse [B*H, SP] fp32, base-2)
@@ -549,12 +661,28 @@ at::Tensor attention_backward(const at::Tensor& dout, const at::Tensor& qkv, con
                   lse.size(0) == B * H && lse.size(1) == sp, "attention: lse shape");
   auto dqkv = at::empty({B * S, 3 * H * DH}, qkv.options());
   hipStream_t st = at::hip::getCurrentHIPStream();
-  DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_bwd_kernel<SPC>), dim3(B * H), dim3(kThreads), 0, st,
-                                           (const bf16*)qkv.data_ptr(), qkv.stride(0),
-                                           (const bf16*)dout.data_ptr(), dout.stride(0),
-                                           (const bf16*)o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
-                                           (int)S, (int)H, (float)scale, (bf16*)dqkv.data_ptr(),
-                                           dqkv.stride(0)));
+  if (g_attn_bwd_variant == 1) {
+    if (g_num_cus_attn == 0) {
+      int dev = 0;
+      DMP_HIP_CHECK(hipGetDevice(&dev));
+      DMP_HIP_CHECK(hipDeviceGetAttribute(&g_num_cus_attn, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int nbh = (int)(B * H);
+    const int grid = std::min(nbh, 2 * g_num_cus_attn);
+    DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_bwd_pp_kernel<SPC>), dim3(grid), dim3(kThreads), 0, st,
+                                             (const bf16*)qkv.data_ptr(), qkv.stride(0),
+                                             (const bf16*)dout.data_ptr(), dout.stride(0),
+                                             (const bf16*)o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
+                                             (int)S, (int)H, (float)scale, (bf16*)dqkv.data_ptr(),
+                                             dqkv.stride(0), nbh));
+  } else {
+    DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_bwd_kernel<SPC>), dim3(B * H), dim3(kThreads), 0, st,
+                                             (const bf16*)qkv.data_ptr(), qkv.stride(0),
+                                             (const bf16*)dout.data_ptr(), dout.stride(0),
+                                             (const bf16*)o.data_ptr(), o.stride(0), lse.data_ptr<float>(),
+                                             (int)S, (int)H, (float)scale, (bf16*)dqkv.data_ptr(),
+                                             dqkv.stride(0)));
+  }
   DMP_HIP_CHECK(hipGetLastError());
   return dqkv;
 }

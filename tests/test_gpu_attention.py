@@ -63,7 +63,7 @@ def test_attention_matches_sdpa_path_in_vit_block():
     assert torch.isfinite(y).all()
 
 
-def test_persistent_forward_equals_per_head_forward():
+def test_attention_variants_agree_bitwise():
     """The persistent forward (next-head K / V / Q prefetch) computes exactly
     what the one-workgroup-per-head kernel computes (same MFMA order)."""
     from distributed_model_parallel_amd import _native
@@ -71,14 +71,18 @@ def test_persistent_forward_equals_per_head_forward():
     torch.manual_seed(9)
     B, S, H = 40, 197, 12  # 480 heads: fewer and more than 2 x CUs per wave of the grid
     qkv = torch.randn(B * S, 3 * H * 64, device="cuda").bfloat16()
+    do = torch.randn(B * S, H * 64, device="cuda").bfloat16()
     try:
-        C.set_attention_variant(0)
+        C.set_attention_variant(0, 0)
         o0, l0 = C.attention_forward(qkv, B, S, H, 0.125)
-        C.set_attention_variant(1)
+        g0 = C.attention_backward(do, qkv, o0, l0, B, S, H, 0.125)
+        C.set_attention_variant(1, 1)
         o1, l1 = C.attention_forward(qkv, B, S, H, 0.125)
-        C.set_attention_variant(2)
+        g1 = C.attention_backward(do, qkv, o0, l0, B, S, H, 0.125)
+        C.set_attention_variant(2, 1)
         o2, l2 = C.attention_forward(qkv, B, S, H, 0.125)
     finally:
-        C.set_attention_variant(1)
+        C.set_attention_variant(1, 1)
     assert torch.equal(o0, o1) and torch.equal(o0, o2)
     assert torch.equal(l0[:, :S], l1[:, :S]) and torch.equal(l0[:, :S], l2[:, :S])
+    assert torch.equal(g0, g1), "persistent backward differs from the per-head backward"

@@ -40,13 +40,13 @@ def main():
     from distributed_model_parallel_amd import _native
     C = _native.require("attn bench")
 
-    def variant(v):
+    def variant(v, vb):
         def f():
-            C.set_attention_variant(v)
+            C.set_attention_variant(v, vb)
             return A.self_attention_packed(qkv, H)
         return f
-    for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("hip per-head", variant(0)),
-                     ("hip persistent", variant(1)), ("hip 8-wave", variant(2))):
+    for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("hip per-head", variant(0, 0)),
+                     ("hip persistent", variant(1, 1)), ("hip 8-wave fwd", variant(2, 1))):
         tf = timeit(lambda: fn())
         o = fn()
         tb = timeit(lambda: torch.autograd.grad(o, qkv, go, retain_graph=True))
