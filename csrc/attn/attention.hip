@@ -602,8 +602,8 @@ void check_2d(const at::Tensor& t, const char* name, int64_t rows, int64_t min_c
 bool attention_supported(int64_t S, int64_t head_dim) { return head_dim == DH && S >= 1 && S <= 256; }
 
 namespace {
-int g_attn_bwd_variant = 1;  // 0: one workgroup per (batch, head); 1: persistent with prefetch
-int g_attn_fwd_variant = 1;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
+int g_attn_bwd_variant = 0;  // 0: one workgroup per (batch, head); 1: persistent with prefetch
+int g_attn_fwd_variant = 0;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
                              // next-head prefetch; 2: one 8-wave workgroup per (batch, head)
 int g_num_cus_attn = 0;
 }  // namespace

@@ -11,11 +11,19 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "unvalidated: new GPU test not yet run on an MI355X this round "
+                                       "(skipped unless DMP_RUN_UNVALIDATED=1, so a first-run failure cannot "
+                                       "stop the suite under -x)")
 
 
 def pytest_collection_modifyitems(config, items):
     import torch
 
+    if os.environ.get("DMP_RUN_UNVALIDATED", "0") != "1":
+        gate = pytest.mark.skip(reason="unvalidated on MI355X yet (DMP_RUN_UNVALIDATED=1 runs it)")
+        for item in items:
+            if "unvalidated" in item.keywords:
+                item.add_marker(gate)
     if torch.cuda.is_available():
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")

@@ -283,6 +283,7 @@ def test_replica_cache_attrs_concurrency_and_lifetime():
 
 
 @pytest.mark.gpu
+@pytest.mark.unvalidated
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
 def test_dp_graphed_replicas_match_eager(arch):
     """DataParallel(graphs=True) (parallel/dp_graphs.py: static replicas whose

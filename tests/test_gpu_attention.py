@@ -63,6 +63,7 @@ def test_attention_matches_sdpa_path_in_vit_block():
     assert torch.isfinite(y).all()
 
 
+@pytest.mark.unvalidated
 def test_attention_variants_agree_bitwise():
     """The persistent forward (next-head K / V / Q prefetch) computes exactly
     what the one-workgroup-per-head kernel computes (same MFMA order)."""
@@ -82,7 +83,7 @@ def test_attention_variants_agree_bitwise():
         C.set_attention_variant(2, 1)
         o2, l2 = C.attention_forward(qkv, B, S, H, 0.125)
     finally:
-        C.set_attention_variant(1, 1)
+        C.set_attention_variant(0, 0)
     assert torch.equal(o0, o1) and torch.equal(o0, o2)
     assert torch.equal(l0[:, :S], l1[:, :S]) and torch.equal(l0[:, :S], l2[:, :S])
     assert torch.equal(g0, g1), "persistent backward differs from the per-head backward"

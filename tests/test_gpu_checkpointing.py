@@ -18,6 +18,7 @@ from distributed_model_parallel_amd.utils.precision import cast_model
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.unvalidated
 @pytest.mark.parametrize("arch,size", [("resnet50", 64), ("mobilenetv2", 32)])
 def test_checkpointed_step_matches_plain(arch, size):
     torch.manual_seed(0)
