@@ -107,6 +107,8 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& out);
 void set_gemm_xl_bn(int bn, int pipe, int group_m);
 int get_gemm_xl_pipe();
+void set_gemm_xl_x2(int mode);
+int get_gemm_xl_x2();
 int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
                                 int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
@@ -327,6 +329,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "wide 1x1-conv GEMM with conv epilogues: moments | add | bnbwd | affine (scale, shift, residual, relu); "
         "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
   m.def("get_gemm_xl_pipe", &dmp::get_gemm_xl_pipe);
+  m.def("set_gemm_xl_x2", &dmp::set_gemm_xl_x2, py::arg("mode"),
+        "conv-epilogue GEMMs on the two-blocks-per-CU 256x128 kernel: 0 off, 1 short K (<= 512), 2 always");
+  m.def("get_gemm_xl_x2", &dmp::get_gemm_xl_x2);
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");

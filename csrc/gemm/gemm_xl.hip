@@ -914,6 +914,254 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Two-blocks-per-CU conv-epilogue GEMM for the SHORT-K 1x1 convolutions of
+// ResNet-50 (K = 64..512 over M = 0.1-6.4 M rows, N = 256..2048) -- finding 43.
+//
+// With one 512-thread block per CU (gemm_xl_nt_kernel: 256x256 tile, 240
+// VGPRs, 128-135 KB LDS), a CU alternates a compute phase (the main loop: no
+// HBM traffic once the operands have landed) and a memory phase (the epilogue:
+// residual / BN operand loads and the C stores), so HBM is busy only during
+// the epilogue share of every tile: l3/l4 affine and BN-backward epilogues ran
+// at 42-62 % of the HBM roofline, ~0.5 of it.  Here a 256 x 128 tile
+// (8 waves as 2 x 4, 128 x 32 outputs = 64 accumulator VGPRs per wave), a
+// single 48 KB operand buffer and NO LDS staging of C leave room for two
+// blocks per CU (launch bounds: 4 waves per SIMD, <= 128 VGPRs; 2 x 48 KB LDS): one
+// block's epilogue overlaps the other's main loop.
+//
+// The MFMA operands are swapped (B fragment first), so the accumulator holds
+// C^T: lane l owns 4 consecutive output CHANNELS (n = 16 j + 4 (l >> 4) + e)
+// of one pixel row (m = 16 i + (l & 15)), and every epilogue operand is one
+// 8-byte load / store per lane; the 4 lane groups of a row cover 32 B, the
+// two N fragments of a wave 128 B (one L2 line) of each row.  Rounding points
+// and per-column affines are those of gemm_xl_nt_kernel (finding 33: the
+// affine is applied to the fp32 accumulator before the bf16 rounding).
+// ---------------------------------------------------------------------------
+constexpr int X2_BM = 256, X2_BN = 128;
+
+template <int EPI>
+__global__ __launch_bounds__(XTHREADS, 4) void gemm_x2_kernel(const XlArgs p) {  // 4 waves per SIMD = 2 blocks per CU
+  static_assert(EPI == XL_MOMENTS || EPI == XL_AFFINE || EPI == XL_BNBWD || EPI == XL_ADD || EPI == XL_STORE,
+                "conv epilogues only");
+  constexpr int RA = X2_BM * 64, RB = X2_BN * 64;   // one k32 half: 16 KB of A, 8 KB of B
+  constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;  // glds per wave per half: 2, 1
+  __shared__ __attribute__((aligned(16))) char smem[2 * RA + 2 * RB];
+  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD;
+  if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int mtiles = (M + X2_BM - 1) / X2_BM, ntiles = N / X2_BN;
+  int mt, nt;
+  tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
+  const int m0 = mt * X2_BM, n0 = nt * X2_BN;
+  const int ktiles = K / XBK;
+
+  // staging: glds lane L carries 16 B of row (L >> 2) of a 16-row x 64-B block,
+  // logical chunk (L & 3) ^ chunk_xor(L >> 4) (the read undoes the swizzle)
+  const int srow = lane >> 2;
+  const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
+  const bf16* asrc[NA];
+  const bf16* asrc2[NA];
+  const bf16* bsrc[NB];
+#pragma unroll
+  for (int q = 0; q < NA; ++q) {
+    const int r = min(m0 + (wave * NA + q) * 16 + srow, M - 1);
+    asrc[q] = p.A + (int64_t)r * p.lda + schunk * 8;
+    asrc2[q] = p.A2 ? p.A2 + xl_out_row(p.a2m, r) * p.lda2 + schunk * 8 - p.K1 : nullptr;
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) bsrc[q] = p.B + (int64_t)(n0 + (wave * NB + q) * 16 + srow) * p.ldb + schunk * 8;
+
+  f32x4 acc[8][2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int lrow = lane & 15, lk = lane >> 4;
+  const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
+
+  for (int kt = 0; kt < ktiles; ++kt) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int koff = kt * XBK + ks * 32;
+      const bool second = p.A2 && koff >= p.K1;
+      char* da = smem + ks * RA + wave * NA * 1024;
+      char* db = smem + 2 * RA + ks * RB + wave * NB * 1024;
+#pragma unroll
+      for (int q = 0; q < NA; ++q) glds16((second ? asrc2[q] : asrc[q]) + koff, da + q * 1024);
+#pragma unroll
+      for (int q = 0; q < NB; ++q) glds16(bsrc[q] + koff, db + q * 1024);
+    }
+    vmcnt<0>();
+    barrier();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const char* ar = smem + ks * RA + (wr * 128) * 64 + frag_off;
+      const char* br = smem + 2 * RA + ks * RB + (wc * 32) * 64 + frag_off;
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(br);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(br + 16 * 64);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + (h * 4 + i) * 16 * 64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[h * 4 + i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0, fa[i], acc[h * 4 + i][0], 0, 0, 0);
+          acc[h * 4 + i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, fa[i], acc[h * 4 + i][1], 0, 0, 0);
+        }
+      }
+    }
+    barrier();  // every wave read this K tile before the next one overwrites it
+  }
+
+  // ---- epilogue straight from the accumulators (C^T layout) ----
+  // per-column constants of the block's 128 columns in LDS (the operand buffer
+  // is free after the last barrier): few VGPRs, read where used
+  float* cst = reinterpret_cast<float*>(smem + 4096);  // [5][128]: scale, shift/bias, mean, mask scale, mask shift
+  if (tid < X2_BN) {
+    const int col = n0 + tid;
+    float c0 = 1.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, c4 = 0.f;
+    if constexpr (EPI == XL_AFFINE) {
+      c0 = p.esc ? p.esc[col] : 1.f;
+      c1 = p.esh ? p.esh[col] : 0.f;
+    }
+    if constexpr (EPI == XL_BNBWD) {
+      c1 = p.ebias ? p.ebias[col] : 0.f;
+      c2 = p.bmean ? p.bmean[col] : 0.f;
+      if (!p.bny) {
+        c3 = p.binv[col] * (p.bw ? p.bw[col] : 1.f);
+        c4 = (p.bb ? p.bb[col] : 0.f) - c2 * c3;
+      }
+    }
+    cst[0 * X2_BN + tid] = c0;
+    cst[1 * X2_BN + tid] = c1;
+    cst[2 * X2_BN + tid] = c2;
+    cst[3 * X2_BN + tid] = c3;
+    cst[4 * X2_BN + tid] = c4;
+  }
+  __syncthreads();
+  const int lg = lane >> 4;
+  float ms[2][4], mq[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ms[j][e] = mq[j][e] = 0.f;
+  constexpr bool kRes = EPI == XL_AFFINE || EPI == XL_BNBWD || EPI == XL_ADD;
+  const bf16* rbase = p.R ? p.R : p.C;  // absent operands read a valid dummy row (branch-free loads)
+  const int64_t rld = p.R ? p.ldr : 0;
+  const bf16* xbase = p.bx ? p.bx : p.C;
+  const int64_t xld = p.bx ? p.ldbx : 0;
+  const bf16* ybase = p.bny ? p.bny : p.C;
+  const int64_t yld = p.bny ? p.ldby : 0;
+  // pixel fragments per batch: every operand load of a batch before its stores
+  constexpr int PI = EPI == XL_BNBWD ? 1 : 2;
+#pragma unroll
+  for (int h = 0; h < 8 / PI; ++h) {
+    bf16x4 l0[PI][2], l1[PI][2], l2[PI][2];
+    unsigned rok = 0;
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const int row = min(m0 + wr * 128 + (h * PI + i) * 16 + lrow, M - 1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wc * 32 + j * 16 + 4 * lg;
+        if constexpr (kRes) {
+          int64_t rr = row;
+          if constexpr (EPI == XL_BNBWD) {
+            rr = p.R ? compact_row(p.rmap, row) : -1;
+            rok |= (rr >= 0 ? 1u : 0u) << (2 * i + j);
+            rr = rr >= 0 ? rr : 0;
+          }
+          l0[i][j] = *reinterpret_cast<const bf16x4*>(rbase + rr * rld + col);
+        }
+        if constexpr (EPI == XL_BNBWD) {
+          l1[i][j] = *reinterpret_cast<const bf16x4*>(xbase + (int64_t)row * xld + col);
+          l2[i][j] = *reinterpret_cast<const bf16x4*>(ybase + (int64_t)row * yld + col);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PI; ++i) {
+      const int row = m0 + wr * 128 + (h * PI + i) * 16 + lrow;
+      const bool rin = row < M;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int cl = wc * 32 + j * 16 + 4 * lg;  // column within the block
+        const f32x4 a = acc[h * PI + i][j];
+        bf16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (bf16)fmaf(a[e], cst[cl + e], cst[X2_BN + cl + e]);  // staging rounding
+        if constexpr (EPI == XL_MOMENTS) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float f = rin ? (float)v[e] : 0.f;
+            ms[j][e] += f;
+            mq[j][e] = fmaf(f, f, mq[j][e]);
+          }
+        } else if constexpr (EPI == XL_ADD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (bf16)((float)v[e] + (float)l0[i][j][e]);
+        } else if constexpr (EPI == XL_AFFINE) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float f = (float)v[e];
+            if (p.R) f += (float)l0[i][j][e];
+            if (p.erelu) f = fmaxf(f, 0.f);
+            v[e] = (bf16)f;
+          }
+        } else if constexpr (EPI == XL_BNBWD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float g = (float)v[e];
+            if (p.R) {
+              if ((rok >> (2 * i + j)) & 1u) g += (float)l0[i][j][e];
+              g = (float)(bf16)g;
+            }
+            const float xv = (float)l1[i][j][e], yv = (float)l2[i][j][e];
+            const bool on = p.bny ? (yv > 0.f)
+                                  : (fmaf(xv, cst[3 * X2_BN + cl + e], cst[4 * X2_BN + cl + e]) > 0.f);
+            const float dz = (on && rin) ? g : 0.f;
+            ms[j][e] += dz;
+            if (p.bx) mq[j][e] = fmaf(dz, xv - cst[2 * X2_BN + cl + e], mq[j][e]);
+            v[e] = (bf16)dz;
+          }
+        }
+        if (rin) *reinterpret_cast<bf16x4*>(p.C + (int64_t)row * p.ldc + n0 + cl) = v;
+      }
+    }
+  }
+  if constexpr (kMom) {
+    // per column: the 16 lanes of a lane group hold 16 different pixel rows
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+          ms[j][e] += __shfl_xor(ms[j][e], off, 64);
+          mq[j][e] += __shfl_xor(mq[j][e], off, 64);
+        }
+    __syncthreads();  // the operand buffer is free: reuse it for the two wave rows' partials
+    float* red = reinterpret_cast<float*>(smem);  // [2 stats][2 wr][128 cols]
+    if (lrow == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = wc * 32 + j * 16 + 4 * lg + e;
+          red[(0 * 2 + wr) * X2_BN + c] = ms[j][e];
+          red[(1 * 2 + wr) * X2_BN + c] = mq[j][e];
+        }
+    }
+    __syncthreads();
+    for (int c = tid; c < X2_BN; c += XTHREADS) {
+      p.part[(int64_t)mt * N + n0 + c] = red[(0 * 2 + 0) * X2_BN + c] + red[(0 * 2 + 1) * X2_BN + c];
+      p.part[(int64_t)(mtiles + mt) * N + n0 + c] = red[(1 * 2 + 0) * X2_BN + c] + red[(1 * 2 + 1) * X2_BN + c];
+    }
+  }
+}
+
 // Epilogue transform of one 8-column bf16 vector of row `row` (already holding
 // bf16(acc [+ bias])); writes the side output of XL_BIAS_GELU.
 template <int EPI>
@@ -1475,8 +1723,29 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
 }
 
+// two-blocks-per-CU short-K kernel (gemm_x2_kernel): 0 = off, 1 = where it
+// measured faster (short K), 2 = every conv-epilogue GEMM with N % 128 == 0
+int g_xl_x2 = 0;
+
+bool use_x2(const XlArgs& a) {
+  if (g_xl_x2 == 0 || a.N % X2_BN != 0) return false;
+  return g_xl_x2 == 2 || a.K <= 512;
+}
+
+template <int EPI>
+void launch_x2(const XlArgs& a, hipStream_t s) {
+  const int blocks = ((a.M + X2_BM - 1) / X2_BM) * (a.N / X2_BN);
+  hipLaunchKernelGGL((gemm_x2_kernel<EPI>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+}
+
 template <int EPI>
 void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
+  if constexpr (EPI == XL_MOMENTS || EPI == XL_AFFINE || EPI == XL_BNBWD || EPI == XL_ADD) {
+    if (use_x2(a)) {
+      launch_x2<EPI>(a, s);
+      return;
+    }
+  }
   if constexpr (EPI >= XL_MOMENTS) {  // conv epilogues: ring kernel only (no persistent form)
     const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + bn - 1) / bn);
     if (bn == 128)
@@ -1954,6 +2223,11 @@ void set_tn_xl_ablation(int a) {
 void set_tn_xl_ring(int r) { g_tn_xl_ring = r != 0; }
 
 int get_gemm_xl_pipe() { return g_xl_pipe; }
+void set_gemm_xl_x2(int mode) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "x2 mode: 0 off, 1 short K, 2 always");
+  g_xl_x2 = mode;
+}
+int get_gemm_xl_x2() { return g_xl_x2; }
 int get_tn_xl_ring() { return g_tn_xl_ring; }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {

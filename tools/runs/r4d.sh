@@ -14,4 +14,7 @@ bash tools/gpu_steps.sh \
   "400|r4d_dp_tests|$P tests/test_data_parallel.py tests/test_gpu_checkpointing.py tests/test_gpu_bn_fold.py -m gpu" \
   "200|r4d_dp4_eager|python bench.py --parallel dp --dp-replicas 4 --batch-size 256 --steps 10 --warmup 5 --phase-times" \
   "200|r4d_dp4_graphs|python bench.py --parallel dp --dp-replicas 4 --batch-size 256 --steps 10 --warmup 5 --dp-graphs" \
-  "400|r4d_conv224|DMP_CONVERGENCE_OUT=gpurun_out/r4d_conv.json $P --timeout 380 tests/test_gpu_convergence.py -k 224"
+  "400|r4d_conv224|DMP_CONVERGENCE_OUT=gpurun_out/r4d_conv.json $P --timeout 380 tests/test_gpu_convergence.py -k 224" || exit $?
+bash tools/gpu_steps.sh \
+  "200|r4d_x2_tests|$P tests/test_gpu_gemm_x2.py" \
+  "200|r4d_x2_bench|python -u tools/x2_bench.py > gpurun_out/r4d_x2_bench.md"
