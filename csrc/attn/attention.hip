@@ -63,6 +63,14 @@ __device__ __forceinline__ bf16x8 pack_pi(const float (&a)[4], const float (&b)[
   return __builtin_convertvector(f, bf16x8);
 }
 
+// v_exp_f32 / v_log_f32 / v_rcp_f32 directly: exp2f / log2f / 1/x expand to
+// 4-5 VALU each for denormal range handling (a compare, two selects and a
+// v_ldexp around the v_exp), which the softmax never needs -- its exp2
+// arguments are <= 0 (a tiny result flushing to 0 is the right answer), l >= 1
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float lg2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -142,13 +150,27 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(const bf16* __rest
       f32x4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) a = mfma(lds8(Ks, kt * 16 + li, ks * 32 + g * 8), qf[i][ks], a);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (kt * 16 + 4 * g + e >= S) a[e] = -INFINITY;
-        m = fmaxf(m, a[e]);
-      }
       st[kt] = a;
     }
+    // padded keys -> -inf after the whole MFMA chain (a branch inside it would
+    // split the block the scheduler hoists the LDS reads across)
+    if (S < SP) {
+      // opaque per tile: hoisted out of the head / tile loops, the 4 * NKT
+      // lane masks would live in (spilled) SGPR pairs
+      int lim = S - 4 * g;
+      asm volatile("" : "+v"(lim));
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+        if (kt * 16 + 16 > S) {  // uniform
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (kt * 16 + e >= lim) st[kt][e] = -INFINITY;
+        }
+    }
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m = fmaxf(m, st[kt][e]);
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     const float mb = m * sl2;
@@ -157,7 +179,7 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(const bf16* __rest
     for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float p = exp2f(st[kt][e] * sl2 - mb);
+        const float p = ex2(st[kt][e] * sl2 - mb);
         st[kt][e] = p;
         l += p;
       }
@@ -176,11 +198,11 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(const bf16* __rest
       for (int t = 0; t < 4; ++t) acc[t] = mfma(lds_tr8(Vs, kc * 32, t * 16, lane), pb, acc[t]);
     }
     if (q < S) {
-      const float inv = 1.f / l;
+      const float inv = rcp(l);
       bf16* orow = o + ((int64_t)b * S + q) * ldo + h * DH;
 #pragma unroll
       for (int t = 0; t < 4; ++t) store4(orow + t * 16 + 4 * g, acc[t], inv);
-      if (g == 0) lse[(int64_t)bh * SP + q] = mb + log2f(l);  // base-2 logsumexp of the scaled scores
+      if (g == 0) lse[(int64_t)bh * SP + q] = mb + lg2(l);  // base-2 logsumexp of the scaled scores
     }
   }
 }
@@ -258,13 +280,27 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_pp_kernel(const bf16* __
         f32x4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) a = mfma(lds8(Ks, kt * 16 + li, ks * 32 + g * 8), qf[i][ks], a);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (kt * 16 + 4 * g + e >= S) a[e] = -INFINITY;
-          m = fmaxf(m, a[e]);
-        }
         st[kt] = a;
       }
+      // padded keys -> -inf after the whole MFMA chain (a branch inside it would
+      // split the block the scheduler hoists the LDS reads across)
+      if (S < SP) {
+        // opaque per tile: hoisted out of the head / tile loops, the 4 * NKT
+        // lane masks would live in (spilled) SGPR pairs
+        int lim = S - 4 * g;
+        asm volatile("" : "+v"(lim));
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt)
+          if (kt * 16 + 16 > S) {  // uniform
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (kt * 16 + e >= lim) st[kt][e] = -INFINITY;
+          }
+      }
+#pragma unroll
+      for (int kt = 0; kt < NKT; ++kt)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m = fmaxf(m, st[kt][e]);
       m = fmaxf(m, __shfl_xor(m, 16, 64));
       m = fmaxf(m, __shfl_xor(m, 32, 64));
       const float mb = m * sl2;
@@ -273,7 +309,7 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_pp_kernel(const bf16* __
       for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pv = exp2f(st[kt][e] * sl2 - mb);
+          const float pv = ex2(st[kt][e] * sl2 - mb);
           st[kt][e] = pv;
           l += pv;
         }
@@ -292,11 +328,11 @@ __global__ __launch_bounds__(kThreads, 2) void attn_fwd_pp_kernel(const bf16* __
         for (int t = 0; t < 4; ++t) acc[t] = mfma(lds_tr8(Vs, kc * 32, t * 16, lane), pb, acc[t]);
       }
       if (q < S) {
-        const float inv = 1.f / l;
+        const float inv = rcp(l);
         bf16* orow = o + ((int64_t)b * S + q) * ldo + h * DH;
 #pragma unroll
         for (int t = 0; t < 4; ++t) store4(orow + t * 16 + 4 * g, acc[t], inv);
-        if (g == 0) lse[(int64_t)bh * SP + q] = mb + log2f(l);
+        if (g == 0) lse[(int64_t)bh * SP + q] = mb + lg2(l);
       }
     }
   }
@@ -357,6 +393,7 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx<SP>& c, const bf16* Qs,
     if (kb + 4 < c.nt) frag(kb + 4, kn, vn);
     const int key = kb * 16 + c.li;
     const bool kin = key < c.S;
+    const float km = kin ? 1.f : 0.f;
     f32x4 dv[4], dk[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) { dv[t] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[t] = dv[t]; }
@@ -372,12 +409,14 @@ __device__ __forceinline__ void bwd_phase_a(const BwdCtx<SP>& c, const bf16* Qs,
           sv = mfma(lds8(Qs, q0 + c.li, ks * 32 + c.g * 8), kf[ks], sv);
           dp = mfma(lds8(dOs, q0 + c.li, ks * 32 + c.g * 8), vf[ks], dp);
         }
+        // the 4 query rows of this lane: one 16-B LDS read per row constant
+        const f32x4 ls = *reinterpret_cast<const f32x4*>(lse_s + q0 + 4 * c.g);
+        const f32x4 dd = *reinterpret_cast<const f32x4*>(dd_s + q0 + 4 * c.g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int q = q0 + 4 * c.g + e;
-          const float pv = kin ? exp2f(sv[e] * c.sl2 - lse_s[q]) : 0.f;
+          const float pv = ex2(sv[e] * c.sl2 - ls[e]) * km;  // a multiply, not a branch around the exp
           pp[hf][e] = pv;
-          dss[hf][e] = pv * (dp[e] - dd_s[q]);
+          dss[hf][e] = pv * (dp[e] - dd[e]);
         }
       }
       const bf16x8 pb = pack_pi(pp[0], pp[1]);
@@ -439,12 +478,12 @@ __device__ __forceinline__ void bwd_phase_b(const BwdCtx<SP>& c, const bf16* Ks,
           sv = mfma(lds8(Ks, k0 + c.li, ks * 32 + c.g * 8), qf[ks], sv);
           dp = mfma(lds8(Vs, k0 + c.li, ks * 32 + c.g * 8), dof[ks], dp);
         }
+        // no key mask: a padded key's K and V rows are zero in LDS, so its dS
+        // multiplies a zero K row into dQ; the clamp keeps that dS finite
+        // (exp2 of a real key's argument is <= 0 already: lq is the row's
+        // logsumexp)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int key = k0 + 4 * c.g + e;
-          const float pv = key < c.S ? exp2f(sv[e] * c.sl2 - lq) : 0.f;
-          dss[hf][e] = pv * (dp[e] - dq_d);
-        }
+        for (int e = 0; e < 4; ++e) dss[hf][e] = ex2(fminf(sv[e] * c.sl2 - lq, 0.f)) * (dp[e] - dq_d);
       }
       const bf16x8 dsb = pack_pi(dss[0], dss[1]);
 #pragma unroll
