@@ -109,7 +109,12 @@ __device__ __forceinline__ void store4(bf16* p, const f32x4& v, float s) {
   *reinterpret_cast<bf16x4*>(p) = o;
 }
 
-template <int SP, int NW = 4>
+// QT query tiles per wave pass: every K fragment (ds_read_b128) and V
+// fragment (ds_read_b64_tr_b16) read from LDS feeds QT MFMAs instead of one,
+// halving the LDS read traffic per FLOP at QT = 2 (LDS bandwidth, not MFMA,
+// bounds the QT = 1 loop: 448 LDS cycles vs 224 MFMA cycles per SIMD and
+// 16-query tile); costs QT x the score registers (NKT x 4 each).
+template <int SP, int NW = 4, int QT = 1>
 __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(const bf16* __restrict__ qkv, int64_t ld,
                                                             int S, int H, float scale,
                                                             bf16* __restrict__ o, int64_t ldo,
@@ -124,85 +129,107 @@ __global__ __launch_bounds__(NW * 64, 2) void attn_fwd_kernel(const bf16* __rest
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int nqt = (S + 15) / 16;
-  // This wave's query tiles are wave, wave + NW, ...: their Q fragments are
-  // loaded up front, in flight together with the K / V staging, instead of one
-  // dependent global load at the head of every tile.
-  constexpr int MAXT = (SP / 16 + NW - 1) / NW;
-  bf16x8 qf[MAXT][2];
+  // This wave's query groups (QT tiles each) are wave, wave + NW, ...: their Q
+  // fragments are loaded up front, in flight together with the K / V staging,
+  // instead of one dependent global load at the head of every group.
+  constexpr int NGRP = (NKT + QT - 1) / QT;
+  constexpr int MAXT = (NGRP + NW - 1) / NW;
+  bf16x8 qf[MAXT][QT][2];
 #pragma unroll
-  for (int i = 0; i < MAXT; ++i) {
-    const int qc = min((wave + NW * i) * 16 + li, S - 1);
+  for (int i = 0; i < MAXT; ++i)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) qf[i][ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)qc * ld + ks * 32 + g * 8);
-  }
+    for (int u = 0; u < QT; ++u) {
+      const int qc = min(((wave + NW * i) * QT + u) * 16 + li, S - 1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        qf[i][u][ks] = *reinterpret_cast<const bf16x8*>(qb + (int64_t)qc * ld + ks * 32 + g * 8);
+    }
   stage2<SP, NW * 64>(Ks, qb + D, ld, Vs, qb + 2 * D, ld, S);
   __syncthreads();
   const float sl2 = scale * kLog2e;
 #pragma unroll
   for (int i = 0; i < MAXT; ++i) {
-    const int qt = wave + NW * i;
-    if (qt >= nqt) break;
-    const int q = qt * 16 + li;
-    f32x4 st[NKT];
-    float m = -INFINITY;
+    const int grp = wave + NW * i;
+    if (grp * QT >= nqt) break;
+    f32x4 st[QT][NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+      const bf16x8 k0 = lds8(Ks, kt * 16 + li, g * 8), k1 = lds8(Ks, kt * 16 + li, 32 + g * 8);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) a = mfma(lds8(Ks, kt * 16 + li, ks * 32 + g * 8), qf[i][ks], a);
-      st[kt] = a;
+      for (int u = 0; u < QT; ++u) st[u][kt] = mfma(k1, qf[i][u][1], mfma(k0, qf[i][u][0], f32x4{0.f, 0.f, 0.f, 0.f}));
     }
     // padded keys -> -inf after the whole MFMA chain (a branch inside it would
     // split the block the scheduler hoists the LDS reads across)
     if (S < SP) {
-      // opaque per tile: hoisted out of the head / tile loops, the 4 * NKT
-      // lane masks would live in (spilled) SGPR pairs
+      // opaque per group: hoisted out of the tile loop, the 4 * NKT lane masks
+      // would live in (spilled) SGPR pairs
       int lim = S - 4 * g;
       asm volatile("" : "+v"(lim));
 #pragma unroll
       for (int kt = 0; kt < NKT; ++kt)
         if (kt * 16 + 16 > S) {  // uniform
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (kt * 16 + e >= lim) st[kt][e] = -INFINITY;
+          for (int u = 0; u < QT; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (kt * 16 + e >= lim) st[u][kt][e] = -INFINITY;
         }
     }
+    float mb[QT], l[QT];
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+    for (int u = 0; u < QT; ++u) {
+      float m = -INFINITY;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) m = fmaxf(m, st[kt][e]);
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float mb = m * sl2;
-    float l = 0.f;
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-    for (int kt = 0; kt < NKT; ++kt)
+        for (int e = 0; e < 4; ++e) m = fmaxf(m, st[u][kt][e]);
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      mb[u] = m * sl2;
+      float ls = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float p = ex2(st[kt][e] * sl2 - mb);
-        st[kt][e] = p;
-        l += p;
-      }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    f32x4 acc[4];
+      for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int e = 0; e < 4; ++e) {
+          const float p = ex2(st[u][kt][e] * sl2 - mb[u]);
+          st[u][kt][e] = p;
+          ls += p;
+        }
+      ls += __shfl_xor(ls, 16, 64);
+      l[u] = ls + __shfl_xor(ls, 32, 64);
+    }
+    f32x4 acc[QT][4];
+#pragma unroll
+    for (int u = 0; u < QT; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kc = 0; kc < NKT / 2; ++kc) {
-      float p0[4], p1[4];
+      bf16x8 pb[QT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) { p0[e] = st[2 * kc][e]; p1[e] = st[2 * kc + 1][e]; }
-      const bf16x8 pb = pack_pi(p0, p1);
+      for (int u = 0; u < QT; ++u) {
+        float p0[4], p1[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = mfma(lds_tr8(Vs, kc * 32, t * 16, lane), pb, acc[t]);
+        for (int e = 0; e < 4; ++e) { p0[e] = st[u][2 * kc][e]; p1[e] = st[u][2 * kc + 1][e]; }
+        pb[u] = pack_pi(p0, p1);
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 vf = lds_tr8(Vs, kc * 32, t * 16, lane);
+#pragma unroll
+        for (int u = 0; u < QT; ++u) acc[u][t] = mfma(vf, pb[u], acc[u][t]);
+      }
     }
-    if (q < S) {
-      const float inv = rcp(l);
-      bf16* orow = o + ((int64_t)b * S + q) * ldo + h * DH;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) store4(orow + t * 16 + 4 * g, acc[t], inv);
-      if (g == 0) lse[(int64_t)bh * SP + q] = mb + lg2(l);  // base-2 logsumexp of the scaled scores
+    for (int u = 0; u < QT; ++u) {
+      const int q = (grp * QT + u) * 16 + li;
+      if (q < S) {
+        const float inv = rcp(l[u]);
+        bf16* orow = o + ((int64_t)b * S + q) * ldo + h * DH;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) store4(orow + t * 16 + 4 * g, acc[u][t], inv);
+        if (g == 0) lse[(int64_t)bh * SP + q] = mb[u] + lg2(l[u]);  // base-2 logsumexp of the scaled scores
+      }
     }
   }
 }
@@ -643,16 +670,20 @@ bool attention_supported(int64_t S, int64_t head_dim) { return head_dim == DH &&
 namespace {
 int g_attn_bwd_variant = 0;  // 0: one workgroup per (batch, head); 1: persistent with prefetch
 int g_attn_fwd_variant = 0;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
-                             // next-head prefetch; 2: one 8-wave workgroup per (batch, head)
+                             // next-head prefetch; 2: one 8-wave workgroup per (batch, head);
+                             // 3: as 0 with two query tiles per wave pass
 int g_num_cus_attn = 0;
 }  // namespace
 
 void set_attention_variant(int fwd, int bwd) {
-  TORCH_CHECK(fwd >= 0 && fwd <= 2, "attention forward variant: 0 (per head), 1 (persistent), 2 (per head, 8 waves)");
+  TORCH_CHECK(fwd >= 0 && fwd <= 3, "attention forward variant: 0 (per head), 1 (persistent), 2 (per head, 8 waves), "
+              "3 (per head, 2 query tiles per wave pass)");
   TORCH_CHECK(bwd >= 0 && bwd <= 1, "attention backward variant: 0 (per head), 1 (persistent)");
   g_attn_fwd_variant = fwd;
   g_attn_bwd_variant = bwd;
 }
+
+std::vector<int64_t> get_attention_variant() { return {g_attn_fwd_variant, g_attn_bwd_variant}; }
 
 // qkv [B*S, >= 3*H*64] -> (o [B*S, H*64], lse [B*H, SP] fp32, base-2)
 std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale) {
@@ -674,6 +705,11 @@ std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int6
                                              (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,
                                              (float)scale, (bf16*)o.data_ptr(), o.stride(0),
                                              lse.data_ptr<float>(), nbh));
+  } else if (g_attn_fwd_variant == 3) {
+    DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_fwd_kernel<SPC, 4, 2>), dim3(B * H), dim3(kThreads), 0, st,
+                                             (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,
+                                             (float)scale, (bf16*)o.data_ptr(), o.stride(0),
+                                             lse.data_ptr<float>()));
   } else if (g_attn_fwd_variant == 2) {
     DMP_ATTN_DISPATCH(sp, hipLaunchKernelGGL((attn_fwd_kernel<SPC, 8>), dim3(B * H), dim3(512), 0, st,
                                              (const bf16*)qkv.data_ptr(), qkv.stride(0), (int)S, (int)H,

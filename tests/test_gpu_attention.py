@@ -82,8 +82,25 @@ def test_attention_variants_agree_bitwise():
         g1 = C.attention_backward(do, qkv, o0, l0, B, S, H, 0.125)
         C.set_attention_variant(2, 1)
         o2, l2 = C.attention_forward(qkv, B, S, H, 0.125)
+        C.set_attention_variant(3, 0)
+        o3, l3 = C.attention_forward(qkv, B, S, H, 0.125)
     finally:
         C.set_attention_variant(0, 0)
-    assert torch.equal(o0, o1) and torch.equal(o0, o2)
-    assert torch.equal(l0[:, :S], l1[:, :S]) and torch.equal(l0[:, :S], l2[:, :S])
+    assert torch.equal(o0, o1) and torch.equal(o0, o2) and torch.equal(o0, o3)
+    assert torch.equal(l0[:, :S], l1[:, :S]) and torch.equal(l0[:, :S], l2[:, :S]) and torch.equal(l0[:, :S], l3[:, :S])
     assert torch.equal(g0, g1), "persistent backward differs from the per-head backward"
+
+
+@pytest.mark.unvalidated
+@pytest.mark.parametrize("fv,bv", [(1, 1), (2, 0), (3, 0)])
+@pytest.mark.parametrize("B,S,H", [(4, 197, 12), (2, 17, 3), (2, 130, 2), (1, 256, 2)])
+def test_attention_variant_numerics(fv, bv, B, S, H):
+    """Every forward / backward variant against the fp32 reference, at padded
+    and unpadded lengths (the key-padding masks differ per variant)."""
+    C = _native.require("attention")
+    old = C.get_attention_variant()
+    try:
+        C.set_attention_variant(fv, bv)
+        test_attention_fwd_bwd(B, S, H)
+    finally:
+        C.set_attention_variant(*old)

@@ -35,6 +35,8 @@ def sdpa_path(qkv, heads):
 
 def main():
     B, S, H = int(os.environ.get("B", 128)), 197, 12
+    # VARIANT="f,b" ITERS=n: only that variant, n forward + backward passes (profiling)
+    only = os.environ.get("VARIANT")
     qkv = torch.randn(B, S, 3 * H * 64, device="cuda", dtype=torch.bfloat16, requires_grad=True)
     go = torch.randn(B, S, H * 64, device="cuda", dtype=torch.bfloat16)
     from distributed_model_parallel_amd import _native
@@ -45,8 +47,16 @@ def main():
             C.set_attention_variant(v, vb)
             return A.self_attention_packed(qkv, H)
         return f
+    if only:
+        f = variant(*(int(x) for x in only.split(",")))
+        for _ in range(int(os.environ.get("ITERS", 3))):
+            torch.autograd.grad(f(), qkv, go)
+        torch.cuda.synchronize()
+        print("done", only)
+        return
     for name, fn in (("sdpa+copies", lambda: sdpa_path(qkv, H)), ("hip per-head", variant(0, 0)),
-                     ("hip persistent", variant(1, 1)), ("hip 8-wave fwd", variant(2, 1))):
+                     ("hip persistent", variant(1, 1)), ("hip 8-wave fwd", variant(2, 1)),
+                     ("hip pers fwd + per-head bwd", variant(1, 0)), ("hip 2-tile fwd", variant(3, 0))):
         tf = timeit(lambda: fn())
         o = fn()
         tb = timeit(lambda: torch.autograd.grad(o, qkv, go, retain_graph=True))
