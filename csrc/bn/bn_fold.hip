@@ -27,6 +27,13 @@ using bf16 = __bf16;
 constexpr int kFoldThreads = 256;
 constexpr int kFwdRows = 8;      // output channels per forward block (2 blocks / CU)
 constexpr int kMaxCin = 1024;
+// 1: the two [Cout x Cin x Cin] / [Cin x Cin x Cout] products (W G and
+// W^T diag(be) W) as library fp32 GEMMs (hipBLASLt) -- they are plain GEMMs,
+// and the VALU kernels ran them at ~8 TF/s with one block per CU (2.1 ms of
+// a 23 ms batch-256 ResNet-50 step: the algebra does not shrink with the
+// batch); 0: the fused VALU kernels (fold_fwd_kernel, role B of
+// fold_bwd_coef_kernel)
+int g_fold_blas = 1;
 
 // grid = Cout / kFwdRows.  Thread t owns columns j = t + 256 q (q < NQ) of WG rows
 // k0..k0+7; G streams through LDS in 4-row chunks (double buffered), so the
@@ -108,6 +115,29 @@ __global__ __launch_bounds__(kFoldThreads, 2) void fold_fwd_kernel(const bf16* _
     sums[which * Cout + k0 + r] = t;  // sum_m y[m, k] | sum_m y[m, k]^2
   }
   if (blockIdx.x == 0 && tid == 0) sums[2 * Cout] = asums[2 * Cin];  // rows
+}
+
+// Forward row sums from a library WG = W G (fold_blas mode): one wave per
+// output channel, sums = [W s, rowdot(WG, W)] in fp64, plus the row count.
+__global__ __launch_bounds__(kFoldThreads) void fold_fwd_sums_kernel(const bf16* __restrict__ W,
+                                                                     const float* __restrict__ WG,
+                                                                     const double* __restrict__ asums, int Cout,
+                                                                     int Cin, double* __restrict__ sums) {
+  const int k = blockIdx.x * (kFoldThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (k >= Cout) return;
+  double qd = 0.0, md = 0.0;
+  for (int i = lane; i < Cin; i += 64) {
+    const double w = (double)(float)W[(int64_t)k * Cin + i];
+    qd += (double)WG[(int64_t)k * Cin + i] * w;
+    md += w * asums[i];
+  }
+  qd = wave_sum(qd);
+  md = wave_sum(md);
+  if (lane == 0) {
+    sums[k] = md;          // sum_m y[m, k]
+    sums[Cout + k] = qd;   // sum_m y[m, k]^2
+    if (k == 0) sums[2 * Cout] = asums[2 * Cin];  // rows
+  }
 }
 
 // One wave per output channel.  local = [sdz, sum dz*(y - mean)].
@@ -398,6 +428,14 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
   check_f32(G, Cin * Cin, "G");
   check_f64(asums, 2 * Cin + 1, "asums");
   auto sums = at::empty({2 * Cout + 1}, W.options().dtype(at::kDouble));
+  if (g_fold_blas) {
+    auto WG = at::mm(W.to(at::kFloat), G.view({Cin, Cin}));
+    hipLaunchKernelGGL(fold_fwd_sums_kernel, dim3((unsigned)((Cout + 3) / 4)), dim3(kFoldThreads), 0,
+                       at::hip::getCurrentHIPStream(), reinterpret_cast<const bf16*>(W.data_ptr()),
+                       WG.data_ptr<float>(), asums.data_ptr<double>(), (int)Cout, (int)Cin, sums.data_ptr<double>());
+    DMP_HIP_CHECK(hipGetLastError());
+    return {sums, WG};
+  }
   auto WG = at::empty({Cout, Cin}, W.options().dtype(at::kFloat));
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3((unsigned)(Cout / kFwdRows)), dim3(kFoldThreads), 0,
@@ -469,6 +507,16 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   p.ebias = ebias.data_ptr<float>();
   p.Cout = (int)Cout; p.Cin = (int)Cin;
   p.nA = (int)((Cout / kTK) * (Cin / kTI));
+  if (g_fold_blas) {
+    // role A in the kernel; role B = W^T diag(be) W and ebias = W^T c as library fp32 products
+    hipLaunchKernelGGL(fold_bwd_coef_kernel<1>, dim3((unsigned)p.nA), dim3(kFoldThreads), 0, stream, p);
+    DMP_HIP_CHECK(hipGetLastError());
+    const auto Wf = W.to(at::kFloat);
+    const auto WfT = Wf.t();
+    Bm.narrow(1, Cout, Cin).copy_(at::mm(WfT * coef.select(0, 1), Wf));
+    ebias.copy_(at::mv(WfT, coef.select(0, 2)));
+    return {dW, dgb[0], dgb[1], Bm, ebias};
+  }
   // split the channel range until role B has >= 256 blocks (one per CU), chunks of kKC channels
   int ksplit = 1;
   while ((Cin / kTR) * ksplit < 256 && Cout % (2 * ksplit * kKC) == 0) ksplit *= 2;
@@ -488,6 +536,9 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   DMP_HIP_CHECK(hipGetLastError());
   return {dW, dgb[0], dgb[1], Bm, ebias};
 }
+
+void set_fold_blas(int on) { g_fold_blas = on ? 1 : 0; }
+int get_fold_blas() { return g_fold_blas; }
 
 // fp64 [2C+1] = (colsum, colsum of squares, rows) of x's rows sampled through
 // map [s, Ho, Wo, Hi, Wi] (empty: all rows).
