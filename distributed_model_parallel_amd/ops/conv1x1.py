@@ -197,11 +197,16 @@ _TN_XL = not _native.disabled("tn_xl")
 _STATS["tn_xl"] = 0
 
 
+_TN_XL_MIN_ROWS = 150_000
+
+
 def _tn_xl(m: int, cout: int, cin: int) -> bool:
     """Ping-pong TN weight gradient: layer-3-sized 1x1 convs (both output dims
     >= 256, M >= 150k rows), where it measured 0.17 vs 0.20 ms
-    (tools/tn_xl_bench.py); deeper-K / shorter-M layer-4 shapes tie."""
-    return _TN_XL and cout >= 256 and cin >= 256 and m >= 150_000
+    (tools/tn_xl_bench.py); deeper-K / shorter-M layer-4 shapes tie.  (The
+    224-px convergence test lowers the row threshold so its batch-64 run
+    trains through this route too.)"""
+    return _TN_XL and cout >= 256 and cin >= 256 and m >= _TN_XL_MIN_ROWS
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,
