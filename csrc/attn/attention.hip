@@ -668,8 +668,11 @@ void check_2d(const at::Tensor& t, const char* name, int64_t rows, int64_t min_c
 bool attention_supported(int64_t S, int64_t head_dim) { return head_dim == DH && S >= 1 && S <= 256; }
 
 namespace {
+// defaults measured at ViT-B/16 batch 256 (tools/attn_bench.py, profiles/raw_r4/attn_bench_r4e.log):
+// forward 8-wave 0.081 ms vs 4-wave 0.090 / two-tile 0.084 / persistent 0.096;
+// backward per-head 0.249-0.258 ms vs persistent 0.264-0.266
 int g_attn_bwd_variant = 0;  // 0: one workgroup per (batch, head); 1: persistent with prefetch
-int g_attn_fwd_variant = 0;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
+int g_attn_fwd_variant = 2;  // 0: one 4-wave workgroup per (batch, head); 1: persistent with
                              // next-head prefetch; 2: one 8-wave workgroup per (batch, head);
                              // 3: as 0 with two query tiles per wave pass
 int g_num_cus_attn = 0;

@@ -333,7 +333,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
   m.def("get_gemm_xl_pipe", &dmp::get_gemm_xl_pipe);
   m.def("set_gemm_xl_x2", &dmp::set_gemm_xl_x2, py::arg("mode"),
-        "conv-epilogue GEMMs on the two-blocks-per-CU 256x128 kernel: 0 off, 1 short K (<= 512), 2 always");
+        "conv-epilogue GEMMs on the two-blocks-per-CU 256x128 kernel: 0 off, 1 where N % 256 != 0, 2 always");
   m.def("get_gemm_xl_x2", &dmp::get_gemm_xl_x2);
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,

@@ -1723,13 +1723,16 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
 }
 
-// two-blocks-per-CU short-K kernel (gemm_x2_kernel): 0 = off, 1 = where it
-// measured faster (short K), 2 = every conv-epilogue GEMM with N % 128 == 0
-int g_xl_x2 = 0;
+// two-blocks-per-CU kernel (gemm_x2_kernel): 0 = off, 1 = where it measured
+// faster than this kernel's 256 x 128 tile (N = 128 + 256 j: 1.14-1.59x on
+// ResNet-50 l2 conv1 at batch 256, profiles/raw_r4/x2_bench_r4d.md; on
+// N % 256 == 0 the 256 x 256 tile wins 0.76-1.08x), 2 = every conv-epilogue
+// GEMM with N % 128 == 0 (A/B)
+int g_xl_x2 = 1;
 
 bool use_x2(const XlArgs& a) {
   if (g_xl_x2 == 0 || a.N % X2_BN != 0) return false;
-  return g_xl_x2 == 2 || a.K <= 512;
+  return g_xl_x2 == 2 || a.N % 256 != 0;
 }
 
 template <int EPI>

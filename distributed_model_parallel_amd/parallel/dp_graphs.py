@@ -77,6 +77,10 @@ class GraphedReplicas:
             x.copy_(chunk)
             self.inputs.append(x)
         self.rparams = [list(r.parameters()) for r in self.replicas]
+        # one stream per replica: replicas sharing a device replay concurrently
+        # (a 64-image ResNet-50 pass leaves most of an MI355X idle); autograd
+        # runs each replica's backward graph on the stream its forward used
+        self.streams = [torch.cuda.Stream(device=d) for d in self.devices]
         self.rbuffers = [list(r.buffers()) for r in self.replicas]
         self.graphed = []
         # the capture's warm-up iterations run replica 0 for real: keep the
@@ -113,8 +117,15 @@ class _GraphedDPFn(torch.autograd.Function):
         with torch.no_grad():
             for x, c in zip(gr.inputs, chunks):
                 x.copy_(c, non_blocking=True)
+        mains = {d: torch.cuda.current_stream(d) for d in gr.devices}
+        outs = []
         with torch.enable_grad():
-            outs = [g(x) for g, x in zip(gr.graphed, gr.inputs)]
+            for g, x, d, st in zip(gr.graphed, gr.inputs, gr.devices, gr.streams):
+                st.wait_stream(mains[d])  # refreshed parameters and copied inputs
+                with torch.cuda.stream(st):
+                    outs.append(g(x))
+        for d, st in zip(gr.devices, gr.streams):
+            mains[d].wait_stream(st)
         ctx.gr, ctx.outs = gr, outs
         ctx.sizes = [o.shape[0] for o in outs]
         return comm_ops.gather_tensors([o.detach() for o in outs], output_device, 0)

@@ -282,15 +282,29 @@ def test_replica_cache_attrs_concurrency_and_lifetime():
     assert ref() is None, "the replica cache kept the network alive"
 
 
+def _grad_rel(ref: torch.nn.Module, other: torch.nn.Module) -> float:
+    num = den = 0.0
+    for a, b in zip(ref.parameters(), other.parameters()):
+        num += (a.grad.float() - b.grad.float()).pow(2).sum().item()
+        den += a.grad.float().pow(2).sum().item()
+    return (num / den) ** 0.5
+
+
 @pytest.mark.gpu
 @pytest.mark.unvalidated
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
 def test_dp_graphed_replicas_match_eager(arch):
     """DataParallel(graphs=True) (parallel/dp_graphs.py: static replicas whose
-    forward / backward are captured hipGraphs) against the eager thread path:
-    outputs, parameter gradients and running statistics over three steps with
-    optimizer updates between them (the replicas must re-read the updated
-    weights every step)."""
+    forward / backward are captured hipGraphs, replayed on per-replica streams)
+    and the eager thread path, both against one module running the replicas'
+    chunks one after another (per-chunk BN statistics, outputs concatenated
+    before the loss: DataParallel's math), over three steps with optimizer
+    updates between them (the replicas must re-read the updated weights).
+
+    bf16 BN over a few images is noisy (round 4, tools/dp_graph_diag.py:
+    eager and graphed both sit 7-10 % from the reference in gradient norm at
+    4 images per replica), so the graphed path must be as close to the
+    reference as the eager one is, not bitwise equal to it."""
     import copy as _copy
     from distributed_model_parallel_amd.models import build_model
     from distributed_model_parallel_amd.ops.loss import cross_entropy
@@ -298,29 +312,29 @@ def test_dp_graphed_replicas_match_eager(arch):
     torch.manual_seed(0)
     base = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
     cast_model(base, torch.bfloat16)
-    m_e, m_g = base, _copy.deepcopy(base)
+    m_e, m_g, m_s = base, _copy.deepcopy(base), _copy.deepcopy(base)
     dp_e = DataParallel(m_e, device_ids=[0, 0, 0, 0])
     dp_g = DataParallel(m_g, device_ids=[0, 0, 0, 0], graphs=True)
-    opt_e = torch.optim.SGD(m_e.parameters(), lr=0.05)
-    opt_g = torch.optim.SGD(m_g.parameters(), lr=0.05)
+    opts = [torch.optim.SGD(m.parameters(), lr=0.05) for m in (m_e, m_g, m_s)]
     for step in range(3):
-        x = torch.randn(16, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-        y = torch.arange(16, device="cuda") % 10
+        x = torch.randn(64, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        y = torch.arange(64, device="cuda") % 10
         outs = []
-        for dp, opt in ((dp_e, opt_e), (dp_g, opt_g)):
+        for dp in (dp_e, dp_g, lambda v: torch.cat([m_s(c) for c in v.chunk(4)])):
             out = dp(x)
             cross_entropy(out, y).backward()
             outs.append(out.float())
-        torch.testing.assert_close(outs[1], outs[0], atol=3e-2, rtol=3e-2)
-        num = den = 0.0
-        for a, b in zip(m_e.parameters(), m_g.parameters()):
-            num += (a.grad.float() - b.grad.float()).pow(2).sum().item()
-            den += a.grad.float().pow(2).sum().item()
-        assert (num / den) ** 0.5 < 3e-2, (step, (num / den) ** 0.5)
-        for opt in (opt_e, opt_g):
+        e_out = (outs[0] - outs[2]).abs().max().item()
+        g_out = (outs[1] - outs[2]).abs().max().item()
+        assert g_out <= 2 * e_out + 2e-2, (step, g_out, e_out)
+        e_rel, g_rel = _grad_rel(m_s, m_e), _grad_rel(m_s, m_g)
+        assert g_rel <= 1.5 * e_rel + 1e-2, (step, g_rel, e_rel)
+        for opt in opts:
             opt.step()
             opt.zero_grad()
     assert dp_g._graphed is not None, "graphed path not taken"
+    # running statistics: DataParallel updates them from replica 0's chunk only
+    # (the single-module reference updates them per chunk), eager == graphed
     for (n, a), b in zip(m_e.named_buffers(), m_g.buffers()):
         if a.dtype.is_floating_point:
             torch.testing.assert_close(b.float(), a.float(), atol=3e-2, rtol=3e-2, msg=n)

@@ -9,7 +9,7 @@ import torch
 
 from distributed_model_parallel_amd import _native
 
-pytestmark = [pytest.mark.gpu, pytest.mark.unvalidated]
+pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
