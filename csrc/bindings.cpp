@@ -167,8 +167,8 @@ std::vector<at::Tensor> bn_fold_scale_concat(const at::Tensor& W3, const at::Ten
 // attention.hip
 bool attention_supported(int64_t S, int64_t head_dim);
 void set_attention_variant(int fwd, int bwd);
-void set_fold_blas(int on);
-int get_fold_blas();
+void set_fold_gemm(int mode);
+int get_fold_gemm();
 std::vector<int64_t> get_attention_variant();
 std::vector<at::Tensor> attention_forward(const at::Tensor& qkv, int64_t B, int64_t S, int64_t H, double scale);
 at::Tensor attention_backward(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& o,
@@ -357,9 +357,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- fused self-attention on packed qkv (ViT) ----
   m.def("attention_supported", &dmp::attention_supported);
-  m.def("set_fold_blas", &dmp::set_fold_blas, py::arg("on"),
-        "BN-fold coefficient products: 1 library fp32 GEMMs (default), 0 the fused VALU kernels");
-  m.def("get_fold_blas", &dmp::get_fold_blas);
+  m.def("set_fold_gemm", &dmp::set_fold_gemm, py::arg("mode"),
+        "BN-fold coefficient products: 0 fused VALU kernels, 1 library fp32 GEMMs, 2 tiled kernel (default)");
+  m.def("get_fold_gemm", &dmp::get_fold_gemm);
   m.def("get_attention_variant", &dmp::get_attention_variant);
   m.def("set_attention_variant", &dmp::set_attention_variant, py::arg("fwd"), py::arg("bwd") = 1,
         "attention kernels: fwd 0 = one workgroup per (batch, head), 1 = persistent with next-head prefetch, "

@@ -27,13 +27,17 @@ using bf16 = __bf16;
 constexpr int kFoldThreads = 256;
 constexpr int kFwdRows = 8;      // output channels per forward block (2 blocks / CU)
 constexpr int kMaxCin = 1024;
-// 1: the two [Cout x Cin x Cin] / [Cin x Cin x Cout] products (W G and
-// W^T diag(be) W) as library fp32 GEMMs (hipBLASLt) -- they are plain GEMMs,
-// and the VALU kernels ran them at ~8 TF/s with one block per CU (2.1 ms of
-// a 23 ms batch-256 ResNet-50 step: the algebra does not shrink with the
-// batch); 0: the fused VALU kernels (fold_fwd_kernel, role B of
-// fold_bwd_coef_kernel)
-int g_fold_blas = 1;
+// How the two [Cout x Cin x Cin] / [Cin x Cin x Cout] products of the fold
+// (W G forward, W^T diag(be) W and c^T W backward) run:
+//   0  the fused VALU kernels (fold_fwd_kernel, role B of fold_bwd_coef_kernel):
+//      one block per CU, ~8 TF/s, 2.4 ms of a 23 ms batch-256 ResNet-50 step
+//      (the algebra does not shrink with the batch);
+//   1  library fp32 GEMMs (hipBLASLt): fast kernels, but 30-280 us of host
+//      time per call stalls the launch-bound batch-256 forward;
+//   2  fold_sgemm_kernel: a 64 x 64-tiled fp32 GEMM reading W (bf16) and G /
+//      the coefficients directly (no fp32 copies, no concatenated operand),
+//      with the backward's epilogue writing Bm's bf16 block and ebias in place.
+int g_fold_gemm = 2;
 
 // grid = Cout / kFwdRows.  Thread t owns columns j = t + 256 q (q < NQ) of WG rows
 // k0..k0+7; G streams through LDS in 4-row chunks (double buffered), so the
@@ -117,7 +121,97 @@ __global__ __launch_bounds__(kFoldThreads, 2) void fold_fwd_kernel(const bf16* _
   if (blockIdx.x == 0 && tid == 0) sums[2 * Cout] = asums[2 * Cin];  // rows
 }
 
-// Forward row sums from a library WG = W G (fold_blas mode): one wave per
+// ---- fold_sgemm_kernel: C[m][n] = sum_k A(m, k) B(k, n), fp32 accumulation ----
+// 64 x 64 tile per 256-thread block, 4 x 4 outputs per thread, K staged
+// through LDS 16 at a time (register-prefetched one chunk ahead).
+//   FWD: A(m, k) = W[m][k] (bf16 [Cout, Cin]), B(k, n) = G[k][n] (fp32 [Cin, Cin]);
+//        C = WG fp32 [Cout, Cin]
+//   BWD: A(m, k) = be[k] W[k][m] for m < Cin, c[k] for m == Cin (the rows of
+//        [W^T diag(be) ; c^T], built on load from W and the coefficients),
+//        B(k, n) = W[k][n]; rows m < Cin go to Bm[m][Cout + n] (bf16), row Cin
+//        to ebias[n]  (W^T diag(be) W is symmetric: its rows are Bm's columns)
+constexpr int kSgT = 64, kSgK = 16;
+template <bool BWD>
+__global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __restrict__ W,
+                                                                  const float* __restrict__ G,
+                                                                  const float* __restrict__ be,
+                                                                  const float* __restrict__ cc, int M, int N,
+                                                                  int K, float* __restrict__ C,
+                                                                  bf16* __restrict__ Bm, int ldbm, int bm_off,
+                                                                  float* __restrict__ ebias) {
+  __shared__ __attribute__((aligned(16))) float As[kSgK][kSgT + 4];
+  __shared__ __attribute__((aligned(16))) float Bs[kSgK][kSgT + 4];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int m0 = blockIdx.y * kSgT, n0 = blockIdx.x * kSgT;
+  // loaders: A as [kk][m] (4 elements per thread), B as [kk][n] (4 per thread)
+  float ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * kFoldThreads;  // 0..1023
+      if constexpr (BWD) {
+        const int kk = e >> 6, m = e & 63, k = k0 + kk, mm = m0 + m;  // coalesced along m
+        float v = 0.f;
+        if (k < K) v = mm < N ? be[k] * (float)W[(int64_t)k * N + mm] : (mm == N ? cc[k] : 0.f);
+        ra[u] = v;
+      } else {
+        const int m = e >> 4, kk = e & 15, k = k0 + kk, mm = m0 + m;  // 16 consecutive k per row
+        ra[u] = (mm < M && k < K) ? (float)W[(int64_t)mm * K + k] : 0.f;
+      }
+      const int kk = e >> 6, n = e & 63, k = k0 + kk;
+      if constexpr (BWD) rb[u] = k < K ? (float)W[(int64_t)k * N + n0 + n] : 0.f;
+      else rb[u] = k < K ? G[(int64_t)k * N + n0 + n] : 0.f;
+    }
+  };
+  auto store = [&] {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + u * kFoldThreads;
+      if constexpr (BWD) As[e >> 6][e & 63] = ra[u];
+      else As[e & 15][e >> 4] = ra[u];
+      Bs[e >> 6][e & 63] = rb[u];
+    }
+  };
+  float acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += kSgK) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (k0 + kSgK < K) load(k0 + kSgK);  // next chunk in flight during this one's FMAs
+#pragma unroll
+    for (int kk = 0; kk < kSgK; ++kk) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&As[kk][ty * 4]);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(&Bs[kk][tx * 4]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + ty * 4 + i;
+    if (m >= M) continue;
+    const int n = n0 + tx * 4;
+    if constexpr (BWD) {
+      if (m < N) {
+        bf16x4 v = {(bf16)acc[i][0], (bf16)acc[i][1], (bf16)acc[i][2], (bf16)acc[i][3]};
+        *reinterpret_cast<bf16x4*>(Bm + (int64_t)m * ldbm + bm_off + n) = v;
+      } else {
+        *reinterpret_cast<f32x4*>(ebias + n) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+      }
+    } else {
+      *reinterpret_cast<f32x4*>(C + (int64_t)m * N + n) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+    }
+  }
+}
+
+// Forward row sums from WG = W G (fold_gemm modes 1, 2): one wave per
 // output channel, sums = [W s, rowdot(WG, W)] in fp64, plus the row count.
 __global__ __launch_bounds__(kFoldThreads) void fold_fwd_sums_kernel(const bf16* __restrict__ W,
                                                                      const float* __restrict__ WG,
@@ -173,6 +267,8 @@ struct FoldBwdArgs {
   int ksplit;           // role B: channel (K) range split over this many blocks per row group
   float* bpart;         // role B partials [ksplit][Cin][Cin]
   float* epart;         // role B ebias partials [ksplit][Cin]
+  float* Wf;            // fold_gemm 1: fp32 copy of W [Cout, Cin] (role A writes it)
+  float* R;             // fold_gemm 1: [Cout, Cin + 1] = [be o W | c] (role A writes it)
 };
 
 // al, be, c per output channel from the (all-reduced) backward sums -- once,
@@ -219,7 +315,13 @@ __global__ __launch_bounds__(kFoldThreads) void fold_bwd_coef_kernel(const FoldB
       const int64_t o = (int64_t)k * Cin + i;
       const float dw = fmaf(al, p.D[o], fmaf(be, p.WG[o], (float)((double)c * p.s[i])));
       p.dW[o] = (bf16)dw;
-      tr[il][r] = al * (float)p.W[o];
+      const float w = (float)p.W[o];
+      tr[il][r] = al * w;
+      if (p.R) {  // operands of the library product [W^T diag(be) W ; c^T W] = [be o W | c]^T W
+        p.Wf[o] = w;
+        p.R[(int64_t)k * (Cin + 1) + i] = be * w;
+        if (i == Cin - 1) p.R[(int64_t)k * (Cin + 1) + Cin] = c;
+      }
       if (i0 == 0 && il == 0) {
         p.dgamma[k] = (float)(p.local[Cout + k] * (double)p.invstd[k]);
         p.dbeta[k] = (float)p.local[k];
@@ -428,7 +530,19 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
   check_f32(G, Cin * Cin, "G");
   check_f64(asums, 2 * Cin + 1, "asums");
   auto sums = at::empty({2 * Cout + 1}, W.options().dtype(at::kDouble));
-  if (g_fold_blas) {
+  if (g_fold_gemm == 2) {
+    auto WG = at::empty({Cout, Cin}, W.options().dtype(at::kFloat));
+    hipStream_t stream = at::hip::getCurrentHIPStream();
+    hipLaunchKernelGGL(fold_sgemm_kernel<false>, dim3((unsigned)(Cin / kSgT), (unsigned)((Cout + kSgT - 1) / kSgT)),
+                       dim3(kFoldThreads), 0, stream, reinterpret_cast<const bf16*>(W.data_ptr()), G.data_ptr<float>(),
+                       nullptr, nullptr, (int)Cout, (int)Cin, (int)Cin, WG.data_ptr<float>(), nullptr, 0, 0, nullptr);
+    hipLaunchKernelGGL(fold_fwd_sums_kernel, dim3((unsigned)((Cout + 3) / 4)), dim3(kFoldThreads), 0, stream,
+                       reinterpret_cast<const bf16*>(W.data_ptr()), WG.data_ptr<float>(), asums.data_ptr<double>(),
+                       (int)Cout, (int)Cin, sums.data_ptr<double>());
+    DMP_HIP_CHECK(hipGetLastError());
+    return {sums, WG};
+  }
+  if (g_fold_gemm == 1) {
     auto WG = at::mm(W.to(at::kFloat), G.view({Cin, Cin}));
     hipLaunchKernelGGL(fold_fwd_sums_kernel, dim3((unsigned)((Cout + 3) / 4)), dim3(kFoldThreads), 0,
                        at::hip::getCurrentHIPStream(), reinterpret_cast<const bf16*>(W.data_ptr()),
@@ -507,15 +621,30 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   p.ebias = ebias.data_ptr<float>();
   p.Cout = (int)Cout; p.Cin = (int)Cin;
   p.nA = (int)((Cout / kTK) * (Cin / kTI));
-  if (g_fold_blas) {
-    // role A in the kernel; role B = W^T diag(be) W and ebias = W^T c as library fp32 products
+  if (g_fold_gemm == 2) {
+    // role A in the coefficient kernel; [W^T diag(be) W ; c^T W] in the tiled
+    // kernel, straight into Bm's second block and ebias
+    hipLaunchKernelGGL(fold_bwd_coef_kernel<1>, dim3((unsigned)p.nA), dim3(kFoldThreads), 0, stream, p);
+    hipLaunchKernelGGL(fold_sgemm_kernel<true>, dim3((unsigned)(Cin / kSgT), (unsigned)((Cin + 1 + kSgT - 1) / kSgT)),
+                       dim3(kFoldThreads), 0, stream, p.W, nullptr, coef.data_ptr<float>() + Cout,
+                       coef.data_ptr<float>() + 2 * Cout, (int)(Cin + 1), (int)Cin, (int)Cout, nullptr, p.Bm,
+                       (int)(Cout + Cin), (int)Cout, p.ebias);
+    DMP_HIP_CHECK(hipGetLastError());
+    return {dW, dgb[0], dgb[1], Bm, ebias};
+  }
+  if (g_fold_gemm == 1) {
+    // role A in the kernel (also writing fp32 W and R = [be o W | c]); role B and
+    // ebias as ONE library fp32 product R^T W = [W^T diag(be) W ; c^T W]
+    // (W^T diag(be) W is symmetric, so its rows are Bm's columns as they are)
+    auto Wf = at::empty({Cout, Cin}, W.options().dtype(at::kFloat));
+    auto R = at::empty({Cout, Cin + 1}, W.options().dtype(at::kFloat));
+    p.Wf = Wf.data_ptr<float>();
+    p.R = R.data_ptr<float>();
     hipLaunchKernelGGL(fold_bwd_coef_kernel<1>, dim3((unsigned)p.nA), dim3(kFoldThreads), 0, stream, p);
     DMP_HIP_CHECK(hipGetLastError());
-    const auto Wf = W.to(at::kFloat);
-    const auto WfT = Wf.t();
-    Bm.narrow(1, Cout, Cin).copy_(at::mm(WfT * coef.select(0, 1), Wf));
-    ebias.copy_(at::mv(WfT, coef.select(0, 2)));
-    return {dW, dgb[0], dgb[1], Bm, ebias};
+    const auto out = at::mm(R.t(), Wf);  // [Cin + 1, Cin]
+    Bm.narrow(1, Cout, Cin).copy_(out.narrow(0, 0, Cin));
+    return {dW, dgb[0], dgb[1], Bm, out.select(0, Cin)};
   }
   // split the channel range until role B has >= 256 blocks (one per CU), chunks of kKC channels
   int ksplit = 1;
@@ -537,8 +666,11 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
   return {dW, dgb[0], dgb[1], Bm, ebias};
 }
 
-void set_fold_blas(int on) { g_fold_blas = on ? 1 : 0; }
-int get_fold_blas() { return g_fold_blas; }
+void set_fold_gemm(int mode) {
+  TORCH_CHECK(mode >= 0 && mode <= 2, "fold gemm mode: 0 VALU kernels, 1 library, 2 tiled kernel");
+  g_fold_gemm = mode;
+}
+int get_fold_gemm() { return g_fold_gemm; }
 
 // fp64 [2C+1] = (colsum, colsum of squares, rows) of x's rows sampled through
 // map [s, Ho, Wo, Hi, Wi] (empty: all rows).

@@ -259,20 +259,21 @@ def test_fold_ds_kernels():
     _check(out_xl, ref, 1e-2)
 
 
-@pytest.fixture(params=[1, 0], ids=["blas", "valu"])
+@pytest.fixture(params=[2, 1, 0], ids=["tiled", "blas", "valu"])
 def fold_mode(request):
     C = _native.require("fold kernels")
-    old = C.get_fold_blas()
-    C.set_fold_blas(request.param)
+    old = C.get_fold_gemm()
+    C.set_fold_gemm(request.param)
     yield request.param
-    C.set_fold_blas(old)
+    C.set_fold_gemm(old)
 
 
 @pytest.mark.parametrize("cout,cin", [(256, 64), (512, 128), (1024, 256), (2048, 512), (2048, 1024), (512, 256)])
 def test_fold_coefficient_kernels_match_fp64(cout, cin, fold_mode):
     """bn_fold_fwd / bn_fold_bwd_sums / bn_fold_bwd_coef against the same
     algebra in fp64 torch ops (the framework's CPU path), with the coefficient
-    products as library fp32 GEMMs (blas) and as the fused VALU kernels."""
+    products on the tiled fp32 kernel, as library fp32 GEMMs and on the fused
+    VALU kernels."""
     C = _native.require("fold kernels")
     torch.manual_seed(5)
     W = (torch.randn(cout, cin, device=DEV) * 0.05).bfloat16()

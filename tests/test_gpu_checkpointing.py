@@ -18,28 +18,51 @@ from distributed_model_parallel_amd.utils.precision import cast_model
 pytestmark = pytest.mark.gpu
 
 
+def _grad_rel(a_mod, b_mod):
+    num = den = 0.0
+    for a, b in zip(a_mod.parameters(), b_mod.parameters()):
+        num += (a.grad.float() - b.grad.float()).pow(2).sum().item()
+        den += a.grad.float().pow(2).sum().item()
+    return (num / max(den, 1e-30)) ** 0.5
+
+
 @pytest.mark.unvalidated
 @pytest.mark.parametrize("arch,size", [("resnet50", 64), ("mobilenetv2", 32)])
-def test_checkpointed_step_matches_plain(arch, size):
+def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
+    """Reference: the same segments run WITHOUT recomputation but inside the
+    checkpoint context (so the same unfused kernels run): the checkpointed
+    step's recompute must rebuild the first forward's saved tensors exactly,
+    so loss, gradients and running statistics match it to rounding.  The
+    plain fused step is a looser sanity bound (different kernels; bf16 BN over
+    8 images amplifies their rounding differences: 3 % in the loss, round 4)."""
+    from distributed_model_parallel_amd.utils import checkpointing
     torch.manual_seed(0)
     m = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
     cast_model(m, torch.bfloat16)
-    m2 = copy.deepcopy(m)
+    m2, m3 = copy.deepcopy(m), copy.deepcopy(m)
     enable_activation_checkpointing(m2, 4)
+    enable_activation_checkpointing(m3, 4)
     x = torch.randn(8, 3, size, size, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     y = torch.arange(8, device="cuda") % 10
     l1 = cross_entropy(m(x), y)
     l1.backward()
     l2 = cross_entropy(m2(x), y)
     l2.backward()
-    torch.testing.assert_close(l2.float(), l1.float(), atol=2e-2, rtol=2e-2)
-    num = den = 0.0
-    for a, b in zip(m.parameters(), m2.parameters()):
-        num += (a.grad.float() - b.grad.float()).pow(2).sum().item()
-        den += a.grad.float().pow(2).sum().item()
-    assert (num / max(den, 1e-30)) ** 0.5 < 0.05, f"relative grad error {(num / den) ** 0.5:.3g}"
-    for (n, a), b in zip(m.named_buffers(), m2.buffers()):
+
+    def no_recompute(fn, *args, **kw):
+        with checkpointing._flags(False):
+            return fn(*args)
+    monkeypatch.setattr(checkpointing, "checkpoint", no_recompute)
+    l3 = cross_entropy(m3(x), y)
+    l3.backward()
+    monkeypatch.undo()
+    torch.testing.assert_close(l2.float(), l3.float(), atol=1e-3, rtol=1e-3)
+    rel = _grad_rel(m3, m2)
+    assert rel < 1e-2, f"checkpointed vs same-kernel reference: relative grad error {rel:.3g}"
+    for (n, a), b in zip(m3.named_buffers(), m2.buffers()):
         if a.dtype.is_floating_point:
-            torch.testing.assert_close(a.float(), b.float(), atol=2e-2, rtol=2e-2, msg=n)
+            torch.testing.assert_close(b.float(), a.float(), atol=1e-3, rtol=1e-3, msg=n)
         else:
             assert torch.equal(a, b), n  # num_batches_tracked: one update, not two
+    torch.testing.assert_close(l2.float(), l1.float(), atol=0.1, rtol=0.1)
+    assert _grad_rel(m, m2) < 0.3
