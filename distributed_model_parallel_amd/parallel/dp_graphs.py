@@ -80,7 +80,12 @@ class GraphedReplicas:
         # one stream per replica: replicas sharing a device replay concurrently
         # (a 64-image ResNet-50 pass leaves most of an MI355X idle); autograd
         # runs each replica's backward graph on the stream its forward used
-        self.streams = [torch.cuda.Stream(device=d) for d in self.devices]
+        # (DMP_DP_GRAPH_STREAMS=0: replay everything on the current stream)
+        import os
+        if os.environ.get("DMP_DP_GRAPH_STREAMS", "1") == "1":
+            self.streams = [torch.cuda.Stream(device=d) for d in self.devices]
+        else:
+            self.streams = [torch.cuda.current_stream(d) for d in self.devices]
         self.rbuffers = [list(r.buffers()) for r in self.replicas]
         self.graphed = []
         # the capture's warm-up iterations run replica 0 for real: keep the
