@@ -358,7 +358,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // ---- fused self-attention on packed qkv (ViT) ----
   m.def("attention_supported", &dmp::attention_supported);
   m.def("set_fold_gemm", &dmp::set_fold_gemm, py::arg("mode"),
-        "BN-fold coefficient products: 0 fused VALU kernels, 1 library fp32 GEMMs, 2 tiled kernel (default)");
+        "BN-fold coefficient products: 0 fused VALU kernels, 1 library fp32 GEMMs (default), 2 tiled kernel");
   m.def("get_fold_gemm", &dmp::get_fold_gemm);
   m.def("get_attention_variant", &dmp::get_attention_variant);
   m.def("set_attention_variant", &dmp::set_attention_variant, py::arg("fwd"), py::arg("bwd") = 1,

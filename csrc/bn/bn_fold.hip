@@ -37,7 +37,9 @@ constexpr int kMaxCin = 1024;
 //   2  fold_sgemm_kernel: a 64 x 64-tiled fp32 GEMM reading W (bf16) and G /
 //      the coefficients directly (no fp32 copies, no concatenated operand),
 //      with the backward's epilogue writing Bm's bf16 block and ebias in place.
-int g_fold_gemm = 2;
+// Default 1: batch-256 step 22.0 ms (1) vs 23.3 (0) vs 24.3 (2), interleaved
+// runs (profiles/raw_r4/fold_gemm_ab_r4i.md).
+int g_fold_gemm = 1;
 
 // grid = Cout / kFwdRows.  Thread t owns columns j = t + 256 q (q < NQ) of WG rows
 // k0..k0+7; G streams through LDS in 4-row chunks (double buffered), so the
@@ -131,6 +133,9 @@ __global__ __launch_bounds__(kFoldThreads, 2) void fold_fwd_kernel(const bf16* _
 //        B(k, n) = W[k][n]; rows m < Cin go to Bm[m][Cout + n] (bf16), row Cin
 //        to ebias[n]  (W^T diag(be) W is symmetric: its rows are Bm's columns)
 constexpr int kSgT = 64, kSgK = 16;
+// BWD splits K (= Cout, up to 2048, while M x N = Cin^2 is small) over
+// gridDim.z: split z writes its fp32 partials to C[z] ([Cin][Cin] rows) and
+// ebias[z] ([Cin]), summed into Bm / ebias by fold_bwd_reduce_kernel.
 template <bool BWD>
 __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __restrict__ W,
                                                                   const float* __restrict__ G,
@@ -139,6 +144,11 @@ __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __
                                                                   int K, float* __restrict__ C,
                                                                   bf16* __restrict__ Bm, int ldbm, int bm_off,
                                                                   float* __restrict__ ebias) {
+  const int kchunk = K / gridDim.z, kbeg = blockIdx.z * kchunk, kend = kbeg + kchunk;
+  if constexpr (BWD) {
+    C += (int64_t)blockIdx.z * N * N;
+    ebias += (int64_t)blockIdx.z * N;
+  }
   __shared__ __attribute__((aligned(16))) float As[kSgK][kSgT + 4];
   __shared__ __attribute__((aligned(16))) float Bs[kSgK][kSgT + 4];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
@@ -152,15 +162,15 @@ __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __
       if constexpr (BWD) {
         const int kk = e >> 6, m = e & 63, k = k0 + kk, mm = m0 + m;  // coalesced along m
         float v = 0.f;
-        if (k < K) v = mm < N ? be[k] * (float)W[(int64_t)k * N + mm] : (mm == N ? cc[k] : 0.f);
+        if (k < kend) v = mm < N ? be[k] * (float)W[(int64_t)k * N + mm] : (mm == N ? cc[k] : 0.f);
         ra[u] = v;
       } else {
         const int m = e >> 4, kk = e & 15, k = k0 + kk, mm = m0 + m;  // 16 consecutive k per row
-        ra[u] = (mm < M && k < K) ? (float)W[(int64_t)mm * K + k] : 0.f;
+        ra[u] = (mm < M && k < kend) ? (float)W[(int64_t)mm * K + k] : 0.f;
       }
       const int kk = e >> 6, n = e & 63, k = k0 + kk;
-      if constexpr (BWD) rb[u] = k < K ? (float)W[(int64_t)k * N + n0 + n] : 0.f;
-      else rb[u] = k < K ? G[(int64_t)k * N + n0 + n] : 0.f;
+      if constexpr (BWD) rb[u] = k < kend ? (float)W[(int64_t)k * N + n0 + n] : 0.f;
+      else rb[u] = k < kend ? G[(int64_t)k * N + n0 + n] : 0.f;
     }
   };
   auto store = [&] {
@@ -177,12 +187,12 @@ __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
-  load(0);
-  for (int k0 = 0; k0 < K; k0 += kSgK) {
+  load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += kSgK) {
     __syncthreads();
     store();
     __syncthreads();
-    if (k0 + kSgK < K) load(k0 + kSgK);  // next chunk in flight during this one's FMAs
+    if (k0 + kSgK < kend) load(k0 + kSgK);  // next chunk in flight during this one's FMAs
 #pragma unroll
     for (int kk = 0; kk < kSgK; ++kk) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(&As[kk][ty * 4]);
@@ -199,12 +209,8 @@ __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __
     if (m >= M) continue;
     const int n = n0 + tx * 4;
     if constexpr (BWD) {
-      if (m < N) {
-        bf16x4 v = {(bf16)acc[i][0], (bf16)acc[i][1], (bf16)acc[i][2], (bf16)acc[i][3]};
-        *reinterpret_cast<bf16x4*>(Bm + (int64_t)m * ldbm + bm_off + n) = v;
-      } else {
-        *reinterpret_cast<f32x4*>(ebias + n) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
-      }
+      float* dst = m < N ? C + (int64_t)m * N + n : ebias + n;
+      *reinterpret_cast<f32x4*>(dst) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
     } else {
       *reinterpret_cast<f32x4*>(C + (int64_t)m * N + n) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
     }
@@ -625,10 +631,21 @@ std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tenso
     // role A in the coefficient kernel; [W^T diag(be) W ; c^T W] in the tiled
     // kernel, straight into Bm's second block and ebias
     hipLaunchKernelGGL(fold_bwd_coef_kernel<1>, dim3((unsigned)p.nA), dim3(kFoldThreads), 0, stream, p);
-    hipLaunchKernelGGL(fold_sgemm_kernel<true>, dim3((unsigned)(Cin / kSgT), (unsigned)((Cin + 1 + kSgT - 1) / kSgT)),
+    const int tiles = (int)((Cin / kSgT) * ((Cin + 1 + kSgT - 1) / kSgT));
+    int ks = 1;  // split K (= Cout) until ~2 blocks per CU, chunks of >= 64 channels
+    while (tiles * ks < 512 && Cout % (2 * ks * kSgK) == 0 && Cout / (2 * ks) >= 64) ks *= 2;
+    auto bpart = at::empty({ks, Cin, Cin}, W.options().dtype(at::kFloat));
+    auto epart = at::empty({ks, Cin}, W.options().dtype(at::kFloat));
+    hipLaunchKernelGGL(fold_sgemm_kernel<true>,
+                       dim3((unsigned)(Cin / kSgT), (unsigned)((Cin + 1 + kSgT - 1) / kSgT), (unsigned)ks),
                        dim3(kFoldThreads), 0, stream, p.W, nullptr, coef.data_ptr<float>() + Cout,
-                       coef.data_ptr<float>() + 2 * Cout, (int)(Cin + 1), (int)Cin, (int)Cout, nullptr, p.Bm,
-                       (int)(Cout + Cin), (int)Cout, p.ebias);
+                       coef.data_ptr<float>() + 2 * Cout, (int)(Cin + 1), (int)Cin, (int)Cout,
+                       bpart.data_ptr<float>(), nullptr, 0, 0, epart.data_ptr<float>());
+    const int64_t nred = Cin * Cin + Cin;
+    hipLaunchKernelGGL(fold_bwd_reduce_kernel,
+                       dim3((unsigned)std::min<int64_t>(1024, (nred + kFoldThreads - 1) / kFoldThreads)),
+                       dim3(kFoldThreads), 0, stream, bpart.data_ptr<float>(), epart.data_ptr<float>(), ks,
+                       (int)Cout, (int)Cin, p.Bm, p.ebias);
     DMP_HIP_CHECK(hipGetLastError());
     return {dW, dgb[0], dgb[1], Bm, ebias};
   }

@@ -267,7 +267,7 @@ def _gram(C, inp, geom, native, n):
     return C.gemm_tn_xl(inp, inp, torch.float32) if _tn_xl(inp.shape[0], c, c) else C.gemm_tn(inp, inp, torch.float32)
 
 
-_FOLD_GEMM_ENV = os.environ.get("DMP_FOLD_GEMM")  # A/B: 0 VALU, 1 hipBLASLt, 2 tiled kernel (default)
+_FOLD_GEMM_ENV = os.environ.get("DMP_FOLD_GEMM")  # A/B: 0 VALU, 1 hipBLASLt (default), 2 tiled kernel
 _fold_gemm_set = False
 
 
