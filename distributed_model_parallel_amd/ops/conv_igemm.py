@@ -19,6 +19,8 @@ uses ``F.conv2d``.  The reference uses torchvision's cuDNN convolutions
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -34,12 +36,34 @@ ENABLED = not _native.disabled("igemm")
 # MIOpen: the generic implicit-GEMM backward (conv_nt transposed / conv_wgrad)
 # measured slower on every ResNet-50 shape (profiles/raw_r2/roofline_*.log).
 # set_generic_backward(True) routes them to it (any shape; tests).
-NATIVE_BWD = False
+NATIVE_BWD = os.environ.get("DMP_GENERIC_BWD", "0") == "1"
 
 
 def set_generic_backward(on: bool) -> None:
     global NATIVE_BWD
     NATIVE_BWD = bool(on)
+
+
+def _capturing() -> bool:
+    """Inside a hipGraph capture (bench --graph, DataParallel(graphs=True)):
+    MIOpen is left out of every captured conv.  Its small-map weight gradient
+    replays garbage from the second replay on (round 4,
+    tools/graph_replay_bisect.py: a bare nn.Conv2d 512 -> 512 on 2 x 2 maps,
+    1e36 gradients from step 1; eager runs of the same module agree bitwise),
+    so a captured step takes the native forward / backward for every shape."""
+    return torch.cuda.is_current_stream_capturing()
+
+
+# Weight gradients of 3x3 convs the halo kernel does not cover with Cin % 256
+# == 0 (layer 4's stride-2 first block at every batch; any layer-3/4 shape at
+# small maps) on the ping-pong TN tap-gather kernel (gemm_xl.hip
+# conv_wgrad_xl) instead of MIOpen's igemm_wrw.
+_XL_WGRAD = not _native.disabled("xl_conv3")
+_STATS["xl_wgrad"] = 0
+
+
+def _xl_wgrad_ok(cin: int, kh: int, kw: int) -> bool:
+    return _XL_WGRAD and cin % 256 == 0 and kh == kw and kh > 1
 
 # 256x256 ping-pong implicit GEMM (csrc/gemm/gemm_xl.hip conv_xl), used where
 # its 256-wide output tile is full: forward (with the BN moments) when
@@ -261,8 +285,16 @@ class _ConvIGFn(torch.autograd.Function):
             dw = C.wgrad3x3(dy, x, stride)
             if not weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous()
-        nat_d = ctx.needs_input_grad[0] and dx is None and NATIVE_BWD
-        nat_w = ctx.needs_input_grad[1] and dw is None and NATIVE_BWD
+        if ctx.needs_input_grad[1] and dw is None and _xl_wgrad_ok(cin, kh, kw):
+            _STATS["xl_wgrad"] += 1
+            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+            g = C.conv_wgrad_xl(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
+            dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
+            if not weight.is_contiguous(memory_format=torch.channels_last):
+                dw = dw.contiguous()
+        generic = NATIVE_BWD or _capturing()
+        nat_d = ctx.needs_input_grad[0] and dx is None and generic
+        nat_w = ctx.needs_input_grad[1] and dw is None and generic
         want_d = ctx.needs_input_grad[0] and not nat_d and dx is None
         want_w = ctx.needs_input_grad[1] and not nat_w and dw is None
         if want_d or want_w:
@@ -290,7 +322,8 @@ def conv2d_igemm(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding
                  moments: bool = False, groups: int = 1,
                  dilation=(1, 1)) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """Returns (y, moments-or-None); moments = fp64 [2*Cout+1] of y (see BatchNormAct2d)."""
-    if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]) and not \
+    if _native_ok(x, weight, groups, dilation) and _miopen_fwd(weight.shape[0], weight.shape[2]) and \
+            not _capturing() and not \
             _halo_kind(x.shape[1], weight.shape[0], weight.shape[2], weight.shape[3], stride, padding, x.shape[2],
                        x.shape[3]):
         _STATS["miopen_fwd"] += 1
