@@ -55,15 +55,19 @@ def _capturing() -> bool:
 
 
 # Weight gradients of 3x3 convs the halo kernel does not cover with Cin % 256
-# == 0 (layer 4's stride-2 first block at every batch; any layer-3/4 shape at
-# small maps) on the ping-pong TN tap-gather kernel (gemm_xl.hip
-# conv_wgrad_xl) instead of MIOpen's igemm_wrw.
+# == 0 (layer 4's stride-2 first block; any layer-3/4 shape at small maps) on
+# the ping-pong TN tap-gather kernel (gemm_xl.hip conv_wgrad_xl) instead of
+# MIOpen's igemm_wrw -- always inside a capture, and eagerly up to
+# _XL_WGRAD_MAX_ROWS output pixels: l4 stride-2 at batch 256 0.133 vs
+# 0.138 ms, at batch 2048 0.908 vs 0.655 ms (profiles/raw_r4/wgrad_s2_r4o.md).
 _XL_WGRAD = not _native.disabled("xl_conv3")
+_XL_WGRAD_MAX_ROWS = 50_000
 _STATS["xl_wgrad"] = 0
 
 
-def _xl_wgrad_ok(cin: int, kh: int, kw: int) -> bool:
-    return _XL_WGRAD and cin % 256 == 0 and kh == kw and kh > 1
+def _xl_wgrad_ok(cin: int, kh: int, kw: int, rows: int) -> bool:
+    return (_XL_WGRAD and cin % 256 == 0 and kh == kw and kh > 1
+            and (rows <= _XL_WGRAD_MAX_ROWS or _capturing()))
 
 # 256x256 ping-pong implicit GEMM (csrc/gemm/gemm_xl.hip conv_xl), used where
 # its 256-wide output tile is full: forward (with the BN moments) when
@@ -285,7 +289,7 @@ class _ConvIGFn(torch.autograd.Function):
             dw = C.wgrad3x3(dy, x, stride)
             if not weight.is_contiguous(memory_format=torch.channels_last):
                 dw = dw.contiguous()
-        if ctx.needs_input_grad[1] and dw is None and _xl_wgrad_ok(cin, kh, kw):
+        if ctx.needs_input_grad[1] and dw is None and _xl_wgrad_ok(cin, kh, kw, n * ho * wo):
             _STATS["xl_wgrad"] += 1
             dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
             g = C.conv_wgrad_xl(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)

@@ -301,14 +301,26 @@ def test_dp_graphed_replicas_match_eager(arch):
     before the loss: DataParallel's math), over three steps with optimizer
     updates between them (the replicas must re-read the updated weights).
 
-    bf16 BN over a few images is noisy (round 4, tools/dp_graph_diag.py:
-    eager and graphed both sit 7-10 % from the reference in gradient norm at
-    4 images per replica), so the graphed path must be as close to the
-    reference as the eager one is, not bitwise equal to it."""
+    All three run the same kernels: a capture leaves MIOpen out (its weight
+    gradient is not replay-safe, ops/conv_igemm._capturing), so the eager
+    paths here do too (generic native backward, no MIOpen forward) -- with
+    MIOpen in the eager paths, bf16 BN over 16 images amplifies its different
+    rounding to 7-10 % in the gradients (round 4, tools/dp_graph_diag.py).
+    What remains is the order of the replica-gradient sum."""
     import copy as _copy
     from distributed_model_parallel_amd.models import build_model
+    from distributed_model_parallel_amd.ops import conv_igemm
     from distributed_model_parallel_amd.ops.loss import cross_entropy
     from distributed_model_parallel_amd.utils.precision import cast_model
+    nb, mf = conv_igemm.NATIVE_BWD, conv_igemm._MIOPEN_FWD
+    conv_igemm.NATIVE_BWD, conv_igemm._MIOPEN_FWD = True, False
+    try:
+        _graphed_dp_check(arch, build_model, cross_entropy, cast_model, _copy)
+    finally:
+        conv_igemm.NATIVE_BWD, conv_igemm._MIOPEN_FWD = nb, mf
+
+
+def _graphed_dp_check(arch, build_model, cross_entropy, cast_model, _copy):
     torch.manual_seed(0)
     base = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
     cast_model(base, torch.bfloat16)
@@ -324,11 +336,10 @@ def test_dp_graphed_replicas_match_eager(arch):
             out = dp(x)
             cross_entropy(out, y).backward()
             outs.append(out.float())
-        e_out = (outs[0] - outs[2]).abs().max().item()
-        g_out = (outs[1] - outs[2]).abs().max().item()
-        assert g_out <= 2 * e_out + 2e-2, (step, g_out, e_out)
+        for k in (0, 1):
+            assert (outs[k] - outs[2]).abs().max().item() <= 5e-2, (step, k)
         e_rel, g_rel = _grad_rel(m_s, m_e), _grad_rel(m_s, m_g)
-        assert g_rel <= 1.5 * e_rel + 1e-2, (step, g_rel, e_rel)
+        assert g_rel < 3e-2 and e_rel < 3e-2, (step, g_rel, e_rel)
         for opt in opts:
             opt.step()
             opt.zero_grad()
