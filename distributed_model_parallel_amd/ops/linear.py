@@ -44,6 +44,10 @@ def set_xl_linear(on: bool) -> None:
     _XL = bool(on)
 
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
+# The PLAIN GEMMs (no epilogue to fuse: the qkv projection's bias aside, the
+# data gradients) on gemm_xl ("xl") or hipBLASLt ("lib").  DMP_LINEAR_PLAIN
+# selects; A/B in tools/runs (profiles/README.md round-4 findings).
+_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "xl") == "lib"
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> bool:
@@ -91,7 +95,7 @@ def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dx = dy @ W on the ping-pong MFMA GEMM (B operand = W^T [in, out], a
     transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16) instead of
     hipBLASLt (the data gradients were 17 % of the ViT step)."""
-    if w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
+    if not _PLAIN_LIB and w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
         _STATS["xl_dgrad"] += 1
         return _native.native().gemm_xl(dy2, w.t().contiguous())
     return dy2.mm(w)
@@ -107,7 +111,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        if _xl_gemm_ok(x2, w.shape[0]):  # the qkv projection: bias in the MFMA GEMM's store
+        if not _PLAIN_LIB and _xl_gemm_ok(x2, w.shape[0]):  # the qkv projection: bias in the MFMA GEMM's store
             _STATS["xl_fwd"] += 1
             y = _native.native().gemm_xl(x2, w, "bias", bias=b)
         else:
