@@ -980,39 +980,46 @@ __global__ __launch_bounds__(XTHREADS, 4) void gemm_x2_kernel(const XlArgs p) { 
   const int lrow = lane & 15, lk = lane >> 4;
   const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
 
-  for (int kt = 0; kt < ktiles; ++kt) {
+  // two-stage LDS ring of k32 units (24 KB each: 256 x 32 A + 128 x 32 B):
+  // unit u + 1's LDS-DMA is in flight while unit u's 16 MFMAs per wave run
+  // (a single buffer waited on the full L2 / HBM latency every K tile: 32 x
+  // ~1.5 us at K = 2048), and the second block on the CU overlaps the rest
+  const int nk = ktiles * 2;
+  auto issue = [&](int u) {
+    const int koff = u * 32;
+    const bool second = p.A2 && koff >= p.K1;
+    char* da = smem + (u & 1) * RA + wave * NA * 1024;
+    char* db = smem + 2 * RA + (u & 1) * RB + wave * NB * 1024;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int koff = kt * XBK + ks * 32;
-      const bool second = p.A2 && koff >= p.K1;
-      char* da = smem + ks * RA + wave * NA * 1024;
-      char* db = smem + 2 * RA + ks * RB + wave * NB * 1024;
+    for (int q = 0; q < NA; ++q) glds16((second ? asrc2[q] : asrc[q]) + koff, da + q * 1024);
 #pragma unroll
-      for (int q = 0; q < NA; ++q) glds16((second ? asrc2[q] : asrc[q]) + koff, da + q * 1024);
-#pragma unroll
-      for (int q = 0; q < NB; ++q) glds16(bsrc[q] + koff, db + q * 1024);
+    for (int q = 0; q < NB; ++q) glds16(bsrc[q] + koff, db + q * 1024);
+  };
+  issue(0);
+  for (int u = 0; u < nk; ++u) {
+    if (u + 1 < nk) {
+      issue(u + 1);
+      vmcnt<NA + NB>();  // unit u landed, unit u + 1 still in flight
+    } else {
+      vmcnt<0>();
     }
-    vmcnt<0>();
     barrier();
+    const char* ar = smem + (u & 1) * RA + (wr * 128) * 64 + frag_off;
+    const char* br = smem + 2 * RA + (u & 1) * RB + (wc * 32) * 64 + frag_off;
+    const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(br);
+    const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(br + 16 * 64);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const char* ar = smem + ks * RA + (wr * 128) * 64 + frag_off;
-      const char* br = smem + 2 * RA + ks * RB + (wc * 32) * 64 + frag_off;
-      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(br);
-      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(br + 16 * 64);
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 fa[4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        bf16x8 fa[4];
+      for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + (h * 4 + i) * 16 * 64);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + (h * 4 + i) * 16 * 64);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[h * 4 + i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0, fa[i], acc[h * 4 + i][0], 0, 0, 0);
-          acc[h * 4 + i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, fa[i], acc[h * 4 + i][1], 0, 0, 0);
-        }
+      for (int i = 0; i < 4; ++i) {
+        acc[h * 4 + i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0, fa[i], acc[h * 4 + i][0], 0, 0, 0);
+        acc[h * 4 + i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, fa[i], acc[h * 4 + i][1], 0, 0, 0);
       }
     }
-    barrier();  // every wave read this K tile before the next one overwrites it
+    barrier();  // every wave read buffer u & 1 before unit u + 2 overwrites it
   }
 
   // ---- epilogue straight from the accumulators (C^T layout) ----
