@@ -65,6 +65,29 @@ template <> __device__ __forceinline__ void st8<float>(float* p, const float (&v
   *reinterpret_cast<f32x4*>(p + 4) = b;
 }
 
+// raw 8-element activation vectors held across a row (the prefetch buffer)
+template <typename T> struct Raw8;
+template <> struct Raw8<__bf16> {
+  bf16x8 v;
+  __device__ void load(const __bf16* p) { v = *reinterpret_cast<const bf16x8*>(p); }
+  __device__ void get(float (&o)[8]) const {
+    const f32x8 f = __builtin_convertvector(v, f32x8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = f[i];
+  }
+};
+template <> struct Raw8<float> {
+  f32x4 a, b;
+  __device__ void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  __device__ void get(float (&o)[8]) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[i + 4] = b[i]; }
+  }
+};
+
 template <typename T, typename P, int kMaxV>
 __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict__ x,
                                                             const P* __restrict__ w,
@@ -87,19 +110,31 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
       else for (int i = 0; i < 8; ++i) gb[k][i] = 0.f;
     }
   }
+  // the next row's vectors are loaded before this row is reduced and written
+  // (as ln_bwd_kernel): one row of loads always in flight per wave instead of
+  // a dependent HBM round trip at the head of every row
+  Raw8<T> nx[kMaxV];
+  auto fetch = [&](int64_t r) {
+#pragma unroll
+    for (int k = 0; k < kMaxV; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nv) nx[k].load(x + r * D + c * 8);
+    }
+  };
+  if (wave < rows) fetch(wave);
   for (int64_t r = wave; r < rows; r += nwaves) {
-    const T* xr = x + r * D;
     float v[kMaxV][8];
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
       const int c = lane + 64 * k;
       if (c < nv) {
-        ld8<T>(xr + c * 8, v[k]);
+        nx[k].get(v[k]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) s += v[k][i];
       }
     }
+    if (r + nwaves < rows) fetch(r + nwaves);
     const float mean = wave_sum(s) / (float)D;
     float q = 0.f;
 #pragma unroll
@@ -131,29 +166,6 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
     }
   }
 }
-
-// raw 8-element activation vectors held across a row (the prefetch buffer)
-template <typename T> struct Raw8;
-template <> struct Raw8<__bf16> {
-  bf16x8 v;
-  __device__ void load(const __bf16* p) { v = *reinterpret_cast<const bf16x8*>(p); }
-  __device__ void get(float (&o)[8]) const {
-    const f32x8 f = __builtin_convertvector(v, f32x8);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = f[i];
-  }
-};
-template <> struct Raw8<float> {
-  f32x4 a, b;
-  __device__ void load(const float* p) {
-    a = *reinterpret_cast<const f32x4*>(p);
-    b = *reinterpret_cast<const f32x4*>(p + 4);
-  }
-  __device__ void get(float (&o)[8]) const {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[i + 4] = b[i]; }
-  }
-};
 
 // dgamma/dbeta partials: part[block][0:D] = sum dy*xhat, part[block][D:2D] = sum dy.
 // The next row's x / dy / residual-gradient vectors are loaded before the
