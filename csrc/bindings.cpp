@@ -109,6 +109,7 @@ void set_gemm_xl_bn(int bn, int pipe, int group_m);
 int get_gemm_xl_pipe();
 void set_gemm_xl_x2(int mode);
 int get_gemm_xl_x2();
+void set_gemm_xl_nt(int on);
 int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
                                 int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
@@ -335,6 +336,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_xl_x2", &dmp::set_gemm_xl_x2, py::arg("mode"),
         "conv-epilogue GEMMs on the two-blocks-per-CU 256x128 kernel: 0 off, 1 where N % 256 != 0, 2 always");
   m.def("get_gemm_xl_x2", &dmp::get_gemm_xl_x2);
+  m.def("set_gemm_xl_nt", &dmp::set_gemm_xl_nt, py::arg("on"),
+        "conv-epilogue GEMMs: non-temporal C stores / residual loads (A/B; env DMP_XL_NT)");
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");

@@ -37,6 +37,7 @@
 //   * bijective XCD-aware block remap (T1); the N tiles of an M tile are
 //     adjacent (they share the A panel in L2);
 //   * epilogue restages the tile through LDS for 16-B row-contiguous stores.
+#include <cstdlib>
 #include <torch/extension.h>
 #include <type_traits>
 #include <ATen/hip/HIPContext.h>
@@ -187,6 +188,7 @@ struct XlArgs {
   const float* ebias;           // XL_BNBWD: per-column constant added to the GEMM output
   const float *esc, *esh;       // XL_AFFINE coefficients (null: 1 / 0)
   int erelu;                    // XL_AFFINE ReLU
+  int cnt;                      // conv epilogues: non-temporal C stores / residual loads (streamed once)
 };
 
 template <int BN, int EPI, int PIPE>
@@ -798,7 +800,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
             rok |= (rr >= 0 ? 1u : 0u) << i;
             rr = rr >= 0 ? rr : 0;
           }
-          l0[i] = *reinterpret_cast<const bf16x8*>(rbase + rr * rld + col);
+          const bf16x8* rp = reinterpret_cast<const bf16x8*>(rbase + rr * rld + col);
+          l0[i] = p.cnt ? __builtin_nontemporal_load(rp) : *rp;
         }
         if constexpr (kL12) {
           l1[i] = *reinterpret_cast<const bf16x8*>(xbase + (int64_t)row * xld + col);
@@ -863,7 +866,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           for (int j = 0; j < 8; ++j) msum[j] += fv[j];
         }
         const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
-        *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
+        bf16x8* cp = reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col);
+        if (p.cnt) __builtin_nontemporal_store(v, cp);
+        else *cp = v;
       }
     }
     if constexpr (!kBatch) {
@@ -885,7 +890,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           v = __builtin_convertvector(f, bf16x8);
         }
         const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
-        *reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col) = v;
+        bf16x8* cp = reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col);
+        if (p.cnt) __builtin_nontemporal_store(v, cp);
+        else *cp = v;
       }
     }
   }
@@ -1737,6 +1744,11 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
 // GEMM with N % 128 == 0 (A/B)
 int g_xl_x2 = 1;
 
+// conv-epilogue GEMMs: non-temporal C stores and residual loads (A/B:
+// DMP_XL_NT=1 or set_gemm_xl_nt; the outputs are consumed by the next layer,
+// so at batch 256 they may still profit from the 256 MB last-level cache)
+int g_xl_nt = [] { const char* e = std::getenv("DMP_XL_NT"); return e ? std::atoi(e) : 0; }();
+
 bool use_x2(const XlArgs& a) {
   if (g_xl_x2 == 0 || a.N % X2_BN != 0) return false;
   return g_xl_x2 == 2 || a.N % 256 != 0;
@@ -1936,6 +1948,7 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   auto C = at::empty({M, N}, A.options());
   a.C = reinterpret_cast<bf16*>(C.data_ptr()); a.ldc = C.stride(0);
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+  a.cnt = g_xl_nt;
   if (!res_map.empty()) {
     TORCH_CHECK(mode == "bnbwd" && res_map.size() == 5, "res_map: bnbwd only, [stride, Ho, Wo, Hi, Wi]");
     a.rmap.s = (int)res_map[0]; a.rmap.ho = (int)res_map[1]; a.rmap.wo = (int)res_map[2];
@@ -2238,6 +2251,7 @@ void set_gemm_xl_x2(int mode) {
   g_xl_x2 = mode;
 }
 int get_gemm_xl_x2() { return g_xl_x2; }
+void set_gemm_xl_nt(int on) { g_xl_nt = on ? 1 : 0; }
 int get_tn_xl_ring() { return g_tn_xl_ring; }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
