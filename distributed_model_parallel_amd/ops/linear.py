@@ -44,10 +44,14 @@ def set_xl_linear(on: bool) -> None:
     _XL = bool(on)
 
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
-# The PLAIN GEMMs (no epilogue to fuse: the qkv projection's bias aside, the
-# data gradients) on gemm_xl ("xl") or hipBLASLt ("lib").  DMP_LINEAR_PLAIN
-# selects; A/B in tools/runs (profiles/README.md round-4 findings).
-_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "xl") == "lib"
+# The PLAIN GEMMs -- nothing to fuse but a bias: the qkv projection forward
+# and the data gradients of qkv / proj / fc1 -- on hipBLASLt ("lib", default)
+# or gemm_xl ("xl"): ViT-B/16 batch 256, 41.82 vs 43.06 ms per step,
+# interleaved runs (profiles/README.md finding 50).  The fused-epilogue GEMMs
+# (fc1 bias+GELU, fc2 / proj bias+residual, fc2's GELU' data gradient with
+# fc1's bias gradient) and every weight gradient (gemm_tn_xl: 44.04 ms with
+# those on the library too) stay on our MFMA kernels.
+_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "lib") == "lib"
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> bool:
@@ -92,9 +96,9 @@ def _xl_gemm_ok(a: torch.Tensor, n: int) -> bool:
 
 
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dx = dy @ W on the ping-pong MFMA GEMM (B operand = W^T [in, out], a
-    transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16) instead of
-    hipBLASLt (the data gradients were 17 % of the ViT step)."""
+    """dx = dy @ W: hipBLASLt by default (measured faster, finding 50), or
+    the ping-pong MFMA GEMM with DMP_LINEAR_PLAIN=xl (B operand = W^T [in,
+    out], a transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16)."""
     if not _PLAIN_LIB and w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
         _STATS["xl_dgrad"] += 1
         return _native.native().gemm_xl(dy2, w.t().contiguous())
