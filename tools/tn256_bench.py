@@ -44,8 +44,8 @@ def main():
              ("l3 ds 1024<-512", 14 * 14, 1024, 512), ("l4 conv1 512<-2048", 7 * 7, 512, 2048),
              ("l4 conv3 2048<-512", 7 * 7, 2048, 512), ("l4 ds 2048<-1024", 7 * 7, 2048, 1024)]
     print(f"# 1x1 weight gradients, ResNet-50 batch {n}, 1x MI355X\n")
-    print("| shape | M | tn | tn_xl auto | r=1 | r=2 | r=4 | best/tn | rule picks |")
-    print("|---|---|---|---|---|---|---|---|---|")
+    print("| shape | M | tn | tn_xl auto | r=1 | r=2 | r=4 | hipBLASLt | best/tn | rule picks |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for name, px, cout, cin in cases:
         m = n * px
         dy = torch.randn(m, cout, device="cuda").to(dt)
@@ -56,9 +56,10 @@ def main():
             C.set_tn_xl_rounds(r)
             ts.append(timeit(lambda: C.gemm_tn_xl(dy, x, dt)))
         C.set_tn_xl_rounds(0)
+        t_lib = timeit(lambda: dy.t().mm(x))
         pick = "tn_xl" if conv1x1._tn_xl(m, cout, cin) else "tn"
         print(f"| {name} | {m} | {t_tn:.4f} | " + " | ".join(f"{t:.4f}" for t in ts) +
-              f" | {min(ts) / t_tn:.2f} | {pick} |", flush=True)
+              f" | {t_lib:.4f} | {min(ts) / t_tn:.2f} | {pick} |", flush=True)
         del dy, x
         torch.cuda.empty_cache()
 
