@@ -197,15 +197,16 @@ _TN_XL = not _native.disabled("tn_xl")
 _STATS["tn_xl"] = 0
 
 
-_TN_XL_MIN_ROWS = 150_000
+_TN_XL_MIN_ROWS = 100_000
 
 
 def _tn_xl(m: int, cout: int, cin: int) -> bool:
-    """Ping-pong TN weight gradient: layer-3-sized 1x1 convs (both output dims
-    >= 256, M >= 150k rows), where it measured 0.17 vs 0.20 ms
-    (tools/tn_xl_bench.py); deeper-K / shorter-M layer-4 shapes tie.  (The
-    224-px convergence test lowers the row threshold so its batch-64 run
-    trains through this route too.)"""
+    """Ping-pong TN weight gradient for 1x1 convs with both output dims >= 256
+    from 100k rows: batch 2048 layer 3 0.31-0.56 vs 0.37-0.65 ms and layer 4
+    (100352 rows) 0.29-0.55 vs 0.35-0.60 ms; at batch 256 (50k rows and less)
+    the split-M 4-wave kernel wins 1.07-1.14x; hipBLASLt is 1.5-8x slower on
+    every shape (profiles/raw_r4/tn_wgrad_r4t.md).  (The 224-px convergence
+    test lowers the row threshold so its batch-64 run trains this route.)"""
     return _TN_XL and cout >= 256 and cin >= 256 and m >= _TN_XL_MIN_ROWS
 
 
