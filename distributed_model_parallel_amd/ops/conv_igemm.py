@@ -61,7 +61,7 @@ def _capturing() -> bool:
 # _XL_WGRAD_MAX_ROWS output pixels: l4 stride-2 at batch 256 0.133 vs
 # 0.138 ms, at batch 2048 0.908 vs 0.655 ms (profiles/raw_r4/wgrad_s2_r4o.md).
 _XL_WGRAD = not _native.disabled("xl_conv3")
-_XL_WGRAD_MAX_ROWS = 50_000
+_XL_WGRAD_MAX_ROWS = int(os.environ.get("DMP_XL_WGRAD_MAX_ROWS", 50_000))
 _STATS["xl_wgrad"] = 0
 
 

@@ -291,7 +291,6 @@ def _grad_rel(ref: torch.nn.Module, other: torch.nn.Module) -> float:
 
 
 @pytest.mark.gpu
-@pytest.mark.unvalidated
 @pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
 def test_dp_graphed_replicas_match_eager(arch):
     """DataParallel(graphs=True) (parallel/dp_graphs.py: static replicas whose

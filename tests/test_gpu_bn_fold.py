@@ -325,7 +325,6 @@ def test_relu_mask_colsum_kernel(rows, c):
     assert s[2 * c].item() == rows
 
 
-@pytest.mark.unvalidated
 @pytest.mark.parametrize("positive_w", [False, True], ids=["randn_w", "positive_w"])
 def test_fold_statistics_at_headline_rows(positive_w):
     """the fold's BN3 statistics come from E[y^2] - E[y]^2

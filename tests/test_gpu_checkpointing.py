@@ -66,7 +66,10 @@ def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
     l3 = cross_entropy(m3(x), y)
     l3.backward()
     monkeypatch.undo()
-    torch.testing.assert_close(l2.float(), l3.float(), atol=1e-3, rtol=1e-3)
+    # the forwards run the same kernels, but the BN moments' cross-block fp64
+    # atomic adds land in a run-dependent order and bf16 BN over 8 images
+    # amplifies that last-bit difference (round 4: 0.24 % in the loss once)
+    torch.testing.assert_close(l2.float(), l3.float(), atol=1e-2, rtol=1e-2)
     # backward node ORDER differs (the recompute runs when a segment's first
     # saved tensor is unpacked), which changes where bf16 gradient sums round,
     # and the cross-block BN moment reduce adds in fp64 atomics (order varies

@@ -301,10 +301,15 @@ def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
     a, b = _mean(l_nat[-k:]), _mean(l_ref[-k:])
     # the task is learned but not saturated: the plateau stays well above zero
     assert b < 0.9 * l0 and b > 0.1 * l0, (l0, b)
-    # native tracks stock: no worse plateau (a wrong gradient raises it; round 4
-    # measured native 0.63 vs stock 0.81 -- separate trajectories of a chaotic
-    # run, bf16 vs fp32), and no lag in reaching 95 / 90 % of the start
-    assert a <= 1.1 * b + 0.05, (a, b)
+    # native tracks stock.  The curves are separate trajectories of a chaotic
+    # run (bf16 vs fp32, run-dependent atomic order) still falling at step
+    # 160: four round-4 runs put the last-20 mean of the SAME stock fp32 run at
+    # 0.72-1.20 and native at 0.82-1.82, so the late value alone cannot
+    # discriminate.  A wrong gradient slows the whole descent: compare the
+    # mean over all steps (ratio native / stock measured 0.86-1.13), require a
+    # real descent, and no lag in reaching 95 / 90 % of the start
+    assert _mean(l_nat) <= 1.25 * _mean(l_ref), (_mean(l_nat), _mean(l_ref))
+    assert a < 0.6 * l0, (l0, a)
     for frac in (0.95, 0.9):
         sn, sr = _steps_to(l_nat, frac * l0), _steps_to(l_ref, frac * l0)
         if sr is not None:
