@@ -424,6 +424,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    // operands swapped: acc holds C^T blocks (lane = output row, registers =
+    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -431,7 +433,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[MQ * 4 + i][NQ * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     barrier();
@@ -589,6 +591,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    // operands swapped: acc holds C^T blocks (lane = output row, registers =
+    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
@@ -596,7 +600,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[MQ * 4 + i][NQ * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     barrier();
@@ -715,6 +719,38 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   // per-column affine applied to the fp32 accumulator BEFORE the bf16 staging:
   // a bias / BN shift that nearly cancels acc (XL_BNBWD's folded-BN constant,
   // XL_AFFINE's -mean*scale) must not meet a bf16-rounded acc (finding 33)
+  if constexpr (PIPE == 7 || PIPE == 8) {
+    // transposed accumulators (see quad()): lane l holds row l & 15 and the 4
+    // consecutive columns 4 (l >> 4) + e of each 16 x 16 block -> one 8-B LDS
+    // write per block (a half-wave covers 16 rows x 16 B at a 528-B row pitch:
+    // all 64 banks once) instead of four 2-B writes
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int lc = wc * WTN + j * 16 + (lane >> 4) * 4;
+      const int col = n0 + lc;
+      f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
+      if (col < N) {  // N % 8 == 0: the 4 columns are all in or all out
+        if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES) {
+          const bf16x4 bb4 = *reinterpret_cast<const bf16x4*>(p.bias + col);
+          b4 = __builtin_convertvector(bb4, f32x4);
+        }
+        if constexpr (EPI == XL_BNBWD)
+          if (p.ebias) b4 = *reinterpret_cast<const f32x4*>(p.ebias + col);
+        if constexpr (EPI == XL_AFFINE) {
+          if (p.esc) s4 = *reinterpret_cast<const f32x4*>(p.esc + col);
+          if (p.esh) b4 = *reinterpret_cast<const f32x4*>(p.esh + col);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wr * WTM + i * 16 + (lane & 15);
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[i][j][e], s4[e], b4[e]);
+        *reinterpret_cast<bf16x4*>(ct + row * CT_STRIDE + lc) = __builtin_convertvector(v, bf16x4);
+      }
+    }
+  } else {
   float bv[NI], sv[NI];
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
@@ -741,6 +777,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         ct[row * CT_STRIDE + col] = (bf16)fmaf(acc[i][j][e], sv[j], bv[j]);
       }
     }
+  }
   __syncthreads();
   constexpr int CV = BN / 8, RPP = XTHREADS / CV;
   const int cvi = tid % CV, rr0 = tid / CV;
@@ -786,26 +823,41 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     const int64_t xld = p.bx ? p.ldbx : 0;
     const bf16* ybase = p.bny ? p.bny : p.C;
     const int64_t yld = p.bny ? p.ldby : 0;
+    // row pointers advance by a uniform RPP-row step (no per-row 64-bit
+    // multiply); a row past M reads row 0 of the same operand instead
+    const bf16* rrow = rbase + (int64_t)(m0 + rr0) * rld + col;
+    const int64_t rstep = (int64_t)RPP * rld;
+    const bf16* xrow = xbase + (int64_t)(m0 + rr0) * xld + col;
+    const bf16* yrow = ybase + (int64_t)(m0 + rr0) * yld + col;
+    const int64_t xstep = (int64_t)RPP * xld, ystep = (int64_t)RPP * yld;
+    bf16* const crow = p.C + (int64_t)(m0 + rr0) * p.ldc + col;
+    const int64_t cstep = (int64_t)RPP * p.ldc;
+    // XL_AFFINE without a residual still loads (a dummy row of C: branch-free
+    // batch) and masks the bits to +0 instead of branching around the add
+    const unsigned rmask = p.R ? 0xffffffffu : 0u;
 #pragma unroll 1
     for (int pb = 0; pb < NP; pb += PB) {
       bf16x8 l0[PB], l1[PB], l2[PB];
       unsigned rok = 0;  // bit i: row pass i has a residual row (compact map)
 #pragma unroll
       for (int i = 0; i < PB; ++i) {
-        const int row = min(m0 + rr0 + (pb + i) * RPP, M - 1);
+        const int row_u = m0 + rr0 + (pb + i) * RPP;
+        const int row = min(row_u, M - 1);
         if constexpr (kL0) {
-          int64_t rr = row;
+          const bf16x8* rp;
           if constexpr (EPI == XL_BNBWD) {
-            rr = p.R ? compact_row(p.rmap, row) : -1;
+            int64_t rr = p.R ? compact_row(p.rmap, row) : -1;
             rok |= (rr >= 0 ? 1u : 0u) << i;
             rr = rr >= 0 ? rr : 0;
+            rp = reinterpret_cast<const bf16x8*>(rbase + rr * rld + col);
+          } else {
+            rp = reinterpret_cast<const bf16x8*>(row_u < M ? rrow + (pb + i) * rstep : rbase + col);
           }
-          const bf16x8* rp = reinterpret_cast<const bf16x8*>(rbase + rr * rld + col);
           l0[i] = p.cnt ? __builtin_nontemporal_load(rp) : *rp;
         }
         if constexpr (kL12) {
-          l1[i] = *reinterpret_cast<const bf16x8*>(xbase + (int64_t)row * xld + col);
-          l2[i] = *reinterpret_cast<const bf16x8*>(ybase + (int64_t)row * yld + col);
+          l1[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? xrow + (pb + i) * xstep : xbase + col);
+          l2[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? yrow + (pb + i) * ystep : ybase + col);
         }
       }
 #pragma unroll
@@ -824,7 +876,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           v = __builtin_convertvector(f, bf16x8);
         } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
           f32x8 f = __builtin_convertvector(v, f32x8);
-          if (p.R) f += __builtin_convertvector(l0[i], f32x8);
+          u32x4 rb = __builtin_bit_cast(u32x4, l0[i]);
+          rb &= rmask;
+          f += __builtin_convertvector(__builtin_bit_cast(bf16x8, rb), f32x8);
           if (p.erelu) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
@@ -865,8 +919,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
 #pragma unroll
           for (int j = 0; j < 8; ++j) msum[j] += fv[j];
         }
-        const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
-        bf16x8* cp = reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col);
+        static_assert(!kBatch || EPI != XL_STORE, "batched epilogues write C rows unmapped");
+        bf16x8* cp = reinterpret_cast<bf16x8*>(crow + (pb + i) * cstep);
         if (p.cnt) __builtin_nontemporal_store(v, cp);
         else *cp = v;
       }
