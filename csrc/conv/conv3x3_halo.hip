@@ -84,7 +84,10 @@ __device__ __forceinline__ int halo_key(int q) { return (0x31165572u >> (4 * (q 
 
 // output stage [pixel][64 ch]: 16-B chunk swizzle by pixel (even values, so a
 // channel pair of chunks stays adjacent)
-__device__ __forceinline__ int stage_key(int p) { return ((p >> 2) & 3) << 1; }
+// 16-B chunk swizzle of a staged pixel row: the epilogue writes 16 pixels x
+// 16 B per half-wave (transposed accumulators), (p & 1) picks the 128-B half
+// of a 256-B bank row and (p >> 1) & 7 the chunk: conflict-free
+__device__ __forceinline__ int stage_key(int p) { return (p >> 1) & 7; }
 
 // LDS-DMA from inline asm (see wgrad3x3.hip): with the builtin, hipcc cannot
 // tell which LDS bytes a pending copy writes and drains it (vmcnt(0)) at the
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_c64_kernel(
       for (int f = 0; f < G::MF_WAVE; ++f)
 #pragma unroll
         for (int nf = 0; nf < NFW; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s & 1][f], bw[nf][s], acc[f][nf], 0, 0, 0);
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[nf][s], a[s & 1][f], acc[f][nf], 0, 0, 0);  // C^T
       // interleave: the next step's 7 ds_reads go one per MFMA over the first
       // half of this step, leaving 7 MFMAs (~112 cycles) for the last to land
       if (s + 1 < KSTEPS) {
@@ -279,19 +282,17 @@ __global__ __launch_bounds__(64 * NW, 1) void conv3x3_c64_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // epilogue: C/D row = 4 lh + i (pixel), col = l15 (channel) -> LDS stage
+    // epilogue (transposed accumulators): pixel (fragment row) = l15, channels
+    // 16 (NFW wn + nf) + 4 lh + i -> one 8-B LDS write per fragment
 #pragma unroll
     for (int f = 0; f < G::MF_WAVE; ++f)
 #pragma unroll
-      for (int nf = 0; nf < NFW; ++nf)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = (wm * G::MF_WAVE + f) * 16 + 4 * lh + i;
-          // chunk swizzle: the 4 rows a write touches (4 lh + i, stride 4) land
-          // on 4 different 32-B spans of their bank window
-          const int ch = (2 * (NFW * wn + nf) + (l15 >> 3)) ^ stage_key(p);
-          ostage[p * C64 + ch * 8 + (l15 & 7)] = (bf16)acc[f][nf][i];
-        }
+      for (int nf = 0; nf < NFW; ++nf) {
+        const int p = (wm * G::MF_WAVE + f) * 16 + l15;
+        const int ch = (2 * (NFW * wn + nf) + (lh >> 1)) ^ stage_key(p);
+        *reinterpret_cast<bf16x4*>(ostage + p * C64 + ch * 8 + (lh & 1) * 4) =
+            __builtin_convertvector(acc[f][nf], bf16x4);
+      }
     __syncthreads();
     // the tile = R whole output rows of one image = one contiguous run of y
     {

@@ -323,11 +323,13 @@ void gemm_nt_kernel(const NtArgs p) {
 #pragma unroll
       for (int j = 0; j < NI; ++j)
         fb[j] = *reinterpret_cast<const bf16x8*>(bs + swz(wn * WTN + j * 16 + lrow, ks * 4 + lk));
+      // operands swapped: acc[i][j] holds the C^T block (lane = output row,
+      // registers = 4 consecutive output columns) -> 8-B row pieces in the epilogue
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < ktiles) {
       store_tile(cur ^ 1);
@@ -341,32 +343,33 @@ void gemm_nt_kernel(const NtArgs p) {
   // Per-column affine on the fp32 accumulator before the bf16 staging
   // (EPI_AFFINE scale/shift, EPI_BNBWD's folded-BN constant): a shift that
   // nearly cancels acc must not meet a bf16-rounded acc (finding 33).
-  float cs[NI], cb[NI];
+  // Transposed accumulators: lane l holds row l & 15 and columns 4 (l >> 4) + e
+  // of each 16 x 16 block -> one 8-B LDS write per block (host: N % 8 == 0, so
+  // a 4-column group is wholly in or out; coefficient vectors 16-B aligned).
+  // Residual / activation are applied in the row-contiguous store pass.
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
-    const int gc = n0 + wn * WTN + j * 16 + (lane & 15);
-    cs[j] = 1.f;
-    cb[j] = 0.f;
-    if constexpr (EPI == EPI_AFFINE) {
-      if (gc < N && epi_s) cs[j] = epi_s[gc];
-      if (gc < N && epi_t) cb[j] = epi_t[gc];
-    }
-    if constexpr (EPI == EPI_BNBWD) {
-      if (gc < N && p.ebias) cb[j] = p.ebias[gc];
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int col = wn * WTN + j * 16 + (lane & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + e;
-        // residual / activation are applied in the row-contiguous store pass
-        ct[row * CT_STRIDE + col] = (bf16)fmaf(acc[i][j][e], cs[j], cb[j]);
+    const int lc = wn * WTN + j * 16 + (lane >> 4) * 4;
+    const int gc = n0 + lc;
+    f32x4 cs = {1.f, 1.f, 1.f, 1.f}, cb = {0.f, 0.f, 0.f, 0.f};
+    if (gc < N) {
+      if constexpr (EPI == EPI_AFFINE) {
+        if (epi_s) cs = *reinterpret_cast<const f32x4*>(epi_s + gc);
+        if (epi_t) cb = *reinterpret_cast<const f32x4*>(epi_t + gc);
+      }
+      if constexpr (EPI == EPI_BNBWD) {
+        if (p.ebias) cb = *reinterpret_cast<const f32x4*>(p.ebias + gc);
       }
     }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int row = wm * WTM + i * 16 + (lane & 15);
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaf(acc[i][j][e], cs[e], cb[e]);
+      *reinterpret_cast<bf16x4*>(ct + row * CT_STRIDE + lc) = __builtin_convertvector(v, bf16x4);
+    }
+  }
   __syncthreads();
 
   // ---- store pass: each thread moves 8 contiguous columns of a row ----
@@ -1038,8 +1041,9 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
       TORCH_CHECK(hs || ht, "affine epilogue needs scale and/or shift (missing = 1 / 0)");
       for (const auto* t : {&epi_scale, &epi_shift})
         if (t->has_value() && (*t)->defined())
-          TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() == a.N,
-                      "affine coefficients must be contiguous fp32 [N]");
+          TORCH_CHECK((*t)->scalar_type() == at::kFloat && (*t)->is_contiguous() && (*t)->numel() == a.N &&
+                          reinterpret_cast<uintptr_t>((*t)->data_ptr()) % 16 == 0,
+                      "affine coefficients must be contiguous 16-B aligned fp32 [N]");
       a.epi_s = hs ? epi_scale->data_ptr<float>() : nullptr;
       a.epi_t = ht ? epi_shift->data_ptr<float>() : nullptr;
     } else {
@@ -1289,8 +1293,9 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
   TORCH_CHECK(B.size(1) == a.K, "A/B K mismatch");
   TORCH_CHECK(a.K % 8 == 0 && a.N % 8 == 0, "K and N must be multiples of 8");
   auto f32vec = [&](const at::Tensor& t, const char* name) {
-    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == a.N,
-                name, " must be a contiguous fp32 [N] GPU tensor");
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == a.N &&
+                    reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+                name, " must be a contiguous 16-B aligned fp32 [N] GPU tensor");
     return t.data_ptr<float>();
   };
   if (has_x) {

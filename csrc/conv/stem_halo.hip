@@ -102,7 +102,10 @@ constexpr int F_STAGE = F_PIX * kCo * 2;    // 57344
 constexpr int F_SMEM = 2 * F_BUF + F_STAGE + 2 * kCo * 4;
 constexpr int F_KS = kK / 32;               // 8 k-steps (2 taps each)
 
-__device__ __forceinline__ int stage_key(int p) { return ((p >> 2) & 3) << 1; }
+// 16-B chunk swizzle of a staged pixel row: the epilogue writes 16 pixels x
+// 16 B per half-wave (transposed accumulators), (p & 1) picks the 128-B half
+// of a 256-B bank row and (p >> 1) & 7 the chunk: conflict-free
+__device__ __forceinline__ int stage_key(int p) { return (p >> 1) & 7; }
 
 template <bool MOM>
 __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(const bf16* __restrict__ s, const bf16* __restrict__ wm,
@@ -179,7 +182,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(const bf16* __restrict
       for (int f = 0; f < F_FW; ++f)
 #pragma unroll
         for (int nf = 0; nf < 4; ++nf)
-          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks & 1][f], bw[nf][ks], acc[f][nf], 0, 0, 0);
+          acc[f][nf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[nf][ks], a[ks & 1][f], acc[f][nf], 0, 0, 0);  // C^T
       if (ks + 1 < F_KS) {
 #pragma unroll
         for (int f = 0; f < F_FW; ++f) {
@@ -190,17 +193,17 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(const bf16* __restrict
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    // epilogue: C/D row = pixel 4 lh + i of fragment f, col = channel 16 nf + l15
+    // epilogue (transposed accumulators): pixel = 16 (F_FW wave + f) + l15,
+    // channels 16 nf + 4 lh + i -> one 8-B LDS write per fragment
 #pragma unroll
     for (int f = 0; f < F_FW; ++f)
 #pragma unroll
-      for (int nf = 0; nf < 4; ++nf)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = 16 * (F_FW * wave + f) + 4 * lh + i;
-          const int ch = (2 * nf + (l15 >> 3)) ^ stage_key(p);
-          ostage[p * kCo + ch * 8 + (l15 & 7)] = (bf16)acc[f][nf][i];
-        }
+      for (int nf = 0; nf < 4; ++nf) {
+        const int p = 16 * (F_FW * wave + f) + l15;
+        const int ch = (2 * nf + (lh >> 1)) ^ stage_key(p);
+        *reinterpret_cast<bf16x4*>(ostage + p * kCo + ch * 8 + (lh & 1) * 4) =
+            __builtin_convertvector(acc[f][nf], bf16x4);
+      }
     __syncthreads();
     {
       const int n = t / tiles_per_img;

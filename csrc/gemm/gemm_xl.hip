@@ -731,8 +731,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
       if (col < N) {  // N % 8 == 0: the 4 columns are all in or all out
         if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES) {
-          const bf16x4 bb4 = *reinterpret_cast<const bf16x4*>(p.bias + col);
-          b4 = __builtin_convertvector(bb4, f32x4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) b4[e] = (float)p.bias[col + e];  // a bias view may be 2-B aligned only
         }
         if constexpr (EPI == XL_BNBWD)
           if (p.ebias) b4 = *reinterpret_cast<const f32x4*>(p.ebias + col);
@@ -2021,7 +2021,8 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   TORCH_CHECK(epi != XL_ADD || a.R, "gemm_xl_conv: add needs a residual");
   auto f32vec = [&](const c10::optional<at::Tensor>& t, const char* name) {
     TORCH_CHECK(t.has_value() && t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() &&
-                    t->numel() == N, name, " must be a contiguous fp32 [N] GPU tensor");
+                    t->numel() == N && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                name, " must be a contiguous 16-B aligned fp32 [N] GPU tensor");
     return t->data_ptr<float>();
   };
   if (epi == XL_AFFINE) {
