@@ -155,9 +155,13 @@ base = ddp_step()
 slow = ddp_step(lambda d: C.RcclReduceBackend(d.comm.native, 2.0, 200_000_000))
 # MIOpen's weight gradients are not bit-deterministic (profiles/README.md finding 4),
 # so compare per parameter with a noise allowance; a missing event makes the
-# optimizer see the UNdoubled gradient: relative error 0.5 on every parameter
+# optimizer see the UNdoubled gradient: relative error 0.5 on every parameter it
+# hits.  Measured noise between two correct steps: median 6e-6 warmed, but
+# 0.085 (max 0.10) in two full-suite runs -- the random-init ResNet-18 at batch
+# 8 amplifies one nondeterministic sum chaotically -- so the signature checked
+# is "no parameter near 0.5", with the median well under it
 errs = rel_errs(slow, [2 * b for b in base])
-assert errs[len(errs) // 2] < 0.02 and errs[-1] < 0.25, ("optimizer read the gradient before the comm stream finished", errs[len(errs) // 2], errs[-1])
+assert errs[len(errs) // 2] < 0.2 and errs[-1] < 0.35, ("optimizer read the gradient before the comm stream finished", errs[len(errs) // 2], errs[-1])
 print("ordering ok", errs[len(errs) // 2], errs[-1])
 
 # 2) precision parity: one bf16 DP step (device_ids=[0]) and one bf16 DDP step
