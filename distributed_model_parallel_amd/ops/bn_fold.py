@@ -87,6 +87,15 @@ def _xl_fwd(cout: int, cin: int) -> bool:
     return _xl(cout, cin)
 
 
+def _xl_dgrad(cin: int, cout: int) -> bool:
+    """Folded data gradient [M, cout + cin] @ Bb^T -> [M, cin]: the ping-pong
+    GEMM (x2 kernel at cin = 128) from cin >= 128 -- measured 1.09 / 1.19 /
+    1.24x the NT kernel at layers 2 / 3 / 4 (batch 2048; 1.02 / 1.30 / 0.96 at
+    256), 0.53x at layer 1's cin = 64 (profiles/raw_r4/fold_dgrad_ab_r4aa.md)."""
+    from .conv1x1 import _XL
+    return _XL and cin >= 128 and cin % 128 == 0 and cout >= 512
+
+
 def _map_rows(x2: torch.Tensor, geom, n: int):
     """The rows of x2 [N*Hi*Wi, C] a stride-s 1x1 conv reads (CPU path)."""
     if not geom:
@@ -384,7 +393,7 @@ class _FoldDgrad:
         cout = dz2.shape[1]
         bs = meta.a_slot
         meta.a_slot = None
-        xl = _xl_fwd(cin, cout)
+        xl = _xl_dgrad(cin, cout)
         if bs is not None and bs.consumers == 1 and bs.x2 is not None:
             _STATS["fold_bnbwd_epilogue"] += 1
             inv = bs.invstd if bs.y2 is None else None

@@ -49,6 +49,16 @@ def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
     from distributed_model_parallel_amd.utils import checkpointing
     torch.manual_seed(0)
     m = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
+    if arch == "resnet50":
+        # tame the random-init residual branches (gamma 0.25 on each block's
+        # last BN, between the stock 1 and zero_init_residual's 0): at gamma 1 the
+        # 16 blocks amplify bf16 rounding so much at batch 8 that even the SAME
+        # kernels in a different backward order land at gradient cosine 0.86-0.99
+        # run to run (round 4), and both bf16 paths at 0.13 from fp32
+        with torch.no_grad():
+            for mod in m.modules():
+                if hasattr(mod, "bn3"):
+                    mod.bn3.weight.mul_(0.25)
     m0_state = {k: v.clone() for k, v in m.state_dict().items()}
     cast_model(m, torch.bfloat16)
     m2, m3 = copy.deepcopy(m), copy.deepcopy(m)
@@ -90,6 +100,12 @@ def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
     # and ~0.24-0.29 from each other (tools/ckpt_grad_diag.py, round 4: rounding
     # chaos, no stage worse on either path), so judge each against an fp32
     # oracle of the same weights: the checkpointed path no further than the fused
+    # (MobileNetV2 at 32 px is not chaotic that way: fused ~ checkpointed > 0.9
+    # directly; its stock fp32 channels-last backward aborted inside MIOpen on
+    # the box once, so no oracle there)
+    if arch != "resnet50":
+        assert _grad_cos(m, m2) > 0.9
+        return
     ref = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
     ref.load_state_dict({k: v.float() for k, v in m0_state.items()})
     with _native.reference_mode():

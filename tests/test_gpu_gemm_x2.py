@@ -159,3 +159,27 @@ def test_x2_falls_back_when_n_not_multiple_of_128(C):
     (c0, m0), (c1, m1) = both(C, lambda: C.gemm_xl_conv(a, b, "moments"))
     torch.testing.assert_close(c0, c1)
     torch.testing.assert_close(m0, m1)
+
+
+@pytest.mark.parametrize("w,rows", [(128, 4096 + 77), (256, 2048 + 33)])
+def test_fold_dgrad_bnbwd_xl_matches_nt(C, w, rows):
+    """The folded bottleneck data gradient da = [dz | a] @ Bb^T + ebias with the
+    producer BN's backward in the epilogue, as ops/bn_fold._FoldDgrad routes it
+    from round 4 (N = 128 / 256 on gemm_xl_conv: x2 / ping-pong kernel) against
+    the NT conv GEMM it used before (same operands, same reduction)."""
+    torch.manual_seed(5)
+    dz = torch.randn(rows, 4 * w, device=DEV).bfloat16()
+    a = torch.randn(rows, w, device=DEV).bfloat16()
+    Bb = (torch.randn(w, 5 * w, device=DEV) * 0.05).bfloat16()
+    eb = torch.randn(w, device=DEV) * 0.1
+    x = torch.randn(rows, w, device=DEV).bfloat16()
+    mean = torch.randn(w, device=DEV) * 0.1
+    inv = torch.rand(w, device=DEV) + 0.5
+    bw = torch.rand(w, device=DEV) + 0.5
+    bb = torch.randn(w, device=DEV) * 0.1
+    ref, rs = C.gemm_nt_bnbwd(dz, Bb, None, x, None, mean, inv, bw, bb, a2=a, ebias=eb)
+    out, os_ = C.gemm_xl_conv(dz, Bb, "bnbwd", bn_x=x, mean=mean, invstd=inv, weight=bw, bias=bb, a2=a, ebias=eb)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.float(), ref.float(), atol=3e-2, rtol=1e-2)
+    tol = 2e-2 * rows ** 0.5
+    torch.testing.assert_close(os_[: 2 * w], rs[: 2 * w], atol=tol, rtol=1e-2)

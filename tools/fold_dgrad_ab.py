@@ -75,6 +75,19 @@ def main():
         print(f"| {name} | {M} | {w} | {4 * w} | {t_nt:.4f} | {t_xl:.4f} | {t_nt / t_xl:.2f} | {pick} |", flush=True)
         del a, W, res
         torch.cuda.empty_cache()
+    print(f"\n# bottleneck conv1 forward with BN moments (K = block input, N = width), batch {n}\n")
+    print("| stage | M | K | N | gemm_nt moments ms | gemm_xl_conv moments ms | nt/xl | rule picks |")
+    print("|---|---|---|---|---|---|---|---|")
+    for name, w, hw in (("l1", 64, 56), ("l2", 128, 28), ("l3", 256, 14), ("l4", 512, 7)):
+        M = n * hw * hw
+        a = torch.randn(M, 4 * w, device="cuda").to(dt)
+        W = (torch.randn(w, 4 * w, device="cuda") * 0.05).to(dt)
+        t_nt = timeit(lambda: C.gemm_nt(a, W, mode="moments"))
+        t_xl = timeit(lambda: C.gemm_xl_conv(a, W, "moments"))
+        pick = "xl" if conv1x1._xl(w, 4 * w) else "nt"
+        print(f"| {name} | {M} | {4 * w} | {w} | {t_nt:.4f} | {t_xl:.4f} | {t_nt / t_xl:.2f} | {pick} |", flush=True)
+        del a, W
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
