@@ -59,11 +59,14 @@ _XL = not _native.disabled("xl_conv")
 
 
 def _xl(n: int, k: int) -> bool:
-    """Output width N, reduction K of a 1x1-conv GEMM where the 8-wave glds-ring
+    """Output width N, reduction K of a 1x1-conv GEMM where the ping-pong
     kernel (gemm_xl_conv) measured faster than the 4-wave NT kernel with the
-    same epilogue (profiles/conv1x1_xl.md, batch 1024): wide outputs with a
-    moderate K.  Narrow N (<= 128) and very short / very deep K stay on NT."""
-    return _XL and k >= 128 and k % 64 == 0 and (n >= 512 or (n >= 256 and k <= 512))
+    same epilogue: N >= 256 with K >= 128.  Round 2 kept N = 256 / K > 512 on
+    NT (profiles/conv1x1_xl.md); after the round-4 epilogue changes layer 3's
+    conv1 forward (N = 256, K = 1024) runs 1.24x faster on it at batch 2048 and
+    1.31x at 256 (profiles/raw_r4/fold_dgrad_ab_r4ac.md).  Narrow N (<= 128)
+    and K = 64 stay on NT."""
+    return _XL and k >= 128 and k % 64 == 0 and n >= 256
 
 
 def _geom(stride: int, hi: int, wi: int):

@@ -37,7 +37,6 @@ def _grad_rel(a_mod, b_mod):
     return (num / max(den, 1e-30)) ** 0.5
 
 
-@pytest.mark.unvalidated
 @pytest.mark.parametrize("arch,size", [("resnet50", 64), ("mobilenetv2", 32)])
 def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
     """Reference: the same segments run WITHOUT recomputation but inside the

@@ -255,7 +255,6 @@ def _bench_routes(steps=2):
     return out
 
 
-@pytest.mark.unvalidated
 def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
     """ResNet-50 at 224 px (the bench's kernel routing:
     stem_halo, halo c64/c128 forward / dgrad / wgrad, stride-phase dgrads,
