@@ -88,21 +88,35 @@ template <> struct Raw8<float> {
   }
 };
 
-template <typename T, typename P, int kMaxV>
+// Sum over the LPR lanes of a row group (xor offsets < LPR stay inside it).
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// RPW rows per wave pass: LPR = 64 / RPW lanes per row, lane l serves vectors
+// (l % LPR) + LPR k of row 2 pass + l / LPR.  RPW = 2 for D = 768 (ViT-B): 32
+// lanes x 3 vectors cover a row exactly (one row per wave left half the lanes
+// idle on the third vector) and a wave keeps two rows = 3 KB of loads in
+// flight instead of one.
+template <typename T, typename P, int kMaxV, int RPW = 1>
 __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict__ x,
                                                             const P* __restrict__ w,
                                                             const P* __restrict__ b, int64_t rows,
                                                             int D, float eps, T* __restrict__ y,
                                                             float* __restrict__ mean_out,
                                                             float* __restrict__ rstd_out) {
-  const int lane = threadIdx.x & 63;
+  constexpr int LPR = 64 / RPW;
+  const int lane = (threadIdx.x & 63) % LPR, sub = (threadIdx.x & 63) / LPR;
   const int nv = D / 8;
-  const int64_t wave = (int64_t)blockIdx.x * (kLnThreads / 64) + (threadIdx.x >> 6);
-  const int64_t nwaves = (int64_t)gridDim.x * (kLnThreads / 64);
+  const int64_t wave = ((int64_t)blockIdx.x * (kLnThreads / 64) + (threadIdx.x >> 6)) * RPW + sub;
+  const int64_t nwaves = (int64_t)gridDim.x * (kLnThreads / 64) * RPW;
   float gw[kMaxV][8], gb[kMaxV][8];
 #pragma unroll
   for (int k = 0; k < kMaxV; ++k) {
-    const int c = lane + 64 * k;
+    const int c = lane + LPR * k;
     if (c < nv) {
       if (w) PVec<P>::load(w + c * 8, gw[k]);
       else for (int i = 0; i < 8; ++i) gw[k][i] = 1.f;
@@ -117,7 +131,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
   auto fetch = [&](int64_t r) {
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) nx[k].load(x + r * D + c * 8);
     }
   };
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) {
         nx[k].get(v[k]);
 #pragma unroll
@@ -135,11 +149,11 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
       }
     }
     if (r + nwaves < rows) fetch(r + nwaves);
-    const float mean = wave_sum(s) / (float)D;
+    const float mean = group_sum<LPR>(s) / (float)D;
     float q = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -148,11 +162,11 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
         }
       }
     }
-    const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+    const float rstd = rsqrtf(group_sum<LPR>(q) / (float)D + eps);
     T* yr = y + r * D;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) {
         float o[8];
 #pragma unroll
@@ -172,19 +186,20 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
 // current row is reduced and written (one row of loads always in flight per
 // wave): with one wave per row the kernel is otherwise latency-bound, not
 // bandwidth-bound (85 us -> see profiles/vit_b16_bs128_1gpu_v3.md).
-template <typename T, typename P, int kMaxV>
+template <typename T, typename P, int kMaxV, int RPW = 1>
 __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const P* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, int64_t rows, int D,
     T* __restrict__ dx, float* __restrict__ part, const T* __restrict__ dres) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int LPR = 64 / RPW;  // lanes per row (see ln_fwd_kernel)
+  const int lane = (threadIdx.x & 63) % LPR, sub = (threadIdx.x & 63) / LPR, wid = threadIdx.x >> 6;
   const int nv = D / 8;
-  const int64_t wave = (int64_t)blockIdx.x * (kLnThreads / 64) + wid;
-  const int64_t nwaves = (int64_t)gridDim.x * (kLnThreads / 64);
+  const int64_t wave = ((int64_t)blockIdx.x * (kLnThreads / 64) + wid) * RPW + sub;
+  const int64_t nwaves = (int64_t)gridDim.x * (kLnThreads / 64) * RPW;
   float gw[kMaxV][8], accw[kMaxV][8], accb[kMaxV][8];
 #pragma unroll
   for (int k = 0; k < kMaxV; ++k) {
-    const int c = lane + 64 * k;
+    const int c = lane + LPR * k;
 #pragma unroll
     for (int i = 0; i < 8; ++i) { accw[k][i] = 0.f; accb[k][i] = 0.f; gw[k][i] = 1.f; }
     if (c < nv && w) PVec<P>::load(w + c * 8, gw[k]);
@@ -196,7 +211,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
     nrstd = rstd_in[r];
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) {
         nx[k].load(x + r * D + c * 8);
         ndy[k].load(dy + r * D + c * 8);
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) {
         float dv[8];
         nx[k].get(xh[k]);
@@ -229,10 +244,10 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
       }
     }
     if (r + nwaves < rows) fetch(r + nwaves);  // next row in flight during the reduce + store
-    const float c1 = wave_sum(s1) / (float)D, c2 = wave_sum(s2) / (float)D;
+    const float c1 = group_sum<LPR>(s1) / (float)D, c2 = group_sum<LPR>(s2) / (float)D;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + 64 * k;
+      const int c = lane + LPR * k;
       if (c < nv) {
         float o[8];
 #pragma unroll
@@ -245,24 +260,26 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
       }
     }
   }
-  // combine the 4 waves' column partials through LDS, one partial row per block
-  __shared__ float red[2][kLnThreads / 64][64 * 8];
+  // combine the column partials of the 4 waves x RPW row groups through LDS,
+  // one partial row per block
+  constexpr int G = kLnThreads / 64 * RPW;
+  __shared__ float red[2][G][LPR * 8];
 #pragma unroll
   for (int k = 0; k < kMaxV; ++k) {
-    const int c = lane + 64 * k;
-    if (k * 64 >= nv) break;
+    const int c = lane + LPR * k;
+    if (k * LPR >= nv) break;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      red[0][wid][lane * 8 + i] = accw[k][i];
-      red[1][wid][lane * 8 + i] = accb[k][i];
+      red[0][wid * RPW + sub][lane * 8 + i] = accw[k][i];
+      red[1][wid * RPW + sub][lane * 8 + i] = accb[k][i];
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 64 * 8; e += kLnThreads) {
-      const int col = (k * 64 + e / 8) * 8 + (e % 8);
+    for (int e = threadIdx.x; e < LPR * 8; e += kLnThreads) {
+      const int col = (k * LPR + e / 8) * 8 + (e % 8);
       if (col < D) {
         float sw = 0.f, sb = 0.f;
 #pragma unroll
-        for (int q = 0; q < kLnThreads / 64; ++q) { sw += red[0][q][e]; sb += red[1][q][e]; }
+        for (int q = 0; q < G; ++q) { sw += red[0][q][e]; sb += red[1][q][e]; }
         part[(int64_t)blockIdx.x * 2 * D + col] = sw;
         part[(int64_t)blockIdx.x * 2 * D + D + col] = sb;
       }
@@ -307,7 +324,7 @@ std::vector<at::Tensor> layernorm_forward(const at::Tensor& x, const c10::option
   const bool pbf = (hw && w->scalar_type() == at::kBFloat16) || (!hw && hb && b->scalar_type() == at::kBFloat16);
   const dim3 grid(ln_blocks(rows)), block(kLnThreads);
 #define DMP_LN_FWD(T, P)                                                                       \
-  hipLaunchKernelGGL((D <= 1024 ? ln_fwd_kernel<T, P, 2> : ln_fwd_kernel<T, P, 4>), grid, block, 0, stream, \
+  hipLaunchKernelGGL((D == 768 ? ln_fwd_kernel<T, P, 3, 2> : D <= 1024 ? ln_fwd_kernel<T, P, 2> : ln_fwd_kernel<T, P, 4>), grid, block, 0, stream, \
                      reinterpret_cast<const T*>(x.data_ptr()),                                 \
                      hw ? reinterpret_cast<const P*>(w->data_ptr()) : nullptr,                 \
                      hb ? reinterpret_cast<const P*>(b->data_ptr()) : nullptr, rows, (int)D,   \
@@ -349,7 +366,7 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
   auto part = at::empty({nb, 2 * D}, x.options().dtype(at::kFloat));
   const bool pbf = hw && w->scalar_type() == at::kBFloat16;
 #define DMP_LN_BWD(T, P)                                                                        \
-  hipLaunchKernelGGL((D <= 1024 ? ln_bwd_kernel<T, P, 2> : ln_bwd_kernel<T, P, 4>), dim3(nb), dim3(kLnThreads), 0, stream, \
+  hipLaunchKernelGGL((D == 768 ? ln_bwd_kernel<T, P, 3, 2> : D <= 1024 ? ln_bwd_kernel<T, P, 2> : ln_bwd_kernel<T, P, 4>), dim3(nb), dim3(kLnThreads), 0, stream, \
                      reinterpret_cast<const T*>(dy.data_ptr()),                                 \
                      reinterpret_cast<const T*>(x.data_ptr()),                                  \
                      hw ? reinterpret_cast<const P*>(w->data_ptr()) : nullptr,                  \

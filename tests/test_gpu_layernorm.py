@@ -10,7 +10,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("dtype,pdtype", [(torch.bfloat16, torch.bfloat16), (torch.bfloat16, torch.float32),
                                           (torch.float32, torch.float32)])
-@pytest.mark.parametrize("shape", [(128, 197, 768), (7, 1024), (3, 5, 1536), (2, 2048), (1000, 64)])
+@pytest.mark.parametrize("shape", [(128, 197, 768), (3, 5, 768), (7, 1024), (3, 5, 1536), (2, 2048), (1000, 64)])
 def test_layernorm_fwd_bwd(dtype, pdtype, shape):
     torch.manual_seed(0)
     d = shape[-1]
