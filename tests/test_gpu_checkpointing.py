@@ -92,7 +92,10 @@ def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
     assert cos > 0.95, f"checkpointed vs same-kernel reference: gradient cosine {cos:.4f}"
     for (n, a), b in zip(m3.named_buffers(), m2.buffers()):
         if a.dtype.is_floating_point:
-            torch.testing.assert_close(b.float(), a.float(), atol=1e-3, rtol=1e-3, msg=n)
+            # (1e-2: the forward's rare fp64-atomic-order rounding flips reach
+            # layer 3's batch variance; a second running-stat update in the
+            # recompute is caught exactly by num_batches_tracked below)
+            torch.testing.assert_close(b.float(), a.float(), atol=1e-2, rtol=1e-2, msg=n)
         else:
             assert torch.equal(a, b), n  # num_batches_tracked: one update, not two
     torch.testing.assert_close(l2.float(), l1.float(), atol=0.1, rtol=0.1)
