@@ -110,6 +110,8 @@ int get_gemm_xl_pipe();
 void set_gemm_xl_x2(int mode);
 int get_gemm_xl_x2();
 void set_gemm_xl_nt(int on);
+void set_gemm_xl_tail(int on);
+int get_gemm_xl_tail();
 int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
                                 int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
@@ -338,6 +340,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_gemm_xl_x2", &dmp::get_gemm_xl_x2);
   m.def("set_gemm_xl_nt", &dmp::set_gemm_xl_nt, py::arg("on"),
         "conv-epilogue GEMMs: non-temporal C stores / residual loads (A/B; env DMP_XL_NT)");
+  m.def("set_gemm_xl_tail", &dmp::set_gemm_xl_tail, py::arg("on"),
+        "256x256 ping-pong GEMMs: split-K for the last partial round of tiles (default on; env DMP_XL_TAIL)");
+  m.def("get_gemm_xl_tail", &dmp::get_gemm_xl_tail);
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");

@@ -106,6 +106,13 @@ __device__ __forceinline__ int chunk_xor(int q) { return (0x78 >> (2 * (q & 3)))
 // run concurrently), then groups of GM M-tiles walked column by column, so
 // the ~32 tiles resident on one XCD form a GM x 32/GM patch whose A and B
 // panels are both reused from that XCD's L2.
+__device__ __forceinline__ void tile_coords_id(int bid, int mtiles, int ntiles, int gm_max, int& mt, int& nt) {
+  const int per_group = gm_max * ntiles;
+  const int g = bid / per_group, r = bid - g * per_group;
+  const int gm = min(gm_max, mtiles - g * gm_max);
+  mt = g * gm_max + r % gm;
+  nt = r / gm;
+}
 __device__ __forceinline__ void tile_coords(int nblocks, int mtiles, int ntiles, int gm_max,
                                             int& mt, int& nt) {
   const int bid = xcd_remap(blockIdx.x, nblocks);
@@ -189,532 +196,28 @@ struct XlArgs {
   const float *esc, *esh;       // XL_AFFINE coefficients (null: 1 / 0)
   int erelu;                    // XL_AFFINE ReLU
   int cnt;                      // conv epilogues: non-temporal C stores / residual loads (streamed once)
+  // split-K tail (PIPE 7): a launch with tbase > 0, ksplit == 0 runs tiles
+  // [0, tbase) of the tile order; one with ksplit > 0 runs each tile
+  // tbase + b / ksplit over K tiles [(b % ksplit) kper, +kper) and writes fp32
+  // partials to skws (gemm_xl_tail_epi sums them and runs the epilogue)
+  int tbase, ksplit, kper;
+  float* skws;
 };
 
-template <int BN, int EPI, int PIPE>
-__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p) {
+// Epilogue of the NT kernel (and of a split-K tail tile, gemm_xl_tail_epi):
+// (acc [+ bias]) -> bf16 tile in LDS, then the row-contiguous pass with the
+// fused operation; acc in the PIPE's register layout (7 / 8: transposed).
+template <int BN, int EPI, int PIPE, int LDS>
+__device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN / 64], char* smem, int m0, int n0,
+                                            int mt, int mtiles) {
   constexpr int WTM = 128, WTN = BN / 4;
-  constexpr int MI = WTM / 16, NI = WTN / 16;       // 8 x (4 | 2) accumulators
-  constexpr int RA = XBM * 64, RB = BN * 64;        // bytes of one k32 region
-  constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;  // glds per wave per region
-  constexpr int STAGE_LDS = PIPE == 8 ? XL_RING_SLOTS * 16384 : 4 * RA + 4 * RB;
+  constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int CT_STRIDE = BN + 8;
-  constexpr int EPI_LDS = XBM * CT_STRIDE * 2;
-  constexpr int LDS = STAGE_LDS > EPI_LDS ? STAGE_LDS : EPI_LDS;
-  constexpr int W2 = 2 * (NA + NB);  // glds per wave per K tile
-  static_assert(NA >= 1 && NB >= 1, "region smaller than one glds round");
-  __shared__ __attribute__((aligned(16))) char smem[LDS];
-  // XL_DGELU: column sums of the output (fc1's bias gradient) when p.part is set
   constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD || EPI == XL_DGELU;
-  if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
-
-  const bf16* __restrict__ A = p.A;
-  const bf16* __restrict__ B = p.B;
-  const int64_t lda = p.lda, ldb = p.ldb;
-  const int M = p.M, N = p.N, K = p.K;
+  const int M = p.M, N = p.N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + BN - 1) / BN;
-  int mt, nt;
-  tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
-  const int m0 = mt * XBM, n0 = nt * BN;
-  const int ktiles = K / XBK;
-
-  // ---- staging: lane L of a 1 KB glds instruction writes LDS bytes L*16..+16
-  // of 16 rows x 64 B; the logical 16-B chunk it carries is the physical one
-  // XOR swz(row) (row & 15 = L >> 2, so the XOR depends on L >> 4 only).
-  const int srow = lane >> 2;
-  const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
-  const bf16* asrc[NA];
-  const bf16* asrc2[NA];
-  const bf16* bsrc[NB];
-#pragma unroll
-  for (int q = 0; q < NA; ++q) {
-    const int r = (wave * NA + q) * 16 + srow;
-    asrc[q] = A + (int64_t)min(m0 + r, M - 1) * lda + schunk * 8;
-    asrc2[q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + r, M - 1)) * p.lda2 + schunk * 8 - p.K1 : nullptr;
-  }
-#pragma unroll
-  for (int q = 0; q < NB; ++q) {
-    const int r = (wave * NB + q) * 16 + srow;
-    bsrc[q] = B + (int64_t)min(n0 + r, N - 1) * ldb + schunk * 8;
-  }
-  auto a_region = [&](int ks, int buf) { return smem + (buf * 2 + ks) * RA; };
-  auto b_region = [&](int ks, int buf) { return smem + 4 * RA + (buf * 2 + ks) * RB; };
-  auto stage_a = [&](int ks, int kt, int buf) {
-    char* dst = a_region(ks, buf) + wave * NA * 1024;
-    const int koff = kt * XBK + ks * 32;
-    const bool second = p.A2 && koff >= p.K1;
-#pragma unroll
-    for (int q = 0; q < NA; ++q) glds16((second ? asrc2[q] : asrc[q]) + koff, dst + q * 1024);
-  };
-  auto stage_b = [&](int ks, int kt, int buf) {
-    char* dst = b_region(ks, buf) + wave * NB * 1024;
-    const int koff = kt * XBK + ks * 32;
-#pragma unroll
-    for (int q = 0; q < NB; ++q) glds16(bsrc[q] + koff, dst + q * 1024);
-  };
-
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int lrow = lane & 15, lk = lane >> 4;
-  // fragment byte offset of row r (multiple of 16 + lrow) in a k32 region
-  const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
-  bf16x8 fb[NI];
-
-  auto phase = [&](int ks, int mh, int buf) {
-    const char* ar = a_region(ks, buf) + (wr * WTM + mh * 64) * 64 + frag_off;
-    bf16x8 fa[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
-    if (mh == 0) {
-      const char* br = b_region(ks, buf) + (wc * WTN) * 64 + frag_off;
-#pragma unroll
-      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-        acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[mh * 4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  if constexpr (PIPE == 0) {
-  // ---- prologue: tile 0 (both halves) and tile 1's k0 half in flight ----
-  stage_a(0, 0, 0);
-  stage_b(0, 0, 0);
-  stage_a(1, 0, 0);
-  stage_b(1, 0, 0);
-  if (ktiles > 1) {
-    stage_a(0, 1, 1);
-    stage_b(0, 1, 1);
-    vmcnt<W2>();
-  } else {
-    vmcnt<NA + NB>();
-  }
-  barrier();
-
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const int buf = kt & 1;
-    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
-    // phase 0: k0 half, M half 0; stage tile kt+1's A k1 half
-    if (has1) stage_a(1, kt + 1, buf ^ 1);
-    phase(0, 0, buf);
-    barrier();
-    // phase 1: k0, M half 1; stage tile kt+1's B k1; retire tile kt's k1 half
-    if (has1) stage_b(1, kt + 1, buf ^ 1);
-    phase(0, 1, buf);
-    if (has1) vmcnt<W2>(); else vmcnt<0>();
-    barrier();
-    // phase 2: k1, M half 0; this tile's k0 regions are free: stage tile kt+2's A k0
-    if (has2) stage_a(0, kt + 2, buf);
-    phase(1, 0, buf);
-    barrier();
-    // phase 3: k1, M half 1; stage kt+2's B k0; retire tile kt+1's k0 half
-    if (has2) stage_b(0, kt + 2, buf);
-    phase(1, 1, buf);
-    if (has2) vmcnt<W2>(); else if (has1) vmcnt<NA + NB>(); else vmcnt<0>();
-    barrier();
-  }
-  } else if constexpr (PIPE == 7) {
-  // ---- PIPE 7: ping-pong quadrant schedule (cdna_hip_programming.md §5 "256²
-  // 8-phase template").  The two wave rows (wr) run one barrier apart: while
-  // one group's 4 waves run a phase's 16 MFMAs, the other group (one wave on
-  // each SIMD) issues that phase's ds_reads and LDS-DMA copies, so every SIMD
-  // alternates a MFMA wave and a memory wave between consecutive barriers.
-  // A K tile is 4 phases, one per quadrant (m half, n half) of the wave's
-  // 128 x 64 outputs, in the order (0,0) (0,1) (1,1) (1,0) so that each phase
-  // re-reads only one operand.  A tile's operands are staged as 4 units of
-  // 16 KB (2 glds per wave): U0 = A rows of m half 0, U3 = m half 1, U1 = B
-  // cols of n half 0, U2 = n half 1.  Phase r of tile t stages U3(t+1),
-  // U1(t+1), U0(t+2), U2(t+2) (r = 0..3): every unit is written >= 2 barrier
-  // slots after its previous contents were last read (WAR), and is retired by
-  // the vmcnt(4) of a phase >= 2 before its first reader (RAW: the counted
-  // wait -- never 0 in steady state -- then a barrier, then the ds_read).
-  static_assert(BN == 256, "ping-pong schedule is written for 256 x 256 tiles");
-  const int pks = wave >> 2;  // k32 half carried by this wave's two copies of a unit
-  const bf16* pa[2][2];
-  const bf16* pa2[2][2];
-  const bf16* pb[2][2];
-  int oa[2][2], ob[2][2];
-#pragma unroll
-  for (int v = 0; v < 2; ++v)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int j = (2 * wave + q) & 7;
-      const int ba = (j & 3) + 8 * (j >> 2) + 4 * v, bb = (j & 1) + 4 * (j >> 1) + 2 * v;
-      pa[v][q] = A + (int64_t)min(m0 + ba * 16 + srow, M - 1) * lda + schunk * 8 + pks * 32;
-      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ba * 16 + srow, M - 1)) * p.lda2 + schunk * 8 + pks * 32 -
-                             p.K1
-                       : nullptr;
-      pb[v][q] = B + (int64_t)min(n0 + bb * 16 + srow, N - 1) * ldb + schunk * 8 + pks * 32;
-      oa[v][q] = ba * 1024;
-      ob[v][q] = bb * 1024;
-    }
-  // conv gather: per staged A row, its top-left input pixel and coordinates
-  const XlConv cv = p.cv;
-  const bool gather = cv.cin > 0;
-  const int loff = schunk * 8 + pks * 32;
-  int gpix[2][2], gih[2][2], giw[2][2];
-  if (gather) {
-    const int hw = cv.ho * cv.wo;
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int j = (2 * wave + q) & 7;
-        const int row = min(m0 + ((j & 3) + 8 * (j >> 2) + 4 * v) * 16 + srow, M - 1);
-        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
-        gih[v][q] = oh * cv.stride - cv.pad;
-        giw[v][q] = ow * cv.stride - cv.pad;
-        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
-      }
-  }
-  auto stage_unit = [&](auto u, int kt) {
-    constexpr int U = decltype(u)::value;
-    const int buf = kt & 1, koff = kt * XBK;
-    if constexpr (U == 0 || U == 3) {
-      if (gather) {  // tap (tr, tc), channels c0.. of every staged output pixel, or zeros
-        const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
-        const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int ih = gih[U == 3][q] + tr, iw = giw[U == 3][q] + tc;
-          const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
-          const bf16* src = ok ? A + (int64_t)(gpix[U == 3][q] + tr * cv.wi + tc) * lda + c0 + loff
-                               : g_zero_row + loff;
-          glds16(src, a_region(pks, buf) + oa[U == 3][q]);
-        }
-        return;
-      }
-    }
-    const bool second = p.A2 && koff >= p.K1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if constexpr (U == 0 || U == 3)
-        glds16((second ? pa2[U == 3][q] : pa[U == 3][q]) + koff, a_region(pks, buf) + oa[U == 3][q]);
-      else
-        glds16(pb[U == 2][q] + koff, b_region(pks, buf) + ob[U == 2][q]);
-    }
-  };
-  bf16x8 qa[2][4], qb[2][2];
-  auto read_a = [&](int mq, int buf) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        qa[ks][i] = *reinterpret_cast<const bf16x8*>(a_region(ks, buf) + (wr * WTM + mq * 64 + i * 16) * 64 + frag_off);
-  };
-  auto read_b = [&](int nq, int buf) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        qb[ks][j] = *reinterpret_cast<const bf16x8*>(b_region(ks, buf) + (wc * WTN + nq * 32 + j * 16) * 64 + frag_off);
-  };
-  auto quad = [&](auto mqc, auto nqc) {
-    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    // operands swapped: acc holds C^T blocks (lane = output row, registers =
-    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[MQ * 4 + i][NQ * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    barrier();
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  stage_unit(I0{}, 0);
-  stage_unit(I2{}, 0);
-  stage_unit(I3{}, 0);
-  stage_unit(I1{}, 0);
-  if (ktiles > 1) {
-    stage_unit(I0{}, 1);
-    stage_unit(I2{}, 1);
-    vmcnt<4>();
-  } else {
-    vmcnt<0>();
-  }
-  barrier();
-  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const int buf = kt & 1;
-    const bool n1 = kt + 1 < ktiles, n2 = kt + 2 < ktiles;
-    read_a(0, buf);
-    read_b(0, buf);
-    if (n1) { stage_unit(I3{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I0{}, I0{});
-    read_b(1, buf);
-    if (n1) { stage_unit(I1{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I0{}, I1{});
-    read_a(1, buf);
-    if (n2) { stage_unit(I0{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I1{}, I1{});
-    read_b(0, buf);
-    if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I1{}, I0{});
-  }
-  if (wr == 0) barrier();  // equal barrier counts before the epilogue
-  barrier();
-  } else if constexpr (PIPE == 8) {
-  // ---- PIPE 8: the ping-pong quadrant schedule of PIPE 7 on a ring of NS
-  // 16 KB unit slots instead of two fixed tile buffers (finding 42: PIPE 7
-  // keeps only two units = 32 KB in flight per CU, ~650-700 TF/s; the same
-  // schedule without the operand stream runs 1.2 PF/s).  Units are numbered
-  // in issue order i = 4 t + k, k = 0..3 <-> U0 (A m half 0), U2 (B n half 1),
-  // U3 (A m half 1), U1 (B n half 0) of K tile t; with the quadrant order
-  // (0,0) (0,1) (1,1) (1,0) unit i is last read in phase i (phase g = 4 t + r).
-  // Unit i lives in slot i % NS and is issued in phase i - D, D = NS - 1, so
-  // it overwrites unit i - NS, last read in phase i - NS = (issue phase) - 1
-  // (WAR: >= 2 barriers, as PIPE 7).  Phase g may read up to unit g + 4 (U1 of
-  // the next tile), so the phase-g wait retires every unit <= g + 4 and leaves
-  // V = D - 4 = NS - 5 units in flight: 80 KB at NS = 10 (vmcnt 10).
-  // Slot layout: [k32 half 2][8 blocks][16 rows x 64 B] (the 1 KB block is
-  // PIPE 7's 16-row swizzled image); block bj holds rows (bj >> 2) * 128 +
-  // mq * 64 + (bj & 3) * 16 of an A unit, cols (bj >> 1) * 64 + nq * 32 +
-  // (bj & 1) * 16 of a B unit -- the same rows PIPE 7's staging lanes fetch.
-  static_assert(BN == 256, "ring schedule is written for 256 x 256 tiles");
-  constexpr int NS = XL_RING_SLOTS, D = NS - 1, V = NS - 5, SLOT = 16384;
-  static_assert(NS * SLOT <= 160 * 1024, "ring exceeds LDS");
-  const int pks = wave >> 2;
-  const int bj0 = (2 * wave) & 7;  // block of copy q is bj0 + q
-  const bf16* pa[2][2];
-  const bf16* pa2[2][2];
-  const bf16* pb[2][2];
-#pragma unroll
-  for (int v = 0; v < 2; ++v)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int j = bj0 + q;
-      const int ra = (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow;
-      const int rb = (j >> 1) * 64 + v * 32 + (j & 1) * 16 + srow;
-      pa[v][q] = A + (int64_t)min(m0 + ra, M - 1) * lda + schunk * 8 + pks * 32;
-      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ra, M - 1)) * p.lda2 + schunk * 8 + pks * 32 - p.K1
-                       : nullptr;
-      pb[v][q] = B + (int64_t)min(n0 + rb, N - 1) * ldb + schunk * 8 + pks * 32;
-    }
-  const XlConv cv = p.cv;
-  const bool gather = cv.cin > 0;
-  const int loff = schunk * 8 + pks * 32;
-  int gpix[2][2], gih[2][2], giw[2][2];
-  if (gather) {
-    const int hw = cv.ho * cv.wo;
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int j = bj0 + q;
-        const int row = min(m0 + (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow, M - 1);
-        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
-        gih[v][q] = oh * cv.stride - cv.pad;
-        giw[v][q] = ow * cv.stride - cv.pad;
-        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
-      }
-  }
-  const int U = 4 * ktiles;
-  // issue unit i (kind k = i & 3) into its slot; the per-kind operand tables
-  // are indexed by compile-time constants only (a runtime index would put
-  // them in scratch, cdna_hip_programming.md rule 20)
-  auto stage_a8 = [&](auto vc, int kt, char* dst) {
-    constexpr int VV = decltype(vc)::value;  // U0: m half 0, U3: m half 1
-    const int koff = kt * XBK;
-    if (gather) {
-      const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
-      const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int ih = gih[VV][q] + tr, iw = giw[VV][q] + tc;
-        const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
-        const bf16* src = ok ? A + (int64_t)(gpix[VV][q] + tr * cv.wi + tc) * lda + c0 + loff : g_zero_row + loff;
-        glds16(src, dst + q * 1024);
-      }
-      return;
-    }
-    const bool second = p.A2 && koff >= p.K1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) glds16((second ? pa2[VV][q] : pa[VV][q]) + koff, dst + q * 1024);
-  };
-  auto stage_b8 = [&](auto vc, int kt, char* dst) {
-    constexpr int VV = decltype(vc)::value;  // U1: n half 0, U2: n half 1
-#pragma unroll
-    for (int q = 0; q < 2; ++q) glds16(pb[VV][q] + kt * XBK, dst + q * 1024);
-  };
-  auto stage_i = [&](int i) {
-    const int kt = i >> 2, k = i & 3;
-    char* dst = smem + (i % NS) * SLOT + pks * 8192 + bj0 * 1024;
-    if (k == 0) stage_a8(std::integral_constant<int, 0>{}, kt, dst);
-    else if (k == 1) stage_b8(std::integral_constant<int, 1>{}, kt, dst);
-    else if (k == 2) stage_a8(std::integral_constant<int, 1>{}, kt, dst);
-    else stage_b8(std::integral_constant<int, 0>{}, kt, dst);
-  };
-  // retire every unit <= g + 4 given units < issued are in flight or done
-  auto wait_for = [&](int g, int issued) {
-    const int n = min(V, issued - 1 - (g + 4));
-    vmcnt_upto<2 * V>(n > 0 ? 2 * n : 0);
-  };
-  bf16x8 qa[2][4], qb[2][2];
-  auto read_a = [&](int slot) {
-    const char* base = smem + slot * SLOT + (wr * 4) * 1024 + frag_off;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) qa[ks][i] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + i * 1024);
-  };
-  auto read_b = [&](int slot) {
-    const char* base = smem + slot * SLOT + (wc * 2) * 1024 + frag_off;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) qb[ks][j] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + j * 1024);
-  };
-  auto quad = [&](auto mqc, auto nqc) {
-    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    // operands swapped: acc holds C^T blocks (lane = output row, registers =
-    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[MQ * 4 + i][NQ * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    barrier();
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  const int pro = min(D, U);
-  for (int i = 0; i < pro; ++i) stage_i(i);
-  wait_for(-1, pro);  // units 0..3 (tile 0) landed
-  barrier();
-  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
-  int issued = pro;
-  int s0 = 0;  // slot of unit 4 kt
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const int g = 4 * kt;
-    const int sU0 = s0, sU2 = s0 + 1 >= NS ? s0 + 1 - NS : s0 + 1;
-    const int sU3 = s0 + 2 >= NS ? s0 + 2 - NS : s0 + 2, sU1 = s0 + 3 >= NS ? s0 + 3 - NS : s0 + 3;
-    read_a(sU0);
-    read_b(sU1);
-    if (issued < U) stage_i(issued++);
-    wait_for(g, issued);
-    quad(I0{}, I0{});
-    read_b(sU2);
-    if (issued < U) stage_i(issued++);
-    wait_for(g + 1, issued);
-    quad(I0{}, I1{});
-    read_a(sU3);
-    if (issued < U) stage_i(issued++);
-    wait_for(g + 2, issued);
-    quad(I1{}, I1{});
-    read_b(sU1);
-    if (issued < U) stage_i(issued++);
-    wait_for(g + 3, issued);
-    quad(I1{}, I0{});
-    s0 = s0 + 4 >= NS ? s0 + 4 - NS : s0 + 4;
-  }
-  if (wr == 0) barrier();  // equal barrier counts before the epilogue
-  barrier();
-  } else {
-  // ---- PIPE 1: half-step ring.  Half-step s (K tile s/2, k32 half s%2) lives
-  // in LDS region s%4.  During half-step s: stage region s%4 with the data of
-  // half-step s+4 (its fragments were read in s-1 and retired before that
-  // step's barrier), ds_read the fragments of s+1 into the other register set
-  // (retired by the vmcnt at the end of s-1), run the 32 MFMAs of s.  One
-  // barrier per half-step; three half-steps of copies in flight.
-  const int S = 2 * ktiles;
-  auto stage_h = [&](int h) {
-    stage_a(h & 1, h >> 1, (h >> 1) & 1);
-    stage_b(h & 1, h >> 1, (h >> 1) & 1);
-  };
-  bf16x8 xa[MI], xb[NI], ya[MI], yb[NI];
-  auto read_frags = [&](bf16x8 (&fa)[MI], bf16x8 (&fbb)[NI], int h) {
-    const char* ar = smem + (h & 3) * RA + (wr * WTM) * 64 + frag_off;
-    const char* br = smem + 4 * RA + (h & 3) * RB + (wc * WTN) * 64 + frag_off;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) fbb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
-  };
-  auto mfmas = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fbb)[NI]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbb[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
-  // prologue: half-steps 0..3 in flight; retire 0, read it, retire 1
-  stage_h(0);
-  stage_h(1);
-  if (S >= 4) {
-    stage_h(2);
-    stage_h(3);
-    vmcnt<3 * (NA + NB)>();
-  } else {
-    vmcnt<NA + NB>();
-  }
-  barrier();
-  read_frags(xa, xb, 0);
-  if (S >= 4) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
-  lgkm0();
-  barrier();
-  // PIPE 2..4 are timing-only ablations (wrong results): 2 = no copies in the
-  // loop, 3 = no fragment reads in the loop, 4 = MFMAs only
-  constexpr bool kStage = PIPE != 2 && PIPE != 4, kRead = PIPE != 3 && PIPE != 4;  // 5: no epilogue
-  if constexpr (!kRead) read_frags(ya, yb, 1);
-  for (int s = 0; s < S; s += 2) {
-    if (kStage && s + 4 < S) stage_h(s + 4);
-    if (kRead) read_frags(ya, yb, s + 1);
-    mfmas(xa, xb);
-    if (s + 4 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
-    lgkm0();
-    barrier();
-    if (kStage && s + 5 < S) stage_h(s + 5);
-    if (kRead && s + 2 < S) read_frags(xa, xb, s + 2);
-    mfmas(ya, yb);
-    if (s + 5 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
-    lgkm0();
-    barrier();
-  }
-  }
-
-  // ---- epilogue: (acc [+ bias]) -> bf16 tile in LDS, then row-contiguous pass ----
-  if constexpr (PIPE == 5) {  // timing-only ablation: no epilogue (acc kept live)
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][3];
-    if (t == 12345.678f) p.C[tid] = (bf16)t;
-    return;
-  }
+  (void)lane;
   bf16* ct = reinterpret_cast<bf16*>(smem);
   // per-column affine applied to the fp32 accumulator BEFORE the bf16 staging:
   // a bias / BN shift that nearly cancels acc (XL_BNBWD's folded-BN constant,
@@ -973,6 +476,584 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       }
     }
   }
+}
+
+template <int BN, int EPI, int PIPE>
+__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p) {
+  constexpr int WTM = 128, WTN = BN / 4;
+  constexpr int MI = WTM / 16, NI = WTN / 16;       // 8 x (4 | 2) accumulators
+  constexpr int RA = XBM * 64, RB = BN * 64;        // bytes of one k32 region
+  constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;  // glds per wave per region
+  constexpr int STAGE_LDS = PIPE == 8 ? XL_RING_SLOTS * 16384 : 4 * RA + 4 * RB;
+  constexpr int CT_STRIDE = BN + 8;
+  constexpr int EPI_LDS = XBM * CT_STRIDE * 2;
+  constexpr int LDS = STAGE_LDS > EPI_LDS ? STAGE_LDS : EPI_LDS;
+  constexpr int W2 = 2 * (NA + NB);  // glds per wave per K tile
+  static_assert(NA >= 1 && NB >= 1, "region smaller than one glds round");
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  // XL_DGELU: column sums of the output (fc1's bias gradient) when p.part is set
+  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD || EPI == XL_DGELU;
+  if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
+
+  const bf16* __restrict__ A = p.A;
+  const bf16* __restrict__ B = p.B;
+  const int64_t lda = p.lda, ldb = p.ldb;
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + BN - 1) / BN;
+  int mt, nt;
+  int kt_begin = 0, kt_end = K / XBK;
+  if constexpr (PIPE == 9) {  // split-K tail launch: PIPE 7's loop over one K split, fp32 partials out
+    tile_coords_id(p.tbase + (int)blockIdx.x / p.ksplit, mtiles, ntiles, p.group_m, mt, nt);
+    kt_begin = ((int)blockIdx.x % p.ksplit) * p.kper;
+    kt_end = min(kt_end, kt_begin + p.kper);
+  } else if (p.tbase > 0) {  // the full rounds of a split-tail GEMM
+    tile_coords_id(xcd_remap(blockIdx.x, p.tbase), mtiles, ntiles, p.group_m, mt, nt);
+  } else {
+    tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
+  }
+  const int m0 = mt * XBM, n0 = nt * BN;
+  const int ktiles = K / XBK;
+
+  // ---- staging: lane L of a 1 KB glds instruction writes LDS bytes L*16..+16
+  // of 16 rows x 64 B; the logical 16-B chunk it carries is the physical one
+  // XOR swz(row) (row & 15 = L >> 2, so the XOR depends on L >> 4 only).
+  const int srow = lane >> 2;
+  const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
+  const bf16* asrc[NA];
+  const bf16* asrc2[NA];
+  const bf16* bsrc[NB];
+#pragma unroll
+  for (int q = 0; q < NA; ++q) {
+    const int r = (wave * NA + q) * 16 + srow;
+    asrc[q] = A + (int64_t)min(m0 + r, M - 1) * lda + schunk * 8;
+    asrc2[q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + r, M - 1)) * p.lda2 + schunk * 8 - p.K1 : nullptr;
+  }
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int r = (wave * NB + q) * 16 + srow;
+    bsrc[q] = B + (int64_t)min(n0 + r, N - 1) * ldb + schunk * 8;
+  }
+  auto a_region = [&](int ks, int buf) { return smem + (buf * 2 + ks) * RA; };
+  auto b_region = [&](int ks, int buf) { return smem + 4 * RA + (buf * 2 + ks) * RB; };
+  auto stage_a = [&](int ks, int kt, int buf) {
+    char* dst = a_region(ks, buf) + wave * NA * 1024;
+    const int koff = kt * XBK + ks * 32;
+    const bool second = p.A2 && koff >= p.K1;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) glds16((second ? asrc2[q] : asrc[q]) + koff, dst + q * 1024);
+  };
+  auto stage_b = [&](int ks, int kt, int buf) {
+    char* dst = b_region(ks, buf) + wave * NB * 1024;
+    const int koff = kt * XBK + ks * 32;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) glds16(bsrc[q] + koff, dst + q * 1024);
+  };
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int lrow = lane & 15, lk = lane >> 4;
+  // fragment byte offset of row r (multiple of 16 + lrow) in a k32 region
+  const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
+  bf16x8 fb[NI];
+
+  auto phase = [&](int ks, int mh, int buf) {
+    const char* ar = a_region(ks, buf) + (wr * WTM + mh * 64) * 64 + frag_off;
+    bf16x8 fa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
+    if (mh == 0) {
+      const char* br = b_region(ks, buf) + (wc * WTN) * 64 + frag_off;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[mh * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[mh * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if constexpr (PIPE == 0) {
+  // ---- prologue: tile 0 (both halves) and tile 1's k0 half in flight ----
+  stage_a(0, 0, 0);
+  stage_b(0, 0, 0);
+  stage_a(1, 0, 0);
+  stage_b(1, 0, 0);
+  if (ktiles > 1) {
+    stage_a(0, 1, 1);
+    stage_b(0, 1, 1);
+    vmcnt<W2>();
+  } else {
+    vmcnt<NA + NB>();
+  }
+  barrier();
+
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int buf = kt & 1;
+    const bool has1 = kt + 1 < ktiles, has2 = kt + 2 < ktiles;
+    // phase 0: k0 half, M half 0; stage tile kt+1's A k1 half
+    if (has1) stage_a(1, kt + 1, buf ^ 1);
+    phase(0, 0, buf);
+    barrier();
+    // phase 1: k0, M half 1; stage tile kt+1's B k1; retire tile kt's k1 half
+    if (has1) stage_b(1, kt + 1, buf ^ 1);
+    phase(0, 1, buf);
+    if (has1) vmcnt<W2>(); else vmcnt<0>();
+    barrier();
+    // phase 2: k1, M half 0; this tile's k0 regions are free: stage tile kt+2's A k0
+    if (has2) stage_a(0, kt + 2, buf);
+    phase(1, 0, buf);
+    barrier();
+    // phase 3: k1, M half 1; stage kt+2's B k0; retire tile kt+1's k0 half
+    if (has2) stage_b(0, kt + 2, buf);
+    phase(1, 1, buf);
+    if (has2) vmcnt<W2>(); else if (has1) vmcnt<NA + NB>(); else vmcnt<0>();
+    barrier();
+  }
+  } else if constexpr (PIPE == 7 || PIPE == 9) {
+  // ---- PIPE 7: ping-pong quadrant schedule (cdna_hip_programming.md §5 "256²
+  // 8-phase template").  The two wave rows (wr) run one barrier apart: while
+  // one group's 4 waves run a phase's 16 MFMAs, the other group (one wave on
+  // each SIMD) issues that phase's ds_reads and LDS-DMA copies, so every SIMD
+  // alternates a MFMA wave and a memory wave between consecutive barriers.
+  // A K tile is 4 phases, one per quadrant (m half, n half) of the wave's
+  // 128 x 64 outputs, in the order (0,0) (0,1) (1,1) (1,0) so that each phase
+  // re-reads only one operand.  A tile's operands are staged as 4 units of
+  // 16 KB (2 glds per wave): U0 = A rows of m half 0, U3 = m half 1, U1 = B
+  // cols of n half 0, U2 = n half 1.  Phase r of tile t stages U3(t+1),
+  // U1(t+1), U0(t+2), U2(t+2) (r = 0..3): every unit is written >= 2 barrier
+  // slots after its previous contents were last read (WAR), and is retired by
+  // the vmcnt(4) of a phase >= 2 before its first reader (RAW: the counted
+  // wait -- never 0 in steady state -- then a barrier, then the ds_read).
+  static_assert(BN == 256, "ping-pong schedule is written for 256 x 256 tiles");
+  const int pks = wave >> 2;  // k32 half carried by this wave's two copies of a unit
+  const bf16* pa[2][2];
+  const bf16* pa2[2][2];
+  const bf16* pb[2][2];
+  int oa[2][2], ob[2][2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = (2 * wave + q) & 7;
+      const int ba = (j & 3) + 8 * (j >> 2) + 4 * v, bb = (j & 1) + 4 * (j >> 1) + 2 * v;
+      pa[v][q] = A + (int64_t)min(m0 + ba * 16 + srow, M - 1) * lda + schunk * 8 + pks * 32;
+      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ba * 16 + srow, M - 1)) * p.lda2 + schunk * 8 + pks * 32 -
+                             p.K1
+                       : nullptr;
+      pb[v][q] = B + (int64_t)min(n0 + bb * 16 + srow, N - 1) * ldb + schunk * 8 + pks * 32;
+      oa[v][q] = ba * 1024;
+      ob[v][q] = bb * 1024;
+    }
+  // conv gather: per staged A row, its top-left input pixel and coordinates
+  const XlConv cv = p.cv;
+  const bool gather = cv.cin > 0;
+  const int loff = schunk * 8 + pks * 32;
+  int gpix[2][2], gih[2][2], giw[2][2];
+  if (gather) {
+    const int hw = cv.ho * cv.wo;
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = (2 * wave + q) & 7;
+        const int row = min(m0 + ((j & 3) + 8 * (j >> 2) + 4 * v) * 16 + srow, M - 1);
+        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+        gih[v][q] = oh * cv.stride - cv.pad;
+        giw[v][q] = ow * cv.stride - cv.pad;
+        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
+      }
+  }
+  auto stage_unit = [&](auto u, int kt) {
+    constexpr int U = decltype(u)::value;
+    const int buf = kt & 1, koff = kt * XBK;
+    if constexpr (U == 0 || U == 3) {
+      if (gather) {  // tap (tr, tc), channels c0.. of every staged output pixel, or zeros
+        const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
+        const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ih = gih[U == 3][q] + tr, iw = giw[U == 3][q] + tc;
+          const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
+          const bf16* src = ok ? A + (int64_t)(gpix[U == 3][q] + tr * cv.wi + tc) * lda + c0 + loff
+                               : g_zero_row + loff;
+          glds16(src, a_region(pks, buf) + oa[U == 3][q]);
+        }
+        return;
+      }
+    }
+    const bool second = p.A2 && koff >= p.K1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if constexpr (U == 0 || U == 3)
+        glds16((second ? pa2[U == 3][q] : pa[U == 3][q]) + koff, a_region(pks, buf) + oa[U == 3][q]);
+      else
+        glds16(pb[U == 2][q] + koff, b_region(pks, buf) + ob[U == 2][q]);
+    }
+  };
+  bf16x8 qa[2][4], qb[2][2];
+  auto read_a = [&](int mq, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        qa[ks][i] = *reinterpret_cast<const bf16x8*>(a_region(ks, buf) + (wr * WTM + mq * 64 + i * 16) * 64 + frag_off);
+  };
+  auto read_b = [&](int nq, int buf) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        qb[ks][j] = *reinterpret_cast<const bf16x8*>(b_region(ks, buf) + (wc * WTN + nq * 32 + j * 16) * 64 + frag_off);
+  };
+  auto quad = [&](auto mqc, auto nqc) {
+    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    // operands swapped: acc holds C^T blocks (lane = output row, registers =
+    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[MQ * 4 + i][NQ * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  // K tiles [kt_begin, kt_end): the whole K, or one split of a tail tile
+  // (kt_begin even, so K tile kt still lives in buffer kt & 1)
+  stage_unit(I0{}, kt_begin);
+  stage_unit(I2{}, kt_begin);
+  stage_unit(I3{}, kt_begin);
+  stage_unit(I1{}, kt_begin);
+  if (kt_end - kt_begin > 1) {
+    stage_unit(I0{}, kt_begin + 1);
+    stage_unit(I2{}, kt_begin + 1);
+    vmcnt<4>();
+  } else {
+    vmcnt<0>();
+  }
+  barrier();
+  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = kt & 1;
+    const bool n1 = kt + 1 < kt_end, n2 = kt + 2 < kt_end;
+    read_a(0, buf);
+    read_b(0, buf);
+    if (n1) { stage_unit(I3{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I0{}, I0{});
+    read_b(1, buf);
+    if (n1) { stage_unit(I1{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I0{}, I1{});
+    read_a(1, buf);
+    if (n2) { stage_unit(I0{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I1{}, I1{});
+    read_b(0, buf);
+    if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I1{}, I0{});
+  }
+  if (wr == 0) barrier();  // equal barrier counts before the epilogue
+  barrier();
+  } else if constexpr (PIPE == 8) {
+  // ---- PIPE 8: the ping-pong quadrant schedule of PIPE 7 on a ring of NS
+  // 16 KB unit slots instead of two fixed tile buffers (finding 42: PIPE 7
+  // keeps only two units = 32 KB in flight per CU, ~650-700 TF/s; the same
+  // schedule without the operand stream runs 1.2 PF/s).  Units are numbered
+  // in issue order i = 4 t + k, k = 0..3 <-> U0 (A m half 0), U2 (B n half 1),
+  // U3 (A m half 1), U1 (B n half 0) of K tile t; with the quadrant order
+  // (0,0) (0,1) (1,1) (1,0) unit i is last read in phase i (phase g = 4 t + r).
+  // Unit i lives in slot i % NS and is issued in phase i - D, D = NS - 1, so
+  // it overwrites unit i - NS, last read in phase i - NS = (issue phase) - 1
+  // (WAR: >= 2 barriers, as PIPE 7).  Phase g may read up to unit g + 4 (U1 of
+  // the next tile), so the phase-g wait retires every unit <= g + 4 and leaves
+  // V = D - 4 = NS - 5 units in flight: 80 KB at NS = 10 (vmcnt 10).
+  // Slot layout: [k32 half 2][8 blocks][16 rows x 64 B] (the 1 KB block is
+  // PIPE 7's 16-row swizzled image); block bj holds rows (bj >> 2) * 128 +
+  // mq * 64 + (bj & 3) * 16 of an A unit, cols (bj >> 1) * 64 + nq * 32 +
+  // (bj & 1) * 16 of a B unit -- the same rows PIPE 7's staging lanes fetch.
+  static_assert(BN == 256, "ring schedule is written for 256 x 256 tiles");
+  constexpr int NS = XL_RING_SLOTS, D = NS - 1, V = NS - 5, SLOT = 16384;
+  static_assert(NS * SLOT <= 160 * 1024, "ring exceeds LDS");
+  const int pks = wave >> 2;
+  const int bj0 = (2 * wave) & 7;  // block of copy q is bj0 + q
+  const bf16* pa[2][2];
+  const bf16* pa2[2][2];
+  const bf16* pb[2][2];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = bj0 + q;
+      const int ra = (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow;
+      const int rb = (j >> 1) * 64 + v * 32 + (j & 1) * 16 + srow;
+      pa[v][q] = A + (int64_t)min(m0 + ra, M - 1) * lda + schunk * 8 + pks * 32;
+      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ra, M - 1)) * p.lda2 + schunk * 8 + pks * 32 - p.K1
+                       : nullptr;
+      pb[v][q] = B + (int64_t)min(n0 + rb, N - 1) * ldb + schunk * 8 + pks * 32;
+    }
+  const XlConv cv = p.cv;
+  const bool gather = cv.cin > 0;
+  const int loff = schunk * 8 + pks * 32;
+  int gpix[2][2], gih[2][2], giw[2][2];
+  if (gather) {
+    const int hw = cv.ho * cv.wo;
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int j = bj0 + q;
+        const int row = min(m0 + (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow, M - 1);
+        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+        gih[v][q] = oh * cv.stride - cv.pad;
+        giw[v][q] = ow * cv.stride - cv.pad;
+        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
+      }
+  }
+  const int U = 4 * ktiles;
+  // issue unit i (kind k = i & 3) into its slot; the per-kind operand tables
+  // are indexed by compile-time constants only (a runtime index would put
+  // them in scratch, cdna_hip_programming.md rule 20)
+  auto stage_a8 = [&](auto vc, int kt, char* dst) {
+    constexpr int VV = decltype(vc)::value;  // U0: m half 0, U3: m half 1
+    const int koff = kt * XBK;
+    if (gather) {
+      const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
+      const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ih = gih[VV][q] + tr, iw = giw[VV][q] + tc;
+        const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
+        const bf16* src = ok ? A + (int64_t)(gpix[VV][q] + tr * cv.wi + tc) * lda + c0 + loff : g_zero_row + loff;
+        glds16(src, dst + q * 1024);
+      }
+      return;
+    }
+    const bool second = p.A2 && koff >= p.K1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) glds16((second ? pa2[VV][q] : pa[VV][q]) + koff, dst + q * 1024);
+  };
+  auto stage_b8 = [&](auto vc, int kt, char* dst) {
+    constexpr int VV = decltype(vc)::value;  // U1: n half 0, U2: n half 1
+#pragma unroll
+    for (int q = 0; q < 2; ++q) glds16(pb[VV][q] + kt * XBK, dst + q * 1024);
+  };
+  auto stage_i = [&](int i) {
+    const int kt = i >> 2, k = i & 3;
+    char* dst = smem + (i % NS) * SLOT + pks * 8192 + bj0 * 1024;
+    if (k == 0) stage_a8(std::integral_constant<int, 0>{}, kt, dst);
+    else if (k == 1) stage_b8(std::integral_constant<int, 1>{}, kt, dst);
+    else if (k == 2) stage_a8(std::integral_constant<int, 1>{}, kt, dst);
+    else stage_b8(std::integral_constant<int, 0>{}, kt, dst);
+  };
+  // retire every unit <= g + 4 given units < issued are in flight or done
+  auto wait_for = [&](int g, int issued) {
+    const int n = min(V, issued - 1 - (g + 4));
+    vmcnt_upto<2 * V>(n > 0 ? 2 * n : 0);
+  };
+  bf16x8 qa[2][4], qb[2][2];
+  auto read_a = [&](int slot) {
+    const char* base = smem + slot * SLOT + (wr * 4) * 1024 + frag_off;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) qa[ks][i] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + i * 1024);
+  };
+  auto read_b = [&](int slot) {
+    const char* base = smem + slot * SLOT + (wc * 2) * 1024 + frag_off;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) qb[ks][j] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + j * 1024);
+  };
+  auto quad = [&](auto mqc, auto nqc) {
+    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
+    barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    // operands swapped: acc holds C^T blocks (lane = output row, registers =
+    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[MQ * 4 + i][NQ * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  const int pro = min(D, U);
+  for (int i = 0; i < pro; ++i) stage_i(i);
+  wait_for(-1, pro);  // units 0..3 (tile 0) landed
+  barrier();
+  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
+  int issued = pro;
+  int s0 = 0;  // slot of unit 4 kt
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int g = 4 * kt;
+    const int sU0 = s0, sU2 = s0 + 1 >= NS ? s0 + 1 - NS : s0 + 1;
+    const int sU3 = s0 + 2 >= NS ? s0 + 2 - NS : s0 + 2, sU1 = s0 + 3 >= NS ? s0 + 3 - NS : s0 + 3;
+    read_a(sU0);
+    read_b(sU1);
+    if (issued < U) stage_i(issued++);
+    wait_for(g, issued);
+    quad(I0{}, I0{});
+    read_b(sU2);
+    if (issued < U) stage_i(issued++);
+    wait_for(g + 1, issued);
+    quad(I0{}, I1{});
+    read_a(sU3);
+    if (issued < U) stage_i(issued++);
+    wait_for(g + 2, issued);
+    quad(I1{}, I1{});
+    read_b(sU1);
+    if (issued < U) stage_i(issued++);
+    wait_for(g + 3, issued);
+    quad(I1{}, I0{});
+    s0 = s0 + 4 >= NS ? s0 + 4 - NS : s0 + 4;
+  }
+  if (wr == 0) barrier();  // equal barrier counts before the epilogue
+  barrier();
+  } else {
+  // ---- PIPE 1: half-step ring.  Half-step s (K tile s/2, k32 half s%2) lives
+  // in LDS region s%4.  During half-step s: stage region s%4 with the data of
+  // half-step s+4 (its fragments were read in s-1 and retired before that
+  // step's barrier), ds_read the fragments of s+1 into the other register set
+  // (retired by the vmcnt at the end of s-1), run the 32 MFMAs of s.  One
+  // barrier per half-step; three half-steps of copies in flight.
+  const int S = 2 * ktiles;
+  auto stage_h = [&](int h) {
+    stage_a(h & 1, h >> 1, (h >> 1) & 1);
+    stage_b(h & 1, h >> 1, (h >> 1) & 1);
+  };
+  bf16x8 xa[MI], xb[NI], ya[MI], yb[NI];
+  auto read_frags = [&](bf16x8 (&fa)[MI], bf16x8 (&fbb)[NI], int h) {
+    const char* ar = smem + (h & 3) * RA + (wr * WTM) * 64 + frag_off;
+    const char* br = smem + 4 * RA + (h & 3) * RB + (wc * WTN) * 64 + frag_off;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) fbb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
+  };
+  auto mfmas = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fbb)[NI]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbb[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto lgkm0 = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+  // prologue: half-steps 0..3 in flight; retire 0, read it, retire 1
+  stage_h(0);
+  stage_h(1);
+  if (S >= 4) {
+    stage_h(2);
+    stage_h(3);
+    vmcnt<3 * (NA + NB)>();
+  } else {
+    vmcnt<NA + NB>();
+  }
+  barrier();
+  read_frags(xa, xb, 0);
+  if (S >= 4) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+  lgkm0();
+  barrier();
+  // PIPE 2..4 are timing-only ablations (wrong results): 2 = no copies in the
+  // loop, 3 = no fragment reads in the loop, 4 = MFMAs only
+  constexpr bool kStage = PIPE != 2 && PIPE != 4, kRead = PIPE != 3 && PIPE != 4;  // 5: no epilogue
+  if constexpr (!kRead) read_frags(ya, yb, 1);
+  for (int s = 0; s < S; s += 2) {
+    if (kStage && s + 4 < S) stage_h(s + 4);
+    if (kRead) read_frags(ya, yb, s + 1);
+    mfmas(xa, xb);
+    if (s + 4 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+    lgkm0();
+    barrier();
+    if (kStage && s + 5 < S) stage_h(s + 5);
+    if (kRead && s + 2 < S) read_frags(xa, xb, s + 2);
+    mfmas(ya, yb);
+    if (s + 5 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
+    lgkm0();
+    barrier();
+  }
+  }
+
+  // ---- epilogue: (acc [+ bias]) -> bf16 tile in LDS, then row-contiguous pass ----
+  if constexpr (PIPE == 5) {  // timing-only ablation: no epilogue (acc kept live)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 12345.678f) p.C[tid] = (bf16)t;
+    return;
+  }
+  if constexpr (PIPE == 9) {  // split-K tail tile: fp32 partials, the epilogue runs in gemm_xl_tail_epi
+    // (a compile-time variant: as a runtime branch the write path cost the
+    // BN-backward epilogue 220 B of scratch per lane)
+    // thread-contiguous 512-B records (immediate store offsets: no per-store
+    // address registers in the epilogue's register budget)
+    f32x4* ws = reinterpret_cast<f32x4*>(p.skws) + ((int64_t)blockIdx.x * XTHREADS + tid) * (MI * NI);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) ws[i * NI + j] = acc[i][j];
+    return;
+  }
+  xl_epilogue<BN, EPI, PIPE, LDS>(p, acc, smem, m0, n0, mt, mtiles);
+}
+
+// Epilogue of the split-K tail tiles: block b sums the ksplit fp32 partials of
+// tile tbase + b (PIPE 7 register layout, written by the ksplit launch of
+// gemm_xl_nt_kernel) and runs that tile's epilogue.
+template <int EPI>
+__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_tail_epi(const XlArgs p) {
+  constexpr int BN = 256, MI = 8, NI = BN / 64;
+  constexpr int LDS = XBM * (BN + 8) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  const int mtiles = (p.M + XBM - 1) / XBM, ntiles = (p.N + BN - 1) / BN;
+  int mt, nt;
+  tile_coords_id(p.tbase + (int)blockIdx.x, mtiles, ntiles, p.group_m, mt, nt);
+  const int tid = threadIdx.x;
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sp = 0; sp < p.ksplit; ++sp) {  // split launch block blockIdx.x * ksplit + sp, same record layout
+    const f32x4* ws = reinterpret_cast<const f32x4*>(p.skws) +
+                      (((int64_t)blockIdx.x * p.ksplit + sp) * XTHREADS + tid) * (MI * NI);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] += ws[i * NI + j];
+  }
+  xl_epilogue<BN, EPI, 7, LDS>(p, acc, smem, mt * XBM, nt * BN, mt, mtiles);
 }
 
 // ---------------------------------------------------------------------------
@@ -1749,12 +1830,53 @@ constexpr int kXlPipeDefault = 7;
 int g_xl_pipe = kXlPipeDefault;
 
 // 256 x 256 ping-pong launch (PIPE 7 or its ring form, PIPE 8)
+// Split-K tail (DMP_XL_TAIL=1, set_gemm_xl_tail; default OFF): one block per
+// CU makes a grid's last, partly filled round cost a whole round (conv_xl at
+// batch 2048: layer 3, 6.1 rounds, 0.619 ms vs 0.513 ms at 6.0; layer 4, 3.06
+// rounds, 0.579 vs 0.448 ms; profiles/raw_r4/tile_tail_r4aj.md).  Here the
+// last round's tiles run with their K split over the otherwise idle CUs (fp32
+// partials, gemm_xl_tail_epi sums them and runs the epilogue), the full rounds
+// as before; a grid smaller than half the chip is split the same way.
+// Measured no faster (l3 0.634 -> 0.639 ms, l4 0.576 -> 0.570, bench 125.2 vs
+// 125.7 ms; profiles/README.md finding 54): the tail's epilogue then runs on
+// only `rem` CUs and reads ksplit fp32 partials each.  Kept for A/B.
+int g_xl_tail = [] { const char* e = std::getenv("DMP_XL_TAIL"); return e ? std::atoi(e) : 0; }();
+
+int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0;
+    DMP_HIP_CHECK(hipGetDevice(&dev));
+    DMP_HIP_CHECK(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return g_num_cus;
+}
+
 template <int EPI>
 void launch_pp256(const XlArgs& a, int blocks, hipStream_t s) {
-  if (g_xl_pipe == 8)
+  if (g_xl_pipe == 8) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 8>), dim3(blocks), dim3(XTHREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    return;
+  }
+  const int cus = num_cus(), ktiles = a.K / XBK, rem = blocks % cus;
+  int ks = rem > 0 ? std::min(cus / rem, ktiles / 6) : 0;
+  if (g_xl_tail && ktiles >= 16 && rem > 0 && 2 * rem <= cus && ks >= 2) {
+    const int kper = ((ktiles + ks - 1) / ks + 1) & ~1;  // even: K tile kt stays in buffer kt & 1
+    ks = (ktiles + kper - 1) / kper;
+    int dev = 0;
+    DMP_HIP_CHECK(hipGetDevice(&dev));
+    auto ws = at::empty({(int64_t)rem * ks * 32 * XTHREADS * 4}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+    XlArgs m = a;
+    m.tbase = blocks - rem;
+    if (m.tbase > 0) hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(m.tbase), dim3(XTHREADS), 0, s, m);
+    XlArgs t = m;
+    t.ksplit = ks;
+    t.kper = kper;
+    t.skws = ws.data_ptr<float>();
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 9>), dim3(rem * ks), dim3(XTHREADS), 0, s, t);
+    hipLaunchKernelGGL((gemm_xl_tail_epi<EPI>), dim3(rem), dim3(XTHREADS), 0, s, t);
+    return;
+  }
+  hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
 }
 
 template <int BN, int EPI>
@@ -2307,6 +2429,8 @@ void set_gemm_xl_x2(int mode) {
 }
 int get_gemm_xl_x2() { return g_xl_x2; }
 void set_gemm_xl_nt(int on) { g_xl_nt = on ? 1 : 0; }
+void set_gemm_xl_tail(int on) { g_xl_tail = on ? 1 : 0; }
+int get_gemm_xl_tail() { return g_xl_tail; }
 int get_tn_xl_ring() { return g_tn_xl_ring; }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
