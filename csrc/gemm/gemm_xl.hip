@@ -55,7 +55,12 @@ enum XlEpi { XL_STORE = 0, XL_BIAS = 1, XL_BIAS_GELU = 2, XL_DGELU = 3, XL_BIAS_
              XL_MOMENTS = 5, XL_ADD = 6, XL_BNBWD = 7,
              // C = act(acc * s[n] + t[n] (+ R)): conv + training-mode BN (+ residual)
              // + ReLU when the BN statistics were formed before the GEMM (ops/bn_fold.py)
-             XL_AFFINE = 8 };
+             XL_AFFINE = 8,
+             // XL_BNBWD with its operand set fixed at compile time (the runtime
+             // flags cost the epilogue ~2x the VALU of the moments epilogue):
+             // mask from y with x moments / mask from y, no x
+             XL_BNBWD_Y = 9, XL_BNBWD_YO = 10 };
+__host__ __device__ constexpr bool is_bnbwd(int e) { return e == XL_BNBWD || e == XL_BNBWD_Y || e == XL_BNBWD_YO; }
 
 using gptr_t = const __attribute__((address_space(1))) void*;
 using lptr_t = __attribute__((address_space(3))) void*;
@@ -213,7 +218,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
   constexpr int WTM = 128, WTN = BN / 4;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int CT_STRIDE = BN + 8;
-  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD || EPI == XL_DGELU;
+  constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
   const int M = p.M, N = p.N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
@@ -237,7 +242,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
 #pragma unroll
           for (int e = 0; e < 4; ++e) b4[e] = (float)p.bias[col + e];  // a bias view may be 2-B aligned only
         }
-        if constexpr (EPI == XL_BNBWD)
+        if constexpr (is_bnbwd(EPI))
           if (p.ebias) b4 = *reinterpret_cast<const f32x4*>(p.ebias + col);
         if constexpr (EPI == XL_AFFINE) {
           if (p.esc) s4 = *reinterpret_cast<const f32x4*>(p.esc + col);
@@ -262,7 +267,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
     sv[j] = 1.f;
     if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES)
       bv[j] = col < N ? (float)p.bias[col] : 0.f;
-    if constexpr (EPI == XL_BNBWD)
+    if constexpr (is_bnbwd(EPI))
       bv[j] = (col < N && p.ebias) ? p.ebias[col] : 0.f;
     if constexpr (EPI == XL_AFFINE) {
       sv[j] = (col < N && p.esc) ? p.esc[col] : 1.f;
@@ -288,12 +293,12 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
   float msum[8], msq[8], bmu[8], bsc[8], bsh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = 0.f; }
-  if constexpr (EPI == XL_BNBWD) {
+  if constexpr (is_bnbwd(EPI)) {
     if (col < N) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         bmu[j] = p.bmean ? p.bmean[col + j] : 0.f;
-        if (!p.bny) {
+        if (EPI == XL_BNBWD) {
           bsc[j] = p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f);
           bsh[j] = (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j];
         }
@@ -309,11 +314,12 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
     // short-K conv epilogues at 1 block/CU (tools/epi_bench.py).
     // Batched for every epilogue with operand loads (XL_BNBWD 1.72 -> 1.24 ms
     // at l2 shapes); the load-free ones keep the row-at-a-time loop below.
-    constexpr bool kBatch = EPI == XL_BNBWD || EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BIAS_RES ||
+    constexpr bool kBatch = is_bnbwd(EPI) || EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BIAS_RES ||
                             EPI == XL_DGELU;
     constexpr int NP = kBatch ? XBM / RPP : 0, PB = 8;
     constexpr bool kL0 = kBatch;
-    constexpr bool kL12 = EPI == XL_BNBWD;
+    constexpr bool kL12 = is_bnbwd(EPI);
+    constexpr bool kLx = EPI == XL_BNBWD || EPI == XL_BNBWD_Y, kLy = EPI == XL_BNBWD_Y || EPI == XL_BNBWD_YO;
     // operand bases for branch-free loads: a missing operand reads a valid
     // dummy row (row 0 of C / of itself), its value is never used -- a
     // per-load branch would split every load into its own block, and the
@@ -348,7 +354,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
         const int row = min(row_u, M - 1);
         if constexpr (kL0) {
           const bf16x8* rp;
-          if constexpr (EPI == XL_BNBWD) {
+          if constexpr (is_bnbwd(EPI)) {
             int64_t rr = p.R ? compact_row(p.rmap, row) : -1;
             rok |= (rr >= 0 ? 1u : 0u) << i;
             rr = rr >= 0 ? rr : 0;
@@ -359,8 +365,8 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
           l0[i] = p.cnt ? __builtin_nontemporal_load(rp) : *rp;
         }
         if constexpr (kL12) {
-          l1[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? xrow + (pb + i) * xstep : xbase + col);
-          l2[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? yrow + (pb + i) * ystep : ybase + col);
+          if constexpr (kLx) l1[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? xrow + (pb + i) * xstep : xbase + col);
+          if constexpr (kLy) l2[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? yrow + (pb + i) * ystep : ybase + col);
         }
       }
 #pragma unroll
@@ -387,23 +393,31 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
             for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
           }
           v = __builtin_convertvector(f, bf16x8);
-        } else if constexpr (EPI == XL_BNBWD) {
+        } else if constexpr (is_bnbwd(EPI)) {
           f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
           if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
             if ((rok >> i) & 1u) g += __builtin_convertvector(l0[i], f32x8);
             v = __builtin_convertvector(g, bf16x8);
             g = __builtin_convertvector(v, f32x8);
           }
-          // bx null: BN input never materialised (ops/bn_fold.py) -- mask from y, sum dz only
-          const f32x8 xv = __builtin_convertvector(l1[i], f32x8);
-          const f32x8 yv = __builtin_convertvector(l2[i], f32x8);
+          // bx null: BN input never materialised (ops/bn_fold.py) -- mask from y, sum dz only.
+          // XL_BNBWD keeps the operand set a runtime choice (the x2 kernel's
+          // contract); _Y / _YO fix it: mask from y, with / without x moments
+          constexpr bool kY = EPI != XL_BNBWD, kX = EPI != XL_BNBWD_YO;
+          f32x8 xv = {}, yv = {};
+          if constexpr (kLx) xv = __builtin_convertvector(l1[i], f32x8);
+          if constexpr (kLy) yv = __builtin_convertvector(l2[i], f32x8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const bool on = p.bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);
+            // (xl_conv_run maps an operand set with y to _Y / _YO: plain
+            // XL_BNBWD here always has x and no y)
+            bool on;
+            if constexpr (kY) on = yv[j] > 0.f;
+            else on = fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
             const float dz = on ? g[j] : 0.f;
             g[j] = dz;
             msum[j] += dz;
-            if (p.bx) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+            if constexpr (kX) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
           }
           v = __builtin_convertvector(g, bf16x8);
         } else if constexpr (EPI == XL_BIAS_GELU) {
@@ -492,7 +506,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   static_assert(NA >= 1 && NB >= 1, "region smaller than one glds round");
   __shared__ __attribute__((aligned(16))) char smem[LDS];
   // XL_DGELU: column sums of the output (fc1's bias gradient) when p.part is set
-  constexpr bool kMom = EPI == XL_MOMENTS || EPI == XL_BNBWD || EPI == XL_DGELU;
+  constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
   if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
 
   const bf16* __restrict__ A = p.A;
@@ -1938,9 +1952,9 @@ void launch_x2(const XlArgs& a, hipStream_t s) {
 
 template <int EPI>
 void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
-  if constexpr (EPI == XL_MOMENTS || EPI == XL_AFFINE || EPI == XL_BNBWD || EPI == XL_ADD) {
+  if constexpr (EPI == XL_MOMENTS || EPI == XL_AFFINE || is_bnbwd(EPI) || EPI == XL_ADD) {
     if (use_x2(a)) {
-      launch_x2<EPI>(a, s);
+      launch_x2<is_bnbwd(EPI) ? (int)XL_BNBWD : EPI>(a, s);  // the x2 kernel keeps the runtime operand flags
       return;
     }
   }
@@ -2155,6 +2169,8 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   }
   if (epi == XL_BNBWD) {
     const bool has_x = bn_x.has_value() && bn_x->defined();
+    const bool has_y = bn_y.has_value() && bn_y->defined();
+    epi = !has_y ? XL_BNBWD : has_x ? XL_BNBWD_Y : XL_BNBWD_YO;
     TORCH_CHECK(has_x || (bn_y.has_value() && bn_y->defined()), "bnbwd needs bn_x and/or bn_y");
     if (has_x) {
       check_bf16_2d(*bn_x, "bn_x");
@@ -2177,7 +2193,7 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   const int bn = conv ? 256 : pick_bn((int)M, (int)N);
   at::Tensor sums, part;
   const int mtiles = (int)((M + XBM - 1) / XBM);
-  const bool moments = epi == XL_MOMENTS || epi == XL_BNBWD;
+  const bool moments = epi == XL_MOMENTS || is_bnbwd(epi);
   if (moments) {
     part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
     sums = at::empty({2 * N + 1}, A.options().dtype(at::kDouble));
@@ -2192,6 +2208,8 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
       case XL_MOMENTS: launch_pp256<XL_MOMENTS>(a, blocks, s); break;
       case XL_ADD: launch_pp256<XL_ADD>(a, blocks, s); break;
       case XL_BNBWD: launch_pp256<XL_BNBWD>(a, blocks, s); break;
+      case XL_BNBWD_Y: launch_pp256<XL_BNBWD_Y>(a, blocks, s); break;
+      case XL_BNBWD_YO: launch_pp256<XL_BNBWD_YO>(a, blocks, s); break;
       default: TORCH_CHECK(false, "conv_xl: mode ", mode, " has no implicit-GEMM variant");
     }
   } else {
@@ -2199,6 +2217,8 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
       case XL_MOMENTS: dispatch_bn<XL_MOMENTS>(a, bn, s); break;
       case XL_ADD: dispatch_bn<XL_ADD>(a, bn, s); break;
       case XL_AFFINE: dispatch_bn<XL_AFFINE>(a, bn, s); break;
+      case XL_BNBWD_Y: dispatch_bn<XL_BNBWD_Y>(a, bn, s); break;
+      case XL_BNBWD_YO: dispatch_bn<XL_BNBWD_YO>(a, bn, s); break;
       default: dispatch_bn<XL_BNBWD>(a, bn, s); break;
     }
   }
