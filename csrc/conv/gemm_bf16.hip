@@ -53,7 +53,12 @@ using bf16 = __bf16;
 constexpr int BK = 64;
 constexpr int kThreads = 256;
 
-enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2, EPI_BNBWD = 3 };
+enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2, EPI_BNBWD = 3,
+           // EPI_BNBWD with the mask taken from the BN output y, fixed at compile
+           // time (with / without the x moments); plain EPI_BNBWD = mask from x
+           // (gemm_xl.hip finding 55: the runtime operand flags cost the epilogue)
+           EPI_BNBWD_Y = 4, EPI_BNBWD_YO = 5 };
+__host__ __device__ constexpr bool nt_bnbwd(int e) { return e == EPI_BNBWD || e == EPI_BNBWD_Y || e == EPI_BNBWD_YO; }
 
 // Logical GEMM row -> physical activation row for strided 1x1 convs: logical
 // row (n, oh, ow) of an [N, Ho, Wo] output grid reads/writes physical row
@@ -148,7 +153,7 @@ void gemm_nt_kernel(const NtArgs p) {
   const RowMap& amap = p.amap;
   const RowMap& cmap = p.cmap;
   const ConvMap& cv = p.cv;
-  if constexpr (EPI == EPI_MOMENTS || EPI == EPI_BNBWD) zero_moments(p.zsums, 2 * N);
+  if constexpr (EPI == EPI_MOMENTS || nt_bnbwd(EPI)) zero_moments(p.zsums, 2 * N);
   constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int A_VECS = BM * BK / 8 / kThreads;  // 16-B vectors per thread per A tile
@@ -357,7 +362,7 @@ void gemm_nt_kernel(const NtArgs p) {
         if (epi_s) cs = *reinterpret_cast<const f32x4*>(epi_s + gc);
         if (epi_t) cb = *reinterpret_cast<const f32x4*>(epi_t + gc);
       }
-      if constexpr (EPI == EPI_BNBWD) {
+      if constexpr (nt_bnbwd(EPI)) {
         if (p.ebias) cb = *reinterpret_cast<const f32x4*>(p.ebias + gc);
       }
     }
@@ -375,7 +380,7 @@ void gemm_nt_kernel(const NtArgs p) {
   // ---- store pass: each thread moves 8 contiguous columns of a row ----
   constexpr int CV = BN / 8;                  // 16-B vectors per row
   constexpr int RPP = kThreads / CV;          // rows per pass
-  constexpr bool kMom = EPI == EPI_MOMENTS || EPI == EPI_BNBWD;
+  constexpr bool kMom = EPI == EPI_MOMENTS || nt_bnbwd(EPI);
   static_assert(!kMom || 2 * RPP * BN * 4 <= LDS_BYTES, "moments scratch exceeds LDS");
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
@@ -388,12 +393,12 @@ void gemm_nt_kernel(const NtArgs p) {
   const bf16* __restrict__ bny = p.bny;
   const int64_t ldbx = p.ldbx, ldby = p.ldby;
   const CompactMap rmap = p.rmap;
-  if constexpr (EPI == EPI_BNBWD) {
+  if constexpr (nt_bnbwd(EPI)) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bmu[j] = (col_ok && p.bmean) ? p.bmean[col + j] : 0.f;
-      bsc[j] = (col_ok && !p.bny) ? p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f) : 0.f;
-      bsh[j] = (col_ok && !p.bny) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
+      bsc[j] = (EPI == EPI_BNBWD && col_ok) ? p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f) : 0.f;
+      bsh[j] = (EPI == EPI_BNBWD && col_ok) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
     }
   }
   // Phase 1 issues every global operand load of the tile's row passes
@@ -401,7 +406,7 @@ void gemm_nt_kernel(const NtArgs p) {
   // sit behind possibly-aliasing stores would keep ~2 per lane in flight
   // (tools/epi_bench.py; same structure as gemm_xl.hip's conv epilogues).
   constexpr int NP = BM / RPP;
-  constexpr bool kLR = EPI == EPI_BNBWD || EPI == EPI_AFFINE;
+  constexpr bool kLR = nt_bnbwd(EPI) || EPI == EPI_AFFINE;
   // branch-free operand loads (dummy row 0 of C when an operand is absent; see gemm_xl.hip)
   const bf16* rbase = R ? R : C;
   const int64_t rld = R ? ldr : 0;
@@ -417,17 +422,17 @@ void gemm_nt_kernel(const NtArgs p) {
     const int row = min(m0 + rr0 + i * RPP, M - 1);
     if constexpr (kLR) {
       int64_t rr = row;
-      if constexpr (EPI == EPI_BNBWD) {
+      if constexpr (nt_bnbwd(EPI)) {
         rr = R ? compact_row(rmap, row) : -1;
         rok |= (rr >= 0 ? 1u : 0u) << i;
         rr = rr >= 0 ? rr : 0;
       }
       l0[i] = *reinterpret_cast<const bf16x8*>(rbase + rr * rld + colc);
     }
-    if constexpr (EPI == EPI_BNBWD) {
+    if constexpr (EPI == EPI_BNBWD || EPI == EPI_BNBWD_Y)
       l1[i] = *reinterpret_cast<const bf16x8*>(xbase + (int64_t)row * xld + colc);
+    if constexpr (EPI == EPI_BNBWD_Y || EPI == EPI_BNBWD_YO)
       l2[i] = *reinterpret_cast<const bf16x8*>(ybase + (int64_t)row * yld + colc);
-    }
   }
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
@@ -444,7 +449,7 @@ void gemm_nt_kernel(const NtArgs p) {
         }
         v = __builtin_convertvector(f, bf16x8);
       }
-      if constexpr (EPI == EPI_BNBWD) {
+      if constexpr (nt_bnbwd(EPI)) {
         f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
         if (R) {  // the other branch's gradient, summed in fp32 then rounded once (as "add")
           if ((rok >> i) & 1u) g += __builtin_convertvector(l0[i], f32x8);
@@ -453,15 +458,21 @@ void gemm_nt_kernel(const NtArgs p) {
         }
         // bnx null (the BN input was never materialised, ops/bn_fold.py): mask
         // from y, only sum dz is reduced (sum dz*(x-mean) is formed from dz^T a)
-        const f32x8 xv = __builtin_convertvector(l1[i], f32x8);
-        const f32x8 yv = __builtin_convertvector(l2[i], f32x8);
+        // the operand set is compile-time: EPI_BNBWD = mask from x (run_nt maps
+        // any set with y to _Y / _YO), _Y = mask from y with x moments, _YO = y only
+        constexpr bool kX = EPI != EPI_BNBWD_YO, kY = EPI != EPI_BNBWD;
+        f32x8 xv = {}, yv = {};
+        if constexpr (kX) xv = __builtin_convertvector(l1[i], f32x8);
+        if constexpr (kY) yv = __builtin_convertvector(l2[i], f32x8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const bool on = bny ? (yv[j] > 0.f) : (fmaf(xv[j], bsc[j], bsh[j]) > 0.f);
+          bool on;
+          if constexpr (kY) on = yv[j] > 0.f;
+          else on = fmaf(xv[j], bsc[j], bsh[j]) > 0.f;
           const float dz = on ? g[j] : 0.f;
           g[j] = dz;
           msum[j] += dz;
-          if (bnx) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
+          if constexpr (kX) msq[j] = fmaf(dz, xv[j] - bmu[j], msq[j]);
         }
         v = __builtin_convertvector(g, bf16x8);  // exact: dz is G or 0
       }
@@ -980,9 +991,11 @@ void dispatch_mode(const NtArgs& a, bool pro, int epi, int bm, hipStream_t s) {
   } else if (epi == EPI_MOMENTS) {
     if (pro) dispatch_tile<true, EPI_MOMENTS, CONV>(a, bm, s);
     else dispatch_tile<false, EPI_MOMENTS, CONV>(a, bm, s);
-  } else if (epi == EPI_BNBWD) {
+  } else if (nt_bnbwd(epi)) {
     TORCH_CHECK(!pro, "bnbwd epilogue has no prologue variant");
-    dispatch_tile<false, EPI_BNBWD, CONV>(a, bm, s);
+    if (epi == EPI_BNBWD_Y) dispatch_tile<false, EPI_BNBWD_Y, CONV>(a, bm, s);
+    else if (epi == EPI_BNBWD_YO) dispatch_tile<false, EPI_BNBWD_YO, CONV>(a, bm, s);
+    else dispatch_tile<false, EPI_BNBWD, CONV>(a, bm, s);
   } else {
     if (pro) dispatch_tile<true, EPI_AFFINE, CONV>(a, bm, s);
     else dispatch_tile<false, EPI_AFFINE, CONV>(a, bm, s);
@@ -1020,7 +1033,9 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   if (mode == "store") {
   } else if (mode == "moments" || mode == "bnbwd") {
     epi = mode == "moments" ? EPI_MOMENTS : EPI_BNBWD;
-    if (epi == EPI_BNBWD && residual.has_value() && residual->defined()) {
+    TORCH_CHECK(epi != EPI_BNBWD || a.bx || a.bny, "bnbwd needs bn_x or bn_y (gemm_nt_bnbwd)");
+    if (epi == EPI_BNBWD && a.bny) epi = a.bx ? EPI_BNBWD_Y : EPI_BNBWD_YO;
+    if (nt_bnbwd(epi) && residual.has_value() && residual->defined()) {
       check_operand(*residual, "residual");
       const int64_t rrows = a.rmap.s == 1 ? a.M
                                           : (int64_t)a.M / ((int64_t)a.rmap.hi * a.rmap.wi) * a.rmap.ho * a.rmap.wo;
@@ -1061,7 +1076,7 @@ std::vector<at::Tensor> run_nt(NtArgs a, bool conv, const at::Tensor& like,
   }
   if (conv) dispatch_mode<true>(a, pro, epi, bm, stream);
   else dispatch_mode<false>(a, pro, epi, bm, stream);
-  if (epi == EPI_MOMENTS || epi == EPI_BNBWD)
+  if (epi == EPI_MOMENTS || nt_bnbwd(epi))
     bn_reduce_partials_launch(a.part, (a.M + tbm - 1) / tbm, a.N, moments.data_ptr<double>(),
                               (double)a.M, stream);
   return {C, moments};

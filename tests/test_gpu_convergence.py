@@ -309,7 +309,9 @@ def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
     # real descent, and no lag in reaching 95 / 90 % of the start
     assert _mean(l_nat) <= 1.25 * _mean(l_ref), (_mean(l_nat), _mean(l_ref))
     assert a < 0.6 * l0, (l0, a)
+    # lag band: 1.5x + 10 steps (round 4: 46-56 vs 46-53 in four runs, once
+    # 74 vs 51 on a correct build -- the onset of the descent is chaotic too)
     for frac in (0.95, 0.9):
         sn, sr = _steps_to(l_nat, frac * l0), _steps_to(l_ref, frac * l0)
         if sr is not None:
-            assert sn is not None and sn <= 1.25 * sr + 8, (frac, sn, sr)
+            assert sn is not None and sn <= 1.5 * sr + 10, (frac, sn, sr)
