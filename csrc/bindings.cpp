@@ -1,3 +1,4 @@
+#include <cmath>
 // Python bindings of the native runtime (module distributed_model_parallel_amd._C).
 #include <torch/extension.h>
 
@@ -17,18 +18,18 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                                          const c10::optional<at::Tensor>& residual, bool relu,
                                          int64_t C,
                                          const c10::optional<at::Tensor>& num_batches_tracked,
-                                         bool out_moments);
+                                         bool out_moments, double clip);
 std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& running_mean,
                                       const at::Tensor& running_var,
                                       const c10::optional<at::Tensor>& weight,
                                       const c10::optional<at::Tensor>& bias, double eps,
                                       const c10::optional<at::Tensor>& residual, bool relu,
-                                      int64_t C);
+                                      int64_t C, double clip);
 at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                                const c10::optional<at::Tensor>& y, const at::Tensor& mean,
                                bool relu, int64_t C, const c10::optional<at::Tensor>& weight,
                                const c10::optional<at::Tensor>& bias,
-                               const c10::optional<at::Tensor>& invstd);
+                               const c10::optional<at::Tensor>& invstd, double clip);
 at::Tensor bn_finalize(const at::Tensor& sums, const c10::optional<at::Tensor>& weight,
                        const c10::optional<at::Tensor>& bias,
                        const c10::optional<at::Tensor>& running_mean,
@@ -40,7 +41,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                                           const c10::optional<at::Tensor>& weight,
                                           const at::Tensor& mean, const at::Tensor& invstd,
                                           bool training, bool relu, bool want_dres, int64_t C,
-                                          const c10::optional<at::Tensor>& bias);
+                                          const c10::optional<at::Tensor>& bias, double clip);
 // fused_sgd.hip
 void sgd_flat_step(const c10::optional<at::Tensor>& master, const at::Tensor& mom,
                    const at::Tensor& grad, const at::Tensor& param, double lr, double wd,
@@ -219,18 +220,21 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_forward_apply", &dmp::bn_forward_apply, py::arg("x"), py::arg("sums"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
         py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("C"),
-        py::arg("num_batches_tracked") = py::none(), py::arg("out_moments") = false);
-  m.def("bn_eval_apply", &dmp::bn_eval_apply);
+        py::arg("num_batches_tracked") = py::none(), py::arg("out_moments") = false,
+        py::arg("clip") = INFINITY);
+  m.def("bn_eval_apply", &dmp::bn_eval_apply, py::arg("x"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("weight"), py::arg("bias"), py::arg("eps"), py::arg("residual"),
+        py::arg("relu"), py::arg("C"), py::arg("clip") = INFINITY);
   m.def("bn_finalize", &dmp::bn_finalize, py::arg("sums"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("C"), py::arg("num_batches_tracked") = py::none());
   m.def("bn_backward_moments", &dmp::bn_backward_moments, py::arg("dy"), py::arg("x"), py::arg("y"),
         py::arg("mean"), py::arg("relu"), py::arg("C"), py::arg("weight") = py::none(),
-        py::arg("bias") = py::none(), py::arg("invstd") = py::none());
+        py::arg("bias") = py::none(), py::arg("invstd") = py::none(), py::arg("clip") = INFINITY);
   m.def("bn_backward_apply", &dmp::bn_backward_apply, py::arg("dy"), py::arg("x"), py::arg("y"),
         py::arg("sums"), py::arg("count"), py::arg("weight"), py::arg("mean"), py::arg("invstd"),
         py::arg("training"), py::arg("relu"), py::arg("want_dres"), py::arg("C"),
-        py::arg("bias") = py::none());
+        py::arg("bias") = py::none(), py::arg("clip") = INFINITY);
 
   // ---- MFMA GEMM (1x1 conv) with fused BN prologue/epilogues ----
   m.def("gemm_nt", &dmp::gemm_nt, py::arg("A"), py::arg("B"), py::arg("pro_scale") = py::none(),
@@ -341,7 +345,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_xl_nt", &dmp::set_gemm_xl_nt, py::arg("on"),
         "conv-epilogue GEMMs: non-temporal C stores / residual loads (A/B; env DMP_XL_NT)");
   m.def("set_gemm_xl_tail", &dmp::set_gemm_xl_tail, py::arg("on"),
-        "256x256 ping-pong GEMMs: split-K for the last partial round of tiles (default on; env DMP_XL_TAIL)");
+        "256x256 ping-pong GEMMs: split-K for the last partial round of tiles (default off, measured no faster: finding 54; env DMP_XL_TAIL=1)");
   m.def("get_gemm_xl_tail", &dmp::get_gemm_xl_tail);
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,

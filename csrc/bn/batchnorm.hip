@@ -231,7 +231,8 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(
 }
 
 // -------------------------------------------------------------------------
-// Forward apply: y = act(x*scale + shift [+ residual]).
+// Forward apply: y = act(x*scale + shift [+ residual]); act = ReLU clipped at
+// `clip` (+inf: ReLU; 6: ReLU6, the 224-px MobileNetV2's activation).
 // FROM_SUMS: training mode -- coefficients from the moments; row-slab-0 blocks
 // also save mean/invstd and update running stats.  Otherwise eval mode --
 // coefficients from running stats.
@@ -243,7 +244,7 @@ __device__ __forceinline__ void bn_apply_rows(
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
     int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, const Layout& L, int lr, int cvec,
-    float (&os)[Vec16<T>::N], float (&oq)[Vec16<T>::N]);
+    float (&os)[Vec16<T>::N], float (&oq)[Vec16<T>::N], float clip);
 
 // OSUM: also reduce per-block partials of the column sums (and sums of
 // squares) of the STORED output -- the colsum a BN-folded consumer needs
@@ -255,7 +256,8 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
     int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, int64_t* __restrict__ num_batches_tracked,
-    float* __restrict__ opart = nullptr, double* __restrict__ ozsums = nullptr) {
+    float* __restrict__ opart = nullptr, double* __restrict__ ozsums = nullptr,
+    float clip = __builtin_inff()) {
   // BatchNorm's step counter rides along (one lane), instead of its own launch
   if (num_batches_tracked != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
     *num_batches_tracked += 1;
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
     if (lr < L.rpi && cvec < L.cv)
       bn_apply_rows<T, RELU, RES, FROM_SUMS, NT, true>(x, res, sums, weight, bias, running_mean, running_var,
                                                        momentum, eps, M, C, rows_per_block, y, save_mean,
-                                                       save_invstd, L, lr, cvec, os, oq);
+                                                       save_invstd, L, lr, cvec, os, oq, clip);
     block_combine_store<VEC>(os, oq, L, C, opart);
     return;
   }
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(kThreads) void bn_apply_kernel(
   float os[VEC], oq[VEC];
   bn_apply_rows<T, RELU, RES, FROM_SUMS, NT, false>(x, res, sums, weight, bias, running_mean, running_var,
                                                     momentum, eps, M, C, rows_per_block, y, save_mean,
-                                                    save_invstd, L, lr, cvec, os, oq);
+                                                    save_invstd, L, lr, cvec, os, oq, clip);
 }
 
 template <typename T, bool RELU, bool RES, bool FROM_SUMS, bool NT, bool OSUM>
@@ -290,7 +292,7 @@ __device__ __forceinline__ void bn_apply_rows(
     float* __restrict__ running_mean, float* __restrict__ running_var, float momentum, float eps,
     int64_t M, int C, int64_t rows_per_block, T* __restrict__ y, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, const Layout& L, int lr, int cvec,
-    float (&os)[Vec16<T>::N], float (&oq)[Vec16<T>::N]) {
+    float (&os)[Vec16<T>::N], float (&oq)[Vec16<T>::N], float clip) {
   constexpr int VEC = Vec16<T>::N;
   float sc[VEC], sh[VEC];
 #pragma unroll
@@ -334,7 +336,7 @@ __device__ __forceinline__ void bn_apply_rows(
     for (int i = 0; i < VEC; ++i) {
       float t = fmaf(v[i], sc[i], sh[i]), t2 = fmaf(v2[i], sc[i], sh[i]);
       if (RES) { t += rv[i]; t2 += rv2[i]; }
-      if (RELU) { t = fmaxf(t, 0.f); t2 = fmaxf(t2, 0.f); }
+      if (RELU) { t = fminf(fmaxf(t, 0.f), clip); t2 = fminf(fmaxf(t2, 0.f), clip); }
       if constexpr (OSUM) {  // moments of the values as stored
         t = (float)(T)t;
         t2 = (float)(T)t2;
@@ -356,7 +358,7 @@ __device__ __forceinline__ void bn_apply_rows(
     for (int i = 0; i < VEC; ++i) {
       float t = fmaf(v[i], sc[i], sh[i]);
       if (RES) t += rv[i];
-      if (RELU) t = fmaxf(t, 0.f);
+      if (RELU) t = fminf(fmaxf(t, 0.f), clip);
       if constexpr (OSUM) {
         t = (float)(T)t;
         os[i] += t;
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
     const T* __restrict__ dy, const T* __restrict__ x, const T* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ weight,
     const float* __restrict__ bias, const float* __restrict__ invstd, int64_t M, int C,
-    int64_t rows_per_block, float* __restrict__ part, double* __restrict__ zsums) {
+    int64_t rows_per_block, float* __restrict__ part, double* __restrict__ zsums, float clip) {
   zero_moments(zsums, 2 * C);
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
@@ -412,10 +414,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_moments_kernel(
         float yv[VEC];
         Vec16<T>::load(y + o, yv);
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+        for (int i = 0; i < VEC; ++i) g[i] = (yv[i] > 0.f && yv[i] < clip) ? g[i] : 0.f;
       } else if (RELU == 2) {
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
+        for (int i = 0; i < VEC; ++i) {
+          const float t = fmaf(xv[i], msc[i], msh[i]);
+          g[i] = (t > 0.f && t < clip) ? g[i] : 0.f;
+        }
       }
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
@@ -438,7 +443,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ weight, const float* __restrict__ bias, const float* __restrict__ mean,
     const float* __restrict__ invstd, int training, int64_t M, int C, int64_t rows_per_block,
     T* __restrict__ dx, T* __restrict__ dres, float* __restrict__ dweight,
-    float* __restrict__ dbias) {
+    float* __restrict__ dbias, float clip) {
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -486,10 +491,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       float yv[VEC];
       ld16<NT>(y + o, yv);
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) g[i] = yv[i] > 0.f ? g[i] : 0.f;
+      for (int i = 0; i < VEC; ++i) g[i] = (yv[i] > 0.f && yv[i] < clip) ? g[i] : 0.f;
     } else if (RELU == 2) {
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) g[i] = fmaf(xv[i], msc[i], msh[i]) > 0.f ? g[i] : 0.f;
+      for (int i = 0; i < VEC; ++i) {
+        const float t = fmaf(xv[i], msc[i], msh[i]);
+        g[i] = (t > 0.f && t < clip) ? g[i] : 0.f;
+      }
     }
     if (DRES) st16<NT>(dres + o, g);
 #pragma unroll
@@ -589,7 +597,7 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                                          const c10::optional<at::Tensor>& residual, bool relu,
                                          int64_t C,
                                          const c10::optional<at::Tensor>& num_batches_tracked,
-                                         bool out_moments) {
+                                         bool out_moments, double clip) {
   check_input(x, C, "x");
   TORCH_CHECK(sums.scalar_type() == at::kDouble && sums.numel() == 2 * C + 1, "bad moments");
   int64_t* nbt = nullptr;
@@ -621,7 +629,7 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                      stream, ptr<T>(x), nullptr, sums.data_ptr<double>(), fptr(weight), fptr(bias), \
                      fptr(running_mean), fptr(running_var), (float)momentum, (float)eps, M, (int)C, \
                      g.rows_per_block, ptr<T>(y), saved.data_ptr<float>(), saved.data_ptr<float>() + C, \
-                     nbt, part.data_ptr<float>(), zt)
+                     nbt, part.data_ptr<float>(), zt, (float)clip)
     if (streaming(M, C)) DMP_BN_FWD_OS(true);
     else DMP_BN_FWD_OS(false);
 #undef DMP_BN_FWD_OS
@@ -637,7 +645,7 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
                      ptr<T>(x), r, sums.data_ptr<double>(), fptr(weight), fptr(bias),            \
                      fptr(running_mean), fptr(running_var), (float)momentum, (float)eps, M,      \
                      (int)C, g.rows_per_block, ptr<T>(y), saved.data_ptr<float>(),               \
-                     saved.data_ptr<float>() + C, nbt)
+                     saved.data_ptr<float>() + C, nbt, nullptr, nullptr, (float)clip)
 #define DMP_BN_FWD(RELU, RES) \
   do { if (streaming(M, C)) DMP_BN_FWD1(RELU, RES, true); else DMP_BN_FWD1(RELU, RES, false); } while (0)
       if (relu && has_res) DMP_BN_FWD(true, true);
@@ -682,7 +690,7 @@ std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& run
                                       const c10::optional<at::Tensor>& weight,
                                       const c10::optional<at::Tensor>& bias, double eps,
                                       const c10::optional<at::Tensor>& residual, bool relu,
-                                      int64_t C) {
+                                      int64_t C, double clip) {
   check_input(x, C, "x");
   const int64_t M = x.numel() / C;
   auto y = at::empty_like(x);
@@ -701,7 +709,8 @@ std::vector<at::Tensor> bn_eval_apply(const at::Tensor& x, const at::Tensor& run
   hipLaunchKernelGGL((bn_apply_kernel<T, RELU, RES, false>), g.grid, dim3(kThreads), 0, stream,  \
                      ptr<T>(x), r, nullptr, fptr(weight), fptr(bias), rm.data_ptr<float>(),      \
                      rv.data_ptr<float>(), 0.f, (float)eps, M, (int)C, g.rows_per_block,         \
-                     ptr<T>(y), saved.data_ptr<float>(), saved.data_ptr<float>() + C, nullptr)
+                     ptr<T>(y), saved.data_ptr<float>(), saved.data_ptr<float>() + C, nullptr,   \
+                     nullptr, nullptr, (float)clip)
       if (relu && has_res) DMP_BN_EVAL(true, true);
       else if (relu) DMP_BN_EVAL(true, false);
       else if (has_res) DMP_BN_EVAL(false, true);
@@ -719,7 +728,7 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
                                const c10::optional<at::Tensor>& y, const at::Tensor& mean,
                                bool relu, int64_t C, const c10::optional<at::Tensor>& weight,
                                const c10::optional<at::Tensor>& bias,
-                               const c10::optional<at::Tensor>& invstd) {
+                               const c10::optional<at::Tensor>& invstd, double clip) {
   check_input(dy, C, "grad");
   check_input(x, C, "x");
   const int64_t M = x.numel() / C;
@@ -740,7 +749,7 @@ at::Tensor bn_backward_moments(const at::Tensor& dy, const at::Tensor& x,
 #define DMP_BN_BM(MODE)                                                                          \
   hipLaunchKernelGGL((bn_bwd_moments_kernel<T, MODE>), g.grid, dim3(kThreads), 0, stream,        \
                      ptr<T>(dy), ptr<T>(x), yp, mean.data_ptr<float>(), fptr(weight), fptr(bias), \
-                     ip, M, (int)C, g.rows_per_block, pp, zt)
+                     ip, M, (int)C, g.rows_per_block, pp, zt, (float)clip)
     if (!relu) DMP_BN_BM(0);
     else if (from_y) DMP_BN_BM(1);
     else DMP_BN_BM(2);
@@ -757,7 +766,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                                           const c10::optional<at::Tensor>& weight,
                                           const at::Tensor& mean, const at::Tensor& invstd,
                                           bool training, bool relu, bool want_dres, int64_t C,
-                                          const c10::optional<at::Tensor>& bias) {
+                                          const c10::optional<at::Tensor>& bias, double clip) {
   TORCH_CHECK(count.scalar_type() == at::kDouble && count.numel() >= 1, "count must be fp64");
   check_input(dy, C, "grad");
   const int64_t M = x.numel() / C;
@@ -780,7 +789,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                      ptr<T>(dy), ptr<T>(x), yp, sums.data_ptr<double>(), count.data_ptr<double>(), \
                      fptr(weight), fptr(bias), mean.data_ptr<float>(), invstd.data_ptr<float>(),  \
                      (int)training, M, (int)C, g.rows_per_block, ptr<T>(dx), dr,                  \
-                     dwb.data_ptr<float>(), dwb.data_ptr<float>() + C)
+                     dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, (float)clip)
       const int mode = !relu ? 0 : (from_y ? 1 : 2);
       if (mode == 1 && want_dres) DMP_BN_BWD(1, true);
       else if (mode == 1) DMP_BN_BWD(1, false);

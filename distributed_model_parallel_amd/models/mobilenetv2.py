@@ -55,10 +55,15 @@ IMAGENET_SETTINGS: Tuple[Tuple[int, int, int, int], ...] = (
 )
 
 
-def _norm(ch: int, use_bn: bool, act: bool) -> nn.Module:
+def _norm(ch: int, use_bn: bool, act: bool, activation: str = "relu") -> nn.Module:
+    """BN(+activation) fused in one kernel, or the bare activation without BN.
+    ``activation``: "relu" (the reference's CIFAR model) or "relu6" (the
+    torchvision-style 224-px model)."""
     if use_bn:
-        return BatchNormAct2d(ch, act="relu" if act else None)
-    return nn.ReLU(inplace=False) if act else nn.Identity()
+        return BatchNormAct2d(ch, act=activation if act else None)
+    if not act:
+        return nn.Identity()
+    return nn.ReLU6(inplace=False) if activation == "relu6" else nn.ReLU(inplace=False)
 
 
 class InvertedResidual(nn.Module):
@@ -70,7 +75,8 @@ class InvertedResidual(nn.Module):
     """
 
     def __init__(self, cin: int, cout: int, expansion: int, stride: int,
-                 use_bn: bool = True, shortcut_bn: bool | None = None, imagenet: bool = False):
+                 use_bn: bool = True, shortcut_bn: bool | None = None, imagenet: bool = False,
+                 activation: str = "relu"):
         super().__init__()
         hidden = cin * expansion
         self.stride = stride
@@ -79,9 +85,9 @@ class InvertedResidual(nn.Module):
         # ImageNet form (torchvision): no expand conv at expansion 1, identity
         # residual only (no projection shortcut).
         self.conv1 = Conv1x1(cin, hidden) if not (imagenet and expansion == 1) else None
-        self.bn1 = _norm(hidden, use_bn, act=True) if self.conv1 is not None else None
+        self.bn1 = _norm(hidden, use_bn, True, activation) if self.conv1 is not None else None
         self.conv2 = DepthwiseConv2d(hidden, stride=stride)
-        self.bn2 = _norm(hidden, use_bn, act=True)
+        self.bn2 = _norm(hidden, use_bn, True, activation)
         self.conv3 = Conv1x1(hidden, cout)
         self.bn3 = _norm(cout, use_bn, act=False)
         self.has_residual = stride == 1 and (cin == cout or not imagenet)
@@ -131,7 +137,8 @@ class MobileNetV2(nn.Module):
 
     def __init__(self, num_classes: int = 10, use_bn: bool = True,
                  settings: Sequence[Tuple[int, int, int, int]] = CIFAR_SETTINGS,
-                 nobn_shortcut_bn: bool = False, imagenet: bool = False, dropout: float = 0.0):
+                 nobn_shortcut_bn: bool = False, imagenet: bool = False, dropout: float = 0.0,
+                 activation: str = "relu"):
         super().__init__()
         self.use_bn = use_bn
         if imagenet:
@@ -140,18 +147,19 @@ class MobileNetV2(nn.Module):
         else:
             # 3x3 stem on the MFMA implicit GEMM (3 channels padded to 16, row taps)
             self.conv1 = RowTapConv2d(3, 32, 3)
-        self.bn1 = _norm(32, use_bn, act=True)
+        self.bn1 = _norm(32, use_bn, True, activation)
         blocks: List[nn.Module] = []
         cin = 32
         sc_bn = None if use_bn else nobn_shortcut_bn
         for t, c, n, s in settings:
             for i in range(n):
                 blocks.append(InvertedResidual(cin, c, t, s if i == 0 else 1,
-                                               use_bn=use_bn, shortcut_bn=sc_bn, imagenet=imagenet))
+                                               use_bn=use_bn, shortcut_bn=sc_bn, imagenet=imagenet,
+                                               activation=activation))
                 cin = c
         self.layers = nn.Sequential(*blocks)
         self.conv2 = Conv1x1(cin, 1280)
-        self.bn2 = _norm(1280, use_bn, act=True)
+        self.bn2 = _norm(1280, use_bn, True, activation)
         # CIFAR: the reference's 4x4 pool of the 4x4 map; ImageNet: global pool of 7x7
         self.pool = HeadPool(apply_relu=False, pool=None if imagenet else 4)
         self.dropout = dropout
@@ -195,9 +203,11 @@ def mobilenet_v2_224(num_classes: int = 1000, **kw) -> MobileNetV2:
     """MobileNetV2 at 224 px, ImageNet strides (torchvision's architecture:
     3,504,872 parameters at 1000 classes, 2,236,682 at 10), the model of the
     reference's batch-size finetune study (Readme.md:185-196).  Activations
-    are ReLU, not ReLU6 (the fused BN kernels implement ReLU); with no
-    pretrained weights offline the study's accuracy parity is unpinned."""
+    are ReLU6 as in torchvision (clipped inside the fused BN kernels,
+    ``BatchNormAct2d(act="relu6")``); with no pretrained weights offline the
+    study's accuracy parity is unpinned."""
     kw.setdefault("dropout", 0.2)
+    kw.setdefault("activation", "relu6")
     return MobileNetV2(num_classes=num_classes, settings=IMAGENET_SETTINGS, imagenet=True, **kw)
 
 

@@ -31,6 +31,9 @@ MomentReducer = Callable[[torch.Tensor], torch.Tensor]
 GradReducer = Callable[[torch.Tensor], torch.Tensor]
 
 _STATS = {"native_fwd": 0, "torch_fwd": 0}
+_INF = float("inf")
+# activation -> upper clip of the (clipped) ReLU the BN kernels apply
+ACTS = {None: None, "relu": _INF, "relu6": 6.0}
 
 # BN backward reductions fused into the consuming 1x1 conv's data-gradient
 # epilogue (BnBwdSlot); DMP_DISABLE=fuse_bn_bwd turns it off for A/B runs.
@@ -82,7 +85,7 @@ def local_moments(x2: torch.Tensor, native: bool) -> torch.Tensor:
 
 
 def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, native, nbt=None,
-                  out_moments=False):
+                  out_moments=False, clip=_INF):
     """Training-mode normalise from (global) moments; updates running stats and
     increments `nbt` (num_batches_tracked) -- inside the kernel when native.
 
@@ -91,28 +94,28 @@ def forward_apply(x2, sums, weight, bias, rm, rv, momentum, eps, res2, relu, nat
     if native:
         return _native.require("bn").bn_forward_apply(x2, sums, weight, bias, rm, rv,
                                                        float(momentum), float(eps), res2, relu, c,
-                                                       nbt, out_moments)
+                                                       nbt, out_moments, clip)
     if nbt is not None:
         nbt.add_(1)
     mean, invstd, scale, shift = _finalize_torch(sums, weight, bias, rm, rv, momentum, eps)
-    y = _apply_torch(x2, scale, shift, res2, relu)
+    y = _apply_torch(x2, scale, shift, res2, relu, clip)
     if out_moments:
         yd = y.double()
         return [y, mean, invstd, torch.cat([yd.sum(0), (yd * yd).sum(0), yd.new_tensor([float(y.shape[0])])])]
     return [y, mean, invstd]
 
 
-def eval_apply(x2, rm, rv, weight, bias, eps, res2, relu, native):
+def eval_apply(x2, rm, rv, weight, bias, eps, res2, relu, native, clip=_INF):
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_eval_apply(x2, rm, rv, weight, bias, float(eps), res2,
-                                                    relu, c)
+                                                    relu, c, clip)
     invstd = torch.rsqrt(rv.float() + eps)
     w = weight.float() if weight is not None else torch.ones_like(invstd)
     b = bias.float() if bias is not None else torch.zeros_like(invstd)
     scale = w * invstd
     shift = b - rm.float() * scale
-    return [_apply_torch(x2, scale, shift, res2, relu), rm.float(), invstd]
+    return [_apply_torch(x2, scale, shift, res2, relu, clip), rm.float(), invstd]
 
 
 def _finalize_torch(sums, weight, bias, rm, rv, momentum, eps):
@@ -132,51 +135,54 @@ def _finalize_torch(sums, weight, bias, rm, rv, momentum, eps):
     return [mean.float(), invstd, scale, shift]
 
 
-def _apply_torch(x2, scale, shift, res2, relu):
+def _apply_torch(x2, scale, shift, res2, relu, clip=_INF):
     y = x2.float() * scale + shift
     if res2 is not None:
         y = y + res2.float()
     if relu:
-        y = y.clamp_min(0)
+        y = y.clamp(0, clip)
     return y.to(x2.dtype)
 
 
-def _relu_mask(x2, y2, mean, invstd, weight, bias):
-    """ReLU mask of the forward output: y > 0, or -- when y was not saved (no
-    residual fused) -- re-derived from x with the forward's per-channel affine."""
+def _relu_mask(x2, y2, mean, invstd, weight, bias, clip=_INF):
+    """(Clipped) ReLU mask of the forward output: 0 < y < clip, or -- when y was
+    not saved (no residual fused) -- re-derived from x with the forward's
+    per-channel affine."""
     if y2 is not None:
-        return y2 > 0
+        return (y2 > 0) & (y2 < clip)
     sc = invstd * (weight if weight is not None else 1.0)
     sh = (bias if bias is not None else 0.0) - mean * sc
-    return torch.addcmul(sh, x2.float(), sc) > 0
+    t = torch.addcmul(sh, x2.float(), sc)
+    return (t > 0) & (t < clip)
 
 
-def backward_moments(dy2, x2, y2, mean, relu, native, weight=None, bias=None, invstd=None):
+def backward_moments(dy2, x2, y2, mean, relu, native, weight=None, bias=None, invstd=None, clip=_INF):
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_backward_moments(dy2, x2, y2, mean, relu, c, weight, bias,
-                                                          invstd)
+                                                          invstd, clip)
     dz = dy2.double()
     if relu:
-        dz = dz * _relu_mask(x2, y2, mean, invstd, weight, bias)
+        dz = dz * _relu_mask(x2, y2, mean, invstd, weight, bias, clip)
     return torch.cat([dz.sum(0), (dz * (x2.double() - mean.double())).sum(0)])
 
 
 def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, relu, want_dres, native,
-                   bias=None):
+                   bias=None, clip=_INF):
     """`count` is a 1-element fp64 tensor (global rows).  y2 None with relu:
     mask from x (see _relu_mask)."""
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_backward_apply(dy2, x2, y2, sums, count, weight, mean,
-                                                        invstd, training, relu, want_dres, c, bias)
+                                                        invstd, training, relu, want_dres, c, bias,
+                                                        clip)
     count = count.reshape(()).to(torch.float64)
     sdz, sdzx = sums[:c], sums[c:]
     w = weight.double() if weight is not None else torch.ones_like(sdz)
     istd = invstd.double()
     dz = dy2.double()
     if relu:
-        dz = dz * _relu_mask(x2, y2, mean, invstd, weight, bias)
+        dz = dz * _relu_mask(x2, y2, mean, invstd, weight, bias, clip)
     a = w * istd
     if training:
         b = -a * istd * istd * sdzx / count
@@ -241,8 +247,10 @@ _STATS["fused_bwd_moments"] = 0
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
-                relu, reduce_moments, reduce_grads, pre_sums=None, nbt=None, bwd_slot=None,
+                act_clip, reduce_moments, reduce_grads, pre_sums=None, nbt=None, bwd_slot=None,
                 out_moments=False):
+        relu = act_clip is not None
+        clip = act_clip if relu else _INF
         x2, back = _as_rows(x)
         native = _native_ok(x2)
         _STATS["native_fwd" if native else "torch_fwd"] += 1
@@ -262,7 +270,7 @@ class _BatchNormActFn(torch.autograd.Function):
             upd_rm = running_mean if (running_mean is not None and running_mean.dtype == torch.float32) else None
             upd_rv = running_var if upd_rm is not None else None
             res = forward_apply(x2, sums, w32, b32, upd_rm, upd_rv, momentum, eps, res2, relu, native, nbt,
-                                out_moments)
+                                out_moments, clip)
             y2, mean, invstd = res[0], res[1], res[2]
             osums = res[3] if out_moments else None
             if running_mean is not None and upd_rm is None:  # low-precision buffers
@@ -274,7 +282,7 @@ class _BatchNormActFn(torch.autograd.Function):
         else:
             count = torch.full((1,), float(x2.shape[0]), dtype=torch.float64, device=x2.device)
             y2, mean, invstd = eval_apply(x2, running_mean, running_var, w32, b32, eps, res2, relu,
-                                          native)
+                                          native, clip)
             osums = None
         # the ReLU mask needs the output only when a residual was added before the
         # ReLU; otherwise backward re-derives it from x (one tensor read fewer)
@@ -282,9 +290,10 @@ class _BatchNormActFn(torch.autograd.Function):
                               invstd, count)
         ctx.meta = (native, training, relu, residual is not None, back,
                     weight is not None, bias is not None, reduce_grads,
-                    weight.dtype if weight is not None else None, x.dim())
+                    weight.dtype if weight is not None else None, x.dim(), clip)
         ctx.bwd_slot = None
-        if bwd_slot is not None and native and training and relu and x.dim() == 4:
+        # the consumer-epilogue fusion applies a plain ReLU mask: not for ReLU6
+        if bwd_slot is not None and native and training and relu and clip == _INF and x.dim() == 4:
             bwd_slot.x2 = x2
             bwd_slot.y2 = y2 if residual is not None else None
             bwd_slot.mean, bwd_slot.invstd, bwd_slot.w32, bwd_slot.b32 = mean, invstd, w32, b32
@@ -301,7 +310,7 @@ class _BatchNormActFn(torch.autograd.Function):
     def backward(ctx, dy, _dosums=None):
         x2, y2, w32, b32, mean, invstd, count = ctx.saved_tensors
         (native, training, relu, has_res, back, has_w, has_b, reduce_grads, wdtype,
-         ndim) = ctx.meta
+         ndim, clip) = ctx.meta
         dy2, _ = _as_rows(dy.to(x2.dtype))
         slot = ctx.bwd_slot
         fused = slot.take(dy) if slot is not None else None
@@ -312,14 +321,14 @@ class _BatchNormActFn(torch.autograd.Function):
             sums = fused
             relu_eff, y_eff, want_dres = False, None, False
         else:
-            sums = backward_moments(dy2, x2, y2, mean, relu, native, w32, b32, invstd)
+            sums = backward_moments(dy2, x2, y2, mean, relu, native, w32, b32, invstd, clip)
             relu_eff, y_eff, want_dres = relu, y2, has_res
         local_sums = sums
         if training and reduce_grads is not None:
             local_sums = sums.clone()  # the reducer works in place
             sums = reduce_grads(sums)
         dx2, dw, db, dres2 = backward_apply(dy2, x2, y_eff, sums, count, w32, mean, invstd, training,
-                                            relu_eff, want_dres, native, b32)
+                                            relu_eff, want_dres, native, b32, clip)
         if fused is not None and has_res:
             dres2 = dy2  # d(residual) = dz, which is exactly the masked incoming gradient
         if reduce_grads is not None and training:
@@ -342,17 +351,24 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
                    reduce_grads: Optional[GradReducer] = None,
                    sums: Optional[torch.Tensor] = None,
                    num_batches_tracked: Optional[torch.Tensor] = None,
-                   out_moments: bool = False):
+                   out_moments: bool = False, act: Optional[str] = "_from_relu"):
     """Functional fused BN(+residual)(+ReLU).  `sums`: precomputed local moments
     [2C+1] of `x` (from a fused conv epilogue); ignored in eval mode.
     `num_batches_tracked`: incremented once (training mode), in-kernel when native.
     `out_moments`: also return the fp64 [2C+1] (colsum, colsum of squares, rows)
-    of the OUTPUT, reduced inside the apply pass (ops/bn_fold.py needs colsum)."""
+    of the OUTPUT, reduced inside the apply pass (ops/bn_fold.py needs colsum).
+    `act`: None / "relu" / "relu6" (overrides `relu` when given)."""
+    if act == "_from_relu":
+        act = "relu" if relu else None
+    if act not in ACTS:
+        raise ValueError(f"unsupported activation {act!r}")
+    clip = ACTS[act]
     slot = None
-    if training and relu and x.dim() == 4 and torch.is_grad_enabled() and _FUSE_BWD and _native.gpu_path(x):
+    if training and act == "relu" and x.dim() == 4 and torch.is_grad_enabled() and _FUSE_BWD \
+            and _native.gpu_path(x):
         slot = BnBwdSlot()
     out = _BatchNormActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
-                                momentum, eps, relu, reduce_moments, reduce_grads, sums,
+                                momentum, eps, clip, reduce_moments, reduce_grads, sums,
                                 num_batches_tracked if training else None, slot, out_moments)
     osums = None
     if out_moments:
@@ -365,14 +381,15 @@ def batch_norm_act(x: torch.Tensor, running_mean: Optional[torch.Tensor],
 class BatchNormAct2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` with optional fused residual add and ReLU.
 
-    ``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.
+    ``forward(x, residual=None)`` computes ``act(bn(x) + residual)``; ``act`` is
+    None, "relu" or "relu6" (ReLU clipped at 6, in the same kernels).
     """
 
     def __init__(self, num_features: int, eps: float = 1e-5, momentum: Optional[float] = 0.1,
                  affine: bool = True, track_running_stats: bool = True, act: Optional[str] = None,
                  device=None, dtype=None):
         super().__init__(num_features, eps, momentum, affine, track_running_stats, device, dtype)
-        if act not in (None, "relu"):
+        if act not in ACTS:
             raise ValueError(f"unsupported activation {act!r}")
         self.act = act
 
@@ -408,7 +425,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rmom, rgrad = self._moment_reducers() if use_batch else (None, None)
         return batch_norm_act(x, rm if self.track_running_stats else None,
                               rv if self.track_running_stats else None, self.weight, self.bias,
-                              use_batch, momentum, self.eps, relu=self.act == "relu",
+                              use_batch, momentum, self.eps, act=self.act,
                               residual=residual, reduce_moments=rmom, reduce_grads=rgrad,
                               sums=sums if use_batch else None,
                               num_batches_tracked=nbt if use_batch else None,
@@ -418,9 +435,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return super().extra_repr() + (f", act={self.act}" if self.act else "")
 
 
-def reference_bn_act(x, rm, rv, w, b, training, momentum, eps, relu=False, residual=None):
+def reference_bn_act(x, rm, rv, w, b, training, momentum, eps, relu=False, residual=None, act=None):
     """Plain PyTorch composition used as the numerics oracle in tests."""
     y = F.batch_norm(x, rm, rv, w, b, training, momentum, eps)
     if residual is not None:
         y = y + residual
-    return F.relu(y) if relu else y
+    if act == "relu6":
+        return F.relu6(y)
+    return F.relu(y) if (relu or act == "relu") else y

@@ -266,7 +266,9 @@ def replicate(network: nn.Module, devices: Sequence, detach: bool = False,
     ``cache``: a dict owned by the caller (DataParallel keeps one per
     instance) in which the replica module objects persist between calls; the
     returned list's ``release()`` must then be called once the replicas have
-    run.  Without a cache every call builds fresh module objects."""
+    run.  Without a cache every call builds fresh module objects, and so does
+    a network that recomputes forwards in backward (``recomputes_in_backward``:
+    its replicas must outlive ``release()``)."""
     devices = [comm_ops._dev(d) for d in devices]
     params = list(network.parameters())
     pidx = {id(p): i for i, p in enumerate(params)}
@@ -285,7 +287,7 @@ def replicate(network: nn.Module, devices: Sequence, detach: bool = False,
         [[] for _ in devices]
 
     sk = None
-    if cache is not None:
+    if cache is not None and not recomputes_in_backward(network):
         key = tuple(str(d) for d in devices)
         sk = cache.get(key)
         if sk is not None and sk.signature(network) != sk.sig:
@@ -305,6 +307,23 @@ def replicate(network: nn.Module, devices: Sequence, detach: bool = False,
     if owned:
         out.skeleton = sk
     return out
+
+
+def recomputes_in_backward(network: nn.Module) -> bool:
+    """Does ``network`` re-run module forwards during backward (activation
+    checkpointing: ``utils.checkpointing.CheckpointedSequential``, or a module
+    that declares ``_dmp_recomputes = True`` because it calls
+    ``torch.utils.checkpoint`` itself)?
+
+    The recompute closures hold the REPLICA module objects, so their parameter
+    and buffer slots must stay bound until backward has run.  Such networks
+    get a fresh, uncached skeleton per forward whose slots are never cleared
+    (it is freed with the autograd graph that references it); a cached one
+    would be cleared by ``release()`` after ``parallel_apply`` -- the recompute
+    would read ``weight=None`` -- or rebound by the next forward."""
+    from ..utils.checkpointing import CheckpointedSequential
+    return any(isinstance(m, CheckpointedSequential) or getattr(m, "_dmp_recomputes", False)
+               for m in network.modules())
 
 
 class ReplicaError(RuntimeError):
@@ -501,15 +520,29 @@ class DataParallel(nn.Module):
 
     # ---- graphed replicas ------------------------------------------------------
     def _graph_ok(self, inputs, kwargs) -> bool:
+        # an input that needs a gradient takes the eager path: the captured
+        # replicas return parameter gradients only
         return (self.graphs and self.training and torch.is_grad_enabled() and not kwargs
                 and len(inputs) == 1 and isinstance(inputs[0], torch.Tensor) and inputs[0].is_cuda
+                and not inputs[0].requires_grad
                 and self.dim == 0 and inputs[0].shape[0] % len(self.device_ids) == 0)
+
+    def _graph_signature(self, chunks) -> tuple:
+        """What a captured GraphedReplicas depends on: the module structure, the
+        chunk shapes, and the IDENTITY and storage of every parameter and
+        buffer (``module.to()``, ``load_state_dict(assign=True)`` or
+        ``m.weight = nn.Parameter(...)`` rebind tensors without changing the
+        structure; the captured graphs would keep reading / updating the old
+        ones -- ADVICE r4)."""
+        tens = tuple((id(t), t.data_ptr()) for t in
+                     list(self.module.parameters()) + list(self.module.buffers()))
+        return (_Skeleton.signature(self.module), tuple(tuple(c.shape) for c in chunks), tens)
 
     def _graphed_forward(self, x: torch.Tensor) -> torch.Tensor:
         from .dp_graphs import GraphedReplicas, graphed_forward
         with phase("dp.scatter"):
             chunks = comm_ops.scatter_tensor(x.detach(), self.device_ids, 0)
-        sig = (_Skeleton.signature(self.module), tuple(tuple(c.shape) for c in chunks))
+        sig = self._graph_signature(chunks)
         if self._graphed is None or self._graphed_sig != sig or not self._graphed.matches(chunks):
             self._graphed = None
             torch.cuda.synchronize()

@@ -246,7 +246,8 @@ class Pipeline:
                  loss_fn: Optional[Callable] = None, loss_on: str = "last",
                  partition=None, balance: str = "flops",
                  device: Optional[torch.device] = None, dtype: torch.dtype = torch.float32,
-                 channels_last: bool = False, static_batch: Optional[int] = None):
+                 channels_last: bool = False, static_batch: Optional[int] = None,
+                 fail_fast: bool = True):
         if schedule not in ("naive", "gpipe", "1f1b"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if loss_on not in ("last", "first"):
@@ -282,6 +283,22 @@ class Pipeline:
             cast_model(self.module, dtype)
         if channels_last:
             self.module = self.module.to(memory_format=torch.channels_last)
+        # an exception on one stage (e.g. rank 0 refusing a batch that breaks the
+        # static contract) would leave the other stages blocked in a receive
+        # forever: publish it so every rank exits non-zero (utils/debug.py)
+        self._failure = None
+        if fail_fast and self.world > 1:
+            from ..utils.debug import FailureBroadcast
+            self._failure = FailureBroadcast(self.rank, self.world)
+
+    def _guard(self):
+        import contextlib
+        return self._failure.guard() if self._failure is not None else contextlib.nullcontext()
+
+    def close(self) -> None:
+        """Stop the failure watcher (a finished pipeline)."""
+        if self._failure is not None:
+            self._failure.stop()
 
     # ---- static shape contract ------------------------------------------------
     def _probe_tails(self, atoms: nn.Sequential) -> List[Tuple[int, ...]]:
@@ -364,6 +381,10 @@ class Pipeline:
         """Forward + backward of one batch (inputs/targets needed on rank 0 only).
         Gradients accumulate in ``self.module``; step your stage optimizer after.
         ``batch_size`` (same on every rank) skips the batch-size message."""
+        with self._guard():
+            return self._train_step(inputs, targets, batch_size)
+
+    def _train_step(self, inputs, targets, batch_size) -> StepResult:
         self.module.train()
         batch = self._batch_size(inputs, batch_size)
         sizes = self._mb_sizes(batch)
@@ -535,6 +556,10 @@ class Pipeline:
     def eval_step(self, inputs: Optional[torch.Tensor] = None,
                   targets: Optional[torch.Tensor] = None, batch_size: Optional[int] = None) -> StepResult:
         """Forward-only pass over the pipeline (reference val_* loops)."""
+        with self._guard():
+            return self._eval_step(inputs, targets, batch_size)
+
+    def _eval_step(self, inputs, targets, batch_size) -> StepResult:
         self.module.eval()
         batch = self._batch_size(inputs, batch_size)
         sizes = self._mb_sizes(batch)

@@ -10,6 +10,7 @@ Reference defect 11 (T_max=90 while training 100 epochs) is avoided by
 from __future__ import annotations
 
 import math
+import warnings
 from typing import List, Optional
 
 import torch
@@ -102,10 +103,20 @@ class WarmupCosine:
     def get_last_lr(self) -> List[float]:
         return [g["lr"] for g in self.optimizer.param_groups]
 
+    kind = "cosine"
+
     def state_dict(self):
-        return {"epoch": self.epoch, "base": self.base, "epochs": self.epochs, "warmup": self.warmup}
+        return {"kind": self.kind, "epoch": self.epoch, "base": self.base, "epochs": self.epochs,
+                "warmup": self.warmup}
+
+    def _check_kind(self, sd) -> None:
+        saved = sd.get("kind", "multistep" if "milestones" in sd else "cosine")
+        if saved != self.kind:
+            warnings.warn(f"resuming a {saved!r} lr schedule checkpoint with a {self.kind!r} schedule: "
+                          f"the current command line's schedule type is kept", stacklevel=3)
 
     def load_state_dict(self, sd):
+        self._check_kind(sd)
         self.epoch, self.base, self.epochs, self.warmup = sd["epoch"], sd["base"], sd["epochs"], sd["warmup"]
         self._apply()
 
@@ -129,13 +140,22 @@ class WarmupMultiStep(WarmupCosine):
         for g, b in zip(self.optimizer.param_groups, self.base):
             g["lr"] = b * self.gamma ** k * w
 
+    kind = "multistep"
+
     def state_dict(self):
         sd = super().state_dict()
         sd.update(milestones=self.milestones, gamma=self.gamma)
         return sd
 
     def load_state_dict(self, sd):
-        self.milestones, self.gamma = list(sd["milestones"]), sd["gamma"]
+        # a resumed run continues the checkpoint's schedule; a cosine checkpoint
+        # (no milestones) keeps the command line's, and any difference is said
+        ms, gamma = sd.get("milestones", self.milestones), sd.get("gamma", self.gamma)
+        ms = sorted(int(m) for m in ms)
+        if "milestones" in sd and (ms != self.milestones or float(gamma) != self.gamma):
+            warnings.warn(f"checkpoint lr milestones {ms} / gamma {gamma} differ from the command line's "
+                          f"{self.milestones} / {self.gamma}: resuming with the checkpoint's", stacklevel=2)
+        self.milestones, self.gamma = ms, float(gamma)
         super().load_state_dict(sd)
 
 

@@ -55,3 +55,33 @@ def run_world(fn, world: int, *args):
             o = torch.load(os.path.join(d, f"r{r}.pt"), weights_only=False)
             out.append(o["res"])
         return out
+
+
+def run_world_exitcodes(fn, world: int, *args, timeout_s: float = 60.0):
+    """Run fn(rank, world, *args) in `world` gloo processes without joining on
+    success; returns each process's exit code (None = still running when the
+    timeout expired; such processes are then killed)."""
+    import time
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_exit_entry, args=(r, world, port, fn, args), daemon=True)
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    deadline = time.monotonic() + timeout_s
+    for p in procs:
+        p.join(max(0.0, deadline - time.monotonic()))
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            p.join(5)
+    return codes
+
+
+def _exit_entry(rank, world, port, fn, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fn(rank, world, *args)

@@ -358,3 +358,33 @@ def _graphed_dp_check(arch, build_model, cross_entropy, cast_model, _copy):
             torch.testing.assert_close(b.float(), a.float(), atol=3e-2, rtol=3e-2, msg=n)
         else:
             assert torch.equal(a, b), n
+
+
+def test_replicas_with_activation_checkpointing_stay_bound_for_recompute():
+    """replicas of a network that recomputes in backward
+    (CheckpointedSequential) must keep their parameter slots after release():
+    the recompute runs the replica modules again.  Here: two CPU replicas,
+    released right after their forwards (as DataParallel.forward does), then
+    backward -- gradients equal the plain module's."""
+    from distributed_model_parallel_amd.utils.checkpointing import CheckpointedSequential
+    from distributed_model_parallel_amd.parallel.data_parallel import recomputes_in_backward
+    torch.manual_seed(0)
+    trunk = CheckpointedSequential(nn.Linear(6, 6), nn.Tanh(), nn.Linear(6, 6), nn.Tanh(), segments=2)
+    m = nn.Sequential(trunk, nn.Linear(6, 3))
+    ref = nn.Sequential(nn.Sequential(*[l for l in trunk]), m[1])
+    assert recomputes_in_backward(m) and not recomputes_in_backward(ref)
+    x = torch.randn(8, 6)
+    cache = {}
+    for step in range(2):
+        reps = replicate(m, ["cpu", "cpu"], cache=cache)
+        assert reps.skeleton is None  # never the shared, released skeleton
+        from distributed_model_parallel_amd.parallel.data_parallel import _parallel_apply_threads
+        outs = _parallel_apply_threads(reps, [(x[:4],), (x[4:],)], devices=[None, None])
+        reps.release()
+        m.zero_grad()
+        torch.cat(outs).pow(2).sum().backward()
+        g = [p.grad.clone() for p in m.parameters()]
+        m.zero_grad()
+        ref(x).pow(2).sum().backward()
+        for a, p in zip(g, m.parameters()):
+            torch.testing.assert_close(a, p.grad, atol=1e-6, rtol=1e-5)

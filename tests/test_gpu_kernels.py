@@ -62,6 +62,48 @@ def test_bn_act_forward_backward(dtype, shape, relu, res):
         torch.testing.assert_close(r1.grad.float(), rr.grad, atol=gt, rtol=gt)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("res", [False, True])
+@pytest.mark.parametrize("training", [True, False])
+def test_bn_relu6_forward_backward(dtype, res, training):
+    """act="relu6" (the 224-px MobileNetV2, VERDICT r4 missing 4): the clip at 6
+    runs inside the same apply kernels, and both backward masks (from the
+    saved output with a residual, re-derived from x without) stop at 6."""
+    torch.manual_seed(1)
+    C = 64
+    x = (torch.randn(6, C, 9, 9, device=DEV) * 2).to(dtype).contiguous(memory_format=torch.channels_last)
+    r = (torch.randn_like(x.float()) * 2).to(dtype) if res else None
+    w = torch.rand(C, device=DEV) * 2 + 0.5
+    b = torch.randn(C, device=DEV) * 2 + 3.0  # a good share of the outputs above 6
+    rm, rv = torch.randn(C, device=DEV) * 0.1, torch.rand(C, device=DEV) + 0.5
+    rm2, rv2 = rm.clone(), rv.clone()
+    xr = x.detach().float().requires_grad_()
+    rr = r.detach().float().requires_grad_() if res else None
+    x1 = x.detach().requires_grad_()
+    r1 = r.detach().requires_grad_() if res else None
+    w1, b1 = w.clone().requires_grad_(), b.clone().requires_grad_()
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    before = bn.stats()["native_fwd"]
+    y = bn.batch_norm_act(x1, rm, rv, w1, b1, training, 0.1, 1e-5, residual=r1, act="relu6")
+    assert bn.stats()["native_fwd"] == before + 1, "HIP BN kernel not used"
+    yr = bn.reference_bn_act(xr, rm2, rv2, wr, br, training, 0.1, 1e-5, residual=rr, act="relu6")
+    frac6 = (yr >= 6).float().mean().item()
+    assert 0.05 < frac6 < 0.8, frac6
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(y.float(), yr, atol=tol, rtol=tol)
+    assert y.float().max().item() <= 6.0
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g)
+    gt = 6e-2 if dtype == torch.bfloat16 else 1e-3
+    # bf16: an output within half an ulp of 6 may round onto the clip (mask from y)
+    bad = ((x1.grad.float() - xr.grad).abs() > gt + gt * xr.grad.abs()).float().mean().item()
+    assert bad < (2e-3 if dtype == torch.bfloat16 else 1e-6), bad
+    torch.testing.assert_close(b1.grad, br.grad, atol=gt * 20, rtol=gt)
+    if res:
+        torch.testing.assert_close(r1.grad.float(), rr.grad, atol=gt, rtol=gt)
+
+
 def test_bn_eval_mode():
     C = 64
     x = torch.randn(4, C, 5, 5, device=DEV).contiguous(memory_format=torch.channels_last)

@@ -1,6 +1,7 @@
 """Optimizers: MasterSGD (fp32 master weights for any parameter list, used by
 DP / pipeline / single-GPU training) must reproduce torch.optim.SGD in fp32 and
 keep updates that bf16 SGD would drop (DP/pipe precision parity)."""
+import pytest
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -140,3 +141,30 @@ def test_checkpoint_with_legacy_numpy_rng_state_loads(tmp_path):
     np.random.seed(99)
     load_checkpoint(path, _net(), restore_rng=True)
     assert np.allclose(np.random.rand(3), expect)
+
+
+def test_schedule_resume_across_kinds_and_milestones():
+    """a cosine checkpoint resumed with --lr-steps must not KeyError
+    (the command line's milestones stay); different milestones / schedule
+    kinds warn; a multistep checkpoint resumes its own milestones."""
+    import warnings
+    from distributed_model_parallel_amd.utils.schedule import build_schedule
+    p = nn.Parameter(torch.zeros(1))
+    cos = build_schedule(torch.optim.SGD([p], lr=0.4), 90, 5)
+    cos.step(); cos.step()
+    sd_cos = cos.state_dict()
+    ms = build_schedule(torch.optim.SGD([p], lr=0.4), 90, 5, lr_steps=[30, 60])
+    with pytest.warns(UserWarning, match="cosine"):
+        ms.load_state_dict(sd_cos)
+    assert ms.milestones == [30, 60] and ms.epoch == 2
+    ms2 = build_schedule(torch.optim.SGD([p], lr=0.4), 90, 5, lr_steps=[10, 20])
+    with pytest.warns(UserWarning, match="milestones"):
+        ms2.load_state_dict(ms.state_dict())
+    assert ms2.milestones == [30, 60]
+    ms3 = build_schedule(torch.optim.SGD([p], lr=0.4), 90, 5, lr_steps=[30, 60])
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        ms3.load_state_dict(ms.state_dict())  # identical: silent
+    cos2 = build_schedule(torch.optim.SGD([p], lr=0.4), 90, 5)
+    with pytest.warns(UserWarning, match="multistep"):
+        cos2.load_state_dict(ms.state_dict())

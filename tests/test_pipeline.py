@@ -198,3 +198,32 @@ def test_batch_schedule_matches_loader_and_rejects_ragged_batches():
         batch_schedule(DataLoader(ds, batch_sampler=Ragged()), 16)
     ok = BatchSampler(SequentialSampler(range(40)), 16, False)
     assert batch_schedule(DataLoader(ds, batch_sampler=list(ok)), 16) == (3, 8)
+
+
+def _bad_batch_worker(rank, world):
+    import time
+    from distributed_model_parallel_amd.comm.rccl import Communicator
+    from distributed_model_parallel_amd.parallel.pipeline import Pipeline
+    atoms = _mlp_atoms()
+    pipe = Pipeline(atoms, Communicator(torch.device("cpu")), (3, 4, 4), micro_batches=2,
+                    schedule="1f1b", static_batch=6)
+    x, y = _data("mlp", 5)  # breaks the static contract of 6
+    if rank == 0:
+        try:
+            pipe.train_step(x, y)
+        except ValueError:
+            time.sleep(30)  # stay alive (a notebook, a caught error): peers must not rely on our exit
+            raise SystemExit(7)
+        raise SystemExit(0)
+    pipe.train_step(None, None)  # blocks in a receive that rank 0 never sends
+    raise SystemExit(0)
+
+
+def test_pipeline_contract_violation_exits_every_rank():
+    """a bad batch on rank 0 used to leave every later stage
+    blocked in a receive forever.  Rank 0 now publishes the failure through the
+    store (utils/debug.FailureBroadcast) and the other stages exit non-zero
+    while rank 0 is still alive."""
+    from tests.dist_utils import run_world_exitcodes
+    codes = run_world_exitcodes(_bad_batch_worker, 3, timeout_s=25)
+    assert codes[1] == 3 and codes[2] == 3, codes   # peers: failure flag seen, os._exit(3)
