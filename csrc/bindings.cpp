@@ -1,6 +1,7 @@
 #include <cmath>
 // Python bindings of the native runtime (module distributed_model_parallel_amd._C).
 #include <torch/extension.h>
+#include <torch/csrc/autograd/variable.h>
 
 #include "comm/rccl_comm.h"
 #include "ddp/reducer.h"
@@ -483,4 +484,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.def("compute_bucket_assignment", &dmp::compute_bucket_assignment, py::arg("params"),
         py::arg("cap_bytes"), py::arg("first_cap_bytes"));
+  // ops/wgrad_stream.py: which stream a leaf's AccumulateGrad node runs on
+  // (-1: the leaf has no accumulator yet; -2: no accelerator stream)
+  m.def("grad_accumulator_stream", [](const at::Tensor& t) -> int64_t {
+    auto acc = torch::autograd::impl::try_get_grad_accumulator(t);
+    if (!acc) return -1;
+    auto s = acc->stream();
+    return s.has_value() ? (int64_t)s->id() : -2;
+  });
 }

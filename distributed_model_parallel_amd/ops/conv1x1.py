@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 
 from .. import _native
+from . import wgrad_stream
 
 _STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0, "compact_dgrad": 0,
           "compact_residual": 0}
@@ -186,14 +187,16 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             # split-M MFMA GEMM with transposing LDS reads (hipBLASLt picks a 4-tile,
             # no-split kernel for this tiny-output / huge-reduction shape); the
-            # ping-pong form where both output dims fill its 256x256 tile
-            if not ctx.geom and _tn_xl(dy2.shape[0], cout, cin):
-                _STATS["tn_xl"] += 1
-                dw = C.gemm_tn_xl(dy2, _rows(x), weight.dtype).view(cout, cin, 1, 1)
-            else:
-                dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
-            if weight.is_contiguous(memory_format=torch.channels_last):
-                dw = dw.contiguous(memory_format=torch.channels_last)
+            # ping-pong form where both output dims fill its 256x256 tile.  On the
+            # weight-gradient side stream, beside the data-gradient chain.
+            with wgrad_stream.side(weight, dy2, x):
+                if not ctx.geom and _tn_xl(dy2.shape[0], cout, cin):
+                    _STATS["tn_xl"] += 1
+                    dw = C.gemm_tn_xl(dy2, _rows(x), weight.dtype).view(cout, cin, 1, 1)
+                else:
+                    dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
+                if weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous(memory_format=torch.channels_last)
         return dx, dw, None, None, None, None, None
 
 

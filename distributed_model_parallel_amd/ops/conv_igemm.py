@@ -19,6 +19,8 @@ uses ``F.conv2d``.  The reference uses torchvision's cuDNN convolutions
 """
 from __future__ import annotations
 
+import contextlib
+
 import os
 
 from typing import Optional, Tuple
@@ -28,6 +30,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from . import wgrad_stream
 
 _STATS = {"native": 0, "torch": 0}
 # DMP_DISABLE=igemm routes these convs to MIOpen (A/B comparisons, debugging)
@@ -283,28 +286,34 @@ class _ConvIGFn(torch.autograd.Function):
             _STATS["xl_dgrad_s2"] += 1
             dx2 = C.conv_xl_dgrad_s2(dy, _phase_weights(weight), h, w)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        # weight gradients on the side stream (ops/wgrad_stream.py), beside the
+        # data-gradient chain
         if ctx.needs_input_grad[1] and _halo_wgrad_ok(C, cin, cout, kh, kw, stride, pad, h, w):
             # persistent halo-tiled MFMA weight gradient (csrc/conv/wgrad3x3.hip)
             _STATS["halo_wgrad"] += 1
-            dw = C.wgrad3x3(dy, x, stride)
-            if not weight.is_contiguous(memory_format=torch.channels_last):
-                dw = dw.contiguous()
+            with wgrad_stream.side(weight, dy, x):
+                dw = C.wgrad3x3(dy, x, stride)
+                if not weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous()
         if ctx.needs_input_grad[1] and dw is None and _xl_wgrad_ok(cin, kh, kw, n * ho * wo):
             _STATS["xl_wgrad"] += 1
-            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
-            g = C.conv_wgrad_xl(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
-            dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
-            if not weight.is_contiguous(memory_format=torch.channels_last):
-                dw = dw.contiguous()
+            with wgrad_stream.side(weight, dy, x):
+                dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+                g = C.conv_wgrad_xl(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
+                dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
+                if not weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous()
         generic = NATIVE_BWD or _capturing()
         nat_d = ctx.needs_input_grad[0] and dx is None and generic
         nat_w = ctx.needs_input_grad[1] and dw is None and generic
         want_d = ctx.needs_input_grad[0] and not nat_d and dx is None
         want_w = ctx.needs_input_grad[1] and not nat_w and dw is None
         if want_d or want_w:
-            dx_l, dw_l, _ = torch.ops.aten.convolution_backward(
-                dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
-                [want_d, want_w, False])
+            # a weight-gradient-only library call also goes to the side stream
+            with (wgrad_stream.side(weight, dy, x) if not want_d else contextlib.nullcontext()):
+                dx_l, dw_l, _ = torch.ops.aten.convolution_backward(
+                    dy, x, weight, None, [stride, stride], [pad, pad], [1, 1], False, [0, 0], 1,
+                    [want_d, want_w, False])
             if want_d:
                 dx = dx_l
             if want_w:
@@ -314,11 +323,12 @@ class _ConvIGFn(torch.autograd.Function):
             dx2, _ = C.conv_nt(dy, wt, kh, kw, stride, pad, h, w, transposed=True)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
         if nat_w:
-            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
-            g = C.conv_wgrad(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
-            dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
-            if not weight.is_contiguous(memory_format=torch.channels_last):
-                dw = dw.contiguous()
+            with wgrad_stream.side(weight, dy, x):
+                dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+                g = C.conv_wgrad(dy2, x, kh, kw, stride, pad, ho, wo, weight.dtype)
+                dw = g.view(cout, kh, kw, cin).permute(0, 3, 1, 2)
+                if not weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = dw.contiguous()
         return dx, dw, None, None, None, None
 
 

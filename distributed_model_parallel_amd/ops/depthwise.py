@@ -47,7 +47,11 @@ class _DWConvFn(torch.autograd.Function):
         C = _native.require("depthwise conv backward")
         dy = dy.contiguous(memory_format=torch.channels_last).to(x.dtype)
         dx = C.dwconv3x3_dgrad(dy, w, ctx.stride, x.shape[2], x.shape[3]) if ctx.needs_input_grad[0] else None
-        dw = C.dwconv3x3_wgrad(dy, x, ctx.stride, w.dtype) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            from . import wgrad_stream
+            with wgrad_stream.side(w, dy, x):  # beside the data-gradient chain
+                dw = C.dwconv3x3_wgrad(dy, x, ctx.stride, w.dtype)
         return dx, dw, None, None
 
 

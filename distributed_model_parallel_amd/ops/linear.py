@@ -33,6 +33,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from . import wgrad_stream
 
 _STATS = {"native": 0, "torch": 0, "xl": 0, "tn_wgrad": 0, "xl_dgrad": 0, "xl_fwd": 0}
 _XL = not _native.disabled("xl_linear")
@@ -80,12 +81,14 @@ def _gemm_operand_ok(t: torch.Tensor) -> bool:
 
 
 def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    if (_TN_WGRAD and dy2.shape[0] >= _TN_MIN_ROWS and dy2.shape[1] >= 256 and x2.shape[1] >= 256
-            and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and _gemm_operand_ok(dy2)
-            and _gemm_operand_ok(x2) and w.dtype == torch.bfloat16):
-        _STATS["tn_wgrad"] += 1
-        return _native.native().gemm_tn_xl(dy2, x2, w.dtype)
-    return dy2.t().mm(x2)
+    # on the weight-gradient side stream, beside the data-gradient chain (ops/wgrad_stream.py)
+    with wgrad_stream.side(w, dy2, x2):
+        if (_TN_WGRAD and dy2.shape[0] >= _TN_MIN_ROWS and dy2.shape[1] >= 256 and x2.shape[1] >= 256
+                and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and _gemm_operand_ok(dy2)
+                and _gemm_operand_ok(x2) and w.dtype == torch.bfloat16):
+            _STATS["tn_wgrad"] += 1
+            return _native.native().gemm_tn_xl(dy2, x2, w.dtype)
+        return dy2.t().mm(x2)
 
 
 def _xl_gemm_ok(a: torch.Tensor, n: int) -> bool:

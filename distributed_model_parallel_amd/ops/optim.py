@@ -18,6 +18,7 @@ from typing import List, Optional
 import torch
 
 from .. import _native
+from . import wgrad_stream
 
 
 
@@ -79,6 +80,8 @@ class FlatSGD(torch.optim.Optimizer):
         self._ensure_state()
         g = self.param_groups[0]
         first = self._steps == 0
+        if self._flat_state and self._flat_state[0]["param"].is_cuda:
+            wgrad_stream.join(self._flat_state[0]["param"].device)  # gradients from the side stream
         for st in self._flat_state:
             pflat, gflat = st["param"], st["grad"]
             master = st.get("master")
@@ -211,6 +214,8 @@ class MasterSGD(torch.optim.Optimizer):
                 loss = closure()
         g = self.param_groups[0]
         first = self._steps == 0
+        if self._groups and self._groups[0]["param"].is_cuda:
+            wgrad_stream.join(self._groups[0]["param"].device)  # gradients from the side stream
         for st in self._groups:
             self._adopt_grads(st)
             pflat, gflat, master = st["param"], st["grad"], st.get("master")

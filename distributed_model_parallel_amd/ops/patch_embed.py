@@ -56,10 +56,12 @@ class _PatchEmbedFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, d).contiguous()
         dw = db = dx = None
         if ctx.needs_input_grad[1]:
-            dwm = _wgrad(dy2, patches, weight)  # [D, (kh, kw, c)]
-            dw = dwm.view(d, p, p, c).permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last) \
-                if weight.is_contiguous(memory_format=torch.channels_last) else \
-                dwm.view(d, p, p, c).permute(0, 3, 1, 2).contiguous()
+            from . import wgrad_stream
+            with wgrad_stream.side(weight, dy2, patches):  # the layout copy follows the GEMM on S
+                dwm = _wgrad(dy2, patches, weight)  # [D, (kh, kw, c)]
+                dw = dwm.view(d, p, p, c).permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last) \
+                    if weight.is_contiguous(memory_format=torch.channels_last) else \
+                    dwm.view(d, p, p, c).permute(0, 3, 1, 2).contiguous()
         if ctx.needs_input_grad[2]:
             db = C.bias_grad(dy2, weight.dtype)
         if ctx.needs_input_grad[0]:  # the image rarely needs a gradient: plain GEMM + un-patchify

@@ -164,7 +164,14 @@ class DistributedDataParallel(nn.Module):
                                "with `python csrc/build.py`")
         self._C = C
         buckets = C.compute_bucket_assignment(params, self.bucket_cap, self.first_bucket_cap)
-        self.reducer = C.Reducer(params, buckets, self._make_backend(), find_unused_parameters)
+        # The reducer creates the parameters' AccumulateGrad nodes: create them on
+        # the weight-gradient side stream, so the weight-gradient kernels, the
+        # bucket flushes and the all-reduce launches all run off the data-gradient
+        # chain (ops/wgrad_stream.py)
+        from ..ops import wgrad_stream
+        with wgrad_stream.creating_on_side(dev):
+            self.reducer = C.Reducer(params, buckets, self._make_backend(), find_unused_parameters)
+        self.async_wgrad_params = wgrad_stream.mark_bound(params) if dev.type == "cuda" else 0
         self._buffers_flat: Optional[List[torch.Tensor]] = None
         if flat_parameters:
             self._install_flat_params()
