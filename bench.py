@@ -224,6 +224,7 @@ def main() -> int:
         enable_phase_timing()
     from distributed_model_parallel_amd.utils import routes
     routes0 = routes.route_counts()
+    bcast0 = getattr(st.wrapped, "buffer_broadcasts", None)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         with trace_range("bench.step"):
@@ -238,6 +239,17 @@ def main() -> int:
                    sorted(routes.diff(routes.route_counts(), routes0).items())}
     phases = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] / args.steps}
               for k, v in phase_summary().items()} if args.phase_times else None
+
+    # multi-rank facts the gloo rehearsal (tests/test_bench_multirank_cpu.py) checks:
+    # every rank holds the same (rebuilt) bucket layout -- RCCL would deadlock on a
+    # mismatch -- and module buffers cost one broadcast per dtype group per forward
+    ddp_facts = None
+    if hasattr(st.wrapped, "bucket_summary"):
+        ddp_facts = st.wrapped.bucket_summary()
+        dig = float(ddp_facts["digest"])
+        ddp_facts["same_on_all_ranks"] = comm.max_scalar(dig) == -comm.max_scalar(-dig)
+        ddp_facts["buffer_broadcasts_per_step"] = (st.wrapped.buffer_broadcasts - bcast0) / args.steps
+        ddp_facts["buffer_dtype_groups"] = len(st.wrapped._buffers_flat or [])
 
     import torch.distributed as dist
     n = dist.get_world_size()
@@ -301,6 +313,7 @@ def main() -> int:
             "first_step_ms": round(first_step_ms, 1) if first_step_ms is not None else None,
             "final_loss": round(final_loss, 4),
             "routes_per_step": step_routes,
+            **({"ddp_buckets": ddp_facts} if ddp_facts is not None else {}),
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
             if dev.type == "cuda" else None,
         },

@@ -129,6 +129,7 @@ class DistributedDataParallel(nn.Module):
         self._iteration = 0
         self._layout_version = 0
         self._flat_params: Optional[List[torch.Tensor]] = None
+        self.buffer_broadcasts = 0  # collectives issued for module buffers (diagnostics)
 
         params = []
         seen = set()
@@ -286,6 +287,17 @@ class DistributedDataParallel(nn.Module):
     def param_layout(self):
         return self.reducer.layout()
 
+    def bucket_summary(self) -> dict:
+        """Bucket layout facts for diagnostics / the multi-rank rehearsal: the
+        parameter indices per bucket (launch order), their MB, a digest, and
+        whether the ready-order rebuild has happened."""
+        import zlib
+        buckets = [[int(i) for i in b] for b in self.reducer.buckets()]
+        mb = [round(sum(self._params[i].numel() * self._params[i].element_size() for i in b) / _MB, 3)
+              for b in buckets]
+        return {"buckets": len(buckets), "bucket_mb": mb, "digest": zlib.crc32(repr(buckets).encode()),
+                "rebuilt": not self._rebuild_pending}
+
     def _maybe_rebuild_buckets(self) -> None:
         if not self._rebuild_pending or self._iteration < 1:
             return
@@ -332,8 +344,9 @@ class DistributedDataParallel(nn.Module):
             self._maybe_rebuild_buckets()
         if self.broadcast_buffers and self.world_size > 1 and self._buffers_flat:
             with trace_range("ddp.broadcast_buffers"):
-                for f in self._buffers_flat:
+                for f in self._buffers_flat:  # one collective per buffer dtype group
                     self.comm.broadcast(f, 0)
+                    self.buffer_broadcasts += 1
                 self.comm.wait()
         with trace_range("ddp.forward"):
             out = self.module(*inputs, **kwargs)

@@ -30,3 +30,20 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True, scope="session")
+def _destroy_process_group_at_exit():
+    """GPU tests that need a process group in the pytest process (the pipeline
+    and convergence tests: world size 1 over RCCL) create it lazily; destroy it
+    once at the end of the session (the suite exited with
+    'destroy_process_group() was not called')."""
+    yield
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        try:
+            from distributed_model_parallel_amd.comm.rccl import reset_default_communicator
+            reset_default_communicator()
+        except Exception:  # noqa: BLE001 - best effort before the destroy
+            pass
+        dist.destroy_process_group()
