@@ -139,6 +139,8 @@ def main() -> int:
     ap.add_argument("--dp-graphs", action="store_true",
                     help="--parallel dp: run every replica's forward / backward as captured hipGraphs "
                          "(parallel/dp_graphs.py) instead of Python threads")
+    ap.add_argument("--no-pipe-graphs", action="store_true",
+                    help="--parallel pipe: run the micro-batches eagerly instead of on captured stage graphs")
     ap.add_argument("--phase-times", action="store_true",
                     help="record HIP events around the DataParallel phases and report their GPU "
                          "ms per step in the JSON (config.phase_ms_per_step)")
@@ -191,7 +193,8 @@ def main() -> int:
                      dp_replicas=args.dp_replicas, graph=args.graph,
                      lr=args.lr if args.lr is not None else (0.005 if args.model.startswith("vit") else 0.1),
                      micro_batches=args.micro_batches, schedule=args.schedule, partition=args.partition,
-                     checkpoint_segments=args.checkpoint_segments, dp_graphs=args.dp_graphs)
+                     checkpoint_segments=args.checkpoint_segments, dp_graphs=args.dp_graphs,
+                     pipe_graphs=not args.no_pipe_graphs)
     if args.parallel == "dp" and env.world_size > 1:
         raise SystemExit("--parallel dp is single-process multi-GPU: run `python bench.py --parallel dp "
                          "--gpus N` without torchrun")
@@ -300,7 +303,8 @@ def main() -> int:
             "channels_last": not args.no_channels_last,
             "grad_comm": getattr(st.wrapped, "comm_backend", None),
             **({"micro_batches": args.micro_batches, "schedule": args.schedule,
-                "stage_partition": st.wrapped.partition} if args.parallel == "pipe" else {}),
+                "stage_partition": st.wrapped.partition,
+                "stage_graphs": bool(st.wrapped._graphs)} if args.parallel == "pipe" else {}),
             **({"reference_images_per_sec": round(ref, 1)} if ref else {}),
             "hip_graph": args.graph,
             "checkpoint_segments": args.checkpoint_segments,

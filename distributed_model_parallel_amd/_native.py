@@ -93,6 +93,8 @@ FEATURES = {
     "rowtap_stem": "row-tap stem implicit GEMM (stem.hip) -> MIOpen",
     "bn_fold": "bottleneck bn3 folded through conv3 (ops/bn_fold.py) -> conv + BN apply passes",
     "bn_fold_ds": "downsample conv + BN folded into the same GEMM as bn3 (ops/bn_fold.py) -> separate shortcut",
+    "fuse_stem_wgrad": "stem BN backward apply folded into the stem weight gradient (ops/fused.py) "
+                       "-> the apply pass + one weight gradient",
     "async_wgrad": "weight gradients on a side stream beside the data-gradient chain (ops/wgrad_stream.py) "
                    "-> inline on the compute stream",
 }

@@ -274,6 +274,99 @@ class _BNReLUMaxPoolFn(torch.autograd.Function):
 _STATS_FUSED["bn_relu_maxpool"] = 0
 
 
+class _StemBNReLUMaxPoolFn(torch.autograd.Function):
+    """pool(relu(bn(stem_conv(img)))) with the stem's BN backward apply folded
+    into its weight gradient (the image needs no gradient).
+
+    The BN backward's output dx = a*dz + b*y + c (per-channel a, b, c from the
+    reduced sums; y the conv output, dz the pool-scattered, ReLU-masked
+    gradient) feeds ONLY the stem's weight gradient dW = dx^T P (P the
+    implicit patch matrix of the space-to-depth image).  That is linear in dx:
+
+        dW[o, k] = a_o (dz^T P)[o, k] + b_o (y^T P)[o, k] + c_o colsum(P)[k]
+
+    so the step runs the halo weight-gradient kernel on dz and on y (fp32
+    outputs) plus a column sum of P (one pass over the small s2d image)
+    instead of writing dx -- the 2048 x 64 x 112 x 112 apply pass (1.85 ms at
+    batch 2048, its read of dz and y and its write of dx) is gone.  b*(y^T P)
+    and c*colsum(P) partly cancel (through the mean); both are fp32 sums."""
+
+    @staticmethod
+    def forward(ctx, img, wmat, bn_w, bn_b, running_mean, running_var, momentum, eps, nbt, reduce_moments,
+                reduce_grads, pad):
+        from .. import _native
+        C = _native.require("stem + bn + maxpool")
+        n, _, h, w = img.shape
+        ho, wo = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1
+        s = C.space_to_depth2(img, 3)
+        y2, sums = C.stem_halo_fwd(s, wmat.contiguous(), ho, True)
+        co = wmat.shape[0]
+        y = y2.view(n, ho, wo, co).permute(0, 3, 1, 2)
+        if reduce_moments is not None:
+            sums = reduce_moments(sums)
+        w32 = bn_w.float() if bn_w is not None else None
+        b32 = bn_b.float() if bn_b is not None else None
+        coef = C.bn_finalize(sums, w32, b32, running_mean, running_var, float(momentum), float(eps), co, nbt)
+        out, idx = C.maxpool2d_bn_forward(y, coef[0].contiguous(), coef[1].contiguous(), 3, 2, pad)
+        ctx.save_for_backward(s, y, idx, w32, b32, coef, sums[-1:])
+        ctx.meta = (reduce_grads, bn_w.dtype if bn_w is not None else None, bn_w is not None, bn_b is not None,
+                    pad, n, ho, wo, wmat.dtype)
+        ctx.mark_non_differentiable(idx)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .. import _native
+        C = _native.require("stem + bn + maxpool backward")
+        s, y, idx, w32, b32, coef, count = ctx.saved_tensors
+        reduce_grads, wdtype, has_w, has_b, pad, n, ho, wo, mdtype = ctx.meta
+        co = y.shape[1]
+        scale, shift, mean, invstd = (coef[i].contiguous() for i in range(4))
+        dz, sums = C.maxpool2d_bn_backward(dy.contiguous(memory_format=torch.channels_last), idx, y,
+                                           scale, shift, mean, 3, 2, pad)
+        sums = sums[: 2 * co]
+        local = sums
+        if reduce_grads is not None:
+            local = sums.clone()  # the reducer works in place
+            sums = reduce_grads(sums)
+        cnt = count.reshape(()).double()
+        sdz, sdzx = sums[:co], sums[co:]
+        istd = invstd.double()
+        al = istd * (w32.double() if w32 is not None else 1.0)
+        be = -al * istd * istd * sdzx / cnt
+        cc = -al * sdz / cnt - be * mean.double()
+        rows = lambda t: t.permute(0, 2, 3, 1).reshape(n * ho * wo, co)  # noqa: E731
+        t_dz = C.stem_halo_wgrad(rows(dz), s, ho, torch.float32)
+        t_y = C.stem_halo_wgrad(rows(y), s, ho, torch.float32)
+        # colsum(P)[r*64 + q*16 + ch] = sum over images and output pixels of s[n, ch, oh+r, ow+q]
+        ssum = s.sum(0, dtype=torch.float32)                       # [16, Hs, Ws]
+        cols = torch.stack([ssum[:, r:r + ho, q:q + wo].sum((1, 2)) for r in range(4) for q in range(4)])
+        dw = (al.float()[:, None] * t_dz + be.float()[:, None] * t_y
+              + cc.float()[:, None] * cols.reshape(1, -1)).to(mdtype)
+        if reduce_grads is not None:
+            dg = (local[co:] * invstd.double()).float()
+            db = local[:co].float()
+        else:
+            dg, db = (sdzx * istd).float(), sdz.float()
+        gw = dg.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
+        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
+        return None, dw, gw, gb, None, None, None, None, None, None, None, None
+
+
+_STATS_FUSED["stem_bn_relu_maxpool"] = 0
+
+
+def _stem_fold_ok(conv: nn.Module, x: torch.Tensor) -> bool:
+    from .. import _native
+    from .stem import StemConv2d, _HALO, _native_ok
+    if not (_FUSE_STEM_WGRAD and _HALO and isinstance(conv, StemConv2d) and _native_ok(conv, x)):
+        return False
+    C = _native.native()
+    n, _, h, w = x.shape
+    ho, wo = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1
+    return C.stem_halo_supported((h + 7) // 2, (w + 7) // 2, ho, wo) and conv.out_channels == 64
+
+
 def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """pool(bn_relu(conv(x))) -- the ResNet stem.  BN apply + ReLU run inside the
     pool (forward) and the BN backward's reductions inside the pool's backward
@@ -288,6 +381,15 @@ def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Te
                and pool.dilation in (1, (1, 1)) and _FUSE_STEM_POOL)
     if not fusable:
         return pool(conv_bn(conv, bn, x))
+    pad = pool.padding if isinstance(pool.padding, int) else pool.padding[0]
+    if _stem_fold_ok(conv, x) and bn.running_mean is not None and bn.running_mean.dtype == torch.float32:
+        from .stem import stem_wmat
+        rmom, rgrad = bn._moment_reducers()
+        _STATS_FUSED["stem_bn_relu_maxpool"] += 1
+        _STATS_FUSED["bn_relu_maxpool"] += 1
+        return _StemBNReLUMaxPoolFn.apply(x, stem_wmat(conv.weight), bn.weight, bn.bias, bn.running_mean,
+                                          bn.running_var, bn.momentum, bn.eps, bn.num_batches_tracked, rmom,
+                                          rgrad, pad)
     y, sums = conv.forward_with_moments(x)
     if (sums is None or not _native.gpu_path(y) or y.dtype != torch.bfloat16
             or not y.is_contiguous(memory_format=torch.channels_last)
@@ -295,7 +397,6 @@ def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Te
             or bn.running_mean is None or bn.running_mean.dtype != torch.float32):
         return pool(bn(y, sums=sums))
     rmom, rgrad = bn._moment_reducers()
-    pad = pool.padding if isinstance(pool.padding, int) else pool.padding[0]
     _STATS_FUSED["bn_relu_maxpool"] += 1
     return _BNReLUMaxPoolFn.apply(y, bn.weight, bn.bias, sums, bn.running_mean, bn.running_var, bn.momentum,
                                   bn.eps, bn.num_batches_tracked, rmom, rgrad, 3, 2, pad)
@@ -303,3 +404,5 @@ def conv_bn_maxpool(conv: nn.Module, bn: nn.Module, pool: nn.Module, x: torch.Te
 
 from .. import _native as _nat  # noqa: E402
 _FUSE_STEM_POOL = not _nat.disabled("fuse_stem_pool")
+# DMP_DISABLE=fuse_stem_wgrad: keep the stem's BN backward apply pass (A/B runs)
+_FUSE_STEM_WGRAD = not _nat.disabled("fuse_stem_wgrad")

@@ -70,6 +70,11 @@ def creating_on_side(device: torch.device) -> Iterator[None]:
     if not (ENABLED and device.type == "cuda" and torch.cuda.is_available()):
         yield
         return
+    if torch.cuda.current_stream(device) != torch.cuda.default_stream(device):
+        # the caller manages streams itself (bench --graph builds the whole
+        # state on its capture stream, whose accumulators must stay there)
+        yield
+        return
     s = stream(device)
     s.wait_stream(torch.cuda.current_stream(device))
     with torch.cuda.stream(s):

@@ -29,6 +29,17 @@ loops in ``utils.py:34-210``, partition at ``model_parallel.py:101-104,
   there, dlogits to the last stage; gpipe/naive only).
 * **Transport.**  :class:`~..comm.rccl.Communicator` -- RCCL send/recv on its
   own HIP stream on GPU (ordered with events, no blocking), gloo on CPU.
+* **Device speed** (``graphs=True``, GPU, 1F1B, loss on the last stage).  Eagerly
+  every micro-batch is hundreds of Python-dispatched kernel launches, so a
+  64-image MobileNetV2 micro-batch costs as much host time as a whole
+  512-image DDP step.  :class:`_StageGraphs` captures the
+  stage's forward (with the loss and top-k statistics on the last stage) and
+  backward once per in-flight slot as hipGraphs over static input / output /
+  gradient buffers; a micro-batch is then a receive into the slot's static
+  input, one forward replay, a send, a receive of the output gradient, one
+  backward replay (parameter gradients accumulate in place inside the graph)
+  and a send.  1F1B keeps at most ``S - r`` micro-batches in flight on stage
+  r, so that many slots (memory pools) suffice.
 """
 from __future__ import annotations
 
@@ -247,7 +258,7 @@ class Pipeline:
                  partition=None, balance: str = "flops",
                  device: Optional[torch.device] = None, dtype: torch.dtype = torch.float32,
                  channels_last: bool = False, static_batch: Optional[int] = None,
-                 fail_fast: bool = True):
+                 fail_fast: bool = True, graphs: bool = False):
         if schedule not in ("naive", "gpipe", "1f1b"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if loss_on not in ("last", "first"):
@@ -286,6 +297,8 @@ class Pipeline:
         # an exception on one stage (e.g. rank 0 refusing a batch that breaks the
         # static contract) would leave the other stages blocked in a receive
         # forever: publish it so every rank exits non-zero (utils/debug.py)
+        self.graphs = bool(graphs)
+        self._graphs: Dict[int, "_StageGraphs"] = {}  # micro-batch size -> captured slots
         self._failure = None
         if fail_fast and self.world > 1:
             from ..utils.debug import FailureBroadcast
@@ -408,7 +421,9 @@ class Pipeline:
         else:
             tgt_mbs = [t.to(self.device) for t in ts] if self.is_first else None
         stats = torch.zeros(3, dtype=torch.float64, device=self.device)
-        if self.schedule == "1f1b":
+        if self._graphed_ok(sizes):
+            stats = self._run_1f1b_graphed(xs, tgt_mbs, sizes)
+        elif self.schedule == "1f1b":
             self._run_1f1b(xs, tgt_mbs, sizes, stats)
         else:
             self._run_gpipe(xs, tgt_mbs, sizes, stats)
@@ -552,6 +567,67 @@ class Pipeline:
             if not self.is_first:
                 self.comm.send(gx.contiguous(), r - 1)
 
+    # 1F1B on captured stage graphs ------------------------------------------------------
+    def _graphed_ok(self, sizes) -> bool:
+        return (self.graphs and self.schedule == "1f1b" and self.loss_on == "last"
+                and self.device.type == "cuda" and len(set(sizes)) == 1
+                and not torch.cuda.is_current_stream_capturing())
+
+    def _run_1f1b_graphed(self, xs, tgts, sizes) -> torch.Tensor:
+        M = len(sizes)
+        S, r = self.world, self.rank
+        mb = sizes[0]
+        depth = min(M, S - r)
+        G = self._graphs.get(mb)
+        if G is None or G.depth < depth or not G.valid():
+            G = self._graphs[mb] = _StageGraphs(self, mb, depth)
+        G.stats.zero_()
+        warm = min(S - r - 1, M)
+        slot = lambda m: m % G.depth  # noqa: E731 - at most `depth` in flight (FIFO)
+
+        def forward(m):
+            k = slot(m)
+            if self.is_first:
+                G.inputs[k].copy_(xs[m])
+            else:
+                with trace_range("pipe.recv_fwd"):
+                    self.comm.recv(G.inputs[k].detach(), r - 1)
+                    self.comm.wait()
+            if self.is_last:
+                G.targets[k].copy_(tgts[m])
+            G.fwd[k].replay()
+
+        def backward(m, recv_grad: bool):
+            k = slot(m)
+            if not self.is_last and recv_grad:
+                with trace_range("pipe.recv_bwd"):
+                    self.comm.recv(G.gouts[k], r + 1)
+                    self.comm.wait()
+            G.bwd[k].replay()
+
+        for m in range(warm):
+            forward(m)
+            if not self.is_last:
+                self.comm.send(G.outs[slot(m)], r + 1)
+        b = 0
+        for m in range(warm, M):
+            forward(m)
+            if not self.is_last:
+                # send this output, receive the oldest in-flight micro-batch's gradient
+                with trace_range("pipe.send_fwd+recv_bwd"):
+                    self.comm.batch_p2p([(G.outs[slot(m)], r + 1, True), (G.gouts[slot(b)], r + 1, False)])
+                    self.comm.wait()
+            backward(b, recv_grad=False)
+            if not self.is_first:
+                self.comm.send(G.inputs[slot(b)].grad, r - 1)
+            b += 1
+        while b < M:
+            backward(b, recv_grad=True)
+            if not self.is_first:
+                self.comm.send(G.inputs[slot(b)].grad, r - 1)
+            b += 1
+        return G.stats.clone()  # the slots' statistics buffer is reused by the next step
+
     @torch.no_grad()
     def eval_step(self, inputs: Optional[torch.Tensor] = None,
                   targets: Optional[torch.Tensor] = None, batch_size: Optional[int] = None) -> StepResult:
@@ -608,3 +684,101 @@ class Pipeline:
             return StepResult(stats=stats, batch=batch)
         return StepResult(None, None, None)
 
+
+
+class _StageGraphs:
+    """``depth`` captured copies (slots) of one stage's forward and backward for
+    micro-batch size ``mb`` (``Pipeline(graphs=True)``).
+
+    Slot k owns a memory pool, a static input (the received activation, or the
+    data on stage 0), a static output (sent on; NCHW-contiguous like the eager
+    path's payload), a static output-gradient buffer and -- last stage -- the
+    static targets and the micro-batch's loss / top-1 / top-5 accumulated into
+    :attr:`stats` inside the forward graph.  The backward graph accumulates
+    the parameter gradients IN PLACE into ``p.grad`` (which must exist and keep
+    its storage: :meth:`valid` re-captures otherwise) and leaves the input
+    gradient in ``inputs[k].grad``.  Capture follows ``make_graphed_callables``:
+    two eager warm-up iterations on the capture stream (their effect on the
+    running statistics and gradients is undone), then per slot the forward and
+    the backward into one pool."""
+
+    def __init__(self, pipe: "Pipeline", mb: int, depth: int):
+        self.pipe, self.mb, self.depth = pipe, mb, depth
+        dev = pipe.device
+        self.params = [p for p in pipe.module.parameters() if p.requires_grad]
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)  # accumulated in place by the captured backward
+        self.grad_ptrs = [p.grad.data_ptr() for p in self.params]
+        self.param_ptrs = [p.data_ptr() for p in self.params]  # an optimizer may re-home them (flat buffers)
+        self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        in_shape, out_shape = pipe._in_shape(mb), pipe._out_shape(mb)
+        mk_in = lambda: torch.zeros(in_shape, dtype=pipe.dtype, device=dev)  # noqa: E731
+        if pipe.is_first and pipe.channels_last and len(in_shape) == 4:
+            mk_in = lambda: torch.zeros(in_shape, dtype=pipe.dtype, device=dev).contiguous(  # noqa: E731
+                memory_format=torch.channels_last)
+        self.inputs = [mk_in().requires_grad_(not pipe.is_first) for _ in range(depth)]
+        self.targets = [torch.zeros(mb, dtype=torch.int64, device=dev) for _ in range(depth)]
+        self.gouts = [torch.zeros(out_shape, dtype=pipe.dtype, device=dev) for _ in range(depth)]
+        self.outs: List[Optional[torch.Tensor]] = []
+        self.fwd: List[torch.cuda.CUDAGraph] = []
+        self.bwd: List[torch.cuda.CUDAGraph] = []
+        self.stream = torch.cuda.Stream(device=dev)
+        self._capture()
+
+    def _forward(self, k: int) -> torch.Tensor:
+        pipe = self.pipe
+        y = pipe.module(self.inputs[k])
+        if not pipe.is_last:
+            return y.contiguous()  # the wire layout of the eager path (its backward: a copy)
+        logits = y.float()
+        loss = pipe.loss_fn(logits, self.targets[k]) / pipe.micro_batches
+        with torch.no_grad():
+            c1, c5 = _topk_correct(logits, self.targets[k])
+            self.stats[0] += loss.detach().double()
+            self.stats[1] += c1.double()
+            self.stats[2] += c5.double()
+        return loss
+
+    def _backward(self, k: int, out: torch.Tensor) -> None:
+        if self.pipe.is_last:
+            out.backward()
+        else:
+            out.backward(self.gouts[k])
+
+    def _capture(self) -> None:
+        pipe = self.pipe
+        bufs = [b for b in pipe.module.buffers()]
+        saved_b = [b.detach().clone() for b in bufs]
+        saved_g = [p.grad.detach().clone() for p in self.params]
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream(pipe.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # lazy library initialisation outside the capture
+                self._backward(0, self._forward(0))
+        torch.cuda.current_stream(pipe.device).wait_stream(s)
+        with torch.no_grad():
+            for b, v in zip(bufs, saved_b):
+                b.copy_(v)
+            for p, v in zip(self.params, saved_g):
+                p.grad.copy_(v)
+            self.stats.zero_()
+        for x in self.inputs:
+            x.grad = None
+        torch.cuda.synchronize(pipe.device)
+        for k in range(self.depth):
+            pool = torch.cuda.graph_pool_handle()
+            gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gf, pool=pool, stream=s):
+                out = self._forward(k)
+            with torch.cuda.graph(gb, pool=pool, stream=s):
+                self._backward(k, out)
+            self.fwd.append(gf)
+            self.bwd.append(gb)
+            self.outs.append(out.detach() if not pipe.is_last else None)
+        torch.cuda.synchronize(pipe.device)
+
+    def valid(self) -> bool:
+        """The captured backward adds into the gradient storage seen at capture."""
+        return all(p.grad is not None and p.grad.data_ptr() == g and p.data_ptr() == d
+                   for p, g, d in zip(self.params, self.grad_ptrs, self.param_ptrs))

@@ -60,6 +60,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-channels-last", dest="channels_last", action="store_false")
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--micro-batches", default=1, type=int)
+    p.add_argument("--no-pipe-graphs", action="store_true",
+                   help="--parallel pipe on GPU: eager micro-batches instead of captured stage graphs")
     p.add_argument("--schedule", default="1f1b", choices=["naive", "gpipe", "1f1b"])
     p.add_argument("--partition", default="balanced", choices=["balanced", "reference"],
                    help="pipeline stage cut: FLOP-balanced (any ws) or the reference's MobileNetV2 cut")
@@ -257,7 +259,8 @@ def run_pipeline(args, env) -> None:
     comm = Communicator(env.device)
     pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=args.micro_batches,
                     schedule=args.schedule, dtype=parse_dtype(args.dtype),
-                    channels_last=args.channels_last, partition=args.partition)
+                    channels_last=args.channels_last, partition=args.partition,
+                    graphs=env.device.type == "cuda" and not args.no_pipe_graphs)
     opt = MasterSGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
                     weight_decay=args.weight_decay)
     sched = build_schedule(opt, args.epochs, args.warmup_epochs, _lr_steps(args), args.lr_gamma)

@@ -46,6 +46,7 @@ class StepConfig:
     partition: str = "balanced"     # parallel == "pipe": balanced | reference
     checkpoint_segments: int = 0    # activation checkpointing of the block trunk (0 = off)
     dp_graphs: bool = False         # parallel == "dp": replicas as captured hipGraphs (dp_graphs.py)
+    pipe_graphs: bool = True        # parallel == "pipe" on GPU: 1F1B micro-batches on captured stage graphs
     extra: dict = field(default_factory=dict)
 
 
@@ -190,7 +191,8 @@ def build_pipeline_state(cfg: StepConfig, device: torch.device) -> TrainState:
     pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=cfg.micro_batches,
                     schedule=cfg.schedule, device=device, dtype=cfg.dtype,
                     channels_last=cfg.channels_last, partition=cfg.partition,
-                    static_batch=cfg.batch_size)  # every rank knows it: no per-step size message
+                    static_batch=cfg.batch_size,  # every rank knows it: no per-step size message
+                    graphs=cfg.pipe_graphs and device.type == "cuda")
     opt = MasterSGD(pipe.module.parameters(), lr=cfg.lr, momentum=cfg.momentum,
                     weight_decay=cfg.weight_decay)
     x, y = synthetic_batch(cfg, device) if pipe.is_first else (None, None)

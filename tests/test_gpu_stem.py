@@ -126,3 +126,45 @@ def test_stem_halo_kernels_224(n):
     # no-moments forward path too
     y2 = m(x)
     assert torch.equal(y2, y)
+
+
+@pytest.mark.parametrize("shift", [0.0, 2.0])
+def test_stem_bn_backward_folded_into_wgrad(shift):
+    """224 px: the stem's BN backward apply folded into its weight gradient
+    (ops/fused.py _StemBNReLUMaxPoolFn: dW = a dz^T P + b y^T P + c colsum P,
+    no dx pass) == the pool-fused path that materialises dx.  ``shift`` moves
+    the conv outputs' mean away from 0 (the b and c terms then cancel more)."""
+    import copy
+
+    from distributed_model_parallel_amd.ops import fused
+    from distributed_model_parallel_amd.ops.batchnorm import BatchNormAct2d
+    from distributed_model_parallel_amd.ops.pool import MaxPool2d
+    torch.manual_seed(0)
+    conv = StemConv2d(3, 64).cuda().bfloat16().to(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(64, act="relu").cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_(0.0, 0.2)
+    pool = MaxPool2d(3, 2, 1)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = (torch.randn(8, 3, 224, 224, device="cuda") + shift).bfloat16().contiguous(memory_format=torch.channels_last)
+    n0 = fused._STATS_FUSED["stem_bn_relu_maxpool"]
+    y = fused.conv_bn_maxpool(conv, bn, pool, x)
+    assert fused._STATS_FUSED["stem_bn_relu_maxpool"] == n0 + 1, "folded stem did not run"
+    old = fused._FUSE_STEM_WGRAD
+    fused._FUSE_STEM_WGRAD = False
+    try:
+        yr = fused.conv_bn_maxpool(conv2, bn2, pool, x)
+    finally:
+        fused._FUSE_STEM_WGRAD = old
+    assert fused._STATS_FUSED["stem_bn_relu_maxpool"] == n0 + 1
+    torch.testing.assert_close(y.float(), yr.float())
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    for a, b, name in ((conv.weight.grad, conv2.weight.grad, "conv w"), (bn.weight.grad, bn2.weight.grad, "bn w"),
+                       (bn.bias.grad, bn2.bias.grad, "bn b")):
+        err = (a.float() - b.float()).norm() / b.float().norm()
+        # the reference rounds dx to bf16 before its weight gradient; the fold does not
+        assert err < 2e-2, (name, err.item())
+    torch.testing.assert_close(bn.running_var, bn2.running_var)
