@@ -99,6 +99,7 @@ def test_pipeline_world1_bf16_trains():
     assert last < 0.5 * first, (first, last)
 
 
+@pytest.mark.unvalidated
 @pytest.mark.parametrize("dtype,cl", [(torch.float32, False), (torch.bfloat16, True)])
 def test_pipeline_graphed_stage_matches_eager(dtype, cl):
     """Pipeline(graphs=True): the 1F1B micro-batches replay
