@@ -225,6 +225,9 @@ def main() -> int:
         torch.cuda.synchronize()
     if args.phase_times:
         enable_phase_timing()
+        if args.parallel == "dp":
+            from distributed_model_parallel_amd.parallel.data_parallel import reset_host_times
+            reset_host_times()
     from distributed_model_parallel_amd.utils import routes
     routes0 = routes.route_counts()
     bcast0 = getattr(st.wrapped, "buffer_broadcasts", None)
@@ -242,6 +245,14 @@ def main() -> int:
                    sorted(routes.diff(routes.route_counts(), routes0).items())}
     phases = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "calls_per_step": v["calls"] / args.steps}
               for k, v in phase_summary().items()} if args.phase_times else None
+    dp_host = None
+    if args.parallel == "dp" and args.phase_times:
+        from distributed_model_parallel_amd.parallel import data_parallel as _dpm
+        ht = _dpm.HOST_TIMES
+        if ht["applies"]:
+            dp_host = {"apply_ms_per_step": round(ht["apply_ms"] / args.steps, 3),
+                       "replicas": {str(i): {k: round(v / args.steps, 3) for k, v in r.items()}
+                                    for i, r in sorted(ht["replicas"].items())}}
 
     # multi-rank facts the gloo rehearsal (tests/test_bench_multirank_cpu.py) checks:
     # every rank holds the same (rebuilt) bucket layout -- RCCL would deadlock on a
@@ -292,6 +303,7 @@ def main() -> int:
             **({"dp_replicas_per_gpu": args.dp_replicas, "dp_graphs": args.dp_graphs,
                 "dp_device_ids": getattr(st.wrapped, "device_ids", None)} if args.parallel == "dp" else {}),
             **({"phase_ms_per_step": phases} if phases is not None else {}),
+            **({"dp_host_ms_per_step": dp_host} if dp_host is not None else {}),
             "single_rank_comm": bool(args.single_rank_comm),
             "ranks": dist.get_world_size(),
             "rccl_ranks": comm.size if comm.native is not None else None,

@@ -449,7 +449,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def(py::init<>())
       .def("apply", &dmp::ParallelApply::apply, py::arg("modules"), py::arg("inputs"),
            py::arg("kwargs"), py::arg("devices"))
-      .def("num_workers", &dmp::ParallelApply::num_workers);
+      .def("num_workers", &dmp::ParallelApply::num_workers)
+      .def("last_times", &dmp::ParallelApply::last_times);
 
   // ---- DDP reducer ----
   py::class_<dmp::ReduceBackend, std::shared_ptr<dmp::ReduceBackend>>(m, "ReduceBackend");

@@ -5,6 +5,7 @@
 #include <c10/core/GradMode.h>
 #include <c10/hip/HIPGuard.h>
 
+#include <chrono>
 #include <string>
 
 #include "../trace.h"
@@ -73,7 +74,14 @@ void ParallelApply::run_job(Job& job) {
 }
 
 // Runs with the GIL NOT held; takes it only around the Python call.
+namespace {
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
 void ParallelApply::run_job_impl(Job& job) {
+  const auto t0 = std::chrono::steady_clock::now();
   char name[48];
   std::snprintf(name, sizeof(name), "dp.replica%lld", (long long)job.index);
   trace::Range range(name);
@@ -87,9 +95,13 @@ void ParallelApply::run_job_impl(Job& job) {
   at::autocast::set_autocast_enabled(at::kCUDA, job.autocast);
   at::autocast::set_autocast_dtype(at::kCUDA, job.autocast_dtype);
   {
+    const auto tg = std::chrono::steady_clock::now();
     py::gil_scoped_acquire gil;
+    job.gil_wait_ms = ms_since(tg);
+    const auto tc = std::chrono::steady_clock::now();
     try {
       py::object out = job.fn(*job.args, **job.kwargs);
+      job.call_ms = ms_since(tc);
       job.result = py::make_tuple(true, out);
     } catch (py::error_already_set& e) {
       std::string tb;
@@ -110,6 +122,7 @@ void ParallelApply::run_job_impl(Job& job) {
     job.args = py::object();
     job.kwargs = py::object();
   }
+  job.wall_ms = ms_since(t0);
 }
 
 void ParallelApply::worker_main(Worker* w) {
@@ -158,6 +171,7 @@ py::object ParallelApply::apply(const py::list& modules, const py::list& inputs,
     j.autocast_dtype = ac_dtype;
   }
   ensure_workers(n - 1);
+  const auto t_apply = std::chrono::steady_clock::now();
   {
     py::gil_scoped_release nogil;
     {
@@ -175,6 +189,12 @@ py::object ParallelApply::apply(const py::list& modules, const py::list& inputs,
     run_job(jobs[0]);  // replica 0 on the calling thread
     std::unique_lock<std::mutex> lk(done_mu_);
     done_cv_.wait(lk, [this] { return outstanding_ == 0; });
+  }
+  last_times_.assign(1, ms_since(t_apply));
+  for (auto& j : jobs) {
+    last_times_.push_back(j.wall_ms);
+    last_times_.push_back(j.gil_wait_ms);
+    last_times_.push_back(j.call_ms);
   }
   py::list out;
   for (auto& j : jobs) out.append(j.result);

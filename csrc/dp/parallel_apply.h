@@ -40,6 +40,11 @@ class ParallelApply {
   pybind11::object apply(const pybind11::list& modules, const pybind11::list& inputs,
                        const pybind11::list& kwargs, const std::vector<int64_t>& devices);
   int64_t num_workers() const { return (int64_t)workers_.size(); }
+  // Host-time breakdown of the last apply(): [apply wall ms, then per replica
+  // (wall ms, ms waiting for the GIL before its module call started,
+  // ms inside the module call)] -- the "threshing" of Readme.md:10 made
+  // visible: replicas that serialise on the GIL show wall ~ sum of the calls.
+  std::vector<double> last_times() const { return last_times_; }
 
  private:
   struct Job {
@@ -51,6 +56,7 @@ class ParallelApply {
     bool autocast = false;
     at::ScalarType autocast_dtype = at::kBFloat16;
     pybind11::object result;  // (ok, value)
+    double wall_ms = 0, gil_wait_ms = 0, call_ms = 0;
   };
   struct Worker {
     std::thread thread;
@@ -70,6 +76,7 @@ class ParallelApply {
   std::mutex done_mu_;
   std::condition_variable done_cv_;
   int64_t outstanding_ = 0;
+  std::vector<double> last_times_;
 };
 
 }  // namespace dmp

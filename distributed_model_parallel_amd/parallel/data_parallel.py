@@ -357,6 +357,28 @@ def _reraise(i: int, payload) -> None:
     raise exc
 
 
+# Host-time breakdown of the native launcher's applies:
+# totals since the last reset -- apply wall ms, and per replica index the wall
+# ms, the ms spent waiting for the GIL before its module call, and the call ms.
+HOST_TIMES: Dict[str, Any] = {"applies": 0, "apply_ms": 0.0, "replicas": {}}
+
+
+def _record_host_times(t: Sequence[float]) -> None:
+    if not t:
+        return
+    HOST_TIMES["applies"] += 1
+    HOST_TIMES["apply_ms"] += t[0]
+    for i in range((len(t) - 1) // 3):
+        r = HOST_TIMES["replicas"].setdefault(i, {"wall_ms": 0.0, "gil_wait_ms": 0.0, "call_ms": 0.0})
+        r["wall_ms"] += t[1 + 3 * i]
+        r["gil_wait_ms"] += t[2 + 3 * i]
+        r["call_ms"] += t[3 + 3 * i]
+
+
+def reset_host_times() -> None:
+    HOST_TIMES.update(applies=0, apply_ms=0.0, replicas={})
+
+
 def parallel_apply(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=None,
                    devices: Optional[Sequence] = None) -> List[Any]:
     """Run modules[i](*inputs[i], **kwargs_tup[i]) on devices[i] concurrently.
@@ -381,6 +403,7 @@ def parallel_apply(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=No
         res = launcher.apply(list(modules), ins, [dict(k) for k in kwargs_tup], devs)
         if res is None:  # launcher busy (another thread / a nested DataParallel): own threads
             return _parallel_apply_threads(modules, inputs, kwargs_tup, devices)
+        _record_host_times(launcher.last_times())
         outs = []
         for i, (ok, val) in enumerate(res):
             if not ok:

@@ -388,3 +388,21 @@ def test_replicas_with_activation_checkpointing_stay_bound_for_recompute():
         ref(x).pow(2).sum().backward()
         for a, p in zip(g, m.parameters()):
             torch.testing.assert_close(a, p.grad, atol=1e-6, rtol=1e-5)
+
+
+def test_native_launcher_reports_host_time_breakdown():
+    """the eager DataParallel path's host time per replica
+    (wall, GIL wait before the module call, the call itself) is recorded by
+    the C++ launcher for every apply (bench.py --phase-times reports it)."""
+    from distributed_model_parallel_amd.parallel import data_parallel as dpm
+    if dpm._native_launcher() is None:
+        pytest.skip("native launcher not built")
+    dpm.reset_host_times()
+    mods = [nn.Linear(8, 8) for _ in range(3)]
+    for _ in range(2):
+        parallel_apply(mods, [(torch.zeros(4, 8),)] * 3, devices=[None] * 3)
+    ht = dpm.HOST_TIMES
+    assert ht["applies"] == 2 and ht["apply_ms"] > 0
+    assert sorted(ht["replicas"]) == [0, 1, 2]
+    for r in ht["replicas"].values():
+        assert r["wall_ms"] >= r["call_ms"] > 0 and r["gil_wait_ms"] >= 0
