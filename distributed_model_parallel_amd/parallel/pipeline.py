@@ -569,9 +569,11 @@ class Pipeline:
 
     # 1F1B on captured stage graphs ------------------------------------------------------
     def _graphed_ok(self, sizes) -> bool:
+        # on CPU the same slot schedule runs on eager stand-ins of the graphs
+        # (_EagerGraph): the gloo tests exercise it at any world size
         return (self.graphs and self.schedule == "1f1b" and self.loss_on == "last"
-                and self.device.type == "cuda" and len(set(sizes)) == 1
-                and not torch.cuda.is_current_stream_capturing())
+                and len(set(sizes)) == 1
+                and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()))
 
     def _run_1f1b_graphed(self, xs, tgts, sizes) -> torch.Tensor:
         M = len(sizes)
@@ -686,6 +688,16 @@ class Pipeline:
 
 
 
+class _EagerGraph:
+    """CPU stand-in for a captured graph: ``replay()`` runs the function."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def replay(self) -> None:
+        self.fn()
+
+
 class _StageGraphs:
     """``depth`` captured copies (slots) of one stage's forward and backward for
     micro-batch size ``mb`` (``Pipeline(graphs=True)``).
@@ -723,8 +735,36 @@ class _StageGraphs:
         self.outs: List[Optional[torch.Tensor]] = []
         self.fwd: List[torch.cuda.CUDAGraph] = []
         self.bwd: List[torch.cuda.CUDAGraph] = []
-        self.stream = torch.cuda.Stream(device=dev)
-        self._capture()
+        if dev.type == "cuda":
+            self.stream = torch.cuda.Stream(device=dev)
+            self._capture()
+        else:
+            self._eager_slots()
+
+    def _eager_slots(self) -> None:
+        """CPU: the replays re-run forward / backward eagerly with the same static
+        buffers and in-place semantics (the input gradient is replaced, the
+        parameter gradients accumulate, the last stage's stats accumulate)."""
+        live = [None] * self.depth
+
+        def fwd(k):
+            out = self._forward(k)
+            live[k] = out
+            if self.outs[k] is not None:
+                with torch.no_grad():
+                    self.outs[k].copy_(out)
+
+        def bwd(k):
+            self.inputs[k].grad = None
+            self._backward(k, live[k])
+            live[k] = None
+
+        shape = self.pipe._out_shape(self.mb)
+        for k in range(self.depth):
+            self.fwd.append(_EagerGraph(lambda k=k: fwd(k)))
+            self.bwd.append(_EagerGraph(lambda k=k: bwd(k)))
+            self.outs.append(None if self.pipe.is_last else
+                             torch.zeros(shape, dtype=self.pipe.dtype, device=self.pipe.device))
 
     def _forward(self, k: int) -> torch.Tensor:
         pipe = self.pipe
