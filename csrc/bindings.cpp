@@ -218,25 +218,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X-native runtime: RCCL communicator, DDP reducer, HIP kernels (gfx950)";
 
   // ---- batch norm ----
-  m.def("bn_local_moments", &dmp::bn_local_moments);
+  m.def("bn_local_moments", &dmp::bn_local_moments,
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_forward_apply", &dmp::bn_forward_apply, py::arg("x"), py::arg("sums"), py::arg("weight"),
         py::arg("bias"), py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"),
         py::arg("eps"), py::arg("residual"), py::arg("relu"), py::arg("C"),
         py::arg("num_batches_tracked") = py::none(), py::arg("out_moments") = false,
-        py::arg("clip") = INFINITY);
+        py::arg("clip") = INFINITY,
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_eval_apply", &dmp::bn_eval_apply, py::arg("x"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("weight"), py::arg("bias"), py::arg("eps"), py::arg("residual"),
-        py::arg("relu"), py::arg("C"), py::arg("clip") = INFINITY);
+        py::arg("relu"), py::arg("C"), py::arg("clip") = INFINITY,
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_finalize", &dmp::bn_finalize, py::arg("sums"), py::arg("weight"), py::arg("bias"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
-        py::arg("C"), py::arg("num_batches_tracked") = py::none());
+        py::arg("C"), py::arg("num_batches_tracked") = py::none(),
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_backward_moments", &dmp::bn_backward_moments, py::arg("dy"), py::arg("x"), py::arg("y"),
         py::arg("mean"), py::arg("relu"), py::arg("C"), py::arg("weight") = py::none(),
-        py::arg("bias") = py::none(), py::arg("invstd") = py::none(), py::arg("clip") = INFINITY);
+        py::arg("bias") = py::none(), py::arg("invstd") = py::none(), py::arg("clip") = INFINITY,
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_backward_apply", &dmp::bn_backward_apply, py::arg("dy"), py::arg("x"), py::arg("y"),
         py::arg("sums"), py::arg("count"), py::arg("weight"), py::arg("mean"), py::arg("invstd"),
         py::arg("training"), py::arg("relu"), py::arg("want_dres"), py::arg("C"),
-        py::arg("bias") = py::none(), py::arg("clip") = INFINITY);
+        py::arg("bias") = py::none(), py::arg("clip") = INFINITY,
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- MFMA GEMM (1x1 conv) with fused BN prologue/epilogues ----
   m.def("gemm_nt", &dmp::gemm_nt, py::arg("A"), py::arg("B"), py::arg("pro_scale") = py::none(),
@@ -244,21 +250,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
         py::arg("residual") = py::none(), py::arg("relu") = false,
         py::arg("a_map") = std::vector<int64_t>{}, py::arg("c_map") = std::vector<int64_t>{},
-        py::arg("a2") = py::none(), py::arg("a2_map") = std::vector<int64_t>{});
+        py::arg("a2") = py::none(), py::arg("a2_map") = std::vector<int64_t>{},
+        py::call_guard<py::gil_scoped_release>());
 
   m.def("cross_entropy_fwd", &dmp::cross_entropy_fwd, py::arg("x"), py::arg("target"),
-        py::arg("ignore_index") = -100);
+        py::arg("ignore_index") = -100,
+        py::call_guard<py::gil_scoped_release>());
   m.def("cross_entropy_bwd", &dmp::cross_entropy_bwd, py::arg("grad"), py::arg("x"), py::arg("target"),
-        py::arg("lse"), py::arg("stats"), py::arg("ignore_index") = -100);
+        py::arg("lse"), py::arg("stats"), py::arg("ignore_index") = -100,
+        py::call_guard<py::gil_scoped_release>());
   m.def("gemm_nt_bnbwd", &dmp::gemm_nt_bnbwd, py::arg("A"), py::arg("B"), py::arg("residual"),
         py::arg("bn_x"), py::arg("bn_y"), py::arg("mean"), py::arg("invstd"), py::arg("weight"),
         py::arg("bias"), py::arg("res_map") = std::vector<int64_t>{}, py::arg("a2") = py::none(),
-        py::arg("ebias") = py::none(), py::arg("a2_map") = std::vector<int64_t>{});
+        py::arg("ebias") = py::none(), py::arg("a2_map") = std::vector<int64_t>{},
+        py::call_guard<py::gil_scoped_release>());
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none(), py::arg("a_mapped") = false,
-        "C = A^T B (weight gradient); b_map reads B's rows through a strided map, a_mapped A's too (Gram of a sample)");
+        "C = A^T B (weight gradient); b_map reads B's rows through a strided map, a_mapped A's too (Gram of a sample)",
+        py::call_guard<py::gil_scoped_release>());
 
   m.def("set_tn_wide", &dmp::set_tn_wide, py::arg("on"),
         "128 x 256 TN tiles for deep weight gradients (default on)");
@@ -276,50 +287,65 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("transposed") = false, py::arg("pro_scale") = py::none(),
         py::arg("pro_shift") = py::none(), py::arg("mode") = "store",
         py::arg("epi_scale") = py::none(), py::arg("epi_shift") = py::none(),
-        py::arg("residual") = py::none(), py::arg("relu") = false, py::arg("kc") = 0);
+        py::arg("residual") = py::none(), py::arg("relu") = false, py::arg("kc") = 0,
+        py::call_guard<py::gil_scoped_release>());
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
-        py::arg("kc") = 0);
+        py::arg("kc") = 0,
+        py::call_guard<py::gil_scoped_release>());
   m.def("maxpool2d_bn_forward", &dmp::maxpool2d_bn_forward, py::arg("x"), py::arg("scale"),
-        py::arg("shift"), py::arg("k"), py::arg("s"), py::arg("p"));
+        py::arg("shift"), py::arg("k"), py::arg("s"), py::arg("p"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("maxpool2d_bn_backward", &dmp::maxpool2d_bn_backward, py::arg("dy"), py::arg("idx"), py::arg("x"),
-        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("k"), py::arg("s"), py::arg("p"));
-  m.def("pad_channels16", &dmp::pad_channels16, py::arg("x"), py::arg("pad"), py::arg("extra_w") = 0);
-  m.def("space_to_depth2", &dmp::space_to_depth2, py::arg("x"), py::arg("pad"), py::arg("out_channels") = 16);
+        py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("k"), py::arg("s"), py::arg("p"),
+        py::call_guard<py::gil_scoped_release>());
+  m.def("pad_channels16", &dmp::pad_channels16, py::arg("x"), py::arg("pad"), py::arg("extra_w") = 0,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("space_to_depth2", &dmp::space_to_depth2, py::arg("x"), py::arg("pad"), py::arg("out_channels") = 16,
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- large-tile transformer GEMM with fused bias / GELU / residual epilogues ----
   m.def("gemm_xl", &dmp::gemm_xl, py::arg("A"), py::arg("B"), py::arg("mode") = "store",
         py::arg("bias") = py::none(), py::arg("aux") = py::none(),
-        py::arg("residual") = py::none(), py::arg("out") = py::none());
+        py::arg("residual") = py::none(), py::arg("out") = py::none(),
+        py::call_guard<py::gil_scoped_release>());
   m.def("conv_xl", &dmp::conv_xl, py::arg("x"), py::arg("wmat"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("mode") = "moments",
         py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
         py::arg("bias") = py::none(),
-        "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues");
+        "Implicit-GEMM conv (NHWC gather) on the 256x256 ping-pong MFMA kernel with conv epilogues",
+        py::call_guard<py::gil_scoped_release>());
   m.def("stem_halo_supported", &dmp::stem_halo_supported);
   m.def("stem_halo_fwd", &dmp::stem_halo_fwd, py::arg("s"), py::arg("wm"), py::arg("ho"), py::arg("moments") = false,
-        "ResNet stem (s2d 4x4 conv, 16 -> 64 ch, Wo = 112) forward: halo-tiled, weights in VGPRs");
+        "ResNet stem (s2d 4x4 conv, 16 -> 64 ch, Wo = 112) forward: halo-tiled, weights in VGPRs",
+        py::call_guard<py::gil_scoped_release>());
   m.def("stem_halo_wgrad", &dmp::stem_halo_wgrad, py::arg("dy"), py::arg("s"), py::arg("ho"), py::arg("out_dtype"),
-        "ResNet stem weight gradient [64, 256]: halo-tiled, dW in VGPRs");
+        "ResNet stem weight gradient [64, 256]: halo-tiled, dW in VGPRs",
+        py::call_guard<py::gil_scoped_release>());
   m.def("wgrad3x3", &dmp::wgrad3x3, py::arg("dy"), py::arg("x"), py::arg("stride") = 1,
-        "dW [C, C, 3, 3] (channels_last) of a 3x3/s1/p1 conv: persistent halo-tiled MFMA kernel");
+        "dW [C, C, 3, 3] (channels_last) of a 3x3/s1/p1 conv: persistent halo-tiled MFMA kernel",
+        py::call_guard<py::gil_scoped_release>());
   m.def("wgrad3x3_supported", &dmp::wgrad3x3_supported, py::arg("C"), py::arg("Ho"), py::arg("Wo"),
         py::arg("stride") = 1);
   m.def("set_wgrad3x3_waves", &dmp::set_wgrad3x3_waves);
   m.def("conv3x3_c64", &dmp::conv3x3_c64, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
         "3x3/s1/p1 64->64-channel conv (W = 56) on the persistent halo-tiled MFMA kernel; "
-        "returns (y [N*H*W, 64], fp64 moments [129] or empty)");
+        "returns (y [N*H*W, 64], fp64 moments [129] or empty)",
+        py::call_guard<py::gil_scoped_release>());
   m.def("conv3x3_c128", &dmp::conv3x3_c128, py::arg("x"), py::arg("wmat"), py::arg("moments") = false,
         "3x3/s1/p1 128->128-channel conv (W = 28, H % 4 == 0) on the persistent halo-tiled MFMA kernel "
-        "(Cout split over grid halves, K split over wave pairs); returns (y [N*H*W, 128], fp64 moments [257] or empty)");
+        "(Cout split over grid halves, K split over wave pairs); returns (y [N*H*W, 128], fp64 moments [257] or empty)",
+        py::call_guard<py::gil_scoped_release>());
   m.def("conv3x3_c128_dgrad_s2", &dmp::conv3x3_c128_dgrad_s2, py::arg("dy"), py::arg("wt"),
         "data gradient of a 3x3/s2/p1 128->128 conv (dy 28 wide) as its four stride phases on the halo kernel; "
-        "wt = W.permute(1, 2, 3, 0) as [128, 1152]; returns dx [N*2H*56, 128]");
+        "wt = W.permute(1, 2, 3, 0) as [128, 1152]; returns dx [N*2H*56, 128]",
+        py::call_guard<py::gil_scoped_release>());
   m.def("conv3x3_c128_supported", &dmp::conv3x3_c128_supported, py::arg("C"), py::arg("H"), py::arg("W"));
   m.def("conv_xl_dgrad_s2", &dmp::conv_xl_dgrad_s2, py::arg("dy"), py::arg("wph"), py::arg("hi"), py::arg("wi"),
         "data gradient of a 3x3/s2/p1 conv as four stride-phase implicit GEMMs on the ping-pong kernel; "
-        "returns dx [N*hi*wi, Cin]");
+        "returns dx [N*hi*wi, Cin]",
+        py::call_guard<py::gil_scoped_release>());
   m.def("set_bn_streaming", &dmp::set_bn_streaming, py::arg("on"),
         "A/B: non-temporal streaming in the BN apply passes over > 256 MB tensors (default on)");
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
@@ -329,11 +355,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_tn_xl_ring", &dmp::set_tn_xl_ring, py::arg("ring"),
         "gemm_tn_xl main loop: 0 = two tile buffers, 1 = the 10-slot LDS unit ring");
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
-        "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M");
+        "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M",
+        py::call_guard<py::gil_scoped_release>());
   m.def("conv_wgrad_xl", &dmp::conv_wgrad_xl, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
-        "kh x kw conv weight gradient (tap gather) on the ping-pong TN kernel; Cin % 256 == 0");
-  m.def("gemm_xl_dgelu_bgrad", &dmp::gemm_xl_dgelu_bgrad, py::arg("A"), py::arg("B"), py::arg("aux"));
+        "kh x kw conv weight gradient (tap gather) on the ping-pong TN kernel; Cin % 256 == 0",
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gemm_xl_dgelu_bgrad", &dmp::gemm_xl_dgelu_bgrad, py::arg("A"), py::arg("B"), py::arg("aux"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("gemm_xl_conv", &dmp::gemm_xl_conv, py::arg("A"), py::arg("B"), py::arg("mode"),
         py::arg("residual") = py::none(), py::arg("bn_x") = py::none(), py::arg("bn_y") = py::none(),
         py::arg("mean") = py::none(), py::arg("invstd") = py::none(), py::arg("weight") = py::none(),
@@ -341,7 +370,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a2") = py::none(), py::arg("ebias") = py::none(), py::arg("scale") = py::none(),
         py::arg("shift") = py::none(), py::arg("relu") = false, py::arg("a2_map") = std::vector<int64_t>{},
         "wide 1x1-conv GEMM with conv epilogues: moments | add | bnbwd | affine (scale, shift, residual, relu); "
-        "a2: second A source concatenated along K; ebias: bnbwd per-column constant");
+        "a2: second A source concatenated along K; ebias: bnbwd per-column constant",
+        py::call_guard<py::gil_scoped_release>());
   m.def("get_gemm_xl_pipe", &dmp::get_gemm_xl_pipe);
   m.def("set_gemm_xl_x2", &dmp::set_gemm_xl_x2, py::arg("mode"),
         "conv-epilogue GEMMs on the two-blocks-per-CU 256x128 kernel: 0 off, 1 where N % 256 != 0, 2 always");
@@ -358,18 +388,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // ---- BN folded through an expanding 1x1 conv (ops/bn_fold.py) ----
   m.def("bn_fold_supported", &dmp::bn_fold_supported, py::arg("cout"), py::arg("cin"));
   m.def("bn_fold_fwd", &dmp::bn_fold_fwd, py::arg("W"), py::arg("G"), py::arg("asums"),
-        "(sums fp64 [2Cout+1], WG fp32 [Cout, Cin]) of y = a W^T from G = a^T a and colsum(a)");
+        "(sums fp64 [2Cout+1], WG fp32 [Cout, Cin]) of y = a W^T from G = a^T a and colsum(a)",
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_fold_bwd_sums", &dmp::bn_fold_bwd_sums, py::arg("D"), py::arg("W"), py::arg("sdz"), py::arg("mean"),
-        "local fp64 [2Cout] = (sum dz, sum dz*(y - mean)) from D = dz^T a");
+        "local fp64 [2Cout] = (sum dz, sum dz*(y - mean)) from D = dz^T a",
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_fold_bwd_coef", &dmp::bn_fold_bwd_coef, py::arg("sums"), py::arg("local"), py::arg("count"),
         py::arg("invstd"), py::arg("mean"), py::arg("gamma"), py::arg("D"), py::arg("WG"), py::arg("s"),
-        py::arg("W"), "(dW, dgamma, dbeta, Bm = [(al o W)^T | W^T diag(be) W], ebias = c^T W)");
+        py::arg("W"), "(dW, dgamma, dbeta, Bm = [(al o W)^T | W^T diag(be) W], ebias = c^T W)",
+        py::call_guard<py::gil_scoped_release>());
 
-  m.def("bn_fold_relu_mask", &dmp::bn_fold_relu_mask, py::arg("dy"), py::arg("y"));
+  m.def("bn_fold_relu_mask", &dmp::bn_fold_relu_mask, py::arg("dy"), py::arg("y"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_fold_colsum", &dmp::bn_fold_colsum, py::arg("x"), py::arg("map") = std::vector<int64_t>{},
-        "fp64 [2C+1] (colsum, colsum of squares, rows) of x's rows sampled through a strided map");
+        "fp64 [2C+1] (colsum, colsum of squares, rows) of x's rows sampled through a strided map",
+        py::call_guard<py::gil_scoped_release>());
   m.def("bn_fold_scale_concat", &dmp::bn_fold_scale_concat, py::arg("W3"), py::arg("s3"), py::arg("t3"),
-        py::arg("Wd"), py::arg("sd"), py::arg("td"), "([s3 o W3 | sd o Wd] bf16, t3 + td)");
+        py::arg("Wd"), py::arg("sd"), py::arg("td"), "([s3 o W3 | sd o Wd] bf16, t3 + td)",
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- fused self-attention on packed qkv (ViT) ----
   m.def("attention_supported", &dmp::attention_supported);
@@ -381,40 +417,56 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "attention kernels: fwd 0 = one workgroup per (batch, head), 1 = persistent with next-head prefetch, "
         "2 = 8-wave per head; bwd 0 = per head, 1 = persistent with prefetch");
   m.def("attention_forward", &dmp::attention_forward, py::arg("qkv"), py::arg("B"), py::arg("S"),
-        py::arg("H"), py::arg("scale"));
+        py::arg("H"), py::arg("scale"),
+        py::call_guard<py::gil_scoped_release>());
   m.def("attention_backward", &dmp::attention_backward, py::arg("dout"), py::arg("qkv"), py::arg("o"),
-        py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("scale"));
+        py::arg("lse"), py::arg("B"), py::arg("S"), py::arg("H"), py::arg("scale"),
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- Linear side passes: bias gradient, GELU backward + bias gradient ----
   m.def("colsum_supported", &dmp::colsum_supported);
-  m.def("bias_grad", &dmp::bias_grad, py::arg("dy"), py::arg("out_dtype"));
-  m.def("gelu_bwd_bias_grad", &dmp::gelu_bwd_bias_grad, py::arg("dy"), py::arg("h"), py::arg("out_dtype"));
+  m.def("bias_grad", &dmp::bias_grad, py::arg("dy"), py::arg("out_dtype"),
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gelu_bwd_bias_grad", &dmp::gelu_bwd_bias_grad, py::arg("dy"), py::arg("h"), py::arg("out_dtype"),
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- LayerNorm (last dim) ----
-  m.def("layernorm_forward", &dmp::layernorm_forward);
+  m.def("layernorm_forward", &dmp::layernorm_forward,
+        py::call_guard<py::gil_scoped_release>());
   m.def("layernorm_backward", &dmp::layernorm_backward, py::arg("dy"), py::arg("x"), py::arg("w"),
         py::arg("mean"), py::arg("rstd"), py::arg("D"), py::arg("param_dtype"),
-        py::arg("dres") = py::none());
+        py::arg("dres") = py::none(),
+        py::call_guard<py::gil_scoped_release>());
   m.def("layernorm_supported", &dmp::layernorm_supported);
 
   // ---- NHWC max pooling with byte argmax ----
-  m.def("maxpool2d_forward", &dmp::maxpool2d_forward);
-  m.def("maxpool2d_backward", &dmp::maxpool2d_backward);
-  m.def("global_avgpool_backward", &dmp::global_avgpool_backward);
+  m.def("maxpool2d_forward", &dmp::maxpool2d_forward,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("maxpool2d_backward", &dmp::maxpool2d_backward,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("global_avgpool_backward", &dmp::global_avgpool_backward,
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- depthwise 3x3 (NHWC) ----
   m.def("dwconv3x3_forward", &dmp::dwconv3x3_forward, py::arg("x"), py::arg("w"),
-        py::arg("stride"), py::arg("moments") = false);
-  m.def("dwconv3x3_dgrad", &dmp::dwconv3x3_dgrad);
-  m.def("dwconv3x3_wgrad", &dmp::dwconv3x3_wgrad);
+        py::arg("stride"), py::arg("moments") = false,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("dwconv3x3_dgrad", &dmp::dwconv3x3_dgrad,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("dwconv3x3_wgrad", &dmp::dwconv3x3_wgrad,
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- optimizer ----
-  m.def("sgd_flat_step", &dmp::sgd_flat_step);
+  m.def("sgd_flat_step", &dmp::sgd_flat_step,
+        py::call_guard<py::gil_scoped_release>());
 
   // ---- coalesced movement ----
-  m.def("multi_copy", &dmp::multi_copy);
-  m.def("reduce_add_into", &dmp::reduce_add_into);
-  m.def("gather_slabs", &dmp::gather_slabs);
+  m.def("multi_copy", &dmp::multi_copy,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("reduce_add_into", &dmp::reduce_add_into,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gather_slabs", &dmp::gather_slabs,
+        py::call_guard<py::gil_scoped_release>());
   m.def("enable_peer_access", &dmp::enable_peer_access);
 
   // ---- RCCL ----
