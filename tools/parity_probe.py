@@ -49,7 +49,7 @@ def grads_native(m0, x, y, tn_all: bool = True):
         loss.backward()
     finally:
         conv1x1._TN_XL_MIN_ROWS = old
-    return float(loss), {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    return float(loss.detach()), {n: p.grad.float().clone() for n, p in m.named_parameters()}
 
 
 def grads_stock(m0, x, y, dtype=torch.float32):
@@ -68,8 +68,13 @@ def compare(a, b):
         cs.append(((ga @ gb).item() / den if den > 0 else 1.0, n))
     cs.sort()
     vals = torch.tensor([c for c, _ in cs])
+    conv = torch.tensor([c for c, n in cs if n.endswith("weight") and a[n].dim() == 4])
+    fa = torch.cat([a[n].flatten() for n in a])
+    fb = torch.cat([b[n].flatten() for n in a])
+    whole = ((fa @ fb) / (fa.norm() * fb.norm()).clamp_min(1e-30)).item()
     return {"median": vals.median().item(), "p05": vals.quantile(0.05).item(), "min": cs[0][0],
-            "worst": cs[0][1]}
+            "worst": cs[0][1], "conv_median": conv.median().item(), "conv_min": conv.min().item(),
+            "whole": whole}
 
 
 def main() -> int:
@@ -96,10 +101,12 @@ def main() -> int:
                     ("native vs native (run 2)", compare(gn, gn2), ln, ln2),
                     ("stock fp32 vs fp32, input +1 ulp", compare(g32p, g32), l32p, l32)]
             print(f"\n## gamma {gamma}, batch {batch}, {a.size} px\n")
-            print("| pair | median cos | p05 | min | worst parameter | loss a | loss b | rel |")
-            print("|---|---|---|---|---|---|---|---|")
+            print("| pair | median cos | p05 | min | worst parameter | conv median | conv min | whole-model cos "
+                  "| loss a | loss b | rel |")
+            print("|---|---|---|---|---|---|---|---|---|---|---|")
             for name, c, la, lb in rows:
                 print(f"| {name} | {c['median']:.5f} | {c['p05']:.5f} | {c['min']:.5f} | {c['worst']} | "
+                      f"{c['conv_median']:.5f} | {c['conv_min']:.5f} | {c['whole']:.5f} | "
                       f"{la:.5f} | {lb:.5f} | {abs(la - lb) / abs(lb):.2e} |", flush=True)
             torch.cuda.empty_cache()
     return 0

@@ -48,6 +48,8 @@ def main() -> int:
         ks.append((s, e, r["Kernel_Name"], q, st))
     ks.sort()
     marks = [i for i, k in enumerate(ks) if a.marker in k[2]]
+    # one optimizer launch per dtype group: keep the first of each run of markers
+    marks = [m for j, m in enumerate(marks) if j == 0 or m - marks[j - 1] > 8]
     if len(marks) < 2:
         print("fewer than two step markers", file=sys.stderr)
         return 1
