@@ -21,6 +21,7 @@ import os, sys, torch
 sys.path.insert(0, os.environ["ROOT"])
 from distributed_model_parallel_amd import _native
 from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed
+from distributed_model_parallel_amd.ops import wgrad_stream
 from distributed_model_parallel_amd.models import build_model
 from distributed_model_parallel_amd.parallel.distributed import DistributedDataParallel
 from distributed_model_parallel_amd.ops import wgrad_stream
@@ -28,6 +29,7 @@ from distributed_model_parallel_amd.ops.loss import cross_entropy
 from distributed_model_parallel_amd.utils.precision import cast_model
 env = init_distributed()
 dev = env.device
+wgrad_stream.ENABLED = True  # off by default (measured no faster); the mechanism must still be exact
 C = _native.require("test")
 import torch.nn as nn
 from distributed_model_parallel_amd.ops.conv1x1 import Conv1x1
