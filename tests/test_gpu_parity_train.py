@@ -4,13 +4,19 @@ epilogues, the stride-phase data gradients and every other route the
 headline bench takes, against stock PyTorch fp32 on the same weights and the
 same input.
 
-Regime: 224 px, batch 64, residual branches tamed (each bottleneck's last BN
-gamma x 0.25, as in test_gpu_checkpointing.py) -- a random-init ResNet-50 at
-tiny batches is chaotic in bf16 (profiles/README.md finding 4), which made the
-earlier whole-model checks loose.  The bounds sit next to the measured noise
-floors (tools/parity_probe.py; profiles/parity_r5.md): stock bf16 vs fp32,
-native vs native (a second run: atomic order), and fp32 vs fp32 with the input
-moved by one ulp."""
+Regime: 224 px, batch 128, residual branches tamed (each bottleneck's last BN
+gamma x 0.1; test_gpu_checkpointing.py uses 0.25) -- a random-init ResNet-50
+at small batches is chaotic in bf16 (profiles/README.md finding 4).
+
+What bf16 itself costs is measured, not assumed (tools/parity_probe.py,
+profiles/parity_r5.md): STOCK PyTorch in bf16 lands at a per-parameter
+gradient cosine of 0.971 median / 0.947 min from fp32 in this regime (0.90 /
+0.83 at gamma 0.25, batch 64; 0.19 at gamma 1), while fp32 vs fp32 with the
+input moved by one ulp stays at 0.99999.  So the bound is relative: the
+native bf16 step must be at least as close to fp32 as stock bf16 is (the
+native kernels measured 0.974 / 0.953, whole-model cosine 0.995), and a
+second native run must agree with the first (0.99 median: the BN moments'
+cross-block fp64 atomics land in run-dependent order at this batch)."""
 import copy
 import os
 import sys
@@ -23,7 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 pytestmark = [pytest.mark.gpu, pytest.mark.unvalidated]
 
-BATCH, SIZE, GAMMA, NCLS = 64, 224, 0.25, 100
+BATCH, SIZE, GAMMA, NCLS = 128, 224, 0.1, 100
 
 
 @pytest.fixture(scope="module")
@@ -52,16 +58,19 @@ def test_native_train_gradients_match_fp32(runs):
     c = pp.compare(gn, g32)
     floor = pp.compare(runs["bf16"][1], g32)  # what bf16 itself costs, stock kernels
     print("native vs fp32", c, "stock bf16 vs fp32", floor)
-    assert c["median"] >= 0.99, (c, floor)
-    assert c["min"] >= 0.95, (c, floor)
-    assert abs(ln - l32) <= 0.01 * abs(l32), (ln, l32)
+    assert c["median"] >= floor["median"] - 0.005, (c, floor)
+    assert c["p05"] >= floor["p05"] - 0.01, (c, floor)
+    assert c["min"] >= floor["min"] - 0.02, (c, floor)
+    assert c["conv_median"] >= floor["conv_median"] - 0.005, (c, floor)
+    assert c["whole"] >= 0.99 and c["whole"] >= floor["whole"] - 0.002, (c, floor)
+    assert abs(ln - l32) <= 1e-3 * abs(l32), (ln, l32)
 
 
 def test_native_train_runs_are_consistent(runs):
     pp = runs["pp"]
     c = pp.compare(runs["native"][1], runs["native2"][1])
     print("native vs native", c)
-    assert c["median"] >= 0.999 and c["min"] >= 0.99, c
+    assert c["median"] >= 0.98 and c["min"] >= 0.95 and c["whole"] >= 0.995, c
 
 
 def test_parity_run_takes_the_bench_routes(runs):
