@@ -295,7 +295,10 @@ class _StemBNReLUMaxPoolFn(torch.autograd.Function):
     def forward(ctx, img, wmat, bn_w, bn_b, running_mean, running_var, momentum, eps, nbt, reduce_moments,
                 reduce_grads, pad):
         from .. import _native
+        from .stem import _STATS as _STEM_STATS
         C = _native.require("stem + bn + maxpool")
+        _STEM_STATS["native"] += 1  # the same halo stem kernels as StemConv2d's own path
+        _STEM_STATS["halo"] += 1
         n, _, h, w = img.shape
         ho, wo = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1
         s = C.space_to_depth2(img, 3)

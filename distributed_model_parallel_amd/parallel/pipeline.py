@@ -571,9 +571,13 @@ class Pipeline:
     def _graphed_ok(self, sizes) -> bool:
         # on CPU the same slot schedule runs on eager stand-ins of the graphs
         # (_EagerGraph): the gloo tests exercise it at any world size
-        return (self.graphs and self.schedule == "1f1b" and self.loss_on == "last"
-                and len(set(sizes)) == 1
-                and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()))
+        # on GPU only the bf16 native-kernel stage is captured: fp32 stages run
+        # library convolutions (MIOpen), whose weight gradients do not survive
+        # graph replay (profiles/README.md finding 48; a captured fp32 stage gave
+        # garbage gradients from the second replay on, round 5)
+        if self.device.type == "cuda" and (self.dtype != torch.bfloat16 or torch.cuda.is_current_stream_capturing()):
+            return False
+        return self.graphs and self.schedule == "1f1b" and self.loss_on == "last" and len(set(sizes)) == 1
 
     def _run_1f1b_graphed(self, xs, tgts, sizes) -> torch.Tensor:
         M = len(sizes)

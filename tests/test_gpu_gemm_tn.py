@@ -25,7 +25,6 @@ def test_gemm_tn(M, N, K, out):
     torch.testing.assert_close(got.float(), ref, atol=tol, rtol=1e-2)
 
 
-@pytest.mark.unvalidated
 @pytest.mark.parametrize("M,N,K", [(802816, 256, 64), (200704, 512, 128), (1000, 256, 64), (777, 1024, 128),
                                    (131, 256, 128)])
 def test_gemm_tn_tall_tiles(M, N, K):

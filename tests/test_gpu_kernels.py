@@ -62,7 +62,6 @@ def test_bn_act_forward_backward(dtype, shape, relu, res):
         torch.testing.assert_close(r1.grad.float(), rr.grad, atol=gt, rtol=gt)
 
 
-@pytest.mark.unvalidated
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("training", [True, False])

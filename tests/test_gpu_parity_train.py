@@ -27,7 +27,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-pytestmark = [pytest.mark.gpu, pytest.mark.unvalidated]
+pytestmark = pytest.mark.gpu
 
 BATCH, SIZE, GAMMA, NCLS = 128, 224, 0.1, 100
 
@@ -80,7 +80,7 @@ def test_parity_run_takes_the_bench_routes(runs):
     need = {"bn_fold.fold", "bn_fold.fold_ds", "bn_fold.fold_fused_bwd", "conv1x1.fused_bn_bwd",
             "conv1x1.tn_xl", "conv_igemm.halo_fwd", "conv_igemm.halo_dgrad", "conv_igemm.halo_wgrad",
             "conv_igemm.xl_fwd", "conv_igemm.xl_dgrad", "conv_igemm.xl_dgrad_s2", "stem.halo",
-            "fused.bn_relu_maxpool", "batchnorm.fused_bwd_moments"}
+            "fused.bn_relu_maxpool", "fused.stem_bn_relu_maxpool", "batchnorm.fused_bwd_moments"}
     from distributed_model_parallel_amd.utils import routes
     miss = routes.missing(need, runs["routes"])
     assert not miss, miss

@@ -127,7 +127,8 @@ def test_pipeline_graphed_stage_matches_eager(dtype, cl):
         x = torch.randn(64, 3, 32, 32, generator=g)
         y = torch.randint(0, 10, (64,), generator=g)
         res = [p.train_step(x, y) for p in pipes]
-        assert pipes[1]._graphs, "graphed path not taken"
+        # fp32 stages run library convolutions, which are not replay-safe: eager
+        assert bool(pipes[1]._graphs) == (dtype == torch.bfloat16), "graphed path taken / not taken"
         la, lb = float(res[0].loss), float(res[1].loss)
         assert abs(la - lb) <= tol * max(1.0, abs(la)), (step, la, lb)
         assert abs(res[0].top1 - res[1].top1) <= 100.0 / 64 * 2, step

@@ -128,7 +128,6 @@ def test_stem_halo_kernels_224(n):
     assert torch.equal(y2, y)
 
 
-@pytest.mark.unvalidated
 @pytest.mark.parametrize("shift", [0.0, 2.0])
 def test_stem_bn_backward_folded_into_wgrad(shift):
     """224 px: the stem's BN backward apply folded into its weight gradient

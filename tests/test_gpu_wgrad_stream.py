@@ -13,7 +13,7 @@ import sys
 
 import pytest
 
-pytestmark = [pytest.mark.gpu, pytest.mark.unvalidated]
+pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SCRIPT = r'''
