@@ -99,11 +99,9 @@ def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
         else:
             assert torch.equal(a, b), n  # num_batches_tracked: one update, not two
     torch.testing.assert_close(l2.float(), l1.float(), atol=0.1, rtol=0.1)
-    # fused vs checkpointed (different kernels): in a random-init ResNet-50 at
-    # batch 8 both bf16 gradients sit at cosine ~0.12-0.16 from the fp32 one
-    # and ~0.24-0.29 from each other (tools/ckpt_grad_diag.py, round 4: rounding
-    # chaos, no stage worse on either path), so judge each against an fp32
-    # oracle of the same weights: the checkpointed path no further than the fused
+    # fused vs checkpointed (different kernels): judge each against an fp32
+    # oracle of the same weights, relative to stock PyTorch bf16's own distance
+    # from it: the checkpointed path no further than the fused
     # (MobileNetV2 at 32 px is not chaotic that way: fused ~ checkpointed > 0.9
     # directly; its stock fp32 channels-last backward aborted inside MIOpen on
     # the box once, so no oracle there)
@@ -114,5 +112,16 @@ def test_checkpointed_step_matches_plain(arch, size, monkeypatch):
     ref.load_state_dict({k: v.float() for k, v in m0_state.items()})
     with _native.reference_mode():
         cross_entropy(ref(x.float()), y).backward()
-    cf, cc = _grad_cos(m, ref), _grad_cos(m2, ref)
-    assert cc > cf - 0.1 and cc > 0.03, (cf, cc)
+    # what bf16 itself costs here: stock PyTorch in bf16 on the same weights
+    # (judge the native paths against that, not against a fixed 0.03;
+    # tests/test_gpu_parity_train.py pins native == stock-bf16 distance in a
+    # well-conditioned regime)
+    sb = build_model(arch, num_classes=10).cuda().to(memory_format=torch.channels_last)
+    sb.load_state_dict({k: v.float() for k, v in m0_state.items()})
+    sb = sb.bfloat16()
+    with _native.reference_mode():
+        cross_entropy(sb(x).float(), y).backward()
+    cf, cc, cb = _grad_cos(m, ref), _grad_cos(m2, ref), _grad_cos(sb, ref)
+    print("gradient cosine to fp32: fused", cf, "checkpointed", cc, "stock bf16", cb)
+    # round 5: fused 0.889, checkpointed 0.892, stock bf16 0.889
+    assert cc > cb - 0.05 and cf > cb - 0.05, (cf, cc, cb)
