@@ -115,6 +115,8 @@ int get_gemm_xl_x2();
 void set_gemm_xl_nt(int on);
 void set_gemm_xl_tail(int on);
 int get_gemm_xl_tail();
+void set_gemm_xl_bm(int bm);
+int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K);
 int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
                                 int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
@@ -381,6 +383,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_xl_tail", &dmp::set_gemm_xl_tail, py::arg("on"),
         "256x256 ping-pong GEMMs: split-K for the last partial round of tiles (default off, measured no faster: finding 54; env DMP_XL_TAIL=1)");
   m.def("get_gemm_xl_tail", &dmp::get_gemm_xl_tail);
+  m.def("set_gemm_xl_bm", &dmp::set_gemm_xl_bm, py::arg("bm"),
+        "256x256 ping-pong GEMMs: rows per tile (0 auto: trimmed to fill whole rounds when K >= 768; "
+        "-1 always 256; 192..240 forced; env DMP_XL_BM)");
+  m.def("get_gemm_xl_bm", &dmp::get_gemm_xl_bm, py::arg("M"), py::arg("N"), py::arg("K"),
+        "rows per tile the ping-pong GEMM would take for this shape");
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,
         "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");

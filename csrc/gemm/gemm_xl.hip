@@ -207,6 +207,9 @@ struct XlArgs {
   // partials to skws (gemm_xl_tail_epi sums them and runs the epilogue)
   int tbase, ksplit, kper;
   float* skws;
+  // rows per tile of the PIPE 7 kernel (0 = 256): 192..240 trims the tile so
+  // that an MFMA-bound grid fills whole 1-block/CU rounds (pick_bm)
+  int bm;
 };
 
 // Epilogue of the NT kernel (and of a split-K tail tile, gemm_xl_tail_epi):
@@ -214,12 +217,14 @@ struct XlArgs {
 // fused operation; acc in the PIPE's register layout (7 / 8: transposed).
 template <int BN, int EPI, int PIPE, int LDS>
 __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN / 64], char* smem, int m0, int n0,
-                                            int mt, int mtiles) {
+                                            int mt, int mtiles, int tbm = XBM) {
   constexpr int WTM = 128, WTN = BN / 4;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int CT_STRIDE = BN + 8;
   constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
-  const int M = p.M, N = p.N;
+  // rows of this tile: [m0, min(M, m0 + tbm)); a trimmed tile's staged rows
+  // past tbm belong to the next tile and are neither stored nor summed
+  const int M = min(p.M, m0 + tbm), N = p.N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   (void)lane;
@@ -515,7 +520,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   const int M = p.M, N = p.N, K = p.K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + BN - 1) / BN;
+  const int tbm = (PIPE == 7 && p.bm > 0) ? p.bm : XBM;  // rows per tile (pick_bm)
+  const int mtiles = (M + tbm - 1) / tbm, ntiles = (N + BN - 1) / BN;
   int mt, nt;
   int kt_begin = 0, kt_end = K / XBK;
   if constexpr (PIPE == 9) {  // split-K tail launch: PIPE 7's loop over one K split, fp32 partials out
@@ -527,7 +533,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   } else {
     tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
   }
-  const int m0 = mt * XBM, n0 = nt * BN;
+  const int m0 = mt * tbm, n0 = nt * BN;
   const int ktiles = K / XBK;
 
   // ---- staging: lane L of a 1 KB glds instruction writes LDS bytes L*16..+16
@@ -728,6 +734,9 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       for (int j = 0; j < 2; ++j)
         qb[ks][j] = *reinterpret_cast<const bf16x8*>(b_region(ks, buf) + (wc * WTN + nq * 32 + j * 16) * 64 + frag_off);
   };
+  // a trimmed tile (tbm < 256, >= 192): wave row 1's m-half-1 blocks past
+  // row tbm are the next tile's rows -- their MFMAs are skipped (wave-uniform)
+  const int ilim = wr ? ((tbm - 192) >> 4) : 4;
   auto quad = [&](auto mqc, auto nqc) {
     constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
     barrier();
@@ -736,14 +745,27 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     __builtin_amdgcn_s_setprio(1);
     // operands swapped: acc holds C^T blocks (lane = output row, registers =
     // 4 consecutive output columns), so the epilogue stages 8-B row pieces
+    if (MQ == 0 || ilim >= 4) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[MQ * 4 + i][NQ * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+          for (int j = 0; j < 2; ++j)
+            acc[MQ * 4 + i][NQ * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i < ilim) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[MQ * 4 + i][NQ * 2 + j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+          }
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     barrier();
@@ -1039,7 +1061,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       for (int j = 0; j < NI; ++j) ws[i * NI + j] = acc[i][j];
     return;
   }
-  xl_epilogue<BN, EPI, PIPE, LDS>(p, acc, smem, m0, n0, mt, mtiles);
+  xl_epilogue<BN, EPI, PIPE, LDS>(p, acc, smem, m0, n0, mt, mtiles, tbm);
 }
 
 // Epilogue of the split-K tail tiles: block b sums the ksplit fp32 partials of
@@ -1865,6 +1887,28 @@ int num_cus() {
   return g_num_cus;
 }
 
+// Rows per tile of the PIPE 7 kernel.  One 256 x 256 block per CU makes a
+// partly filled last round cost a full one (finding 54: layer-3 3x3s at batch
+// 2048 are 1568 tiles = 6.1 rounds, ViT's N = 768 GEMMs 591 tiles = 2.3).
+// An MFMA-bound GEMM (K >= 768) instead takes the tile height in
+// {256, 240, .., 192} that minimises rounds x height: the skipped rows of a
+// trimmed tile cost their staging only.  0 = auto, -1 = always 256, else forced (A/B).
+int g_xl_bm = [] { const char* e = std::getenv("DMP_XL_BM"); return e ? std::atoi(e) : 0; }();
+
+int pick_bm(int64_t M, int64_t N, int64_t K) {
+  if (g_xl_pipe != 7 || g_xl_tail) return 256;
+  if (g_xl_bm > 0) return g_xl_bm;
+  if (g_xl_bm < 0 || K < 768) return 256;
+  const int64_t cus = num_cus(), nt = (N + 255) / 256;
+  int best = 256;
+  int64_t best_cost = ((M + 255) / 256 * nt + cus - 1) / cus * 256;
+  for (int bm = 240; bm >= 192; bm -= 16) {
+    const int64_t cost = ((M + bm - 1) / bm * nt + cus - 1) / cus * bm;
+    if (cost * 100 < best_cost * 97) { best = bm; best_cost = cost; }
+  }
+  return best;
+}
+
 template <int EPI>
 void launch_pp256(const XlArgs& a, int blocks, hipStream_t s) {
   if (g_xl_pipe == 8) {
@@ -1895,7 +1939,8 @@ void launch_pp256(const XlArgs& a, int blocks, hipStream_t s) {
 
 template <int BN, int EPI>
 void launch_xl(const XlArgs& a, hipStream_t s) {
-  const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + BN - 1) / BN);
+  const int tbm = (BN == 256 && a.bm > 0) ? a.bm : XBM;
+  const int blocks = ((a.M + tbm - 1) / tbm) * ((a.N + BN - 1) / BN);
   if constexpr (EPI == XL_STORE) {
     switch (g_xl_pipe) {  // timing-only ablations of the ring pipeline
       case 2: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 2>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
@@ -1959,7 +2004,8 @@ void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
     }
   }
   if constexpr (EPI >= XL_MOMENTS) {  // conv epilogues: ring kernel only (no persistent form)
-    const int blocks = ((a.M + XBM - 1) / XBM) * ((a.N + bn - 1) / bn);
+    const int tbm = (bn == 256 && a.bm > 0) ? a.bm : XBM;
+    const int blocks = ((a.M + tbm - 1) / tbm) * ((a.N + bn - 1) / bn);
     if (bn == 128)
       hipLaunchKernelGGL((gemm_xl_nt_kernel<128, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     else if (g_xl_pipe >= 7)
@@ -2057,6 +2103,7 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
   }
   const int bn = pick_bn((int)M, (int)N);
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
+  a.bm = bn == 256 ? pick_bm(M, N, K) : 256;
   hipStream_t s = at::hip::getCurrentHIPStream();
   switch (epi) {
     case XL_STORE: dispatch_bn<XL_STORE>(a, bn, s); break;
@@ -2088,7 +2135,9 @@ std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tenso
   a.M = (int)M; a.N = (int)N; a.K = (int)K;
   a.aux = const_cast<bf16*>(reinterpret_cast<const bf16*>(aux.data_ptr())); a.ldaux = aux.stride(0);
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
-  const int mtiles = (int)((M + XBM - 1) / XBM);
+  const int bn = pick_bn((int)M, (int)N);
+  a.bm = bn == 256 ? pick_bm(M, N, K) : 256;
+  const int mtiles = (int)((M + a.bm - 1) / a.bm);
   const bool fused = g_xl_pipe != 6;  // the persistent ablation kernel has no column sums
   at::Tensor part;
   if (fused) {
@@ -2096,7 +2145,7 @@ std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tenso
     a.part = part.data_ptr<float>();
   }
   hipStream_t s = at::hip::getCurrentHIPStream();
-  dispatch_bn<XL_DGELU>(a, pick_bn((int)M, (int)N), s);
+  dispatch_bn<XL_DGELU>(a, bn, s);
   DMP_HIP_CHECK(hipGetLastError());
   auto bgrad = fused ? part[0].sum(0) : C.to(at::kFloat).sum(0);
   return {C, bgrad};
@@ -2191,8 +2240,11 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   }
   const bool conv = a.cv.cin > 0;
   const int bn = conv ? 256 : pick_bn((int)M, (int)N);
+  // the two-blocks-per-CU route (dispatch_bn -> use_x2) keeps 256-row tiles
+  const bool x2 = !conv && epi >= XL_MOMENTS && use_x2(a);
+  a.bm = (bn == 256 && !x2) ? pick_bm(M, N, a.K) : 256;
   at::Tensor sums, part;
-  const int mtiles = (int)((M + XBM - 1) / XBM);
+  const int mtiles = (int)((M + a.bm - 1) / a.bm);
   const bool moments = epi == XL_MOMENTS || is_bnbwd(epi);
   if (moments) {
     part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
@@ -2350,7 +2402,8 @@ at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>&
     a.cv.stride = 1; a.cv.pad = 0; a.cv.kw = tx;
     a.omap.s = 2; a.omap.ho = (int)ho; a.omap.wo = (int)wo; a.omap.hi = (int)hi; a.omap.wi = (int)wi;
     a.omap.oy = py; a.omap.ox = px;
-    const int blocks = (int)((a.M + XBM - 1) / XBM) * (int)(cin / 256);
+    a.bm = pick_bm(a.M, a.N, a.K);
+    const int blocks = (int)((a.M + a.bm - 1) / a.bm) * (int)(cin / 256);
     launch_pp256<XL_STORE>(a, blocks, s);
   }
   DMP_HIP_CHECK(hipGetLastError());
@@ -2450,6 +2503,12 @@ void set_gemm_xl_x2(int mode) {
 int get_gemm_xl_x2() { return g_xl_x2; }
 void set_gemm_xl_nt(int on) { g_xl_nt = on ? 1 : 0; }
 void set_gemm_xl_tail(int on) { g_xl_tail = on ? 1 : 0; }
+void set_gemm_xl_bm(int bm) {
+  TORCH_CHECK(bm == 0 || bm == -1 || (bm >= 192 && bm <= 256 && bm % 16 == 0),
+              "bm: 0 (auto), -1 (always 256) or 192..256 in steps of 16");
+  g_xl_bm = bm;
+}
+int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K) { return pick_bm(M, N, K); }
 int get_gemm_xl_tail() { return g_xl_tail; }
 int get_tn_xl_ring() { return g_tn_xl_ring; }
 

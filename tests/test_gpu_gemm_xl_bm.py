@@ -1,0 +1,162 @@
+"""Trimmed tiles of the 256x256 ping-pong GEMM (csrc/gemm/gemm_xl.hip
+pick_bm / set_gemm_xl_bm): an MFMA-bound grid whose last round of 256-row
+tiles would be mostly empty runs 192..240-row tiles instead, so that the grid
+fills whole rounds.  Each output element still accumulates the same K
+sequence with the same MFMA, so every stored tensor must be BITWISE equal to
+the 256-row launch; only the per-tile BN moment partials regroup (fp32 order).
+Covered: every epilogue the ping-pong kernel runs (plain / bias / GELU /
+GELU' + column sums / residual; conv moments / add / BN backward with x, with
+y; the two-source folded dgrad; the stride-phase dgrad's row map), row counts
+that leave a partial last tile, and the auto choice on the shapes it exists
+for."""
+import pytest
+import torch
+
+from distributed_model_parallel_amd import _native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+CL = torch.channels_last
+BMS = [240, 224, 208, 192]
+
+
+@pytest.fixture
+def C():
+    c = _native.require("gemm_xl bm tests")
+    c.set_gemm_xl_bn(256)  # these small grids would otherwise take 128-wide tiles (pick_bn)
+    yield c
+    c.set_gemm_xl_bm(0)
+    c.set_gemm_xl_bn(0)
+
+
+def run(C, bm, fn):
+    C.set_gemm_xl_bm(bm)
+    out = fn()
+    torch.cuda.synchronize()
+    return out
+
+
+def wmat(w):
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous()
+
+
+def test_pick_bm_auto(C):
+    C.set_gemm_xl_bm(0)
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("the expected choices assume 256 CUs")
+    assert C.get_gemm_xl_bm(401408, 256, 2304) == 224   # layer-3 3x3 at batch 2048: 6.1 -> 7 full rounds
+    assert C.get_gemm_xl_bm(100352, 512, 4608) == 208   # layer-4 3x3: 3.06 rounds
+    assert C.get_gemm_xl_bm(50432, 768, 2304) == 208    # ViT qkv data gradient: 2.3 rounds
+    assert C.get_gemm_xl_bm(50432, 2304, 768) == 256    # ViT qkv forward: 6.9 rounds already
+    assert C.get_gemm_xl_bm(401408, 1024, 256) == 256   # short K: HBM-bound, never trimmed
+    C.set_gemm_xl_bm(-1)
+    assert C.get_gemm_xl_bm(401408, 256, 2304) == 256
+
+
+@pytest.mark.parametrize("bm", BMS)
+@pytest.mark.parametrize("mode", ["store", "bias", "bias_gelu", "bias_res"])
+def test_gemm_xl_plain_bitwise(C, bm, mode):
+    torch.manual_seed(0)
+    M, K, N = 40 * 256 + 37, 768, 768
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    kw = {}
+    if mode != "store":
+        kw["bias"] = bias
+    if mode == "bias_res":
+        kw["residual"] = res
+    aux0 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aux1 = torch.empty_like(aux0)
+    c0 = run(C, -1, lambda: C.gemm_xl(a, b, mode, aux=aux0 if mode == "bias_gelu" else None, **kw))
+    c1 = run(C, bm, lambda: C.gemm_xl(a, b, mode, aux=aux1 if mode == "bias_gelu" else None, **kw))
+    assert torch.equal(c0, c1)
+    if mode == "bias_gelu":
+        assert torch.equal(aux0, aux1)
+    ref = a.float() @ b.float().t() + (bias.float() if mode != "store" else 0)
+    if mode == "bias_res":
+        ref = ref.bfloat16().float() + res.float()
+    if mode != "bias_gelu":
+        torch.testing.assert_close(c1.float(), ref, atol=6e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("bm", [224, 192])
+def test_gemm_xl_dgelu_bgrad(C, bm):
+    torch.manual_seed(1)
+    M, K, N = 30 * 256 + 5, 1024, 512
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    d0, g0 = run(C, -1, lambda: C.gemm_xl_dgelu_bgrad(a, b, aux))
+    d1, g1 = run(C, bm, lambda: C.gemm_xl_dgelu_bgrad(a, b, aux))
+    assert torch.equal(d0, d1)
+    torch.testing.assert_close(g1, d1.float().sum(0), atol=2e-2 * M ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(g1, g0, atol=1e-2 * M ** 0.5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("bm", [224, 208])
+@pytest.mark.parametrize("n,c,h", [(41, 256, 14), (23, 512, 7)])
+def test_conv_xl_moments_add_bnbwd(C, bm, n, c, h):
+    torch.manual_seed(2)
+    rows = n * h * h
+    x = torch.randn(n, c, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = wmat((torch.randn(c, c, 3, 3, device=DEV) * 0.03).bfloat16())
+    (y0, s0) = run(C, -1, lambda: C.conv_xl(x, w, 3, 3, 1, 1, h, h, "moments"))
+    (y1, s1) = run(C, bm, lambda: C.conv_xl(x, w, 3, 3, 1, 1, h, h, "moments"))
+    assert torch.equal(y0, y1)
+    torch.testing.assert_close(s1[:2 * c], s0[:2 * c], atol=1e-2 * rows ** 0.5, rtol=1e-4)
+    assert s1[2 * c].item() == rows
+    f = y1.float()
+    torch.testing.assert_close(s1[:c].float(), f.sum(0).double().float(), atol=2e-2 * rows ** 0.5, rtol=1e-3)
+    res = torch.randn(rows, c, device=DEV).bfloat16()
+    a0, _ = run(C, -1, lambda: C.conv_xl(x, w, 3, 3, 1, 1, h, h, "add", residual=res))
+    a1, _ = run(C, bm, lambda: C.conv_xl(x, w, 3, 3, 1, 1, h, h, "add", residual=res))
+    assert torch.equal(a0, a1)
+    bx = torch.randn(rows, c, device=DEV).bfloat16()
+    by = torch.relu(torch.randn(rows, c, device=DEV)).bfloat16()
+    mean = torch.randn(c, device=DEV) * 0.1
+    inv = torch.rand(c, device=DEV) + 0.5
+    bw = torch.rand(c, device=DEV) + 0.5
+    bb = torch.randn(c, device=DEV) * 0.1
+    for kw in ({"bn_x": bx, "mean": mean, "invstd": inv, "weight": bw, "bias": bb},
+               {"bn_x": bx, "bn_y": by, "mean": mean}, {"bn_y": by}):
+        g0, t0 = run(C, -1, lambda: C.conv_xl(x, w, 3, 3, 1, 1, h, h, "bnbwd", residual=res, **kw))
+        g1, t1 = run(C, bm, lambda: C.conv_xl(x, w, 3, 3, 1, 1, h, h, "bnbwd", residual=res, **kw))
+        assert torch.equal(g0, g1)
+        torch.testing.assert_close(t1[:2 * c], t0[:2 * c], atol=1e-2 * rows ** 0.5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("bm", [240, 192])
+def test_gemm_xl_conv_fold_dgrad(C, bm):
+    """The folded dgrad: two-source A ([dz | a]), ebias, BN backward, K = 1280."""
+    torch.manual_seed(3)
+    w, rows = 256, 37 * 256 - 9
+    dz = torch.randn(rows, 4 * w, device=DEV).bfloat16()
+    a = torch.randn(rows, w, device=DEV).bfloat16()
+    Bb = (torch.randn(w, 5 * w, device=DEV) * 0.03).bfloat16()
+    eb = torch.randn(w, device=DEV) * 0.1
+    x = torch.randn(rows, w, device=DEV).bfloat16()
+    mean = torch.randn(w, device=DEV) * 0.1
+    inv = torch.rand(w, device=DEV) + 0.5
+    bw = torch.rand(w, device=DEV) + 0.5
+    bb = torch.randn(w, device=DEV) * 0.1
+    f = lambda: C.gemm_xl_conv(dz, Bb, "bnbwd", bn_x=x, mean=mean, invstd=inv, weight=bw, bias=bb, a2=a, ebias=eb)
+    o0, s0 = run(C, -1, f)
+    o1, s1 = run(C, bm, f)
+    assert torch.equal(o0, o1)
+    torch.testing.assert_close(s1[:2 * w], s0[:2 * w], atol=1e-2 * rows ** 0.5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("bm", [224, 208])
+def test_conv_xl_dgrad_s2_row_map(C, bm):
+    """The stride-phase data gradient writes through an output row map."""
+    from distributed_model_parallel_amd.ops import conv_igemm
+    torch.manual_seed(4)
+    n, cin, cout, hi = 19, 256, 512, 14
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.03).bfloat16()
+    dy = torch.randn(n, cout, hi // 2, hi // 2, device=DEV).bfloat16().contiguous(memory_format=CL)
+    wph = conv_igemm._phase_weights(w)
+    d0 = run(C, -1, lambda: C.conv_xl_dgrad_s2(dy, wph, hi, hi))
+    d1 = run(C, bm, lambda: C.conv_xl_dgrad_s2(dy, wph, hi, hi))
+    assert torch.equal(d0, d1)
