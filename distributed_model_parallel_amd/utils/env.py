@@ -100,11 +100,17 @@ def init_distributed(backend: Optional[str] = None, dist_url: Optional[str] = No
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
     if not dist.is_initialized():
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", str(29500 + (os.getpid() % 1000)))
         kw = dict(backend=backend, rank=e.rank, world_size=e.world_size,
                   timeout=datetime.timedelta(seconds=timeout_s))
-        kw["init_method"] = dist_url or "env://"
+        if e.world_size == 1 and dist_url is None:
+            # one rank: an in-process store, no TCP rendezvous -- a port picked
+            # for it can be taken by another process between the pick and the
+            # bind (EADDRINUSE on shared boxes)
+            kw["store"] = dist.HashStore()
+        else:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(29500 + (os.getpid() % 1000)))
+            kw["init_method"] = dist_url or "env://"
         dist.init_process_group(**kw)
     return e
 
