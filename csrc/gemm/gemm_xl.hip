@@ -210,9 +210,6 @@ struct XlArgs {
   // rows per tile of the PIPE 7 kernel (0 = 256): 192..240 trims the tile so
   // that an MFMA-bound grid fills whole 1-block/CU rounds (pick_bm)
   int bm;
-  // PIPE 7: first-round blocks of every other CU wait this many 10-ns ticks
-  // before starting (phase stagger, g_xl_stagger); 0 = off
-  int stagger, scus;
 };
 
 // Epilogue of the NT kernel (and of a split-K tail tile, gemm_xl_tail_epi):
@@ -538,17 +535,6 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   }
   const int m0 = mt * tbm, n0 = nt * BN;
   const int ktiles = K / XBK;
-  if constexpr (PIPE == 7) {
-    // Identical tiles started together keep every CU in the same phase (all
-    // staging, then all in the HBM-bound epilogue).  Holding back the first
-    // block of every other CU of an XCD by about half a tile shifts those
-    // CUs' whole sequence of tiles, so that half the chip is in its epilogue
-    // while the other half runs its main loop.
-    if (p.stagger > 0 && (int)blockIdx.x < p.scus && ((blockIdx.x >> 3) & 1)) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)p.stagger) __builtin_amdgcn_s_sleep(4);
-    }
-  }
 
   // ---- staging: lane L of a 1 KB glds instruction writes LDS bytes L*16..+16
   // of 16 rows x 64 B; the logical 16-B chunk it carries is the physical one
@@ -1923,14 +1909,8 @@ int pick_bm(int64_t M, int64_t N, int64_t K) {
   return best;
 }
 
-// first-round phase stagger of the PIPE 7 kernel in 10-ns ticks (A/B: DMP_XL_STAGGER)
-int g_xl_stagger = [] { const char* e = std::getenv("DMP_XL_STAGGER"); return e ? std::atoi(e) : 0; }();
-
 template <int EPI>
-void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
-  XlArgs a = a_in;
-  a.stagger = blocks > num_cus() ? g_xl_stagger : 0;
-  a.scus = num_cus();
+void launch_pp256(const XlArgs& a, int blocks, hipStream_t s) {
   if (g_xl_pipe == 8) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 8>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     return;
@@ -2523,10 +2503,6 @@ void set_gemm_xl_x2(int mode) {
 int get_gemm_xl_x2() { return g_xl_x2; }
 void set_gemm_xl_nt(int on) { g_xl_nt = on ? 1 : 0; }
 void set_gemm_xl_tail(int on) { g_xl_tail = on ? 1 : 0; }
-void set_gemm_xl_stagger(int ticks) {
-  TORCH_CHECK(ticks >= 0 && ticks <= 100000, "stagger: 0..100000 ticks of 10 ns");
-  g_xl_stagger = ticks;
-}
 void set_gemm_xl_bm(int bm) {
   TORCH_CHECK(bm == 0 || bm == -1 || (bm >= 192 && bm <= 256 && bm % 16 == 0),
               "bm: 0 (auto), -1 (always 256) or 192..256 in steps of 16");
