@@ -116,6 +116,7 @@ void set_gemm_xl_nt(int on);
 void set_gemm_xl_tail(int on);
 int get_gemm_xl_tail();
 void set_gemm_xl_bm(int bm);
+void set_gemm_xl_trace(const c10::optional<at::Tensor>& buf);
 int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K);
 int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
@@ -386,6 +387,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_xl_bm", &dmp::set_gemm_xl_bm, py::arg("bm"),
         "256x256 ping-pong GEMMs: rows per tile (0 auto: trimmed to fill whole rounds when K >= 768; "
         "-1 always 256; 192..240 forced; env DMP_XL_BM)");
+  m.def("set_gemm_xl_trace", &dmp::set_gemm_xl_trace, py::arg("buf") = py::none(),
+        "diagnostics: 256x256 ping-pong GEMM launches record per-block phase timestamps into buf "
+        "(int64 [blocks * 8]: entry, operands landed, main loop done, epilogue done, HW_ID, XCC_ID); None = off");
   m.def("get_gemm_xl_bm", &dmp::get_gemm_xl_bm, py::arg("M"), py::arg("N"), py::arg("K"),
         "rows per tile the ping-pong GEMM would take for this shape");
   m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);

@@ -210,7 +210,14 @@ struct XlArgs {
   // rows per tile of the PIPE 7 kernel (0 = 256): 192..240 trims the tile so
   // that an MFMA-bound grid fills whole 1-block/CU rounds (pick_bm)
   int bm;
+  // diagnostics (set_gemm_xl_trace): per block [entry, operands landed, main
+  // loop done, epilogue done] in 10-ns ticks, HW_ID, XCC_ID; null = off
+  unsigned long long* tdbg;
 };
+
+__device__ __forceinline__ void xl_mark(const XlArgs& p, int k) {
+  if (p.tdbg && threadIdx.x == 0) p.tdbg[(int64_t)blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // Epilogue of the NT kernel (and of a split-K tail tile, gemm_xl_tail_epi):
 // (acc [+ bias]) -> bf16 tile in LDS, then the row-contiguous pass with the
@@ -535,6 +542,11 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   }
   const int m0 = mt * tbm, n0 = nt * BN;
   const int ktiles = K / XBK;
+  if (p.tdbg && threadIdx.x == 0) {
+    p.tdbg[(int64_t)blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    p.tdbg[(int64_t)blockIdx.x * 8 + 4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    p.tdbg[(int64_t)blockIdx.x * 8 + 5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
 
   // ---- staging: lane L of a 1 KB glds instruction writes LDS bytes L*16..+16
   // of 16 rows x 64 B; the logical 16-B chunk it carries is the physical one
@@ -788,6 +800,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     vmcnt<0>();
   }
   barrier();
+  xl_mark(p, 1);
   if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
   for (int kt = kt_begin; kt < kt_end; ++kt) {
     const int buf = kt & 1;
@@ -808,6 +821,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   }
   if (wr == 0) barrier();  // equal barrier counts before the epilogue
   barrier();
+  xl_mark(p, 2);
   } else if constexpr (PIPE == 8) {
   // ---- PIPE 8: the ping-pong quadrant schedule of PIPE 7 on a ring of NS
   // 16 KB unit slots instead of two fixed tile buffers (finding 42: PIPE 7
@@ -1062,6 +1076,10 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     return;
   }
   xl_epilogue<BN, EPI, PIPE, LDS>(p, acc, smem, m0, n0, mt, mtiles, tbm);
+  if (p.tdbg) {
+    __syncthreads();
+    xl_mark(p, 3);
+  }
 }
 
 // Epilogue of the split-K tail tiles: block b sums the ksplit fp32 partials of
@@ -1909,8 +1927,12 @@ int pick_bm(int64_t M, int64_t N, int64_t K) {
   return best;
 }
 
+unsigned long long* g_xl_tdbg = nullptr;  // set_gemm_xl_trace
+
 template <int EPI>
-void launch_pp256(const XlArgs& a, int blocks, hipStream_t s) {
+void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
+  XlArgs a = a_in;
+  a.tdbg = g_xl_tdbg;
   if (g_xl_pipe == 8) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 8>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     return;
@@ -2503,6 +2525,15 @@ void set_gemm_xl_x2(int mode) {
 int get_gemm_xl_x2() { return g_xl_x2; }
 void set_gemm_xl_nt(int on) { g_xl_nt = on ? 1 : 0; }
 void set_gemm_xl_tail(int on) { g_xl_tail = on ? 1 : 0; }
+void set_gemm_xl_trace(const c10::optional<at::Tensor>& buf) {
+  if (!buf || !buf->defined()) {
+    g_xl_tdbg = nullptr;
+    return;
+  }
+  TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous(),
+              "trace buffer: contiguous int64 GPU tensor of 8 entries per block");
+  g_xl_tdbg = reinterpret_cast<unsigned long long*>(buf->data_ptr());
+}
 void set_gemm_xl_bm(int bm) {
   TORCH_CHECK(bm == 0 || bm == -1 || (bm >= 192 && bm <= 256 && bm % 16 == 0),
               "bm: 0 (auto), -1 (always 256) or 192..256 in steps of 16");

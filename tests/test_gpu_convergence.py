@@ -298,20 +298,23 @@ def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
     k = 20
     l0 = _mean(l_ref[:5])
     a, b = _mean(l_nat[-k:]), _mean(l_ref[-k:])
-    # the task is learned but not saturated: the plateau stays well above zero
-    assert b < 0.9 * l0 and b > 0.1 * l0, (l0, b)
-    # native tracks stock.  The curves are separate trajectories of a chaotic
-    # run (bf16 vs fp32, run-dependent atomic order) still falling at step
-    # 160: four round-4 runs put the last-20 mean of the SAME stock fp32 run at
-    # 0.72-1.20 and native at 0.82-1.82, so the late value alone cannot
-    # discriminate.  A wrong gradient slows the whole descent: compare the
-    # mean over all steps (ratio native / stock measured 0.86-1.13), require a
-    # real descent, and no lag in reaching 95 / 90 % of the start
-    assert _mean(l_nat) <= 1.25 * _mean(l_ref), (_mean(l_nat), _mean(l_ref))
+    # the task is learned by the reference.  (Round 4 also required its plateau
+    # to stay above 0.1 x start; a round-5 stock fp32 run ended at 0.087 x --
+    # the stock curve's late value is as chaotic as the native one, and the
+    # comparisons below do not need an unsaturated plateau.  Gradient parity
+    # itself is pinned by tests/test_gpu_parity_train.py.)
+    assert b < 0.9 * l0, (l0, b)
+    # native tracks stock.  Before the descent sets in the two runs are
+    # near-deterministic: over steps 0-29 the native / stock mean loss ratio
+    # measured 1.001-1.018 per 10-step window (round 5, profiles/README.md
+    # finding 66) -- a wrong gradient shows here first, so this is the tight
+    # check.  From the descent's onset on the curves are separate trajectories
+    # of a chaotic run: three round-5 runs of the SAME stock fp32 code put its
+    # whole-curve mean at 3.03, 3.33 and 3.73 (native 3.44-3.95), so the
+    # whole-curve ratio (measured 0.86-1.31) gets a band of that width, and a
+    # real descent is required.  (Round 4's steps-to-95 / 90 % lag check is
+    # dropped: the onset is the most chaotic part of the curve.)
+    early_n, early_r = _mean(l_nat[:30]), _mean(l_ref[:30])
+    assert abs(early_n / early_r - 1.0) <= 0.05, (early_n, early_r)
+    assert _mean(l_nat) <= 1.4 * _mean(l_ref), (_mean(l_nat), _mean(l_ref))
     assert a < 0.6 * l0, (l0, a)
-    # lag band: 1.5x + 10 steps (round 4: 46-56 vs 46-53 in four runs, once
-    # 74 vs 51 on a correct build -- the onset of the descent is chaotic too)
-    for frac in (0.95, 0.9):
-        sn, sr = _steps_to(l_nat, frac * l0), _steps_to(l_ref, frac * l0)
-        if sr is not None:
-            assert sn is not None and sn <= 1.5 * sr + 10, (frac, sn, sr)
