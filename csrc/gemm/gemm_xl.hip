@@ -235,6 +235,97 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   (void)lane;
+  // ---- batched epilogue operand loads (residual / BN input / BN output / aux).
+  // Row passes of RPP rows; batch b covers passes [b PB, b PB + PB).  The
+  // first batch goes out BEFORE the accumulator staging below and every later
+  // batch one batch ahead of its use, so a whole tile's operand rows are in
+  // flight through the epilogue instead of one batch at a time (finding 66:
+  // the residual epilogue was ~10 us of an 18-20 us short-K tile, its two
+  // batches each a full HBM round trip).
+  constexpr int CV = BN / 8, RPP = XTHREADS / CV;
+  const int cvi = tid % CV, rr0 = tid / CV;
+  const int col = n0 + cvi * 8;
+  constexpr bool kBatch = is_bnbwd(EPI) || EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BIAS_RES ||
+                          EPI == XL_DGELU;
+  constexpr bool kL0 = kBatch;
+  constexpr bool kL12 = is_bnbwd(EPI);
+  constexpr bool kLx = EPI == XL_BNBWD || EPI == XL_BNBWD_Y, kLy = EPI == XL_BNBWD_Y || EPI == XL_BNBWD_YO;
+  constexpr int NT = (kL0 ? 1 : 0) + (kLx ? 1 : 0) + (kLy ? 1 : 0);
+  constexpr int NP = kBatch ? XBM / RPP : 0;
+  constexpr int PB = NT >= 3 ? 2 : NT == 2 ? 4 : 8;  // two batches in flight: 2 PB NT 16-B loads per lane
+  constexpr int NB = kBatch ? NP / PB : 1;
+  // operand bases for branch-free loads: a missing operand reads a valid
+  // dummy row (row 0 of C / of itself), its value is never used -- a
+  // per-load branch would split every load into its own block, and the
+  // compiler then waits for each one before the next (measured: the
+  // forward affine epilogue kept exactly one load per lane in flight)
+  const bf16* rsrc = EPI == XL_DGELU ? p.aux : p.R;  // GELU' reads the pre-activation
+  const bf16* rbase = rsrc ? rsrc : p.C;
+  const int64_t rld = rsrc ? (EPI == XL_DGELU ? p.ldaux : p.ldr) : 0;
+  const bf16* xbase = p.bx ? p.bx : p.C;
+  const int64_t xld = p.bx ? p.ldbx : 0;
+  const bf16* ybase = p.bny ? p.bny : p.C;
+  const int64_t yld = p.bny ? p.ldby : 0;
+  // row pointers advance by a uniform RPP-row step (no per-row 64-bit
+  // multiply); a row past M reads row 0 of the same operand instead
+  // loads are issued by every lane (a load under a branch makes the compiler
+  // drain the whole batch at the join): lanes past N read column N - 8
+  const int coll = min(col, N - 8);
+  const bf16* rrow = rbase + (int64_t)(m0 + rr0) * rld + coll;
+  const int64_t rstep = (int64_t)RPP * rld;
+  const bf16* xrow = xbase + (int64_t)(m0 + rr0) * xld + coll;
+  const bf16* yrow = ybase + (int64_t)(m0 + rr0) * yld + coll;
+  const int64_t xstep = (int64_t)RPP * xld, ystep = (int64_t)RPP * yld;
+  bf16x8 L0[NB][PB], L1[NB][PB], L2[NB][PB];
+  unsigned rok[NB];  // bit i: row pass b PB + i has a residual row (compact map)
+  auto issue = [&](const int b) {
+    rok[b] = 0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      const int pass = b * PB + i;
+      const int row_u = m0 + rr0 + pass * RPP;
+      const int row = min(row_u, M - 1);
+      if constexpr (kL0) {
+        const bf16x8* rp;
+        if constexpr (is_bnbwd(EPI)) {
+          int64_t rr = p.R ? compact_row(p.rmap, row) : -1;
+          rok[b] |= (rr >= 0 ? 1u : 0u) << i;
+          rr = rr >= 0 ? rr : 0;
+          rp = reinterpret_cast<const bf16x8*>(rbase + rr * rld + coll);
+        } else {
+          rp = reinterpret_cast<const bf16x8*>(row_u < M ? rrow + pass * rstep : rbase + coll);
+        }
+        L0[b][i] = p.cnt ? __builtin_nontemporal_load(rp) : *rp;
+      }
+      if constexpr (kL12) {
+        if constexpr (kLx) L1[b][i] = *reinterpret_cast<const bf16x8*>(row_u < M ? xrow + pass * xstep : xbase + coll);
+        if constexpr (kLy) L2[b][i] = *reinterpret_cast<const bf16x8*>(row_u < M ? yrow + pass * ystep : ybase + coll);
+      }
+    }
+  };
+  // BN-backward column constants, loaded ahead of everything else (branch-free:
+  // an absent operand reads the zero row, a select picks the default)
+  float bmu[8], bsc[8], bsh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bmu[j] = bsc[j] = bsh[j] = 0.f;
+  if constexpr (is_bnbwd(EPI)) {
+    const float* zf0 = reinterpret_cast<const float*>(g_zero_row);
+    const f32x8 mu = *reinterpret_cast<const f32x8*>(p.bmean ? p.bmean + coll : zf0);
+    f32x8 iv = {}, ww = {}, bb = {};
+    if constexpr (EPI == XL_BNBWD) {
+      iv = *reinterpret_cast<const f32x8*>(p.binv ? p.binv + coll : zf0);
+      ww = *reinterpret_cast<const f32x8*>(p.bw ? p.bw + coll : zf0);
+      bb = *reinterpret_cast<const f32x8*>(p.bb ? p.bb + coll : zf0);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bmu[j] = mu[j];
+      if constexpr (EPI == XL_BNBWD) {
+        bsc[j] = iv[j] * (p.bw ? ww[j] : 1.f);
+        bsh[j] = bb[j] - bmu[j] * bsc[j];
+      }
+    }
+  }
   bf16* ct = reinterpret_cast<bf16*>(smem);
   // per-column affine applied to the fp32 accumulator BEFORE the bf16 staging:
   // a bias / BN shift that nearly cancels acc (XL_BNBWD's folded-BN constant,
@@ -244,23 +335,38 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
     // consecutive columns 4 (l >> 4) + e of each 16 x 16 block -> one 8-B LDS
     // write per block (a half-wave covers 16 rows x 16 B at a 528-B row pitch:
     // all 64 banks once) instead of four 2-B writes
+    // the per-column coefficients first, then the first operand batch: a use
+    // of a load waits for everything issued before it (in-order vmcnt), so
+    // coefficients loaded after the batch would drain it before the staging
+    // (branch-free as the batch: absent coefficients read the zero row,
+    // columns past N read column N - 4, and selects pick the defaults)
+    f32x4 s4a[NI], b4a[NI];
+    const float* zf = reinterpret_cast<const float*>(g_zero_row);
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int colj = min(n0 + wc * WTN + j * 16 + (lane >> 4) * 4, N - 4);  // N % 8 == 0
+      f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b4[e] = (float)p.bias[colj + e];  // a bias view may be 2-B aligned only
+      }
+      if constexpr (is_bnbwd(EPI))
+        b4 = *reinterpret_cast<const f32x4*>(p.ebias ? p.ebias + colj : zf);
+      if constexpr (EPI == XL_AFFINE) {
+        const f32x4 sl = *reinterpret_cast<const f32x4*>(p.esc ? p.esc + colj : zf);
+        s4 = p.esc ? sl : s4;
+        b4 = *reinterpret_cast<const f32x4*>(p.esh ? p.esh + colj : zf);
+      }
+      s4a[j] = s4;
+      b4a[j] = b4;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the coefficient loads ahead of the batch
+    if constexpr (kBatch) issue(0);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       const int lc = wc * WTN + j * 16 + (lane >> 4) * 4;
-      const int col = n0 + lc;
-      f32x4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
-      if (col < N) {  // N % 8 == 0: the 4 columns are all in or all out
-        if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) b4[e] = (float)p.bias[col + e];  // a bias view may be 2-B aligned only
-        }
-        if constexpr (is_bnbwd(EPI))
-          if (p.ebias) b4 = *reinterpret_cast<const f32x4*>(p.ebias + col);
-        if constexpr (EPI == XL_AFFINE) {
-          if (p.esc) s4 = *reinterpret_cast<const f32x4*>(p.esc + col);
-          if (p.esh) b4 = *reinterpret_cast<const f32x4*>(p.esh + col);
-        }
-      }
+      const f32x4 s4 = s4a[j], b4 = b4a[j];
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int row = wr * WTM + i * 16 + (lane & 15);
@@ -286,6 +392,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
       bv[j] = (col < N && p.esh) ? p.esh[col] : 0.f;
     }
   }
+  if constexpr (kBatch) issue(0);
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -299,91 +406,29 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
     }
   }
   __syncthreads();
-  constexpr int CV = BN / 8, RPP = XTHREADS / CV;
-  const int cvi = tid % CV, rr0 = tid / CV;
-  const int col = n0 + cvi * 8;
-  float msum[8], msq[8], bmu[8], bsc[8], bsh[8];
+  float msum[8], msq[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; bmu[j] = bsc[j] = bsh[j] = 0.f; }
-  if constexpr (is_bnbwd(EPI)) {
-    if (col < N) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        bmu[j] = p.bmean ? p.bmean[col + j] : 0.f;
-        if (EPI == XL_BNBWD) {
-          bsc[j] = p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f);
-          bsh[j] = (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j];
-        }
-      }
-    }
-  }
+  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; }
   if (col < N) {
-    // Epilogue in batches of PB row passes: phase 1 issues every global operand
-    // load of the batch (residual / BN input / BN output / aux), phase 2
-    // computes and stores.  The loads must not sit behind the batch's stores:
-    // C may alias them for all the compiler knows, so a load-compute-store loop
-    // keeps ~2 loads per lane in flight -- measured 2.2-3.1 TB/s on the
-    // short-K conv epilogues at 1 block/CU (tools/epi_bench.py).
-    // Batched for every epilogue with operand loads (XL_BNBWD 1.72 -> 1.24 ms
-    // at l2 shapes); the load-free ones keep the row-at-a-time loop below.
-    constexpr bool kBatch = is_bnbwd(EPI) || EPI == XL_ADD || EPI == XL_AFFINE || EPI == XL_BIAS_RES ||
-                            EPI == XL_DGELU;
-    constexpr int NP = kBatch ? XBM / RPP : 0, PB = 8;
-    constexpr bool kL0 = kBatch;
-    constexpr bool kL12 = is_bnbwd(EPI);
-    constexpr bool kLx = EPI == XL_BNBWD || EPI == XL_BNBWD_Y, kLy = EPI == XL_BNBWD_Y || EPI == XL_BNBWD_YO;
-    // operand bases for branch-free loads: a missing operand reads a valid
-    // dummy row (row 0 of C / of itself), its value is never used -- a
-    // per-load branch would split every load into its own block, and the
-    // compiler then waits for each one before the next (measured: the
-    // forward affine epilogue kept exactly one load per lane in flight)
-    const bf16* rsrc = EPI == XL_DGELU ? p.aux : p.R;  // GELU' reads the pre-activation
-    const bf16* rbase = rsrc ? rsrc : p.C;
-    const int64_t rld = rsrc ? (EPI == XL_DGELU ? p.ldaux : p.ldr) : 0;
-    const bf16* xbase = p.bx ? p.bx : p.C;
-    const int64_t xld = p.bx ? p.ldbx : 0;
-    const bf16* ybase = p.bny ? p.bny : p.C;
-    const int64_t yld = p.bny ? p.ldby : 0;
-    // row pointers advance by a uniform RPP-row step (no per-row 64-bit
-    // multiply); a row past M reads row 0 of the same operand instead
-    const bf16* rrow = rbase + (int64_t)(m0 + rr0) * rld + col;
-    const int64_t rstep = (int64_t)RPP * rld;
-    const bf16* xrow = xbase + (int64_t)(m0 + rr0) * xld + col;
-    const bf16* yrow = ybase + (int64_t)(m0 + rr0) * yld + col;
-    const int64_t xstep = (int64_t)RPP * xld, ystep = (int64_t)RPP * yld;
+    // Epilogue in batches of PB row passes (issued above / one batch ahead):
+    // the loads must not sit behind the batch's stores -- C may alias them for
+    // all the compiler knows, so a load-compute-store loop keeps ~2 loads per
+    // lane in flight (measured 2.2-3.1 TB/s on the short-K conv epilogues at 1
+    // block/CU, tools/epi_bench.py).  The load-free epilogues keep the
+    // row-at-a-time loop below.
     bf16* const crow = p.C + (int64_t)(m0 + rr0) * p.ldc + col;
     const int64_t cstep = (int64_t)RPP * p.ldc;
     // XL_AFFINE without a residual still loads (a dummy row of C: branch-free
     // batch) and masks the bits to +0 instead of branching around the add
     const unsigned rmask = p.R ? 0xffffffffu : 0u;
-#pragma unroll 1
-    for (int pb = 0; pb < NP; pb += PB) {
-      bf16x8 l0[PB], l1[PB], l2[PB];
-      unsigned rok = 0;  // bit i: row pass i has a residual row (compact map)
+    (void)rmask;
+    if constexpr (kBatch) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (b + 1 < NB) issue(b + 1);
 #pragma unroll
       for (int i = 0; i < PB; ++i) {
-        const int row_u = m0 + rr0 + (pb + i) * RPP;
-        const int row = min(row_u, M - 1);
-        if constexpr (kL0) {
-          const bf16x8* rp;
-          if constexpr (is_bnbwd(EPI)) {
-            int64_t rr = p.R ? compact_row(p.rmap, row) : -1;
-            rok |= (rr >= 0 ? 1u : 0u) << i;
-            rr = rr >= 0 ? rr : 0;
-            rp = reinterpret_cast<const bf16x8*>(rbase + rr * rld + col);
-          } else {
-            rp = reinterpret_cast<const bf16x8*>(row_u < M ? rrow + (pb + i) * rstep : rbase + col);
-          }
-          l0[i] = p.cnt ? __builtin_nontemporal_load(rp) : *rp;
-        }
-        if constexpr (kL12) {
-          if constexpr (kLx) l1[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? xrow + (pb + i) * xstep : xbase + col);
-          if constexpr (kLy) l2[i] = *reinterpret_cast<const bf16x8*>(row_u < M ? yrow + (pb + i) * ystep : ybase + col);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < PB; ++i) {
-        const int lr = rr0 + (pb + i) * RPP;
+        const int lr = rr0 + (b * PB + i) * RPP;
         const int row = m0 + lr;
         if (row >= M) continue;
         bf16x8 v = *reinterpret_cast<const bf16x8*>(ct + lr * CT_STRIDE + cvi * 8);
@@ -393,11 +438,11 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
           for (int j = 0; j < 8; ++j) { msum[j] += f[j]; msq[j] = fmaf(f[j], f[j], msq[j]); }
         } else if constexpr (EPI == XL_ADD || EPI == XL_BIAS_RES) {
           f32x8 f = __builtin_convertvector(v, f32x8);
-          f += __builtin_convertvector(l0[i], f32x8);
+          f += __builtin_convertvector(L0[b][i], f32x8);
           v = __builtin_convertvector(f, bf16x8);
         } else if constexpr (EPI == XL_AFFINE) {  // v = bf16(acc * s + t) (staged)
           f32x8 f = __builtin_convertvector(v, f32x8);
-          u32x4 rb = __builtin_bit_cast(u32x4, l0[i]);
+          u32x4 rb = __builtin_bit_cast(u32x4, L0[b][i]);
           rb &= rmask;
           f += __builtin_convertvector(__builtin_bit_cast(bf16x8, rb), f32x8);
           if (p.erelu) {
@@ -408,7 +453,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
         } else if constexpr (is_bnbwd(EPI)) {
           f32x8 g = __builtin_convertvector(v, f32x8);  // ebias already in (staging)
           if (p.R) {  // the other branch's gradient: summed in fp32, rounded once (as XL_ADD)
-            if ((rok >> i) & 1u) g += __builtin_convertvector(l0[i], f32x8);
+            if ((rok[b] >> i) & 1u) g += __builtin_convertvector(L0[b][i], f32x8);
             v = __builtin_convertvector(g, bf16x8);
             g = __builtin_convertvector(v, f32x8);
           }
@@ -417,8 +462,8 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
           // contract); _Y / _YO fix it: mask from y, with / without x moments
           constexpr bool kY = EPI != XL_BNBWD, kX = EPI != XL_BNBWD_YO;
           f32x8 xv = {}, yv = {};
-          if constexpr (kLx) xv = __builtin_convertvector(l1[i], f32x8);
-          if constexpr (kLy) yv = __builtin_convertvector(l2[i], f32x8);
+          if constexpr (kLx) xv = __builtin_convertvector(L1[b][i], f32x8);
+          if constexpr (kLy) yv = __builtin_convertvector(L2[b][i], f32x8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             // (xl_conv_run maps an operand set with y to _Y / _YO: plain
@@ -440,7 +485,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
           v = __builtin_convertvector(f, bf16x8);
         } else if constexpr (EPI == XL_DGELU) {
           f32x8 f = __builtin_convertvector(v, f32x8);
-          const f32x8 x = __builtin_convertvector(l0[i], f32x8);
+          const f32x8 x = __builtin_convertvector(L0[b][i], f32x8);
 #pragma unroll
           for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
           v = __builtin_convertvector(f, bf16x8);
@@ -449,10 +494,11 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
           for (int j = 0; j < 8; ++j) msum[j] += fv[j];
         }
         static_assert(!kBatch || EPI != XL_STORE, "batched epilogues write C rows unmapped");
-        bf16x8* cp = reinterpret_cast<bf16x8*>(crow + (pb + i) * cstep);
+        bf16x8* cp = reinterpret_cast<bf16x8*>(crow + (b * PB + i) * cstep);
         if (p.cnt) __builtin_nontemporal_store(v, cp);
         else *cp = v;
       }
+    }
     }
     if constexpr (!kBatch) {
 #pragma unroll 8
@@ -1075,6 +1121,11 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
       for (int j = 0; j < NI; ++j) ws[i * NI + j] = acc[i][j];
     return;
   }
+  // every operand copy has landed (the main loops end on vmcnt(0) in inline
+  // asm, which the compiler cannot see): say so with a wait it does see, or it
+  // drains the epilogue's first operand batch before its first LDS write to
+  // order that write after the copies into LDS
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   xl_epilogue<BN, EPI, PIPE, LDS>(p, acc, smem, m0, n0, mt, mtiles, tbm);
   if (p.tdbg) {
     __syncthreads();
