@@ -139,6 +139,10 @@ at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride);
 bool stem_halo_supported(int64_t hs, int64_t ws, int64_t ho, int64_t wo);
 std::vector<at::Tensor> stem_halo_fwd(const at::Tensor& s, const at::Tensor& wm, int64_t ho, bool moments);
 at::Tensor stem_halo_wgrad(const at::Tensor& dy, const at::Tensor& s, int64_t ho, at::ScalarType out_dtype);
+at::Tensor stem_fold_finish(const at::Tensor& img, int64_t ho, int64_t wo, const at::Tensor& t_dz,
+                            const at::Tensor& t_y, const at::Tensor& sums, const at::Tensor& cnt,
+                            const at::Tensor& invstd, const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
+                            at::ScalarType out_dtype);
 bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
@@ -322,6 +326,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_halo_supported", &dmp::stem_halo_supported);
   m.def("stem_halo_fwd", &dmp::stem_halo_fwd, py::arg("s"), py::arg("wm"), py::arg("ho"), py::arg("moments") = false,
         "ResNet stem (s2d 4x4 conv, 16 -> 64 ch, Wo = 112) forward: halo-tiled, weights in VGPRs",
+        py::call_guard<py::gil_scoped_release>());
+  m.def("stem_fold_finish", &dmp::stem_fold_finish, py::arg("img"), py::arg("ho"), py::arg("wo"), py::arg("t_dz"),
+        py::arg("t_y"), py::arg("sums"), py::arg("cnt"), py::arg("invstd"), py::arg("weight"), py::arg("mean"),
+        py::arg("out_dtype"),
+        "folded stem weight gradient: BN-backward coefficients, the 16 window sums of the batch-summed "
+        "space-to-depth image, and al t_dz + be t_y + cc cols in one launch",
         py::call_guard<py::gil_scoped_release>());
   m.def("stem_halo_wgrad", &dmp::stem_halo_wgrad, py::arg("dy"), py::arg("s"), py::arg("ho"), py::arg("out_dtype"),
         "ResNet stem weight gradient [64, 256]: halo-tiled, dW in VGPRs",

@@ -527,4 +527,108 @@ at::Tensor stem_halo_wgrad(const at::Tensor& dy, const at::Tensor& s, int64_t ho
   return out;
 }
 
+
+// ---------------------------------------------------------------------------
+// Tail of the folded stem weight gradient (ops/fused.py _StemBNReLUMaxPoolFn):
+//   dW[o][(r*4 + q)*16 + c] = al[o] t_dz[o][k] + be[o] t_y[o][k] + cc[o] cols[k]
+// with the BN-backward coefficients of output channel o
+//   al = invstd w,  be = -al invstd^2 sum(dz (x - mean)) / cnt,
+//   cc = -al sum(dz) / cnt - be mean
+// and cols[(r, q, c)] = sum over oh < ho, ow < wo of img[oh + r][ow + q][c],
+// img = the batch sum of the space-to-depth image.  One block: the 4 column
+// window sums of every img row by a sliding window (fp64), then the 4 row
+// windows of those -- the 16 x 16 rectangle sums the torch version formed from
+// fp64 2-D prefix sums over ~20 small launches (~0.24 ms a step at any batch).
+namespace {
+constexpr int kFoldThreads = 256;
+
+__global__ __launch_bounds__(kFoldThreads) void stem_fold_finish_kernel(
+    const float* __restrict__ img, int hs, int ws, int ho, int wo, const float* __restrict__ tdz,
+    const float* __restrict__ ty, const double* __restrict__ sums, const double* __restrict__ cnt,
+    const float* __restrict__ invstd, const float* __restrict__ w, const float* __restrict__ mean,
+    float* __restrict__ out32, bf16* __restrict__ out16) {
+  constexpr int CH = 16, NQ = 4, CO = kCo, KK = 256;
+  extern __shared__ __attribute__((aligned(16))) char fold_smem[];
+  double* rw = reinterpret_cast<double*>(fold_smem);  // [hs][NQ][CH] row-window sums
+  __shared__ double cols[KK];
+  __shared__ double coef[3][CO];
+  const int tid = threadIdx.x;
+  // phase 1: rw[h][q][c] = sum_{x = q}^{q + wo - 1} img[h][x][c]
+  for (int hc = tid; hc < hs * CH; hc += kFoldThreads) {
+    const int h = hc / CH, c = hc - h * CH;
+    const float* row = img + (int64_t)h * ws * CH + c;
+    double s = 0.0;
+    for (int x = 0; x < wo; ++x) s += (double)row[x * CH];
+    rw[(h * NQ + 0) * CH + c] = s;
+    for (int q = 1; q < NQ; ++q) {
+      s += (double)row[(q + wo - 1) * CH] - (double)row[(q - 1) * CH];
+      rw[(h * NQ + q) * CH + c] = s;
+    }
+  }
+  if (tid < CO) {
+    const double n = cnt[0], is = (double)invstd[tid];
+    const double al = is * (w ? (double)w[tid] : 1.0);
+    const double be = -al * is * is * sums[CO + tid] / n;
+    coef[0][tid] = al;
+    coef[1][tid] = be;
+    coef[2][tid] = -al * sums[tid] / n - be * (double)mean[tid];
+  }
+  __syncthreads();
+  // phase 2: cols[(r*4 + q)*16 + c] = sum_{y = r}^{r + ho - 1} rw[y][q][c]
+  if (tid < NQ * CH) {
+    const int q = tid / CH, c = tid - q * CH;
+    double s = 0.0;
+    for (int y = 0; y < ho; ++y) s += rw[(y * NQ + q) * CH + c];
+    cols[(0 * NQ + q) * CH + c] = s;
+    for (int r = 1; r < NQ; ++r) {
+      s += rw[((r + ho - 1) * NQ + q) * CH + c] - rw[((r - 1) * NQ + q) * CH + c];
+      cols[(r * NQ + q) * CH + c] = s;
+    }
+  }
+  __syncthreads();
+  // phase 3: the weight gradient
+  for (int e = tid; e < CO * KK; e += kFoldThreads) {
+    const int o = e / KK, k = e - o * KK;
+    const double v = coef[0][o] * (double)tdz[e] + coef[1][o] * (double)ty[e] + coef[2][o] * cols[k];
+    if (out16) out16[e] = (bf16)(float)v;
+    else out32[e] = (float)v;
+  }
+}
+}  // namespace
+
+at::Tensor stem_fold_finish(const at::Tensor& img, int64_t ho, int64_t wo, const at::Tensor& t_dz,
+                            const at::Tensor& t_y, const at::Tensor& sums, const at::Tensor& cnt,
+                            const at::Tensor& invstd, const c10::optional<at::Tensor>& weight, const at::Tensor& mean,
+                            at::ScalarType out_dtype) {
+  TORCH_CHECK(img.is_cuda() && img.scalar_type() == at::kFloat && img.dim() == 3 && img.size(2) == 16 &&
+                  img.is_contiguous(), "stem_fold_finish: img must be contiguous fp32 [hs, ws, 16]");
+  const int64_t hs = img.size(0), ws = img.size(1);
+  TORCH_CHECK(ho >= 1 && wo >= 1 && ho + 3 <= hs && wo + 3 <= ws, "stem_fold_finish: window geometry");
+  auto f32 = [&](const at::Tensor& t, int64_t n, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == n &&
+                    t.device() == img.device(), "stem_fold_finish: ", name, " must be contiguous fp32 [", n, "]");
+    return t.data_ptr<float>();
+  };
+  const float* tdz = f32(t_dz, (int64_t)kCo * 256, "t_dz");
+  const float* ty = f32(t_y, (int64_t)kCo * 256, "t_y");
+  const float* is = f32(invstd, kCo, "invstd");
+  const float* mu = f32(mean, kCo, "mean");
+  const float* wp = nullptr;
+  if (weight.has_value() && weight->defined()) wp = f32(*weight, kCo, "weight");
+  TORCH_CHECK(sums.is_cuda() && sums.scalar_type() == at::kDouble && sums.is_contiguous() && sums.numel() >= 2 * kCo,
+              "stem_fold_finish: sums must be fp64 [>= 2 * 64] (sum dz, sum dz (x - mean))");
+  TORCH_CHECK(cnt.is_cuda() && cnt.scalar_type() == at::kDouble && cnt.numel() >= 1, "stem_fold_finish: cnt fp64");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "stem_fold_finish: fp32 or bf16 output");
+  auto out = at::empty({kCo, 256}, img.options().dtype(out_dtype));
+  const size_t lds = (size_t)hs * 4 * 16 * sizeof(double);
+  TORCH_CHECK(lds <= 96 * 1024, "stem_fold_finish: image too tall for the row-window buffer");
+  hipStream_t st = at::hip::getCurrentHIPStream();
+  hipLaunchKernelGGL(stem_fold_finish_kernel, dim3(1), dim3(kFoldThreads), lds, st, img.data_ptr<float>(), (int)hs,
+                     (int)ws, (int)ho, (int)wo, tdz, ty, sums.data_ptr<double>(), cnt.data_ptr<double>(), is, wp, mu,
+                     out_dtype == at::kFloat ? out.data_ptr<float>() : nullptr,
+                     out_dtype == at::kBFloat16 ? reinterpret_cast<bf16*>(out.data_ptr()) : nullptr);
+  DMP_HIP_CHECK(hipGetLastError());
+  return out;
+}
+
 }  // namespace dmp

@@ -332,26 +332,20 @@ class _StemBNReLUMaxPoolFn(torch.autograd.Function):
         if reduce_grads is not None:
             local = sums.clone()  # the reducer works in place
             sums = reduce_grads(sums)
-        cnt = count.reshape(()).double()
         sdz, sdzx = sums[:co], sums[co:]
         istd = invstd.double()
-        al = istd * (w32.double() if w32 is not None else 1.0)
-        be = -al * istd * istd * sdzx / cnt
-        cc = -al * sdz / cnt - be * mean.double()
         rows = lambda t: t.permute(0, 2, 3, 1).reshape(n * ho * wo, co)  # noqa: E731
         t_dz = C.stem_halo_wgrad(rows(dz), s, ho, torch.float32)
         t_y = C.stem_halo_wgrad(rows(y), s, ho, torch.float32)
         # colsum(P)[r*64 + q*16 + ch] = sum over images and output pixels of s[n, ch, oh+r, ow+q]:
-        # the batch sum of the (channels-last) s2d image as one column reduction, then
-        # the 4 x 4 window sums of that small image through 2-D prefix sums
+        # the batch sum of the (channels-last) s2d image as one column reduction; its 4 x 4
+        # window sums (fp64), the BN-backward coefficients al / be / cc and
+        # dW = al t_dz + be t_y + cc colsum(P) in one launch (stem_halo.hip stem_fold_finish)
         hs, ws = s.shape[2], s.shape[3]
         img = s.permute(0, 2, 3, 1).reshape(n, -1).sum(0, dtype=torch.float32).view(hs, ws, -1)
-        pre = torch.nn.functional.pad(img.double().cumsum(0).cumsum(1), (0, 0, 1, 0, 1, 0))  # fp64 prefix sums
-        r4 = torch.arange(4, device=s.device)
-        rows_ = pre[r4 + ho] - pre[r4]                              # [4, ws+1, 16]: rows r .. r+ho-1
-        cols = (rows_[:, r4 + wo] - rows_[:, r4]).reshape(16, -1).float()  # [(r, q), 16]
-        dw = (al.float()[:, None] * t_dz + be.float()[:, None] * t_y
-              + cc.float()[:, None] * cols.reshape(1, -1)).to(mdtype)
+        dw = C.stem_fold_finish(img.contiguous(), ho, wo, t_dz, t_y, sums.contiguous(),
+                                count.reshape(1).to(torch.float64), invstd.float().contiguous(),
+                                None if w32 is None else w32.float().contiguous(), mean.float().contiguous(), mdtype)
         if reduce_grads is not None:
             dg = (local[co:] * invstd.double()).float()
             db = local[:co].float()
