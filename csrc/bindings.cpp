@@ -524,7 +524,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<dmp::ParallelApply, std::shared_ptr<dmp::ParallelApply>>(m, "ParallelApply")
       .def(py::init<>())
       .def("apply", &dmp::ParallelApply::apply, py::arg("modules"), py::arg("inputs"),
-           py::arg("kwargs"), py::arg("devices"))
+           py::arg("kwargs"), py::arg("devices"), py::arg("streams") = std::vector<int64_t>{})
       .def("num_workers", &dmp::ParallelApply::num_workers)
       .def("last_times", &dmp::ParallelApply::last_times);
 

@@ -145,12 +145,14 @@ void ParallelApply::worker_main(Worker* w) {
 }
 
 py::object ParallelApply::apply(const py::list& modules, const py::list& inputs,
-                                const py::list& kwargs, const std::vector<int64_t>& devices) {
+                                const py::list& kwargs, const std::vector<int64_t>& devices,
+                                const std::vector<int64_t>& streams) {
   std::unique_lock<std::mutex> busy(apply_mu_, std::try_to_lock);
   if (!busy.owns_lock()) return py::none();  // re-entered: the caller uses its own threads
   const size_t n = py::len(modules);
   TORCH_CHECK(py::len(inputs) == n && py::len(kwargs) == n && devices.size() == n,
               "parallel_apply: modules, inputs, kwargs and devices must have the same length");
+  TORCH_CHECK(streams.empty() || streams.size() == n, "parallel_apply: one stream handle per replica (or none)");
   if (n == 0) return py::list();
   // caller's thread-local state, captured here (GIL held, calling thread)
   const bool grad = c10::GradMode::is_enabled();
@@ -165,7 +167,11 @@ py::object ParallelApply::apply(const py::list& modules, const py::list& inputs,
     j.kwargs = kwargs[i].is_none() ? py::dict() : py::object(kwargs[i]);
     j.index = (int64_t)i;
     j.device = devices[i];
-    if (j.device >= 0) j.stream = c10::hip::getCurrentHIPStream((c10::DeviceIndex)j.device);
+    if (j.device >= 0) {
+      const int64_t h = streams.empty() ? 0 : streams[i];
+      j.stream = h ? c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(h), (c10::DeviceIndex)j.device)
+                   : c10::hip::getCurrentHIPStream((c10::DeviceIndex)j.device);
+    }
     j.grad_enabled = grad;
     j.autocast = ac;
     j.autocast_dtype = ac_dtype;

@@ -37,8 +37,13 @@ class ParallelApply {
   // Not reentrant: a call made while another is in flight (a second Python
   // thread, or a DataParallel nested inside a replica) returns None at once and
   // the caller falls back to its own threads.
+  // streams[i] (optional, raw hipStream_t handles; 0 = the caller's current
+  // stream of devices[i]): replicas that share a device run on streams of
+  // their own, so their kernels can overlap on the GPU (the Python layer
+  // orders those streams after the caller's and joins them afterwards).
   pybind11::object apply(const pybind11::list& modules, const pybind11::list& inputs,
-                       const pybind11::list& kwargs, const std::vector<int64_t>& devices);
+                       const pybind11::list& kwargs, const std::vector<int64_t>& devices,
+                       const std::vector<int64_t>& streams = {});
   int64_t num_workers() const { return (int64_t)workers_.size(); }
   // Host-time breakdown of the last apply(): [apply wall ms, then per replica
   // (wall ms, ms waiting for the GIL before its module call started,

@@ -400,17 +400,90 @@ def parallel_apply(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=No
             dd = comm_ops._dev(d) if d is not None else None
             devs.append(dd.index if (dd is not None and dd.type == "cuda") else -1)
         ins = [tuple(x) if isinstance(x, (list, tuple)) else (x,) for x in inputs]
-        res = launcher.apply(list(modules), ins, [dict(k) for k in kwargs_tup], devs)
+        side = _alias_streams(devs, ins)
+        handles = [s.cuda_stream if s is not None else 0 for s in side] if side else []
+        res = launcher.apply(list(modules), ins, [dict(k) for k in kwargs_tup], devs, handles)
         if res is None:  # launcher busy (another thread / a nested DataParallel): own threads
+            _join_alias_streams(devs, side, None)
             return _parallel_apply_threads(modules, inputs, kwargs_tup, devices)
         _record_host_times(launcher.last_times())
         outs = []
         for i, (ok, val) in enumerate(res):
             if not ok:
+                _join_alias_streams(devs, side, None)
                 _reraise(i, val)
             outs.append(val)
+        _join_alias_streams(devs, side, outs)
         return outs
     return _parallel_apply_threads(modules, inputs, kwargs_tup, devices)
+
+
+# Replicas that share a GPU (DataParallel over repeated device ids, e.g. the
+# single-GPU rehearsal `bench.py --parallel dp --dp-replicas 4`) run on side
+# streams of their own: with the caller's one stream per device their kernels
+# serialised on the GPU although the launcher runs them on separate host
+# threads.  Each side stream starts after the caller's current stream (the
+# scattered inputs and replicated parameters are ready there) and the caller's
+# stream waits for all of them before gather; autograd then runs each
+# replica's backward on its side stream too and joins it at the end.
+# DMP_DP_ALIAS_STREAMS=0 keeps every replica on the caller's stream.
+_ALIAS_STREAMS = os.environ.get("DMP_DP_ALIAS_STREAMS", "1") != "0"
+_SIDE: Dict[tuple, "torch.cuda.Stream"] = {}
+
+
+def _alias_streams(devs: List[int], ins) -> list:
+    if not _ALIAS_STREAMS or not torch.cuda.is_available():
+        return []
+    seen: Dict[int, int] = {}
+    side: list = []
+    for d in devs:
+        if d < 0:
+            side.append(None)
+            continue
+        k = seen.get(d, 0)
+        seen[d] = k + 1
+        if k == 0:
+            side.append(None)  # the first replica on a device keeps the caller's stream
+            continue
+        st = _SIDE.get((d, k))
+        if st is None:
+            st = _SIDE[(d, k)] = torch.cuda.Stream(device=d)
+        side.append(st)
+    if not any(s is not None for s in side):
+        return []
+    for i, st in enumerate(side):
+        if st is None:
+            continue
+        st.wait_stream(torch.cuda.current_stream(devs[i]))
+        for t in _tensors(ins[i]):  # inputs allocated on the caller's stream, read on the side stream
+            if t.is_cuda:
+                t.record_stream(st)
+    return side
+
+
+def _join_alias_streams(devs: List[int], side: list, outs) -> None:
+    if not side:
+        return
+    for i, st in enumerate(side):
+        if st is None:
+            continue
+        main = torch.cuda.current_stream(devs[i])
+        main.wait_stream(st)
+        if outs is not None:
+            for t in _tensors(outs[i]):  # outputs allocated on the side stream, read on the caller's
+                if t.is_cuda:
+                    t.record_stream(main)
+
+
+def _tensors(obj):
+    if isinstance(obj, torch.Tensor):
+        yield obj
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            yield from _tensors(o)
+    elif isinstance(obj, dict):
+        for o in obj.values():
+            yield from _tensors(o)
 
 
 def _parallel_apply_threads(modules: Sequence[nn.Module], inputs: Sequence, kwargs_tup=None,

@@ -131,22 +131,34 @@ def test_broadcast_and_reduce_add_coalesced():
 
 @pytest.mark.gpu
 def test_native_launcher_propagates_current_stream_and_host_time():
-    """Replicas run on the caller's current stream of their device; the C++
+    """The first replica on a device runs on the caller's current stream of
+    that device; replicas aliased onto the same device run on side streams of
+    their own (ordered after the caller's stream and joined back into it:
+    data_parallel._alias_streams), so their kernels can overlap.  The C++
     launcher (persistent threads) costs less host time than a thread per
     replica per call (the upstream / Python design)."""
     import time
+    from distributed_model_parallel_amd.parallel import data_parallel as dpm
     from distributed_model_parallel_amd.parallel.data_parallel import _parallel_apply_threads
 
     class StreamProbe(nn.Module):
         def forward(self, x):
+            torch.cuda._sleep(200000)  # a slow kernel first: a missing ordering shows up as stale reads
             return x + 1, torch.cuda.current_stream().cuda_stream
 
     side = torch.cuda.Stream()
     mods = [StreamProbe() for _ in range(4)]
-    ins = [(torch.zeros(4, device="cuda"),) for _ in range(4)]
     with torch.cuda.stream(side):
+        ins = [(torch.full((4,), float(i), device="cuda"),) for i in range(4)]
         outs = parallel_apply(mods, ins, devices=[0] * 4)
-    assert all(s == side.cuda_stream for _, s in outs)
+        vals = torch.stack([o for o, _ in outs]).cpu()  # read on the caller's stream
+    assert outs[0][1] == side.cuda_stream
+    streams = [s for _, s in outs]
+    if dpm._ALIAS_STREAMS:
+        assert len(set(streams)) == 4, streams
+    else:
+        assert all(s == side.cuda_stream for s in streams)
+    assert torch.equal(vals, torch.arange(4.0)[:, None].expand(4, 4) + 1)
 
     def host_us(fn, reps=200):
         for _ in range(10):
