@@ -309,6 +309,75 @@ __global__ __launch_bounds__(kPoolThreads) void bnpool_fwd_kernel(
   *reinterpret_cast<uint64_t*>(idx + pix * g.C + c0) = w;
 }
 
+// Two vertically adjacent output rows per thread (K = 3, S = 2): the five
+// input rows they span are loaded once (15 taps for 2 outputs instead of 18),
+// as raw bf16 vectors all in flight together, then normalised and pooled.
+template <int K, int S>
+__global__ __launch_bounds__(kPoolThreads) void bnpool_fwd2_kernel(
+    const __bf16* __restrict__ x, const float* __restrict__ sc, const float* __restrict__ sh,
+    __bf16* __restrict__ y, uint8_t* __restrict__ idx, PoolGeo g, int row_len) {
+  static_assert(K == 3 && S == 2, "two-row stem pool: 3x3 / stride 2");
+  constexpr int VEC = 8, NR = K + S;  // 5 input rows
+  const int j = blockIdx.y * blockDim.x + threadIdx.x;
+  if (j >= row_len) return;
+  const int prow = blockIdx.x;           // output row pair
+  const int hp = (g.Ho + 1) / 2;
+  const int n = prow / hp, oh0 = (prow - n * hp) * 2;
+  const int ow = j / g.cv, cvi = j - ow * g.cv;
+  const int c0 = cvi * VEC;
+  const int h0 = oh0 * S - g.p, w0 = ow * S - g.p;
+  const __bf16* xn = x + (int64_t)n * g.H * g.W * g.C + c0;
+  bf16x8 raw[NR][K];
+#pragma unroll
+  for (int a = 0; a < NR; ++a) {
+    const int ih = min(max(h0 + a, 0), g.H - 1);
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      const int iw = min(max(w0 + b, 0), g.W - 1);
+      raw[a][b] = *reinterpret_cast<const bf16x8*>(xn + ((int64_t)ih * g.W + iw) * g.C);
+    }
+  }
+  float s8[VEC], t8[VEC];
+  {
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(sc + c0), s1 = *reinterpret_cast<const f32x4*>(sc + c0 + 4);
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(sh + c0), t1 = *reinterpret_cast<const f32x4*>(sh + c0 + 4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) { s8[c] = s0[c]; s8[c + 4] = s1[c]; t8[c] = t0[c]; t8[c + 4] = t1[c]; }
+  }
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int oh = oh0 + r;
+    if (oh >= g.Ho) break;
+    const int hr = h0 + r * S;
+    const uint8_t tap0 = (uint8_t)(max(0, -hr) * K + max(0, -w0));
+    float m[VEC];
+    uint8_t am[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) { m[c] = -INFINITY; am[c] = tap0; }
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      const bool ha = (unsigned)(hr + a) < (unsigned)g.H;
+#pragma unroll
+      for (int b = 0; b < K; ++b) {
+        const bool ok = ha && (unsigned)(w0 + b) < (unsigned)g.W;
+        const f32x8 v = __builtin_convertvector(raw[r * S + a][b], f32x8);
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) {
+          // the BN+ReLU output as the unfused apply pass would have stored it
+          const float t = (float)(__bf16)fmaxf(fmaf(v[c], s8[c], t8[c]), 0.f);
+          if (ok && (t > m[c] || (t != t && m[c] == m[c]))) { m[c] = t; am[c] = (uint8_t)(a * K + b); }
+        }
+      }
+    }
+    const int64_t pix = ((int64_t)n * g.Ho + oh) * g.Wo + ow;
+    Vec16<__bf16>::store(y + pix * g.C + c0, m);
+    uint64_t w = 0;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) w |= (uint64_t)am[c] << (8 * c);
+    *reinterpret_cast<uint64_t*>(idx + pix * g.C + c0) = w;
+  }
+}
+
 template <int K, int S>
 __global__ __launch_bounds__(kPoolThreads) void bnpool_bwd_kernel(
     const __bf16* __restrict__ dy, const uint8_t* __restrict__ idx, const __bf16* __restrict__ x,
@@ -542,10 +611,18 @@ std::vector<at::Tensor> maxpool2d_bn_forward(const at::Tensor& x, const at::Tens
   auto idx = at::empty({(int64_t)g.N * g.Ho * g.Wo * g.C}, x.options().dtype(at::kByte));
   const int row_len = g.Wo * g.cv;
   if ((int64_t)g.N * g.Ho * row_len == 0) return {y, idx};
-  const dim3 blocks((unsigned)(g.N * g.Ho), (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads));
-  hipLaunchKernelGGL((bnpool_fwd_kernel<3, 2>), blocks, dim3(kPoolThreads), 0, at::hip::getCurrentHIPStream(),
-                     reinterpret_cast<const __bf16*>(x.data_ptr()), scale.data_ptr<float>(), shift.data_ptr<float>(),
-                     reinterpret_cast<__bf16*>(y.data_ptr()), idx.data_ptr<uint8_t>(), g, row_len);
+  static const bool one_row = [] { const char* e = std::getenv("DMP_POOL_FWD1"); return e && e[0] == '1'; }();
+  if (one_row) {  // A/B: one output row per thread
+    const dim3 blocks((unsigned)(g.N * g.Ho), (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads));
+    hipLaunchKernelGGL((bnpool_fwd_kernel<3, 2>), blocks, dim3(kPoolThreads), 0, at::hip::getCurrentHIPStream(),
+                       reinterpret_cast<const __bf16*>(x.data_ptr()), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                       reinterpret_cast<__bf16*>(y.data_ptr()), idx.data_ptr<uint8_t>(), g, row_len);
+  } else {
+    const dim3 blocks((unsigned)(g.N * ((g.Ho + 1) / 2)), (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads));
+    hipLaunchKernelGGL((bnpool_fwd2_kernel<3, 2>), blocks, dim3(kPoolThreads), 0, at::hip::getCurrentHIPStream(),
+                       reinterpret_cast<const __bf16*>(x.data_ptr()), scale.data_ptr<float>(), shift.data_ptr<float>(),
+                       reinterpret_cast<__bf16*>(y.data_ptr()), idx.data_ptr<uint8_t>(), g, row_len);
+  }
   DMP_HIP_CHECK(hipGetLastError());
   return {y, idx};
 }
