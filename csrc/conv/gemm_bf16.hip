@@ -53,6 +53,9 @@ using bf16 = __bf16;
 constexpr int BK = 64;
 constexpr int kThreads = 256;
 
+// zeros an absent per-column coefficient vector is read from (branch-free epilogue loads)
+__device__ __attribute__((aligned(32))) float g_nt_zero[16] = {};
+
 enum Epi { EPI_STORE = 0, EPI_MOMENTS = 1, EPI_AFFINE = 2, EPI_BNBWD = 3,
            // EPI_BNBWD with the mask taken from the BN output y, fixed at compile
            // time (with / without the x moments); plain EPI_BNBWD = mask from x
@@ -352,20 +355,41 @@ void gemm_nt_kernel(const NtArgs p) {
   // of each 16 x 16 block -> one 8-B LDS write per block (host: N % 8 == 0, so
   // a 4-column group is wholly in or out; coefficient vectors 16-B aligned).
   // Residual / activation are applied in the row-contiguous store pass.
+  // every per-column coefficient first, with branch-free loads (an absent
+  // vector reads zeros, columns past N read column N - 4, selects pick the
+  // defaults): a load under a runtime condition made the compiler wait for
+  // each one before the next -- 4-8 dependent round trips per tile.  The
+  // BN-backward constants of the store pass go out in the same batch.
+  constexpr int CVS = BN / 8;
+  const int colb = n0 + (tid % CVS) * 8;
+  const int colbc = min(colb, N - 8);
+  f32x4 csa[NI], cba[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int gcc = min(n0 + wn * WTN + j * 16 + (lane >> 4) * 4, N - 4);
+    f32x4 cs = {1.f, 1.f, 1.f, 1.f}, cb = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (EPI == EPI_AFFINE) {
+      const f32x4 sl = *reinterpret_cast<const f32x4*>(epi_s ? epi_s + gcc : g_nt_zero);
+      cs = epi_s ? sl : cs;
+      cb = *reinterpret_cast<const f32x4*>(epi_t ? epi_t + gcc : g_nt_zero);
+    }
+    if constexpr (nt_bnbwd(EPI)) cb = *reinterpret_cast<const f32x4*>(p.ebias ? p.ebias + gcc : g_nt_zero);
+    csa[j] = cs;
+    cba[j] = cb;
+  }
+  f32x8 bmu8 = {}, biv8 = {}, bw8 = {}, bb8 = {};
+  if constexpr (nt_bnbwd(EPI)) {
+    bmu8 = *reinterpret_cast<const f32x8*>(p.bmean ? p.bmean + colbc : g_nt_zero);
+    if constexpr (EPI == EPI_BNBWD) {
+      biv8 = *reinterpret_cast<const f32x8*>(p.binv ? p.binv + colbc : g_nt_zero);
+      bw8 = *reinterpret_cast<const f32x8*>(p.bw ? p.bw + colbc : g_nt_zero);
+      bb8 = *reinterpret_cast<const f32x8*>(p.bb ? p.bb + colbc : g_nt_zero);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const int lc = wn * WTN + j * 16 + (lane >> 4) * 4;
-    const int gc = n0 + lc;
-    f32x4 cs = {1.f, 1.f, 1.f, 1.f}, cb = {0.f, 0.f, 0.f, 0.f};
-    if (gc < N) {
-      if constexpr (EPI == EPI_AFFINE) {
-        if (epi_s) cs = *reinterpret_cast<const f32x4*>(epi_s + gc);
-        if (epi_t) cb = *reinterpret_cast<const f32x4*>(epi_t + gc);
-      }
-      if constexpr (nt_bnbwd(EPI)) {
-        if (p.ebias) cb = *reinterpret_cast<const f32x4*>(p.ebias + gc);
-      }
-    }
+    const f32x4 cs = csa[j], cb = cba[j];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int row = wm * WTM + i * 16 + (lane & 15);
@@ -380,25 +404,25 @@ void gemm_nt_kernel(const NtArgs p) {
   // ---- store pass: each thread moves 8 contiguous columns of a row ----
   constexpr int CV = BN / 8;                  // 16-B vectors per row
   constexpr int RPP = kThreads / CV;          // rows per pass
-  constexpr bool kMom = EPI == EPI_MOMENTS || nt_bnbwd(EPI);
-  static_assert(!kMom || 2 * RPP * BN * 4 <= LDS_BYTES, "moments scratch exceeds LDS");
   const int cvi = tid % CV, rr0 = tid / CV;
   const int col = n0 + cvi * 8;
   const bool col_ok = col < N;
-  float msum[8], msq[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; }
-  float bmu[8], bsc[8], bsh[8];
   const bf16* __restrict__ bnx = p.bx;
   const bf16* __restrict__ bny = p.bny;
   const int64_t ldbx = p.ldbx, ldby = p.ldby;
   const CompactMap rmap = p.rmap;
+  constexpr bool kMom = EPI == EPI_MOMENTS || nt_bnbwd(EPI);
+  static_assert(!kMom || 2 * RPP * BN * 4 <= LDS_BYTES, "moments scratch exceeds LDS");
+  float msum[8], msq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { msum[j] = 0.f; msq[j] = 0.f; }
+  float bmu[8], bsc[8], bsh[8];
   if constexpr (nt_bnbwd(EPI)) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      bmu[j] = (col_ok && p.bmean) ? p.bmean[col + j] : 0.f;
-      bsc[j] = (EPI == EPI_BNBWD && col_ok) ? p.binv[col + j] * (p.bw ? p.bw[col + j] : 1.f) : 0.f;
-      bsh[j] = (EPI == EPI_BNBWD && col_ok) ? (p.bb ? p.bb[col + j] : 0.f) - bmu[j] * bsc[j] : 0.f;
+      bmu[j] = bmu8[j];
+      bsc[j] = EPI == EPI_BNBWD ? biv8[j] * (p.bw ? bw8[j] : 1.f) : 0.f;
+      bsh[j] = EPI == EPI_BNBWD ? bb8[j] - bmu[j] * bsc[j] : 0.f;
     }
   }
   // Phase 1 issues every global operand load of the tile's row passes
