@@ -37,6 +37,10 @@
 namespace dmp {
 namespace {
 
+// ones / zeros an absent BN weight / bias is read from (branch-free loads)
+__device__ float g_bn_ones[16] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+__device__ float g_bn_zeros[16] = {};
+
 constexpr int kThreads = 256;
 
 struct Layout {
@@ -452,15 +456,33 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
   if (lr >= L.rpi || cvec >= L.cv) return;
   const double n = *count_ptr;
   float a[VEC], b[VEC], c[VEC], msc[VEC], msh[VEC];
+  // per-channel constants: every load issued up front and branch-free (an
+  // absent weight / bias reads ones / zeros) -- a `weight ? weight[ch] : 1`
+  // per element made the compiler wait for each load before the next, eight
+  // dependent round trips before a block's first row
+  const int ch0 = cvec * VEC;
+  const float* wp = weight ? weight + ch0 : g_bn_ones;
+  const float* bp = bias ? bias + ch0 : g_bn_zeros;
+  float wv[VEC], bv[VEC], isv[VEC], muv[VEC];
+  double s1[VEC], s2[VEC];
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
-    const int ch = cvec * VEC + i;
-    const double sdz = sums[ch], sdzx = sums[C + ch];
-    const double is = invstd[ch];
-    const double aa = (double)(weight ? weight[ch] : 1.f) * is;
+    wv[i] = wp[i];
+    bv[i] = bp[i];
+    isv[i] = invstd[ch0 + i];
+    muv[i] = mean[ch0 + i];
+    s1[i] = sums[ch0 + i];
+    s2[i] = sums[C + ch0 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    const int ch = ch0 + i;
+    const double sdz = s1[i], sdzx = s2[i];
+    const double is = isv[i];
+    const double aa = (double)wv[i] * is;
     if (RELU == 2) {  // the forward's affine, as in bn_bwd_moments_kernel
-      msc[i] = (weight ? weight[ch] : 1.f) * invstd[ch];
-      msh[i] = (bias ? bias[ch] : 0.f) - mean[ch] * msc[i];
+      msc[i] = wv[i] * isv[i];
+      msh[i] = bv[i] - muv[i] * msc[i];
     } else {
       msc[i] = msh[i] = 0.f;
     }
@@ -468,7 +490,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       const double bb = -aa * is * is * sdzx / n;
       a[i] = (float)aa;
       b[i] = (float)bb;
-      c[i] = (float)(-aa * sdz / n - bb * (double)mean[ch]);
+      c[i] = (float)(-aa * sdz / n - bb * (double)muv[i]);
     } else {
       a[i] = (float)aa;
       b[i] = 0.f;

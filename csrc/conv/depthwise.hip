@@ -48,6 +48,32 @@ struct Geo {
 template <typename T>
 __device__ __forceinline__ void ldv(const T* p, float (&v)[Vec16<T>::N]) { Vec16<T>::load(p, v); }
 
+// Window loads are issued unconditionally from clamped addresses and the
+// out-of-range ones zeroed afterwards (a select, not a branch): a load under a
+// per-column branch is waited for before the next one is issued, which made
+// every column of the 3 x (TW+2) window a full memory round trip (ISA showed
+// 18-54 serialized load -> vmcnt(0) pairs per kernel).
+template <typename T>
+__device__ __forceinline__ typename Vec16<T>::raw ldraw(const T* p) {
+  return *reinterpret_cast<const typename Vec16<T>::raw*>(p);
+}
+
+template <typename T>
+__device__ __forceinline__ void cvt_masked(typename Vec16<T>::raw r, bool ok, float (&v)[Vec16<T>::N]) {
+  using R = typename Vec16<T>::raw;
+  r = ok ? r : R{};
+  if constexpr (Vec16<T>::N == 8) {
+    const f32x8 f = __builtin_convertvector(r, f32x8);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = f[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = r[i];
+  }
+}
+
+__device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
+
 // ---------------------------------------------------------------------------
 // forward: y[n,oh,ow,c] = sum_{kh,kw} x[n, oh*s-1+kh, ow*s-1+kw, c] * w[kh,kw,c]
 // grid.x = ceil(N*OH*strips / spp), grid.y = channel chunks
@@ -89,20 +115,21 @@ __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ 
     for (int o = 0; o < TW; ++o)
 #pragma unroll
       for (int j = 0; j < VEC; ++j) acc[o][j] = 0.f;
-    constexpr int MAXW = (TW - 1) * 2 + 3;  // input columns touched (stride <= 2)
+    constexpr int NCI = (TW - 1) * S + 3;  // input columns touched
+    const int iw0 = ow0 * S - 1;
 #pragma unroll
     for (int kh = 0; kh < 3; ++kh) {
       const int ih = oh * S - 1 + kh;
       if (ih < 0 || ih >= g.H) continue;
       const T* row = x + (((int64_t)n * g.H + ih) * g.W) * g.C + c0;
-      const int iw0 = ow0 * S - 1;
+      typename Vec16<T>::raw raw[NCI];
 #pragma unroll
-      for (int ci = 0; ci < MAXW; ++ci) {
+      for (int ci = 0; ci < NCI; ++ci) raw[ci] = ldraw<T>(row + (int64_t)clampi(iw0 + ci, g.W - 1) * g.C);
+#pragma unroll
+      for (int ci = 0; ci < NCI; ++ci) {
         const int iw = iw0 + ci;
-        if (ci >= (TW - 1) * S + 3) break;
-        if (iw < 0 || iw >= g.W) continue;
         float v[VEC];
-        ldv<T>(row + (int64_t)iw * g.C, v);
+        cvt_masked<T>(raw[ci], iw >= 0 && iw < g.W, v);
 #pragma unroll
         for (int o = 0; o < TW; ++o) {
           const int kw = ci - o * S;
@@ -155,7 +182,7 @@ __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ 
 // ow = (iw+1-kw)/s integral and in range of dy[n,oh,ow,c] * w[kh,kw,c].
 // One lane: 8 channels x TW consecutive input columns of one input row.
 // ---------------------------------------------------------------------------
-template <typename T>
+template <typename T, int S>
 __global__ __launch_bounds__(kThreads) void dw_dgrad_kernel(const T* __restrict__ dy,
                                                            const float* __restrict__ w9,
                                                            T* __restrict__ dx, Geo g,
@@ -184,44 +211,33 @@ __global__ __launch_bounds__(kThreads) void dw_dgrad_kernel(const T* __restrict_
   for (int o = 0; o < TW; ++o)
 #pragma unroll
     for (int j = 0; j < VEC; ++j) acc[o][j] = 0.f;
+  static_assert(TW % 2 == 0, "stride-2 column mapping assumes an even strip start");
+  // stride 1: output columns iw0-1 .. iw0+TW feed the strip; stride 2: only
+  // the even taps hit, output columns iw0/2 .. iw0/2+2
+  constexpr int NCO = S == 1 ? TW + 2 : TW / 2 + 1;
+  const int owb = S == 1 ? iw0 - 1 : iw0 / 2;
 #pragma unroll
   for (int kh = 0; kh < 3; ++kh) {
     const int th = ih + 1 - kh;
-    if (th < 0 || th % g.stride) continue;
-    const int oh = th / g.stride;
+    if (th < 0 || th % S) continue;
+    const int oh = th / S;
     if (oh >= g.OH) continue;
     const T* row = dy + (((int64_t)n * g.OH + oh) * g.OW) * g.C + c0;
-    if (g.stride == 1) {
-      // output columns iw0-1 .. iw0+TW feed this strip
+    typename Vec16<T>::raw raw[NCO];
 #pragma unroll
-      for (int ci = 0; ci < TW + 2; ++ci) {
-        const int ow = iw0 - 1 + ci;
-        if (ow < 0 || ow >= g.OW) continue;
-        float v[VEC];
-        ldv<T>(row + (int64_t)ow * g.C, v);
+    for (int ci = 0; ci < NCO; ++ci) raw[ci] = ldraw<T>(row + (int64_t)clampi(owb + ci, g.OW - 1) * g.C);
 #pragma unroll
-        for (int o = 0; o < TW; ++o) {
-          const int kw = o + 1 - (ci - 1);  // iw = ow - 1 + kw  ->  kw = iw + 1 - ow
-          if (kw < 0 || kw > 2) continue;
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) acc[o][j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[o][j]);
-        }
-      }
-    } else {
+    for (int ci = 0; ci < NCO; ++ci) {
+      const int ow = owb + ci;
+      float v[VEC];
+      cvt_masked<T>(raw[ci], ow >= 0 && ow < g.OW, v);
 #pragma unroll
       for (int o = 0; o < TW; ++o) {
-        const int iw = iw0 + o;
+        // iw = ow*S - 1 + kw  ->  kw = iw0 + o + 1 - ow*S
+        const int kw = S == 1 ? o + 1 - (ci - 1) : o + 1 - 2 * ci;
+        if (kw < 0 || kw > 2) continue;
 #pragma unroll
-        for (int kw = 0; kw < 3; ++kw) {
-          const int tw = iw + 1 - kw;
-          if (tw < 0 || tw % g.stride) continue;
-          const int ow = tw / g.stride;
-          if (ow >= g.OW) continue;
-          float v[VEC];
-          ldv<T>(row + (int64_t)ow * g.C, v);
-#pragma unroll
-          for (int j = 0; j < VEC; ++j) acc[o][j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[o][j]);
-        }
+        for (int j = 0; j < VEC; ++j) acc[o][j] = fmaf(v[j], wr[kh * 3 + kw][j], acc[o][j]);
       }
     }
   }
@@ -264,27 +280,29 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(const T* __restrict_
       const int n = (int)(nr / g.OH);
       const int ow0 = st * TW;
       float gv[TW][VEC];
+      {
+        const T* grow = dy + (((int64_t)n * g.OH + oh) * g.OW) * g.C + c0;
+        typename Vec16<T>::raw graw[TW];
 #pragma unroll
-      for (int o = 0; o < TW; ++o) {
-        const int ow = ow0 + o;
-        if (ow < g.OW) ldv<T>(dy + (((int64_t)n * g.OH + oh) * g.OW + ow) * g.C + c0, gv[o]);
-        else
+        for (int o = 0; o < TW; ++o) graw[o] = ldraw<T>(grow + (int64_t)min(ow0 + o, g.OW - 1) * g.C);
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) gv[o][j] = 0.f;
+        for (int o = 0; o < TW; ++o) cvt_masked<T>(graw[o], ow0 + o < g.OW, gv[o]);
       }
+      constexpr int NCI = (TW - 1) * S + 3;
+      const int iw0 = ow0 * S - 1;
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const int ih = oh * S - 1 + kh;
         if (ih < 0 || ih >= g.H) continue;
         const T* row = x + (((int64_t)n * g.H + ih) * g.W) * g.C + c0;
-        const int iw0 = ow0 * S - 1;
+        typename Vec16<T>::raw raw[NCI];
 #pragma unroll
-        for (int ci = 0; ci < (TW - 1) * 2 + 3; ++ci) {
-          if (ci >= (TW - 1) * S + 3) break;
+        for (int ci = 0; ci < NCI; ++ci) raw[ci] = ldraw<T>(row + (int64_t)clampi(iw0 + ci, g.W - 1) * g.C);
+#pragma unroll
+        for (int ci = 0; ci < NCI; ++ci) {
           const int iw = iw0 + ci;
-          if (iw < 0 || iw >= g.W) continue;
           float v[VEC];
-          ldv<T>(row + (int64_t)iw * g.C, v);
+          cvt_masked<T>(raw[ci], iw >= 0 && iw < g.W, v);
 #pragma unroll
           for (int o = 0; o < TW; ++o) {
             const int kw = ci - o * S;
@@ -429,7 +447,7 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
   dim3 grid((unsigned)((total + g.spp - 1) / g.spp), (unsigned)cchunks);
   dispatch_t(dy, [&](auto tag) {
     using T = decltype(tag);
-    hipLaunchKernelGGL((dw_dgrad_kernel<T>), grid, dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((g.stride == 1 ? dw_dgrad_kernel<T, 1> : dw_dgrad_kernel<T, 2>), grid, dim3(kThreads), 0, stream,
                        reinterpret_cast<const T*>(dy.data_ptr()), w9.data_ptr<float>(),
                        reinterpret_cast<T*>(shape_x.data_ptr()), g, istrips);
   });

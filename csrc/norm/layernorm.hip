@@ -113,29 +113,27 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
   const int nv = D / 8;
   const int64_t wave = ((int64_t)blockIdx.x * (kLnThreads / 64) + (threadIdx.x >> 6)) * RPW + sub;
   const int64_t nwaves = (int64_t)gridDim.x * (kLnThreads / 64) * RPW;
+  // w / b are never null (the host passes ones / zeros for an absent one) and
+  // every load below goes to a clamped valid address with no branch around
+  // it: a load under a lane- or row-guard is waited for before the next one
+  // issues (the ISA had 8 serialized load -> vmcnt(0) round trips per row).
   float gw[kMaxV][8], gb[kMaxV][8];
 #pragma unroll
   for (int k = 0; k < kMaxV; ++k) {
-    const int c = lane + LPR * k;
-    if (c < nv) {
-      if (w) PVec<P>::load(w + c * 8, gw[k]);
-      else for (int i = 0; i < 8; ++i) gw[k][i] = 1.f;
-      if (b) PVec<P>::load(b + c * 8, gb[k]);
-      else for (int i = 0; i < 8; ++i) gb[k][i] = 0.f;
-    }
+    const int c = min(lane + LPR * k, nv - 1);
+    PVec<P>::load(w + c * 8, gw[k]);
+    PVec<P>::load(b + c * 8, gb[k]);
   }
   // the next row's vectors are loaded before this row is reduced and written
   // (as ln_bwd_kernel): one row of loads always in flight per wave instead of
   // a dependent HBM round trip at the head of every row
   Raw8<T> nx[kMaxV];
   auto fetch = [&](int64_t r) {
+    const T* xr = x + min(r, rows - 1) * D;
 #pragma unroll
-    for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + LPR * k;
-      if (c < nv) nx[k].load(x + r * D + c * 8);
-    }
+    for (int k = 0; k < kMaxV; ++k) nx[k].load(xr + min(lane + LPR * k, nv - 1) * 8);
   };
-  if (wave < rows) fetch(wave);
+  fetch(wave);
   for (int64_t r = wave; r < rows; r += nwaves) {
     float v[kMaxV][8];
     float s = 0.f;
@@ -148,7 +146,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_fwd_kernel(const T* __restrict_
         for (int i = 0; i < 8; ++i) s += v[k][i];
       }
     }
-    if (r + nwaves < rows) fetch(r + nwaves);
+    fetch(r + nwaves);
     const float mean = group_sum<LPR>(s) / (float)D;
     float q = 0.f;
 #pragma unroll
@@ -201,25 +199,27 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
   for (int k = 0; k < kMaxV; ++k) {
     const int c = lane + LPR * k;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { accw[k][i] = 0.f; accb[k][i] = 0.f; gw[k][i] = 1.f; }
-    if (c < nv && w) PVec<P>::load(w + c * 8, gw[k]);
+    for (int i = 0; i < 8; ++i) { accw[k][i] = 0.f; accb[k][i] = 0.f; }
+    PVec<P>::load(w + min(c, nv - 1) * 8, gw[k]);  // never null (see ln_fwd_kernel)
   }
   Raw8<T> nx[kMaxV], ndy[kMaxV], nres[kMaxV];
   float nmean = 0.f, nrstd = 0.f;
-  auto fetch = [&](int64_t r) {
+  auto fetch = [&](int64_t r) {  // clamped, branch-free loads (see ln_fwd_kernel)
+    r = min(r, rows - 1);
     nmean = mean_in[r];
     nrstd = rstd_in[r];
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
-      const int c = lane + LPR * k;
-      if (c < nv) {
-        nx[k].load(x + r * D + c * 8);
-        ndy[k].load(dy + r * D + c * 8);
-        if (dres) nres[k].load(dres + r * D + c * 8);
-      }
+      const int64_t o = r * D + min(lane + LPR * k, nv - 1) * 8;
+      nx[k].load(x + o);
+      ndy[k].load(dy + o);
+    }
+    if (dres) {
+#pragma unroll
+      for (int k = 0; k < kMaxV; ++k) nres[k].load(dres + r * D + min(lane + LPR * k, nv - 1) * 8);
     }
   };
-  if (wave < rows) fetch(wave);
+  fetch(wave);
   for (int64_t r = wave; r < rows; r += nwaves) {
     const float mean = nmean, rstd = nrstd;
     float xh[kMaxV][8], g[kMaxV][8], rv[kMaxV][8];
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kLnThreads) void ln_bwd_kernel(
         }
       }
     }
-    if (r + nwaves < rows) fetch(r + nwaves);  // next row in flight during the reduce + store
+    fetch(r + nwaves);  // next row in flight during the reduce + store
     const float c1 = group_sum<LPR>(s1) / (float)D, c2 = group_sum<LPR>(s2) / (float)D;
 #pragma unroll
     for (int k = 0; k < kMaxV; ++k) {
@@ -322,12 +322,15 @@ std::vector<at::Tensor> layernorm_forward(const at::Tensor& x, const c10::option
   if (rows == 0) return {y, mean, rstd};
   auto stream = at::hip::getCurrentHIPStream();
   const bool pbf = (hw && w->scalar_type() == at::kBFloat16) || (!hw && hb && b->scalar_type() == at::kBFloat16);
+  // an absent weight / bias is passed as ones / zeros (branch-free kernel loads)
+  const auto popt = x.options().dtype(pbf ? at::kBFloat16 : at::kFloat);
+  const at::Tensor wt = hw ? *w : at::ones({D}, popt), bt = hb ? *b : at::zeros({D}, popt);
   const dim3 grid(ln_blocks(rows)), block(kLnThreads);
 #define DMP_LN_FWD(T, P)                                                                       \
   hipLaunchKernelGGL((D == 768 ? ln_fwd_kernel<T, P, 3, 2> : D <= 1024 ? ln_fwd_kernel<T, P, 2> : ln_fwd_kernel<T, P, 4>), grid, block, 0, stream, \
                      reinterpret_cast<const T*>(x.data_ptr()),                                 \
-                     hw ? reinterpret_cast<const P*>(w->data_ptr()) : nullptr,                 \
-                     hb ? reinterpret_cast<const P*>(b->data_ptr()) : nullptr, rows, (int)D,   \
+                     reinterpret_cast<const P*>(wt.data_ptr()),                                \
+                     reinterpret_cast<const P*>(bt.data_ptr()), rows, (int)D,                  \
                      (float)eps, reinterpret_cast<T*>(y.data_ptr()), mean.data_ptr<float>(),   \
                      rstd.data_ptr<float>())
   if (x.scalar_type() == at::kBFloat16) {
@@ -365,11 +368,12 @@ std::vector<at::Tensor> layernorm_backward(const at::Tensor& dy, const at::Tenso
   const int nb = ln_blocks(rows, 1024);
   auto part = at::empty({nb, 2 * D}, x.options().dtype(at::kFloat));
   const bool pbf = hw && w->scalar_type() == at::kBFloat16;
+  const at::Tensor wt = hw ? *w : at::ones({D}, x.options().dtype(at::kFloat));  // see forward
 #define DMP_LN_BWD(T, P)                                                                        \
   hipLaunchKernelGGL((D == 768 ? ln_bwd_kernel<T, P, 3, 2> : D <= 1024 ? ln_bwd_kernel<T, P, 2> : ln_bwd_kernel<T, P, 4>), dim3(nb), dim3(kLnThreads), 0, stream, \
                      reinterpret_cast<const T*>(dy.data_ptr()),                                 \
                      reinterpret_cast<const T*>(x.data_ptr()),                                  \
-                     hw ? reinterpret_cast<const P*>(w->data_ptr()) : nullptr,                  \
+                     reinterpret_cast<const P*>(wt.data_ptr()),                                 \
                      mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, (int)D,               \
                      reinterpret_cast<T*>(dx.data_ptr()), part.data_ptr<float>(),             \
                      hr ? reinterpret_cast<const T*>(dres->data_ptr()) : nullptr)

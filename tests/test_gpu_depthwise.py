@@ -13,7 +13,8 @@ DEV = "cuda"
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("N,C,H,W,stride", [(4, 96, 32, 32, 1), (3, 144, 32, 32, 2), (2, 960, 4, 4, 1),
-                                            (5, 8, 9, 7, 2), (2, 24, 7, 9, 1), (1, 384, 8, 8, 2)])
+                                            (5, 8, 9, 7, 2), (2, 24, 7, 9, 1), (1, 384, 8, 8, 2),
+                                            (2, 16, 1, 1, 1), (2, 16, 2, 3, 2), (3, 40, 6, 10, 2)])
 def test_depthwise_fwd_bwd(dtype, N, C, H, W, stride):
     torch.manual_seed(0)
     x = torch.randn(N, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)

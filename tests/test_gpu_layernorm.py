@@ -58,3 +58,34 @@ def test_vit_block_residual_grad_fused_into_layernorm():
     assert _STATS["fused_residual_grad"] == n0 + 2
     err = (xa.grad.float() - xb.grad.float()).norm() / xb.grad.float().norm()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("has_w,has_b", [(False, False), (True, False), (False, True)])
+def test_layernorm_absent_affine(has_w, has_b):
+    """An absent weight / bias reaches the kernel as ones / zeros."""
+    torch.manual_seed(0)
+    d = 768
+    x = torch.randn(6, 33, d, device="cuda").bfloat16()
+    w = (torch.rand(d, device="cuda") + 0.5).requires_grad_() if has_w else None
+    b = torch.randn(d, device="cuda").requires_grad_() if has_b else None
+    xi = x.detach().requires_grad_()
+    y = layer_norm(xi, (d,), w, b, 1e-5)
+    xr = x.detach().float().requires_grad_()
+    yr = F.layer_norm(xr, (d,), w, None, 1e-5)  # stock ROCm backward rejects (None, bias)
+    if has_b:
+        yr = yr + b
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+    g = torch.randn_like(yr)
+    y.backward(g.bfloat16())
+    wg = w.grad.clone() if has_w else None
+    if has_w:
+        w.grad = None
+    if has_b:
+        bg = b.grad.clone()
+        b.grad = None
+    yr.backward(g.bfloat16().float())
+    torch.testing.assert_close(xi.grad.float(), xr.grad, atol=6e-2, rtol=3e-2)
+    if has_w:
+        torch.testing.assert_close(wg, w.grad, atol=0.5, rtol=2e-2)
+    if has_b:
+        torch.testing.assert_close(bg, b.grad, atol=0.5, rtol=2e-2)
