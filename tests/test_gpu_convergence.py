@@ -53,12 +53,16 @@ def _lr(lr, i):
 
 def _ensure_pg():
     import torch.distributed as dist
-    if not dist.is_initialized():
-        import socket
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    if not dist.is_initialized():  # one rank: an in-process store, no TCP port to race for
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _destroy_pg():
+    yield
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def _train_native(model, xs, ys, steps, batch, lr):

@@ -7,7 +7,6 @@ schedule, fused cross-entropy, stats returned without a host sync), and the
 RCCL send/recv path itself as a grouped self-exchange through the native
 communicator (the same ncclSend/ncclRecv pair every pipeline hop issues).
 """
-import socket
 
 import pytest
 import torch
@@ -18,11 +17,17 @@ pytestmark = pytest.mark.gpu
 
 
 def _pg():
-    if not dist.is_initialized():
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    import torch.distributed as dist
+    if not dist.is_initialized():  # one rank: an in-process store, no TCP port to race for
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _destroy_pg():
+    yield
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
 
 
 def _comm():
