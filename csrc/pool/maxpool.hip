@@ -641,6 +641,8 @@ std::vector<at::Tensor> maxpool2d_bn_backward(const at::Tensor& dy, const at::Te
   TORCH_CHECK(idx.numel() == dy.numel() && idx.scalar_type() == at::kByte, "bad argmax tensor");
   auto dz = at::empty_like(x, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto sums = at::empty({2 * (int64_t)g.C + 1}, x.options().dtype(at::kDouble));
+  // (one thread per 2 x 2 input quad -- a quarter of the dy / argmax loads --
+  // measured 2.54 vs 2.15 ms at batch 2048 with 164 VGPRs; profiles finding 68)
   const int row_len = g.W * g.cv;
   const int rows = g.N * g.H;
   const unsigned gx = (unsigned)std::min(rows, 1024), gy = (unsigned)((row_len + kPoolThreads - 1) / kPoolThreads);
@@ -653,7 +655,8 @@ std::vector<at::Tensor> maxpool2d_bn_backward(const at::Tensor& dy, const at::Te
                      shift.data_ptr<float>(), mean.data_ptr<float>(), reinterpret_cast<__bf16*>(dz.data_ptr()),
                      part.data_ptr<float>(), moments_zero_target(sums.data_ptr<double>(), rb), g, row_len, rows);
   DMP_HIP_CHECK(hipGetLastError());
-  bn_reduce_partials_launch(part.data_ptr<float>(), rb, g.C, sums.data_ptr<double>(), (double)rows * g.W, stream);
+  bn_reduce_partials_launch(part.data_ptr<float>(), rb, g.C, sums.data_ptr<double>(), (double)g.N * g.H * g.W,
+                            stream);
   return {dz, sums};
 }
 

@@ -168,3 +168,41 @@ def test_stem_bn_backward_folded_into_wgrad(shift):
         # the reference rounds dx to bf16 before its weight gradient; the fold does not
         assert err < 2e-2, (name, err.item())
     torch.testing.assert_close(bn.running_var, bn2.running_var)
+
+
+@pytest.mark.parametrize("n,c,h,w", [(3, 64, 16, 16), (2, 32, 14, 10), (2, 64, 9, 11), (1, 128, 8, 8)])
+def test_bn_pool_backward_kernel_vs_fp32(n, c, h, w):
+    """maxpool2d_bn_backward (quad kernel for even H/W, one-pixel kernel for odd)
+    against an fp32 scatter of dy through the forward's argmax taps."""
+    from distributed_model_parallel_amd import _native
+    C = _native.require("bn pool backward")
+    torch.manual_seed(0)
+    x = torch.randn(n, c, h, w, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    sc = (torch.rand(c, device="cuda") + 0.5).contiguous()
+    sh = (torch.randn(c, device="cuda") * 0.3).contiguous()
+    mean = (torch.randn(c, device="cuda") * 0.1).contiguous()
+    y, idx = C.maxpool2d_bn_forward(x, sc, sh, 3, 2, 1)
+    ho, wo = y.shape[2], y.shape[3]
+    dy = torch.randn(n, c, ho, wo, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    dz, sums = C.maxpool2d_bn_backward(dy, idx, x, sc, sh, mean, 3, 2, 1)
+    # reference: output (oh, ow) sends dy to input (2oh-1+a, 2ow-1+b), tap = 3a+b
+    tap = idx.view(n, ho, wo, c).long()
+    oh = torch.arange(ho, device="cuda").view(1, ho, 1, 1)
+    ow = torch.arange(wo, device="cuda").view(1, 1, wo, 1)
+    ih = 2 * oh - 1 + tap // 3
+    iw = 2 * ow - 1 + tap % 3
+    assert bool(((ih >= 0) & (ih < h) & (iw >= 0) & (iw < w)).all())
+    nn_ = torch.arange(n, device="cuda").view(n, 1, 1, 1).expand_as(tap)
+    cc = torch.arange(c, device="cuda").view(1, 1, 1, c).expand_as(tap)
+    flat = ((nn_ * h + ih) * w + iw) * c + cc
+    g = torch.zeros(n * h * w * c, device="cuda")
+    g.index_add_(0, flat.reshape(-1), dy.permute(0, 2, 3, 1).reshape(-1).float())
+    g = g.view(n, h, w, c).bfloat16().float()
+    xf = x.permute(0, 2, 3, 1).float()
+    dref = torch.where(xf * sc + sh > 0, g, torch.zeros_like(g))
+    torch.testing.assert_close(dz.permute(0, 2, 3, 1).float(), dref, atol=0, rtol=0)
+    d64 = dref.double().reshape(-1, c)
+    torch.testing.assert_close(sums[:c], d64.sum(0), atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(sums[c:2 * c], (d64 * (xf.double().reshape(-1, c) - mean.double())).sum(0),
+                               atol=1e-3, rtol=1e-4)
+    assert sums[2 * c].item() == n * h * w
