@@ -14,7 +14,8 @@
 //     vector is loaded once per strip instead of 9 times;
 //   * consecutive lanes take consecutive channel vectors of the same pixel, so a
 //     wave reads/writes whole 16-B-aligned pixel rows of C channels;
-//   * the 9 taps x 8 channels of weights (pre-transposed to [9][C]) live in
+//   * the 9 taps x 8 channels of weights (read from the module's own [C][9]
+//     tensor and transposed in registers) live in
 //     registers for the whole launch;
 //   * forward can emit per-block BatchNorm moment partials of its OUTPUT
 //     (sum, sum^2) for the following BN -- same partial format the BN and GEMM
@@ -74,6 +75,28 @@ __device__ __forceinline__ void cvt_masked(typename Vec16<T>::raw r, bool ok, fl
 
 __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
+// The lane's VEC channels x 9 taps straight from the [C][9] weight (the
+// module's own [C,1,3,3] tensor, bf16 or fp32): channels c0..c0+VEC-1 are one
+// contiguous run of 9*VEC elements, read as 16-B (or 8-B) vectors and
+// transposed in registers -- no per-call fp32 [9][C] copy (two torch launches
+// per forward and per data gradient).  The host checks 16-B base alignment.
+template <typename WT, int VEC>
+__device__ __forceinline__ void load_taps(const WT* __restrict__ wc, int c0, float (&wr)[9][VEC]) {
+  constexpr int NE = 9 * VEC, NB = NE * (int)sizeof(WT);
+  using U = typename std::conditional<NB % 16 == 0, uint4, uint2>::type;
+  constexpr int NU = NB / (int)sizeof(U);
+  const U* p = reinterpret_cast<const U*>(wc + (int64_t)c0 * 9);
+  U r[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) r[i] = p[i];
+  WT e[NE];
+  __builtin_memcpy(e, r, NB);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) wr[t][j] = (float)e[j * 9 + t];
+}
+
 // ---------------------------------------------------------------------------
 // forward: y[n,oh,ow,c] = sum_{kh,kw} x[n, oh*s-1+kh, ow*s-1+kw, c] * w[kh,kw,c]
 // grid.x = ceil(N*OH*strips / spp), grid.y = channel chunks
@@ -81,9 +104,9 @@ __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > h
 // S = stride as a template constant: every tap index in the unrolled loops is
 // then a compile-time constant, so wr/acc stay in registers (a runtime stride
 // made the compiler index them dynamically -> scratch memory, measured 2-4x).
-template <typename T, bool MOMENTS, int S>
+template <typename T, typename WT, bool MOMENTS, int S>
 __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ x,
-                                                         const float* __restrict__ w9,
+                                                         const WT* __restrict__ wc,
                                                          T* __restrict__ y, Geo g,
                                                          float* __restrict__ part,
                                                          double* __restrict__ zsums) {
@@ -101,10 +124,7 @@ __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ 
   const int64_t total = (int64_t)g.N * g.OH * g.strips;
   const int64_t sidx = (int64_t)blockIdx.x * g.spp + ls;
   if (active_c && sidx < total) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int j = 0; j < VEC; ++j) wr[t][j] = w9[t * g.C + c0 + j];
+    load_taps<WT, VEC>(wc, c0, wr);
     const int st = (int)(sidx % g.strips);
     const int64_t nr = sidx / g.strips;
     const int oh = (int)(nr % g.OH);
@@ -182,9 +202,9 @@ __global__ __launch_bounds__(kThreads) void dw_fwd_kernel(const T* __restrict__ 
 // ow = (iw+1-kw)/s integral and in range of dy[n,oh,ow,c] * w[kh,kw,c].
 // One lane: 8 channels x TW consecutive input columns of one input row.
 // ---------------------------------------------------------------------------
-template <typename T, int S>
+template <typename T, typename WT, int S>
 __global__ __launch_bounds__(kThreads) void dw_dgrad_kernel(const T* __restrict__ dy,
-                                                           const float* __restrict__ w9,
+                                                           const WT* __restrict__ wc,
                                                            T* __restrict__ dx, Geo g,
                                                            int istrips) {
   constexpr int VEC = Vec16<T>::N;
@@ -197,10 +217,7 @@ __global__ __launch_bounds__(kThreads) void dw_dgrad_kernel(const T* __restrict_
   if (sidx >= total) return;
   const int c0 = cvec * VEC;
   float wr[9][VEC];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int j = 0; j < VEC; ++j) wr[t][j] = w9[t * g.C + c0 + j];
+  load_taps<WT, VEC>(wc, c0, wr);
   const int st = (int)(sidx % istrips);
   const int64_t nr = sidx / istrips;
   const int ih = (int)(nr % g.H);
@@ -336,7 +353,7 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(const T* __restrict_
 // out[c] = sum_b part[b][c]  (fp64 accumulation, 32 row-groups x 32 columns per block)
 template <typename OT>
 __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __restrict__ part, int rb,
-                                                             int ncol, OT* __restrict__ out) {
+                                                             int ncol, int C, OT* __restrict__ out) {
   const int cl = threadIdx.x % 32, g = threadIdx.x / 32;
   const int c = blockIdx.x * 32 + cl;
   double a = 0.0;
@@ -349,7 +366,7 @@ __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __rest
     if (g < s) l[threadIdx.x] += l[threadIdx.x + s * 32];
     __syncthreads();
   }
-  if (g == 0 && c < ncol) out[c] = (OT)l[threadIdx.x];
+  if (g == 0 && c < ncol) out[(c % C) * 9 + c / C] = (OT)l[threadIdx.x];  // [C][9] = [C,1,3,3]
 }
 
 Geo make_geo(const at::Tensor& x4, int stride, int VEC) {
@@ -378,11 +395,23 @@ void check_nhwc(const at::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-B aligned");
 }
 
-at::Tensor taps_first(const at::Tensor& w) {
-  // [C,1,3,3] (any memory format) -> fp32 [9][C]
+// The weight as the kernels read it: [C][9] contiguous, bf16 or fp32, 16-B
+// aligned -- the module's own tensor when it already is (flat parameter views
+// are padded to 8 elements), else one converted copy.
+at::Tensor taps(const at::Tensor& w) {
   TORCH_CHECK(w.dim() == 4 && w.size(1) == 1 && w.size(2) == 3 && w.size(3) == 3,
               "depthwise weight must be [C,1,3,3]");
-  return w.reshape({w.size(0), 9}).to(at::kFloat).t().contiguous();
+  TORCH_CHECK(w.is_cuda(), "depthwise weight must be a GPU tensor");
+  if (w.is_contiguous() && (w.scalar_type() == at::kBFloat16 || w.scalar_type() == at::kFloat) &&
+      reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0)
+    return w;
+  return w.to(at::kFloat).contiguous();
+}
+
+template <typename F>
+void dispatch_w(const at::Tensor& w, F&& f) {
+  if (w.scalar_type() == at::kBFloat16) f(__bf16{});
+  else f(float{});
 }
 
 template <typename F>
@@ -401,7 +430,8 @@ std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor&
   const int VEC = x.scalar_type() == at::kBFloat16 ? 8 : 4;
   Geo g = make_geo(x, (int)stride, VEC);
   auto y = at::empty({g.N, g.C, g.OH, g.OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  auto w9 = taps_first(w);
+  const auto wt = taps(w);
+  TORCH_CHECK(wt.size(0) == g.C, "weight channels do not match x");
   auto stream = at::hip::getCurrentHIPStream();
   const int64_t total = (int64_t)g.N * g.OH * g.strips;
   const int cchunks = (g.cv + g.tc - 1) / g.tc;
@@ -415,14 +445,18 @@ std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor&
   }
   dispatch_t(x, [&](auto tag) {
     using T = decltype(tag);
-    if (moments)
-      hipLaunchKernelGGL((g.stride == 1 ? dw_fwd_kernel<T, true, 1> : dw_fwd_kernel<T, true, 2>), grid, dim3(kThreads), 0, stream,
-                         reinterpret_cast<const T*>(x.data_ptr()), w9.data_ptr<float>(),
-                         reinterpret_cast<T*>(y.data_ptr()), g, part.data_ptr<float>(), zt);
-    else
-      hipLaunchKernelGGL((g.stride == 1 ? dw_fwd_kernel<T, false, 1> : dw_fwd_kernel<T, false, 2>), grid, dim3(kThreads), 0, stream,
-                         reinterpret_cast<const T*>(x.data_ptr()), w9.data_ptr<float>(),
-                         reinterpret_cast<T*>(y.data_ptr()), g, nullptr, nullptr);
+    dispatch_w(wt, [&](auto wtag) {
+      using WT = decltype(wtag);
+      const WT* wp = reinterpret_cast<const WT*>(wt.data_ptr());
+      if (moments)
+        hipLaunchKernelGGL((g.stride == 1 ? dw_fwd_kernel<T, WT, true, 1> : dw_fwd_kernel<T, WT, true, 2>), grid,
+                           dim3(kThreads), 0, stream, reinterpret_cast<const T*>(x.data_ptr()), wp,
+                           reinterpret_cast<T*>(y.data_ptr()), g, part.data_ptr<float>(), zt);
+      else
+        hipLaunchKernelGGL((g.stride == 1 ? dw_fwd_kernel<T, WT, false, 1> : dw_fwd_kernel<T, WT, false, 2>), grid,
+                           dim3(kThreads), 0, stream, reinterpret_cast<const T*>(x.data_ptr()), wp,
+                           reinterpret_cast<T*>(y.data_ptr()), g, nullptr, nullptr);
+    });
   });
   if (moments) {
     bn_reduce_partials_launch(part.data_ptr<float>(), (int)grid.x, g.C, mom.data_ptr<double>(),
@@ -439,7 +473,8 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
   auto shape_x = at::empty({dy.size(0), dy.size(1), H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   Geo g = make_geo(shape_x, (int)stride, VEC);
   TORCH_CHECK(g.OH == dy.size(2) && g.OW == dy.size(3), "dy shape does not match the input size");
-  auto w9 = taps_first(w);
+  const auto wt = taps(w);
+  TORCH_CHECK(wt.size(0) == g.C, "weight channels do not match dy");
   auto stream = at::hip::getCurrentHIPStream();
   const int istrips = (g.W + TW - 1) / TW;
   const int64_t total = (int64_t)g.N * g.H * istrips;
@@ -447,9 +482,13 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
   dim3 grid((unsigned)((total + g.spp - 1) / g.spp), (unsigned)cchunks);
   dispatch_t(dy, [&](auto tag) {
     using T = decltype(tag);
-    hipLaunchKernelGGL((g.stride == 1 ? dw_dgrad_kernel<T, 1> : dw_dgrad_kernel<T, 2>), grid, dim3(kThreads), 0, stream,
-                       reinterpret_cast<const T*>(dy.data_ptr()), w9.data_ptr<float>(),
-                       reinterpret_cast<T*>(shape_x.data_ptr()), g, istrips);
+    dispatch_w(wt, [&](auto wtag) {
+      using WT = decltype(wtag);
+      hipLaunchKernelGGL((g.stride == 1 ? dw_dgrad_kernel<T, WT, 1> : dw_dgrad_kernel<T, WT, 2>), grid,
+                         dim3(kThreads), 0, stream, reinterpret_cast<const T*>(dy.data_ptr()),
+                         reinterpret_cast<const WT*>(wt.data_ptr()), reinterpret_cast<T*>(shape_x.data_ptr()), g,
+                         istrips);
+    });
   });
   return shape_x;
 }
@@ -477,11 +516,17 @@ at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t st
                        reinterpret_cast<const T*>(dy.data_ptr()),
                        reinterpret_cast<const T*>(x.data_ptr()), g, spl, part.data_ptr<float>());
   });
-  auto out9 = at::empty({9, (int64_t)g.C}, x.options().dtype(at::kFloat));
+  // reduced straight into [C,1,3,3] in the parameter dtype (no transpose / cast launches)
+  TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kFloat, "weight gradient must be bf16 or fp32");
+  auto out = at::empty({(int64_t)g.C, 1, 3, 3}, x.options().dtype(out_dtype));
   const int ncol = 9 * g.C;
-  hipLaunchKernelGGL((column_reduce_kernel<float>), dim3((ncol + 31) / 32), dim3(1024), 0, stream,
-                     part.data_ptr<float>(), (int)grid.x, ncol, out9.data_ptr<float>());
-  return out9.t().reshape({g.C, 1, 3, 3}).to(out_dtype);
+  if (out_dtype == at::kBFloat16)
+    hipLaunchKernelGGL((column_reduce_kernel<__bf16>), dim3((ncol + 31) / 32), dim3(1024), 0, stream,
+                       part.data_ptr<float>(), (int)grid.x, ncol, g.C, reinterpret_cast<__bf16*>(out.data_ptr()));
+  else
+    hipLaunchKernelGGL((column_reduce_kernel<float>), dim3((ncol + 31) / 32), dim3(1024), 0, stream,
+                       part.data_ptr<float>(), (int)grid.x, ncol, g.C, out.data_ptr<float>());
+  return out;
 }
 
 }  // namespace dmp

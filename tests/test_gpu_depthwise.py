@@ -47,3 +47,36 @@ def test_depthwise_forward_moments():
     torch.testing.assert_close(mom[:64], yf.sum(0), atol=1e-2, rtol=1e-4)
     torch.testing.assert_close(mom[64:128], (yf * yf).sum(0), atol=1e-2, rtol=1e-4)
     assert mom[128].item() == 8 * 16 * 16
+
+
+@pytest.mark.parametrize("wkind", ["fp32", "bf16_offset1", "fp32_offset2"])
+def test_depthwise_weight_layouts(wkind):
+    """The kernels read the [C,1,3,3] weight in place (bf16 or fp32, 16-B aligned);
+    an fp32 weight with bf16 activations and a misaligned view (converted copy)
+    give the same results as conv2d."""
+    C = _native.require("dw")
+    torch.manual_seed(0)
+    n, c, h, w = 3, 48, 10, 12
+    x = torch.randn(n, c, h, w, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    base = torch.randn(c * 9 + 8, device=DEV) * 0.3
+    if wkind == "fp32":
+        wt = base[: c * 9].view(c, 1, 3, 3)
+    elif wkind == "bf16_offset1":
+        wt = base.bfloat16()[1: 1 + c * 9].view(c, 1, 3, 3)
+    else:
+        wt = base[2: 2 + c * 9].view(c, 1, 3, 3)
+    assert wkind == "fp32" or wt.data_ptr() % 16 != 0
+    for stride in (1, 2):
+        y, _ = C.dwconv3x3_forward(x, wt, stride, False)
+        yr = F.conv2d(x.float(), wt.float(), None, stride, 1, 1, c)
+        torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=3e-2)
+        dy = torch.randn_like(yr).bfloat16().contiguous(memory_format=torch.channels_last)
+        dx = C.dwconv3x3_dgrad(dy, wt, stride, h, w)
+        xr = x.float().requires_grad_()
+        F.conv2d(xr, wt.float(), None, stride, 1, 1, c).backward(dy.float())
+        torch.testing.assert_close(dx.float(), xr.grad, atol=6e-2, rtol=3e-2)
+        dw = C.dwconv3x3_wgrad(dy, x, stride, wt.dtype)
+        assert dw.shape == (c, 1, 3, 3) and dw.dtype == wt.dtype and dw.is_contiguous()
+        wr = wt.float().detach().requires_grad_()
+        F.conv2d(x.float(), wr, None, stride, 1, 1, c).backward(dy.float())
+        torch.testing.assert_close(dw.float(), wr.grad, atol=0.05 * (n * h * w) ** 0.5, rtol=5e-2)
