@@ -32,6 +32,7 @@ is (bench.py --graph captures the same ops).
 from __future__ import annotations
 
 import copy
+import gc
 from typing import List, Optional, Sequence
 
 import torch
@@ -91,9 +92,21 @@ class GraphedReplicas:
         # the capture's warm-up iterations run replica 0 for real: keep the
         # module's running statistics as they were (its buffers are shared)
         saved = [b.detach().clone() for b in self.buffers]
-        for rep, x, d in zip(self.replicas, self.inputs, self.devices):
-            with torch.cuda.device(d):
-                self.graphed.append(torch.cuda.make_graphed_callables(rep, (x,)))
+        # no Python garbage collection inside the captures: a collection there
+        # runs tensor / event destructors of earlier eager steps (side-stream
+        # frees, event destroys) while the stream is capturing, which aborted
+        # the process once in the GPU suite (round 5).  Collect first instead.
+        gc.collect()
+        torch.cuda.synchronize()
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            for rep, x, d in zip(self.replicas, self.inputs, self.devices):
+                with torch.cuda.device(d):
+                    self.graphed.append(torch.cuda.make_graphed_callables(rep, (x,)))
+        finally:
+            if gc_was:
+                gc.enable()
         with torch.no_grad():
             for b, v in zip(self.buffers, saved):
                 b.copy_(v)
