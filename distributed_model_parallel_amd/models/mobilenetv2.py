@@ -18,6 +18,7 @@ Differences from the reference that are deliberate:
 """
 from __future__ import annotations
 
+import os
 from typing import Iterable, List, Sequence, Tuple
 
 import torch
@@ -27,7 +28,7 @@ import torch.nn.functional as F
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv1x1 import Conv1x1
 from ..ops.depthwise import DepthwiseConv2d
-from ..ops.fused import conv_bn
+from ..ops.fused import GradSlot, conv_bn, grad_tap
 from ..ops.pool import global_avg_pool
 from ..ops.stem import RowTapConv2d
 
@@ -66,6 +67,10 @@ def _norm(ch: int, use_bn: bool, act: bool, activation: str = "relu") -> nn.Modu
     return nn.ReLU6(inplace=False) if activation == "relu6" else nn.ReLU(inplace=False)
 
 
+# A/B and tests (DMP_MNV2_NOSLOT=1): False = the autograd engine adds the two gradients of x
+_FUSE_SHORTCUT_GRAD = os.environ.get("DMP_MNV2_NOSLOT", "0") != "1"
+
+
 class InvertedResidual(nn.Module):
     """expand 1x1 -> depthwise 3x3 -> project 1x1 (+ residual when stride 1).
 
@@ -101,16 +106,23 @@ class InvertedResidual(nn.Module):
             self.shortcut = nn.Sequential()
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        y = conv_bn(self.conv1, self.bn1, x) if self.conv1 is not None else x
+        # x feeds the expand conv and the shortcut: the expand conv's data-gradient
+        # GEMM absorbs the shortcut's gradient (ops/fused.py GradSlot, as in the
+        # ResNet bottleneck) instead of the autograd engine's add kernel.  The
+        # shortcut is built after conv1 so its backward runs first.
+        slot = (GradSlot() if (_FUSE_SHORTCUT_GRAD and self.has_residual and self.conv1 is not None
+                               and self.training and torch.is_grad_enabled()) else None)
+        y = conv_bn(self.conv1, self.bn1, x, grad_slot=slot) if self.conv1 is not None else x
+        xt = grad_tap(x, slot)
         y = conv_bn(self.conv2, self.bn2, y)
         res = None
         if self.has_residual:
             if len(self.shortcut) == 0:
-                res = x
+                res = xt
             elif len(self.shortcut) == 2:
-                res = conv_bn(self.shortcut[0], self.shortcut[1], x)
+                res = conv_bn(self.shortcut[0], self.shortcut[1], xt)
             else:
-                res = self.shortcut(x)
+                res = self.shortcut(xt)
         # bn3 has no activation: the residual add is fused into its apply pass
         return conv_bn(self.conv3, self.bn3, y, res)
 
