@@ -127,6 +127,8 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
                                 const c10::optional<at::Tensor>& bias);
 std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tensor& B, const at::Tensor& aux);
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
+// gemm_w4.hip
+at::Tensor gemm_w4(const at::Tensor& A, const at::Tensor& B, int64_t group_m, int64_t variant);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat, bool moments);
@@ -367,6 +369,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_tn_xl_ablation", &dmp::set_tn_xl_ablation, py::arg("mode"));
   m.def("set_tn_xl_ring", &dmp::set_tn_xl_ring, py::arg("ring"),
         "gemm_tn_xl main loop: 0 = two tile buffers, 1 = the 10-slot LDS unit ring");
+  m.def("gemm_w4", &dmp::gemm_w4, py::arg("A"), py::arg("B"), py::arg("group_m") = 0, py::arg("variant") = 0,
+        "C = A @ B^T on the 4-wave 256x256 MFMA kernel (128x128 per wave, AGPR accumulators)",
+        py::call_guard<py::gil_scoped_release>());
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M",
         py::call_guard<py::gil_scoped_release>());

@@ -222,10 +222,17 @@ __device__ __forceinline__ void xl_mark(const XlArgs& p, int k) {
 // Epilogue of the NT kernel (and of a split-K tail tile, gemm_xl_tail_epi):
 // (acc [+ bias]) -> bf16 tile in LDS, then the row-contiguous pass with the
 // fused operation; acc in the PIPE's register layout (7 / 8: transposed).
+// PIPE 11 (gemm_xl_w4_kernel): 4 waves as 2 x 2, 128 x 128 outputs per wave,
+// 256 threads in the row passes; every other PIPE: 8 waves as 2 x 4
+__host__ __device__ constexpr int xl_waves(int pipe) { return pipe == 11 ? 4 : 8; }
+template <int BN, int PIPE>
+using XlAcc = f32x4[8][xl_waves(PIPE) == 4 ? BN / 32 : BN / 64];
+
 template <int BN, int EPI, int PIPE, int LDS>
-__device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN / 64], char* smem, int m0, int n0,
+__device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& acc, char* smem, int m0, int n0,
                                             int mt, int mtiles, int tbm = XBM) {
-  constexpr int WTM = 128, WTN = BN / 4;
+  constexpr int NW = xl_waves(PIPE), XTHREADS = NW * 64;
+  constexpr int WTM = 128, WTN = NW == 4 ? BN / 2 : BN / 4;
   constexpr int MI = WTM / 16, NI = WTN / 16;
   constexpr int CT_STRIDE = BN + 8;
   constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
@@ -233,7 +240,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
   // past tbm belong to the next tile and are neither stored nor summed
   const int M = min(p.M, m0 + tbm), N = p.N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
+  const int wr = NW == 4 ? wave >> 1 : wave >> 2, wc = NW == 4 ? wave & 1 : wave & 3;
   (void)lane;
   // ---- batched epilogue operand loads (residual / BN input / BN output / aux).
   // Row passes of RPP rows; batch b covers passes [b PB, b PB + PB).  The
@@ -330,7 +337,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
   // per-column affine applied to the fp32 accumulator BEFORE the bf16 staging:
   // a bias / BN shift that nearly cancels acc (XL_BNBWD's folded-BN constant,
   // XL_AFFINE's -mean*scale) must not meet a bf16-rounded acc (finding 33)
-  if constexpr (PIPE == 7 || PIPE == 8) {
+  if constexpr (PIPE == 7 || PIPE == 8 || PIPE == 10 || PIPE == 11) {
     // transposed accumulators (see quad()): lane l holds row l & 15 and the 4
     // consecutive columns 4 (l >> 4) + e of each 16 x 16 block -> one 8-B LDS
     // write per block (a half-wave covers 16 rows x 16 B at a 528-B row pitch:
@@ -361,7 +368,9 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
       b4a[j] = b4;
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the coefficient loads ahead of the batch
-    if constexpr (kBatch) issue(0);
+    // (4 waves: the 256 accumulators are still live here and the batch would
+    // spill; it goes out after the staging instead)
+    if constexpr (kBatch && NW == 8) issue(0);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -376,6 +385,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, f32x4 (&acc)[8][BN 
         *reinterpret_cast<bf16x4*>(ct + row * CT_STRIDE + lc) = __builtin_convertvector(v, bf16x4);
       }
     }
+    if constexpr (kBatch && NW == 4) issue(0);
   } else {
   float bv[NI], sv[NI];
 #pragma unroll
@@ -573,7 +583,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   const int M = p.M, N = p.N, K = p.K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  const int tbm = (PIPE == 7 && p.bm > 0) ? p.bm : XBM;  // rows per tile (pick_bm)
+  const int tbm = ((PIPE == 7 || PIPE == 10) && p.bm > 0) ? p.bm : XBM;  // rows per tile (pick_bm)
   const int mtiles = (M + tbm - 1) / tbm, ntiles = (N + BN - 1) / BN;
   int mt, nt;
   int kt_begin = 0, kt_end = K / XBK;
@@ -696,7 +706,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     if (has2) vmcnt<W2>(); else if (has1) vmcnt<NA + NB>(); else vmcnt<0>();
     barrier();
   }
-  } else if constexpr (PIPE == 7 || PIPE == 9) {
+  } else if constexpr (PIPE == 7 || PIPE == 9 || PIPE == 10) {
   // ---- PIPE 7: ping-pong quadrant schedule (cdna_hip_programming.md §5 "256²
   // 8-phase template").  The two wave rows (wr) run one barrier apart: while
   // one group's 4 waves run a phase's 16 MFMAs, the other group (one wave on
@@ -777,7 +787,13 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         glds16(pb[U == 2][q] + koff, b_region(pks, buf) + ob[U == 2][q]);
     }
   };
-  bf16x8 qa[2][4], qb[2][2];
+  // PIPE 10 keeps both n halves of B in registers (qb[nq]): B half 0 is
+  // read once per K tile instead of twice, so every unit has one reader phase
+  // and its slot frees two phases earlier -- the copies are issued 4 phases
+  // ahead of their readers instead of 2 (vmcnt(8): 64 KB in flight per wave
+  // group instead of 32 KB)
+  constexpr bool kDeep = PIPE == 10;
+  bf16x8 qa[2][4], qb[kDeep ? 2 : 1][2][2];
   auto read_a = [&](int mq, int buf) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
@@ -790,7 +806,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        qb[ks][j] = *reinterpret_cast<const bf16x8*>(b_region(ks, buf) + (wc * WTN + nq * 32 + j * 16) * 64 + frag_off);
+        qb[kDeep ? nq : 0][ks][j] =
+            *reinterpret_cast<const bf16x8*>(b_region(ks, buf) + (wc * WTN + nq * 32 + j * 16) * 64 + frag_off);
   };
   // a trimmed tile (tbm < 256, >= 192): wave row 1's m-half-1 blocks past
   // row tbm are the next tile's rows -- their MFMAs are skipped (wave-uniform)
@@ -810,8 +827,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[MQ * 4 + i][NQ * 2 + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+            acc[MQ * 4 + i][NQ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                qb[kDeep ? NQ : 0][ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
     } else {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -820,8 +837,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
           if (i < ilim) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-              acc[MQ * 4 + i][NQ * 2 + j] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
+              acc[MQ * 4 + i][NQ * 2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  qb[kDeep ? NQ : 0][ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
           }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -834,6 +851,48 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   using I3 = std::integral_constant<int, 3>;
   // K tiles [kt_begin, kt_end): the whole K, or one split of a tail tile
   // (kt_begin even, so K tile kt still lives in buffer kt & 1)
+  if constexpr (kDeep) {
+  // ---- PIPE 10 unit schedule.  Readers: U0, U1 of tile t in phase 0 (quad
+  // (0,0)), U2 in phase 1, U3 in phase 2; phase 3 reads nothing.  Phase r of
+  // tile t stages U2(t+1), U3(t+1), U0(t+2), U1(t+2): each is written >= 2
+  // phases after its slot's previous reader (WAR) and retired by a vmcnt 4
+  // phases after its issue, one phase before its reader (RAW).  The waits
+  // leave the 4 youngest units (8 copies per wave) in flight; phase 2 has no
+  // reader in the next phase and so no wait.
+  stage_unit(I0{}, kt_begin);
+  stage_unit(I1{}, kt_begin);
+  stage_unit(I2{}, kt_begin);
+  stage_unit(I3{}, kt_begin);
+  if (kt_end - kt_begin > 1) {
+    stage_unit(I0{}, kt_begin + 1);
+    stage_unit(I1{}, kt_begin + 1);
+    vmcnt<8>();
+  } else {
+    vmcnt<4>();
+  }
+  barrier();
+  xl_mark(p, 1);
+  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    const int buf = kt & 1;
+    const bool n1 = kt + 1 < kt_end, n2 = kt + 2 < kt_end;
+    read_a(0, buf);
+    read_b(0, buf);
+    if (n1) { stage_unit(I2{}, kt + 1); vmcnt<8>(); } else { vmcnt<2>(); }
+    quad(I0{}, I0{});
+    read_b(1, buf);
+    if (n1) { stage_unit(I3{}, kt + 1); vmcnt<8>(); } else { vmcnt<0>(); }
+    quad(I0{}, I1{});
+    read_a(1, buf);
+    if (n2) stage_unit(I0{}, kt + 2);
+    quad(I1{}, I1{});
+    if (n2) { stage_unit(I1{}, kt + 2); vmcnt<8>(); } else if (n1) { vmcnt<4>(); } else { vmcnt<0>(); }
+    quad(I1{}, I0{});
+  }
+  if (wr == 0) barrier();  // equal barrier counts before the epilogue
+  barrier();
+  xl_mark(p, 2);
+  } else {
   stage_unit(I0{}, kt_begin);
   stage_unit(I2{}, kt_begin);
   stage_unit(I3{}, kt_begin);
@@ -868,6 +927,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   if (wr == 0) barrier();  // equal barrier counts before the epilogue
   barrier();
   xl_mark(p, 2);
+  }
   } else if constexpr (PIPE == 8) {
   // ---- PIPE 8: the ping-pong quadrant schedule of PIPE 7 on a ring of NS
   // 16 KB unit slots instead of two fixed tile buffers (finding 42: PIPE 7
@@ -1127,6 +1187,184 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   // order that write after the copies into LDS
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   xl_epilogue<BN, EPI, PIPE, LDS>(p, acc, smem, m0, n0, mt, mtiles, tbm);
+  if (p.tdbg) {
+    __syncthreads();
+    xl_mark(p, 3);
+  }
+}
+
+// ---- PIPE 11: 4-wave 256 x 256 kernel (cdna_hip_programming.md §5; profiles/
+// README.md finding 69).  One wave per SIMD computes 128 x 128 outputs (64
+// accumulators, all 256 AGPRs, tied in-place MFMAs: w4_mfma), so each
+// fragment read from LDS feeds 8 MFMAs (128 KB of fragment reads per CU and K
+// tile, against 224 KB for the 8-wave 128 x 64 wave tiles) and the only
+// synchronisation is one barrier per K tile.  Every LDS-DMA instruction copies
+// 8 rows x 128 B -- one whole K tile of 8 rows, 8 full cache lines -- into an
+// [256 rows][128 B] image with 16-B chunk c of row r at c ^ ((r >> 1) & 7)
+// (conflict-free fragment reads).  Copies of half-line pieces (16 rows x 64 B)
+// cost the MFMA issue stream ~25 % at 8192^3; full lines, one per 4 MFMAs
+// spread over the copy segment, brought it from 1.39 to 1.54 PF/s.
+//   S1: k-half 0 MFMAs, reading k-half 1's fragments of tile t (one ds_read
+//       per 4 MFMAs); vmcnt(0) + barrier: tile t + 1 has landed, buffer t & 1
+//       is free;
+//   S2: k-half 1 MFMAs, copying tile t + 2 into buffer t & 1 (one per 4
+//       MFMAs) and reading k-half 0 of tile t + 1 (first half of the segment).
+// Operand staging features: plain A / B, the second A source (A2 from column
+// K1, a strided row map), the conv tap gather (cv; zero taps from g_zero_row).
+__device__ __forceinline__ void w4_mfma(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  // tied dst == srcC in AGPRs: the builtin lets the register allocator pick an
+  // untied dst for some accumulators and rotate all 256 through v_accvgpr
+  // moves every K tile; "memory" pins the order of the interleaved LDS reads /
+  // copies.  srcA/B come from ds_read results the compiler waits for; the
+  // accumulate chain D -> C needs no wait states; reads of the accumulators
+  // after the loop sit behind w4_drain().
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b) : "memory");
+}
+__device__ __forceinline__ void w4_drain() { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory"); }
+__device__ __forceinline__ int w4_swz(int c, int row) { return c ^ ((row >> 1) & 7); }
+
+// SRC (compile-time, so the copy stream between the MFMAs has no branches):
+// 0 = plain A, by buffer_load ... lds with one 32-bit lane offset per piece
+// (operands < 2 GB); 1 = plain A with the second source A2 from column K1;
+// 2 = conv tap gather (global_load_lds, zero taps read g_zero_row)
+template <int EPI, int SRC>
+__global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
+  constexpr int OPB = 256 * 128, BUF = 2 * OPB;  // one operand's K tile, one buffer (A | B)
+  constexpr int EPI_LDS = XBM * (256 + 8) * 2;
+  constexpr int LDS = 2 * BUF > EPI_LDS ? 2 * BUF : EPI_LDS;
+  __shared__ __attribute__((aligned(16))) char smem[LDS];
+  constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
+  if constexpr (kMom) zero_moments(p.zsums, 2 * p.N);
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + 255) / 256;
+  int mt, nt;
+  tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
+  const int m0 = mt * XBM, n0 = nt * 256;
+  const int ktiles = K / XBK;
+
+  // copy c (0..15) of a K tile: operand c >> 3 (A, B), 8-row piece
+  // 8 wave + (c & 7); lane L: row 8 piece + (L >> 3), stored chunk L & 7,
+  // logical chunk w4_swz(L & 7, row)
+  const int lrow8 = lane >> 3;
+  const int64_t abytes = ((int64_t)(M - 1) * p.lda + K) * 2, bbytes = ((int64_t)(N - 1) * p.ldb + K) * 2;
+  const auto rsa = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)min(abytes, (int64_t)0x7fffffff),
+                                                     0x00020000);
+  const auto rsb = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)min(bbytes, (int64_t)0x7fffffff),
+                                                     0x00020000);
+  uint32_t oa[8], ob[8];
+  const bf16* pa2[8];
+  const XlConv cv = p.cv;
+  int gpix[8], gih[8], giw[8], lcq[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int row = (wave * 8 + q) * 8 + lrow8;
+    const int lc = w4_swz(lane & 7, row) * 8;
+    const int ra = min(m0 + row, M - 1);
+    lcq[q] = lc;
+    oa[q] = (uint32_t)(((int64_t)ra * p.lda + lc) * 2);
+    ob[q] = (uint32_t)(((int64_t)min(n0 + row, N - 1) * p.ldb + lc) * 2);
+    if constexpr (SRC == 1) pa2[q] = p.A2 + xl_out_row(p.a2m, ra) * p.lda2 + lc - p.K1;
+    if constexpr (SRC == 2) {
+      const int hw = cv.ho * cv.wo;
+      const int n = ra / hw, r = ra - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
+      gih[q] = oh * cv.stride - cv.pad;
+      giw[q] = ow * cv.stride - cv.pad;
+      gpix[q] = (n * cv.hi + gih[q]) * cv.wi + giw[q];
+    }
+  }
+  const int lcz = w4_swz(lane & 7, lrow8) * 8;  // zero-row chunk (any in-bounds 16 B)
+  auto dma = [&](int kt, int buf, int c) {
+    const int q = c & 7;
+    char* dst = smem + buf * BUF + (c >> 3) * OPB + (wave * 8 + q) * 1024;
+    const int koff = kt * XBK;
+    if (c >= 8) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)dst, 16, ob[q], koff * 2, 0, 0);
+    } else if constexpr (SRC == 2) {  // tap (tr, tc), channels c0.. of this piece's pixels, or zeros
+      const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
+      const int tr = tap / cv.kw, tcol = tap - tr * cv.kw;
+      const int ih = gih[q] + tr, iw = giw[q] + tcol;
+      const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
+      glds16(ok ? p.A + (int64_t)(gpix[q] + tr * cv.wi + tcol) * p.lda + c0 + lcq[q] : g_zero_row + lcz, dst);
+    } else if constexpr (SRC == 1) {
+      if (koff >= p.K1) glds16(pa2[q] + koff, dst);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)dst, 16, oa[q], koff * 2, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lptr_t)dst, 16, oa[q], koff * 2, 0, 0);
+    }
+  };
+
+  const int lrow = lane & 15, lk = lane >> 4;
+  const int fo0 = lrow * 128 + (w4_swz(lk, lrow) << 4), fo1 = lrow * 128 + (w4_swz(4 + lk, lrow) << 4);
+  const int aoff = wr * 128 * 128, boff = OPB + wc * 128 * 128;
+  bf16x8 ra[2][8], rb[2][8];
+  // fragment read r (0..15) in the order the MFMAs consume them: A block 0,
+  // B blocks 0..7, A blocks 1..7
+  auto rd = [&](auto hc, int buf, int r) {
+    constexpr int H = decltype(hc)::value;
+    const bool isb = r >= 1 && r <= 8;
+    const int blk = r == 0 ? 0 : (isb ? r - 1 : r - 8);
+    const char* base = smem + buf * BUF + (isb ? boff : aoff) + blk * 2048 + (H ? fo1 : fo0);
+    if (isb) rb[H][blk] = *reinterpret_cast<const bf16x8*>(base);
+    else ra[H][blk] = *reinterpret_cast<const bf16x8*>(base);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // operands swapped: acc[i][j] holds the transposed 16 x 16 block (lane =
+  // output row i*16 + (l & 15), registers = 4 consecutive output columns),
+  // the layout xl_epilogue stages as 8-B row pieces
+  auto iter = [&](auto st, auto rdn, int kt) {
+    constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
+    const int buf = kt & 1;
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
+      if ((n & 3) == 0) rd(I1{}, buf, n >> 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      w4_mfma(acc[n >> 3][n & 7], rb[1][n & 7], ra[1][n >> 3]);
+      if constexpr (STAGE)
+        if ((n & 3) == 0) dma(kt + 2, buf, n >> 2);
+      if constexpr (READ)
+        if ((n & 1) == 1 && n < 32) rd(I0{}, buf ^ 1, n >> 1);
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < 16; ++c) dma(0, 0, c);
+  if (ktiles > 1) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dma(1, 1, c);
+    vmcnt<16>();
+  } else {
+    vmcnt<0>();
+  }
+  barrier();
+  xl_mark(p, 1);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) rd(I0{}, 0, r);
+  int kt = 0;
+  for (; kt + 2 < ktiles; ++kt) iter(std::true_type{}, std::true_type{}, kt);
+  if (kt + 1 < ktiles) iter(std::false_type{}, std::true_type{}, kt++);
+  iter(std::false_type{}, std::false_type{}, kt);
+  w4_drain();
+  barrier();  // every wave is done with the operand buffers (the epilogue reuses the LDS)
+  xl_mark(p, 2);
+  // every copy has landed (the waits above are inline asm the compiler cannot
+  // see): say so with a wait it does see (finding 66)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  xl_epilogue<256, EPI, 11, LDS>(p, acc, smem, m0, n0, mt, mtiles);
   if (p.tdbg) {
     __syncthreads();
     xl_mark(p, 3);
@@ -1931,7 +2169,7 @@ int g_num_cus = 0;
 // main loop: 7 = ping-pong quadrant schedule on two tile buffers, 8 = the same
 // schedule on the 10-slot unit ring (256-wide tiles; 128-wide tiles use the
 // half-step ring, 1)
-constexpr int kXlPipeDefault = 7;
+constexpr int kXlPipeDefault = 11;
 int g_xl_pipe = kXlPipeDefault;
 
 // 256 x 256 ping-pong launch (PIPE 7 or its ring form, PIPE 8)
@@ -1965,7 +2203,7 @@ int num_cus() {
 int g_xl_bm = [] { const char* e = std::getenv("DMP_XL_BM"); return e ? std::atoi(e) : 0; }();
 
 int pick_bm(int64_t M, int64_t N, int64_t K) {
-  if (g_xl_pipe != 7 || g_xl_tail) return 256;
+  if ((g_xl_pipe != 7 && g_xl_pipe != 10) || g_xl_tail) return 256;
   if (g_xl_bm > 0) return g_xl_bm;
   if (g_xl_bm < 0 || K < 768) return 256;
   const int64_t cus = num_cus(), nt = (N + 255) / 256;
@@ -1980,12 +2218,36 @@ int pick_bm(int64_t M, int64_t N, int64_t K) {
 
 unsigned long long* g_xl_tdbg = nullptr;  // set_gemm_xl_trace
 
+// the 4-wave kernel addresses A (plain) and B through 32-bit buffer offsets
+bool w4_ok(const XlArgs& a) {
+  const int64_t lim = (int64_t)1 << 31;
+  const bool bfit = ((int64_t)(a.N - 1) * a.ldb + a.K) * 2 < lim;
+  const bool afit = a.cv.cin > 0 || ((int64_t)(a.M - 1) * a.lda + (a.A2 ? a.K1 : a.K)) * 2 < lim;
+  return bfit && afit;
+}
+
 template <int EPI>
 void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
   XlArgs a = a_in;
   a.tdbg = g_xl_tdbg;
   if (g_xl_pipe == 8) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 8>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    return;
+  }
+  if (g_xl_pipe == 10) {
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 10>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+    return;
+  }
+  if (g_xl_pipe == 11 && w4_ok(a)) {
+    XlArgs w = a;
+    w.bm = 256;
+    const int wblocks = ((w.M + 255) / 256) * ((w.N + 255) / 256);
+    if (w.cv.cin > 0)
+      hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 2>), dim3(wblocks), dim3(256), 0, s, w);
+    else if (w.A2)
+      hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 1>), dim3(wblocks), dim3(256), 0, s, w);
+    else
+      hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 0>), dim3(wblocks), dim3(256), 0, s, w);
     return;
   }
   const int cus = num_cus(), ktiles = a.K / XBK, rem = blocks % cus;
@@ -2098,6 +2360,7 @@ int g_xl_group_m = 0;
 // grid mostly empty (N = 768: 3 column tiles -> 128-wide gives 2x the blocks).
 int pick_bn(int M, int N) {
   if (g_xl_bn_override) return g_xl_bn_override;
+  if (g_xl_pipe == 11) return 256;  // the 4-wave kernel has 256-wide tiles only
   const int cus = 256;
   auto eff = [&](int bn) {
     const double blocks = (double)((M + XBM - 1) / XBM) * ((N + bn - 1) / bn);
@@ -2599,7 +2862,7 @@ void set_gemm_xl_bn(int bn, int pipe, int group_m) {
   TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");
   g_xl_group_m = group_m;
   TORCH_CHECK(bn == 0 || bn == 128 || bn == 256, "bn must be 0 (auto), 128 or 256");
-  TORCH_CHECK(pipe >= 0 && pipe <= 8,
+  TORCH_CHECK(pipe >= 0 && pipe <= 11 && pipe != 9,
               "pipe must be 0..8 (2..5: timing-only ablations, 6: persistent, 7: ping-pong 256x256, "
               "8: ping-pong on the LDS unit ring)");
   g_xl_bn_override = bn;

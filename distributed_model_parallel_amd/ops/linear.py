@@ -46,13 +46,13 @@ def set_xl_linear(on: bool) -> None:
 
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 # The PLAIN GEMMs -- nothing to fuse but a bias: the qkv projection forward
-# and the data gradients of qkv / proj / fc1 -- on hipBLASLt ("lib", default)
-# or gemm_xl ("xl"): ViT-B/16 batch 256, 41.82 vs 43.06 ms per step,
-# interleaved runs (profiles/README.md finding 50).  The fused-epilogue GEMMs
-# (fc1 bias+GELU, fc2 / proj bias+residual, fc2's GELU' data gradient with
-# fc1's bias gradient) and every weight gradient (gemm_tn_xl: 44.04 ms with
-# those on the library too) stay on our MFMA kernels.
-_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "lib") == "lib"
+# and the data gradients of qkv / proj / fc1 -- on gemm_xl ("xl", default) or
+# hipBLASLt ("lib").  Until round 5 the library won (finding 50: the 8-wave
+# ping-pong kernel ran 0.85-0.93 PF/s on these shapes); the 4-wave kernel
+# (gemm_xl PIPE 11, finding 69) runs them at 1.03-1.07 PF/s, at or above the
+# library's picks (tools/pipe_bench.py).  The fused-epilogue GEMMs and every
+# weight gradient (gemm_tn_xl) were already ours.
+_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "xl") == "lib"
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> bool:
