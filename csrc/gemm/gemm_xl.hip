@@ -2170,7 +2170,10 @@ int g_num_cus = 0;
 // schedule on the 10-slot unit ring (256-wide tiles; 128-wide tiles use the
 // half-step ring, 1)
 constexpr int kXlPipeDefault = 11;
-int g_xl_pipe = kXlPipeDefault;
+int g_xl_pipe = [] {  // DMP_XL_PIPE=<n>: A/B of the main loop (10 = 8-wave ping-pong)
+  const char* e = std::getenv("DMP_XL_PIPE");
+  return e ? std::atoi(e) : kXlPipeDefault;
+}();
 
 // 256 x 256 ping-pong launch (PIPE 7 or its ring form, PIPE 8)
 // Split-K tail (DMP_XL_TAIL=1, set_gemm_xl_tail; default OFF): one block per
@@ -2238,6 +2241,12 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
     hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 10>), dim3(blocks), dim3(XTHREADS), 0, s, a);
     return;
   }
+  // (XL_BNBWD with its runtime operand flags needs more registers than the
+  // 4-wave epilogue has: the compiler spills accumulators right behind the
+  // inline-asm MFMAs that write them -- read before the MFMA completes.  It
+  // keeps the 8-wave kernel; tests/test_kernel_resources.py holds every
+  // gemm_xl_w4_kernel instantiation to zero scratch.)
+  if constexpr (EPI != XL_BNBWD) {
   if (g_xl_pipe == 11 && w4_ok(a)) {
     XlArgs w = a;
     w.bm = 256;
@@ -2249,6 +2258,7 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
     else
       hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 0>), dim3(wblocks), dim3(256), 0, s, w);
     return;
+  }
   }
   const int cus = num_cus(), ktiles = a.K / XBK, rem = blocks % cus;
   int ks = rem > 0 ? std::min(cus / rem, ktiles / 6) : 0;

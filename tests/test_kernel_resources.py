@@ -1,0 +1,28 @@
+"""Build-time guard for the 4-wave GEMM (gemm_xl PIPE 11): its MFMAs are
+inline asm with the accumulators pinned to AGPRs, so the compiler does not
+know they are still being written for ~18 cycles after each issue.  Any
+compiler spill of an accumulator right behind its MFMA reads a stale value
+(seen once: XL_BNBWD's epilogue pushed the kernel to 36 B of scratch and 0.2 %
+of its outputs came out wrong).  Every instantiation must therefore build with
+zero scratch and its 256 accumulators in AGPRs.  CPU only (hipcc
+cross-compiles gfx950)."""
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc") or shutil.which("c++filt") is None,
+                    reason="needs hipcc and c++filt")
+def test_w4_gemm_kernels_never_spill():
+    from tools.kernel_resources import resources
+    ks = [k for k in resources(os.path.join(ROOT, "csrc", "gemm", "gemm_xl.hip"))
+          if k["name"].startswith("gemm_xl_w4_kernel")]
+    assert len(ks) >= 20, [k["name"] for k in ks]
+    bad = [(k["name"], k["scratch"]) for k in ks if k["scratch"] != "0"]
+    assert not bad, f"4-wave GEMM instantiations with scratch (accumulator spills behind asm MFMAs): {bad}"
+    assert all(k["agpr"] == "256" for k in ks), [(k["name"], k["agpr"]) for k in ks]
