@@ -228,6 +228,11 @@ def main() -> int:
         if args.parallel == "dp":
             from distributed_model_parallel_amd.parallel.data_parallel import reset_host_times
             reset_host_times()
+    # per-bucket all-reduce timing of every timed backward (DDP only; a captured
+    # graph replays without the reducer's host-side launches, so not there)
+    timed_comm = hasattr(st.wrapped, "enable_comm_timing") and not args.graph
+    if timed_comm:
+        st.wrapped.enable_comm_timing(True)
     from distributed_model_parallel_amd.utils import routes
     routes0 = routes.route_counts()
     bcast0 = getattr(st.wrapped, "buffer_broadcasts", None)
@@ -239,7 +244,18 @@ def main() -> int:
         torch.cuda.synchronize()
     comm.barrier()
     elapsed = time.perf_counter() - t0
+    rank_ms = 1000.0 * elapsed / args.steps
     elapsed = comm.max_scalar(elapsed)
+    # where DDP time goes (the reference's question, Readme.md:10-15 / 145-157):
+    # the last timed backward's per-bucket all-reduce ms and exposed comm tail,
+    # and the spread of the per-rank step times (a slow rank shows here)
+    ddp_comm = None
+    if timed_comm:
+        ddp_comm = st.wrapped.comm_timing()
+        st.wrapped.enable_comm_timing(False)
+        if "exposed_tail_ms" in ddp_comm:
+            ddp_comm["exposed_tail_ms_max_over_ranks"] = round(comm.max_scalar(ddp_comm["exposed_tail_ms"]), 3)
+    rank_step = {"max": round(comm.max_scalar(rank_ms), 3), "min": round(-comm.max_scalar(-rank_ms), 3)}
     final_loss = float(loss.item())
     step_routes = {k: round(v / args.steps, 2) for k, v in
                    sorted(routes.diff(routes.route_counts(), routes0).items())}
@@ -330,6 +346,8 @@ def main() -> int:
             "final_loss": round(final_loss, 4),
             "routes_per_step": step_routes,
             **({"ddp_buckets": ddp_facts} if ddp_facts is not None else {}),
+            **({"ddp_comm": ddp_comm} if ddp_comm is not None else {}),
+            "rank_step_ms": rank_step,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 2 ** 30, 1)
             if dev.type == "cuda" else None,
         },

@@ -537,8 +537,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<dmp::ReduceBackend, std::shared_ptr<dmp::ReduceBackend>>(m, "ReduceBackend");
   py::class_<dmp::RcclReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::RcclReduceBackend>>(
       m, "RcclReduceBackend")
-      .def(py::init<std::shared_ptr<dmp::RcclComm>, double, int64_t>(), py::arg("comm"),
-           py::arg("postscale") = 1.0, py::arg("debug_delay_cycles") = 0);
+      .def(py::init<std::shared_ptr<dmp::RcclComm>, double, int64_t, bool>(), py::arg("comm"),
+           py::arg("postscale") = 1.0, py::arg("debug_delay_cycles") = 0, py::arg("fp32_accum") = false)
+      .def("set_timing", &dmp::RcclReduceBackend::set_timing, py::arg("on"))
+      .def("last_timing", &dmp::RcclReduceBackend::last_timing,
+           "[ready->done ms per bucket..., collective ms per bucket..., exposed tail ms] of the last backward",
+           py::call_guard<py::gil_scoped_release>());
   py::class_<dmp::NullReduceBackend, dmp::ReduceBackend, std::shared_ptr<dmp::NullReduceBackend>>(
       m, "NullReduceBackend")
       .def(py::init<>());

@@ -1,5 +1,6 @@
 #include "reducer.h"
 #include "../trace.h"
+#include "../check.h"
 
 #include <ATen/hip/Sleep.h>
 #include <ATen/hip/HIPContext.h>
@@ -10,6 +11,7 @@
 #include <torch/csrc/autograd/variable.h>
 #include <torch/csrc/autograd/grad_mode.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <map>
 #include <unordered_set>
@@ -27,15 +29,95 @@ using torch::autograd::variable_list;
 // ---------------------------------------------------------------------------
 // Python comm-hook backend
 // ---------------------------------------------------------------------------
-void RcclReduceBackend::launch(int64_t, at::Tensor& flat) {
-  comm_->all_reduce(flat, "avg");
-  if (delay_ == 0 && postscale_ == 1.0) return;
+namespace {
+hipEvent_t new_timing_event() {
+  hipEvent_t e = nullptr;
+  DMP_HIP_CHECK(hipEventCreate(&e));
+  return e;
+}
+}  // namespace
+
+RcclReduceBackend::~RcclReduceBackend() {
+  if (device_ < 0) return;
+  c10::hip::HIPGuard g(device_);
+  for (auto e : ev_ready_) (void)hipEventDestroy(e);
+  for (auto e : ev_done_) (void)hipEventDestroy(e);
+  if (ev_bwd_end_) (void)hipEventDestroy(ev_bwd_end_);
+  if (ev_tail_) (void)hipEventDestroy(ev_tail_);
+}
+
+void RcclReduceBackend::launch(int64_t index, at::Tensor& flat) {
+  const int dev = flat.device().index();
+  const hipStream_t caller = at::hip::getCurrentHIPStream(dev).stream();
+  if (timing_) {
+    c10::hip::HIPGuard g(dev);
+    device_ = dev;
+    while ((int64_t)ev_ready_.size() <= index) {
+      ev_ready_.push_back(new_timing_event());
+      ev_done_.push_back(new_timing_event());
+    }
+    DMP_HIP_CHECK(hipEventRecord(ev_ready_[index], caller));
+  }
+  if (fp32_ && (flat.scalar_type() == at::kBFloat16 || flat.scalar_type() == at::kHalf)) {
+    // upcast, average and round back on the collective's stream (the copy is
+    // allocated there, so the caching allocator keeps it until the copy-back)
+    if (!comm_->is_inline()) comm_->sync_from_current();
+    c10::hip::HIPStreamGuard guard(comm_->is_inline() ? at::hip::getCurrentHIPStream(dev) : comm_->torch_stream());
+    at::Tensor wide = flat.to(at::kFloat);
+    comm_->all_reduce(wide, "avg", /*on_current_stream=*/true);
+    flat.copy_(wide);
+  } else {
+    comm_->all_reduce(flat, "avg");
+  }
   // the tail runs on the stream the collective used, so wait_all() covers it
-  c10::hip::HIPStreamGuard guard(comm_->is_inline()
-                                     ? at::hip::getCurrentHIPStream(flat.device().index())
-                                     : comm_->torch_stream());
-  if (delay_ > 0) at::cuda::sleep(delay_);
-  if (postscale_ != 1.0) flat.mul_(postscale_);
+  const hipStream_t cs = comm_->is_inline() ? caller : comm_->stream();
+  if (delay_ != 0 || postscale_ != 1.0) {
+    c10::hip::HIPStreamGuard guard(comm_->is_inline() ? at::hip::getCurrentHIPStream(dev) : comm_->torch_stream());
+    if (delay_ > 0) at::cuda::sleep(delay_);
+    if (postscale_ != 1.0) flat.mul_(postscale_);
+  }
+  if (timing_) {
+    DMP_HIP_CHECK(hipEventRecord(ev_done_[index], cs));
+    launched_ = std::max(launched_, index + 1);
+  }
+}
+
+void RcclReduceBackend::wait_all() {
+  if (!timing_ || launched_ == 0) {
+    comm_->wait();
+    return;
+  }
+  c10::hip::HIPGuard g(device_);
+  if (!ev_bwd_end_) {
+    ev_bwd_end_ = new_timing_event();
+    ev_tail_ = new_timing_event();
+  }
+  const hipStream_t cur = at::hip::getCurrentHIPStream(device_).stream();
+  DMP_HIP_CHECK(hipEventRecord(ev_bwd_end_, cur));
+  comm_->wait();
+  DMP_HIP_CHECK(hipEventRecord(ev_tail_, cur));
+  last_n_ = launched_;
+  launched_ = 0;
+}
+
+std::vector<double> RcclReduceBackend::last_timing() {
+  if (last_n_ == 0) return {};
+  c10::hip::HIPGuard g(device_);
+  DMP_HIP_CHECK(hipEventSynchronize(ev_tail_));
+  auto ms = [](hipEvent_t a, hipEvent_t b) {
+    float t = 0.f;
+    DMP_HIP_CHECK(hipEventElapsedTime(&t, a, b));
+    return (double)t;
+  };
+  std::vector<double> ready_done(last_n_), coll(last_n_);
+  for (int64_t i = 0; i < last_n_; ++i) {
+    ready_done[i] = ms(ev_ready_[i], ev_done_[i]);
+    coll[i] = i == 0 ? ready_done[i] : std::min(ready_done[i], ms(ev_done_[i - 1], ev_done_[i]));
+  }
+  std::vector<double> out(ready_done);
+  out.insert(out.end(), coll.begin(), coll.end());
+  out.push_back(ms(ev_bwd_end_, ev_tail_));
+  return out;
 }
 
 PyReduceBackend::~PyReduceBackend() {

@@ -51,16 +51,37 @@ class RcclReduceBackend : public ReduceBackend {
   // debug_delay_cycles: spin the comm stream before the scale -- a test knob
   // that widens any missing comm-stream -> compute-stream ordering into a
   // visible wrong result (tests/test_gpu_ddp.py).
+  // fp32_accum: a bf16 / fp16 bucket is averaged through an fp32 copy on the
+  // comm stream (2x the bytes on the wire; the ring then rounds once, at the
+  // end, instead of after every hop: tests/test_multirank_risks.py bounds both)
   explicit RcclReduceBackend(std::shared_ptr<RcclComm> comm, double postscale = 1.0,
-                             int64_t debug_delay_cycles = 0)
-      : comm_(std::move(comm)), postscale_(postscale), delay_(debug_delay_cycles) {}
+                             int64_t debug_delay_cycles = 0, bool fp32_accum = false)
+      : comm_(std::move(comm)), postscale_(postscale), delay_(debug_delay_cycles), fp32_(fp32_accum) {}
+  ~RcclReduceBackend() override;
   void launch(int64_t, at::Tensor& flat) override;
-  void wait_all() override { comm_->wait(); }
+  void wait_all() override;
+
+  // Communication accounting (bench.py config.ddp_comm): with timing on, each
+  // launch records an event on the launching stream (the bucket is ready) and
+  // one on the collective's stream after it (done); wait_all() records the end
+  // of backward and the point the compute stream may continue.  last_timing()
+  // (host-synchronising) returns, for the last backward: per bucket the
+  // ready -> done ms and the collective's own ms (from the later of its ready
+  // point and the previous bucket's done: the comm stream is serial), then the
+  // exposed tail ms (end of backward -> every bucket reduced).
+  void set_timing(bool on) { timing_ = on; }
+  std::vector<double> last_timing();
 
  private:
   std::shared_ptr<RcclComm> comm_;
   double postscale_;
   int64_t delay_;
+  bool fp32_ = false;
+  bool timing_ = false;
+  int64_t launched_ = 0, last_n_ = 0;
+  int device_ = -1;
+  std::vector<hipEvent_t> ev_ready_, ev_done_;
+  hipEvent_t ev_bwd_end_ = nullptr, ev_tail_ = nullptr;
 };
 
 // world_size == 1: the average over one rank is the identity, nothing to move.

@@ -23,6 +23,20 @@ from .. import _native
 
 _counter = itertools.count()
 
+# Every communicator this process created, in creation order, with what decides
+# its stream's hardware queue: (purpose, group ranks, device type, priority,
+# inline).  DDP's bucket communicator and SyncBatchNorm's moment communicator
+# drive two streams; with GPU_MAX_HW_QUEUES (4) those streams may share a
+# hardware queue, where kernels execute in submission order.  A cross-
+# communicator deadlock needs two ranks whose queues hold the two collectives
+# in opposite orders.  The merged submission order is rank-independent
+# (parallel/sync_batchnorm.py, "Ordering"); the stream -> queue assignment is
+# the runtime's round-robin over streams in creation order, so it is the same
+# on every rank exactly when the communicators (and their streams) were
+# created in the same order with the same flags -- which verify_comm_layout()
+# asserts instead of assuming.
+_LAYOUT: list = []
+
 
 def _store():
     return dist.distributed_c10d._get_default_store()
@@ -36,12 +50,17 @@ class Communicator:
     current stream depend on them, or :meth:`synchronize` to block the host.
     """
 
-    def __init__(self, device: torch.device, group: Optional[dist.ProcessGroup] = None):
+    def __init__(self, device: torch.device, group: Optional[dist.ProcessGroup] = None,
+                 purpose: str = "generic"):
         self.device = torch.device(device)
         self.group = group
         self.rank = dist.get_rank(group)
         self.size = dist.get_world_size(group)
+        self.purpose = purpose
         self._comm = None
+        ranks = None if group is None else tuple(dist.get_process_group_ranks(group))
+        _LAYOUT.append((purpose, ranks, self.device.type, os.environ.get("DMP_COMM_PRIORITY", "normal"),
+                        os.environ.get("DMP_COMM_INLINE", "0")))
         if self.device.type == "cuda":
             C = _native.require("RCCL communicator")
             key = f"dmp/rccl_uid/{next(_counter)}"
@@ -176,6 +195,29 @@ def _torch_op(op: str):
 _default: Optional[Communicator] = None
 
 
+def comm_layout() -> list:
+    """This process's communicators in creation order (see _LAYOUT)."""
+    return list(_LAYOUT)
+
+
+def verify_comm_layout(where: str = "", group: Optional[dist.ProcessGroup] = None) -> int:
+    """Collective over ``group``: raise on every rank unless all its ranks
+    created the same communicators in the same order with the same stream
+    flags.  Returns the layout digest."""
+    import zlib
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return 0
+    dig = zlib.crc32(repr(_LAYOUT).encode())
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([dig, -dig], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if int(t[0]) != dig or int(t[1]) != -dig:
+        raise RuntimeError(f"communicator layout differs across ranks{' at ' + where if where else ''}: this "
+                           f"rank created {_LAYOUT}; collectives of different communicators could then share "
+                           "hardware queues in different orders on different ranks and deadlock")
+    return dig
+
+
 def default_communicator(device: Optional[torch.device] = None) -> Communicator:
     """Process-wide communicator over the default group (created lazily)."""
     global _default
@@ -183,7 +225,7 @@ def default_communicator(device: Optional[torch.device] = None) -> Communicator:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
-        _default = Communicator(device)
+        _default = Communicator(device, purpose="default")
     return _default
 
 
@@ -191,5 +233,6 @@ def reset_default_communicator() -> None:
     """Forget the process-wide communicators (default + SyncBN's own)."""
     global _default
     _default = None
+    _LAYOUT.clear()
     from ..parallel.sync_batchnorm import reset_syncbn_communicators
     reset_syncbn_communicators()

@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import torch
@@ -33,7 +34,7 @@ import torch.nn as nn
 
 from ..utils.env import single_rank_comm
 from .. import _native
-from ..comm.rccl import Communicator, default_communicator
+from ..comm.rccl import Communicator, default_communicator, verify_comm_layout
 from ..ops import flat as flatops
 from ..utils.profiling import trace_range
 
@@ -79,22 +80,55 @@ def _bucket_assignment_py(params: Sequence[torch.Tensor], order: Sequence[int], 
 
 
 class _PyHookBackend:
-    """Python comm hook adapter: average all-reduce over a process group."""
+    """Python comm hook adapter: average all-reduce over a process group.
 
-    def __init__(self, group, world: int):
+    With ``timing`` on it keeps host timestamps per bucket (the gloo / CPU form
+    of the RCCL backend's event timing): the launch (bucket ready), the start
+    and end of its wait.  Waits run in bucket order once backward has finished,
+    so the first wait marks the end of backward and the last one the end of the
+    exposed communication tail."""
+
+    def __init__(self, group, world: int, fp32_accum: bool = False):
         self.group = group
         self.world = world
+        self.fp32_accum = fp32_accum
+        self.timing = False
+        self._t = {}
+        self.last = None
 
     def __call__(self, index: int, bucket: torch.Tensor):
-        work = dist.all_reduce(bucket, group=self.group, async_op=True)
+        red = bucket.float() if self.fp32_accum and bucket.dtype in (torch.bfloat16, torch.float16) else bucket
+        work = dist.all_reduce(red, group=self.group, async_op=True)
         world = self.world
+        backend = self
+        if self.timing:
+            self._t[index] = [time.perf_counter(), 0.0, 0.0]
 
         class _H:
             def wait(self_inner):
+                t = backend._t.get(index) if backend.timing else None
+                if t is not None:
+                    t[1] = time.perf_counter()
                 work.wait()
-                bucket.div_(world)
+                if red is bucket:
+                    bucket.div_(world)
+                else:
+                    bucket.copy_(red.div_(world))
+                if t is not None:
+                    t[2] = time.perf_counter()
+                    if index == max(backend._t):
+                        backend._close()
 
         return _H()
+
+    def _close(self) -> None:
+        ts = [self._t[i] for i in sorted(self._t)]
+        self._t = {}
+        if not ts:
+            return
+        ready_done = [1e3 * (t[2] - t[0]) for t in ts]
+        coll = [ready_done[0]] + [min(ready_done[i], 1e3 * (ts[i][2] - ts[i - 1][2])) for i in range(1, len(ts))]
+        self.last = ready_done + coll + [1e3 * (ts[-1][2] - ts[0][1])]
 
 
 class DistributedDataParallel(nn.Module):
@@ -104,7 +138,8 @@ class DistributedDataParallel(nn.Module):
                  bucket_cap_mb: float = 25.0, find_unused_parameters: bool = False,
                  gradient_as_bucket_view: bool = True, static_graph: bool = False,
                  first_bucket_mb: float = 1.0, flat_parameters: bool = False,
-                 rebuild_buckets: bool = True, communicator: Optional[Communicator] = None):
+                 rebuild_buckets: bool = True, communicator: Optional[Communicator] = None,
+                 reduce_dtype: Optional[torch.dtype] = None):
         super().__init__()
         if not dist.is_initialized():
             raise RuntimeError("DistributedDataParallel requires torch.distributed to be initialised "
@@ -123,6 +158,11 @@ class DistributedDataParallel(nn.Module):
         self.static_graph = static_graph
         self.require_backward_grad_sync = True
         self.require_forward_param_sync = True
+        # reduce_dtype=torch.float32: bf16 / fp16 buckets are averaged through an
+        # fp32 copy (one rounding instead of one per ring hop; 2x the bytes)
+        if reduce_dtype not in (None, torch.float32):
+            raise ValueError("reduce_dtype must be None (the gradient dtype) or torch.float32")
+        self.reduce_fp32 = reduce_dtype == torch.float32
         self.bucket_cap = int(bucket_cap_mb * _MB)
         self.first_bucket_cap = int(first_bucket_mb * _MB)
         self._rebuild_pending = rebuild_buckets and not static_graph
@@ -152,9 +192,10 @@ class DistributedDataParallel(nn.Module):
 
         if dev.type == "cuda":
             self.comm = communicator or (default_communicator(dev) if process_group is None
-                                          else Communicator(dev, process_group))
+                                          else Communicator(dev, process_group, purpose="ddp"))
         else:
-            self.comm = communicator or Communicator(dev, process_group)
+            self.comm = communicator or Communicator(dev, process_group, purpose="ddp")
+        verify_comm_layout("DistributedDataParallel", process_group)
 
         self._verify_params_across_ranks()
         self._sync_module_states()
@@ -181,15 +222,56 @@ class DistributedDataParallel(nn.Module):
     # ------------------------------------------------------------------ #
     def _make_backend(self):
         C = _native.native()
+        self._timing_src = None  # the object whose timing the bench reads
         if self.world_size == 1 and not single_rank_comm():
             # averaging over one rank is the identity: no collective to launch
             self.comm_backend = "none(world_size=1)"
             return C.NullReduceBackend()
         if self.comm.native is not None:
             self.comm_backend = "rccl"
-            return C.RcclReduceBackend(self.comm.native)
+            b = C.RcclReduceBackend(self.comm.native, fp32_accum=self.reduce_fp32)
+            self._timing_src = b
+            return b
         self.comm_backend = "process_group"
-        return C.PyReduceBackend(_PyHookBackend(self.group, self.world_size))
+        hook = _PyHookBackend(self.group, self.world_size, self.reduce_fp32)
+        self._timing_src = hook
+        return C.PyReduceBackend(hook)
+
+    # ------------------------------------------------------------------ #
+    def enable_comm_timing(self, on: bool = True) -> None:
+        """Time every bucket's all-reduce and the exposed communication tail of
+        each backward (HIP events on the RCCL path, host clocks on a process
+        group); read with ``comm_timing()``."""
+        src = self._timing_src
+        if src is None:
+            return
+        if isinstance(src, _PyHookBackend):
+            src.timing = bool(on)
+        else:
+            src.set_timing(bool(on))
+
+    def comm_timing(self) -> dict:
+        """The last backward's communication accounting (the reference's
+        "bucketed ring all-reduce overlapped with backward", Readme.md:145-157,
+        made measurable): per bucket (launch order) the ms from the bucket being
+        ready to its all-reduce done and the all-reduce's own ms, and the exposed
+        tail -- ms from the end of backward until every bucket is reduced."""
+        out = {"backend": self.comm_backend}
+        src = self._timing_src
+        if src is None:
+            return out
+        if isinstance(src, _PyHookBackend):
+            vals, out["source"] = src.last, "host_clock"
+        else:
+            vals, out["source"] = list(src.last_timing()), "hip_events"
+        if not vals:
+            return out
+        n = (len(vals) - 1) // 2
+        r = lambda xs: [round(float(x), 3) for x in xs]  # noqa: E731
+        out.update({"buckets_timed": n, "ready_to_done_ms": r(vals[:n]), "allreduce_ms": r(vals[n:2 * n]),
+                    "allreduce_ms_total": round(float(sum(vals[n:2 * n])), 3),
+                    "exposed_tail_ms": round(float(vals[-1]), 3)})
+        return out
 
     def register_comm_hook(self, state: Any, hook: Callable) -> None:
         """hook(state, bucket_tensor) -> torch.futures.Future (result ignored; the

@@ -18,7 +18,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..comm.rccl import Communicator
+from ..comm.rccl import Communicator, verify_comm_layout
 from ..ops.batchnorm import BatchNormAct2d
 from ..utils.env import single_rank_comm
 
@@ -44,13 +44,20 @@ from ..utils.env import single_rank_comm
 # rank-independent and every blocking kernel waits only for kernels its peers
 # submitted before theirs.  tests/test_comm_ordering.py records the merged
 # order on every rank of a DDP + SyncBN ResNet-18 and requires it identical.
+# Which streams share a hardware queue follows stream creation order; that the
+# communicators (and so their streams) were created in the same order with the
+# same flags on every rank is not assumed but checked collectively when this
+# communicator is created (comm/rccl.py verify_comm_layout).
 _COMMS = {}
 
 
 def syncbn_communicator(device: torch.device, group: Optional[dist.ProcessGroup] = None) -> Communicator:
     key = (str(device), id(group) if group is not None else None)
     if key not in _COMMS:
-        _COMMS[key] = Communicator(device, group)
+        _COMMS[key] = Communicator(device, group, purpose="syncbn")
+        # the second stream-driving communicator exists now: every rank must
+        # have created the same ones in the same order (comm/rccl.py _LAYOUT)
+        verify_comm_layout("SyncBatchNorm communicator", group)
     return _COMMS[key]
 
 

@@ -35,6 +35,17 @@ def _check_ddp(d: dict) -> None:
     assert 4 <= b["buckets"] <= 6 and abs(sum(b["bucket_mb"]) - 97.49) < 0.5, b
     assert b["buffer_broadcasts_per_step"] == b["buffer_dtype_groups"] == 2, b
     assert c["final_loss"] == c["final_loss"]  # not NaN
+    # communication accounting: per-bucket all-reduce
+    # times of the last timed backward, the exposed tail and the rank spread
+    cc = c["ddp_comm"]
+    assert cc["backend"] == "process_group" and cc["source"] == "host_clock", cc
+    n = b["buckets"]
+    assert cc["buckets_timed"] == n and len(cc["ready_to_done_ms"]) == n and len(cc["allreduce_ms"]) == n, cc
+    assert all(x >= 0 for x in cc["ready_to_done_ms"] + cc["allreduce_ms"]) and cc["exposed_tail_ms"] >= 0, cc
+    assert all(a <= r + 1e-6 for a, r in zip(cc["allreduce_ms"], cc["ready_to_done_ms"])), cc
+    assert cc["exposed_tail_ms_max_over_ranks"] >= cc["exposed_tail_ms"] - 1e-6, cc
+    rs = c["rank_step_ms"]
+    assert 0 < rs["min"] <= rs["max"] <= d["ms_per_step"] + 1e-3, rs
 
 
 def test_resnet50_ddp_8_ranks():
