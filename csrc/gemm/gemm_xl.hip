@@ -2221,6 +2221,16 @@ int pick_bm(int64_t M, int64_t N, int64_t K) {
 
 unsigned long long* g_xl_tdbg = nullptr;  // set_gemm_xl_trace
 
+// Epilogues the 4-wave kernel takes.  The operand-heavy conv epilogues
+// (folded-BN affine + residual, every BN-backward form) run on short-K 1x1
+// GEMMs whose time is mostly epilogue, and with one wave per SIMD and half the
+// threads per row pass their HBM round trips are less hidden: in the ResNet-50
+// step XL_BNBWD_YO took 12.9 vs 10.8 ms and XL_AFFINE 10.4 vs 9.8 ms on the
+// 4-wave kernel (profiles/README.md finding 69), so they keep the 8-wave
+// ping-pong (PIPE 10).  XL_BNBWD's runtime operand flags would also spill
+// accumulators behind the inline-asm MFMAs (tests/test_kernel_resources.py).
+__host__ __device__ constexpr bool w4_epi(int e) { return e != XL_AFFINE && !is_bnbwd(e); }
+
 // the 4-wave kernel addresses A (plain) and B through 32-bit buffer offsets
 bool w4_ok(const XlArgs& a) {
   const int64_t lim = (int64_t)1 << 31;
@@ -2246,7 +2256,7 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
   // inline-asm MFMAs that write them -- read before the MFMA completes.  It
   // keeps the 8-wave kernel; tests/test_kernel_resources.py holds every
   // gemm_xl_w4_kernel instantiation to zero scratch.)
-  if constexpr (EPI != XL_BNBWD) {
+  if constexpr (w4_epi(EPI)) {
   if (g_xl_pipe == 11 && w4_ok(a)) {
     XlArgs w = a;
     w.bm = 256;
@@ -2279,7 +2289,10 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
     hipLaunchKernelGGL((gemm_xl_tail_epi<EPI>), dim3(rem), dim3(XTHREADS), 0, s, t);
     return;
   }
-  hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+  if (g_xl_pipe == 11)  // an epilogue / operand the 4-wave kernel does not take
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 10>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
 }
 
 template <int BN, int EPI>

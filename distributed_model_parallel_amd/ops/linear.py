@@ -46,13 +46,15 @@ def set_xl_linear(on: bool) -> None:
 
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 # The PLAIN GEMMs -- nothing to fuse but a bias: the qkv projection forward
-# and the data gradients of qkv / proj / fc1 -- on gemm_xl ("xl", default) or
-# hipBLASLt ("lib").  Until round 5 the library won (finding 50: the 8-wave
-# ping-pong kernel ran 0.85-0.93 PF/s on these shapes); the 4-wave kernel
-# (gemm_xl PIPE 11, finding 69) runs them at 1.03-1.07 PF/s, at or above the
-# library's picks (tools/pipe_bench.py).  The fused-epilogue GEMMs and every
-# weight gradient (gemm_tn_xl) were already ours.
-_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "xl") == "lib"
+# and the data gradients of qkv / proj / fc1 -- on hipBLASLt ("lib", default)
+# or gemm_xl ("xl").  The 4-wave kernel (gemm_xl PIPE 11, finding 69) ties the
+# library in isolation on the N >= 2304 shapes (1.03-1.07 PF/s,
+# tools/pipe_bench.py), but in the step the data gradients are all N = 768
+# (591 tiles = 2.3 rounds of 256 CUs; the library's 256 x 224 tile fills them
+# better) and need a W^T copy: 8.0 + 0.4 ms vs 7.4 ms per step (ViT 41.0 vs
+# 40.3 ms).  The fused-epilogue GEMMs and every weight gradient (gemm_tn_xl)
+# are ours.
+_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "lib") == "lib"
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> bool:

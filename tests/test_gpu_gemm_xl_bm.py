@@ -23,7 +23,9 @@ BMS = [240, 224, 208, 192]
 @pytest.fixture
 def C():
     c = _native.require("gemm_xl bm tests")
-    c.set_gemm_xl_bn(256)  # these small grids would otherwise take 128-wide tiles (pick_bn)
+    # the 8-wave ping-pong kernel (PIPE 10) is the one with trimmed tiles; these
+    # small grids would otherwise take 128-wide tiles (pick_bn)
+    c.set_gemm_xl_bn(256, 10)
     yield c
     c.set_gemm_xl_bm(0)
     c.set_gemm_xl_bn(0)
