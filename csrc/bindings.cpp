@@ -112,13 +112,9 @@ void set_gemm_xl_bn(int bn, int pipe, int group_m);
 int get_gemm_xl_pipe();
 void set_gemm_xl_x2(int mode);
 int get_gemm_xl_x2();
-void set_gemm_xl_nt(int on);
-void set_gemm_xl_tail(int on);
-int get_gemm_xl_tail();
 void set_gemm_xl_bm(int bm);
 void set_gemm_xl_trace(const c10::optional<at::Tensor>& buf);
 int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K);
-int get_tn_xl_ring();
 std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int64_t kh, int64_t kw,
                                 int64_t stride, int64_t pad, int64_t ho, int64_t wo, const std::string& mode,
                                 const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& bn_x,
@@ -127,8 +123,6 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
                                 const c10::optional<at::Tensor>& bias);
 std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tensor& B, const at::Tensor& aux);
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
-// gemm_w4.hip
-at::Tensor gemm_w4(const at::Tensor& A, const at::Tensor& B, int64_t group_m, int64_t variant);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat, bool moments);
@@ -148,8 +142,6 @@ at::Tensor stem_fold_finish(const at::Tensor& img, int64_t ho, int64_t wo, const
 bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
-void set_tn_xl_ablation(int a);
-void set_tn_xl_ring(int r);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
 std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
@@ -366,12 +358,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
         "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
-  m.def("set_tn_xl_ablation", &dmp::set_tn_xl_ablation, py::arg("mode"));
-  m.def("set_tn_xl_ring", &dmp::set_tn_xl_ring, py::arg("ring"),
-        "gemm_tn_xl main loop: 0 = two tile buffers, 1 = the 10-slot LDS unit ring");
-  m.def("gemm_w4", &dmp::gemm_w4, py::arg("A"), py::arg("B"), py::arg("group_m") = 0, py::arg("variant") = 0,
-        "C = A @ B^T on the 4-wave 256x256 MFMA kernel (128x128 per wave, AGPR accumulators)",
-        py::call_guard<py::gil_scoped_release>());
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M",
         py::call_guard<py::gil_scoped_release>());
@@ -394,11 +380,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_gemm_xl_x2", &dmp::set_gemm_xl_x2, py::arg("mode"),
         "conv-epilogue GEMMs on the two-blocks-per-CU 256x128 kernel: 0 off, 1 where N % 256 != 0, 2 always");
   m.def("get_gemm_xl_x2", &dmp::get_gemm_xl_x2);
-  m.def("set_gemm_xl_nt", &dmp::set_gemm_xl_nt, py::arg("on"),
-        "conv-epilogue GEMMs: non-temporal C stores / residual loads (A/B; env DMP_XL_NT)");
-  m.def("set_gemm_xl_tail", &dmp::set_gemm_xl_tail, py::arg("on"),
-        "256x256 ping-pong GEMMs: split-K for the last partial round of tiles (default off, measured no faster: finding 54; env DMP_XL_TAIL=1)");
-  m.def("get_gemm_xl_tail", &dmp::get_gemm_xl_tail);
   m.def("set_gemm_xl_bm", &dmp::set_gemm_xl_bm, py::arg("bm"),
         "256x256 ping-pong GEMMs: rows per tile (0 auto: trimmed to fill whole rounds when K >= 768; "
         "-1 always 256; 192..240 forced; env DMP_XL_BM)");
@@ -407,9 +388,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "(int64 [blocks * 8]: entry, operands landed, main loop done, epilogue done, HW_ID, XCC_ID); None = off");
   m.def("get_gemm_xl_bm", &dmp::get_gemm_xl_bm, py::arg("M"), py::arg("N"), py::arg("K"),
         "rows per tile the ping-pong GEMM would take for this shape");
-  m.def("get_tn_xl_ring", &dmp::get_tn_xl_ring);
   m.def("set_gemm_xl_bn", &dmp::set_gemm_xl_bn, py::arg("bn"), py::arg("pipe") = -1, py::arg("group_m") = 0,
-        "debug: force the gemm_xl N tile (0 auto, 128, 256) and pipeline variant (0, 1)");
+        "debug: force the gemm_xl N tile (0 auto, 128, 256) and main loop (0, 1, 10, 11; -1 default)");
 
   // ---- BN folded through an expanding 1x1 conv (ops/bn_fold.py) ----
   m.def("bn_fold_supported", &dmp::bn_fold_supported, py::arg("cout"), py::arg("cin"));

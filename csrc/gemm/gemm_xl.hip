@@ -144,8 +144,6 @@ __device__ __forceinline__ void vmcnt_upto(int n) {
   }
 }
 
-// LDS ring depth of the PIPE 8 main loops, in 16 KB units (160 KB max)
-constexpr int XL_RING_SLOTS = 10;
 __device__ __forceinline__ void barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -200,13 +198,6 @@ struct XlArgs {
   const float* ebias;           // XL_BNBWD: per-column constant added to the GEMM output
   const float *esc, *esh;       // XL_AFFINE coefficients (null: 1 / 0)
   int erelu;                    // XL_AFFINE ReLU
-  int cnt;                      // conv epilogues: non-temporal C stores / residual loads (streamed once)
-  // split-K tail (PIPE 7): a launch with tbase > 0, ksplit == 0 runs tiles
-  // [0, tbase) of the tile order; one with ksplit > 0 runs each tile
-  // tbase + b / ksplit over K tiles [(b % ksplit) kper, +kper) and writes fp32
-  // partials to skws (gemm_xl_tail_epi sums them and runs the epilogue)
-  int tbase, ksplit, kper;
-  float* skws;
   // rows per tile of the PIPE 7 kernel (0 = 256): 192..240 trims the tile so
   // that an MFMA-bound grid fills whole 1-block/CU rounds (pick_bm)
   int bm;
@@ -302,7 +293,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& ac
         } else {
           rp = reinterpret_cast<const bf16x8*>(row_u < M ? rrow + pass * rstep : rbase + coll);
         }
-        L0[b][i] = p.cnt ? __builtin_nontemporal_load(rp) : *rp;
+        L0[b][i] = *rp;
       }
       if constexpr (kL12) {
         if constexpr (kLx) L1[b][i] = *reinterpret_cast<const bf16x8*>(row_u < M ? xrow + pass * xstep : xbase + coll);
@@ -337,7 +328,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& ac
   // per-column affine applied to the fp32 accumulator BEFORE the bf16 staging:
   // a bias / BN shift that nearly cancels acc (XL_BNBWD's folded-BN constant,
   // XL_AFFINE's -mean*scale) must not meet a bf16-rounded acc (finding 33)
-  if constexpr (PIPE == 7 || PIPE == 8 || PIPE == 10 || PIPE == 11) {
+  if constexpr (PIPE == 10 || PIPE == 11) {
     // transposed accumulators (see quad()): lane l holds row l & 15 and the 4
     // consecutive columns 4 (l >> 4) + e of each 16 x 16 block -> one 8-B LDS
     // write per block (a half-wave covers 16 rows x 16 B at a 528-B row pitch:
@@ -505,8 +496,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& ac
         }
         static_assert(!kBatch || EPI != XL_STORE, "batched epilogues write C rows unmapped");
         bf16x8* cp = reinterpret_cast<bf16x8*>(crow + (b * PB + i) * cstep);
-        if (p.cnt) __builtin_nontemporal_store(v, cp);
-        else *cp = v;
+        *cp = v;
       }
     }
     }
@@ -530,8 +520,7 @@ __device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& ac
         }
         const int64_t orow = EPI == XL_STORE ? xl_out_row(p.omap, row) : (int64_t)row;
         bf16x8* cp = reinterpret_cast<bf16x8*>(p.C + orow * p.ldc + col);
-        if (p.cnt) __builtin_nontemporal_store(v, cp);
-        else *cp = v;
+        *cp = v;
       }
     }
   }
@@ -566,7 +555,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   constexpr int MI = WTM / 16, NI = WTN / 16;       // 8 x (4 | 2) accumulators
   constexpr int RA = XBM * 64, RB = BN * 64;        // bytes of one k32 region
   constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;  // glds per wave per region
-  constexpr int STAGE_LDS = PIPE == 8 ? XL_RING_SLOTS * 16384 : 4 * RA + 4 * RB;
+  constexpr int STAGE_LDS = 4 * RA + 4 * RB;
   constexpr int CT_STRIDE = BN + 8;
   constexpr int EPI_LDS = XBM * CT_STRIDE * 2;
   constexpr int LDS = STAGE_LDS > EPI_LDS ? STAGE_LDS : EPI_LDS;
@@ -583,19 +572,11 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   const int M = p.M, N = p.N, K = p.K;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-  const int tbm = ((PIPE == 7 || PIPE == 10) && p.bm > 0) ? p.bm : XBM;  // rows per tile (pick_bm)
+  const int tbm = (PIPE == 10 && p.bm > 0) ? p.bm : XBM;  // rows per tile (pick_bm)
   const int mtiles = (M + tbm - 1) / tbm, ntiles = (N + BN - 1) / BN;
   int mt, nt;
-  int kt_begin = 0, kt_end = K / XBK;
-  if constexpr (PIPE == 9) {  // split-K tail launch: PIPE 7's loop over one K split, fp32 partials out
-    tile_coords_id(p.tbase + (int)blockIdx.x / p.ksplit, mtiles, ntiles, p.group_m, mt, nt);
-    kt_begin = ((int)blockIdx.x % p.ksplit) * p.kper;
-    kt_end = min(kt_end, kt_begin + p.kper);
-  } else if (p.tbase > 0) {  // the full rounds of a split-tail GEMM
-    tile_coords_id(xcd_remap(blockIdx.x, p.tbase), mtiles, ntiles, p.group_m, mt, nt);
-  } else {
-    tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
-  }
+  const int kt_begin = 0, kt_end = K / XBK;
+  tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
   const int m0 = mt * tbm, n0 = nt * BN;
   const int ktiles = K / XBK;
   if (p.tdbg && threadIdx.x == 0) {
@@ -706,7 +687,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
     if (has2) vmcnt<W2>(); else if (has1) vmcnt<NA + NB>(); else vmcnt<0>();
     barrier();
   }
-  } else if constexpr (PIPE == 7 || PIPE == 9 || PIPE == 10) {
+  } else if constexpr (PIPE == 10) {
   // ---- PIPE 7: ping-pong quadrant schedule (cdna_hip_programming.md §5 "256²
   // 8-phase template").  The two wave rows (wr) run one barrier apart: while
   // one group's 4 waves run a phase's 16 MFMAs, the other group (one wave on
@@ -792,7 +773,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   // and its slot frees two phases earlier -- the copies are issued 4 phases
   // ahead of their readers instead of 2 (vmcnt(8): 64 KB in flight per wave
   // group instead of 32 KB)
-  constexpr bool kDeep = PIPE == 10;
+  constexpr bool kDeep = true;  // (the round-4 schedule re-read B's n half 0: PIPE 7, removed)
   bf16x8 qa[2][4], qb[kDeep ? 2 : 1][2][2];
   auto read_a = [&](int mq, int buf) {
 #pragma unroll
@@ -851,7 +832,6 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   using I3 = std::integral_constant<int, 3>;
   // K tiles [kt_begin, kt_end): the whole K, or one split of a tail tile
   // (kt_begin even, so K tile kt still lives in buffer kt & 1)
-  if constexpr (kDeep) {
   // ---- PIPE 10 unit schedule.  Readers: U0, U1 of tile t in phase 0 (quad
   // (0,0)), U2 in phase 1, U3 in phase 2; phase 3 reads nothing.  Phase r of
   // tile t stages U2(t+1), U3(t+1), U0(t+2), U1(t+2): each is written >= 2
@@ -892,207 +872,6 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   if (wr == 0) barrier();  // equal barrier counts before the epilogue
   barrier();
   xl_mark(p, 2);
-  } else {
-  stage_unit(I0{}, kt_begin);
-  stage_unit(I2{}, kt_begin);
-  stage_unit(I3{}, kt_begin);
-  stage_unit(I1{}, kt_begin);
-  if (kt_end - kt_begin > 1) {
-    stage_unit(I0{}, kt_begin + 1);
-    stage_unit(I2{}, kt_begin + 1);
-    vmcnt<4>();
-  } else {
-    vmcnt<0>();
-  }
-  barrier();
-  xl_mark(p, 1);
-  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
-  for (int kt = kt_begin; kt < kt_end; ++kt) {
-    const int buf = kt & 1;
-    const bool n1 = kt + 1 < kt_end, n2 = kt + 2 < kt_end;
-    read_a(0, buf);
-    read_b(0, buf);
-    if (n1) { stage_unit(I3{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I0{}, I0{});
-    read_b(1, buf);
-    if (n1) { stage_unit(I1{}, kt + 1); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I0{}, I1{});
-    read_a(1, buf);
-    if (n2) { stage_unit(I0{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I1{}, I1{});
-    read_b(0, buf);
-    if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
-    quad(I1{}, I0{});
-  }
-  if (wr == 0) barrier();  // equal barrier counts before the epilogue
-  barrier();
-  xl_mark(p, 2);
-  }
-  } else if constexpr (PIPE == 8) {
-  // ---- PIPE 8: the ping-pong quadrant schedule of PIPE 7 on a ring of NS
-  // 16 KB unit slots instead of two fixed tile buffers (finding 42: PIPE 7
-  // keeps only two units = 32 KB in flight per CU, ~650-700 TF/s; the same
-  // schedule without the operand stream runs 1.2 PF/s).  Units are numbered
-  // in issue order i = 4 t + k, k = 0..3 <-> U0 (A m half 0), U2 (B n half 1),
-  // U3 (A m half 1), U1 (B n half 0) of K tile t; with the quadrant order
-  // (0,0) (0,1) (1,1) (1,0) unit i is last read in phase i (phase g = 4 t + r).
-  // Unit i lives in slot i % NS and is issued in phase i - D, D = NS - 1, so
-  // it overwrites unit i - NS, last read in phase i - NS = (issue phase) - 1
-  // (WAR: >= 2 barriers, as PIPE 7).  Phase g may read up to unit g + 4 (U1 of
-  // the next tile), so the phase-g wait retires every unit <= g + 4 and leaves
-  // V = D - 4 = NS - 5 units in flight: 80 KB at NS = 10 (vmcnt 10).
-  // Slot layout: [k32 half 2][8 blocks][16 rows x 64 B] (the 1 KB block is
-  // PIPE 7's 16-row swizzled image); block bj holds rows (bj >> 2) * 128 +
-  // mq * 64 + (bj & 3) * 16 of an A unit, cols (bj >> 1) * 64 + nq * 32 +
-  // (bj & 1) * 16 of a B unit -- the same rows PIPE 7's staging lanes fetch.
-  static_assert(BN == 256, "ring schedule is written for 256 x 256 tiles");
-  constexpr int NS = XL_RING_SLOTS, D = NS - 1, V = NS - 5, SLOT = 16384;
-  static_assert(NS * SLOT <= 160 * 1024, "ring exceeds LDS");
-  const int pks = wave >> 2;
-  const int bj0 = (2 * wave) & 7;  // block of copy q is bj0 + q
-  const bf16* pa[2][2];
-  const bf16* pa2[2][2];
-  const bf16* pb[2][2];
-#pragma unroll
-  for (int v = 0; v < 2; ++v)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int j = bj0 + q;
-      const int ra = (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow;
-      const int rb = (j >> 1) * 64 + v * 32 + (j & 1) * 16 + srow;
-      pa[v][q] = A + (int64_t)min(m0 + ra, M - 1) * lda + schunk * 8 + pks * 32;
-      pa2[v][q] = p.A2 ? p.A2 + xl_out_row(p.a2m, min(m0 + ra, M - 1)) * p.lda2 + schunk * 8 + pks * 32 - p.K1
-                       : nullptr;
-      pb[v][q] = B + (int64_t)min(n0 + rb, N - 1) * ldb + schunk * 8 + pks * 32;
-    }
-  const XlConv cv = p.cv;
-  const bool gather = cv.cin > 0;
-  const int loff = schunk * 8 + pks * 32;
-  int gpix[2][2], gih[2][2], giw[2][2];
-  if (gather) {
-    const int hw = cv.ho * cv.wo;
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int j = bj0 + q;
-        const int row = min(m0 + (j >> 2) * 128 + v * 64 + (j & 3) * 16 + srow, M - 1);
-        const int n = row / hw, r = row - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
-        gih[v][q] = oh * cv.stride - cv.pad;
-        giw[v][q] = ow * cv.stride - cv.pad;
-        gpix[v][q] = (n * cv.hi + gih[v][q]) * cv.wi + giw[v][q];
-      }
-  }
-  const int U = 4 * ktiles;
-  // issue unit i (kind k = i & 3) into its slot; the per-kind operand tables
-  // are indexed by compile-time constants only (a runtime index would put
-  // them in scratch, cdna_hip_programming.md rule 20)
-  auto stage_a8 = [&](auto vc, int kt, char* dst) {
-    constexpr int VV = decltype(vc)::value;  // U0: m half 0, U3: m half 1
-    const int koff = kt * XBK;
-    if (gather) {
-      const int cpt = cv.cin >> 6, tap = kt / cpt, c0 = (kt - tap * cpt) << 6;
-      const int tr = tap / cv.kw, tc = tap - tr * cv.kw;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int ih = gih[VV][q] + tr, iw = giw[VV][q] + tc;
-        const bool ok = (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
-        const bf16* src = ok ? A + (int64_t)(gpix[VV][q] + tr * cv.wi + tc) * lda + c0 + loff : g_zero_row + loff;
-        glds16(src, dst + q * 1024);
-      }
-      return;
-    }
-    const bool second = p.A2 && koff >= p.K1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) glds16((second ? pa2[VV][q] : pa[VV][q]) + koff, dst + q * 1024);
-  };
-  auto stage_b8 = [&](auto vc, int kt, char* dst) {
-    constexpr int VV = decltype(vc)::value;  // U1: n half 0, U2: n half 1
-#pragma unroll
-    for (int q = 0; q < 2; ++q) glds16(pb[VV][q] + kt * XBK, dst + q * 1024);
-  };
-  auto stage_i = [&](int i) {
-    const int kt = i >> 2, k = i & 3;
-    char* dst = smem + (i % NS) * SLOT + pks * 8192 + bj0 * 1024;
-    if (k == 0) stage_a8(std::integral_constant<int, 0>{}, kt, dst);
-    else if (k == 1) stage_b8(std::integral_constant<int, 1>{}, kt, dst);
-    else if (k == 2) stage_a8(std::integral_constant<int, 1>{}, kt, dst);
-    else stage_b8(std::integral_constant<int, 0>{}, kt, dst);
-  };
-  // retire every unit <= g + 4 given units < issued are in flight or done
-  auto wait_for = [&](int g, int issued) {
-    const int n = min(V, issued - 1 - (g + 4));
-    vmcnt_upto<2 * V>(n > 0 ? 2 * n : 0);
-  };
-  bf16x8 qa[2][4], qb[2][2];
-  auto read_a = [&](int slot) {
-    const char* base = smem + slot * SLOT + (wr * 4) * 1024 + frag_off;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) qa[ks][i] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + i * 1024);
-  };
-  auto read_b = [&](int slot) {
-    const char* base = smem + slot * SLOT + (wc * 2) * 1024 + frag_off;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) qb[ks][j] = *reinterpret_cast<const bf16x8*>(base + ks * 8192 + j * 1024);
-  };
-  auto quad = [&](auto mqc, auto nqc) {
-    constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
-    barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    // operands swapped: acc holds C^T blocks (lane = output row, registers =
-    // 4 consecutive output columns), so the epilogue stages 8-B row pieces
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[MQ * 4 + i][NQ * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(qb[ks][j], qa[ks][i], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    barrier();
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  const int pro = min(D, U);
-  for (int i = 0; i < pro; ++i) stage_i(i);
-  wait_for(-1, pro);  // units 0..3 (tile 0) landed
-  barrier();
-  if (wr == 1) barrier();  // the stagger: wave row 1 runs one barrier behind
-  int issued = pro;
-  int s0 = 0;  // slot of unit 4 kt
-  for (int kt = 0; kt < ktiles; ++kt) {
-    const int g = 4 * kt;
-    const int sU0 = s0, sU2 = s0 + 1 >= NS ? s0 + 1 - NS : s0 + 1;
-    const int sU3 = s0 + 2 >= NS ? s0 + 2 - NS : s0 + 2, sU1 = s0 + 3 >= NS ? s0 + 3 - NS : s0 + 3;
-    read_a(sU0);
-    read_b(sU1);
-    if (issued < U) stage_i(issued++);
-    wait_for(g, issued);
-    quad(I0{}, I0{});
-    read_b(sU2);
-    if (issued < U) stage_i(issued++);
-    wait_for(g + 1, issued);
-    quad(I0{}, I1{});
-    read_a(sU3);
-    if (issued < U) stage_i(issued++);
-    wait_for(g + 2, issued);
-    quad(I1{}, I1{});
-    read_b(sU1);
-    if (issued < U) stage_i(issued++);
-    wait_for(g + 3, issued);
-    quad(I1{}, I0{});
-    s0 = s0 + 4 >= NS ? s0 + 4 - NS : s0 + 4;
-  }
-  if (wr == 0) barrier();  // equal barrier counts before the epilogue
-  barrier();
   } else {
   // ---- PIPE 1: half-step ring.  Half-step s (K tile s/2, k32 half s%2) lives
   // in LDS region s%4.  During half-step s: stage region s%4 with the data of
@@ -1139,19 +918,15 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   if (S >= 4) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
   lgkm0();
   barrier();
-  // PIPE 2..4 are timing-only ablations (wrong results): 2 = no copies in the
-  // loop, 3 = no fragment reads in the loop, 4 = MFMAs only
-  constexpr bool kStage = PIPE != 2 && PIPE != 4, kRead = PIPE != 3 && PIPE != 4;  // 5: no epilogue
-  if constexpr (!kRead) read_frags(ya, yb, 1);
   for (int s = 0; s < S; s += 2) {
-    if (kStage && s + 4 < S) stage_h(s + 4);
-    if (kRead) read_frags(ya, yb, s + 1);
+    if (s + 4 < S) stage_h(s + 4);
+    read_frags(ya, yb, s + 1);
     mfmas(xa, xb);
     if (s + 4 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
     lgkm0();
     barrier();
-    if (kStage && s + 5 < S) stage_h(s + 5);
-    if (kRead && s + 2 < S) read_frags(xa, xb, s + 2);
+    if (s + 5 < S) stage_h(s + 5);
+    if (s + 2 < S) read_frags(xa, xb, s + 2);
     mfmas(ya, yb);
     if (s + 5 < S) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
     lgkm0();
@@ -1160,27 +935,6 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_nt_kernel(const XlArgs p)
   }
 
   // ---- epilogue: (acc [+ bias]) -> bf16 tile in LDS, then row-contiguous pass ----
-  if constexpr (PIPE == 5) {  // timing-only ablation: no epilogue (acc kept live)
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) t += acc[i][j][0] + acc[i][j][3];
-    if (t == 12345.678f) p.C[tid] = (bf16)t;
-    return;
-  }
-  if constexpr (PIPE == 9) {  // split-K tail tile: fp32 partials, the epilogue runs in gemm_xl_tail_epi
-    // (a compile-time variant: as a runtime branch the write path cost the
-    // BN-backward epilogue 220 B of scratch per lane)
-    // thread-contiguous 512-B records (immediate store offsets: no per-store
-    // address registers in the epilogue's register budget)
-    f32x4* ws = reinterpret_cast<f32x4*>(p.skws) + ((int64_t)blockIdx.x * XTHREADS + tid) * (MI * NI);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) ws[i * NI + j] = acc[i][j];
-    return;
-  }
   // every operand copy has landed (the main loops end on vmcnt(0) in inline
   // asm, which the compiler cannot see): say so with a wait it does see, or it
   // drains the epilogue's first operand batch before its first LDS write to
@@ -1369,34 +1123,6 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
     __syncthreads();
     xl_mark(p, 3);
   }
-}
-
-// Epilogue of the split-K tail tiles: block b sums the ksplit fp32 partials of
-// tile tbase + b (PIPE 7 register layout, written by the ksplit launch of
-// gemm_xl_nt_kernel) and runs that tile's epilogue.
-template <int EPI>
-__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_tail_epi(const XlArgs p) {
-  constexpr int BN = 256, MI = 8, NI = BN / 64;
-  constexpr int LDS = XBM * (BN + 8) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[LDS];
-  const int mtiles = (p.M + XBM - 1) / XBM, ntiles = (p.N + BN - 1) / BN;
-  int mt, nt;
-  tile_coords_id(p.tbase + (int)blockIdx.x, mtiles, ntiles, p.group_m, mt, nt);
-  const int tid = threadIdx.x;
-  f32x4 acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int sp = 0; sp < p.ksplit; ++sp) {  // split launch block blockIdx.x * ksplit + sp, same record layout
-    const f32x4* ws = reinterpret_cast<const f32x4*>(p.skws) +
-                      (((int64_t)blockIdx.x * p.ksplit + sp) * XTHREADS + tid) * (MI * NI);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] += ws[i * NI + j];
-  }
-  xl_epilogue<BN, EPI, 7, LDS>(p, acc, smem, mt * XBM, nt * BN, mt, mtiles);
 }
 
 // ---------------------------------------------------------------------------
@@ -1654,216 +1380,6 @@ __global__ __launch_bounds__(XTHREADS, 4) void gemm_x2_kernel(const XlArgs p) { 
   }
 }
 
-// Epilogue transform of one 8-column bf16 vector of row `row` (already holding
-// bf16(acc [+ bias])); writes the side output of XL_BIAS_GELU.
-template <int EPI>
-__device__ __forceinline__ bf16x8 epi_vec(bf16x8 v, int64_t row, int col, const XlArgs& p) {
-  if constexpr (EPI == XL_BIAS_GELU) {
-    *reinterpret_cast<bf16x8*>(p.aux + row * p.ldaux + col) = v;
-    f32x8 f = __builtin_convertvector(v, f32x8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = gelu_f(f[j]);
-    return __builtin_convertvector(f, bf16x8);
-  } else if constexpr (EPI == XL_DGELU) {
-    f32x8 f = __builtin_convertvector(v, f32x8);
-    const f32x8 x = __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.aux + row * p.ldaux + col), f32x8);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] *= gelu_grad_f(x[j]);
-    return __builtin_convertvector(f, bf16x8);
-  } else if constexpr (EPI == XL_BIAS_RES) {
-    f32x8 f = __builtin_convertvector(v, f32x8);
-    f += __builtin_convertvector(*reinterpret_cast<const bf16x8*>(p.R + row * p.ldr + col), f32x8);
-    return __builtin_convertvector(f, bf16x8);
-  } else {
-    return v;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Persistent form: one 512-thread block per CU walks the tiles
-// L = i * gridDim.x + pos(block) (pos = XCD-aware, so each round's tiles on one
-// XCD are 32 consecutive ids of the grouped order).  The half-step ring runs
-// straight across tile boundaries -- the next tile's first K tiles are in
-// flight while the current tile finishes and stores -- which removes the
-// per-tile pipeline fill and the synchronized all-CU prologue burst that
-// dominate short-K (K = 768) transformer GEMMs.  The epilogue cannot use the
-// ring's LDS (it holds the next tile's operands), so each wave stores its
-// 128 x WTN sub-tile through a private 16-row LDS scratch.  It runs at the
-// start of the next tile's first half-step, BEFORE that step's copies: the
-// half-step's closing vmcnt then still retires everything it must (all ops
-// older than the 2 x (NA+NB) youngest are complete), only more conservatively.
-// ---------------------------------------------------------------------------
-template <int BN, int EPI>
-__global__ __launch_bounds__(XTHREADS, 1) void gemm_xl_persistent_kernel(const XlArgs p) {
-  constexpr int WTM = 128, WTN = BN / 4;
-  constexpr int MI = WTM / 16, NI = WTN / 16;
-  constexpr int RA = XBM * 64, RB = BN * 64;
-  constexpr int NA = RA / 1024 / 8, NB = RB / 1024 / 8;
-  constexpr int RING = 4 * RA + 4 * RB;
-  constexpr int SCR_STRIDE = WTN + 8;                 // bf16 elements per scratch row
-  constexpr int SCR_WAVE = 16 * SCR_STRIDE * 2;       // bytes per wave
-  __shared__ __attribute__((aligned(16))) char smem[RING + 8 * SCR_WAVE];
-
-  const int M = p.M, N = p.N, K = p.K;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wc = wave & 3;
-  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + BN - 1) / BN;
-  const int total = mtiles * ntiles;
-  const int G = gridDim.x;
-  const int pos = xcd_remap(blockIdx.x, G);
-  const int my_tiles = pos < total ? (total - pos + G - 1) / G : 0;
-  const int ktiles = K / XBK;
-  const int HS = 2 * ktiles;                // half-steps per tile
-  const int S = my_tiles * HS;
-  if (S == 0) return;
-
-  auto coords = [&](int ti, int& m0, int& n0) {
-    const int L = ti * G + pos;
-    const int per_group = p.group_m * ntiles;
-    const int g = L / per_group, r = L - g * per_group;
-    const int gm = min(p.group_m, mtiles - g * p.group_m);
-    m0 = (g * p.group_m + r % gm) * XBM;
-    n0 = (r / gm) * BN;
-  };
-
-  const int srow = lane >> 2;
-  const int schunk = (lane & 3) ^ chunk_xor(lane >> 4);
-  // staging cursor: tile of the most recent stage call (advanced monotonically)
-  int st_tile = -1, st_m0 = 0, st_n0 = 0;
-  auto stage_h = [&](int h) {
-    const int ti = h / HS, rem = h - ti * HS;
-    if (ti != st_tile) { st_tile = ti; coords(ti, st_m0, st_n0); }
-    const int koff = (rem >> 1) * XBK + (rem & 1) * 32 + schunk * 8;
-    char* da = smem + (h & 3) * RA + wave * NA * 1024;
-    char* db = smem + 4 * RA + (h & 3) * RB + wave * NB * 1024;
-#pragma unroll
-    for (int q = 0; q < NA; ++q) {
-      const int r = min(st_m0 + (wave * NA + q) * 16 + srow, M - 1);
-      glds16(p.A + (int64_t)r * p.lda + koff, da + q * 1024);
-    }
-#pragma unroll
-    for (int q = 0; q < NB; ++q) {
-      const int r = min(st_n0 + (wave * NB + q) * 16 + srow, N - 1);
-      glds16(p.B + (int64_t)r * p.ldb + koff, db + q * 1024);
-    }
-  };
-
-  const int lrow = lane & 15, lk = lane >> 4;
-  const int frag_off = lrow * 64 + ((lk ^ chunk_xor(lrow >> 2)) << 4);
-  f32x4 acc[MI][NI];
-  bf16x8 xa[MI], xb[NI], ya[MI], yb[NI];
-  auto zero_acc = [&] {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-  auto read_frags = [&](bf16x8 (&fa)[MI], bf16x8 (&fbb)[NI], int h) {
-    const char* ar = smem + (h & 3) * RA + (wr * WTM) * 64 + frag_off;
-    const char* br = smem + 4 * RA + (h & 3) * RB + (wc * WTN) * 64 + frag_off;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) fbb[j] = *reinterpret_cast<const bf16x8*>(br + j * 16 * 64);
-#pragma unroll
-    for (int i = 0; i < MI; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(ar + i * 16 * 64);
-  };
-  auto mfmas = [&](const bf16x8 (&fa)[MI], const bf16x8 (&fbb)[NI]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fbb[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  bf16* scr = reinterpret_cast<bf16*>(smem + RING + wave * SCR_WAVE);
-  auto epilogue = [&](int ti) {
-    int m0, n0;
-    coords(ti, m0, n0);
-    float bv[NI];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int col = n0 + wc * WTN + j * 16 + (lane & 15);
-      bv[j] = 0.f;
-      if constexpr (EPI == XL_BIAS || EPI == XL_BIAS_GELU || EPI == XL_BIAS_RES)
-        bv[j] = col < N ? (float)p.bias[col] : 0.f;
-    }
-    constexpr int VPR = WTN / 8;          // 16-B vectors per scratch row
-    constexpr int VPL = 16 * VPR / 64;    // vectors per lane per 16-row block
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          scr[((lane >> 4) * 4 + e) * SCR_STRIDE + j * 16 + (lane & 15)] = (bf16)(acc[i][j][e] + bv[j]);
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        const int idx = lane + v * 64, r = idx / VPR, cv = idx % VPR;
-        bf16x8 val = *reinterpret_cast<const bf16x8*>(scr + r * SCR_STRIDE + cv * 8);
-        const int64_t row = m0 + wr * WTM + i * 16 + r;
-        const int col = n0 + wc * WTN + cv * 8;
-        if (row < M && col < N) {
-          val = epi_vec<EPI>(val, row, col, p);
-          *reinterpret_cast<bf16x8*>(p.C + row * p.ldc + col) = val;
-        }
-      }
-    }
-  };
-
-  zero_acc();
-  // prologue: half-steps 0..3 in flight; retire 0, read it, retire 1
-  stage_h(0);
-  stage_h(1);
-  if (S >= 4) {
-    stage_h(2);
-    stage_h(3);
-    vmcnt<3 * (NA + NB)>();
-  } else {
-    vmcnt<NA + NB>();
-  }
-  barrier();
-  read_frags(xa, xb, 0);
-  if (S >= 4) vmcnt<2 * (NA + NB)>(); else vmcnt<0>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  barrier();
-  int tile_left = HS;  // half-steps left in the current tile
-  int cur_tile = 0;
-  // After an interior tile's epilogue (issued right after the step's copies),
-  // the next three half-step closings may leave its MI*VPL C stores in flight:
-  // every op younger than the copies being retired still includes them.
-  constexpr int W = 2 * (NA + NB), E = MI * ((16 * WTN / 8) / 64);
-  int credit = 0;
-  auto close_step = [&](bool more) {
-    if (!more) vmcnt<0>();
-    else if (credit > 0) vmcnt<W + E>();
-    else vmcnt<W>();
-    credit = credit > 0 ? credit - 1 : 0;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    barrier();
-  };
-  for (int s = 0; s < S; s += 2) {
-    if (s + 4 < S) stage_h(s + 4);
-    if (tile_left == 0) {  // previous tile done: store it, start the next
-      int m0, n0;
-      coords(cur_tile, m0, n0);
-      epilogue(cur_tile);
-      credit = (m0 + XBM <= M && n0 + BN <= N) ? 3 : 0;
-      zero_acc();
-      ++cur_tile;
-      tile_left = HS;
-    }
-    read_frags(ya, yb, s + 1);
-    mfmas(xa, xb);
-    close_step(s + 4 < S);
-    if (s + 5 < S) stage_h(s + 5);
-    if (s + 2 < S) read_frags(xa, xb, s + 2);
-    mfmas(ya, yb);
-    close_step(s + 5 < S);
-    tile_left -= 2;
-  }
-  epilogue(cur_tile);
-}
-
 // ---------------------------------------------------------------------------
 // Weight-gradient GEMM on the ping-pong schedule:
 //   part[split][n][k] = sum_{m in split} A[m, n] * B[m, k]
@@ -1898,18 +1414,9 @@ __device__ __forceinline__ int tn64_off(int row, int col) {
   return row * 64 + ((((byte >> 5) ^ tn64_swz(row))) << 5) + (byte & 31);
 }
 
-// ABL (timing-only ablations, tools/tn_vit_pmc.py --ablate): 1 = no global
-// staging after the prologue (the LDS tiles go stale: schedule + LDS + MFMA
-// bound), 2 = staging kept but no barriers inside the main loop.
-// ABL (timing-only ablations, tools/tn_vit_pmc.py --ablate): 1 = no global
-// staging after the prologue (the LDS tiles go stale: schedule + LDS + MFMA
-// bound), 2 = staging kept but no barriers inside the main loop.  RING: the
-// LDS unit ring of gemm_xl_nt_kernel PIPE 8 instead of two tile buffers.
-template <int ABL, int RING>
 __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs p) {
   constexpr int PLANE = 64 * 64, OPER = 8 * PLANE;  // bytes
-  constexpr int NS = XL_RING_SLOTS, SLOT = 4 * PLANE;
-  __shared__ __attribute__((aligned(16))) char smem[RING ? NS * SLOT : 4 * OPER];
+  __shared__ __attribute__((aligned(16))) char smem[4 * OPER];
   using v4i16 = short __attribute__((ext_vector_type(4)));
   using lds_v4 = __attribute__((address_space(3))) v4i16;
   const int M = p.M, N = p.N, K = p.K;
@@ -1947,7 +1454,6 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
   }
   auto stage_unit = [&](auto u, int kt) {
     constexpr int U = decltype(u)::value;
-    if (ABL == 1 && kt > 1) return;
     const int buf = kt & 1;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -2010,7 +1516,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
   };
   auto quad = [&](auto mqc, auto nqc) {
     constexpr int MQ = decltype(mqc)::value, NQ = decltype(nqc)::value;
-    if (ABL != 2) barrier();
+    barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -2024,100 +1530,13 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks][i], qb[ks][j], acc[MQ * 4 + i][NQ * 2 + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    if (ABL != 2) barrier();
+    barrier();
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using I2 = std::integral_constant<int, 2>;
   using I3 = std::integral_constant<int, 3>;
-  if constexpr (RING) {
-    // the unit ring of gemm_xl_nt_kernel PIPE 8 (same issue order, slot rule
-    // and counted waits); a unit slot holds 4 planes: A units U0 / U3 planes
-    // {0,1,4,5} / {2,3,6,7} as 2 wr + (plane & 1), B units U1 / U2 planes
-    // {0,2,4,6} / {1,3,5,7} as plane >> 1 (= wc of the reading wave)
-    constexpr int D = NS - 1, V = NS - 5;
-    const int U = 4 * KT;
-    auto stage_i = [&](int i) {
-      const int kt = i >> 2, k = i & 3;
-      char* slot = smem + (i % NS) * SLOT + pi * PLANE;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int64_t m = mb + (int64_t)kt * 64 + srow[q];
-        char* dst = slot + ((2 * (wave & 1) + q) << 10);
-        const bf16* src = g_zero_row;
-        if (k == 0 || k == 2) {
-          const int pl = k + (pi & 1) + (pi >> 1) * 4;
-          const int col = n0 + pl * 32 + scol[q];
-          if (m < me && col < N) src = p.A + m * p.lda + col;
-        } else {
-          const int pl = 2 * pi + (k == 1 ? 1 : 0);
-          const int col = pl * 32 + scol[q];
-          if (m < me && k0 + col < K) {
-            if (!gather) {
-              src = p.B + m * p.ldb + k0 + col;
-            } else {
-              const int hw = cv.ho * cv.wo;
-              const int mi = (int)m, n = mi / hw, r = mi - n * hw, oh = r / cv.wo, ow = r - oh * cv.wo;
-              const int ih = oh * cv.stride - cv.pad + tr, iw = ow * cv.stride - cv.pad + tc;
-              if ((unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi)
-                src = p.B + ((int64_t)(n * cv.hi + ih) * cv.wi + iw) * p.ldb + kc0 + col;
-            }
-          }
-        }
-        glds16(src, dst);
-      }
-    };
-    auto wait_for = [&](int g, int issued) {
-      const int n = min(V, issued - 1 - (g + 4));
-      vmcnt_upto<2 * V>(n > 0 ? 2 * n : 0);
-    };
-    auto ring_a = [&](int slot) {
-      const char* base = smem + slot * SLOT + wr * 2 * PLANE;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) qa[ks][i] = tr_frag(base + (i >> 1) * PLANE, ks, (i & 1) * 16 + 4 * p4);
-    };
-    auto ring_b = [&](int slot) {
-      const char* base = smem + slot * SLOT + wc * PLANE;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) qb[ks][j] = tr_frag(base, ks, j * 16 + 4 * p4);
-    };
-    if (U > 0) {
-      const int pro = min(D, U);
-      for (int i = 0; i < pro; ++i) stage_i(i);
-      wait_for(-1, pro);
-      barrier();
-      if (wr == 1) barrier();
-      int issued = pro, s0 = 0;
-      for (int kt = 0; kt < KT; ++kt) {
-        const int g = 4 * kt;
-        const int sU0 = s0, sU2 = s0 + 1 >= NS ? s0 + 1 - NS : s0 + 1;
-        const int sU3 = s0 + 2 >= NS ? s0 + 2 - NS : s0 + 2, sU1 = s0 + 3 >= NS ? s0 + 3 - NS : s0 + 3;
-        ring_a(sU0);
-        ring_b(sU1);
-        if (issued < U) stage_i(issued++);
-        wait_for(g, issued);
-        quad(I0{}, I0{});
-        ring_b(sU2);
-        if (issued < U) stage_i(issued++);
-        wait_for(g + 1, issued);
-        quad(I0{}, I1{});
-        ring_a(sU3);
-        if (issued < U) stage_i(issued++);
-        wait_for(g + 2, issued);
-        quad(I1{}, I1{});
-        ring_b(sU1);
-        if (issued < U) stage_i(issued++);
-        wait_for(g + 3, issued);
-        quad(I1{}, I0{});
-        s0 = s0 + 4 >= NS ? s0 + 4 - NS : s0 + 4;
-      }
-      if (wr == 0) barrier();
-    }
-  } else if (KT > 0) {
+  if (KT > 0) {
     stage_unit(I0{}, 0);
     stage_unit(I2{}, 0);
     stage_unit(I3{}, 0);
@@ -2130,7 +1549,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
       vmcnt<0>();
     }
     barrier();
-    if (ABL != 2 && wr == 1) barrier();
+    if (wr == 1) barrier();
     for (int kt = 0; kt < KT; ++kt) {
       const int buf = kt & 1;
       const bool n1 = kt + 1 < KT, n2 = kt + 2 < KT;
@@ -2148,7 +1567,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
       if (n2) { stage_unit(I2{}, kt + 2); vmcnt<4>(); } else { vmcnt<0>(); }
       quad(I1{}, I0{});
     }
-    if (ABL != 2 && wr == 0) barrier();
+    if (wr == 0) barrier();
   }
   float* out = p.part + (int64_t)split * N * K;
 #pragma unroll
@@ -2166,27 +1585,20 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
 
 int g_num_cus = 0;
 
-// main loop: 7 = ping-pong quadrant schedule on two tile buffers, 8 = the same
-// schedule on the 10-slot unit ring (256-wide tiles; 128-wide tiles use the
-// half-step ring, 1)
+// main loop of the 256 x 256 tiles: 11 = the 4-wave kernel (default), 10 =
+// the 8-wave ping-pong quadrant schedule; 128-wide tiles run the half-step
+// ring (1) or the round-1 two-buffer loop (0).  Measured and removed in round
+// 6 (notes in profiles/README.md): the round-4 ping-pong that re-read B's n
+// half 0 (7), its 10-slot LDS unit ring (8, slower: finding 43), the split-K
+// tail (9, no faster: finding 54), the persistent form (6, slower: finding
+// 66), timing-only ablations (2-5) and the non-temporal epilogue switch.
 constexpr int kXlPipeDefault = 11;
 int g_xl_pipe = [] {  // DMP_XL_PIPE=<n>: A/B of the main loop (10 = 8-wave ping-pong)
   const char* e = std::getenv("DMP_XL_PIPE");
   return e ? std::atoi(e) : kXlPipeDefault;
 }();
 
-// 256 x 256 ping-pong launch (PIPE 7 or its ring form, PIPE 8)
-// Split-K tail (DMP_XL_TAIL=1, set_gemm_xl_tail; default OFF): one block per
-// CU makes a grid's last, partly filled round cost a whole round (conv_xl at
-// batch 2048: layer 3, 6.1 rounds, 0.619 ms vs 0.513 ms at 6.0; layer 4, 3.06
-// rounds, 0.579 vs 0.448 ms; profiles/raw_r4/tile_tail_r4aj.md).  Here the
-// last round's tiles run with their K split over the otherwise idle CUs (fp32
-// partials, gemm_xl_tail_epi sums them and runs the epilogue), the full rounds
-// as before; a grid smaller than half the chip is split the same way.
-// Measured no faster (l3 0.634 -> 0.639 ms, l4 0.576 -> 0.570, bench 125.2 vs
-// 125.7 ms; profiles/README.md finding 54): the tail's epilogue then runs on
-// only `rem` CUs and reads ksplit fp32 partials each.  Kept for A/B.
-int g_xl_tail = [] { const char* e = std::getenv("DMP_XL_TAIL"); return e ? std::atoi(e) : 0; }();
+// 256 x 256 launches: PIPE 11 (4 waves) or PIPE 10 (8-wave ping-pong)
 
 int num_cus() {
   if (g_num_cus == 0) {
@@ -2206,7 +1618,7 @@ int num_cus() {
 int g_xl_bm = [] { const char* e = std::getenv("DMP_XL_BM"); return e ? std::atoi(e) : 0; }();
 
 int pick_bm(int64_t M, int64_t N, int64_t K) {
-  if ((g_xl_pipe != 7 && g_xl_pipe != 10) || g_xl_tail) return 256;
+  if (g_xl_pipe != 10) return 256;
   if (g_xl_bm > 0) return g_xl_bm;
   if (g_xl_bm < 0 || K < 768) return 256;
   const int64_t cus = num_cus(), nt = (N + 255) / 256;
@@ -2243,14 +1655,6 @@ template <int EPI>
 void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
   XlArgs a = a_in;
   a.tdbg = g_xl_tdbg;
-  if (g_xl_pipe == 8) {
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 8>), dim3(blocks), dim3(XTHREADS), 0, s, a);
-    return;
-  }
-  if (g_xl_pipe == 10) {
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 10>), dim3(blocks), dim3(XTHREADS), 0, s, a);
-    return;
-  }
   // (XL_BNBWD with its runtime operand flags needs more registers than the
   // 4-wave epilogue has: the compiler spills accumulators right behind the
   // inline-asm MFMAs that write them -- read before the MFMA completes.  It
@@ -2270,56 +1674,16 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
     return;
   }
   }
-  const int cus = num_cus(), ktiles = a.K / XBK, rem = blocks % cus;
-  int ks = rem > 0 ? std::min(cus / rem, ktiles / 6) : 0;
-  if (g_xl_tail && ktiles >= 16 && rem > 0 && 2 * rem <= cus && ks >= 2) {
-    const int kper = ((ktiles + ks - 1) / ks + 1) & ~1;  // even: K tile kt stays in buffer kt & 1
-    ks = (ktiles + kper - 1) / kper;
-    int dev = 0;
-    DMP_HIP_CHECK(hipGetDevice(&dev));
-    auto ws = at::empty({(int64_t)rem * ks * 32 * XTHREADS * 4}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
-    XlArgs m = a;
-    m.tbase = blocks - rem;
-    if (m.tbase > 0) hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(m.tbase), dim3(XTHREADS), 0, s, m);
-    XlArgs t = m;
-    t.ksplit = ks;
-    t.kper = kper;
-    t.skws = ws.data_ptr<float>();
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 9>), dim3(rem * ks), dim3(XTHREADS), 0, s, t);
-    hipLaunchKernelGGL((gemm_xl_tail_epi<EPI>), dim3(rem), dim3(XTHREADS), 0, s, t);
-    return;
-  }
-  if (g_xl_pipe == 11)  // an epilogue / operand the 4-wave kernel does not take
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 10>), dim3(blocks), dim3(XTHREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 7>), dim3(blocks), dim3(XTHREADS), 0, s, a);
+  // PIPE 10, or an epilogue / operand the 4-wave kernel does not take
+  hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 10>), dim3(blocks), dim3(XTHREADS), 0, s, a);
 }
 
 template <int BN, int EPI>
 void launch_xl(const XlArgs& a, hipStream_t s) {
   const int tbm = (BN == 256 && a.bm > 0) ? a.bm : XBM;
   const int blocks = ((a.M + tbm - 1) / tbm) * ((a.N + BN - 1) / BN);
-  if constexpr (EPI == XL_STORE) {
-    switch (g_xl_pipe) {  // timing-only ablations of the ring pipeline
-      case 2: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 2>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
-      case 3: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 3>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
-      case 4: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 4>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
-      case 5: hipLaunchKernelGGL((gemm_xl_nt_kernel<BN, EPI, 5>), dim3(blocks), dim3(XTHREADS), 0, s, a); return;
-      default: break;
-    }
-  }
-  if (g_xl_pipe == 6) {
-    if (g_num_cus == 0) {
-      int dev = 0;
-      DMP_HIP_CHECK(hipGetDevice(&dev));
-      DMP_HIP_CHECK(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const int grid = std::min(blocks, g_num_cus);
-    hipLaunchKernelGGL((gemm_xl_persistent_kernel<BN, EPI>), dim3(grid), dim3(XTHREADS), 0, s, a);
-    return;
-  }
   if constexpr (BN == 256) {
-    if (g_xl_pipe >= 7) {
+    if (g_xl_pipe >= 10) {
       launch_pp256<EPI>(a, blocks, s);
       return;
     }
@@ -2337,10 +1701,6 @@ void launch_xl(const XlArgs& a, hipStream_t s) {
 // GEMM with N % 128 == 0 (A/B)
 int g_xl_x2 = 1;
 
-// conv-epilogue GEMMs: non-temporal C stores and residual loads (A/B:
-// DMP_XL_NT=1 or set_gemm_xl_nt; the outputs are consumed by the next layer,
-// so at batch 256 they may still profit from the 256 MB last-level cache)
-int g_xl_nt = [] { const char* e = std::getenv("DMP_XL_NT"); return e ? std::atoi(e) : 0; }();
 
 bool use_x2(const XlArgs& a) {
   if (g_xl_x2 == 0 || a.N % X2_BN != 0) return false;
@@ -2366,7 +1726,7 @@ void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
     const int blocks = ((a.M + tbm - 1) / tbm) * ((a.N + bn - 1) / bn);
     if (bn == 128)
       hipLaunchKernelGGL((gemm_xl_nt_kernel<128, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
-    else if (g_xl_pipe >= 7)
+    else if (g_xl_pipe >= 10)
       launch_pp256<EPI>(a, blocks, s);
     else
       hipLaunchKernelGGL((gemm_xl_nt_kernel<256, EPI, 1>), dim3(blocks), dim3(XTHREADS), 0, s, a);
@@ -2391,7 +1751,7 @@ int pick_bn(int M, int N) {
     // useful work / (rounds x tile work); the 128-wide tile runs the ring
     // loop, ~12 % slower per FLOP than the 256-wide ring and ~25 % slower than
     // the 256-wide ping-pong loop (profiles/vit_gemm_backends.md)
-    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : (g_xl_pipe >= 7 ? 0.75 : 0.88));
+    return blocks / (rounds * cus) * (bn == 256 ? 1.0 : (g_xl_pipe >= 10 ? 0.75 : 0.88));
   };
   return eff(128) > eff(256) ? 128 : 256;
 }
@@ -2497,7 +1857,7 @@ std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tenso
   const int bn = pick_bn((int)M, (int)N);
   a.bm = bn == 256 ? pick_bm(M, N, K) : 256;
   const int mtiles = (int)((M + a.bm - 1) / a.bm);
-  const bool fused = g_xl_pipe != 6;  // the persistent ablation kernel has no column sums
+  const bool fused = true;
   at::Tensor part;
   if (fused) {
     part = at::empty({2, mtiles, N}, A.options().dtype(at::kFloat));
@@ -2546,7 +1906,6 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   auto C = at::empty({M, N}, A.options());
   a.C = reinterpret_cast<bf16*>(C.data_ptr()); a.ldc = C.stride(0);
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
-  a.cnt = g_xl_nt;
   if (!res_map.empty()) {
     TORCH_CHECK(mode == "bnbwd" && res_map.size() == 5, "res_map: bnbwd only, [stride, Ho, Wo, Hi, Wi]");
     a.rmap.s = (int)res_map[0]; a.rmap.ho = (int)res_map[1]; a.rmap.wo = (int)res_map[2];
@@ -2773,9 +2132,7 @@ void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out
 
 namespace {
 
-int g_tn_xl_ablate = 0;  // timing-only ablations of the TN main loop (see gemm_tn_pp_kernel)
 int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
-int g_tn_xl_ring = 0;    // 1: main loop on the LDS unit ring (PIPE 8 schedule)
 
 at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype) {
   const int M = a.M, N = a.N, K = a.K;
@@ -2794,14 +2151,7 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
   a.part = part.data_ptr<float>();
   hipStream_t s = at::hip::getCurrentHIPStream();
-  if (g_tn_xl_ablate == 1)
-    hipLaunchKernelGGL((gemm_tn_pp_kernel<1, 0>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
-  else if (g_tn_xl_ablate == 2)
-    hipLaunchKernelGGL((gemm_tn_pp_kernel<2, 0>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
-  else if (g_tn_xl_ring)
-    hipLaunchKernelGGL((gemm_tn_pp_kernel<0, 1>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemm_tn_pp_kernel<0, 0>), dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  hipLaunchKernelGGL(gemm_tn_pp_kernel, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   DMP_HIP_CHECK(hipGetLastError());
   split_reduce_launch(a.part, splits, (int64_t)N * K, out, s);
   return out;
@@ -2848,11 +2198,6 @@ at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, 
 }
 
 void set_tn_xl_rounds(int r) { g_tn_xl_rounds = r; }
-void set_tn_xl_ablation(int a) {
-  TORCH_CHECK(a >= 0 && a <= 2, "tn ablation must be 0 (off), 1 (no staging) or 2 (no barriers)");
-  g_tn_xl_ablate = a;
-}
-void set_tn_xl_ring(int r) { g_tn_xl_ring = r != 0; }
 
 int get_gemm_xl_pipe() { return g_xl_pipe; }
 void set_gemm_xl_x2(int mode) {
@@ -2860,16 +2205,23 @@ void set_gemm_xl_x2(int mode) {
   g_xl_x2 = mode;
 }
 int get_gemm_xl_x2() { return g_xl_x2; }
-void set_gemm_xl_nt(int on) { g_xl_nt = on ? 1 : 0; }
-void set_gemm_xl_tail(int on) { g_xl_tail = on ? 1 : 0; }
+// The trace buffer is held here (not just its pointer) so a tensor freed by
+// the caller can never receive timestamps; tracing cannot be switched on
+// while a stream is being captured (the pointer would be baked into the graph).
+at::Tensor g_xl_tbuf;
 void set_gemm_xl_trace(const c10::optional<at::Tensor>& buf) {
   if (!buf || !buf->defined()) {
     g_xl_tdbg = nullptr;
+    g_xl_tbuf = at::Tensor();
     return;
   }
   TORCH_CHECK(buf->is_cuda() && buf->scalar_type() == at::kLong && buf->is_contiguous(),
               "trace buffer: contiguous int64 GPU tensor of 8 entries per block");
-  g_xl_tdbg = reinterpret_cast<unsigned long long*>(buf->data_ptr());
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  DMP_HIP_CHECK(hipStreamIsCapturing(at::hip::getCurrentHIPStream().stream(), &cs));
+  TORCH_CHECK(cs == hipStreamCaptureStatusNone, "set_gemm_xl_trace: not while a stream is being captured");
+  g_xl_tbuf = *buf;
+  g_xl_tdbg = reinterpret_cast<unsigned long long*>(g_xl_tbuf.data_ptr());
 }
 void set_gemm_xl_bm(int bm) {
   TORCH_CHECK(bm == 0 || bm == -1 || (bm >= 192 && bm <= 256 && bm % 16 == 0),
@@ -2877,17 +2229,15 @@ void set_gemm_xl_bm(int bm) {
   g_xl_bm = bm;
 }
 int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K) { return pick_bm(M, N, K); }
-int get_gemm_xl_tail() { return g_xl_tail; }
-int get_tn_xl_ring() { return g_tn_xl_ring; }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
   if (pipe < 0) pipe = kXlPipeDefault;
   TORCH_CHECK(group_m >= 0, "group_m must be >= 0 (0 = default)");
   g_xl_group_m = group_m;
   TORCH_CHECK(bn == 0 || bn == 128 || bn == 256, "bn must be 0 (auto), 128 or 256");
-  TORCH_CHECK(pipe >= 0 && pipe <= 11 && pipe != 9,
-              "pipe must be 0..8 (2..5: timing-only ablations, 6: persistent, 7: ping-pong 256x256, "
-              "8: ping-pong on the LDS unit ring)");
+  TORCH_CHECK(pipe == 0 || pipe == 1 || pipe == 10 || pipe == 11,
+              "pipe must be 0 / 1 (8-wave 256 x 128 / 256 x 256 ring kernels), 10 (8-wave ping-pong) or "
+              "11 (4-wave, the default)");
   g_xl_bn_override = bn;
   g_xl_pipe = pipe;
 }

@@ -13,16 +13,6 @@ DEV = "cuda"
 CL = torch.channels_last
 
 
-@pytest.fixture(autouse=True, params=[0, 1], ids=["tilebuf", "ring"])
-def ring(request):
-    """Every case on both main loops: two tile buffers and the LDS unit ring."""
-    C = _native.require("gemm_tn_xl")
-    old = C.get_tn_xl_ring()
-    C.set_tn_xl_ring(request.param)
-    yield request.param
-    C.set_tn_xl_ring(old)
-
-
 @pytest.mark.parametrize("M,N,K", [(802816 // 4, 256, 1024), (5000, 200, 264), (100, 256, 256), (64, 512, 512),
                                    (33, 64, 128), (50176, 2048, 512)])
 @pytest.mark.parametrize("out", [torch.float32, torch.bfloat16])

@@ -20,10 +20,8 @@ def _tol(K):
     return dict(atol=0.03 * K ** 0.5, rtol=2e-2)
 
 
-@pytest.fixture(params=[(0, -1), (128, 1), (256, 1), (128, 0), (256, 0), (128, 6), (256, 6), (256, 7), (256, 8),
-                        (256, 10), (256, 11)],
-                ids=["auto", "bn128", "bn256", "bn128-pipe0", "bn256-pipe0", "bn128-persist", "bn256-persist",
-                     "bn256-pingpong", "bn256-ring", "bn256-pingpong-deep", "bn256-w4"])
+@pytest.fixture(params=[(0, -1), (128, 1), (256, 1), (128, 0), (256, 0), (256, 10), (256, 11)],
+                ids=["auto", "bn128", "bn256", "bn128-pipe0", "bn256-pipe0", "bn256-pingpong", "bn256-w4"])
 def bn(request):
     old = C().get_gemm_xl_pipe()
     C().set_gemm_xl_bn(*request.param)

@@ -48,7 +48,7 @@ def main():
         f_nt = timeit(lambda: C.gemm_nt(x, w, mode="moments"))
         d_nt = timeit(lambda: C.gemm_nt_bnbwd(dy, wt, None, x, None, mean, inv, None, None))
         res = {}
-        for pipe in (1, 7):  # ring vs ping-pong main loop (auto tile width)
+        for pipe in (1, 10, 11):  # ring vs ping-pong vs 4-wave main loop (auto tile width)
             C.set_gemm_xl_bn(0, pipe)
             res[pipe] = (
                 timeit(lambda: C.gemm_xl_conv(x, w, "moments")) if cout % 8 == 0 and cin % 64 == 0 else float("nan"),

@@ -58,7 +58,7 @@ def main():
         t_xl = timeit(lambda: C.gemm_xl(a, b)) if (K % 64 == 0 and N % 8 == 0) else float("nan")
         t_pp = float("nan")
         if K % 64 == 0 and N % 8 == 0:
-            C.set_gemm_xl_bn(256, 7)  # 256 x 256 ping-pong schedule (PIPE 7)
+            C.set_gemm_xl_bn(256, 10)  # 256 x 256 8-wave ping-pong schedule (PIPE 10)
             try:
                 t_pp = timeit(lambda: C.gemm_xl(a, b))
                 err = (C.gemm_xl(a, b).float() - (a.float() @ b.float().t())).abs().max().item() if M * N <= 1 << 26 else 0.0

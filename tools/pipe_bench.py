@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the 256 x 256 ping-pong main loops (csrc/gemm/gemm_xl.hip), e.g.
-PIPE 7 (B half 0 read twice per K tile, copies issued 2 phases ahead) vs
-PIPE 10 (both B halves held in registers, copies issued 4 phases ahead), for
+"""A/B of the 256 x 256 main loops (csrc/gemm/gemm_xl.hip): PIPE 10 (8-wave
+ping-pong, both B halves held in registers, copies issued 4 phases ahead) vs
+PIPE 11 (4 waves, 128 x 128 per wave in AGPRs, full-line LDS-DMA), for
 the NT kernel (gemm_xl store / conv epilogues / 3x3 implicit GEMM) and the TN
 weight-gradient kernel (gemm_tn_xl), on the ViT-B/16 and ResNet-50 shapes
 that carry the step time, plus hipBLASLt (torch.matmul) on the plain shapes.
@@ -10,7 +10,7 @@ Interleaved rounds in one process (cdna_hip_programming.md rule 24), random
 operands (rule 25); prints median / min ms and TF/s per arm and checks the two
 arms agree bit for bit (same MFMA order per accumulator).
 
-usage: python tools/pipe_bench.py [--pipes 7,10] [--rounds 5] [--iters 10] [--only name] [--no-tn]
+usage: python tools/pipe_bench.py [--pipes 10,11] [--lib] [--epi] [--rounds 5] [--iters 10] [--only name] [--no-tn]
 """
 import argparse
 import os
@@ -81,14 +81,13 @@ def ab(name, flops, arms, rounds, iters, exact=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--pipes", default="7,10")
+    ap.add_argument("--pipes", default="10,11")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--no-tn", action="store_true")
     ap.add_argument("--epi", action="store_true", help="also the fused ViT epilogues (bias, bias_gelu, dgelu, bias_res)")
     ap.add_argument("--lib", action="store_true", help="add a hipBLASLt arm on the plain shapes")
-    ap.add_argument("--w4", default="", help="gemm_w4 variants to add on the plain shapes, e.g. 0,1 (2/4/6: ablations)")
     a = ap.parse_args()
     pipes = [int(x) for x in a.pipes.split(",")]
     old_pipe = C.get_gemm_xl_pipe()
@@ -105,11 +104,9 @@ def main():
                     return C.gemm_xl(x, w)
                 return f
             arms = {f"pipe{p}": arm(p) for p in pipes}
-            for v in ([int(t) for t in a.w4.split(",")] if a.w4 else []):
-                arms[f"w4v{v}"] = (lambda v: lambda: C.gemm_w4(x, w, 0, v))(v)
             if a.lib:
                 arms["hipblaslt"] = lambda: x @ w.t()
-            ab(name, 2.0 * M * N * K, arms, a.rounds, a.iters, exact={f"pipe{p}" for p in pipes} | {"w4v4", "w4v5", "w4v14", "w4v15", "w4v20", "w4v21"})
+            ab(name, 2.0 * M * N * K, arms, a.rounds, a.iters, exact={f"pipe{p}" for p in pipes})
             if a.epi and name.startswith("vit"):
                 bias = torch.rand(N, device="cuda", dtype=torch.bfloat16) - 0.5
                 aux = torch.rand(M, N, device="cuda", dtype=torch.bfloat16) * 2 - 1

@@ -44,7 +44,7 @@ def main():
         lib = timeit(lambda: torch.addmm(b, x, w.t()))
         lib2 = timeit(lambda: F.gelu(torch.addmm(b, x, w.t()))) if "fc1" in name else \
             timeit(lambda: res + torch.addmm(b, x, w.t()))
-        for pipe in (7, 1, 6):
+        for pipe in (11, 10, 1):
             C.set_gemm_xl_bn(0, pipe)
             ts = [timeit(lambda: C.gemm_xl(x, w, m, **kw[m])) for m in modes]
             print(f"| {name} | {pipe} | " + " | ".join(f"{t:.3f}" for t in ts) + f" | {lib:.3f} | {lib2:.3f} |",
