@@ -100,7 +100,6 @@ std::vector<at::Tensor> conv_nt(const at::Tensor& x, const at::Tensor& wmat, int
 void set_gemm_tile(int64_t t);
 void set_phase_dgrad(bool on);
 void set_tn_wide(bool on);
-void set_tn_tall(int mode);
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
                       at::ScalarType out_dtype, int64_t kc);
@@ -274,8 +273,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.def("set_tn_wide", &dmp::set_tn_wide, py::arg("on"),
         "128 x 256 TN tiles for deep weight gradients (default on)");
-  m.def("set_tn_tall", &dmp::set_tn_tall, py::arg("mode"),
-        "split-M TN weight gradients: 256-row tiles for N >= 256 and K = 64 (1), also K = 128 (2); 0 off");
   m.def("set_phase_dgrad", &dmp::set_phase_dgrad, py::arg("on"),
         "strided implicit-GEMM data gradients as stride-phase launches (default on)");
   m.def("set_gemm_tile", &dmp::set_gemm_tile,
@@ -382,7 +379,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("get_gemm_xl_x2", &dmp::get_gemm_xl_x2);
   m.def("set_gemm_xl_bm", &dmp::set_gemm_xl_bm, py::arg("bm"),
         "256x256 ping-pong GEMMs: rows per tile (0 auto: trimmed to fill whole rounds when K >= 768; "
-        "-1 always 256; 192..240 forced; env DMP_XL_BM)");
+        "-1 always 256; 192..240 forced)");
   m.def("set_gemm_xl_trace", &dmp::set_gemm_xl_trace, py::arg("buf") = py::none(),
         "diagnostics: 256x256 ping-pong GEMM launches record per-block phase timestamps into buf "
         "(int64 [blocks * 8]: entry, operands landed, main loop done, epilogue done, HW_ID, XCC_ID); None = off");

@@ -554,13 +554,6 @@ int g_tile_override = -1;
 bool g_phase_dgrad = true;
 // Wide (128 x 256) TN tiles for deep weight gradients; set_tn_wide for A/B runs.
 bool g_tn_wide = true;
-// Tall (256 x K) TN tiles when N >= 256 and K <= 128 (the BN-fold D = dz^T a
-// and the 1x1 weight gradients of layers 1-2: dz has 4x the columns of a).  A
-// 128-row tile re-reads the narrow operand once per 128 columns of the wide
-// one (layer 1: 1.2x the minimum bytes, layer 2: 1.6x); a 256-row tile halves
-// that.  0 off, 1 for K = 64 (2 blocks / CU, 80 KB LDS), 2 also for K = 128
-// (1 block / CU, 96 KB LDS).  set_tn_tall for A/B runs.
-int g_tn_tall = 0;
 
 template <bool PRO, int EPI, bool CONV>
 void dispatch_tile(const NtArgs& a, int bm, hipStream_t s) {
@@ -898,10 +891,10 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   // 128 x 256 output tiles (1 block/CU) halve the L2 re-reads of A (dy) for deep
   // implicit-GEMM weight gradients (K = taps * Cin, Cin % 256 == 0): g_tn_wide
   const bool wide = g_tn_wide && bps == nullptr && N >= 128 && K >= 256 && kgran % 256 == 0;
-  int bnt = N >= 128 ? 128 : 64;
+  // (256-row split-M tiles for N >= 256, K <= 128 measured slower and were
+  // removed in round 6: profiles/README.md finding 58)
+  const int bnt = N >= 128 ? 128 : 64;
   const int bkt = wide ? 256 : ((K >= 128 && kgran % 128 == 0) ? 128 : 64);
-  if (!wide && N >= 256 && bps == nullptr && ((g_tn_tall >= 1 && bkt == 64) || (g_tn_tall >= 2 && bkt == 128)))
-    bnt = 256;
   const int tiles = ((N + bnt - 1) / bnt) * ((K + bkt - 1) / bkt);
   // ~4 blocks per CU, but keep the fp32 partial traffic well under the operand
   // traffic (the GEMM streams (N+K)*M bf16; partials cost 2 * splits*N*K*4 B).
@@ -919,8 +912,6 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   auto part = at::empty({splits, N, K}, A.options().dtype(at::kFloat));
   float* pp = part.data_ptr<float>();
   if (bkt == 256) launch_tn<128, 256>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
-  else if (bnt == 256 && bkt == 64) launch_tn<256, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
-  else if (bnt == 256) launch_tn<256, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bnt == 128 && bkt == 128) launch_tn<128, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
@@ -1383,6 +1374,5 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
 void set_gemm_tile(int64_t t) { g_tile_override = (int)t; }
 void set_phase_dgrad(bool on) { g_phase_dgrad = on; }
 void set_tn_wide(bool on) { g_tn_wide = on; }
-void set_tn_tall(int mode) { g_tn_tall = mode; }
 
 }  // namespace dmp

@@ -1615,7 +1615,7 @@ int num_cus() {
 // An MFMA-bound GEMM (K >= 768) instead takes the tile height in
 // {256, 240, .., 192} that minimises rounds x height: the skipped rows of a
 // trimmed tile cost their staging only.  0 = auto, -1 = always 256, else forced (A/B).
-int g_xl_bm = [] { const char* e = std::getenv("DMP_XL_BM"); return e ? std::atoi(e) : 0; }();
+int g_xl_bm = 0;
 
 int pick_bm(int64_t M, int64_t N, int64_t K) {
   if (g_xl_pipe != 10) return 256;

@@ -43,9 +43,6 @@ def _load() -> Optional[ModuleType]:
                 return _mod
             from . import _C  # type: ignore[attr-defined]
             _mod = _C
-            tall = os.environ.get("DMP_TN_TALL")
-            if tall not in (None, "") and hasattr(_mod, "set_tn_tall"):
-                _mod.set_tn_tall(int(tall))  # A/B: 256-row split-M TN tiles (csrc/conv/gemm_bf16.hip)
         except ImportError as e:  # pragma: no cover - depends on build state
             _err = e
             _mod = None

@@ -59,8 +59,7 @@ class Communicator:
         self.purpose = purpose
         self._comm = None
         ranks = None if group is None else tuple(dist.get_process_group_ranks(group))
-        _LAYOUT.append((purpose, ranks, self.device.type, os.environ.get("DMP_COMM_PRIORITY", "normal"),
-                        os.environ.get("DMP_COMM_INLINE", "0")))
+        _LAYOUT.append((purpose, ranks, self.device.type, os.environ.get("DMP_COMM_INLINE", "0")))
         if self.device.type == "cuda":
             C = _native.require("RCCL communicator")
             key = f"dmp/rccl_uid/{next(_counter)}"
@@ -70,10 +69,9 @@ class Communicator:
                 store.set(key, uid)
             else:
                 uid = store.get(key)
-            # NOT high priority by default: a high-priority HIP stream slowed the whole
-            # ResNet-50 step 1.9x on MI355X (67.3 vs 36.5 ms, profiles/README.md)
-            high = os.environ.get("DMP_COMM_PRIORITY", "normal") == "high"
-            self._comm = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high)
+            # NOT high priority: a high-priority HIP stream slowed the whole ResNet-50
+            # step 1.9x on MI355X (67.3 vs 36.5 ms, profiles/README.md finding 1)
+            self._comm = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, False)
             # DMP_COMM_INLINE=1: collectives on the compute stream (no overlap, no side queue)
             if os.environ.get("DMP_COMM_INLINE", "0") == "1":
                 self._comm.set_inline(True)

@@ -38,7 +38,6 @@ rounds al o W and W^T diag(be) W to bf16 where the unfused path rounded dy.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
@@ -276,22 +275,8 @@ def _gram(C, inp, geom, native, n):
     return C.gemm_tn_xl(inp, inp, torch.float32) if _tn_xl(inp.shape[0], c, c) else C.gemm_tn(inp, inp, torch.float32)
 
 
-_FOLD_GEMM_ENV = os.environ.get("DMP_FOLD_GEMM")  # A/B: 0 VALU, 1 hipBLASLt (default), 2 tiled kernel
-_fold_gemm_set = False
-
-
-def _apply_fold_gemm_env(C) -> None:
-    global _fold_gemm_set
-    if not _fold_gemm_set:
-        _fold_gemm_set = True
-        if _FOLD_GEMM_ENV not in (None, ""):
-            C.set_fold_gemm(int(_FOLD_GEMM_ENV))
-
-
 def _fold_branch_forward(C, b, n, native):
     """Gram, folded moments, (cross-rank reduce), finalize of one branch."""
-    if native:
-        _apply_fold_gemm_env(C)
     W, asums, geom = b["W"], b["asums"], b["geom"]
     cout, cin = W.shape
     rm, rv, momentum, eps, nbt, rmom, _ = b["spec"]

@@ -15,7 +15,6 @@ subsample copy, no scatter pass.  Anything the kernel does not cover (CPU, fp32,
 """
 from __future__ import annotations
 
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -204,7 +203,7 @@ _TN_XL = not _native.disabled("tn_xl")
 _STATS["tn_xl"] = 0
 
 
-_TN_XL_MIN_ROWS = int(os.environ.get("DMP_TN_XL_MIN_ROWS", 100_000))
+_TN_XL_MIN_ROWS = 100_000
 
 
 def _tn_xl(m: int, cout: int, cin: int) -> bool:

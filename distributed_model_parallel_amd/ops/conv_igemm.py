@@ -21,7 +21,6 @@ from __future__ import annotations
 
 import contextlib
 
-import os
 
 from typing import Optional, Tuple
 
@@ -39,7 +38,7 @@ ENABLED = not _native.disabled("igemm")
 # MIOpen: the generic implicit-GEMM backward (conv_nt transposed / conv_wgrad)
 # measured slower on every ResNet-50 shape (profiles/raw_r2/roofline_*.log).
 # set_generic_backward(True) routes them to it (any shape; tests).
-NATIVE_BWD = os.environ.get("DMP_GENERIC_BWD", "0") == "1"
+NATIVE_BWD = False  # set_generic_backward(True): A/B of the generic native backward
 
 
 def set_generic_backward(on: bool) -> None:
@@ -64,7 +63,7 @@ def _capturing() -> bool:
 # _XL_WGRAD_MAX_ROWS output pixels: l4 stride-2 at batch 256 0.133 vs
 # 0.138 ms, at batch 2048 0.908 vs 0.655 ms (profiles/raw_r4/wgrad_s2_r4o.md).
 _XL_WGRAD = not _native.disabled("xl_conv3")
-_XL_WGRAD_MAX_ROWS = int(os.environ.get("DMP_XL_WGRAD_MAX_ROWS", 50_000))
+_XL_WGRAD_MAX_ROWS = 50_000
 _STATS["xl_wgrad"] = 0
 
 

@@ -28,7 +28,7 @@ Mechanism (no change to the autograd graph):
 A parameter whose accumulator is not bound to S (a DataParallel replica, a
 model without :func:`bind`) keeps its weight gradient on the compute stream,
 and nothing is side-streamed inside a hipGraph capture.  Off by default
-(``DMP_ASYNC_WGRAD=1`` turns it on; see ENABLED).
+(``set_enabled(True)`` turns it on; see ENABLED).
 """
 from __future__ import annotations
 
@@ -45,9 +45,15 @@ from .. import _native
 # batch 2048 (ResNet-50 123.2 ms inline vs 123.8 side; 29 ms of kernels ran
 # "concurrently" while the compute queue's own kernels slowed by as much), and
 # the per-layer stream handshakes cost launch-bound models host time
-# (MobileNetV2 CIFAR 10.9 vs 12.8 ms).  DMP_ASYNC_WGRAD=1 enables it.
-import os as _os
-ENABLED = _os.environ.get("DMP_ASYNC_WGRAD", "0") == "1" and not _native.disabled("async_wgrad")
+# (MobileNetV2 CIFAR 10.9 vs 12.8 ms).  set_enabled(True) enables it.
+ENABLED = False
+
+
+def set_enabled(on: bool) -> None:
+    """Weight gradients on the side stream (off by default: finding 56/57).
+    Takes effect for models / DDP wrappers built afterwards."""
+    global ENABLED
+    ENABLED = bool(on) and not _native.disabled("async_wgrad")
 
 _streams: Dict[int, torch.cuda.Stream] = {}
 # id(param) -> weakref(param) of parameters whose AccumulateGrad lives on S

@@ -38,6 +38,9 @@ from typing import List, Optional, Sequence
 import torch
 import torch.nn as nn
 
+# one replay stream per replica (False: every replica on the current stream; A/B)
+PER_REPLICA_STREAMS = True
+
 from . import comm_ops
 
 
@@ -81,9 +84,8 @@ class GraphedReplicas:
         # one stream per replica: replicas sharing a device replay concurrently
         # (a 64-image ResNet-50 pass leaves most of an MI355X idle); autograd
         # runs each replica's backward graph on the stream its forward used
-        # (DMP_DP_GRAPH_STREAMS=0: replay everything on the current stream)
-        import os
-        if os.environ.get("DMP_DP_GRAPH_STREAMS", "1") == "1":
+        # (PER_REPLICA_STREAMS = False: replay everything on the current stream)
+        if PER_REPLICA_STREAMS:
             self.streams = [torch.cuda.Stream(device=d) for d in self.devices]
         else:
             self.streams = [torch.cuda.current_stream(d) for d in self.devices]

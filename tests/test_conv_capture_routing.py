@@ -18,7 +18,7 @@ def test_xl_wgrad_gate_by_rows_and_capture(monkeypatch):
 
 
 def test_generic_backward_env_default():
-    # the generic native backward is opt-in eagerly (DMP_GENERIC_BWD=1); a
+    # the generic native backward is opt-in eagerly (set_generic_backward); a
     # capture turns it on by itself
     assert conv_igemm.NATIVE_BWD in (False, True)
     assert callable(conv_igemm._capturing)

@@ -25,33 +25,6 @@ def test_gemm_tn(M, N, K, out):
     torch.testing.assert_close(got.float(), ref, atol=tol, rtol=1e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(802816, 256, 64), (200704, 512, 128), (1000, 256, 64), (777, 1024, 128),
-                                   (131, 256, 128)])
-def test_gemm_tn_tall_tiles(M, N, K):
-    """256-row TN tiles (set_tn_tall): the narrow operand read once per 256
-    columns of the wide one."""
-    C = _native.require("gemm_tn")
-    torch.manual_seed(0)
-    a = torch.randn(M, N, device=DEV).bfloat16()
-    b = torch.randn(M, K, device=DEV).bfloat16()
-    C.set_tn_tall(2)
-    try:
-        got = C.gemm_tn(a, b, torch.float32)
-    finally:
-        C.set_tn_tall(0)
-    ref = a.float().t() @ b.float()
-    torch.testing.assert_close(got, ref, atol=1e-3 * M ** 0.5, rtol=1e-2)
-    pat_a = (torch.arange(M * N, device=DEV).reshape(M, N) % 7 - 3).bfloat16()
-    pat_b = (torch.arange(M * K, device=DEV).reshape(M, K) % 5 - 2).bfloat16()
-    C.set_tn_tall(2)
-    try:
-        got = C.gemm_tn(pat_a, pat_b, torch.float32)
-    finally:
-        C.set_tn_tall(0)
-    if M <= 1000:  # exact small integers (sums stay exactly representable)
-        torch.testing.assert_close(got, pat_a.float().t() @ pat_b.float())
-
-
 def test_gemm_tn_asymmetric_pattern():
     """Exact small-integer data: any transpose/mapping slip changes the result."""
     C = _native.require("gemm_tn")
