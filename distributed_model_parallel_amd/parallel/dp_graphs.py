@@ -32,7 +32,6 @@ is (bench.py --graph captures the same ops).
 from __future__ import annotations
 
 import copy
-import gc
 from typing import List, Optional, Sequence
 
 import torch
@@ -42,6 +41,7 @@ import torch.nn as nn
 PER_REPLICA_STREAMS = True
 
 from . import comm_ops
+from ..utils.graphs import no_gc_during_capture
 
 
 def _static_copy(module: nn.Module, device: torch.device, share_buffers_with: Optional[nn.Module]) -> nn.Module:
@@ -94,21 +94,11 @@ class GraphedReplicas:
         # the capture's warm-up iterations run replica 0 for real: keep the
         # module's running statistics as they were (its buffers are shared)
         saved = [b.detach().clone() for b in self.buffers]
-        # no Python garbage collection inside the captures: a collection there
-        # runs tensor / event destructors of earlier eager steps (side-stream
-        # frees, event destroys) while the stream is capturing, which aborted
-        # the process once in the GPU suite (round 5).  Collect first instead.
-        gc.collect()
-        torch.cuda.synchronize()
-        gc_was = gc.isenabled()
-        gc.disable()
-        try:
+        # no Python garbage collection inside the captures (utils/graphs.py)
+        with no_gc_during_capture():
             for rep, x, d in zip(self.replicas, self.inputs, self.devices):
                 with torch.cuda.device(d):
                     self.graphed.append(torch.cuda.make_graphed_callables(rep, (x,)))
-        finally:
-            if gc_was:
-                gc.enable()
         with torch.no_grad():
             for b, v in zip(self.buffers, saved):
                 b.copy_(v)

@@ -50,6 +50,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..comm.rccl import Communicator
+from ..utils.graphs import no_gc_during_capture
 from ..utils.profiling import trace_range
 
 
@@ -299,6 +300,7 @@ class Pipeline:
         # forever: publish it so every rank exits non-zero (utils/debug.py)
         self.graphs = bool(graphs)
         self._graphs: Dict[int, "_StageGraphs"] = {}  # micro-batch size -> captured slots
+        self.recaptures = 0  # forced re-captures of existing stage graphs (moved storage)
         self._failure = None
         if fail_fast and self.world > 1:
             from ..utils.debug import FailureBroadcast
@@ -586,6 +588,18 @@ class Pipeline:
         depth = min(M, S - r)
         G = self._graphs.get(mb)
         if G is None or G.depth < depth or not G.valid():
+            if G is not None and G.depth >= depth:
+                # a re-capture forced by moved gradient / parameter / buffer
+                # storage: legitimate after a re-homing, a silent slowdown when
+                # it repeats (e.g. a torch optimizer's zero_grad(set_to_none=True)
+                # every step): count it, say so once
+                self.recaptures += 1
+                if self.recaptures == 2:
+                    import warnings
+                    warnings.warn("Pipeline(graphs=True): stage graphs re-captured again because parameter "
+                                  "gradients / parameters / buffers moved (set_to_none zero_grad?); every "
+                                  "re-capture costs two eager iterations plus the slot captures",
+                                  RuntimeWarning, stacklevel=2)
             G = self._graphs[mb] = _StageGraphs(self, mb, depth)
         G.stats.zero_()
         warm = min(S - r - 1, M)
@@ -727,6 +741,9 @@ class _StageGraphs:
                 p.grad = torch.zeros_like(p)  # accumulated in place by the captured backward
         self.grad_ptrs = [p.grad.data_ptr() for p in self.params]
         self.param_ptrs = [p.data_ptr() for p in self.params]  # an optimizer may re-home them (flat buffers)
+        # the captured forward updates the running statistics IN these buffers:
+        # load_state_dict(assign=True) / module.to() would leave them behind
+        self.buffer_keys = [(id(b), b.data_ptr()) for b in pipe.module.buffers()]
         self.stats = torch.zeros(3, dtype=torch.float64, device=dev)
         in_shape, out_shape = pipe._in_shape(mb), pipe._out_shape(mb)
         mk_in = lambda: torch.zeros(in_shape, dtype=pipe.dtype, device=dev)  # noqa: E731
@@ -810,19 +827,24 @@ class _StageGraphs:
         for x in self.inputs:
             x.grad = None
         torch.cuda.synchronize(pipe.device)
-        for k in range(self.depth):
-            pool = torch.cuda.graph_pool_handle()
-            gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gf, pool=pool, stream=s):
-                out = self._forward(k)
-            with torch.cuda.graph(gb, pool=pool, stream=s):
-                self._backward(k, out)
-            self.fwd.append(gf)
-            self.bwd.append(gb)
-            self.outs.append(out.detach() if not pipe.is_last else None)
+        # no Python garbage collection inside the captures (utils/graphs.py)
+        with no_gc_during_capture(pipe.device):
+            for k in range(self.depth):
+                pool = torch.cuda.graph_pool_handle()
+                gf, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gf, pool=pool, stream=s):
+                    out = self._forward(k)
+                with torch.cuda.graph(gb, pool=pool, stream=s):
+                    self._backward(k, out)
+                self.fwd.append(gf)
+                self.bwd.append(gb)
+                self.outs.append(out.detach() if not pipe.is_last else None)
         torch.cuda.synchronize(pipe.device)
 
     def valid(self) -> bool:
-        """The captured backward adds into the gradient storage seen at capture."""
-        return all(p.grad is not None and p.grad.data_ptr() == g and p.data_ptr() == d
-                   for p, g, d in zip(self.params, self.grad_ptrs, self.param_ptrs))
+        """The captured backward adds into the gradient storage seen at capture,
+        and the captured forward reads / updates the same parameter and buffer
+        tensors."""
+        return (all(p.grad is not None and p.grad.data_ptr() == g and p.data_ptr() == d
+                    for p, g, d in zip(self.params, self.grad_ptrs, self.param_ptrs))
+                and [(id(b), b.data_ptr()) for b in self.pipe.module.buffers()] == self.buffer_keys)

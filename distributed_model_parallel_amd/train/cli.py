@@ -260,7 +260,8 @@ def run_pipeline(args, env) -> None:
     pipe = Pipeline(model.as_sequential(), comm, (c, h, w), micro_batches=args.micro_batches,
                     schedule=args.schedule, dtype=parse_dtype(args.dtype),
                     channels_last=args.channels_last, partition=args.partition,
-                    graphs=env.device.type == "cuda" and not args.no_pipe_graphs)
+                    # one GPU only (see train/step.py): multi-rank GPU pipelines run eagerly
+                    graphs=env.device.type == "cuda" and not args.no_pipe_graphs and comm.size == 1)
     opt = MasterSGD(pipe.module.parameters(), lr=args.lr, momentum=args.momentum,
                     weight_decay=args.weight_decay)
     sched = build_schedule(opt, args.epochs, args.warmup_epochs, _lr_steps(args), args.lr_gamma)

@@ -192,7 +192,11 @@ def build_pipeline_state(cfg: StepConfig, device: torch.device) -> TrainState:
                     schedule=cfg.schedule, device=device, dtype=cfg.dtype,
                     channels_last=cfg.channels_last, partition=cfg.partition,
                     static_batch=cfg.batch_size,  # every rank knows it: no per-step size message
-                    graphs=cfg.pipe_graphs and device.type == "cuda")
+                    # captured stage slots on one GPU only: the multi-stage slot
+                    # schedule is verified on the CPU stand-ins (tests/test_pipeline.py)
+                    # but never with RCCL between captured stages (a 1-GPU box cannot
+                    # host two RCCL ranks), so multi-rank GPU pipelines run eagerly
+                    graphs=cfg.pipe_graphs and device.type == "cuda" and comm.size == 1)
     opt = MasterSGD(pipe.module.parameters(), lr=cfg.lr, momentum=cfg.momentum,
                     weight_decay=cfg.weight_decay)
     x, y = synthetic_batch(cfg, device) if pipe.is_first else (None, None)

@@ -322,3 +322,18 @@ def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
     assert abs(early_n / early_r - 1.0) <= 0.05, (early_n, early_r)
     assert _mean(l_nat) <= 1.4 * _mean(l_ref), (_mean(l_nat), _mean(l_ref))
     assert a < 0.6 * l0, (l0, a)
+    # the descent itself is still checked, at bands wide enough for its chaos
+    # (ADVICE r5): every 10-step window of steps 30-80 within 2x of stock, and
+    # the native run reaching 90 % of the start loss (10-step running mean) no
+    # later than 2 x stock's step + 15
+    for w0 in range(30, min(80, len(l_nat), len(l_ref)) - 9, 10):
+        wn, wr = _mean(l_nat[w0:w0 + 10]), _mean(l_ref[w0:w0 + 10])
+        assert 0.5 <= wn / wr <= 2.0, (w0, wn, wr)
+
+    def first_below(ls, frac):
+        for i in range(len(ls) - 9):
+            if _mean(ls[i:i + 10]) < frac * l0:
+                return i
+        return len(ls)
+    sn, sr = first_below(l_nat, 0.9), first_below(l_ref, 0.9)
+    assert sn <= 2 * sr + 15, (sn, sr)

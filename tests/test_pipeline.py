@@ -262,3 +262,28 @@ def test_pipeline_graphed_slot_schedule_matches_sequential(world, micro):
         for i, gs in out["grads"].items():
             for g, rg in zip(gs, ref_grads[i]):
                 torch.testing.assert_close(g, rg, atol=1e-6, rtol=1e-5)
+
+
+def _recapture_worker(rank, world):
+    import warnings
+    from distributed_model_parallel_amd.comm.rccl import Communicator
+    from distributed_model_parallel_amd.parallel.pipeline import Pipeline
+    atoms = _mlp_atoms()
+    comm = Communicator(torch.device("cpu"))
+    pipe = Pipeline(atoms, comm, (3, 4, 4), micro_batches=4, schedule="1f1b", graphs=True, static_batch=12)
+    x, y = _data("mlp", 12)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        for step in range(4):
+            for p in atoms.parameters():
+                p.grad = None  # a stock optimizer's zero_grad(set_to_none=True): storage moves
+            pipe.train_step(x if rank == 0 else None, y if rank == 0 else None)
+    return {"recaptures": pipe.recaptures,
+            "warned": sum("re-captured again" in str(w.message) for w in caught)}
+
+
+def test_pipeline_graph_recaptures_are_counted_and_warned():
+    """a re-capture forced by moved gradient storage must not be
+    silent -- counted on the pipeline and warned about once it repeats."""
+    for r in run_world(_recapture_worker, 2):
+        assert r["recaptures"] == 3 and r["warned"] == 1, r
