@@ -1583,6 +1583,178 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
     }
 }
 
+// ---- 4-wave weight-gradient kernel (the TN form of gemm_xl_w4_kernel;
+// profiles/README.md finding 70).  Same output tile, M split and fp32
+// partials as gemm_tn_pp_kernel, but: one wave per SIMD computing 128 (n) x
+// 128 (k) outputs in 256 AGPRs (inline-asm MFMAs, w4_mfma); LDS-DMA pieces of
+// 8 m-rows x 128 B (full cache lines; the ping-pong kernel's 16 x 64 B pieces
+// half-use 16 lines each) into [64 m][64 cols] planes whose 16-B chunk c of
+// row r sits at c ^ tnw_swz(r) (conflict-free ds_read_b64_tr_b16: the 8 rows a
+// half-wave reads -- 4 rows of each of two 16-lane groups, 8 apart -- land on
+// all 64 banks); one barrier per 64-deep K tile:
+//   S1: the k32-half-0 MFMAs, reading half 1's fragments of tile t;
+//       vmcnt(0) + barrier (tile t + 1 landed, buffer t & 1 free);
+//   S2: the half-1 MFMAs, copying tile t + 2 into buffer t & 1 (one copy per
+//       4 MFMAs) and reading half 0 of tile t + 1.
+// SRC: 0 = plain B rows, 2 = the implicit-GEMM tap gather of an NHWC input
+// (not instantiated: 1.5 KB of scratch, see run_tn_pp).
+__device__ __forceinline__ int tnw_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
+
+template <int SRC>
+__global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
+  constexpr int PLANE = 64 * 128, OPER = 4 * PLANE, BUF = 2 * OPER;  // bytes
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  using v4i16 = short __attribute__((ext_vector_type(4)));
+  using lds_v4 = __attribute__((address_space(3))) v4i16;
+  const int M = p.M, N = p.N, K = p.K;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntiles = (N + 255) >> 8, ktiles = (K + 255) >> 8;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = bid % (ntiles * ktiles), split = bid / (ntiles * ktiles);
+  const int n0 = (tile / ktiles) * 256, k0 = (tile % ktiles) * 256;
+  const int64_t mb = (int64_t)split * p.rps;
+  const int64_t me = min((int64_t)M, mb + p.rps);
+  const int KT = (int)((me - mb + 63) >> 6);
+  static_assert(SRC == 0, "the tap gather runs on gemm_tn_pp_kernel");
+
+  // copy c (0..15) of a K tile: operand c >> 3 (A = dy n columns, B = k
+  // columns), plane `wave`, row group c & 7; lane L: row 8 (c & 7) + (L >> 3),
+  // stored chunk L & 7, logical chunk (L & 7) ^ tnw_swz(row)
+  const int prow = lane >> 3;
+  const int lcol = wave * 64 + (((lane & 7) ^ tnw_swz(prow)) << 3);  // row & 15 = 8 (c & 1) + prow: bit 3 from c
+  const int lcol8 = wave * 64 + (((lane & 7) ^ tnw_swz(8 + prow)) << 3);
+  // buffer form (the global_load_lds form made the compiler drain every copy
+  // before each k step's first ds_read): descriptors over THIS split's rows,
+  // so a copy of a row past the split's end is out of range and lands as
+  // zeros; columns past N / K read neighbouring bytes into outputs that are
+  // never stored
+  // The copies are inline asm: as compiler-visible LDS writes (either
+  // builtin) they made it wait vmcnt(0) -- every copy in flight -- before
+  // each transposing fragment read it cannot prove disjoint from them.  The
+  // waits that order them (vmcnt, then the barrier) are explicit anyway.
+  using i32x4 = int __attribute__((ext_vector_type(4)));
+  const int64_t nrow = me - mb;
+  auto desc = [&](const bf16* base, int64_t bytes) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base);
+    i32x4 d;
+    d[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+    d[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));  // stride 0
+    d[2] = __builtin_amdgcn_readfirstlane((int)min(bytes, (int64_t)0x7fffffff));
+    d[3] = 0x00020000;
+    return d;
+  };
+  const i32x4 rsa = desc(p.A + mb * p.lda, nrow * p.lda * 2), rsb = desc(p.B + mb * p.ldb, nrow * p.ldb * 2);
+  const uint32_t oa0 = (uint32_t)((prow * p.lda + n0 + lcol) * 2), oa8 = (uint32_t)((prow * p.lda + n0 + lcol8) * 2);
+  const uint32_t ob0 = (uint32_t)((prow * p.ldb + k0 + lcol) * 2), ob8 = (uint32_t)((prow * p.ldb + k0 + lcol8) * 2);
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+  auto dma = [&](int kt, int buf, int c) {
+    const int rg = c & 7;
+    const bool odd = rg & 1;  // row bit 3
+    const int ldst = __builtin_amdgcn_readfirstlane((int)(lds0 + buf * BUF + (c >> 3) * OPER + wave * PLANE + rg * 1024));
+    const uint32_t voff = c < 8 ? (odd ? oa8 : oa0) + (uint32_t)(8 * rg * p.lda * 2)
+                                : (odd ? ob8 : ob0) + (uint32_t)(8 * rg * p.ldb * 2);
+    const int soff = __builtin_amdgcn_readfirstlane((int)(kt * 64 * (c < 8 ? p.lda : p.ldb) * 2));
+    unsigned keep;
+    if (c < 8)
+      asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                   "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "s"(ldst), "v"(voff), "s"(rsa), "s"(soff) : "memory");
+    else
+      asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                   "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "s"(ldst), "v"(voff), "s"(rsb), "s"(soff) : "memory");
+  };
+
+  // tr-read lane roles (as gemm_tn_pp_kernel): group g = lane >> 4 covers m
+  // rows 8g..8g+7 of a k32 step; lane 4q+p of the group reads row q (+4 for
+  // the high half), cols 4p..4p+3 of the fragment's 16 columns
+  const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+  auto tr_frag = [&](const char* plane, int h, int cin) {  // cin: column within the 64-col plane, % 16 == 0
+    const int r0 = h * 32 + 8 * g + q4, r1 = r0 + 4;
+    const int cb = (cin + 4 * p4) * 2;  // byte within the row
+    const char* a0 = plane + r0 * 128 + ((((cb >> 4) ^ tnw_swz(r0))) << 4) + (cb & 15);
+    const char* a1 = plane + r1 * 128 + ((((cb >> 4) ^ tnw_swz(r1))) << 4) + (cb & 15);
+    v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a0);
+    v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a1);
+    short __attribute__((ext_vector_type(8))) t8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, t8);
+  };
+  bf16x8 ra[2][8], rb[2][8];
+  // fragment read r (0..15) of k32 half H: A block (n) r == 0 ? 0 : r - 8, B blocks (k) 0..7 for r = 1..8
+  auto rd = [&](auto hc, int buf, int r) {
+    constexpr int H = decltype(hc)::value;
+    const bool isb = r >= 1 && r <= 8;
+    const int blk = r == 0 ? 0 : (isb ? r - 1 : r - 8);
+    const int col = (isb ? wc : wr) * 128 + blk * 16;  // within the 256-col operand tile
+    const char* plane = smem + buf * BUF + (isb ? OPER : 0) + (col >> 6) * PLANE;
+    if (isb) rb[H][blk] = tr_frag(plane, H, col & 63);
+    else ra[H][blk] = tr_frag(plane, H, col & 63);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // operands swapped: acc[i][j] holds the transposed 16 x 16 block: lane =
+  // output row n (i), registers = 4 consecutive output columns k (j)
+  auto iter = [&](auto st, auto rdn, int kt) {
+    constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
+    const int buf = kt & 1;
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
+      if ((n & 3) == 0) rd(I1{}, buf, n >> 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 0; n < 64; ++n) {
+      w4_mfma(acc[n >> 3][n & 7], rb[1][n & 7], ra[1][n >> 3]);
+      if constexpr (STAGE)
+        if ((n & 3) == 0) dma(kt + 2, buf, n >> 2);
+      if constexpr (READ)
+        if ((n & 1) == 1 && n < 32) rd(I0{}, buf ^ 1, n >> 1);
+    }
+  };
+  if (KT > 0) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dma(0, 0, c);
+    if (KT > 1) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) dma(1, 1, c);
+      vmcnt<16>();
+    } else {
+      vmcnt<0>();
+    }
+    barrier();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rd(I0{}, 0, r);
+    int kt = 0;
+    for (; kt + 2 < KT; ++kt) iter(std::true_type{}, std::true_type{}, kt);
+    if (kt + 1 < KT) iter(std::false_type{}, std::true_type{}, kt++);
+    iter(std::false_type{}, std::false_type{}, kt);
+    w4_drain();
+  }
+  // fp32 partials: lane = row n, 16-B pieces of 4 consecutive k
+  float* out = p.part + (int64_t)split * N * K;
+  const int lrow = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = n0 + wr * 128 + i * 16 + lrow;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + wc * 128 + j * 16 + lk * 4;
+      if (n < N && k < K) *reinterpret_cast<f32x4*>(out + (int64_t)n * K + k) = acc[i][j];
+    }
+  }
+}
+
 int g_num_cus = 0;
 
 // main loop of the 256 x 256 tiles: 11 = the 4-wave kernel (default), 10 =
@@ -2151,7 +2323,13 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
   a.part = part.data_ptr<float>();
   hipStream_t s = at::hip::getCurrentHIPStream();
-  hipLaunchKernelGGL(gemm_tn_pp_kernel, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
+  // plain weight gradients on the 4-wave kernel (finding 70; DMP_XL_PIPE=10:
+  // the ping-pong one).  The tap gather stays on the ping-pong kernel: its
+  // per-copy pixel division pushed the 4-wave form to 1.5 KB of scratch.
+  if (g_xl_pipe == 11 && a.cv.cin == 0)
+    hipLaunchKernelGGL(gemm_tn_w4_kernel<0>, dim3(tiles * splits), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(gemm_tn_pp_kernel, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   DMP_HIP_CHECK(hipGetLastError());
   split_reduce_launch(a.part, splits, (int64_t)N * K, out, s);
   return out;

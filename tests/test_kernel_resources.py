@@ -21,7 +21,7 @@ sys.path.insert(0, ROOT)
 def test_w4_gemm_kernels_never_spill():
     from tools.kernel_resources import resources
     ks = [k for k in resources(os.path.join(ROOT, "csrc", "gemm", "gemm_xl.hip"))
-          if k["name"].startswith("gemm_xl_w4_kernel")]
+          if k["name"].startswith(("gemm_xl_w4_kernel", "gemm_tn_w4_kernel"))]
     assert len(ks) >= 20, [k["name"] for k in ks]
     bad = [(k["name"], k["scratch"]) for k in ks if k["scratch"] != "0"]
     assert not bad, f"4-wave GEMM instantiations with scratch (accumulator spills behind asm MFMAs): {bad}"

@@ -65,6 +65,8 @@ def ab(name, flops, arms, rounds, iters, exact=None):
     torch.cuda.synchronize()
     ref = next(iter(outs.values()))
     same = {k: (bool(torch.equal(v, ref)) if exact is None or k in exact else True) for k, v in outs.items()}
+    rel = {k: float((v.float() - ref.float()).abs().max() / ref.float().abs().max().clamp_min(1e-30))
+           for k, v in outs.items()}
     del outs
     times = {k: [] for k in arms}
     for _ in range(rounds):
@@ -75,7 +77,7 @@ def ab(name, flops, arms, rounds, iters, exact=None):
     for k, ts in times.items():
         med = statistics.median(ts)
         parts.append(f"{k} {med:.3f} ms (min {min(ts):.3f}) {flops / med / 1e9:.0f} TF/s"
-                     f"{'' if same[k] else ' MISMATCH'}")
+                     f"{'' if same[k] else ' MISMATCH'}{f' rel {rel[k]:.1e}' if rel[k] else ''}")
     print(f"{name}: " + " | ".join(parts), flush=True)
 
 
@@ -157,7 +159,15 @@ def main():
                 continue
             dy = torch.rand(M, N, device="cuda", dtype=torch.bfloat16) * 2 - 1
             xx = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
-            ab(name, 2.0 * M * N * K, {"tn": lambda: C.gemm_tn_xl(dy, xx, torch.float32)}, a.rounds, a.iters)
+            def tarm(pipe):
+                def f():
+                    C.set_gemm_xl_bn(0, pipe, 0)
+                    return C.gemm_tn_xl(dy, xx, torch.float32)
+                return f
+            arms = {f"tn_pipe{p}": tarm(p) for p in pipes}
+            if a.lib:
+                arms["hipblaslt"] = lambda: dy.t().mm(xx)
+            ab(name, 2.0 * M * N * K, arms, a.rounds, a.iters, exact=set())
             del dy, xx
             torch.cuda.empty_cache()
     finally:
