@@ -203,17 +203,19 @@ _TN_XL = not _native.disabled("tn_xl")
 _STATS["tn_xl"] = 0
 
 
-_TN_XL_MIN_ROWS = 100_000
+_TN_XL_MIN_ROWS = 16_384
 
 
 def _tn_xl(m: int, cout: int, cin: int) -> bool:
-    """Ping-pong TN weight gradient for 1x1 convs with both output dims >= 256
-    from 100k rows: batch 2048 layer 3 0.31-0.56 vs 0.37-0.65 ms and layer 4
-    (100352 rows) 0.29-0.55 vs 0.35-0.60 ms; at batch 256 (50k rows and less)
-    the split-M 4-wave kernel wins 1.07-1.14x; hipBLASLt is 1.5-8x slower on
-    every shape (profiles/raw_r4/tn_wgrad_r4t.md).  (The 224-px convergence
-    test lowers the row threshold so its batch-64 run trains this route.)"""
-    return _TN_XL and cout >= 256 and cin >= 256 and m >= _TN_XL_MIN_ROWS
+    """1x1 weight gradients on gemm_tn_xl, whose default main loop is the
+    4-wave kernel (gemm_tn_w4, finding 70): at batch 2048 it beats the split-M
+    gemm_tn on every ResNet-50 shape, 1.15x on the 64-wide layer-1 ones
+    (0.78 vs 0.89 ms) to 1.9x on layer 4 (0.19 vs 0.36 ms), and hipBLASLt by
+    2-5x (tools/pipe_bench.py --only wgrad).  Until round 5 (8-wave ping-pong
+    loop) only >= 256-wide shapes from 100k rows took it.  (The 224-px
+    convergence test lowers the row threshold so its batch-64 run trains this
+    route.)"""
+    return _TN_XL and cout >= 64 and cin >= 64 and m >= _TN_XL_MIN_ROWS
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,

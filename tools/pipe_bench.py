@@ -41,12 +41,17 @@ CONV_SHAPES = [  # name, N, C, H (= W), Cout: 3x3 / stride 1 / pad 1 at ResNet-5
     ("r50_l4_3x3", 2048, 512, 7, 512),
     ("r50_l2_3x3", 2048, 128, 28, 128),
 ]
-TN_SHAPES = [  # name, M (reduction), N, K
+TN_SHAPES = [  # name, M (reduction), N, K  (ResNet-50 at batch 2048: dW[Cout, Cin] = dy^T x)
     ("vit_fc1_wgrad", 50432, 3072, 768),
     ("vit_qkv_wgrad", 50432, 2304, 768),
     ("r50_l3_wgrad", 401408, 1024, 256),
     ("r50_l2_wgrad", 1605632, 512, 128),
     ("r50_l4_wgrad", 100352, 2048, 512),
+    ("r50_l1c1_wgrad", 6422528, 64, 256),
+    ("r50_l1c3_wgrad", 6422528, 256, 64),
+    ("r50_l2c1_wgrad", 1605632, 128, 512),
+    ("r50_l3c1_wgrad", 401408, 256, 1024),
+    ("r50_l4c1_wgrad", 100352, 512, 2048),
 ]
 
 
@@ -165,6 +170,7 @@ def main():
                     return C.gemm_tn_xl(dy, xx, torch.float32)
                 return f
             arms = {f"tn_pipe{p}": tarm(p) for p in pipes}
+            arms["tn_splitm"] = lambda: C.gemm_tn(dy, xx, torch.float32)
             if a.lib:
                 arms["hipblaslt"] = lambda: dy.t().mm(xx)
             ab(name, 2.0 * M * N * K, arms, a.rounds, a.iters, exact=set())
