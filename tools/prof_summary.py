@@ -18,7 +18,8 @@ CATS = [
     ("dmp BN fold coefficients (ours)", ("fold_fwd", "fold_bwd", "fold_coef")),
     ("dmp fused SGD (ours)", ("sgd_flat",)),
     ("dmp coalesced copy/reduce (ours)", ("multi_copy", "reduce_add", "gather_slabs")),
-    ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "gemm_x2", "split_reduce", "dw_fwd",
+    ("dmp GEMM/conv (ours)", ("gemm_nt_kernel", "gemm_tn_kernel", "gemm_xl", "gemm_x2", "gemm_tn_w4", "gemm_tn_pp",
+                              "split_reduce", "dw_fwd",
                               "dw_dgrad", "dw_wgrad", "column_reduce", "conv3x3_c64", "conv3x3_c128", "gemm_tn_pp",
                               "wgrad3x3", "wgrad_reduce", "stem_fwd", "stem_wgrad", "partial_sum_kernel",
                               "s2d_kernel")),
