@@ -42,7 +42,9 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                                           const c10::optional<at::Tensor>& weight,
                                           const at::Tensor& mean, const at::Tensor& invstd,
                                           bool training, bool relu, bool want_dres, int64_t C,
-                                          const c10::optional<at::Tensor>& bias, double clip);
+                                          const c10::optional<at::Tensor>& bias, double clip,
+                                          const c10::optional<at::Tensor>& acc_weight,
+                                          const c10::optional<at::Tensor>& acc_bias);
 // fused_sgd.hip
 void sgd_flat_step(const c10::optional<at::Tensor>& master, const at::Tensor& mom,
                    const at::Tensor& grad, const at::Tensor& param, double lr, double wd,
@@ -73,12 +75,14 @@ std::vector<at::Tensor> gemm_nt_bnbwd(const at::Tensor& A, const at::Tensor& B,
                                       const std::vector<int64_t>& a2_map);
 // cross_entropy.hip
 std::vector<at::Tensor> cross_entropy_fwd(const at::Tensor& x, const at::Tensor& target,
-                                          int64_t ignore_index);
+                                          int64_t ignore_index, double scale,
+                                          const c10::optional<at::Tensor>& acc);
 at::Tensor cross_entropy_bwd(const at::Tensor& grad, const at::Tensor& x, const at::Tensor& target,
                              const at::Tensor& lse, const at::Tensor& stats, int64_t ignore_index);
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
-                   const c10::optional<at::Tensor>& pro_shift, bool a_mapped);
+                   const c10::optional<at::Tensor>& pro_shift, bool a_mapped,
+                   const c10::optional<at::Tensor>& out);
 // stem.hip
 at::Tensor space_to_depth2(const at::Tensor& x, int64_t pad, int64_t out_channels);
 at::Tensor pad_channels16(const at::Tensor& x, int64_t pad, int64_t extra_w);
@@ -102,7 +106,7 @@ void set_phase_dgrad(bool on);
 void set_tn_wide(bool on);
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
-                      at::ScalarType out_dtype, int64_t kc);
+                      at::ScalarType out_dtype, int64_t kc, const c10::optional<at::Tensor>& out);
 // gemm_xl.hip
 at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
                    const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& aux,
@@ -121,7 +125,8 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
                                 const c10::optional<at::Tensor>& invstd, const c10::optional<at::Tensor>& weight,
                                 const c10::optional<at::Tensor>& bias);
 std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tensor& B, const at::Tensor& aux);
-at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype);
+at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
+                      const c10::optional<at::Tensor>& out);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat, bool moments);
@@ -142,7 +147,8 @@ bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
-                         int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype);
+                         int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype,
+                         const c10::optional<at::Tensor>& out);
 std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, const std::string& mode,
                                      const c10::optional<at::Tensor>& residual,
                                      const c10::optional<at::Tensor>& bn_x,
@@ -185,7 +191,7 @@ std::vector<at::Tensor> dwconv3x3_forward(const at::Tensor& x, const at::Tensor&
 at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t stride, int64_t H,
                            int64_t W);
 at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride,
-                           at::ScalarType out_dtype);
+                           at::ScalarType out_dtype, const c10::optional<at::Tensor>& out);
 // bias_act.hip
 bool colsum_supported(int64_t N);
 at::Tensor bias_grad(const at::Tensor& dy, at::ScalarType out_dtype);
@@ -241,7 +247,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_backward_apply", &dmp::bn_backward_apply, py::arg("dy"), py::arg("x"), py::arg("y"),
         py::arg("sums"), py::arg("count"), py::arg("weight"), py::arg("mean"), py::arg("invstd"),
         py::arg("training"), py::arg("relu"), py::arg("want_dres"), py::arg("C"),
-        py::arg("bias") = py::none(), py::arg("clip") = INFINITY,
+        py::arg("bias") = py::none(), py::arg("clip") = INFINITY, py::arg("acc_weight") = py::none(),
+        py::arg("acc_bias") = py::none(),
         py::call_guard<py::gil_scoped_release>());
 
   // ---- MFMA GEMM (1x1 conv) with fused BN prologue/epilogues ----
@@ -254,7 +261,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::call_guard<py::gil_scoped_release>());
 
   m.def("cross_entropy_fwd", &dmp::cross_entropy_fwd, py::arg("x"), py::arg("target"),
-        py::arg("ignore_index") = -100,
+        py::arg("ignore_index") = -100, py::arg("scale") = 1.0, py::arg("acc") = py::none(),
+        "scale * mean softmax cross-entropy; acc (fp64 [3]) += (loss, top-1 correct, top-5 correct)",
         py::call_guard<py::gil_scoped_release>());
   m.def("cross_entropy_bwd", &dmp::cross_entropy_bwd, py::arg("grad"), py::arg("x"), py::arg("target"),
         py::arg("lse"), py::arg("stats"), py::arg("ignore_index") = -100,
@@ -267,8 +275,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   m.def("gemm_tn", &dmp::gemm_tn, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
         py::arg("b_map") = std::vector<int64_t>{}, py::arg("pro_scale") = py::none(),
-        py::arg("pro_shift") = py::none(), py::arg("a_mapped") = false,
-        "C = A^T B (weight gradient); b_map reads B's rows through a strided map, a_mapped A's too (Gram of a sample)",
+        py::arg("pro_shift") = py::none(), py::arg("a_mapped") = false, py::arg("out") = py::none(),
+        "C = A^T B (weight gradient); b_map reads B's rows through a strided map, a_mapped A's too (Gram of a "
+        "sample); out: add into this gradient instead of returning a new tensor",
         py::call_guard<py::gil_scoped_release>());
 
   m.def("set_tn_wide", &dmp::set_tn_wide, py::arg("on"),
@@ -289,7 +298,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::call_guard<py::gil_scoped_release>());
   m.def("conv_wgrad", &dmp::conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
-        py::arg("kc") = 0,
+        py::arg("kc") = 0, py::arg("out") = py::none(),
         py::call_guard<py::gil_scoped_release>());
   m.def("maxpool2d_bn_forward", &dmp::maxpool2d_bn_forward, py::arg("x"), py::arg("scale"),
         py::arg("shift"), py::arg("k"), py::arg("s"), py::arg("p"),
@@ -355,11 +364,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
         "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
-  m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"),
+  m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"), py::arg("out") = py::none(),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M",
         py::call_guard<py::gil_scoped_release>());
   m.def("conv_wgrad_xl", &dmp::conv_wgrad_xl, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
+        py::arg("out") = py::none(),
         "kh x kw conv weight gradient (tap gather) on the ping-pong TN kernel; Cin % 256 == 0",
         py::call_guard<py::gil_scoped_release>());
   m.def("gemm_xl_dgelu_bgrad", &dmp::gemm_xl_dgelu_bgrad, py::arg("A"), py::arg("B"), py::arg("aux"),
@@ -456,7 +466,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::call_guard<py::gil_scoped_release>());
   m.def("dwconv3x3_dgrad", &dmp::dwconv3x3_dgrad,
         py::call_guard<py::gil_scoped_release>());
-  m.def("dwconv3x3_wgrad", &dmp::dwconv3x3_wgrad,
+  m.def("dwconv3x3_wgrad", &dmp::dwconv3x3_wgrad, py::arg("dy"), py::arg("x"), py::arg("stride"),
+        py::arg("out_dtype"), py::arg("out") = py::none(),
         py::call_guard<py::gil_scoped_release>());
 
   // ---- optimizer ----

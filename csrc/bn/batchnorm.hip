@@ -447,7 +447,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
     const float* __restrict__ weight, const float* __restrict__ bias, const float* __restrict__ mean,
     const float* __restrict__ invstd, int training, int64_t M, int C, int64_t rows_per_block,
     T* __restrict__ dx, T* __restrict__ dres, float* __restrict__ dweight,
-    float* __restrict__ dbias, float clip) {
+    float* __restrict__ dbias, float clip, int acc) {
   constexpr int VEC = Vec16<T>::N;
   const Layout L = make_layout(C, VEC);
   const int tid = threadIdx.x;
@@ -497,8 +497,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_apply_kernel(
       c[i] = 0.f;
     }
     if (blockIdx.x == 0 && lr == 0) {
-      if (dweight) dweight[ch] = (float)(sdzx * is);
-      if (dbias) dbias[ch] = (float)sdz;
+      if (dweight) dweight[ch] = (float)(sdzx * is) + (acc ? dweight[ch] : 0.f);
+      if (dbias) dbias[ch] = (float)sdz + (acc ? dbias[ch] : 0.f);
     }
   }
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
@@ -788,12 +788,25 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                                           const c10::optional<at::Tensor>& weight,
                                           const at::Tensor& mean, const at::Tensor& invstd,
                                           bool training, bool relu, bool want_dres, int64_t C,
-                                          const c10::optional<at::Tensor>& bias, double clip) {
+                                          const c10::optional<at::Tensor>& bias, double clip,
+                                          const c10::optional<at::Tensor>& acc_weight,
+                                          const c10::optional<at::Tensor>& acc_bias) {
   TORCH_CHECK(count.scalar_type() == at::kDouble && count.numel() >= 1, "count must be fp64");
   check_input(dy, C, "grad");
   const int64_t M = x.numel() / C;
   auto stream = at::hip::getCurrentHIPStream();
-  auto dwb = at::empty({2, C}, x.options().dtype(at::kFloat));
+  // acc_weight / acc_bias (fp32 [C] gradients, both or neither): the affine
+  // gradients are ADDED into them (micro-batch accumulation, ops/grad_accum.py)
+  const bool acc = acc_weight.has_value() && acc_weight->defined();
+  TORCH_CHECK(acc == (acc_bias.has_value() && acc_bias->defined()), "bn_backward_apply: acc_weight and acc_bias together");
+  if (acc)
+    TORCH_CHECK(acc_weight->scalar_type() == at::kFloat && acc_bias->scalar_type() == at::kFloat &&
+                    acc_weight->is_contiguous() && acc_bias->is_contiguous() && acc_weight->numel() == C &&
+                    acc_bias->numel() == C,
+                "bn_backward_apply: accumulation targets must be contiguous fp32 [C]");
+  auto dwb = acc ? at::Tensor() : at::empty({2, C}, x.options().dtype(at::kFloat));
+  float* dwp = acc ? acc_weight->data_ptr<float>() : dwb.data_ptr<float>();
+  float* dbp = acc ? acc_bias->data_ptr<float>() : dwb.data_ptr<float>() + C;
   auto dx = at::empty_like(x);
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x);
@@ -811,7 +824,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
                      ptr<T>(dy), ptr<T>(x), yp, sums.data_ptr<double>(), count.data_ptr<double>(), \
                      fptr(weight), fptr(bias), mean.data_ptr<float>(), invstd.data_ptr<float>(),  \
                      (int)training, M, (int)C, g.rows_per_block, ptr<T>(dx), dr,                  \
-                     dwb.data_ptr<float>(), dwb.data_ptr<float>() + C, (float)clip)
+                     dwp, dbp, (float)clip, (int)acc)
       const int mode = !relu ? 0 : (from_y ? 1 : 2);
       if (mode == 1 && want_dres) DMP_BN_BWD(1, true);
       else if (mode == 1) DMP_BN_BWD(1, false);
@@ -823,6 +836,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
 #undef DMP_BN_BWD1
     });
   }
+  if (acc) return {dx, at::Tensor(), at::Tensor(), dres};
   return {dx, dwb[0], dwb[1], dres};
 }
 

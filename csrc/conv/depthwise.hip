@@ -353,7 +353,7 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(const T* __restrict_
 // out[c] = sum_b part[b][c]  (fp64 accumulation, 32 row-groups x 32 columns per block)
 template <typename OT>
 __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __restrict__ part, int rb,
-                                                             int ncol, int C, OT* __restrict__ out) {
+                                                             int ncol, int C, OT* __restrict__ out, int acc) {
   const int cl = threadIdx.x % 32, g = threadIdx.x / 32;
   const int c = blockIdx.x * 32 + cl;
   double a = 0.0;
@@ -366,7 +366,10 @@ __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __rest
     if (g < s) l[threadIdx.x] += l[threadIdx.x + s * 32];
     __syncthreads();
   }
-  if (g == 0 && c < ncol) out[(c % C) * 9 + c / C] = (OT)l[threadIdx.x];  // [C][9] = [C,1,3,3]
+  if (g == 0 && c < ncol) {  // [C][9] = [C,1,3,3]; acc: add into the existing gradient
+    OT* o = out + (c % C) * 9 + c / C;
+    *o = (OT)(acc ? l[threadIdx.x] + (double)(float)*o : l[threadIdx.x]);
+  }
 }
 
 Geo make_geo(const at::Tensor& x4, int stride, int VEC) {
@@ -494,8 +497,11 @@ at::Tensor dwconv3x3_dgrad(const at::Tensor& dy, const at::Tensor& w, int64_t st
 }
 
 // Weight gradient: returns [C,1,3,3] in `out_dtype`.
+at::Tensor acc_target(const c10::optional<at::Tensor>& out, int64_t numel, at::ScalarType dtype,
+                      const char* who);
+
 at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t stride,
-                           at::ScalarType out_dtype) {
+                           at::ScalarType out_dtype, const c10::optional<at::Tensor>& acc_out) {
   check_nhwc(dy, "dy");
   check_nhwc(x, "x");
   const int VEC = x.scalar_type() == at::kBFloat16 ? 8 : 4;
@@ -518,14 +524,17 @@ at::Tensor dwconv3x3_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t st
   });
   // reduced straight into [C,1,3,3] in the parameter dtype (no transpose / cast launches)
   TORCH_CHECK(out_dtype == at::kBFloat16 || out_dtype == at::kFloat, "weight gradient must be bf16 or fp32");
-  auto out = at::empty({(int64_t)g.C, 1, 3, 3}, x.options().dtype(out_dtype));
+  at::Tensor acc = acc_target(acc_out, 9 * (int64_t)g.C, out_dtype, "dwconv3x3_wgrad");
+  TORCH_CHECK(!acc.defined() || acc.is_contiguous(), "dwconv3x3_wgrad: the accumulation target must be [C,1,3,3] contiguous");
+  auto out = acc.defined() ? acc : at::empty({(int64_t)g.C, 1, 3, 3}, x.options().dtype(out_dtype));
   const int ncol = 9 * g.C;
   if (out_dtype == at::kBFloat16)
     hipLaunchKernelGGL((column_reduce_kernel<__bf16>), dim3((ncol + 31) / 32), dim3(1024), 0, stream,
-                       part.data_ptr<float>(), (int)grid.x, ncol, g.C, reinterpret_cast<__bf16*>(out.data_ptr()));
+                       part.data_ptr<float>(), (int)grid.x, ncol, g.C, reinterpret_cast<__bf16*>(out.data_ptr()),
+                       (int)acc.defined());
   else
     hipLaunchKernelGGL((column_reduce_kernel<float>), dim3((ncol + 31) / 32), dim3(1024), 0, stream,
-                       part.data_ptr<float>(), (int)grid.x, ncol, g.C, out.data_ptr<float>());
+                       part.data_ptr<float>(), (int)grid.x, ncol, g.C, out.data_ptr<float>(), (int)acc.defined());
   return out;
 }
 

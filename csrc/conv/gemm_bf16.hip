@@ -814,7 +814,7 @@ __global__ __launch_bounds__(kThreads, MINB) void gemm_tn_kernel(
 // (a 64x64 weight with 1024 splits would otherwise be 4 blocks of serial loads).
 template <typename OT>
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restrict__ part, int splits,
-                                                           int64_t n, int sl, OT* __restrict__ out) {
+                                                           int64_t n, int sl, OT* __restrict__ out, int acc) {
   const int cols = 256 / sl;
   const int cl = threadIdx.x % cols, lane_s = threadIdx.x / cols;
   const int64_t i = ((int64_t)blockIdx.x * cols + cl) * 4;
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float* __restri
   if (lane_s == 0 && i < n) {
     a = red[threadIdx.x];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) out[i + e] = (OT)a[e];
+    for (int e = 0; e < 4; ++e) out[i + e] = (OT)(acc ? a[e] + (float)out[i + e] : a[e]);
   }
 }
 
@@ -877,17 +877,21 @@ void launch_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K, fl
 
 }  // namespace
 
-void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream);
+void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream,
+                         bool acc = false);
+at::Tensor acc_target(const c10::optional<at::Tensor>& out, int64_t numel, at::ScalarType dtype,
+                      const char* who);
 
 namespace {
 
-// C[N, K] = sum_m A[m, :]^T Bmapped[m, :]  -> out [N, K] (bf16 or fp32)
+// C[N, K] = sum_m A[m, :]^T Bmapped[m, :]  -> out [N, K] (bf16 or fp32); with
+// `acc` (a contiguous [N, K] gradient) the split reduce adds into it instead
 at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
                   at::ScalarType out_dtype, const ConvMap& bmap, int kgran,
-                  const float* bps = nullptr, const float* bpt = nullptr) {
+                  const float* bps = nullptr, const float* bpt = nullptr, at::Tensor acc = at::Tensor()) {
   auto stream = at::hip::getCurrentHIPStream();
-  auto out = at::empty({N, K}, A.options().dtype(out_dtype));
-  if (M == 0) return out.zero_();
+  auto out = acc.defined() ? acc : at::empty({N, K}, A.options().dtype(out_dtype));
+  if (M == 0) return acc.defined() ? out : out.zero_();
   // 128 x 256 output tiles (1 block/CU) halve the L2 re-reads of A (dy) for deep
   // implicit-GEMM weight gradients (K = taps * Cin, Cin % 256 == 0): g_tn_wide
   const bool wide = g_tn_wide && bps == nullptr && N >= 128 && K >= 256 && kgran % 256 == 0;
@@ -916,23 +920,37 @@ at::Tensor run_tn(const at::Tensor& A, const at::Tensor& B, int M, int N, int K,
   else if (bnt == 128) launch_tn<128, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else if (bkt == 128) launch_tn<64, 128>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
   else launch_tn<64, 64>(A, B, M, N, K, pp, splits, rps, bmap, bps, bpt, stream);
-  split_reduce_launch(pp, splits, (int64_t)N * K, out, stream);
+  split_reduce_launch(pp, splits, (int64_t)N * K, out, stream, acc.defined());
   return out;
 }
 
 }  // namespace
 
-// out[c] = sum over splits of part[s][c] (c < n, n % 4 == 0), bf16 or fp32 out.
-void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream) {
+// The gradient buffer a weight-gradient kernel accumulates into (pipeline
+// micro-batch accumulation, ops/grad_accum.py): contiguous, the parameter's
+// dtype, the gradient's element count.
+at::Tensor acc_target(const c10::optional<at::Tensor>& out, int64_t numel, at::ScalarType dtype,
+                      const char* who) {
+  if (!out.has_value() || !out->defined()) return at::Tensor();
+  TORCH_CHECK(out->is_cuda() && out->scalar_type() == dtype && out->numel() == numel &&
+                  reinterpret_cast<uintptr_t>(out->data_ptr()) % 16 == 0 &&
+                  (out->is_contiguous() || out->is_contiguous(at::MemoryFormat::ChannelsLast)),
+              who, ": the accumulation target must be a 16-B aligned dense gradient of the output dtype and size");
+  return *out;
+}
+
+// out[c] = sum over splits of part[s][c] (c < n, n % 4 == 0), bf16 or fp32 out
+// (acc: out[c] += ..., one read-modify-write per element, no extra launch).
+void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream, bool acc) {
   int sl = 1;  // split lanes per column: grow until >= 512 blocks or lanes cover the splits
   while (sl < 64 && sl < splits && (n / 4 + 256 / sl - 1) / (256 / sl) < 512) sl *= 2;
   const unsigned blocks = (unsigned)((n / 4 + 256 / sl - 1) / (256 / sl));
   if (out.scalar_type() == at::kBFloat16)
     hipLaunchKernelGGL((split_reduce_kernel<bf16>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
-                       sl, reinterpret_cast<bf16*>(out.data_ptr()));
+                       sl, reinterpret_cast<bf16*>(out.data_ptr()), (int)acc);
   else
     hipLaunchKernelGGL((split_reduce_kernel<float>), dim3(blocks), dim3(256), 0, stream, pp, splits, n,
-                       sl, out.data_ptr<float>());
+                       sl, out.data_ptr<float>(), (int)acc);
 }
 
 // Weight gradient of a 1x1 conv: C[N, K] = A^T B with A [M, N], B [M, K] (bf16,
@@ -940,7 +958,8 @@ void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out
 // B's logical row m from the strided physical row (stride-s 1x1 conv input).
 at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                    const std::vector<int64_t>& b_map, const c10::optional<at::Tensor>& pro_scale,
-                   const c10::optional<at::Tensor>& pro_shift, bool a_mapped) {
+                   const c10::optional<at::Tensor>& pro_shift, bool a_mapped,
+                   const c10::optional<at::Tensor>& out) {
   check_operand(A, "A");
   check_operand(B, "B");
   const RowMap rm = parse_map(b_map, "b_map");
@@ -976,14 +995,14 @@ at::Tensor gemm_tn(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_
     bps = pro_scale->data_ptr<float>();
     bpt = pro_shift->data_ptr<float>();
   }
-  return run_tn(A, B, M, N, K, out_dtype, cm, 128, bps, bpt);
+  return run_tn(A, B, M, N, K, out_dtype, cm, 128, bps, bpt, acc_target(out, (int64_t)N * K, out_dtype, "gemm_tn"));
 }
 
 // Weight gradient of an implicit-GEMM conv: dy [N*Ho*Wo, Cout] rows, x NHWC
 // [N, Hi, Wi, Cin] -> dW [Cout, kh*kw*Cin] (channels_last weight memory).
 at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw,
                       int64_t stride, int64_t pad, int64_t ho, int64_t wo,
-                      at::ScalarType out_dtype, int64_t kc) {
+                      at::ScalarType out_dtype, int64_t kc, const c10::optional<at::Tensor>& out) {
   check_operand(dy, "dy");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1005,7 +1024,8 @@ at::Tensor conv_wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int
   const int M = (int)dy.size(0), N = (int)dy.size(1), K = (int)(kh * kw * kcv);
   // B rows are addressed through the map; ldb = Cin (pixel stride)
   auto xv = x.permute({0, 2, 3, 1}).reshape({-1, cin});
-  return run_tn(dy, xv, M, N, K, out_dtype, cm, (int)(kcv % 128 == 0 ? 128 : 64));
+  return run_tn(dy, xv, M, N, K, out_dtype, cm, (int)(kcv % 128 == 0 ? 128 : 64), nullptr, nullptr,
+                acc_target(out, (int64_t)N * K, out_dtype, "conv_wgrad"));
 }
 
 namespace {

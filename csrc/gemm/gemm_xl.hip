@@ -1596,8 +1596,7 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
 //       vmcnt(0) + barrier (tile t + 1 landed, buffer t & 1 free);
 //   S2: the half-1 MFMAs, copying tile t + 2 into buffer t & 1 (one copy per
 //       4 MFMAs) and reading half 0 of tile t + 1.
-// SRC: 0 = plain B rows, 2 = the implicit-GEMM tap gather of an NHWC input
-// (not instantiated: 1.5 KB of scratch, see run_tn_pp).
+// SRC: 0 = plain B rows, 2 = the implicit-GEMM tap gather of an NHWC input.
 __device__ __forceinline__ int tnw_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
 template <int SRC>
@@ -1617,7 +1616,15 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   const int64_t mb = (int64_t)split * p.rps;
   const int64_t me = min((int64_t)M, mb + p.rps);
   const int KT = (int)((me - mb + 63) >> 6);
-  static_assert(SRC == 0, "the tap gather runs on gemm_tn_pp_kernel");
+  // SRC 2: the K tile (256 channels) lies inside one tap (Cin % 256 == 0)
+  const XlConv cv = p.cv;
+  int tr = 0, tc = 0, kc0 = k0;
+  if constexpr (SRC == 2) {
+    const int tap = k0 / cv.cin;
+    tr = tap / cv.kw;
+    tc = tap - tr * cv.kw;
+    kc0 = k0 - tap * cv.cin;
+  }
 
   // copy c (0..15) of a K tile: operand c >> 3 (A = dy n columns, B = k
   // columns), plane `wave`, row group c & 7; lane L: row 8 (c & 7) + (L >> 3),
@@ -1645,17 +1652,57 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
     d[3] = 0x00020000;
     return d;
   };
-  const i32x4 rsa = desc(p.A + mb * p.lda, nrow * p.lda * 2), rsb = desc(p.B + mb * p.ldb, nrow * p.ldb * 2);
+  // SRC 2: B's descriptor spans the whole NHWC input (a padding tap's offset
+  // is past its end: the copy lands zeros); every lane tracks the output pixel
+  // (n, oh, ow) of each of its 8 staged rows, advanced by 64 pixels per K tile
+  // (no per-copy division: the divisions made this form spill)
+  const int64_t bbytes = SRC == 2 ? (int64_t)cv.hi * cv.wi * (M / max(1, cv.ho * cv.wo)) * p.ldb * 2
+                                  : nrow * p.ldb * 2;
+  const i32x4 rsa = desc(p.A + mb * p.lda, nrow * p.lda * 2),
+              rsb = desc(SRC == 2 ? p.B : p.B + mb * p.ldb, bbytes);
   const uint32_t oa0 = (uint32_t)((prow * p.lda + n0 + lcol) * 2), oa8 = (uint32_t)((prow * p.lda + n0 + lcol8) * 2);
   const uint32_t ob0 = (uint32_t)((prow * p.ldb + k0 + lcol) * 2), ob8 = (uint32_t)((prow * p.ldb + k0 + lcol8) * 2);
+  int gn[8], goh[8], gow[8];
+  const int hw = cv.ho * cv.wo, adv_oh = SRC == 2 ? 64 / max(1, cv.wo) : 0, adv_ow = SRC == 2 ? 64 % max(1, cv.wo) : 0;
+  if constexpr (SRC == 2) {
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+      const int mi = (int)min(mb + 8 * rg + prow, (int64_t)M - 1), n = mi / hw, r = mi - n * hw;
+      gn[rg] = n;
+      goh[rg] = r / cv.wo;
+      gow[rg] = r - goh[rg] * cv.wo;
+    }
+  }
+  // SRC 2: the 8 B row offsets of K tile kt, then advance every row by 64 pixels
+  uint32_t bo[8];
+  auto gather_rows = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+      const int ih = goh[rg] * cv.stride - cv.pad + tr, iw = gow[rg] * cv.stride - cv.pad + tc;
+      const bool ok = kt * 64 + 8 * rg + prow < nrow && (unsigned)ih < (unsigned)cv.hi && (unsigned)iw < (unsigned)cv.wi;
+      const int64_t pix = ((int64_t)gn[rg] * cv.hi + ih) * cv.wi + iw;
+      bo[rg] = ok ? (uint32_t)((pix * p.ldb + kc0 + ((rg & 1) ? lcol8 : lcol)) * 2) : 0xfffffff0u;
+      int ow = gow[rg] + adv_ow, oh = goh[rg] + adv_oh, n = gn[rg];
+      if (ow >= cv.wo) { ow -= cv.wo; ++oh; }
+#pragma unroll
+      for (int w = 0; w < 3; ++w)  // adv_oh + 1 <= 3 ho (host-checked)
+        if (oh >= cv.ho) { oh -= cv.ho; ++n; }
+      gow[rg] = ow; goh[rg] = oh; gn[rg] = n;
+    }
+  };
   const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(smem);
-  auto dma = [&](int kt, int buf, int c) {
+  auto dma = [&](int kt, int buf, int c) __attribute__((always_inline)) {
     const int rg = c & 7;
     const bool odd = rg & 1;  // row bit 3
     const int ldst = __builtin_amdgcn_readfirstlane((int)(lds0 + buf * BUF + (c >> 3) * OPER + wave * PLANE + rg * 1024));
-    const uint32_t voff = c < 8 ? (odd ? oa8 : oa0) + (uint32_t)(8 * rg * p.lda * 2)
-                                : (odd ? ob8 : ob0) + (uint32_t)(8 * rg * p.ldb * 2);
-    const int soff = __builtin_amdgcn_readfirstlane((int)(kt * 64 * (c < 8 ? p.lda : p.ldb) * 2));
+    uint32_t voff = c < 8 ? (odd ? oa8 : oa0) + (uint32_t)(8 * rg * p.lda * 2)
+                          : (odd ? ob8 : ob0) + (uint32_t)(8 * rg * p.ldb * 2);
+    int soff = __builtin_amdgcn_readfirstlane((int)(kt * 64 * (c < 8 ? p.lda : p.ldb) * 2));
+    if constexpr (SRC == 2)
+      if (c >= 8) {
+        voff = bo[rg];
+        soff = 0;
+      }
     unsigned keep;
     if (c < 8)
       asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
@@ -1671,7 +1718,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   // rows 8g..8g+7 of a k32 step; lane 4q+p of the group reads row q (+4 for
   // the high half), cols 4p..4p+3 of the fragment's 16 columns
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  auto tr_frag = [&](const char* plane, int h, int cin) {  // cin: column within the 64-col plane, % 16 == 0
+  auto tr_frag = [&](const char* plane, int h, int cin) __attribute__((always_inline)) {  // cin: column within the 64-col plane, % 16 == 0
     const int r0 = h * 32 + 8 * g + q4, r1 = r0 + 4;
     const int cb = (cin + 4 * p4) * 2;  // byte within the row
     const char* a0 = plane + r0 * 128 + ((((cb >> 4) ^ tnw_swz(r0))) << 4) + (cb & 15);
@@ -1683,7 +1730,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   };
   bf16x8 ra[2][8], rb[2][8];
   // fragment read r (0..15) of k32 half H: A block (n) r == 0 ? 0 : r - 8, B blocks (k) 0..7 for r = 1..8
-  auto rd = [&](auto hc, int buf, int r) {
+  auto rd = [&](auto hc, int buf, int r) __attribute__((always_inline)) {
     constexpr int H = decltype(hc)::value;
     const bool isb = r >= 1 && r <= 8;
     const int blk = r == 0 ? 0 : (isb ? r - 1 : r - 8);
@@ -1701,9 +1748,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   using I1 = std::integral_constant<int, 1>;
   // operands swapped: acc[i][j] holds the transposed 16 x 16 block: lane =
   // output row n (i), registers = 4 consecutive output columns k (j)
-  auto iter = [&](auto st, auto rdn, int kt) {
+  auto iter = [&](auto st, auto rdn, int kt) __attribute__((always_inline)) {
     constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
     const int buf = kt & 1;
+    if constexpr (SRC == 2 && STAGE) gather_rows(kt + 2);
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
       w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
@@ -1723,9 +1771,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
     }
   };
   if (KT > 0) {
+    if constexpr (SRC == 2) gather_rows(0);
 #pragma unroll
     for (int c = 0; c < 16; ++c) dma(0, 0, c);
     if (KT > 1) {
+      if constexpr (SRC == 2) gather_rows(1);
 #pragma unroll
       for (int c = 0; c < 16; ++c) dma(1, 1, c);
       vmcnt<16>();
@@ -2300,16 +2350,25 @@ at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>&
   return dx;
 }
 
-void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream);
+void split_reduce_launch(const float* pp, int splits, int64_t n, at::Tensor& out, hipStream_t stream,
+                         bool acc = false);
+at::Tensor acc_target(const c10::optional<at::Tensor>& out, int64_t numel, at::ScalarType dtype,
+                      const char* who);
 
 namespace {
 
 int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
 
-at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype) {
+// the gather form addresses the whole NHWC input through 32-bit offsets
+bool tn_w4_gather_fits(const TnPPArgs& a) {
+  const int64_t nb = a.M / std::max(1, a.cv.ho * a.cv.wo);
+  return (int64_t)a.cv.hi * a.cv.wi * nb * a.ldb * 2 < ((int64_t)1 << 31) - 16;
+}
+
+at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype, at::Tensor acc = at::Tensor()) {
   const int M = a.M, N = a.N, K = a.K;
-  auto out = at::empty({N, K}, like.options().dtype(out_dtype));
-  if (M == 0) return out.zero_();
+  auto out = acc.defined() ? acc : at::empty({N, K}, like.options().dtype(out_dtype));
+  if (M == 0) return acc.defined() ? out : out.zero_();
   const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
   // one or two full rounds of 1-block/CU work; every split >= 16 K tiles
   const int mtl = (M + 63) / 64;
@@ -2323,22 +2382,24 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
   a.part = part.data_ptr<float>();
   hipStream_t s = at::hip::getCurrentHIPStream();
-  // plain weight gradients on the 4-wave kernel (finding 70; DMP_XL_PIPE=10:
-  // the ping-pong one).  The tap gather stays on the ping-pong kernel: its
-  // per-copy pixel division pushed the 4-wave form to 1.5 KB of scratch.
+  // weight gradients on the 4-wave kernel (finding 70; DMP_XL_PIPE=10: the
+  // ping-pong one), the tap gather included when its input fits 32-bit offsets
   if (g_xl_pipe == 11 && a.cv.cin == 0)
     hipLaunchKernelGGL(gemm_tn_w4_kernel<0>, dim3(tiles * splits), dim3(256), 0, s, a);
+  else if (g_xl_pipe == 11 && (64 / a.cv.wo + 1) <= 3 * a.cv.ho && tn_w4_gather_fits(a))
+    hipLaunchKernelGGL(gemm_tn_w4_kernel<2>, dim3(tiles * splits), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(gemm_tn_pp_kernel, dim3(tiles * splits), dim3(XTHREADS), 0, s, a);
   DMP_HIP_CHECK(hipGetLastError());
-  split_reduce_launch(a.part, splits, (int64_t)N * K, out, s);
+  split_reduce_launch(a.part, splits, (int64_t)N * K, out, s, acc.defined());
   return out;
 }
 
 }  // namespace
 
 // dW = A^T B on the ping-pong TN kernel: A [M, N], B [M, K] bf16 row-major.
-at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype) {
+at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
+                      const c10::optional<at::Tensor>& out) {
   check_bf16_2d(A, "A");
   check_bf16_2d(B, "B");
   TORCH_CHECK(A.size(0) == B.size(0), "gemm_tn_xl: M mismatch");
@@ -2349,7 +2410,7 @@ at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType o
   a.A = reinterpret_cast<const bf16*>(A.data_ptr()); a.lda = A.stride(0);
   a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
   a.M = (int)A.size(0); a.N = (int)A.size(1); a.K = (int)B.size(1);
-  return run_tn_pp(a, A, out_dtype);
+  return run_tn_pp(a, A, out_dtype, acc_target(out, (int64_t)a.N * a.K, out_dtype, "gemm_tn_xl"));
 }
 
 // Weight gradient of a kh x kw conv on the ping-pong TN kernel:
@@ -2357,7 +2418,8 @@ at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType o
 // row-major, x NHWC (channels_last), Cin % 256 == 0 (a 256-wide K tile never
 // straddles a tap).
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
-                         int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype) {
+                         int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype,
+                         const c10::optional<at::Tensor>& out) {
   check_bf16_2d(dy, "dy");
   TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast), "conv_wgrad_xl: x must be channels_last bf16");
@@ -2372,7 +2434,7 @@ at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, 
   a.M = (int)dy.size(0); a.N = (int)dy.size(1); a.K = (int)(kh * kw * cin);
   a.cv.cin = (int)cin; a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
   a.cv.stride = (int)stride; a.cv.pad = (int)pad; a.cv.kw = (int)kw;
-  return run_tn_pp(a, dy, out_dtype);
+  return run_tn_pp(a, dy, out_dtype, acc_target(out, (int64_t)a.N * a.K, out_dtype, "conv_wgrad_xl"));
 }
 
 void set_tn_xl_rounds(int r) { g_tn_xl_rounds = r; }

@@ -22,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
+from . import grad_accum
 from ..utils.checkpointing import in_recompute
 
 # A moment reducer maps local fp64 moments [2C+1] = (sum x, sum x^2, rows) to
@@ -168,14 +169,15 @@ def backward_moments(dy2, x2, y2, mean, relu, native, weight=None, bias=None, in
 
 
 def backward_apply(dy2, x2, y2, sums, count, weight, mean, invstd, training, relu, want_dres, native,
-                   bias=None, clip=_INF):
+                   bias=None, clip=_INF, acc_weight=None, acc_bias=None):
     """`count` is a 1-element fp64 tensor (global rows).  y2 None with relu:
-    mask from x (see _relu_mask)."""
+    mask from x (see _relu_mask).  acc_weight / acc_bias (native only): fp32
+    gradients the affine gradients are added into (then returned as None)."""
     c = x2.shape[1]
     if native:
         return _native.require("bn").bn_backward_apply(dy2, x2, y2, sums, count, weight, mean,
                                                         invstd, training, relu, want_dres, c, bias,
-                                                        clip)
+                                                        clip, acc_weight, acc_bias)
     count = count.reshape(()).to(torch.float64)
     sdz, sdzx = sums[:c], sums[c:]
     w = weight.double() if weight is not None else torch.ones_like(sdz)
@@ -291,6 +293,7 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.meta = (native, training, relu, residual is not None, back,
                     weight is not None, bias is not None, reduce_grads,
                     weight.dtype if weight is not None else None, x.dim(), clip)
+        ctx.affine = (weight, bias)  # the leaves: micro-batch accumulation targets (ops/grad_accum.py)
         ctx.bwd_slot = None
         # the consumer-epilogue fusion applies a plain ReLU mask: not for ReLU6
         if bwd_slot is not None and native and training and relu and clip == _INF and x.dim() == 4:
@@ -327,8 +330,20 @@ class _BatchNormActFn(torch.autograd.Function):
         if training and reduce_grads is not None:
             local_sums = sums.clone()  # the reducer works in place
             sums = reduce_grads(sums)
+        acc_w = acc_b = None
+        if native and training and reduce_grads is None and has_w and has_b \
+                and ctx.needs_input_grad[2] and ctx.needs_input_grad[3]:
+            # micro-batch accumulation: the apply kernel adds the affine gradients
+            # into weight.grad / bias.grad (fp32 parameters only)
+            pw, pb = ctx.affine
+            if pw.dtype == torch.float32 and pb.dtype == torch.float32:
+                acc_w = grad_accum.target(pw)
+                acc_b = grad_accum.target(pb) if acc_w is not None else None
+                if acc_b is None:
+                    acc_w = None
+        ctx.affine = None
         dx2, dw, db, dres2 = backward_apply(dy2, x2, y_eff, sums, count, w32, mean, invstd, training,
-                                            relu_eff, want_dres, native, b32, clip)
+                                            relu_eff, want_dres, native, b32, clip, acc_w, acc_b)
         if fused is not None and has_res:
             dres2 = dy2  # d(residual) = dz, which is exactly the masked incoming gradient
         if reduce_grads is not None and training:
@@ -338,8 +353,8 @@ class _BatchNormActFn(torch.autograd.Function):
             db = local_sums[:c].float()
         gx = back(dx2)
         gres = back(dres2) if has_res else None
-        gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] else None
-        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] else None
+        gw = dw.to(wdtype) if has_w and ctx.needs_input_grad[2] and acc_w is None else None
+        gb = db.to(wdtype) if has_b and ctx.needs_input_grad[3] and acc_b is None else None
         return gx, gres, gw, gb, None, None, None, None, None, None, None, None, None, None, None, None
 
 

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 
 from .. import _native
-from . import wgrad_stream
+from . import grad_accum, wgrad_stream
 
 _STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0, "compact_dgrad": 0,
           "compact_residual": 0}
@@ -188,13 +188,18 @@ class _Conv1x1Fn(torch.autograd.Function):
             # no-split kernel for this tiny-output / huge-reduction shape); the
             # ping-pong form where both output dims fill its 256x256 tile.  On the
             # weight-gradient side stream, beside the data-gradient chain.
+            # inside grad_accum.accumulate_param_grads the split-K reduce adds
+            # straight into weight.grad (micro-batch accumulation, no autograd add)
+            acc = grad_accum.target(weight)
             with wgrad_stream.side(weight, dy2, x):
                 if not ctx.geom and _tn_xl(dy2.shape[0], cout, cin):
                     _STATS["tn_xl"] += 1
-                    dw = C.gemm_tn_xl(dy2, _rows(x), weight.dtype).view(cout, cin, 1, 1)
+                    dw = C.gemm_tn_xl(dy2, _rows(x), weight.dtype, out=acc).view(cout, cin, 1, 1)
                 else:
-                    dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom).view(cout, cin, 1, 1)
-                if weight.is_contiguous(memory_format=torch.channels_last):
+                    dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom, out=acc).view(cout, cin, 1, 1)
+                if acc is not None:
+                    dw = None
+                elif weight.is_contiguous(memory_format=torch.channels_last):
                     dw = dw.contiguous(memory_format=torch.channels_last)
         return dx, dw, None, None, None, None, None
 

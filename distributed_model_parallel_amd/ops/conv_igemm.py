@@ -58,18 +58,18 @@ def _capturing() -> bool:
 
 # Weight gradients of 3x3 convs the halo kernel does not cover with Cin % 256
 # == 0 (layer 4's stride-2 first block; any layer-3/4 shape at small maps) on
-# the ping-pong TN tap-gather kernel (gemm_xl.hip conv_wgrad_xl) instead of
-# MIOpen's igemm_wrw -- always inside a capture, and eagerly up to
-# _XL_WGRAD_MAX_ROWS output pixels: l4 stride-2 at batch 256 0.133 vs
-# 0.138 ms, at batch 2048 0.908 vs 0.655 ms (profiles/raw_r4/wgrad_s2_r4o.md).
+# the TN tap-gather kernel (gemm_xl.hip conv_wgrad_xl) instead of MIOpen's
+# igemm_wrw, at every size since round 6: its 4-wave form (gemm_tn_w4 with
+# the incremental pixel walk) takes the ResNet-50 layer-3/4 3x3 weight
+# gradients at batch 2048 in 0.49-0.52 ms against MIOpen's 0.66-0.78
+# (tools/pipe_bench.py --only 3x3wg --lib; the round-4 ping-pong form lost
+# above ~50k rows: 0.908 vs 0.655 ms, profiles/raw_r4/wgrad_s2_r4o.md).
 _XL_WGRAD = not _native.disabled("xl_conv3")
-_XL_WGRAD_MAX_ROWS = 50_000
 _STATS["xl_wgrad"] = 0
 
 
 def _xl_wgrad_ok(cin: int, kh: int, kw: int, rows: int) -> bool:
-    return (_XL_WGRAD and cin % 256 == 0 and kh == kw and kh > 1
-            and (rows <= _XL_WGRAD_MAX_ROWS or _capturing()))
+    return _XL_WGRAD and cin % 256 == 0 and kh == kw and kh > 1
 
 # 256x256 ping-pong implicit GEMM (csrc/gemm/gemm_xl.hip conv_xl), used where
 # its 256-wide output tile is full: forward (with the BN moments) when

@@ -49,9 +49,12 @@ class _DWConvFn(torch.autograd.Function):
         dx = C.dwconv3x3_dgrad(dy, w, ctx.stride, x.shape[2], x.shape[3]) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            from . import wgrad_stream
+            from . import grad_accum, wgrad_stream
+            acc = grad_accum.target(w)  # micro-batch accumulation: the column reduce adds into w.grad
             with wgrad_stream.side(w, dy, x):  # beside the data-gradient chain
-                dw = C.dwconv3x3_wgrad(dy, x, ctx.stride, w.dtype)
+                dw = C.dwconv3x3_wgrad(dy, x, ctx.stride, w.dtype, out=acc)
+            if acc is not None:
+                dw = None
         return dx, dw, None, None
 
 

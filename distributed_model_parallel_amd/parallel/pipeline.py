@@ -40,6 +40,10 @@ loops in ``utils.py:34-210``, partition at ``model_parallel.py:101-104,
   backward replay (parameter gradients accumulate in place inside the graph)
   and a send.  1F1B keeps at most ``S - r`` micro-batches in flight on stage
   r, so that many slots (memory pools) suffice.
+* **Gradient accumulation in the kernels** (``kernel_grad_accum=True``): the
+  weight-gradient kernels of the native ops add each micro-batch's parameter
+  gradient straight into ``p.grad`` (:mod:`..ops.grad_accum`) instead of
+  handing autograd a fresh tensor to add.
 """
 from __future__ import annotations
 
@@ -50,6 +54,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..comm.rccl import Communicator
+from ..ops.grad_accum import accumulate_param_grads
 from ..utils.graphs import no_gc_during_capture
 from ..utils.profiling import trace_range
 
@@ -259,7 +264,7 @@ class Pipeline:
                  partition=None, balance: str = "flops",
                  device: Optional[torch.device] = None, dtype: torch.dtype = torch.float32,
                  channels_last: bool = False, static_batch: Optional[int] = None,
-                 fail_fast: bool = True, graphs: bool = False):
+                 fail_fast: bool = True, graphs: bool = False, kernel_grad_accum: bool = True):
         if schedule not in ("naive", "gpipe", "1f1b"):
             raise ValueError(f"unknown schedule {schedule!r}")
         if loss_on not in ("last", "first"):
@@ -299,6 +304,9 @@ class Pipeline:
         # static contract) would leave the other stages blocked in a receive
         # forever: publish it so every rank exits non-zero (utils/debug.py)
         self.graphs = bool(graphs)
+        # micro-batch gradient accumulation inside the weight-gradient kernels
+        # (ops/grad_accum.py): no AccumulateGrad add per parameter per micro-batch
+        self.kernel_grad_accum = bool(kernel_grad_accum)
         self._graphs: Dict[int, "_StageGraphs"] = {}  # micro-batch size -> captured slots
         self.recaptures = 0  # forced re-captures of existing stage graphs (moved storage)
         self._failure = None
@@ -423,12 +431,13 @@ class Pipeline:
         else:
             tgt_mbs = [t.to(self.device) for t in ts] if self.is_first else None
         stats = torch.zeros(3, dtype=torch.float64, device=self.device)
-        if self._graphed_ok(sizes):
-            stats = self._run_1f1b_graphed(xs, tgt_mbs, sizes)
-        elif self.schedule == "1f1b":
-            self._run_1f1b(xs, tgt_mbs, sizes, stats)
-        else:
-            self._run_gpipe(xs, tgt_mbs, sizes, stats)
+        with accumulate_param_grads(self.kernel_grad_accum):
+            if self._graphed_ok(sizes):
+                stats = self._run_1f1b_graphed(xs, tgt_mbs, sizes)
+            elif self.schedule == "1f1b":
+                self._run_1f1b(xs, tgt_mbs, sizes, stats)
+            else:
+                self._run_gpipe(xs, tgt_mbs, sizes, stats)
         return self._finish_stats(stats, batch)
 
     def _finish_stats(self, stats: torch.Tensor, batch: int) -> StepResult:
@@ -443,7 +452,19 @@ class Pipeline:
             return StepResult(stats=stats, batch=batch)
         return StepResult(None, None, None)
 
+    def _fused_loss(self, y: torch.Tensor, t: torch.Tensor, stats: torch.Tensor) -> Optional[torch.Tensor]:
+        """Loss / micro_batches with the statistics accumulated by the native
+        cross-entropy kernels themselves (ops/loss.py cross_entropy_with_stats),
+        when the stage uses the default loss on the GPU; else None."""
+        from ..ops import loss as L
+        if self.loss_fn is L.cross_entropy and stats.is_cuda and L._native_ce_ok(y, t):
+            return L.cross_entropy_with_stats(y, t, 1.0 / self.micro_batches, stats)
+        return None
+
     def _loss_and_stats(self, y: torch.Tensor, t: torch.Tensor, stats: torch.Tensor) -> torch.Tensor:
+        fused = self._fused_loss(y, t, stats)
+        if fused is not None:
+            return fused
         logits = y.float()
         loss = self.loss_fn(logits, t) / self.micro_batches
         with torch.no_grad():
@@ -792,6 +813,9 @@ class _StageGraphs:
         y = pipe.module(self.inputs[k])
         if not pipe.is_last:
             return y.contiguous()  # the wire layout of the eager path (its backward: a copy)
+        fused = pipe._fused_loss(y, self.targets[k], self.stats)
+        if fused is not None:
+            return fused
         logits = y.float()
         loss = pipe.loss_fn(logits, self.targets[k]) / pipe.micro_batches
         with torch.no_grad():

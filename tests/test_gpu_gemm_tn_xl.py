@@ -38,9 +38,22 @@ def test_gemm_tn_xl_exact_pattern(M):
     assert torch.equal(C.gemm_tn_xl(a, b, torch.float32), a.float().t() @ b.float())
 
 
+@pytest.fixture(params=[10, 11])
+def tn_pipe(request):
+    """10: the ping-pong TN kernel; 11: the 4-wave one (its tap gather walks
+    each staged row's pixel forward 64 at a time: ho 5 / 7 exercise the
+    multi-image wrap, ho 3 falls back to the ping-pong kernel)."""
+    C = _native.require("conv_wgrad_xl")
+    old = C.get_gemm_xl_pipe()
+    C.set_gemm_xl_bn(0, request.param, 0)
+    yield request.param
+    C.set_gemm_xl_bn(0, old, 0)
+
+
 @pytest.mark.parametrize("n,cin,cout,h,k,s", [(4, 256, 256, 9, 3, 1), (3, 256, 512, 15, 3, 2), (2, 512, 256, 7, 3, 1),
-                                              (4, 256, 128, 10, 1, 2)])
-def test_conv_wgrad_xl(n, cin, cout, h, k, s):
+                                              (4, 256, 128, 10, 1, 2), (64, 512, 512, 7, 3, 1),
+                                              (24, 256, 256, 14, 3, 2), (9, 256, 256, 5, 3, 1), (16, 256, 256, 3, 3, 1)])
+def test_conv_wgrad_xl(n, cin, cout, h, k, s, tn_pipe):
     C = _native.require("conv_wgrad_xl")
     torch.manual_seed(1)
     p = k // 2

@@ -40,3 +40,37 @@ def test_cross_entropy_out_of_range_label_is_nan_not_oob(bad):
     assert torch.isnan(loss).item()
     loss.backward()
     assert torch.isnan(x.grad[3]).all().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,C", [(64, 10), (33, 4), (256, 1000)])
+def test_cross_entropy_with_stats_matches_topk(dtype, B, C):
+    """The pipeline's fused loss + statistics (ops/loss.py cross_entropy_with_stats):
+    scale * loss, its gradient, and stats += (loss, top-1, top-min(5,C) correct)
+    against F.cross_entropy and torch.topk (bf16 logits: ties between equal
+    logits resolved by index, as a stable sort)."""
+    from distributed_model_parallel_amd.ops.loss import cross_entropy_with_stats
+    torch.manual_seed(B + C)
+    x = (torch.randn(B, C, device="cuda") * 3).to(dtype)
+    t = torch.randint(0, C, (B,), device="cuda")
+    stats = torch.full((3,), 1.5, dtype=torch.float64, device="cuda")  # accumulates
+    xa = x.clone().requires_grad_()
+    loss = cross_entropy_with_stats(xa, t, 0.25, stats)
+    loss.backward()
+    xr = x.float().clone().requires_grad_()
+    ref = F.cross_entropy(xr, t) * 0.25
+    ref.backward()
+    assert abs(float(loss) - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
+    torch.testing.assert_close(xa.grad.float(), xr.grad, atol=1e-2 if dtype == torch.bfloat16 else 1e-6, rtol=1e-2)
+    k = min(5, C)
+    xf = x.float()
+    xt = xf.gather(1, t[:, None])
+    idx = torch.arange(C, device="cuda")[None, :]
+    rank = ((xf > xt) | ((xf == xt) & (idx < t[:, None]))).sum(1)
+    assert abs(float(stats[0]) - 1.5 - float(ref)) < 1e-5 * max(1.0, abs(float(ref)))
+    assert float(stats[1]) - 1.5 == float((rank < 1).sum())
+    assert float(stats[2]) - 1.5 == float((rank < k).sum())
+    if dtype == torch.float32:  # no ties: the same counts as torch.topk
+        top = xf.topk(k, 1).indices
+        assert float(stats[1]) - 1.5 == float((top[:, 0] == t).sum())
+        assert float(stats[2]) - 1.5 == float((top == t[:, None]).any(1).sum())

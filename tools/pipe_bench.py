@@ -53,6 +53,12 @@ TN_SHAPES = [  # name, M (reduction), N, K  (ResNet-50 at batch 2048: dW[Cout, C
     ("r50_l3c1_wgrad", 401408, 256, 1024),
     ("r50_l4c1_wgrad", 100352, 512, 2048),
 ]
+WGRAD_SHAPES = [  # name, N, Cin, H_in (= W), Cout, stride: 3x3 / pad 1 weight gradients at batch 2048
+    ("r50_l4_3x3wg", 2048, 512, 7, 512, 1),
+    ("r50_l4s2_3x3wg", 2048, 512, 14, 512, 2),
+    ("r50_l3_3x3wg", 2048, 256, 14, 256, 1),
+    ("r50_l3s2_3x3wg", 2048, 256, 28, 256, 2),
+]
 
 
 def timed(fn, iters):
@@ -175,6 +181,30 @@ def main():
                 arms["hipblaslt"] = lambda: dy.t().mm(xx)
             ab(name, 2.0 * M * N * K, arms, a.rounds, a.iters, exact=set())
             del dy, xx
+            torch.cuda.empty_cache()
+        for name, nb, cin, h, cout, st in WGRAD_SHAPES:
+            if a.only and a.only not in name:
+                continue
+            ho = (h - 1) // st + 1
+            x = (torch.rand(nb, cin, h, h, device="cuda", dtype=torch.bfloat16) * 2 - 1).contiguous(
+                memory_format=torch.channels_last)
+            dy = (torch.rand(nb, cout, ho, ho, device="cuda", dtype=torch.bfloat16) * 2 - 1).contiguous(
+                memory_format=torch.channels_last)
+            dy2 = dy.permute(0, 2, 3, 1).reshape(-1, cout)
+            w = torch.empty(cout, cin, 3, 3, device="cuda", dtype=torch.bfloat16).contiguous(
+                memory_format=torch.channels_last)
+
+            def warm(pipe):
+                def f():
+                    C.set_gemm_xl_bn(0, pipe, 0)
+                    return C.conv_wgrad_xl(dy2, x, 3, 3, st, 1, ho, ho, torch.float32)
+                return f
+            arms = {f"tn_pipe{p}": warm(p) for p in pipes}
+            if a.lib:
+                arms["miopen"] = lambda: torch.ops.aten.convolution_backward(
+                    dy, x, w, None, [st, st], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False])[1].permute(0, 2, 3, 1).reshape(cout, -1)
+            ab(name, 2.0 * nb * ho * ho * cout * 9 * cin, arms, a.rounds, a.iters, exact=set())
+            del x, dy, dy2, w
             torch.cuda.empty_cache()
     finally:
         C.set_gemm_xl_bn(0, old_pipe, 0)

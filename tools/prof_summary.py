@@ -48,6 +48,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--marker", default="sgd_flat")
     ap.add_argument("--title", default="")
+    ap.add_argument("--sequence", type=int, default=0,
+                    help="also list the first N kernels of the last step in launch order")
     a = ap.parse_args()
     trace = glob.glob(os.path.join(a.dir, "*kernel_trace.csv"))
     stats = glob.glob(os.path.join(a.dir, "*kernel_stats.csv"))
@@ -95,6 +97,15 @@ def main():
         print("\n## Last step, top kernels\n\n| ms | calls | kernel |\n|---|---|---|", file=out)
         for k, (n, v) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:30]:
             print(f"| {v:.3f} | {n} | `{k}` |", file=out)
+        if a.sequence:
+            print(f"\n## Last step, first {a.sequence} kernels in launch order\n\n| # | us | gap us | kernel |"
+                  "\n|---|---|---|---|", file=out)
+            prev = None
+            for i, r in enumerate(last[: a.sequence]):
+                st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                gap = (st - prev) / 1e3 if prev is not None else 0.0
+                prev = en
+                print(f"| {i} | {(en - st) / 1e3:.1f} | {gap:.1f} | `{r['Kernel_Name'][:90]}` |", file=out)
     elif stats:
         print("| ms | calls | kernel |\n|---|---|---|", file=out)
         for r in list(csv.DictReader(open(stats[0])))[:30]:
