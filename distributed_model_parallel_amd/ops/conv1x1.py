@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 
 from .. import _native
-from . import grad_accum, wgrad_stream
+from . import grad_accum, wgrad_stream, wt_cache
 
 _STATS = {"native": 0, "torch": 0, "fused_dgrad": 0, "fused_bn_bwd": 0, "xl": 0, "compact_dgrad": 0,
           "compact_residual": 0}
@@ -126,7 +126,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0] and ps is not None and ps.can_park_compact():
             # the consumer adds the stride-grid rows itself: no zero-filled full-size dx
             _STATS["compact_dgrad"] += 1
-            ps.compact, _ = C.gemm_nt(dy2, w2.t().contiguous())
+            ps.compact, _ = C.gemm_nt(dy2, wt_cache.transposed(weight))
             ps.compact_geom = list(ctx.geom)
         elif ctx.needs_input_grad[0]:
             # strided: the GEMM scatters into the sampled rows of a zeroed full-size grad
@@ -164,11 +164,11 @@ class _Conv1x1Fn(torch.autograd.Function):
                         _STATS["compact_residual"] += 1
                 if _xl(cin, cout):
                     _STATS["xl"] += 1
-                    dx2, sums = C.gemm_xl_conv(dy2, w2.t().contiguous(), "bnbwd", residual=extra,
+                    dx2, sums = C.gemm_xl_conv(dy2, wt_cache.transposed(weight), "bnbwd", residual=extra,
                                                bn_x=bs.x2, bn_y=bs.y2, mean=bs.mean, invstd=inv,
                                                weight=bw, bias=bb, res_map=rmap)
                 else:
-                    dx2, sums = C.gemm_nt_bnbwd(dy2, w2.t().contiguous(), extra, bs.x2, bs.y2,
+                    dx2, sums = C.gemm_nt_bnbwd(dy2, wt_cache.transposed(weight), extra, bs.x2, bs.y2,
                                                 bs.mean, inv, bw, bb, rmap)
                 dx = _unrows(dx2, n, h, w)
                 bs.park(dx, sums[: 2 * cin])
@@ -176,11 +176,11 @@ class _Conv1x1Fn(torch.autograd.Function):
             elif extra is not None:  # dx = dy @ W + (the shortcut branch's gradient), one pass
                 _STATS["fused_dgrad"] += 1
                 extra = _rows(extra.to(x.dtype).contiguous(memory_format=torch.channels_last))
-                dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), mode="add", residual=extra)
+                dx2, _ = C.gemm_nt(dy2, wt_cache.transposed(weight), mode="add", residual=extra)
             elif not ctx.geom and _blaslt_dgrad(dy2.shape[0], cin, cout):
                 dx2 = dy2 @ w2  # deep-K / short-M: hipBLASLt's stream-K tiles win here
             else:
-                dx2, _ = C.gemm_nt(dy2, w2.t().contiguous(), c_map=ctx.geom)
+                dx2, _ = C.gemm_nt(dy2, wt_cache.transposed(weight), c_map=ctx.geom)
             if dx2 is not None:
                 dx = _unrows(dx2, n, h, w)
         if ctx.needs_input_grad[1]:

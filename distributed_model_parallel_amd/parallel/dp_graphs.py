@@ -60,6 +60,28 @@ def _static_copy(module: nn.Module, device: torch.device, share_buffers_with: Op
     return rep
 
 
+def check_replica_layout(devices: Sequence[torch.device], stream_devices: Sequence[torch.device],
+                         stream_ids: Sequence[int], tensor_devices: Sequence[Sequence[torch.device]],
+                         per_replica_streams: bool = True) -> None:
+    """The invariants a captured replica set relies on:
+    replica i's stream lives on replica i's device; with per-replica streams no
+    two replicas share one (a shared stream would serialise replicas and, on
+    distinct devices, replay a graph on a foreign device's queue); every static
+    parameter / buffer / input of replica i is on device i.  (Each replica is
+    captured by its own make_graphed_callables call, which gives it its own
+    graph memory pool.)  Raises RuntimeError naming the first violation."""
+    if not (len(devices) == len(stream_devices) == len(stream_ids) == len(tensor_devices)):
+        raise RuntimeError("GraphedReplicas: one stream and one tensor set per replica")
+    for i, (d, sd) in enumerate(zip(devices, stream_devices)):
+        if torch.device(sd) != torch.device(d):
+            raise RuntimeError(f"GraphedReplicas: replica {i}'s stream is on {sd}, the replica on {d}")
+        bad = [t for t in tensor_devices[i] if torch.device(t) != torch.device(d)]
+        if bad:
+            raise RuntimeError(f"GraphedReplicas: replica {i} (device {d}) holds a static tensor on {bad[0]}")
+    if per_replica_streams and len(set(zip(map(str, stream_devices), stream_ids))) != len(stream_ids):
+        raise RuntimeError("GraphedReplicas: two replicas share a replay stream")
+
+
 class GraphedReplicas:
     """Per-device static replicas of ``module`` with captured forward and
     backward graphs, for one per-replica input shape."""
@@ -90,6 +112,9 @@ class GraphedReplicas:
         else:
             self.streams = [torch.cuda.current_stream(d) for d in self.devices]
         self.rbuffers = [list(r.buffers()) for r in self.replicas]
+        check_replica_layout(self.devices, [s.device for s in self.streams], [s.stream_id for s in self.streams],
+                             [[t.device for t in (self.rparams[i] + self.rbuffers[i] + [self.inputs[i]])]
+                              for i in range(len(self.devices))], PER_REPLICA_STREAMS)
         self.graphed = []
         # the capture's warm-up iterations run replica 0 for real: keep the
         # module's running statistics as they were (its buffers are shared)

@@ -307,6 +307,11 @@ class Pipeline:
         # micro-batch gradient accumulation inside the weight-gradient kernels
         # (ops/grad_accum.py): no AccumulateGrad add per parameter per micro-batch
         self.kernel_grad_accum = bool(kernel_grad_accum)
+        # one W^T per 1x1-conv weight per step, shared by the micro-batches'
+        # data-gradient GEMMs (ops/wt_cache.py)
+        from ..ops.conv1x1 import Conv1x1
+        from ..ops.wt_cache import WTCache
+        self._wt = WTCache(m.weight for m in self.module.modules() if isinstance(m, Conv1x1))
         self._graphs: Dict[int, "_StageGraphs"] = {}  # micro-batch size -> captured slots
         self.recaptures = 0  # forced re-captures of existing stage graphs (moved storage)
         self._failure = None
@@ -431,7 +436,12 @@ class Pipeline:
         else:
             tgt_mbs = [t.to(self.device) for t in ts] if self.is_first else None
         stats = torch.zeros(3, dtype=torch.float64, device=self.device)
-        with accumulate_param_grads(self.kernel_grad_accum):
+        import contextlib
+        wt = contextlib.nullcontext()
+        if self.device.type == "cuda" and len(self._wt) and self.micro_batches > 1:
+            self._wt.refresh()  # the weights of this step, transposed once
+            wt = self._wt.active()
+        with accumulate_param_grads(self.kernel_grad_accum), wt:
             if self._graphed_ok(sizes):
                 stats = self._run_1f1b_graphed(xs, tgt_mbs, sizes)
             elif self.schedule == "1f1b":

@@ -418,3 +418,21 @@ def test_native_launcher_reports_host_time_breakdown():
     assert sorted(ht["replicas"]) == [0, 1, 2]
     for r in ht["replicas"].values():
         assert r["wall_ms"] >= r["call_ms"] > 0 and r["gil_wait_ms"] >= 0
+
+
+def test_graphed_replica_layout_check():
+    """dp_graphs.check_replica_layout: per device one
+    stream on that device, every static tensor on its replica's device."""
+    import pytest as _pytest
+    import torch as _t
+    from distributed_model_parallel_amd.parallel.dp_graphs import check_replica_layout
+    c0, c1 = _t.device("cuda", 0), _t.device("cuda", 1)
+    check_replica_layout([c0, c1], [c0, c1], [3, 3], [[c0, c0], [c1]])            # distinct devices
+    check_replica_layout([c0, c0], [c0, c0], [3, 4], [[c0], [c0]])                # aliased, two streams
+    with _pytest.raises(RuntimeError, match="share a replay stream"):
+        check_replica_layout([c0, c0], [c0, c0], [3, 3], [[c0], [c0]])
+    with _pytest.raises(RuntimeError, match="stream is on"):
+        check_replica_layout([c0, c1], [c0, c0], [3, 4], [[c0], [c1]])
+    with _pytest.raises(RuntimeError, match="static tensor"):
+        check_replica_layout([c0, c1], [c0, c1], [3, 3], [[c0], [c0]])
+    check_replica_layout([c0, c0], [c0, c0], [3, 3], [[c0], [c0]], per_replica_streams=False)

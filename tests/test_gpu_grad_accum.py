@@ -138,9 +138,11 @@ def test_pipeline_kernel_accumulation_matches_autograd(graphs):
     g = torch.Generator().manual_seed(1)
     x = torch.randn(64, 3, 32, 32, generator=g)
     y = torch.randint(0, 10, (64,), generator=g)
-    before = grad_accum.stats()["kernel"]
+    from distributed_model_parallel_amd.ops import wt_cache
+    before, hits = grad_accum.stats()["kernel"], wt_cache.stats()["hit"]
     res = [p.train_step(x, y) for p in pipes]
     assert grad_accum.stats()["kernel"] > before
+    assert wt_cache.stats()["hit"] > hits  # the step's W^T buffers served the data gradients
     assert abs(float(res[0].loss) - float(res[1].loss)) < 1e-3 * max(1.0, float(res[0].loss))
     norms = sorted(float(p.grad.float().norm()) for p in pipes[0].module.parameters())
     floor = 1e-3 * norms[len(norms) // 2]
