@@ -300,8 +300,15 @@ def _fold_branch_backward(C, dz2, sdz, inp, geom, n, W, WG, asums, mean, invstd,
     """dW, dgamma, dbeta, the dgrad operand Bm = [(al o W)^T | W^T diag(be) W] and c^T W of one branch."""
     cout, cin = W.shape
     if native:
-        from .conv1x1 import _tn_xl
-        if geom:
+        from .conv1x1 import _tn_xl, _tn_xl_strided
+        if geom and _tn_xl_strided(dz2.shape[0], cout, cin):
+            # the strided branch's sampled rows read in place by the 4-wave
+            # TN kernel's tap gather (a 1x1 / stride-s "conv" weight gradient)
+            s, ho, wo, hi, wi = geom
+            x4 = inp.view(n, hi, wi, cin).permute(0, 3, 1, 2)
+            D = C.conv_wgrad_xl(dz2, x4, 1, 1, s, 0, ho, wo, torch.float32)
+            _STATS["fold_ds_wgrad_xl"] = _STATS.get("fold_ds_wgrad_xl", 0) + 1
+        elif geom:
             D = C.gemm_tn(dz2, inp, torch.float32, b_map=geom)
         else:
             D = C.gemm_tn_xl(dz2, inp, torch.float32) if _tn_xl(inp.shape[0], cout, cin) \

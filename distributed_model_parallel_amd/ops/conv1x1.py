@@ -195,6 +195,12 @@ class _Conv1x1Fn(torch.autograd.Function):
                 if not ctx.geom and _tn_xl(dy2.shape[0], cout, cin):
                     _STATS["tn_xl"] += 1
                     dw = C.gemm_tn_xl(dy2, _rows(x), weight.dtype, out=acc).view(cout, cin, 1, 1)
+                elif ctx.geom and _tn_xl_strided(dy2.shape[0], cout, cin):
+                    # stride-s 1x1 (ResNet downsample): the 4-wave TN kernel's
+                    # tap gather reads the sampled rows of x in place
+                    _STATS["tn_xl_strided"] += 1
+                    s, ho, wo = ctx.geom[0], ctx.geom[1], ctx.geom[2]
+                    dw = C.conv_wgrad_xl(dy2, x, 1, 1, s, 0, ho, wo, weight.dtype, out=acc).view(cout, cin, 1, 1)
                 else:
                     dw = C.gemm_tn(dy2, _rows(x), weight.dtype, b_map=ctx.geom, out=acc).view(cout, cin, 1, 1)
                 if acc is not None:
@@ -221,6 +227,16 @@ def _tn_xl(m: int, cout: int, cin: int) -> bool:
     convergence test lowers the row threshold so its batch-64 run trains this
     route.)"""
     return _TN_XL and cout >= 64 and cin >= 64 and m >= _TN_XL_MIN_ROWS
+
+
+_STATS["tn_xl_strided"] = 0
+
+
+def _tn_xl_strided(m: int, cout: int, cin: int) -> bool:
+    """Strided 1x1 weight gradients on the tap-gather TN kernel (conv_wgrad_xl,
+    Cin % 256 == 0): the ResNet-50 downsample convs, which the split-M TN
+    kernel took through its row map."""
+    return _TN_XL and cout >= 64 and cin % 256 == 0 and m >= _TN_XL_MIN_ROWS
 
 
 def conv1x1(x: torch.Tensor, weight: torch.Tensor, stride: int = 1,

@@ -168,16 +168,20 @@ def test_fold_chain_matches_fp32_reference(cin, hw, n):
     torch.testing.assert_close(bn3f.running_var.double(), 0.9 + 0.1 * var, rtol=2e-2, atol=2e-3)
 
 
+@pytest.mark.parametrize("low_rows", [False, True], ids=["default_routes", "strided_wgrad_xl"])
 @pytest.mark.parametrize("cin,planes,stride,hw", [(64, 64, 1, 56), (256, 128, 2, 56), (512, 256, 2, 28),
                                                    (1024, 512, 2, 14), (1024, 512, 2, 4)])
-def test_bottleneck_fold_matches_unfused_model(cin, planes, stride, hw):
+def test_bottleneck_fold_matches_unfused_model(cin, planes, stride, hw, low_rows, monkeypatch):
     """A downsampling bottleneck + a plain one in bf16, fold on (bn3 folded; the
     first block's downsample conv + BN folded into the same GEMM) vs DMP's
     unfused native path (bn_fold.ENABLED off), each measured against the same
     blocks in fp32 stock PyTorch (reference_mode): the fold may not be less accurate."""
     import copy
     from distributed_model_parallel_amd.models.resnet import Bottleneck
+    from distributed_model_parallel_amd.ops import conv1x1 as c1
     from distributed_model_parallel_amd.utils.precision import cast_model
+    if low_rows:  # these small batches through the batch-2048 routes (the 4-wave TN kernels)
+        monkeypatch.setattr(c1, "_TN_XL_MIN_ROWS", 1024)
     torch.manual_seed(4)
     cout = planes * 4
     down = torch.nn.Sequential(Conv1x1(cin, cout, stride), BatchNormAct2d(cout))
@@ -207,6 +211,8 @@ def test_bottleneck_fold_matches_unfused_model(cin, planes, stride, hw):
     got = run(net, torch.bfloat16)
     st1 = bn_fold.stats()
     assert st1["fold"] == st0["fold"] + 1 and st1["fold_ds"] == st0["fold_ds"] + 1
+    if low_rows and stride != 1 and cin % 256 == 0 and nb * ho * ho >= 1024:  # strided branch: tap-gather TN
+        assert st1.get("fold_ds_wgrad_xl", 0) == st0.get("fold_ds_wgrad_xl", 0) + 1
     if stride != 1:
         assert st1["fold_ds_compact"] == st0["fold_ds_compact"] + 1  # shortcut grad parked compact
     old = bn_fold.ENABLED

@@ -149,3 +149,25 @@ def test_pipeline_kernel_accumulation_matches_autograd(graphs):
     for a, b in zip(pipes[0].module.parameters(), pipes[1].module.parameters()):
         err = float((a.grad.float() - b.grad.float()).norm())
         assert err <= 2e-2 * float(a.grad.float().norm()) + floor, (err, float(a.grad.float().norm()))
+
+
+def test_conv1x1_strided_wgrad_on_tap_gather(monkeypatch):
+    """Stride-2 1x1 weight gradients (the ResNet downsample) on the 4-wave TN
+    kernel's tap gather (conv_wgrad_xl): fp32 reference, and accumulation."""
+    from distributed_model_parallel_amd.ops import conv1x1 as c1
+    from distributed_model_parallel_amd.ops.conv1x1 import Conv1x1
+    monkeypatch.setattr(c1, "_TN_XL_MIN_ROWS", 1024)
+    torch.manual_seed(5)
+    conv = Conv1x1(256, 128, stride=2).to(DEV, torch.bfloat16).to(memory_format=CL)
+    xs = [torch.randn(16, 256, 16, 16, device=DEV).bfloat16().contiguous(memory_format=CL) for _ in range(2)]
+    gs = [torch.randn(16, 128, 8, 8, device=DEV).bfloat16() for _ in range(2)]
+    before = c1._STATS["tn_xl_strided"]
+
+    def fn(i):
+        conv(xs[i]).backward(gs[i])
+    (acc,), used = _twice(fn, [conv.weight], True)
+    assert used == 2 and c1._STATS["tn_xl_strided"] - before == 2
+    w32 = conv.weight.detach().float().requires_grad_()
+    for i in range(2):
+        F.conv2d(xs[i].float(), w32, None, 2).backward(gs[i].float())
+    assert _rel(acc, w32.grad) < 1e-2
