@@ -127,6 +127,8 @@ std::vector<at::Tensor> conv_xl(const at::Tensor& x, const at::Tensor& wmat, int
 std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tensor& B, const at::Tensor& aux);
 at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType out_dtype,
                       const c10::optional<at::Tensor>& out);
+at::Tensor gram_strided_xl(const at::Tensor& x, int64_t stride, int64_t ho, int64_t wo);
+bool gram_strided_xl_supported(int64_t nb, int64_t cin, int64_t hi, int64_t wi, int64_t ho, int64_t wo);
 // conv3x3_halo.hip
 std::vector<at::Tensor> conv3x3_c64(const at::Tensor& x, const at::Tensor& wmat, bool moments);
 std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat, bool moments);
@@ -367,6 +369,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"), py::arg("out") = py::none(),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M",
         py::call_guard<py::gil_scoped_release>());
+  m.def("gram_strided_xl", &dmp::gram_strided_xl, py::arg("x"), py::arg("stride"), py::arg("ho"), py::arg("wo"),
+        "fp32 Gram x_s^T x_s of the stride-s sample of an NHWC bf16 input (4-wave TN kernel, both operands gathered)",
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gram_strided_xl_supported", &dmp::gram_strided_xl_supported);
   m.def("conv_wgrad_xl", &dmp::conv_wgrad_xl, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"),
         py::arg("stride"), py::arg("pad"), py::arg("ho"), py::arg("wo"), py::arg("out_dtype"),
         py::arg("out") = py::none(),

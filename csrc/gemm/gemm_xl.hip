@@ -1403,6 +1403,7 @@ struct TnPPArgs {
   int64_t rps;   // rows per split, a multiple of 64
   float* part;   // [splits][N][K]
   XlConv cv;     // cin > 0: B row m of a K tile = input pixel of its tap (K tile inside one tap)
+  int gram = 0;  // 1: A = B = the gathered rows (Gram of a strided 1x1 sample; 4-wave kernel only)
 };
 
 // 32-B chunk XOR: row & 1 separates rows q, q+1 (one 256-B bank row holds 4
@@ -1596,7 +1597,8 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
 //       vmcnt(0) + barrier (tile t + 1 landed, buffer t & 1 free);
 //   S2: the half-1 MFMAs, copying tile t + 2 into buffer t & 1 (one copy per
 //       4 MFMAs) and reading half 0 of tile t + 1.
-// SRC: 0 = plain B rows, 2 = the implicit-GEMM tap gather of an NHWC input.
+// SRC: 0 = plain B rows, 2 = the implicit-GEMM tap gather of an NHWC input,
+// 3 = both operands the gathered rows (the Gram of a strided 1x1 sample).
 __device__ __forceinline__ int tnw_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
 template <int SRC>
@@ -1619,7 +1621,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   // SRC 2: the K tile (256 channels) lies inside one tap (Cin % 256 == 0)
   const XlConv cv = p.cv;
   int tr = 0, tc = 0, kc0 = k0;
-  if constexpr (SRC == 2) {
+  if constexpr (SRC >= 2) {
     const int tap = k0 / cv.cin;
     tr = tap / cv.kw;
     tc = tap - tr * cv.kw;
@@ -1656,19 +1658,22 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   // is past its end: the copy lands zeros); every lane tracks the output pixel
   // (n, oh, ow) of each of its 8 staged rows, advanced by 64 pixels per K tile
   // (no per-copy division: the divisions made this form spill)
-  const int64_t bbytes = SRC == 2 ? (int64_t)cv.hi * cv.wi * (M / max(1, cv.ho * cv.wo)) * p.ldb * 2
-                                  : nrow * p.ldb * 2;
-  const i32x4 rsa = desc(p.A + mb * p.lda, nrow * p.lda * 2),
-              rsb = desc(SRC == 2 ? p.B : p.B + mb * p.ldb, bbytes);
+  // (based at the split's first image: offsets stay 32-bit for inputs > 2 GB)
+  const int64_t img = (int64_t)cv.hi * cv.wi * p.ldb;  // elements per image
+  const int nbase = SRC >= 2 ? (int)(mb / max(1, cv.ho * cv.wo)) : 0;
+  const int64_t bbytes = SRC >= 2 ? ((me - 1) / max(1, cv.ho * cv.wo) - nbase + 1) * img * 2 : nrow * p.ldb * 2;
+  // SRC 3 (the Gram x_s^T x_s of a strided sample): A IS B, both gathered
+  const i32x4 rsb = desc(SRC >= 2 ? p.B + nbase * img : p.B + mb * p.ldb, bbytes),
+              rsa = SRC == 3 ? rsb : desc(p.A + mb * p.lda, nrow * p.lda * 2);
   const uint32_t oa0 = (uint32_t)((prow * p.lda + n0 + lcol) * 2), oa8 = (uint32_t)((prow * p.lda + n0 + lcol8) * 2);
   const uint32_t ob0 = (uint32_t)((prow * p.ldb + k0 + lcol) * 2), ob8 = (uint32_t)((prow * p.ldb + k0 + lcol8) * 2);
   int gn[8], goh[8], gow[8];
-  const int hw = cv.ho * cv.wo, adv_oh = SRC == 2 ? 64 / max(1, cv.wo) : 0, adv_ow = SRC == 2 ? 64 % max(1, cv.wo) : 0;
-  if constexpr (SRC == 2) {
+  const int hw = cv.ho * cv.wo, adv_oh = SRC >= 2 ? 64 / max(1, cv.wo) : 0, adv_ow = SRC >= 2 ? 64 % max(1, cv.wo) : 0;
+  if constexpr (SRC >= 2) {
 #pragma unroll
     for (int rg = 0; rg < 8; ++rg) {
       const int mi = (int)min(mb + 8 * rg + prow, (int64_t)M - 1), n = mi / hw, r = mi - n * hw;
-      gn[rg] = n;
+      gn[rg] = n - nbase;
       goh[rg] = r / cv.wo;
       gow[rg] = r - goh[rg] * cv.wo;
     }
@@ -1703,6 +1708,10 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
         voff = bo[rg];
         soff = 0;
       }
+    if constexpr (SRC == 3) {  // A's columns n0.. of the same gathered rows (a zero row stays zero)
+      voff = c >= 8 || bo[rg] == 0xfffffff0u ? bo[rg] : bo[rg] + (uint32_t)((n0 - kc0) * 2);
+      soff = 0;
+    }
     unsigned keep;
     if (c < 8)
       asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
@@ -1751,7 +1760,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   auto iter = [&](auto st, auto rdn, int kt) __attribute__((always_inline)) {
     constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
     const int buf = kt & 1;
-    if constexpr (SRC == 2 && STAGE) gather_rows(kt + 2);
+    if constexpr (SRC >= 2 && STAGE) gather_rows(kt + 2);
 #pragma unroll
     for (int n = 0; n < 64; ++n) {
       w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
@@ -1771,11 +1780,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
     }
   };
   if (KT > 0) {
-    if constexpr (SRC == 2) gather_rows(0);
+    if constexpr (SRC >= 2) gather_rows(0);
 #pragma unroll
     for (int c = 0; c < 16; ++c) dma(0, 0, c);
     if (KT > 1) {
-      if constexpr (SRC == 2) gather_rows(1);
+      if constexpr (SRC >= 2) gather_rows(1);
 #pragma unroll
       for (int c = 0; c < 16; ++c) dma(1, 1, c);
       vmcnt<16>();
@@ -2359,10 +2368,24 @@ namespace {
 
 int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
 
-// the gather form addresses the whole NHWC input through 32-bit offsets
+// rows per M split (a multiple of 64): one or two full rounds of 1-block/CU
+// work, every split >= 16 K tiles
+int64_t tn_rows_per_split(int M, int N, int K) {
+  const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
+  const int mtl = (M + 63) / 64;
+  int rounds = tiles >= 256 ? (tiles + 255) / 256 : (tiles * std::max(1, 256 / tiles) >= 192 ? 1 : 2);
+  if (g_tn_xl_rounds > 0) rounds = g_tn_xl_rounds;
+  const int splits = std::max(1, std::min(256 * rounds / tiles, mtl / 16));
+  int64_t rps = ((int64_t)M + splits - 1) / splits;
+  return (rps + 63) / 64 * 64;
+}
+
+// the gather form addresses the images one M split touches through 32-bit
+// offsets from the split's first image (the kernel's descriptor base)
 bool tn_w4_gather_fits(const TnPPArgs& a) {
-  const int64_t nb = a.M / std::max(1, a.cv.ho * a.cv.wo);
-  return (int64_t)a.cv.hi * a.cv.wi * nb * a.ldb * 2 < ((int64_t)1 << 31) - 16;
+  const int64_t hw = std::max(1, a.cv.ho * a.cv.wo);
+  const int64_t imgs = std::min<int64_t>(a.M / hw + 1, a.rps / hw + 2);
+  return (int64_t)a.cv.hi * a.cv.wi * imgs * a.ldb * 2 < ((int64_t)1 << 31) - 16;
 }
 
 at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtype, at::Tensor acc = at::Tensor()) {
@@ -2370,14 +2393,8 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   auto out = acc.defined() ? acc : at::empty({N, K}, like.options().dtype(out_dtype));
   if (M == 0) return acc.defined() ? out : out.zero_();
   const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
-  // one or two full rounds of 1-block/CU work; every split >= 16 K tiles
-  const int mtl = (M + 63) / 64;
-  int rounds = tiles >= 256 ? (tiles + 255) / 256 : (tiles * std::max(1, 256 / tiles) >= 192 ? 1 : 2);
-  if (g_tn_xl_rounds > 0) rounds = g_tn_xl_rounds;
-  int splits = std::max(1, std::min(256 * rounds / tiles, mtl / 16));
-  int64_t rps = ((int64_t)M + splits - 1) / splits;
-  rps = (rps + 63) / 64 * 64;
-  splits = (int)(((int64_t)M + rps - 1) / rps);
+  const int64_t rps = tn_rows_per_split(M, N, K);
+  const int splits = (int)(((int64_t)M + rps - 1) / rps);
   a.rps = rps;
   auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
   a.part = part.data_ptr<float>();
@@ -2386,6 +2403,8 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   // ping-pong one), the tap gather included when its input fits 32-bit offsets
   if (g_xl_pipe == 11 && a.cv.cin == 0)
     hipLaunchKernelGGL(gemm_tn_w4_kernel<0>, dim3(tiles * splits), dim3(256), 0, s, a);
+  else if (a.gram)
+    hipLaunchKernelGGL(gemm_tn_w4_kernel<3>, dim3(tiles * splits), dim3(256), 0, s, a);
   else if (g_xl_pipe == 11 && (64 / a.cv.wo + 1) <= 3 * a.cv.ho && tn_w4_gather_fits(a))
     hipLaunchKernelGGL(gemm_tn_w4_kernel<2>, dim3(tiles * splits), dim3(256), 0, s, a);
   else
@@ -2411,6 +2430,37 @@ at::Tensor gemm_tn_xl(const at::Tensor& A, const at::Tensor& B, at::ScalarType o
   a.B = reinterpret_cast<const bf16*>(B.data_ptr()); a.ldb = B.stride(0);
   a.M = (int)A.size(0); a.N = (int)A.size(1); a.K = (int)B.size(1);
   return run_tn_pp(a, A, out_dtype, acc_target(out, (int64_t)a.N * a.K, out_dtype, "gemm_tn_xl"));
+}
+
+// Gram G = x_s^T x_s (fp32 [Cin, Cin]) of the stride-s sample x[:, :, ::s, ::s]
+// of an NHWC input, both operands gathered in place by the 4-wave TN kernel
+// (the folded downsample BN's statistics, ops/bn_fold.py).  Cin % 256 == 0.
+at::Tensor gram_strided_xl(const at::Tensor& x, int64_t stride, int64_t ho, int64_t wo) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kBFloat16 && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast), "gram_strided_xl: x must be channels_last bf16");
+  const int64_t nb = x.size(0), cin = x.size(1), hi = x.size(2), wi = x.size(3);
+  TORCH_CHECK(cin % 256 == 0, "gram_strided_xl: Cin must be a multiple of 256");
+  TORCH_CHECK(stride >= 1 && (ho - 1) * stride < hi && (wo - 1) * stride < wi, "gram_strided_xl: bad geometry");
+  TORCH_CHECK(nb * ho * wo < (1LL << 31), "gram_strided_xl: too many pixels");
+  TnPPArgs a{};
+  a.A = a.B = reinterpret_cast<const bf16*>(x.data_ptr());
+  a.lda = a.ldb = cin;
+  a.M = (int)(nb * ho * wo); a.N = (int)cin; a.K = (int)cin;
+  a.cv.cin = (int)cin; a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
+  a.cv.stride = (int)stride; a.cv.pad = 0; a.cv.kw = 1;
+  a.gram = 1;
+  a.rps = tn_rows_per_split(a.M, a.N, a.K);
+  TORCH_CHECK((64 / wo + 1) <= 3 * ho && tn_w4_gather_fits(a), "gram_strided_xl: geometry outside the 4-wave gather");
+  return run_tn_pp(a, x, at::kFloat);
+}
+
+bool gram_strided_xl_supported(int64_t nb, int64_t cin, int64_t hi, int64_t wi, int64_t ho, int64_t wo) {
+  if (cin % 256 != 0 || (64 / std::max<int64_t>(1, wo) + 1) > 3 * ho || nb * ho * wo >= (1LL << 31)) return false;
+  TnPPArgs a{};
+  a.M = (int)(nb * ho * wo); a.N = a.K = (int)cin; a.ldb = cin;
+  a.cv.hi = (int)hi; a.cv.wi = (int)wi; a.cv.ho = (int)ho; a.cv.wo = (int)wo;
+  a.rps = tn_rows_per_split(a.M, a.N, a.K);
+  return tn_w4_gather_fits(a);
 }
 
 // Weight gradient of a kh x kw conv on the ping-pong TN kernel:

@@ -268,8 +268,14 @@ def _gram(C, inp, geom, native, n):
     if not native:
         xd = _map_rows(inp, geom, n).double()
         return xd.t() @ xd
-    from .conv1x1 import _tn_xl
+    from .conv1x1 import _tn_xl, _tn_xl_strided
     if geom:
+        s, ho, wo, hi, wi = geom
+        c = inp.shape[1]
+        if _tn_xl_strided(n * ho * wo, c, c) and C.gram_strided_xl_supported(n, c, hi, wi, ho, wo):
+            # both operands the sampled rows, gathered in place by the 4-wave TN kernel
+            _STATS["fold_ds_gram_xl"] = _STATS.get("fold_ds_gram_xl", 0) + 1
+            return C.gram_strided_xl(inp.view(n, hi, wi, c).permute(0, 3, 1, 2), s, ho, wo)
         return C.gemm_tn(inp, inp, torch.float32, b_map=geom, a_mapped=True)
     c = inp.shape[1]
     return C.gemm_tn_xl(inp, inp, torch.float32) if _tn_xl(inp.shape[0], c, c) else C.gemm_tn(inp, inp, torch.float32)

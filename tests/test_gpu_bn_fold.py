@@ -213,6 +213,7 @@ def test_bottleneck_fold_matches_unfused_model(cin, planes, stride, hw, low_rows
     assert st1["fold"] == st0["fold"] + 1 and st1["fold_ds"] == st0["fold_ds"] + 1
     if low_rows and stride != 1 and cin % 256 == 0 and nb * ho * ho >= 1024:  # strided branch: tap-gather TN
         assert st1.get("fold_ds_wgrad_xl", 0) == st0.get("fold_ds_wgrad_xl", 0) + 1
+        assert st1.get("fold_ds_gram_xl", 0) == st0.get("fold_ds_gram_xl", 0) + 1
     if stride != 1:
         assert st1["fold_ds_compact"] == st0["fold_ds_compact"] + 1  # shortcut grad parked compact
     old = bn_fold.ENABLED

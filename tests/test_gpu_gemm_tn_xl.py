@@ -65,3 +65,40 @@ def test_conv_wgrad_xl(n, cin, cout, h, k, s, tn_pipe):
     wr = torch.zeros(cout, cin, k, k, device=DEV, requires_grad=True)
     F.conv2d(x.float(), wr, None, s, p).backward(dy.float())
     torch.testing.assert_close(got, wr.grad, atol=2e-3 * (n * ho * ho) ** 0.5, rtol=1e-2)
+
+
+@pytest.mark.parametrize("n,cin,h,s", [(8, 256, 28, 2), (32, 512, 14, 2), (16, 1024, 14, 2), (8, 256, 9, 2)])
+def test_gram_strided_xl(n, cin, h, s):
+    """Gram of a strided 1x1 sample with both operands gathered in place
+    (gemm_tn_w4_kernel<3>) against the fp32 Gram of the sliced sample."""
+    C = _native.require("gram_strided_xl")
+    torch.manual_seed(2)
+    ho = (h - 1) // s + 1
+    x = torch.randn(n, cin, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    assert C.gram_strided_xl_supported(n, cin, h, h, ho, ho)
+    got = C.gram_strided_xl(x, s, ho, ho)
+    xs = x[:, :, ::s, ::s].permute(0, 2, 3, 1).reshape(-1, cin).float()
+    ref = xs.t() @ xs
+    torch.testing.assert_close(got, ref, atol=2e-3 * (n * ho * ho) ** 0.5, rtol=1e-3)
+
+
+def test_strided_gather_over_2gb_input():
+    """ResNet-50 layer-2 downsample at batch 2048: the 3.3 GB NHWC input is
+    past 32-bit offsets from its start; each M split addresses it from its
+    own first image.  Weight gradient and Gram against fp32 references on a
+    sub-sample of the output channels."""
+    C = _native.require("conv_wgrad_xl")
+    torch.manual_seed(3)
+    n, cin, h, cout = 2048, 256, 56, 256
+    x = torch.randn(n, cin, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    assert x.numel() * 2 > 2 ** 31
+    ho = h // 2
+    xs = x[:, :, ::2, ::2].permute(0, 2, 3, 1).reshape(-1, cin)
+    dy2 = torch.randn(n * ho * ho, cout, device=DEV).bfloat16()
+    got = C.conv_wgrad_xl(dy2, x, 1, 1, 2, 0, ho, ho, torch.float32)
+    ref = dy2.float().t() @ xs.float()
+    torch.testing.assert_close(got, ref, atol=3e-3 * (n * ho * ho) ** 0.5, rtol=1e-3)
+    assert C.gram_strided_xl_supported(n, cin, h, h, ho, ho)
+    g = C.gram_strided_xl(x, 2, ho, ho)
+    gr = xs.float().t() @ xs.float()
+    torch.testing.assert_close(g, gr, atol=3e-3 * (n * ho * ho) ** 0.5, rtol=1e-3)
