@@ -37,8 +37,12 @@ constexpr int kMaxCin = 1024;
 //   2  fold_sgemm_kernel: a 64 x 64-tiled fp32 GEMM reading W (bf16) and G /
 //      the coefficients directly (no fp32 copies, no concatenated operand),
 //      with the backward's epilogue writing Bm's bf16 block and ebias in place.
-// Default 1: batch-256 step 22.0 ms (1) vs 23.3 (0) vs 24.3 (2), interleaved
-// runs (profiles/raw_r4/fold_gemm_ab_r4i.md).
+//      On fp32 MFMAs since round 6 (VALU before).
+// Default 1: batch-256 step 22.0 ms (1) vs 23.3 (0) vs 24.3 (2, VALU), round 4
+// (profiles/raw_r4/fold_gemm_ab_r4i.md); round 6 with the MFMA form of 2:
+// 20.67 (1) vs 21.03 (2) at batch 256, 113.77 vs 114.16 at 2048
+// (tools/fold_gemm_ab.py): its 16-deep K stages leave the few blocks of these
+// small products waiting on load round trips (29 / 23 us per call).
 int g_fold_gemm = 1;
 
 // grid = Cout / kFwdRows.  Thread t owns columns j = t + 256 q (q < NQ) of WG rows
@@ -124,15 +128,16 @@ __global__ __launch_bounds__(kFoldThreads, 2) void fold_fwd_kernel(const bf16* _
 }
 
 // ---- fold_sgemm_kernel: C[m][n] = sum_k A(m, k) B(k, n), fp32 accumulation ----
-// 64 x 64 tile per 256-thread block, 4 x 4 outputs per thread, K staged
-// through LDS 16 at a time (register-prefetched one chunk ahead).
+// 64 x 64 tile per 256-thread block on fp32 MFMAs (four waves, 32 x 32 each),
+// K staged through LDS 16 at a time (register-prefetched one chunk ahead; 64-deep
+// stages measured slower in-step: 21.35 vs 21.03 ms at batch 256).
 //   FWD: A(m, k) = W[m][k] (bf16 [Cout, Cin]), B(k, n) = G[k][n] (fp32 [Cin, Cin]);
 //        C = WG fp32 [Cout, Cin]
 //   BWD: A(m, k) = be[k] W[k][m] for m < Cin, c[k] for m == Cin (the rows of
 //        [W^T diag(be) ; c^T], built on load from W and the coefficients),
 //        B(k, n) = W[k][n]; rows m < Cin go to Bm[m][Cout + n] (bf16), row Cin
 //        to ebias[n]  (W^T diag(be) W is symmetric: its rows are Bm's columns)
-constexpr int kSgT = 64, kSgK = 16;
+constexpr int kSgT = 64, kSgK = 16, kSgU = kSgT * kSgK / kFoldThreads;  // elements per thread per operand
 // BWD splits K (= Cout, up to 2048, while M x N = Cin^2 is small) over
 // gridDim.z: split z writes its fp32 partials to C[z] ([Cin][Cin] rows) and
 // ebias[z] ([Cin]), summed into Bm / ebias by fold_bwd_reduce_kernel.
@@ -153,68 +158,84 @@ __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __
   __shared__ __attribute__((aligned(16))) float Bs[kSgK][kSgT + 4];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int m0 = blockIdx.y * kSgT, n0 = blockIdx.x * kSgT;
-  // loaders: A as [kk][m] (4 elements per thread), B as [kk][n] (4 per thread)
-  float ra[4], rb[4];
+  // loaders: A as [kk][m], B as [kk][n] (kSgU elements each per thread)
+  float ra[kSgU], rb[kSgU];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = tid + u * kFoldThreads;  // 0..1023
+    for (int u = 0; u < kSgU; ++u) {
+      const int e = tid + u * kFoldThreads;  // 0 .. kSgT * kSgK - 1
       if constexpr (BWD) {
-        const int kk = e >> 6, m = e & 63, k = k0 + kk, mm = m0 + m;  // coalesced along m
+        const int kk = e / kSgT, m = e % kSgT, k = k0 + kk, mm = m0 + m;  // coalesced along m
         float v = 0.f;
         if (k < kend) v = mm < N ? be[k] * (float)W[(int64_t)k * N + mm] : (mm == N ? cc[k] : 0.f);
         ra[u] = v;
       } else {
-        const int m = e >> 4, kk = e & 15, k = k0 + kk, mm = m0 + m;  // 16 consecutive k per row
+        const int m = e / kSgK, kk = e % kSgK, k = k0 + kk, mm = m0 + m;  // kSgK consecutive k per row
         ra[u] = (mm < M && k < kend) ? (float)W[(int64_t)mm * K + k] : 0.f;
       }
-      const int kk = e >> 6, n = e & 63, k = k0 + kk;
+      const int kk = e / kSgT, n = e % kSgT, k = k0 + kk;
       if constexpr (BWD) rb[u] = k < kend ? (float)W[(int64_t)k * N + n0 + n] : 0.f;
       else rb[u] = k < kend ? G[(int64_t)k * N + n0 + n] : 0.f;
     }
   };
   auto store = [&] {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kSgU; ++u) {
       const int e = tid + u * kFoldThreads;
-      if constexpr (BWD) As[e >> 6][e & 63] = ra[u];
-      else As[e & 15][e >> 4] = ra[u];
-      Bs[e >> 6][e & 63] = rb[u];
+      if constexpr (BWD) As[e / kSgT][e % kSgT] = ra[u];
+      else As[e % kSgK][e / kSgK] = ra[u];
+      Bs[e / kSgT][e % kSgT] = rb[u];
     }
   };
-  float acc[4][4];
+  // fp32 MFMA (v_mfma_f32_16x16x4_f32): wave w owns the 32 x 32 quadrant
+  // (w >> 1, w & 1) as 2 x 2 16x16 blocks; per k4 step lane l feeds A(row
+  // l & 15, k l >> 4) and B(k l >> 4, col l & 15) from the LDS stage and gets
+  // back rows 4 (l >> 4) + v, column l & 15 of each block.
+  (void)tx; (void)ty;
+  const int lane = tid & 63, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
+  const int lr = lane & 15, lk = lane >> 4;
+  f32x4 acc[2][2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += kSgK) {
     __syncthreads();
     store();
     __syncthreads();
-    if (k0 + kSgK < kend) load(k0 + kSgK);  // next chunk in flight during this one's FMAs
+    if (k0 + kSgK < kend) load(k0 + kSgK);  // next chunk in flight during this one's MFMAs
 #pragma unroll
-    for (int kk = 0; kk < kSgK; ++kk) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(&As[kk][ty * 4]);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(&Bs[kk][tx * 4]);
+    for (int s4 = 0; s4 < kSgK; s4 += 4) {
+      const int kk = s4 + lk;
+      float a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 2; ++i) a[i] = As[kk][wr * 32 + i * 16 + lr];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+      for (int j = 0; j < 2; ++j) b[j] = Bs[kk][wc * 32 + j * 16 + lr];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + ty * 4 + i;
-    if (m >= M) continue;
-    const int n = n0 + tx * 4;
-    if constexpr (BWD) {
-      float* dst = m < N ? C + (int64_t)m * N + n : ebias + n;
-      *reinterpret_cast<f32x4*>(dst) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
-    } else {
-      *reinterpret_cast<f32x4*>(C + (int64_t)m * N + n) = f32x4{acc[i][0], acc[i][1], acc[i][2], acc[i][3]};
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int m = m0 + wr * 32 + i * 16 + 4 * lk + v;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wc * 32 + j * 16 + lr;
+        if constexpr (BWD) {
+          float* dst = m < N ? C + (int64_t)m * N + n : ebias + n;
+          *dst = acc[i][j][v];
+        } else {
+          C[(int64_t)m * N + n] = acc[i][j][v];
+        }
+      }
     }
-  }
 }
 
 // Forward row sums from WG = W G (fold_gemm modes 1, 2): one wave per
