@@ -109,13 +109,20 @@ __global__ __launch_bounds__(1024) void bn_reduce_partials_kernel(const float* _
     const float* pa = part + c;
     const float* pb = part + (int64_t)rb * C + c;
     int i = r0 + g;
-    for (; i + kRedGroups < r1; i += 2 * kRedGroups) {
-      const float a0 = pa[(int64_t)i * C], a1 = pa[(int64_t)(i + kRedGroups) * C];
-      const float b0 = pb[(int64_t)i * C], b1 = pb[(int64_t)(i + kRedGroups) * C];
-      a += (double)a0 + (double)a1;
-      b += (double)b0 + (double)b1;
+    // four rows (8 loads) in flight per iteration: at a micro-batch's ~100-400
+    // partial rows that is one or two round trips per thread (round 6: a
+    // 2-row loop made this ~5 us launch latency-bound)
+    for (; i + 3 * kRedGroups < r1; i += 4 * kRedGroups) {
+      float va[4], vb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        va[u] = pa[(int64_t)(i + u * kRedGroups) * C];
+        vb[u] = pb[(int64_t)(i + u * kRedGroups) * C];
+      }
+      a += ((double)va[0] + (double)va[1]) + ((double)va[2] + (double)va[3]);
+      b += ((double)vb[0] + (double)vb[1]) + ((double)vb[2] + (double)vb[3]);
     }
-    if (i < r1) {
+    for (; i < r1; i += kRedGroups) {
       a += (double)pa[(int64_t)i * C];
       b += (double)pb[(int64_t)i * C];
     }
