@@ -46,15 +46,22 @@ def set_xl_linear(on: bool) -> None:
 
 _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 # The PLAIN GEMMs -- nothing to fuse but a bias: the qkv projection forward
-# and the data gradients of qkv / proj / fc1 -- on hipBLASLt ("lib", default)
-# or gemm_xl ("xl").  The 4-wave kernel (gemm_xl PIPE 11, finding 69) ties the
+# and the data gradients of qkv / proj / fc1 -- on hipBLASLt ("lib"), gemm_xl
+# ("xl") or split ("fwd", the default, below).  The 4-wave kernel (gemm_xl PIPE 11, finding 69) ties the
 # library in isolation on the N >= 2304 shapes (1.03-1.07 PF/s,
 # tools/pipe_bench.py), but in the step the data gradients are all N = 768
 # (591 tiles = 2.3 rounds of 256 CUs; the library's 256 x 224 tile fills them
 # better) and need a W^T copy: 8.0 + 0.4 ms vs 7.4 ms per step (ViT 41.0 vs
 # 40.3 ms).  The fused-epilogue GEMMs and every weight gradient (gemm_tn_xl)
 # are ours.
-_PLAIN_LIB = __import__("os").environ.get("DMP_LINEAR_PLAIN", "lib") == "lib"
+# "fwd" (default since round 6): the qkv forward (N = 2304, bias in the
+# store) on ours, the N = 768 data gradients on the library -- ViT step
+# 36.56 / 36.67 ms (fwd) vs 36.55 / 36.61 (lib) vs 37.27 / 37.41 (xl),
+# interleaved on one box.
+_PLAIN_MODE = __import__("os").environ.get("DMP_LINEAR_PLAIN", "fwd")
+_PLAIN_LIB = _PLAIN_MODE == "lib"
+_PLAIN_FWD_XL = _PLAIN_MODE in ("xl", "fwd")
+_PLAIN_DGRAD_XL = _PLAIN_MODE == "xl"
 
 
 def _native_ok(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> bool:
@@ -104,7 +111,7 @@ def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dx = dy @ W: hipBLASLt by default (measured faster, finding 50), or
     the ping-pong MFMA GEMM with DMP_LINEAR_PLAIN=xl (B operand = W^T [in,
     out], a transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16)."""
-    if not _PLAIN_LIB and w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
+    if _PLAIN_DGRAD_XL and w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
         _STATS["xl_dgrad"] += 1
         return _native.native().gemm_xl(dy2, w.t().contiguous())
     return dy2.mm(w)
@@ -120,7 +127,7 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        if not _PLAIN_LIB and _xl_gemm_ok(x2, w.shape[0]):  # the qkv projection: bias in the MFMA GEMM's store
+        if _PLAIN_FWD_XL and _xl_gemm_ok(x2, w.shape[0]):  # the qkv projection: bias in the MFMA GEMM's store
             _STATS["xl_fwd"] += 1
             y = _native.native().gemm_xl(x2, w, "bias", bias=b)
         else:

@@ -126,12 +126,14 @@ def test_dgelu_epilogue_bias_grad(T):
     assert ((db - ref.sum(0)).norm() / ref.sum(0).norm()).item() < 1e-2
 
 
-@pytest.mark.parametrize("plain_lib", [False, True], ids=["xl", "lib"])
-def test_qkv_linear_forward_and_dgrad_on_xl(plain_lib, monkeypatch):
+@pytest.mark.parametrize("mode", ["xl", "fwd", "lib"])
+def test_qkv_linear_forward_and_dgrad_on_xl(mode, monkeypatch):
     """The qkv projection (ops.linear.linear -> _LinearFn): forward with the
     bias in gemm_xl's store and the data gradient on gemm_xl
-    (DMP_LINEAR_PLAIN=xl), or both on hipBLASLt (the default, finding 50)."""
-    monkeypatch.setattr(L, "_PLAIN_LIB", plain_lib)
+    (DMP_LINEAR_PLAIN=xl), the forward only ("fwd", the default), or both on
+    hipBLASLt ("lib")."""
+    monkeypatch.setattr(L, "_PLAIN_FWD_XL", mode in ("xl", "fwd"))
+    monkeypatch.setattr(L, "_PLAIN_DGRAD_XL", mode == "xl")
     torch.manual_seed(4)
     T, D = 8192, 768
     qkv = nn.Linear(D, 3 * D).to(DEV).bfloat16()
@@ -139,14 +141,14 @@ def test_qkv_linear_forward_and_dgrad_on_xl(plain_lib, monkeypatch):
     (xb,) = _leaves(x)
     f0, d0 = L._STATS["xl_fwd"], L._STATS["xl_dgrad"]
     y = L.linear(xb, qkv.weight, qkv.bias)
-    assert L._STATS["xl_fwd"] == f0 + (0 if plain_lib else 1)
+    assert L._STATS["xl_fwd"] == f0 + (1 if mode in ("xl", "fwd") else 0)
     xf, w, b = _leaves(x.float(), qkv.weight.float(), qkv.bias.float())
     yr = F.linear(xf, w, b)
     torch.testing.assert_close(y.float(), yr, atol=0.05, rtol=2e-2)
     g = torch.randn_like(yr)
     y.backward(g.bfloat16())
     yr.backward(g)
-    assert L._STATS["xl_dgrad"] == d0 + (0 if plain_lib else 1)
+    assert L._STATS["xl_dgrad"] == d0 + (1 if mode == "xl" else 0)
     torch.testing.assert_close(xb.grad.float(), xf.grad, atol=0.05 * (3 * D) ** 0.5 / 8, rtol=3e-2)
     err = ((qkv.weight.grad.float() - w.grad).norm() / w.grad.norm()).item()
     assert err < 2e-2, err

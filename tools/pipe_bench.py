@@ -52,6 +52,10 @@ TN_SHAPES = [  # name, M (reduction), N, K  (ResNet-50 at batch 2048: dW[Cout, C
     ("r50_l2c1_wgrad", 1605632, 128, 512),
     ("r50_l3c1_wgrad", 401408, 256, 1024),
     ("r50_l4c1_wgrad", 100352, 512, 2048),
+    ("bs256_l4_wgrad", 12544, 2048, 512),   # batch 256: below the 16k-row threshold
+    ("bs256_l4c1_wgrad", 12544, 512, 2048),
+    ("bs256_l4c2_wgrad", 12544, 512, 512),
+    ("bs256_l3_wgrad", 50176, 1024, 256),
 ]
 WGRAD_SHAPES = [  # name, N, Cin, H_in (= W), Cout, stride: 3x3 / pad 1 weight gradients at batch 2048
     ("r50_l4_3x3wg", 2048, 512, 7, 512, 1),
