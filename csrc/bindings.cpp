@@ -215,6 +215,7 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
                               int64_t k, int64_t s, int64_t p);
 // coalesced.hip
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
+void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
 void gather_slabs(const std::vector<at::Tensor>& inputs, at::Tensor& out, bool along_inner);
 std::vector<std::vector<bool>> enable_peer_access(int64_t num_devices);
@@ -482,6 +483,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- coalesced movement ----
   m.def("multi_copy", &dmp::multi_copy,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("multi_transpose", &dmp::multi_transpose, py::arg("srcs"), py::arg("dsts"),
+        "dst[i] = src[i]^T for contiguous 2-byte matrices, up to 64 per launch",
         py::call_guard<py::gil_scoped_release>());
   m.def("reduce_add_into", &dmp::reduce_add_into,
         py::call_guard<py::gil_scoped_release>());

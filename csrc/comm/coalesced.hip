@@ -79,6 +79,46 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyTable t) {
   copy_range(t.src[lo] + off, t.dst[lo] + off, min(kChunkBytes, t.nbytes[lo] - off));
 }
 
+// ---- multi_transpose: many 2-byte [R, C] -> [C, R] transposes in one launch ----
+// (the W^T operands of a step's 1x1-conv data gradients, ops/wt_cache.py).
+// One 256-thread block per 64 x 64 tile through LDS: loads coalesced along
+// the source rows, stores along the destination rows.
+constexpr int kMaxT = 64, kTT = 64;
+struct TransTable {
+  const uint16_t* src[kMaxT];
+  uint16_t* dst[kMaxT];
+  int rows[kMaxT], cols[kMaxT];
+  int first_tile[kMaxT + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void multi_transpose_kernel(const TransTable t) {
+  const int bid = blockIdx.x;
+  int lo = 0, hi = t.n - 1;  // last entry with first_tile <= bid
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.first_tile[mid] <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const int R = t.rows[lo], Cc = t.cols[lo];
+  const int ctiles = (Cc + kTT - 1) / kTT, local = bid - t.first_tile[lo];
+  const int r0 = (local / ctiles) * kTT, c0 = (local % ctiles) * kTT;
+  __shared__ uint16_t tile[kTT][kTT + 2];
+  const uint16_t* s = t.src[lo];
+  uint16_t* d = t.dst[lo];
+#pragma unroll 4
+  for (int i = threadIdx.x; i < kTT * kTT; i += 256) {
+    const int r = i / kTT, c = i % kTT;
+    if (r0 + r < R && c0 + c < Cc) tile[r][c] = s[(int64_t)(r0 + r) * Cc + c0 + c];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = threadIdx.x; i < kTT * kTT; i += 256) {
+    const int c = i / kTT, r = i % kTT;
+    if (r0 + r < R && c0 + c < Cc) d[(int64_t)(c0 + c) * R + r0 + r] = tile[r][c];
+  }
+}
+
 constexpr int kMaxReduceInputs = 16;
 struct PtrPack {
   const void* p[kMaxReduceInputs];
@@ -194,6 +234,46 @@ at::Tensor upload_table(const std::vector<T>& host, const at::Device& dev) {
 }
 
 }  // namespace
+
+// dst[i] [C, R] = src[i] [R, C]^T for 2-byte (bf16 / fp16) matrices, in as few
+// launches as the table size allows (one for up to 64 matrices).
+void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "multi_transpose: list length mismatch");
+  if (srcs.empty()) return;
+  const at::Device dev = dsts[0].device();
+  auto stream = at::hip::getCurrentHIPStream(dev.index());
+  TransTable t{};
+  int tiles = 0;
+  auto flush = [&]() {
+    if (t.n == 0) return;
+    t.first_tile[t.n] = tiles;
+    hipLaunchKernelGGL(multi_transpose_kernel, dim3((unsigned)tiles), dim3(256), 0, stream, t);
+    DMP_HIP_CHECK(hipGetLastError());
+    t = TransTable{};
+    tiles = 0;
+  };
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const auto& s = srcs[i];
+    const auto& d = dsts[i];
+    TORCH_CHECK(s.is_cuda() && d.device() == dev && s.device() == dev, "multi_transpose: one device");
+    TORCH_CHECK(s.dim() == 2 && d.dim() == 2 && s.is_contiguous() && d.is_contiguous() && s.element_size() == 2 &&
+                    d.scalar_type() == s.scalar_type() && d.size(0) == s.size(1) && d.size(1) == s.size(0),
+                "multi_transpose: contiguous 2-byte [R, C] -> [C, R] pairs");
+    const int64_t R = s.size(0), C = s.size(1);
+    if (R == 0 || C == 0) continue;
+    TORCH_CHECK(R < (1 << 30) && C < (1 << 30), "multi_transpose: matrix too large");
+    const int64_t nt = ((R + kTT - 1) / kTT) * ((C + kTT - 1) / kTT);
+    if (t.n == kMaxT || tiles + nt >= (1LL << 31) - 1) flush();
+    t.src[t.n] = static_cast<const uint16_t*>(s.data_ptr());
+    t.dst[t.n] = static_cast<uint16_t*>(d.data_ptr());
+    t.rows[t.n] = (int)R;
+    t.cols[t.n] = (int)C;
+    t.first_tile[t.n] = tiles;
+    tiles += (int)nt;
+    ++t.n;
+  }
+  flush();
+}
 
 // Copy byte ranges src[i] -> dst[i] (contiguous tensors, equal nbytes) in one launch on
 // the current stream of dst's device.  srcs may live on a peer device (xGMI read).

@@ -156,7 +156,8 @@ class _BNReLUConv1x1Fn(torch.autograd.Function):
         x2 = _rows(x)
         dy2 = _rows(dy.contiguous(memory_format=torch.channels_last).to(x.dtype))
         w2 = conv_w.reshape(cout, cin)
-        g2, _ = C.gemm_nt(dy2, w2.t().contiguous())            # d(relu(bn(x)))
+        from .wt_cache import transposed
+        g2, _ = C.gemm_nt(dy2, transposed(conv_w))            # d(relu(bn(x)))
         dw = C.gemm_tn(dy2, x2, conv_w.dtype, pro_scale=scale, pro_shift=shift).view(cout, cin, 1, 1)
         if conv_w.is_contiguous(memory_format=torch.channels_last):
             dw = dw.contiguous(memory_format=torch.channels_last)

@@ -113,7 +113,8 @@ def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     out], a transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16)."""
     if _PLAIN_DGRAD_XL and w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
         _STATS["xl_dgrad"] += 1
-        return _native.native().gemm_xl(dy2, w.t().contiguous())
+        from .wt_cache import transposed
+        return _native.native().gemm_xl(dy2, transposed(w))
     return dy2.mm(w)
 
 
@@ -253,7 +254,8 @@ class _MLPResidualFn(torch.autograd.Function):
         dw2 = _wgrad(dy2, a, w2)
         # dh = bf16(bf16(dy @ W2) * gelu'(h)): B operand is W2^T [hidden, dim]
         # and fc1's bias gradient (column sums of dh) from the same epilogue
-        dh, db1 = C.gemm_xl_dgelu_bgrad(dy2, w2.t().contiguous(), h)
+        from .wt_cache import transposed
+        dh, db1 = C.gemm_xl_dgelu_bgrad(dy2, transposed(w2), h)
         db1 = db1.to(w1.dtype)
         dw1 = _wgrad(dh, x2, w1)
         dx = _dgrad(dh, w1)

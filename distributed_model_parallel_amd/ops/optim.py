@@ -18,7 +18,7 @@ from typing import List, Optional
 import torch
 
 from .. import _native
-from . import wgrad_stream
+from . import wgrad_stream, wt_cache
 
 
 
@@ -92,6 +92,7 @@ class FlatSGD(torch.optim.Optimizer):
             else:
                 _sgd_reference(master, st["momentum"], gflat, pflat, g, first)
         self._steps += 1
+        wt_cache.after_optimizer_step()  # the updated weights' W^T, one launch (ops/wt_cache.py)
         return loss
 
     def zero_grad(self, set_to_none: bool = False):
@@ -226,6 +227,7 @@ class MasterSGD(torch.optim.Optimizer):
             else:
                 _sgd_reference(master, st["momentum"], gflat, pflat, g, first)
         self._steps += 1
+        wt_cache.after_optimizer_step()  # the updated weights' W^T, one launch (ops/wt_cache.py)
         return loss
 
     def zero_grad(self, set_to_none: bool = False):

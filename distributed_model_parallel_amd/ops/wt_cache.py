@@ -1,32 +1,88 @@
-"""Transposed weights shared by the micro-batches of one pipeline step.
+"""Transposed weights (W^T) of the 1x1-conv data gradients, computed once per
+weight update instead of once per backward use.
 
 The data-gradient GEMM of a 1x1 conv reads W^T ([Cin, Cout], K-contiguous
 rows for the MFMA kernel), so every backward ran ``w.t().contiguous()``: one
-copy kernel per conv per micro-batch (MobileNetV2: ~35 per 64-image
-micro-batch, ~280 per 8-micro-batch step).  The weights do not change between
-the micro-batches of a step, so a :class:`WTCache` holds one persistent W^T
-buffer per registered weight, refreshed once per step (:meth:`refresh`, before
-the first micro-batch), and the ops read it through :func:`transposed` while
-the cache is active.  The buffers keep their storage across refreshes, so
-captured stage graphs (parallel/pipeline.py ``_StageGraphs``) read them too.
+copy kernel per conv per backward (ResNet-50: ~50 per step; a MobileNetV2
+pipeline micro-batch: ~35).  Two caches serve those operands:
 
-Keyed by the weight's storage address and shape: a re-homed parameter (e.g.
-an optimizer flattening parameters) misses and takes the plain copy until
-:meth:`refresh` re-registers it.
+* **Optimizer-driven (global).** A weight whose W^T a backward needed is
+  registered (leaf parameters only).  After every step of our optimizers
+  (``ops/optim.py`` FlatSGD / MasterSGD) :func:`after_optimizer_step`
+  re-transposes every registered weight in ONE launch (``_C.multi_transpose``)
+  and stamps the entries with a generation and the weight's version counter.
+  A backward then takes the buffer iff it was refreshed after the latest
+  optimizer step and the weight has not been modified in place since (its
+  ``_version``).  Our optimizers write through raw pointers, so they bump no
+  version; any other in-place change does, and the op falls back to a fresh
+  copy.  Buffers keep their storage, so captured steps (bench.py --graph)
+  read them and the captured optimizer step refreshes them on every replay.
+* **Per-step (pipeline).** :class:`WTCache` holds buffers for a stage's
+  weights, refreshed by the pipeline before a step's first micro-batch.
+  This covers any optimizer, since the pipeline itself refreshes.
+
+Keyed by storage address and shape: a re-homed parameter misses until it is
+registered again.
 """
 from __future__ import annotations
 
 import contextlib
-from typing import Dict, Iterable, Iterator, Optional, Tuple
+import weakref
+from typing import Dict, Iterable, Iterator, List, Optional, Tuple
 
 import torch
 
-_ACTIVE: list = [None]  # the WTCache consulted by transposed(), or None
-_STATS = {"hit": 0, "miss": 0}
+_ACTIVE: list = [None]  # the per-step WTCache consulted first, or None
+_STATS = {"hit": 0, "miss": 0, "refresh_launches": 0}
+_GEN = [0]  # optimizer step generation
+
+# key -> [weakref(weight), buf, generation, version]
+_GLOBAL: Dict[Tuple[int, Tuple[int, ...]], list] = {}
+_ENABLED = [True]
 
 
 def _key(w: torch.Tensor) -> Tuple[int, Tuple[int, ...]]:
     return w.data_ptr(), tuple(w.shape)
+
+
+def _native_transpose(srcs: List[torch.Tensor], dsts: List[torch.Tensor]) -> None:
+    from .. import _native
+    C = _native.native()
+    if C is not None and srcs and srcs[0].is_cuda and hasattr(C, "multi_transpose") \
+            and all(s.element_size() == 2 for s in srcs):
+        C.multi_transpose(srcs, dsts)
+        _STATS["refresh_launches"] += 1
+        return
+    for s, d in zip(srcs, dsts):
+        d.copy_(s.t())
+
+
+def set_enabled(on: bool) -> None:
+    """Turn the optimizer-driven cache on / off (tests, A/B runs)."""
+    _ENABLED[0] = bool(on)
+    if not on:
+        _GLOBAL.clear()
+
+
+def after_optimizer_step() -> None:
+    """Called by our optimizers after they updated the parameters: re-transpose
+    every registered live weight in one launch and validate the entries."""
+    _GEN[0] += 1
+    if not _GLOBAL:
+        return
+    srcs, dsts, live = [], [], {}
+    with torch.no_grad():
+        for k, e in _GLOBAL.items():
+            w = e[0]()
+            if w is None or _key(w) != k:
+                continue  # freed or re-homed: drop
+            srcs.append(w.detach().reshape(w.shape[0], -1))
+            dsts.append(e[1])
+            e[2], e[3] = _GEN[0], w._version
+            live[k] = e
+        _native_transpose(srcs, dsts)
+    _GLOBAL.clear()
+    _GLOBAL.update(live)
 
 
 class WTCache:
@@ -42,8 +98,10 @@ class WTCache:
         self._params.append(p)
 
     def refresh(self) -> None:
-        """Re-register moved weights and copy every W^T (once per step)."""
+        """Re-register moved weights and transpose every W (once per step, one
+        launch on the GPU)."""
         live = {}
+        srcs, dsts = [], []
         with torch.no_grad():
             for p in self._params:
                 k = _key(p)
@@ -51,8 +109,10 @@ class WTCache:
                 buf = self._bufs.get(k)
                 if buf is None or buf.dtype != p.dtype or buf.device != p.device:
                     buf = torch.empty(w2.shape[1], w2.shape[0], dtype=p.dtype, device=p.device)
-                buf.copy_(w2.t())
+                srcs.append(w2)
+                dsts.append(buf)
                 live[k] = buf
+            _native_transpose(srcs, dsts)
         self._bufs = live
 
     def get(self, w: torch.Tensor) -> Optional[torch.Tensor]:
@@ -72,14 +132,25 @@ class WTCache:
 
 
 def transposed(w: torch.Tensor) -> torch.Tensor:
-    """``w.reshape(out, -1).t().contiguous()``, from the active cache when it
-    holds this weight."""
+    """``w.reshape(out, -1).t().contiguous()``, from a cache when one holds a
+    current copy of this weight."""
     c = _ACTIVE[0]
     if c is not None:
         buf = c.get(w)
         if buf is not None:
             _STATS["hit"] += 1
             return buf
+    if _ENABLED[0]:
+        k = _key(w)
+        e = _GLOBAL.get(k)
+        if e is not None and e[2] == _GEN[0] and e[3] == w._version and e[0]() is not None:
+            _STATS["hit"] += 1
+            return e[1]
+        if e is None and w.is_leaf and w.requires_grad and w.element_size() == 2:
+            # next optimizer step keeps a transposed copy of this weight
+            w2 = w.detach().reshape(w.shape[0], -1)
+            _GLOBAL[k] = [weakref.ref(w), torch.empty(w2.shape[1], w2.shape[0], dtype=w.dtype, device=w.device),
+                          -1, -1]
     _STATS["miss"] += 1
     return w.reshape(w.shape[0], -1).t().contiguous()
 

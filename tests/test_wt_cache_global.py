@@ -1,0 +1,48 @@
+"""ops/wt_cache.py optimizer-driven W^T cache (CPU: the validity rules)."""
+import torch
+
+from distributed_model_parallel_amd.ops import wt_cache
+
+
+def test_global_cache_tracks_optimizer_steps_and_versions():
+    wt_cache.set_enabled(True)
+    w = torch.nn.Parameter(torch.randn(24, 16, 1, 1).bfloat16())
+    s0 = wt_cache.stats()
+    t0 = wt_cache.transposed(w)  # miss: registers the weight
+    assert torch.equal(t0, w.detach().reshape(24, 16).t())
+    assert wt_cache.stats()["miss"] == s0["miss"] + 1
+    assert wt_cache.stats()["hit"] == s0["hit"]
+    with torch.no_grad():
+        w.data.mul_(2.0)  # an optimizer writing through raw pointers (no version bump)
+    wt_cache.after_optimizer_step()  # ... then refreshing the cache
+    t1 = wt_cache.transposed(w)
+    assert wt_cache.stats()["hit"] == s0["hit"] + 1
+    assert torch.equal(t1, w.detach().reshape(24, 16).t())
+    with torch.no_grad():
+        w.add_(1.0)  # an in-place change the cache did not see: version bump -> miss
+    t2 = wt_cache.transposed(w)
+    assert torch.equal(t2, w.detach().reshape(24, 16).t())
+    assert wt_cache.stats()["hit"] == s0["hit"] + 1
+    wt_cache.after_optimizer_step()
+    assert torch.equal(wt_cache.transposed(w), w.detach().reshape(24, 16).t())
+    assert wt_cache.stats()["hit"] == s0["hit"] + 2
+    # a non-leaf (e.g. a DataParallel replica's broadcast weight) is never registered
+    v = (w * 1.0)
+    n0 = len(wt_cache._GLOBAL)
+    wt_cache.transposed(v)
+    assert len(wt_cache._GLOBAL) == n0
+
+
+def test_global_cache_drops_freed_weights():
+    import gc
+    wt_cache.set_enabled(True)
+    wt_cache.after_optimizer_step()  # prune whatever earlier tests left
+
+    def register():
+        w = torch.nn.Parameter(torch.randn(8, 40, 1, 1).bfloat16())
+        wt_cache.transposed(w)
+        return len(wt_cache._GLOBAL)
+    n = register()
+    gc.collect()
+    wt_cache.after_optimizer_step()
+    assert len(wt_cache._GLOBAL) == n - 1
