@@ -92,7 +92,8 @@ class FlatSGD(torch.optim.Optimizer):
             else:
                 _sgd_reference(master, st["momentum"], gflat, pflat, g, first)
         self._steps += 1
-        wt_cache.after_optimizer_step()  # the updated weights' W^T, one launch (ops/wt_cache.py)
+        # the updated weights' W^T, one launch (ops/wt_cache.py)
+        wt_cache.after_optimizer_step(p for grp in self.param_groups for p in grp["params"])
         return loss
 
     def zero_grad(self, set_to_none: bool = False):
@@ -227,7 +228,8 @@ class MasterSGD(torch.optim.Optimizer):
             else:
                 _sgd_reference(master, st["momentum"], gflat, pflat, g, first)
         self._steps += 1
-        wt_cache.after_optimizer_step()  # the updated weights' W^T, one launch (ops/wt_cache.py)
+        # the updated weights' W^T, one launch (ops/wt_cache.py)
+        wt_cache.after_optimizer_step(p for grp in self.param_groups for p in grp["params"])
         return loss
 
     def zero_grad(self, set_to_none: bool = False):

@@ -7,10 +7,12 @@ copy kernel per conv per backward (ResNet-50: ~50 per step; a MobileNetV2
 pipeline micro-batch: ~35).  Two caches serve those operands:
 
 * **Optimizer-driven (global).** A weight whose W^T a backward needed is
-  registered (leaf parameters only).  After every step of our optimizers
-  (``ops/optim.py`` FlatSGD / MasterSGD) :func:`after_optimizer_step`
-  re-transposes every registered weight in ONE launch (``_C.multi_transpose``)
-  and stamps the entries with a generation and the weight's version counter.
+  noted.  After every step of our optimizers (``ops/optim.py`` FlatSGD /
+  MasterSGD) :func:`after_optimizer_step` re-transposes every noted weight
+  THAT OPTIMIZER OWNS in ONE launch (``_C.multi_transpose``) and stamps the
+  entries with a generation and the weight's version counter.  Weights no
+  optimizer of ours updates (e.g. captured DataParallel replicas, refreshed
+  by raw copies) never get an entry.
   A backward then takes the buffer iff it was refreshed after the latest
   optimizer step and the weight has not been modified in place since (its
   ``_version``).  Our optimizers write through raw pointers, so they bump no
@@ -38,6 +40,7 @@ _GEN = [0]  # optimizer step generation
 
 # key -> [weakref(weight), buf, generation, version]
 _GLOBAL: Dict[Tuple[int, Tuple[int, ...]], list] = {}
+_WANTED: set = set()  # keys a backward asked for that have no entry yet
 _ENABLED = [True]
 
 
@@ -62,27 +65,36 @@ def set_enabled(on: bool) -> None:
     _ENABLED[0] = bool(on)
     if not on:
         _GLOBAL.clear()
+        _WANTED.clear()
 
 
-def after_optimizer_step() -> None:
-    """Called by our optimizers after they updated the parameters: re-transpose
-    every registered live weight in one launch and validate the entries."""
+def after_optimizer_step(params: Iterable[torch.Tensor] = ()) -> None:
+    """Called by our optimizers after they updated ``params``: re-transpose
+    every wanted weight among them in one launch and validate its entry;
+    entries of freed or re-homed weights are dropped."""
     _GEN[0] += 1
-    if not _GLOBAL:
+    if not _ENABLED[0] or not (_GLOBAL or _WANTED):
         return
-    srcs, dsts, live = [], [], {}
+    srcs, dsts = [], []
     with torch.no_grad():
-        for k, e in _GLOBAL.items():
-            w = e[0]()
-            if w is None or _key(w) != k:
-                continue  # freed or re-homed: drop
-            srcs.append(w.detach().reshape(w.shape[0], -1))
+        for k in [k for k, e in _GLOBAL.items() if e[0]() is None or _key(e[0]()) != k]:
+            del _GLOBAL[k]
+        for p in params:
+            if p.dim() not in (2, 4) or p.element_size() != 2:
+                continue
+            k = _key(p)
+            e = _GLOBAL.get(k)
+            if e is None and k in _WANTED:
+                w2 = p.detach().reshape(p.shape[0], -1)
+                e = _GLOBAL[k] = [weakref.ref(p), torch.empty(w2.shape[1], w2.shape[0], dtype=p.dtype,
+                                                              device=p.device), -1, -1]
+            if e is None or e[0]() is not p:
+                continue
+            srcs.append(p.detach().reshape(p.shape[0], -1))
             dsts.append(e[1])
-            e[2], e[3] = _GEN[0], w._version
-            live[k] = e
+            e[2], e[3] = _GEN[0], p._version
+        _WANTED.clear()
         _native_transpose(srcs, dsts)
-    _GLOBAL.clear()
-    _GLOBAL.update(live)
 
 
 class WTCache:
@@ -147,10 +159,7 @@ def transposed(w: torch.Tensor) -> torch.Tensor:
             _STATS["hit"] += 1
             return e[1]
         if e is None and w.is_leaf and w.requires_grad and w.element_size() == 2:
-            # next optimizer step keeps a transposed copy of this weight
-            w2 = w.detach().reshape(w.shape[0], -1)
-            _GLOBAL[k] = [weakref.ref(w), torch.empty(w2.shape[1], w2.shape[0], dtype=w.dtype, device=w.device),
-                          -1, -1]
+            _WANTED.add(k)  # the owning optimizer's next step keeps a transposed copy
     _STATS["miss"] += 1
     return w.reshape(w.shape[0], -1).t().contiguous()
 

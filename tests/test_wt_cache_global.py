@@ -14,7 +14,7 @@ def test_global_cache_tracks_optimizer_steps_and_versions():
     assert wt_cache.stats()["hit"] == s0["hit"]
     with torch.no_grad():
         w.data.mul_(2.0)  # an optimizer writing through raw pointers (no version bump)
-    wt_cache.after_optimizer_step()  # ... then refreshing the cache
+    wt_cache.after_optimizer_step([w])  # ... then refreshing the cache
     t1 = wt_cache.transposed(w)
     assert wt_cache.stats()["hit"] == s0["hit"] + 1
     assert torch.equal(t1, w.detach().reshape(24, 16).t())
@@ -23,14 +23,21 @@ def test_global_cache_tracks_optimizer_steps_and_versions():
     t2 = wt_cache.transposed(w)
     assert torch.equal(t2, w.detach().reshape(24, 16).t())
     assert wt_cache.stats()["hit"] == s0["hit"] + 1
-    wt_cache.after_optimizer_step()
+    wt_cache.after_optimizer_step([w])
     assert torch.equal(wt_cache.transposed(w), w.detach().reshape(24, 16).t())
     assert wt_cache.stats()["hit"] == s0["hit"] + 2
     # a non-leaf (e.g. a DataParallel replica's broadcast weight) is never registered
     v = (w * 1.0)
-    n0 = len(wt_cache._GLOBAL)
+    n0 = len(wt_cache._WANTED)
     wt_cache.transposed(v)
-    assert len(wt_cache._GLOBAL) == n0
+    assert len(wt_cache._WANTED) == n0
+    # a weight no optimizer of ours owns (refreshed elsewhere) never gets an entry
+    u = torch.nn.Parameter(torch.randn(16, 32).bfloat16())
+    wt_cache.transposed(u)
+    wt_cache.after_optimizer_step([w])
+    h = wt_cache.stats()["hit"]
+    wt_cache.transposed(u)
+    assert wt_cache.stats()["hit"] == h
 
 
 def test_global_cache_drops_freed_weights():
@@ -41,6 +48,7 @@ def test_global_cache_drops_freed_weights():
     def register():
         w = torch.nn.Parameter(torch.randn(8, 40, 1, 1).bfloat16())
         wt_cache.transposed(w)
+        wt_cache.after_optimizer_step([w])
         return len(wt_cache._GLOBAL)
     n = register()
     gc.collect()
