@@ -219,12 +219,15 @@ __host__ __device__ constexpr int xl_waves(int pipe) { return pipe == 11 ? 4 : 8
 template <int BN, int PIPE>
 using XlAcc = f32x4[8][xl_waves(PIPE) == 4 ? BN / 32 : BN / 64];
 
-template <int BN, int EPI, int PIPE, int LDS>
+// WMB (PIPE 11): 16-row blocks per wave actually computed (7: 224-row tile,
+// wave row 1 starts at row 112; acc[7][*] unused)
+template <int BN, int EPI, int PIPE, int LDS, int WMB = 8>
 __device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& acc, char* smem, int m0, int n0,
                                             int mt, int mtiles, int tbm = XBM) {
   constexpr int NW = xl_waves(PIPE), XTHREADS = NW * 64;
-  constexpr int WTM = 128, WTN = NW == 4 ? BN / 2 : BN / 4;
+  constexpr int WTM = 16 * WMB, WTN = NW == 4 ? BN / 2 : BN / 4;
   constexpr int MI = WTM / 16, NI = WTN / 16;
+  static_assert(WMB == 8 || PIPE == 11, "trimmed wave tiles: 4-wave kernel only");
   constexpr int CT_STRIDE = BN + 8;
   constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
   // rows of this tile: [m0, min(M, m0 + tbm)); a trimmed tile's staged rows
@@ -981,8 +984,13 @@ __device__ __forceinline__ int w4_swz(int c, int row) { return c ^ ((row >> 1) &
 // 0 = plain A, by buffer_load ... lds with one 32-bit lane offset per piece
 // (operands < 2 GB); 1 = plain A with the second source A2 from column K1;
 // 2 = conv tap gather (global_load_lds, zero taps read g_zero_row)
-template <int EPI, int SRC>
+// MB: 16-row MFMA blocks per wave (8: 256-row tiles; 7: 224-row tiles, which
+// fill the last 1-block/CU round of grids such as ViT's N = 768 GEMMs, 591 ->
+// 678 tiles in the same three rounds of 7/8 the work each: pick_bm)
+template <int EPI, int SRC, int MB = 8>
 __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
+  static_assert(MB == 8 || MB == 7, "4-wave tile rows: 256 or 224");
+  constexpr int TBM = 32 * MB, NRD = 8 + MB;  // tile rows; fragment reads per k-half
   constexpr int OPB = 256 * 128, BUF = 2 * OPB;  // one operand's K tile, one buffer (A | B)
   constexpr int EPI_LDS = XBM * (256 + 8) * 2;
   constexpr int LDS = 2 * BUF > EPI_LDS ? 2 * BUF : EPI_LDS;
@@ -993,12 +1001,14 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
-  const int mtiles = (M + XBM - 1) / XBM, ntiles = (N + 255) / 256;
+  const int mtiles = (M + TBM - 1) / TBM, ntiles = (N + 255) / 256;
   int mt, nt;
   tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
-  const int m0 = mt * XBM, n0 = nt * 256;
+  const int m0 = mt * TBM, n0 = nt * 256;
   const int ktiles = K / XBK;
 
+  // (a 224-row tile still stages 256 A rows: the last 32 are the next tile's,
+  // read but never multiplied)
   // copy c (0..15) of a K tile: operand c >> 3 (A, B), 8-row piece
   // 8 wave + (c & 7); lane L: row 8 piece + (L >> 3), stored chunk L & 7,
   // logical chunk w4_swz(L & 7, row)
@@ -1052,10 +1062,10 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
 
   const int lrow = lane & 15, lk = lane >> 4;
   const int fo0 = lrow * 128 + (w4_swz(lk, lrow) << 4), fo1 = lrow * 128 + (w4_swz(4 + lk, lrow) << 4);
-  const int aoff = wr * 128 * 128, boff = OPB + wc * 128 * 128;
+  const int aoff = wr * (16 * MB) * 128, boff = OPB + wc * 128 * 128;
   bf16x8 ra[2][8], rb[2][8];
-  // fragment read r (0..15) in the order the MFMAs consume them: A block 0,
-  // B blocks 0..7, A blocks 1..7
+  // fragment read r (0..NRD-1) in the order the MFMAs consume them: A block 0,
+  // B blocks 0..7, A blocks 1..MB-1
   auto rd = [&](auto hc, int buf, int r) {
     constexpr int H = decltype(hc)::value;
     const bool isb = r >= 1 && r <= 8;
@@ -1078,21 +1088,25 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
     constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
     const int buf = kt & 1;
 #pragma unroll
-    for (int n = 0; n < 64; ++n) {
+    for (int n = 0; n < 8 * MB; ++n) {
       w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
       if ((n & 3) == 0) rd(I1{}, buf, n >> 2);
+      if (MB == 7 && n == 8 * MB - 2) rd(I1{}, buf, NRD - 1);  // 15 reads over 56 MFMAs
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     barrier();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int n = 0; n < 64; ++n) {
+    for (int n = 0; n < 8 * MB; ++n) {
       w4_mfma(acc[n >> 3][n & 7], rb[1][n & 7], ra[1][n >> 3]);
-      if constexpr (STAGE)
+      if constexpr (STAGE) {
         if ((n & 3) == 0) dma(kt + 2, buf, n >> 2);
+        // 56 MFMAs: the last two of the 16 copies go between the last ones
+        if (MB == 7 && (n & 3) == 2 && n >= 8 * MB - 6) dma(kt + 2, buf, 14 + ((n - (8 * MB - 6)) >> 2));
+      }
       if constexpr (READ)
-        if ((n & 1) == 1 && n < 32) rd(I0{}, buf ^ 1, n >> 1);
+        if ((n & 1) == 1 && (n >> 1) < NRD) rd(I0{}, buf ^ 1, n >> 1);
     }
   };
 #pragma unroll
@@ -1107,7 +1121,7 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   barrier();
   xl_mark(p, 1);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) rd(I0{}, 0, r);
+  for (int r = 0; r < NRD; ++r) rd(I0{}, 0, r);
   int kt = 0;
   for (; kt + 2 < ktiles; ++kt) iter(std::true_type{}, std::true_type{}, kt);
   if (kt + 1 < ktiles) iter(std::false_type{}, std::true_type{}, kt++);
@@ -1118,7 +1132,7 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   // every copy has landed (the waits above are inline asm the compiler cannot
   // see): say so with a wait it does see (finding 66)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  xl_epilogue<256, EPI, 11, LDS>(p, acc, smem, m0, n0, mt, mtiles);
+  xl_epilogue<256, EPI, 11, LDS, MB>(p, acc, smem, m0, n0, mt, mtiles, TBM);
   if (p.tdbg) {
     __syncthreads();
     xl_mark(p, 3);
@@ -1848,7 +1862,25 @@ int num_cus() {
 // trimmed tile cost their staging only.  0 = auto, -1 = always 256, else forced (A/B).
 int g_xl_bm = 0;
 
-int pick_bm(int64_t M, int64_t N, int64_t K) {
+__host__ __device__ constexpr bool w4_epi(int e);
+
+// 4-wave kernel (PIPE 11): 256- or 224-row tiles (MB = 8 / 7 blocks per
+// wave), whichever needs fewer rounds x rows of 1-block/CU work: ViT's N = 768
+// GEMMs 591 tiles (3 rounds x 256) -> 678 (3 x 224); ResNet-50 layer-3 3x3s
+// 1568 (7 x 256) -> 1792 (7 x 224), layer-4 784 (4 x 256) -> 896 (4 x 224).
+int pick_bm_w4(int64_t M, int64_t N) {
+  if (g_xl_bm == 224 || g_xl_bm == 256) return g_xl_bm;
+  if (g_xl_bm < 0) return 256;
+  const int64_t cus = num_cus(), nt = (N + 255) / 256;
+  auto cost = [&](int64_t bm) { return ((M + bm - 1) / bm * nt + cus - 1) / cus * bm; };
+  // a 12.5 % cut (whole rounds of 7/8 the rows) only: a tile's fixed cost
+  // (prologue, epilogue) does not shrink with its rows, and ViT's fc1 forward
+  // (N = 3072, K = 768: 10 rounds x 256 vs 11 x 224) measured 0.330 vs 0.339 ms
+  return cost(224) * 100 <= cost(256) * 90 ? 224 : 256;
+}
+
+int pick_bm(int64_t M, int64_t N, int64_t K, int epi) {
+  if (g_xl_pipe == 11 && w4_epi(epi)) return pick_bm_w4(M, N);
   if (g_xl_pipe != 10) return 256;
   if (g_xl_bm > 0) return g_xl_bm;
   if (g_xl_bm < 0 || K < 768) return 256;
@@ -1894,14 +1926,23 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
   if constexpr (w4_epi(EPI)) {
   if (g_xl_pipe == 11 && w4_ok(a)) {
     XlArgs w = a;
-    w.bm = 256;
-    const int wblocks = ((w.M + 255) / 256) * ((w.N + 255) / 256);
-    if (w.cv.cin > 0)
+    // a.bm came from pick_bm (the moments partials are sized by it): 224 or 256
+    w.bm = a.bm == 224 ? 224 : 256;
+    const int wblocks = ((w.M + w.bm - 1) / w.bm) * ((w.N + 255) / 256);
+    if (w.bm == 224) {
+      if (w.cv.cin > 0)
+        hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 2, 7>), dim3(wblocks), dim3(256), 0, s, w);
+      else if (w.A2)
+        hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 1, 7>), dim3(wblocks), dim3(256), 0, s, w);
+      else
+        hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 0, 7>), dim3(wblocks), dim3(256), 0, s, w);
+    } else if (w.cv.cin > 0) {
       hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 2>), dim3(wblocks), dim3(256), 0, s, w);
-    else if (w.A2)
+    } else if (w.A2) {
       hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 1>), dim3(wblocks), dim3(256), 0, s, w);
-    else
+    } else {
       hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 0>), dim3(wblocks), dim3(256), 0, s, w);
+    }
     return;
   }
   }
@@ -2053,7 +2094,7 @@ at::Tensor gemm_xl(const at::Tensor& A, const at::Tensor& B, const std::string& 
   }
   const int bn = pick_bn((int)M, (int)N);
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
-  a.bm = bn == 256 ? pick_bm(M, N, K) : 256;
+  a.bm = bn == 256 ? pick_bm(M, N, K, epi) : 256;
   hipStream_t s = at::hip::getCurrentHIPStream();
   switch (epi) {
     case XL_STORE: dispatch_bn<XL_STORE>(a, bn, s); break;
@@ -2086,7 +2127,7 @@ std::vector<at::Tensor> gemm_xl_dgelu_bgrad(const at::Tensor& A, const at::Tenso
   a.aux = const_cast<bf16*>(reinterpret_cast<const bf16*>(aux.data_ptr())); a.ldaux = aux.stride(0);
   a.group_m = g_xl_group_m > 0 ? g_xl_group_m : 4;
   const int bn = pick_bn((int)M, (int)N);
-  a.bm = bn == 256 ? pick_bm(M, N, K) : 256;
+  a.bm = bn == 256 ? pick_bm(M, N, K, XL_DGELU) : 256;
   const int mtiles = (int)((M + a.bm - 1) / a.bm);
   const bool fused = true;
   at::Tensor part;
@@ -2191,7 +2232,7 @@ std::vector<at::Tensor> xl_conv_run(XlArgs a, const at::Tensor& A, const std::st
   const int bn = conv ? 256 : pick_bn((int)M, (int)N);
   // the two-blocks-per-CU route (dispatch_bn -> use_x2) keeps 256-row tiles
   const bool x2 = !conv && epi >= XL_MOMENTS && use_x2(a);
-  a.bm = (bn == 256 && !x2) ? pick_bm(M, N, a.K) : 256;
+  a.bm = (bn == 256 && !x2) ? pick_bm(M, N, a.K, epi) : 256;
   at::Tensor sums, part;
   const int mtiles = (int)((M + a.bm - 1) / a.bm);
   const bool moments = epi == XL_MOMENTS || is_bnbwd(epi);
@@ -2351,7 +2392,7 @@ at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>&
     a.cv.stride = 1; a.cv.pad = 0; a.cv.kw = tx;
     a.omap.s = 2; a.omap.ho = (int)ho; a.omap.wo = (int)wo; a.omap.hi = (int)hi; a.omap.wi = (int)wi;
     a.omap.oy = py; a.omap.ox = px;
-    a.bm = pick_bm(a.M, a.N, a.K);
+    a.bm = pick_bm(a.M, a.N, a.K, XL_STORE);
     const int blocks = (int)((a.M + a.bm - 1) / a.bm) * (int)(cin / 256);
     launch_pp256<XL_STORE>(a, blocks, s);
   }
@@ -2518,7 +2559,7 @@ void set_gemm_xl_bm(int bm) {
               "bm: 0 (auto), -1 (always 256) or 192..256 in steps of 16");
   g_xl_bm = bm;
 }
-int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K) { return pick_bm(M, N, K); }
+int get_gemm_xl_bm(int64_t M, int64_t N, int64_t K) { return pick_bm(M, N, K, XL_STORE); }
 
 void set_gemm_xl_bn(int bn, int pipe, int group_m) {
   if (pipe < 0) pipe = kXlPipeDefault;

@@ -162,3 +162,95 @@ def test_conv_xl_dgrad_s2_row_map(C, bm):
     d0 = run(C, -1, lambda: C.conv_xl_dgrad_s2(dy, wph, hi, hi))
     d1 = run(C, bm, lambda: C.conv_xl_dgrad_s2(dy, wph, hi, hi))
     assert torch.equal(d0, d1)
+
+
+# ---- 4-wave kernel (PIPE 11, the default): 224-row tiles (7 MFMA blocks per
+# wave, gemm_xl_w4_kernel<EPI, SRC, 7>) against its 256-row tiles, bitwise.
+
+@pytest.fixture
+def C4():
+    c = _native.require("gemm_xl bm tests")
+    c.set_gemm_xl_bn(256, 11)
+    yield c
+    c.set_gemm_xl_bm(0)
+    c.set_gemm_xl_bn(0)
+
+
+def test_pick_bm_w4_auto(C4):
+    C4.set_gemm_xl_bm(0)
+    if torch.cuda.get_device_properties(0).multi_processor_count != 256:
+        pytest.skip("the expected choices assume 256 CUs")
+    assert C4.get_gemm_xl_bm(50432, 768, 3072) == 224     # ViT N = 768: 591 tiles (3 rounds) -> 678 (3 rounds)
+    assert C4.get_gemm_xl_bm(401408, 256, 2304) == 224    # ResNet-50 layer-3 3x3: 1568 -> 1792 tiles, 7 rounds
+    assert C4.get_gemm_xl_bm(100352, 512, 4608) == 224    # layer-4 3x3: 784 -> 896 tiles, 4 rounds
+    assert C4.get_gemm_xl_bm(50432, 2304, 768) == 256     # ViT qkv forward: 7 rounds either way
+    C4.set_gemm_xl_bm(-1)
+    assert C4.get_gemm_xl_bm(50432, 768, 3072) == 256
+
+
+@pytest.mark.parametrize("mode", ["store", "bias", "bias_gelu", "bias_res"])
+def test_w4_trimmed_plain_bitwise(C4, mode):
+    torch.manual_seed(5)
+    M, K, N = 40 * 224 + 37, 768, 768
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    kw = {}
+    if mode != "store":
+        kw["bias"] = bias
+    if mode == "bias_res":
+        kw["residual"] = res
+    aux0 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    aux1 = torch.empty_like(aux0)
+    c0 = run(C4, 256, lambda: C4.gemm_xl(a, b, mode, aux=aux0 if mode == "bias_gelu" else None, **kw))
+    c1 = run(C4, 224, lambda: C4.gemm_xl(a, b, mode, aux=aux1 if mode == "bias_gelu" else None, **kw))
+    assert torch.equal(c0, c1)
+    if mode == "bias_gelu":
+        assert torch.equal(aux0, aux1)
+    ref = a.float() @ b.float().t() + (bias.float() if mode != "store" else 0)
+    if mode == "bias_res":
+        ref = ref.bfloat16().float() + res.float()
+    if mode != "bias_gelu":
+        torch.testing.assert_close(c1.float(), ref, atol=6e-2, rtol=2e-2)
+
+
+def test_w4_trimmed_dgelu_bgrad(C4):
+    torch.manual_seed(6)
+    M, K, N = 30 * 224 + 5, 1024, 512
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    aux = torch.randn(M, N, device=DEV).bfloat16()
+    d0, g0 = run(C4, 256, lambda: C4.gemm_xl_dgelu_bgrad(a, b, aux))
+    d1, g1 = run(C4, 224, lambda: C4.gemm_xl_dgelu_bgrad(a, b, aux))
+    assert torch.equal(d0, d1)
+    torch.testing.assert_close(g1, d1.float().sum(0), atol=2e-2 * M ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.parametrize("n,c,h", [(41, 256, 14), (23, 512, 7)])
+def test_w4_trimmed_conv_moments_store(C4, n, c, h):
+    """3x3 tap gather (SRC 2) with the moments epilogue and the plain store,
+    plus the stride-phase dgrad's output row map."""
+    torch.manual_seed(7)
+    rows = n * h * h
+    x = torch.randn(n, c, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w = wmat((torch.randn(c, c, 3, 3, device=DEV) * 0.03).bfloat16())
+    (y0, s0) = run(C4, 256, lambda: C4.conv_xl(x, w, 3, 3, 1, 1, h, h, "moments"))
+    (y1, s1) = run(C4, 224, lambda: C4.conv_xl(x, w, 3, 3, 1, 1, h, h, "moments"))
+    assert torch.equal(y0, y1)
+    f = y1.float()
+    torch.testing.assert_close(s1[:c].float(), f.sum(0), atol=2e-2 * rows ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(s1[c:2 * c].float(), (f * f).sum(0), atol=2e-2 * rows ** 0.5, rtol=1e-3)
+    assert s1[2 * c].item() == rows
+    ref = torch.nn.functional.conv2d(x.float(), (w.float().reshape(c, 3, 3, c).permute(0, 3, 1, 2)), padding=1)
+    torch.testing.assert_close(y1.float(), ref.permute(0, 2, 3, 1).reshape(rows, c), atol=6e-2, rtol=2e-2)
+    (z0, _) = run(C4, 256, lambda: C4.conv_xl(x, w, 3, 3, 1, 1, h, h, "store"))
+    (z1, _) = run(C4, 224, lambda: C4.conv_xl(x, w, 3, 3, 1, 1, h, h, "store"))
+    assert torch.equal(z0, z1) and torch.equal(z1, y1)
+    from distributed_model_parallel_amd.ops import conv_igemm
+    wc = (torch.randn(2 * c, c, 3, 3, device=DEV) * 0.03).bfloat16()
+    dy = torch.randn(n, 2 * c, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    wph = conv_igemm._phase_weights(wc)
+    d0 = run(C4, 256, lambda: C4.conv_xl_dgrad_s2(dy, wph, 2 * h, 2 * h))
+    d1 = run(C4, 224, lambda: C4.conv_xl_dgrad_s2(dy, wph, 2 * h, 2 * h))
+    assert torch.equal(d0, d1)

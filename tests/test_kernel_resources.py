@@ -4,7 +4,8 @@ know they are still being written for ~18 cycles after each issue.  Any
 compiler spill of an accumulator right behind its MFMA reads a stale value
 (seen once: XL_BNBWD's epilogue pushed the kernel to 36 B of scratch and 0.2 %
 of its outputs came out wrong).  Every instantiation must therefore build with
-zero scratch and its 256 accumulators in AGPRs.  CPU only (hipcc
+zero scratch and its accumulators in AGPRs (256; 224 for the trimmed
+224-row tiles, MB = 7).  CPU only (hipcc
 cross-compiles gfx950)."""
 import os
 import shutil
@@ -25,4 +26,7 @@ def test_w4_gemm_kernels_never_spill():
     assert len(ks) >= 20, [k["name"] for k in ks]
     bad = [(k["name"], k["scratch"]) for k in ks if k["scratch"] != "0"]
     assert not bad, f"4-wave GEMM instantiations with scratch (accumulator spills behind asm MFMAs): {bad}"
-    assert all(k["agpr"] == "256" for k in ks), [(k["name"], k["agpr"]) for k in ks]
+    # trimmed 224-row tiles (template MB = 7, the last template argument) hold 56 accumulators
+    want = {k["name"]: ("224" if k["name"].replace(" ", "").endswith(",7>") else "256") for k in ks}
+    assert all(int(k["agpr"]) >= int(want[k["name"]]) for k in ks), [(k["name"], k["agpr"]) for k in ks]
+    assert any(want[k["name"]] == "224" for k in ks), "no trimmed (MB = 7) instantiation built"
