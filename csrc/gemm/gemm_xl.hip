@@ -220,21 +220,23 @@ template <int BN, int PIPE>
 using XlAcc = f32x4[8][xl_waves(PIPE) == 4 ? BN / 32 : BN / 64];
 
 // WMB (PIPE 11): 16-row blocks per wave actually computed (7: 224-row tile,
-// wave row 1 starts at row 112; acc[7][*] unused)
-template <int BN, int EPI, int PIPE, int LDS, int WMB = 8>
-__device__ __forceinline__ void xl_epilogue(const XlArgs& p, XlAcc<BN, PIPE>& acc, char* smem, int m0, int n0,
+// wave row 1 starts at row 112; acc[7][*] unused).  WWN (PIPE 11): waves along
+// N (1: four waves stacked along M over a BN = 128 tile)
+template <int BN, int EPI, int PIPE, int LDS, int WMB = 8, int WWN = 2, typename ACC>
+__device__ __forceinline__ void xl_epilogue(const XlArgs& p, ACC& acc, char* smem, int m0, int n0,
                                             int mt, int mtiles, int tbm = XBM) {
   constexpr int NW = xl_waves(PIPE), XTHREADS = NW * 64;
-  constexpr int WTM = 16 * WMB, WTN = NW == 4 ? BN / 2 : BN / 4;
+  constexpr int WTM = 16 * WMB, WTN = NW == 4 ? BN / WWN : BN / 4;
   constexpr int MI = WTM / 16, NI = WTN / 16;
-  static_assert(WMB == 8 || PIPE == 11, "trimmed wave tiles: 4-wave kernel only");
+  static_assert((WMB == 8 && WWN == 2) || PIPE == 11, "trimmed wave tiles: 4-wave kernel only");
   constexpr int CT_STRIDE = BN + 8;
   constexpr bool kMom = EPI == XL_MOMENTS || is_bnbwd(EPI) || EPI == XL_DGELU;
   // rows of this tile: [m0, min(M, m0 + tbm)); a trimmed tile's staged rows
   // past tbm belong to the next tile and are neither stored nor summed
   const int M = min(p.M, m0 + tbm), N = p.N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = NW == 4 ? wave >> 1 : wave >> 2, wc = NW == 4 ? wave & 1 : wave & 3;
+  const int wr = NW == 4 ? (WWN == 2 ? wave >> 1 : wave) : wave >> 2;
+  const int wc = NW == 4 ? (WWN == 2 ? wave & 1 : 0) : wave & 3;
   (void)lane;
   // ---- batched epilogue operand loads (residual / BN input / BN output / aux).
   // Row passes of RPP rows; batch b covers passes [b PB, b PB + PB).  The
@@ -986,11 +988,15 @@ __device__ __forceinline__ int w4_swz(int c, int row) { return c ^ ((row >> 1) &
 // 2 = conv tap gather (global_load_lds, zero taps read g_zero_row)
 // MB: 16-row MFMA blocks per wave (8: 256-row tiles; 7: 224-row tiles, which
 // fill the last 1-block/CU round of grids such as ViT's N = 768 GEMMs, 591 ->
-// 678 tiles in the same three rounds of 7/8 the work each: pick_bm)
-template <int EPI, int SRC, int MB = 8>
+// 678 tiles in the same three rounds of 7/8 the work each: pick_bm).
+// WN: waves along N (2: 2 x 2 waves, 256-wide tiles; 1: the four waves stacked
+// along M with 64 x 128 each, a 256 x 128 tile for N = 128 -- ResNet-50's
+// layer-2 stride-2 3x3 forward, which a 256-wide tile would half waste).
+template <int EPI, int SRC, int MB = 8, int WN = 2>
 __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
-  static_assert(MB == 8 || MB == 7, "4-wave tile rows: 256 or 224");
-  constexpr int TBM = 32 * MB, NRD = 8 + MB;  // tile rows; fragment reads per k-half
+  static_assert((WN == 2 && (MB == 8 || MB == 7)) || (WN == 1 && MB == 4), "4-wave tile shapes");
+  constexpr int TBM = (4 / WN) * 16 * MB, TBN = 128 * WN;  // tile rows / columns
+  constexpr int NRD = 8 + MB, NMF = 8 * MB;  // fragment reads / MFMAs per wave and k-half
   constexpr int OPB = 256 * 128, BUF = 2 * OPB;  // one operand's K tile, one buffer (A | B)
   constexpr int EPI_LDS = XBM * (256 + 8) * 2;
   constexpr int LDS = 2 * BUF > EPI_LDS ? 2 * BUF : EPI_LDS;
@@ -1000,11 +1006,11 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   const int M = p.M, N = p.N, K = p.K;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int mtiles = (M + TBM - 1) / TBM, ntiles = (N + 255) / 256;
+  const int wr = WN == 2 ? wave >> 1 : wave, wc = WN == 2 ? wave & 1 : 0;
+  const int mtiles = (M + TBM - 1) / TBM, ntiles = (N + TBN - 1) / TBN;
   int mt, nt;
   tile_coords(mtiles * ntiles, mtiles, ntiles, p.group_m, mt, nt);
-  const int m0 = mt * TBM, n0 = nt * 256;
+  const int m0 = mt * TBM, n0 = nt * TBN;
   const int ktiles = K / XBK;
 
   // (a 224-row tile still stages 256 A rows: the last 32 are the next tile's,
@@ -1087,23 +1093,25 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   auto iter = [&](auto st, auto rdn, int kt) {
     constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
     const int buf = kt & 1;
+    // fragment read r after MFMA (r NMF) / NRD, copy c after MFMA (c NMF) / 16:
+    // spread evenly (MB = 8: a read / copy per 4 MFMAs)
 #pragma unroll
-    for (int n = 0; n < 8 * MB; ++n) {
+    for (int n = 0; n < NMF; ++n) {
       w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
-      if ((n & 3) == 0) rd(I1{}, buf, n >> 2);
-      if (MB == 7 && n == 8 * MB - 2) rd(I1{}, buf, NRD - 1);  // 15 reads over 56 MFMAs
+      // (closed form, no inner loop: every index must fold to a constant)
+      const int r = (n * NRD + NMF - 1) / NMF;  // the read r with r NMF / NRD == n, if any
+      if (r < NRD && r * NMF / NRD == n) rd(I1{}, buf, r);
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     barrier();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int n = 0; n < 8 * MB; ++n) {
+    for (int n = 0; n < NMF; ++n) {
       w4_mfma(acc[n >> 3][n & 7], rb[1][n & 7], ra[1][n >> 3]);
       if constexpr (STAGE) {
-        if ((n & 3) == 0) dma(kt + 2, buf, n >> 2);
-        // 56 MFMAs: the last two of the 16 copies go between the last ones
-        if (MB == 7 && (n & 3) == 2 && n >= 8 * MB - 6) dma(kt + 2, buf, 14 + ((n - (8 * MB - 6)) >> 2));
+        const int c = (n * 16 + NMF - 1) / NMF;  // the copy c with c NMF / 16 == n, if any
+        if (c < 16 && c * NMF / 16 == n) dma(kt + 2, buf, c);
       }
       if constexpr (READ)
         if ((n & 1) == 1 && (n >> 1) < NRD) rd(I0{}, buf ^ 1, n >> 1);
@@ -1132,7 +1140,7 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   // every copy has landed (the waits above are inline asm the compiler cannot
   // see): say so with a wait it does see (finding 66)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  xl_epilogue<256, EPI, 11, LDS, MB>(p, acc, smem, m0, n0, mt, mtiles, TBM);
+  xl_epilogue<TBN, EPI, 11, LDS, MB, WN>(p, acc, smem, m0, n0, mt, mtiles, TBM);
   if (p.tdbg) {
     __syncthreads();
     xl_mark(p, 3);
@@ -1869,6 +1877,7 @@ __host__ __device__ constexpr bool w4_epi(int e);
 // GEMMs 591 tiles (3 rounds x 256) -> 678 (3 x 224); ResNet-50 layer-3 3x3s
 // 1568 (7 x 256) -> 1792 (7 x 224), layer-4 784 (4 x 256) -> 896 (4 x 224).
 int pick_bm_w4(int64_t M, int64_t N) {
+  if (N <= 128) return 256;  // the 256 x 128 tile (WN = 1) has 256 rows only
   if (g_xl_bm == 224 || g_xl_bm == 256) return g_xl_bm;
   if (g_xl_bm < 0) return 256;
   const int64_t cus = num_cus(), nt = (N + 255) / 256;
@@ -1928,6 +1937,16 @@ void launch_pp256(const XlArgs& a_in, int blocks, hipStream_t s) {
     XlArgs w = a;
     // a.bm came from pick_bm (the moments partials are sized by it): 224 or 256
     w.bm = a.bm == 224 ? 224 : 256;
+    if (w.N <= 128 && w.bm == 256) {  // 256 x 128 tiles, the four waves along M
+      const int nblocks = (w.M + 255) / 256;
+      if (w.cv.cin > 0)
+        hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 2, 4, 1>), dim3(nblocks), dim3(256), 0, s, w);
+      else if (w.A2)
+        hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 1, 4, 1>), dim3(nblocks), dim3(256), 0, s, w);
+      else
+        hipLaunchKernelGGL((gemm_xl_w4_kernel<EPI, 0, 4, 1>), dim3(nblocks), dim3(256), 0, s, w);
+      return;
+    }
     const int wblocks = ((w.M + w.bm - 1) / w.bm) * ((w.N + 255) / 256);
     if (w.bm == 224) {
       if (w.cv.cin > 0)

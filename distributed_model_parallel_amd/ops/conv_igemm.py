@@ -144,11 +144,17 @@ def _halo_wgrad_ok(C, cin: int, cout: int, kh: int, kw: int, stride: int, pad: i
 
 
 def _miopen_fwd(cout: int, kh: int) -> bool:
-    return _MIOPEN_FWD and kh > 1 and not (_XL3 and cout >= 256)
+    return _MIOPEN_FWD and kh > 1 and not _xl_fwd(cout, kh, kh)
+
+
+# Cout = 128 (ResNet-50's layer-2 stride-2 3x3, the last MIOpen pass of the
+# step) runs on the 4-wave kernel's 256 x 128 tile (four waves along M,
+# gemm_xl_w4_kernel<EPI, 2, 4, 1>) with the BN moments fused.
+_XL_N128 = True  # (tools/step_ab.py arms n128 / miopen)
 
 
 def _xl_fwd(cout: int, kh: int, kw: int) -> bool:
-    return _XL3 and cout >= 256 and kh == kw and kh > 1
+    return _XL3 and (cout >= 256 or (cout == 128 and _XL_N128)) and kh == kw and kh > 1
 
 
 def _xl_dgrad(cin: int, kh: int, kw: int, stride: int) -> bool:

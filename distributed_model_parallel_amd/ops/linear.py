@@ -54,11 +54,17 @@ _XL_MIN_ROWS = 4096  # below this the 256-row tile grid leaves most CUs idle
 # better) and need a W^T copy: 8.0 + 0.4 ms vs 7.4 ms per step (ViT 41.0 vs
 # 40.3 ms).  The fused-epilogue GEMMs and every weight gradient (gemm_tn_xl)
 # are ours.
-# "fwd" (default since round 6): the qkv forward (N = 2304, bias in the
-# store) on ours, the N = 768 data gradients on the library -- ViT step
-# 36.56 / 36.67 ms (fwd) vs 36.55 / 36.61 (lib) vs 37.27 / 37.41 (xl),
-# interleaved on one box.
-_PLAIN_MODE = __import__("os").environ.get("DMP_LINEAR_PLAIN", "fwd")
+# "fwd": the qkv forward (N = 2304, bias in the store) on ours, the N = 768
+# data gradients on the library -- ViT step 36.56 / 36.67 ms (fwd) vs 36.55 /
+# 36.61 (lib) vs 37.27 / 37.41 (xl), interleaved on one box, with 256-row
+# tiles and a W^T copy per data gradient.
+# "xl" (default since the 224-row tiles and the optimizer-driven W^T cache):
+# the N = 768 grids fill their three rounds (678 tiles of 224 rows), and the
+# data gradients tie the library in isolation (qkv / proj / fc1: 0.169 /
+# 0.068 / 0.221 vs 0.165 / 0.070 / 0.221 ms, tools/w4_trim_bench.py) and in
+# the step (tools/step_ab.py: xl 38.23 vs fwd 38.21 vs lib 38.05 ms on one
+# box): no library GEMM left in the ViT step but the classifier head.
+_PLAIN_MODE = __import__("os").environ.get("DMP_LINEAR_PLAIN", "xl")
 _PLAIN_LIB = _PLAIN_MODE == "lib"
 _PLAIN_FWD_XL = _PLAIN_MODE in ("xl", "fwd")
 _PLAIN_DGRAD_XL = _PLAIN_MODE == "xl"
@@ -108,9 +114,9 @@ def _xl_gemm_ok(a: torch.Tensor, n: int) -> bool:
 
 
 def _dgrad(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """dx = dy @ W: hipBLASLt by default (measured faster, finding 50), or
-    the ping-pong MFMA GEMM with DMP_LINEAR_PLAIN=xl (B operand = W^T [in,
-    out], a transposed copy of the weight per call: 1.2-4.7 MB for ViT-B/16)."""
+    """dx = dy @ W on gemm_xl (B operand = W^T [in, out], from the
+    optimizer-driven W^T cache, ops/wt_cache.py), or hipBLASLt with
+    DMP_LINEAR_PLAIN=lib / fwd."""
     if _PLAIN_DGRAD_XL and w.dtype == torch.bfloat16 and _xl_gemm_ok(dy2, w.shape[1]):
         _STATS["xl_dgrad"] += 1
         from .wt_cache import transposed

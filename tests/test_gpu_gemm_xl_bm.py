@@ -254,3 +254,37 @@ def test_w4_trimmed_conv_moments_store(C4, n, c, h):
     d0 = run(C4, 256, lambda: C4.conv_xl_dgrad_s2(dy, wph, 2 * h, 2 * h))
     d1 = run(C4, 224, lambda: C4.conv_xl_dgrad_s2(dy, wph, 2 * h, 2 * h))
     assert torch.equal(d0, d1)
+
+
+@pytest.mark.parametrize("n,cin,h,stride", [(37, 128, 56, 2), (9, 64, 28, 1), (5, 128, 28, 1)])
+def test_w4_n128_conv_moments(n, cin, h, stride):
+    """Cout = 128 convs on the 256 x 128 tile (WN = 1): output and fused moments
+    against an fp32 conv of the same bf16 operands."""
+    C = _native.require("gemm_xl n128")
+    torch.manual_seed(8)
+    cout = 128
+    x = torch.randn(n, cin, h, h, device=DEV).bfloat16().contiguous(memory_format=CL)
+    w4 = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.05).bfloat16()
+    ho = (h + 2 - 3) // stride + 1
+    rows = n * ho * ho
+    y, s = C.conv_xl(x, wmat(w4), 3, 3, stride, 1, ho, ho, "moments")
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.conv2d(x.float(), w4.float(), stride=stride, padding=1)
+    ref2 = ref.permute(0, 2, 3, 1).reshape(rows, cout)
+    torch.testing.assert_close(y.float(), ref2, atol=6e-2, rtol=2e-2)
+    f = y.float()
+    torch.testing.assert_close(s[:cout].float(), f.sum(0), atol=2e-2 * rows ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(s[cout:2 * cout].float(), (f * f).sum(0), atol=2e-2 * rows ** 0.5, rtol=1e-3)
+    assert s[2 * cout].item() == rows
+    z, _ = C.conv_xl(x, wmat(w4), 3, 3, stride, 1, ho, ho, "store")
+    assert torch.equal(z, y)
+
+
+def test_w4_n128_plain():
+    C = _native.require("gemm_xl n128")
+    torch.manual_seed(9)
+    M, K, N = 13 * 256 + 77, 1152, 128
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
+    c = C.gemm_xl(a, b, "store")
+    torch.testing.assert_close(c.float(), a.float() @ b.float().t(), atol=6e-2, rtol=2e-2)

@@ -130,7 +130,7 @@ def test_dgelu_epilogue_bias_grad(T):
 def test_qkv_linear_forward_and_dgrad_on_xl(mode, monkeypatch):
     """The qkv projection (ops.linear.linear -> _LinearFn): forward with the
     bias in gemm_xl's store and the data gradient on gemm_xl
-    (DMP_LINEAR_PLAIN=xl), the forward only ("fwd", the default), or both on
+    (DMP_LINEAR_PLAIN=xl, the default), the forward only ("fwd"), or both on
     hipBLASLt ("lib")."""
     monkeypatch.setattr(L, "_PLAIN_FWD_XL", mode in ("xl", "fwd"))
     monkeypatch.setattr(L, "_PLAIN_DGRAD_XL", mode == "xl")

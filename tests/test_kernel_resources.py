@@ -5,7 +5,7 @@ compiler spill of an accumulator right behind its MFMA reads a stale value
 (seen once: XL_BNBWD's epilogue pushed the kernel to 36 B of scratch and 0.2 %
 of its outputs came out wrong).  Every instantiation must therefore build with
 zero scratch and its accumulators in AGPRs (256; 224 for the trimmed
-224-row tiles, MB = 7).  CPU only (hipcc
+224-row tiles, MB = 7; 128 for the 256 x 128 tiles, MB = 4).  CPU only (hipcc
 cross-compiles gfx950)."""
 import os
 import shutil
@@ -27,6 +27,10 @@ def test_w4_gemm_kernels_never_spill():
     bad = [(k["name"], k["scratch"]) for k in ks if k["scratch"] != "0"]
     assert not bad, f"4-wave GEMM instantiations with scratch (accumulator spills behind asm MFMAs): {bad}"
     # trimmed 224-row tiles (template MB = 7, the last template argument) hold 56 accumulators
-    want = {k["name"]: ("224" if k["name"].replace(" ", "").endswith(",7>") else "256") for k in ks}
+    # and the 256 x 128 tiles (MB = 4, WN = 1) 32
+    def want_agpr(name):
+        n = name.replace(" ", "")
+        return "224" if n.endswith(",7,2>") else "128" if n.endswith(",4,1>") else "256"
+    want = {k["name"]: want_agpr(k["name"]) for k in ks}
     assert all(int(k["agpr"]) >= int(want[k["name"]]) for k in ks), [(k["name"], k["agpr"]) for k in ks]
     assert any(want[k["name"]] == "224" for k in ks), "no trimmed (MB = 7) instantiation built"

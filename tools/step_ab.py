@@ -11,6 +11,7 @@ arms:
   plain_fwd  qkv forward on gemm_xl, data gradients on hipBLASLt
   plain_xl   every plain GEMM on gemm_xl
   fold1 / fold2  BN-fold coefficient products on hipBLASLt / our fp32 MFMA GEMM
+  n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
 
   python tools/step_ab.py --model vit_b_16 --batch 256 --arms plain_fwd,plain_xl [--steps 10] [--rounds 3]
 """
@@ -22,7 +23,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_model_parallel_amd import _native  # noqa: E402
-from distributed_model_parallel_amd.ops import linear  # noqa: E402
+from distributed_model_parallel_amd.ops import conv_igemm, linear  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
 from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed  # noqa: E402
 
@@ -45,6 +46,8 @@ def _arm(name):
         "plain_xl": _plain("xl"),
         "fold1": lambda: C.set_fold_gemm(1),
         "fold2": lambda: C.set_fold_gemm(2),
+        "n128": lambda: setattr(conv_igemm, "_XL_N128", True),
+        "miopen": lambda: setattr(conv_igemm, "_XL_N128", False),
     }
     return table[name]
 
