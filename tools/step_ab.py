@@ -11,6 +11,8 @@ arms:
   plain_fwd  qkv forward on gemm_xl, data gradients on hipBLASLt
   plain_xl   every plain GEMM on gemm_xl
   fold1 / fold2  BN-fold coefficient products on hipBLASLt / our fp32 MFMA GEMM
+  xln128 / xln256  1x1-conv GEMMs with N = 128 (K >= 128) on gemm_xl_conv (the two-blocks-per-CU x2 kernel) / on gemm_nt
+  fwdn128 / fwdnt  1x1 forwards with moments at N = 128 on the 4-wave 256 x 128 tile / on gemm_nt
   n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
 
   python tools/step_ab.py --model vit_b_16 --batch 256 --arms plain_fwd,plain_xl [--steps 10] [--rounds 3]
@@ -23,7 +25,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_model_parallel_amd import _native  # noqa: E402
-from distributed_model_parallel_amd.ops import conv_igemm, linear  # noqa: E402
+from distributed_model_parallel_amd.ops import conv1x1, conv_igemm, linear  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
 from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed  # noqa: E402
 
@@ -48,6 +50,10 @@ def _arm(name):
         "fold2": lambda: C.set_fold_gemm(2),
         "n128": lambda: setattr(conv_igemm, "_XL_N128", True),
         "miopen": lambda: setattr(conv_igemm, "_XL_N128", False),
+        "xln128": lambda: setattr(conv1x1, "_XL_MIN_N", 128),
+        "xln256": lambda: setattr(conv1x1, "_XL_MIN_N", 256),
+        "fwdn128": lambda: setattr(conv1x1, "_XL_N128_FWD", True),
+        "fwdnt": lambda: setattr(conv1x1, "_XL_N128_FWD", False),
     }
     return table[name]
 
