@@ -148,6 +148,7 @@ at::Tensor stem_fold_finish(const at::Tensor& img, int64_t ho, int64_t wo, const
 bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
+void set_tn_narrow(bool on);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype,
                          const c10::optional<at::Tensor>& out);
@@ -367,6 +368,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
         "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
+  m.def("set_tn_narrow", &dmp::set_tn_narrow, py::arg("on"),
+        "A/B: 4-wave weight-gradient tiles of 64 / 128 on an output side that narrow (default on)");
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"), py::arg("out") = py::none(),
         "A^T B (weight gradient) on the ping-pong MFMA schedule, split over M",
         py::call_guard<py::gil_scoped_release>());

@@ -1623,20 +1623,40 @@ __global__ __launch_bounds__(XTHREADS, 1) void gemm_tn_pp_kernel(const TnPPArgs 
 // 3 = both operands the gathered rows (the Gram of a strided 1x1 sample).
 __device__ __forceinline__ int tnw_swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
 
-template <int SRC>
+// Narrow tiles (SRC 0 only): TNN x TNK = 64 x 256 / 256 x 64 (the four
+// waves along the wide side, 64 x 64 each) or 128 x 256 / 256 x 128 (2 x 2
+// waves, 64 x 128 / 128 x 64 each) for outputs with a side of 64 or 128
+// (ResNet-50 layers 1-2: a 256 x 256 tile multiplied 2-16x the useful MFMA
+// work there); the copies of the operand planes past the tile are skipped.
+template <int TNN, int TNK>
+struct TnShape {
+  static constexpr int WGN = TNN == 64 ? 1 : TNK == 64 ? 4 : 2;  // wave grid along n / k
+  static constexpr int WGK = 4 / WGN;
+  static constexpr int MB = TNN / 16 / WGN, NB = TNK / 16 / WGK;  // 16-blocks per wave along n / k
+};
+
+template <int SRC, int TNN = 256, int TNK = 256>
 __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
+  static_assert(SRC == 0 || (TNN == 256 && TNK == 256), "narrow TN tiles: plain operands only");
   constexpr int PLANE = 64 * 128, OPER = 4 * PLANE, BUF = 2 * OPER;  // bytes
+  using SH = TnShape<TNN, TNK>;
+  constexpr int WGK = SH::WGK, MB = SH::MB, NB = SH::NB;
+  static_assert(MB * 16 * SH::WGN == TNN && NB * 16 * WGK == TNK && (MB == 4 || MB == 8) && (NB == 4 || NB == 8),
+                "TN tile shape");
+  constexpr int NMF = MB * NB, NRD = MB + NB;  // MFMAs / fragment reads per wave and k32 half
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
   using v4i16 = short __attribute__((ext_vector_type(4)));
   using lds_v4 = __attribute__((address_space(3))) v4i16;
   const int M = p.M, N = p.N, K = p.K;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int ntiles = (N + 255) >> 8, ktiles = (K + 255) >> 8;
+  const int wr = wave / WGK, wc = wave % WGK;
+  // this wave's operand planes inside the tile (64 columns each): copies of the others are skipped
+  const bool cpa = wave * 64 < TNN, cpb = wave * 64 < TNK;
+  const int ntiles = (N + TNN - 1) / TNN, ktiles = (K + TNK - 1) / TNK;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tile = bid % (ntiles * ktiles), split = bid / (ntiles * ktiles);
-  const int n0 = (tile / ktiles) * 256, k0 = (tile % ktiles) * 256;
+  const int n0 = (tile / ktiles) * TNN, k0 = (tile % ktiles) * TNK;
   const int64_t mb = (int64_t)split * p.rps;
   const int64_t me = min((int64_t)M, mb + p.rps);
   const int KT = (int)((me - mb + 63) >> 6);
@@ -1735,6 +1755,7 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
       soff = 0;
     }
     unsigned keep;
+    if ((c < 8 && !cpa) || (c >= 8 && !cpb)) return;  // a plane past a narrow tile
     if (c < 8)
       asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
                    "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
@@ -1759,46 +1780,51 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
     short __attribute__((ext_vector_type(8))) t8 = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, t8);
   };
-  bf16x8 ra[2][8], rb[2][8];
-  // fragment read r (0..15) of k32 half H: A block (n) r == 0 ? 0 : r - 8, B blocks (k) 0..7 for r = 1..8
+  bf16x8 ra[2][MB], rb[2][NB];
+  // fragment read r (0..NRD-1) of k32 half H: A block (n) r == 0 ? 0 : r - NB, B blocks (k) 0..NB-1 for r = 1..NB
   auto rd = [&](auto hc, int buf, int r) __attribute__((always_inline)) {
     constexpr int H = decltype(hc)::value;
-    const bool isb = r >= 1 && r <= 8;
-    const int blk = r == 0 ? 0 : (isb ? r - 1 : r - 8);
-    const int col = (isb ? wc : wr) * 128 + blk * 16;  // within the 256-col operand tile
+    const bool isb = r >= 1 && r <= NB;
+    const int blk = r == 0 ? 0 : (isb ? r - 1 : r - NB);
+    const int col = (isb ? wc * NB : wr * MB) * 16 + blk * 16;  // within the operand tile
     const char* plane = smem + buf * BUF + (isb ? OPER : 0) + (col >> 6) * PLANE;
     if (isb) rb[H][blk] = tr_frag(plane, H, col & 63);
     else ra[H][blk] = tr_frag(plane, H, col & 63);
   };
-  f32x4 acc[8][8];
+  f32x4 acc[MB][NB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   // operands swapped: acc[i][j] holds the transposed 16 x 16 block: lane =
-  // output row n (i), registers = 4 consecutive output columns k (j)
+  // output row n (i), registers = 4 consecutive output columns k (j).
+  // Read r follows MFMA (r NMF) / NRD, copy c MFMA (c NMF) / 16 (the 256 x 256
+  // tile: one read / copy per 4 MFMAs); closed forms, so every index folds.
   auto iter = [&](auto st, auto rdn, int kt) __attribute__((always_inline)) {
     constexpr bool STAGE = decltype(st)::value, READ = decltype(rdn)::value;
     const int buf = kt & 1;
     if constexpr (SRC >= 2 && STAGE) gather_rows(kt + 2);
 #pragma unroll
-    for (int n = 0; n < 64; ++n) {
-      w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
-      if ((n & 3) == 0) rd(I1{}, buf, n >> 2);
+    for (int n = 0; n < NMF; ++n) {
+      w4_mfma(acc[n / NB][n % NB], rb[0][n % NB], ra[0][n / NB]);
+      const int r = (n * NRD + NMF - 1) / NMF;
+      if (r < NRD && r * NMF / NRD == n) rd(I1{}, buf, r);
     }
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     barrier();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int n = 0; n < 64; ++n) {
-      w4_mfma(acc[n >> 3][n & 7], rb[1][n & 7], ra[1][n >> 3]);
-      if constexpr (STAGE)
-        if ((n & 3) == 0) dma(kt + 2, buf, n >> 2);
+    for (int n = 0; n < NMF; ++n) {
+      w4_mfma(acc[n / NB][n % NB], rb[1][n % NB], ra[1][n / NB]);
+      if constexpr (STAGE) {
+        const int c = (n * 16 + NMF - 1) / NMF;
+        if (c < 16 && c * NMF / 16 == n) dma(kt + 2, buf, c);
+      }
       if constexpr (READ)
-        if ((n & 1) == 1 && n < 32) rd(I0{}, buf ^ 1, n >> 1);
+        if ((n & 1) == 1 && (n >> 1) < NRD) rd(I0{}, buf ^ 1, n >> 1);
     }
   };
   if (KT > 0) {
@@ -1809,13 +1835,16 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
       if constexpr (SRC >= 2) gather_rows(1);
 #pragma unroll
       for (int c = 0; c < 16; ++c) dma(1, 1, c);
-      vmcnt<16>();
+      // tile 0 landed: at most one tile of this wave's copies (16, 8 or 0) in flight
+      if (cpa && cpb) vmcnt<16>();
+      else if (cpa || cpb) vmcnt<8>();
+      else vmcnt<0>();
     } else {
       vmcnt<0>();
     }
     barrier();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) rd(I0{}, 0, r);
+    for (int r = 0; r < NRD; ++r) rd(I0{}, 0, r);
     int kt = 0;
     for (; kt + 2 < KT; ++kt) iter(std::true_type{}, std::true_type{}, kt);
     if (kt + 1 < KT) iter(std::false_type{}, std::true_type{}, kt++);
@@ -1826,11 +1855,11 @@ __global__ __launch_bounds__(256, 1) void gemm_tn_w4_kernel(const TnPPArgs p) {
   float* out = p.part + (int64_t)split * N * K;
   const int lrow = lane & 15, lk = lane >> 4;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = n0 + wr * 128 + i * 16 + lrow;
+  for (int i = 0; i < MB; ++i) {
+    const int n = n0 + wr * MB * 16 + i * 16 + lrow;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = k0 + wc * 128 + j * 16 + lk * 4;
+    for (int j = 0; j < NB; ++j) {
+      const int k = k0 + wc * NB * 16 + j * 16 + lk * 4;
       if (n < N && k < K) *reinterpret_cast<f32x4*>(out + (int64_t)n * K + k) = acc[i][j];
     }
   }
@@ -2429,11 +2458,12 @@ at::Tensor acc_target(const c10::optional<at::Tensor>& out, int64_t numel, at::S
 namespace {
 
 int g_tn_xl_rounds = 0;  // 0: auto; else rounds of 256 blocks (tools/tn_xl_bench.py sweeps)
+int g_tn_narrow = 1;     // narrow TN tiles for sides of 64 / 128 (set_tn_narrow, A/B)
 
 // rows per M split (a multiple of 64): one or two full rounds of 1-block/CU
 // work, every split >= 16 K tiles
-int64_t tn_rows_per_split(int M, int N, int K) {
-  const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
+int64_t tn_rows_per_split(int M, int N, int K, int tnn = 256, int tnk = 256) {
+  const int tiles = ((N + tnn - 1) / tnn) * ((K + tnk - 1) / tnk);
   const int mtl = (M + 63) / 64;
   int rounds = tiles >= 256 ? (tiles + 255) / 256 : (tiles * std::max(1, 256 / tiles) >= 192 ? 1 : 2);
   if (g_tn_xl_rounds > 0) rounds = g_tn_xl_rounds;
@@ -2454,8 +2484,13 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   const int M = a.M, N = a.N, K = a.K;
   auto out = acc.defined() ? acc : at::empty({N, K}, like.options().dtype(out_dtype));
   if (M == 0) return acc.defined() ? out : out.zero_();
-  const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
-  const int64_t rps = tn_rows_per_split(M, N, K);
+  // plain operands on the 4-wave kernel: the narrowest tile that covers a
+  // side of 64 / 128 (TnShape); the gather forms keep 256 x 256
+  const bool plain_w4 = g_xl_pipe == 11 && a.cv.cin == 0;
+  const int tnn = !plain_w4 || !g_tn_narrow ? 256 : N <= 64 ? 64 : K <= 64 ? 256 : N <= 128 ? 128 : 256;
+  const int tnk = !plain_w4 || !g_tn_narrow || tnn != 256 ? 256 : K <= 64 ? 64 : K <= 128 ? 128 : 256;
+  const int tiles = ((N + tnn - 1) / tnn) * ((K + tnk - 1) / tnk);
+  const int64_t rps = tn_rows_per_split(M, N, K, tnn, tnk);
   const int splits = (int)(((int64_t)M + rps - 1) / rps);
   a.rps = rps;
   auto part = at::empty({splits, N, K}, like.options().dtype(at::kFloat));
@@ -2463,8 +2498,17 @@ at::Tensor run_tn_pp(TnPPArgs a, const at::Tensor& like, at::ScalarType out_dtyp
   hipStream_t s = at::hip::getCurrentHIPStream();
   // weight gradients on the 4-wave kernel (finding 70; DMP_XL_PIPE=10: the
   // ping-pong one), the tap gather included when its input fits 32-bit offsets
-  if (g_xl_pipe == 11 && a.cv.cin == 0)
-    hipLaunchKernelGGL(gemm_tn_w4_kernel<0>, dim3(tiles * splits), dim3(256), 0, s, a);
+  const dim3 grid(tiles * splits);
+  if (plain_w4 && tnn == 64)
+    hipLaunchKernelGGL((gemm_tn_w4_kernel<0, 64, 256>), grid, dim3(256), 0, s, a);
+  else if (plain_w4 && tnk == 64)
+    hipLaunchKernelGGL((gemm_tn_w4_kernel<0, 256, 64>), grid, dim3(256), 0, s, a);
+  else if (plain_w4 && tnn == 128)
+    hipLaunchKernelGGL((gemm_tn_w4_kernel<0, 128, 256>), grid, dim3(256), 0, s, a);
+  else if (plain_w4 && tnk == 128)
+    hipLaunchKernelGGL((gemm_tn_w4_kernel<0, 256, 128>), grid, dim3(256), 0, s, a);
+  else if (plain_w4)
+    hipLaunchKernelGGL(gemm_tn_w4_kernel<0>, grid, dim3(256), 0, s, a);
   else if (a.gram)
     hipLaunchKernelGGL(gemm_tn_w4_kernel<3>, dim3(tiles * splits), dim3(256), 0, s, a);
   else if (g_xl_pipe == 11 && (64 / a.cv.wo + 1) <= 3 * a.cv.ho && tn_w4_gather_fits(a))
@@ -2550,6 +2594,7 @@ at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, 
 }
 
 void set_tn_xl_rounds(int r) { g_tn_xl_rounds = r; }
+void set_tn_narrow(bool on) { g_tn_narrow = on ? 1 : 0; }
 
 int get_gemm_xl_pipe() { return g_xl_pipe; }
 void set_gemm_xl_x2(int mode) {

@@ -102,3 +102,28 @@ def test_strided_gather_over_2gb_input():
     g = C.gram_strided_xl(x, 2, ho, ho)
     gr = xs.float().t() @ xs.float()
     torch.testing.assert_close(g, gr, atol=3e-3 * (n * ho * ho) ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(200000, 64, 256), (200000, 256, 64), (100000, 128, 512), (100000, 512, 128),
+                                   (70000, 64, 64), (5000, 64, 320), (3000, 200, 120), (4133, 128, 256),
+                                   (64, 64, 256)])
+@pytest.mark.parametrize("narrow", [True, False])
+def test_gemm_tn_xl_narrow_tiles(M, N, K, narrow):
+    """The 4-wave weight-gradient kernel's narrow tiles (64 x 256, 256 x 64,
+    128 x 256, 256 x 128: gemm_tn_w4_kernel<0, TNN, TNK>) against fp32, with
+    the accumulate-into-out path; narrow=False: the 256 x 256 tile."""
+    C = _native.require("gemm_tn_xl")
+    C.set_tn_narrow(narrow)
+    try:
+        torch.manual_seed(11)
+        a = torch.randn(M, N, device=DEV).bfloat16()
+        b = torch.randn(M, K, device=DEV).bfloat16()
+        ref = a.float().t() @ b.float()
+        got = C.gemm_tn_xl(a, b, torch.float32)
+        torch.testing.assert_close(got, ref, atol=1e-3 * M ** 0.5, rtol=1e-2)
+        acc = torch.randn(N, K, device=DEV)
+        acc0 = acc.clone()
+        C.gemm_tn_xl(a, b, torch.float32, out=acc)
+        torch.testing.assert_close(acc, acc0 + ref, atol=1e-3 * M ** 0.5, rtol=1e-2)
+    finally:
+        C.set_tn_narrow(True)

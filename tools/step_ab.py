@@ -12,6 +12,7 @@ arms:
   plain_xl   every plain GEMM on gemm_xl
   fold1 / fold2  BN-fold coefficient products on hipBLASLt / our fp32 MFMA GEMM
   xln128 / xln256  1x1-conv GEMMs with N = 128 (K >= 128) on gemm_xl_conv (the two-blocks-per-CU x2 kernel) / on gemm_nt
+  tnnarrow / tnwide  4-wave weight gradients with a side of 64 / 128 on narrow tiles / on 256 x 256
   fwdn128 / fwdnt  1x1 forwards with moments at N = 128 on the 4-wave 256 x 128 tile / on gemm_nt
   n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
 
@@ -52,6 +53,8 @@ def _arm(name):
         "miopen": lambda: setattr(conv_igemm, "_XL_N128", False),
         "xln128": lambda: setattr(conv1x1, "_XL_MIN_N", 128),
         "xln256": lambda: setattr(conv1x1, "_XL_MIN_N", 256),
+        "tnnarrow": lambda: C.set_tn_narrow(True),
+        "tnwide": lambda: C.set_tn_narrow(False),
         "fwdn128": lambda: setattr(conv1x1, "_XL_N128_FWD", True),
         "fwdnt": lambda: setattr(conv1x1, "_XL_N128_FWD", False),
     }
