@@ -992,11 +992,16 @@ __device__ __forceinline__ int w4_swz(int c, int row) { return c ^ ((row >> 1) &
 // WN: waves along N (2: 2 x 2 waves, 256-wide tiles; 1: the four waves stacked
 // along M with 64 x 128 each, a 256 x 128 tile for N = 128 -- ResNet-50's
 // layer-2 stride-2 3x3 forward, which a 256-wide tile would half waste).
-template <int EPI, int SRC, int MB = 8, int WN = 2>
+// NBW: 16-column blocks per wave (8; 4 with WN = 1 gives a 256 x 64 tile: for
+// ResNet-50 layer 1's N = 64 conv1 forward and conv3 data gradient + BN
+// backward it measured slower than gemm_nt's 256 x 64 tile in-step, 112.48
+// vs 111.23 ms, finding 78, so no launch uses it).
+template <int EPI, int SRC, int MB = 8, int WN = 2, int NBW = 8>
 __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
-  static_assert((WN == 2 && (MB == 8 || MB == 7)) || (WN == 1 && MB == 4), "4-wave tile shapes");
-  constexpr int TBM = (4 / WN) * 16 * MB, TBN = 128 * WN;  // tile rows / columns
-  constexpr int NRD = 8 + MB, NMF = 8 * MB;  // fragment reads / MFMAs per wave and k-half
+  static_assert((WN == 2 && (MB == 8 || MB == 7) && NBW == 8) || (WN == 1 && MB == 4 && (NBW == 8 || NBW == 4)),
+                "4-wave tile shapes");
+  constexpr int TBM = (4 / WN) * 16 * MB, TBN = 16 * NBW * WN;  // tile rows / columns
+  constexpr int NRD = NBW + MB, NMF = NBW * MB;  // fragment reads / MFMAs per wave and k-half
   constexpr int OPB = 256 * 128, BUF = 2 * OPB;  // one operand's K tile, one buffer (A | B)
   constexpr int EPI_LDS = XBM * (256 + 8) * 2;
   constexpr int LDS = 2 * BUF > EPI_LDS ? 2 * BUF : EPI_LDS;
@@ -1046,10 +1051,14 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
     }
   }
   const int lcz = w4_swz(lane & 7, lrow8) * 8;  // zero-row chunk (any in-bounds 16 B)
+  // B rows past a narrow tile (TBN < 256) are not copied: this wave's 64 B
+  // rows are either all inside or all past it
+  const bool cpb = wave * 64 < TBN;
   auto dma = [&](int kt, int buf, int c) {
     const int q = c & 7;
     char* dst = smem + buf * BUF + (c >> 3) * OPB + (wave * 8 + q) * 1024;
     const int koff = kt * XBK;
+    if (c >= 8 && !cpb) return;
     if (c >= 8) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lptr_t)dst, 16, ob[q], koff * 2, 0, 0);
     } else if constexpr (SRC == 2) {  // tap (tr, tc), channels c0.. of this piece's pixels, or zeros
@@ -1069,22 +1078,22 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   const int lrow = lane & 15, lk = lane >> 4;
   const int fo0 = lrow * 128 + (w4_swz(lk, lrow) << 4), fo1 = lrow * 128 + (w4_swz(4 + lk, lrow) << 4);
   const int aoff = wr * (16 * MB) * 128, boff = OPB + wc * 128 * 128;
-  bf16x8 ra[2][8], rb[2][8];
+  bf16x8 ra[2][MB], rb[2][NBW];
   // fragment read r (0..NRD-1) in the order the MFMAs consume them: A block 0,
-  // B blocks 0..7, A blocks 1..MB-1
+  // B blocks 0..NBW-1, A blocks 1..MB-1
   auto rd = [&](auto hc, int buf, int r) {
     constexpr int H = decltype(hc)::value;
-    const bool isb = r >= 1 && r <= 8;
-    const int blk = r == 0 ? 0 : (isb ? r - 1 : r - 8);
+    const bool isb = r >= 1 && r <= NBW;
+    const int blk = r == 0 ? 0 : (isb ? r - 1 : r - NBW);
     const char* base = smem + buf * BUF + (isb ? boff : aoff) + blk * 2048 + (H ? fo1 : fo0);
     if (isb) rb[H][blk] = *reinterpret_cast<const bf16x8*>(base);
     else ra[H][blk] = *reinterpret_cast<const bf16x8*>(base);
   };
-  f32x4 acc[8][8];
+  f32x4 acc[MB][NBW];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NBW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   // operands swapped: acc[i][j] holds the transposed 16 x 16 block (lane =
@@ -1097,7 +1106,7 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
     // spread evenly (MB = 8: a read / copy per 4 MFMAs)
 #pragma unroll
     for (int n = 0; n < NMF; ++n) {
-      w4_mfma(acc[n >> 3][n & 7], rb[0][n & 7], ra[0][n >> 3]);
+      w4_mfma(acc[n / NBW][n % NBW], rb[0][n % NBW], ra[0][n / NBW]);
       // (closed form, no inner loop: every index must fold to a constant)
       const int r = (n * NRD + NMF - 1) / NMF;  // the read r with r NMF / NRD == n, if any
       if (r < NRD && r * NMF / NRD == n) rd(I1{}, buf, r);
@@ -1108,7 +1117,7 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int n = 0; n < NMF; ++n) {
-      w4_mfma(acc[n >> 3][n & 7], rb[1][n & 7], ra[1][n >> 3]);
+      w4_mfma(acc[n / NBW][n % NBW], rb[1][n % NBW], ra[1][n / NBW]);
       if constexpr (STAGE) {
         const int c = (n * 16 + NMF - 1) / NMF;  // the copy c with c NMF / 16 == n, if any
         if (c < 16 && c * NMF / 16 == n) dma(kt + 2, buf, c);
@@ -1122,7 +1131,9 @@ __global__ __launch_bounds__(256, 1) void gemm_xl_w4_kernel(const XlArgs p) {
   if (ktiles > 1) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) dma(1, 1, c);
-    vmcnt<16>();
+    // tile 0 landed: one tile of this wave's copies (16, or 8 past a narrow B) in flight
+    if (cpb) vmcnt<16>();
+    else vmcnt<8>();
   } else {
     vmcnt<0>();
   }

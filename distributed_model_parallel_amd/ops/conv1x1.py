@@ -70,6 +70,7 @@ def _xl(n: int, k: int) -> bool:
 
 
 _XL_MIN_N = 256  # (tools/step_ab.py arms xln128 / xln256)
+
 # forward with the BN moments at N = 128 (ResNet-50 layer-2 conv1) on the
 # 4-wave kernel's 256 x 128 tile (tools/step_ab.py arms fwdn128 / fwdnt):
 # off, it measured no faster than gemm_nt's 128 x 128 tile, which is at the

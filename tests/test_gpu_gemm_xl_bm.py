@@ -312,3 +312,4 @@ def test_w4_n128_gemm_xl_conv(mode):
         r = torch.randn(M, N, device=DEV).bfloat16()
         y, _ = C.gemm_xl_conv(a, b, "add", residual=r)
         torch.testing.assert_close(y.float(), ref.bfloat16().float() + r.float(), atol=6e-2, rtol=2e-2)
+

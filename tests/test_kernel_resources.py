@@ -34,7 +34,7 @@ def test_w4_gemm_kernels_never_spill():
         n = name.replace(" ", "")
         if n.startswith("gemm_tn_w4_kernel<0,"):
             return "64" if ",64," in n or n.endswith(",64>") else "128" if ",128," in n or n.endswith(",128>") else "256"
-        return "224" if n.endswith(",7,2>") else "128" if n.endswith(",4,1>") else "256"
+        return "224" if n.endswith(",7,2,8>") else "128" if n.endswith(",4,1,8>") else "256"
     want = {k["name"]: want_agpr(k["name"]) for k in ks}
     assert all(int(k["agpr"]) >= int(want[k["name"]]) for k in ks), [(k["name"], k["agpr"]) for k in ks]
     assert any(want[k["name"]] == "224" for k in ks), "no trimmed (MB = 7) instantiation built"
