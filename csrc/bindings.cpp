@@ -135,6 +135,7 @@ std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat
 bool conv3x3_c128_supported(int64_t c, int64_t h, int64_t w);
 at::Tensor conv3x3_c128_dgrad_s2(const at::Tensor& dy, const at::Tensor& wt);
 void set_bn_streaming(bool on);
+void set_bn_apply_blocks(int n);
 at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>& wph, int64_t hi, int64_t wi);
 void set_pool_generic(bool on);
 at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride);
@@ -216,7 +217,8 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
                               int64_t k, int64_t s, int64_t p);
 // coalesced.hip
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
-void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
+void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
+                     const std::vector<int64_t>& taps);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
 void gather_slabs(const std::vector<at::Tensor>& inputs, at::Tensor& out, bool along_inner);
 std::vector<std::vector<bool>> enable_peer_access(int64_t num_devices);
@@ -363,6 +365,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "data gradient of a 3x3/s2/p1 conv as four stride-phase implicit GEMMs on the ping-pong kernel; "
         "returns dx [N*hi*wi, Cin]",
         py::call_guard<py::gil_scoped_release>());
+  m.def("set_bn_apply_blocks", &dmp::set_bn_apply_blocks, py::arg("n"),
+        "A/B: target block count of the BN apply passes (forward apply, backward apply)");
   m.def("set_bn_streaming", &dmp::set_bn_streaming, py::arg("on"),
         "A/B: non-temporal streaming in the BN apply passes over > 256 MB tensors (default on)");
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
@@ -488,7 +492,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_copy", &dmp::multi_copy,
         py::call_guard<py::gil_scoped_release>());
   m.def("multi_transpose", &dmp::multi_transpose, py::arg("srcs"), py::arg("dsts"),
-        "dst[i] = src[i]^T for contiguous 2-byte matrices, up to 64 per launch",
+        py::arg("taps") = std::vector<int64_t>{},
+        "dst[i] = src[i]^T for contiguous 2-byte matrices, up to 64 per launch; taps[i] = T (-T: "
+        "flipped) transposes [R, T*C] -> [C, T*R] tap by tap",
         py::call_guard<py::gil_scoped_release>());
   m.def("reduce_add_into", &dmp::reduce_add_into,
         py::call_guard<py::gil_scoped_release>());

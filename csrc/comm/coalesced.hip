@@ -83,11 +83,15 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyTable t) {
 // (the W^T operands of a step's 1x1-conv data gradients, ops/wt_cache.py).
 // One 256-thread block per 64 x 64 tile through LDS: loads coalesced along
 // the source rows, stores along the destination rows.
+// Tap-wise form (taps T > 1): src [R, T*C], dst [C, T*R], tap t of src
+// (columns t*C..) transposed into tap t' of dst, t' = T-1-t when flipped --
+// a channels-last kh x kw conv weight [Cout][kh][kw][Cin] becomes the
+// flipped [Cin][kh][kw][Cout] matrix of its data gradient (conv_igemm).
 constexpr int kMaxT = 64, kTT = 64;
 struct TransTable {
   const uint16_t* src[kMaxT];
   uint16_t* dst[kMaxT];
-  int rows[kMaxT], cols[kMaxT];
+  int rows[kMaxT], cols[kMaxT], taps[kMaxT], flip[kMaxT];
   int first_tile[kMaxT + 1];
   int n;
 };
@@ -100,22 +104,25 @@ __global__ __launch_bounds__(256) void multi_transpose_kernel(const TransTable t
     if (t.first_tile[mid] <= bid) lo = mid;
     else hi = mid - 1;
   }
-  const int R = t.rows[lo], Cc = t.cols[lo];
-  const int ctiles = (Cc + kTT - 1) / kTT, local = bid - t.first_tile[lo];
+  const int R = t.rows[lo], Cc = t.cols[lo], T = t.taps[lo];
+  const int ctiles = (Cc + kTT - 1) / kTT, rtiles = (R + kTT - 1) / kTT;
+  const int local0 = bid - t.first_tile[lo], tap = local0 / (rtiles * ctiles), local = local0 - tap * rtiles * ctiles;
   const int r0 = (local / ctiles) * kTT, c0 = (local % ctiles) * kTT;
+  const int dtap = t.flip[lo] ? T - 1 - tap : tap;
   __shared__ uint16_t tile[kTT][kTT + 2];
-  const uint16_t* s = t.src[lo];
-  uint16_t* d = t.dst[lo];
+  const uint16_t* s = t.src[lo] + (int64_t)tap * Cc;  // row stride T*C
+  uint16_t* d = t.dst[lo] + (int64_t)dtap * R;        // row stride T*R
+  const int64_t sld = (int64_t)T * Cc, dld = (int64_t)T * R;
 #pragma unroll 4
   for (int i = threadIdx.x; i < kTT * kTT; i += 256) {
     const int r = i / kTT, c = i % kTT;
-    if (r0 + r < R && c0 + c < Cc) tile[r][c] = s[(int64_t)(r0 + r) * Cc + c0 + c];
+    if (r0 + r < R && c0 + c < Cc) tile[r][c] = s[(int64_t)(r0 + r) * sld + c0 + c];
   }
   __syncthreads();
 #pragma unroll 4
   for (int i = threadIdx.x; i < kTT * kTT; i += 256) {
     const int c = i / kTT, r = i % kTT;
-    if (r0 + r < R && c0 + c < Cc) d[(int64_t)(c0 + c) * R + r0 + r] = tile[r][c];
+    if (r0 + r < R && c0 + c < Cc) d[(int64_t)(c0 + c) * dld + r0 + r] = tile[r][c];
   }
 }
 
@@ -236,9 +243,13 @@ at::Tensor upload_table(const std::vector<T>& host, const at::Device& dev) {
 }  // namespace
 
 // dst[i] [C, R] = src[i] [R, C]^T for 2-byte (bf16 / fp16) matrices, in as few
-// launches as the table size allows (one for up to 64 matrices).
-void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+// launches as the table size allows (one for up to 64 matrices).  taps[i]
+// (optional): T > 1 transposes tap by tap (src [R, T*C] -> dst [C, T*R]),
+// -T also reverses the tap order (the flipped weight of a conv data gradient).
+void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
+                     const std::vector<int64_t>& taps) {
   TORCH_CHECK(srcs.size() == dsts.size(), "multi_transpose: list length mismatch");
+  TORCH_CHECK(taps.empty() || taps.size() == srcs.size(), "multi_transpose: taps length mismatch");
   if (srcs.empty()) return;
   const at::Device dev = dsts[0].device();
   auto stream = at::hip::getCurrentHIPStream(dev.index());
@@ -256,18 +267,23 @@ void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::
     const auto& s = srcs[i];
     const auto& d = dsts[i];
     TORCH_CHECK(s.is_cuda() && d.device() == dev && s.device() == dev, "multi_transpose: one device");
+    const int64_t tp = taps.empty() ? 1 : taps[i], T = tp < 0 ? -tp : tp;
+    TORCH_CHECK(T >= 1 && T <= 64, "multi_transpose: 1..64 taps");
     TORCH_CHECK(s.dim() == 2 && d.dim() == 2 && s.is_contiguous() && d.is_contiguous() && s.element_size() == 2 &&
-                    d.scalar_type() == s.scalar_type() && d.size(0) == s.size(1) && d.size(1) == s.size(0),
-                "multi_transpose: contiguous 2-byte [R, C] -> [C, R] pairs");
-    const int64_t R = s.size(0), C = s.size(1);
+                    d.scalar_type() == s.scalar_type() && s.size(1) % T == 0 && d.size(0) == s.size(1) / T &&
+                    d.size(1) == s.size(0) * T,
+                "multi_transpose: contiguous 2-byte [R, T*C] -> [C, T*R] pairs");
+    const int64_t R = s.size(0), C = s.size(1) / T;
     if (R == 0 || C == 0) continue;
     TORCH_CHECK(R < (1 << 30) && C < (1 << 30), "multi_transpose: matrix too large");
-    const int64_t nt = ((R + kTT - 1) / kTT) * ((C + kTT - 1) / kTT);
+    const int64_t nt = T * ((R + kTT - 1) / kTT) * ((C + kTT - 1) / kTT);
     if (t.n == kMaxT || tiles + nt >= (1LL << 31) - 1) flush();
     t.src[t.n] = static_cast<const uint16_t*>(s.data_ptr());
     t.dst[t.n] = static_cast<uint16_t*>(d.data_ptr());
     t.rows[t.n] = (int)R;
     t.cols[t.n] = (int)C;
+    t.taps[t.n] = (int)T;
+    t.flip[t.n] = tp < 0 ? 1 : 0;
     t.first_tile[t.n] = tiles;
     tiles += (int)nt;
     ++t.n;

@@ -29,7 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native
-from . import wgrad_stream
+from . import wgrad_stream, wt_cache
 
 _STATS = {"native": 0, "torch": 0}
 # DMP_DISABLE=igemm routes these convs to MIOpen (A/B comparisons, debugging)
@@ -265,13 +265,13 @@ class _ConvIGFn(torch.autograd.Function):
         hk = _halo_kind(cin, cout, kh, kw, stride, pad, h, w)
         if ctx.needs_input_grad[0] and hk:
             # dx = conv(dy, flip(W)^T): the same 3x3/s1/p1 C->C conv
-            wfl = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+            wfl = wt_cache.flipped(weight)
             _STATS["halo_dgrad"] += 1
             dx2, _ = _halo_conv(C, hk)(dy, wfl, False)
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
         elif ctx.needs_input_grad[0] and _xl_dgrad(cin, kh, kw, stride):
             # dx = conv(dy, flip(W)^T, pad k-1-p) on the ping-pong implicit GEMM
-            wfl = weight.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1).contiguous()
+            wfl = wt_cache.flipped(weight)
             _STATS["xl_dgrad"] += 1
             if bs is not None and bs.consumers == 1 and bs.x2 is not None:
                 _STATS["xl_bnbwd"] += 1

@@ -19,6 +19,14 @@ pipeline micro-batch: ~35).  Two caches serve those operands:
   version; any other in-place change does, and the op falls back to a fresh
   copy.  Buffers keep their storage, so captured steps (bench.py --graph)
   read them and the captured optimizer step refreshes them on every replay.
+* **Flipped kh x kw weights (optimizer-driven).** The data gradient of a
+  stride-1 kh x kw conv is the same conv over the flipped, transposed weight
+  ``w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, -1)`` (conv_igemm: two
+  torch kernels per 3x3 per backward, 13 per ResNet-50 step).  :func:`flipped`
+  keeps it in the same cache (key kind ``"flip"``) and the optimizer's
+  refresh forms it tap by tap in the same single ``multi_transpose`` launch.
+  Channels-last weights only (their [Cout][kh][kw][Cin] storage is the
+  [Cout, T*Cin] matrix the tap-wise transpose reads).
 * **Per-step (pipeline).** :class:`WTCache` holds buffers for a stage's
   weights, refreshed by the pipeline before a step's first micro-batch.
   This covers any optimizer, since the pipeline itself refreshes.
@@ -39,25 +47,40 @@ _STATS = {"hit": 0, "miss": 0, "refresh_launches": 0}
 _GEN = [0]  # optimizer step generation
 
 # key -> [weakref(weight), buf, generation, version]
-_GLOBAL: Dict[Tuple[int, Tuple[int, ...]], list] = {}
+_GLOBAL: Dict[tuple, list] = {}
 _WANTED: set = set()  # keys a backward asked for that have no entry yet
 _ENABLED = [True]
+_FLIP = [True]  # flipped kh x kw entries (tools/step_ab.py arms flipc / flipt)
 
 
-def _key(w: torch.Tensor) -> Tuple[int, Tuple[int, ...]]:
-    return w.data_ptr(), tuple(w.shape)
+def _key(w: torch.Tensor, kind: str = "t") -> tuple:
+    return (w.data_ptr(), tuple(w.shape)) if kind == "t" else (w.data_ptr(), tuple(w.shape), kind)
 
 
-def _native_transpose(srcs: List[torch.Tensor], dsts: List[torch.Tensor]) -> None:
+def _flip_src(p: torch.Tensor) -> Optional[torch.Tensor]:
+    """The [Cout, T*Cin] storage view of a channels-last kh x kw weight, or None."""
+    if p.dim() != 4 or not p.is_contiguous(memory_format=torch.channels_last):
+        return None
+    return p.detach().permute(0, 2, 3, 1).reshape(p.shape[0], -1)
+
+
+def _native_transpose(srcs: List[torch.Tensor], dsts: List[torch.Tensor], taps: Optional[List[int]] = None) -> None:
+    """dst = src^T; taps[i] = T (-T: flipped) transposes [R, T*C] -> [C, T*R] tap by tap."""
     from .. import _native
+    taps = taps or [1] * len(srcs)
     C = _native.native()
     if C is not None and srcs and srcs[0].is_cuda and hasattr(C, "multi_transpose") \
             and all(s.element_size() == 2 for s in srcs):
-        C.multi_transpose(srcs, dsts)
+        C.multi_transpose(srcs, dsts, taps)
         _STATS["refresh_launches"] += 1
         return
-    for s, d in zip(srcs, dsts):
-        d.copy_(s.t())
+    for s, d, tp in zip(srcs, dsts, taps):
+        T = abs(tp)
+        r, c = s.shape[0], s.shape[1] // T
+        blk = s.reshape(r, T, c)
+        if tp < 0:
+            blk = blk.flip(1)
+        d.copy_(blk.permute(2, 1, 0).reshape(c, T * r))
 
 
 def set_enabled(on: bool) -> None:
@@ -75,26 +98,38 @@ def after_optimizer_step(params: Iterable[torch.Tensor] = ()) -> None:
     _GEN[0] += 1
     if not _ENABLED[0] or not (_GLOBAL or _WANTED):
         return
-    srcs, dsts = [], []
+    srcs, dsts, taps = [], [], []
     with torch.no_grad():
-        for k in [k for k, e in _GLOBAL.items() if e[0]() is None or _key(e[0]()) != k]:
+        for k in [k for k, e in _GLOBAL.items()
+                  if e[0]() is None or _key(e[0](), k[2] if len(k) > 2 else "t") != k]:
             del _GLOBAL[k]
         for p in params:
             if p.dim() not in (2, 4) or p.element_size() != 2:
                 continue
-            k = _key(p)
-            e = _GLOBAL.get(k)
-            if e is None and k in _WANTED:
-                w2 = p.detach().reshape(p.shape[0], -1)
-                e = _GLOBAL[k] = [weakref.ref(p), torch.empty(w2.shape[1], w2.shape[0], dtype=p.dtype,
-                                                              device=p.device), -1, -1]
-            if e is None or e[0]() is not p:
-                continue
-            srcs.append(p.detach().reshape(p.shape[0], -1))
-            dsts.append(e[1])
-            e[2], e[3] = _GEN[0], p._version
+            for kind in ("t", "flip"):
+                k = _key(p, kind)
+                e = _GLOBAL.get(k)
+                if kind == "t":
+                    src, tp = p.detach().reshape(p.shape[0], -1), 1
+                else:
+                    if e is None and k not in _WANTED:
+                        continue
+                    src, tp = _flip_src(p), -(p.shape[2] * p.shape[3])
+                    if src is None:  # no longer channels-last: drop the entry
+                        _GLOBAL.pop(k, None)
+                        continue
+                if e is None and k in _WANTED:
+                    T = abs(tp)
+                    e = _GLOBAL[k] = [weakref.ref(p), torch.empty(src.shape[1] // T, src.shape[0] * T,
+                                                                  dtype=p.dtype, device=p.device), -1, -1]
+                if e is None or e[0]() is not p:
+                    continue
+                srcs.append(src)
+                dsts.append(e[1])
+                taps.append(tp)
+                e[2], e[3] = _GEN[0], p._version
         _WANTED.clear()
-        _native_transpose(srcs, dsts)
+        _native_transpose(srcs, dsts, taps)
 
 
 class WTCache:
@@ -162,6 +197,23 @@ def transposed(w: torch.Tensor) -> torch.Tensor:
             _WANTED.add(k)  # the owning optimizer's next step keeps a transposed copy
     _STATS["miss"] += 1
     return w.reshape(w.shape[0], -1).t().contiguous()
+
+
+def flipped(w: torch.Tensor) -> torch.Tensor:
+    """``w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, -1).contiguous()`` (the
+    data-gradient weight of a stride-1 kh x kw conv), from the optimizer-driven
+    cache when it holds a current copy of this weight."""
+    if _ENABLED[0] and _FLIP[0] and w.dim() == 4:
+        k = _key(w, "flip")
+        e = _GLOBAL.get(k)
+        if e is not None and e[2] == _GEN[0] and e[3] == w._version and e[0]() is not None:
+            _STATS["hit"] += 1
+            return e[1]
+        if e is None and w.is_leaf and w.requires_grad and w.element_size() == 2 and \
+                w.is_contiguous(memory_format=torch.channels_last):
+            _WANTED.add(k)
+    _STATS["miss"] += 1
+    return w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1).contiguous()
 
 
 def stats() -> dict:

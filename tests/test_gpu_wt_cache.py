@@ -50,3 +50,56 @@ def test_training_with_cached_wt_matches_uncached():
         wt_cache.set_enabled(True)
     for a, b in zip(*out):
         assert torch.allclose(a, b, atol=1e-6, rtol=1e-5), float((a - b).abs().max())
+
+
+@pytest.mark.parametrize("cout,cin,k", [(64, 64, 3), (256, 256, 3), (512, 128, 3), (96, 64, 5), (128, 128, 1)])
+def test_multi_transpose_flipped_taps(cout, cin, k):
+    """Tap-wise, flipped transposes: a channels-last [Cout, Cin, k, k] weight's
+    storage [Cout, k*k*Cin] -> w.flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, -1),
+    mixed with plain transposes in one launch."""
+    from distributed_model_parallel_amd import _native
+    from distributed_model_parallel_amd.ops import wt_cache
+    C = _native.require("multi_transpose")
+    torch.manual_seed(1)
+    w = torch.randn(cout, cin, k, k, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    p = torch.randn(300, 70, device="cuda").bfloat16()
+    src = wt_cache._flip_src(w)
+    d = torch.empty(cin, k * k * cout, device="cuda", dtype=torch.bfloat16)
+    dp = torch.empty(70, 300, device="cuda", dtype=torch.bfloat16)
+    dn = torch.empty(cin, k * k * cout, device="cuda", dtype=torch.bfloat16)
+    C.multi_transpose([src, p, src], [d, dp, dn], [-k * k, 1, k * k])
+    assert torch.equal(d, w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, -1))
+    assert torch.equal(dn, w.permute(1, 2, 3, 0).reshape(cin, -1))
+    assert torch.equal(dp, p.t())
+
+
+def test_flipped_weights_cached_by_the_optimizer():
+    """ResNet-50 bf16 + MasterSGD: after each optimizer step every cached
+    flipped 3x3 weight equals the torch expression on the UPDATED weight, and
+    the next backward reads it (hits).  (Whole-run weights are not compared
+    bitwise: ResNet-50's fp64-atomic BN moment reduction is not bit-
+    reproducible from run to run.)"""
+    from distributed_model_parallel_amd.models import build_model
+    from distributed_model_parallel_amd.ops import wt_cache
+    from distributed_model_parallel_amd.ops.optim import MasterSGD
+    from distributed_model_parallel_amd.utils.precision import cast_model
+    torch.manual_seed(0)
+    m = cast_model(build_model("resnet50", num_classes=10).cuda()).to(memory_format=torch.channels_last)
+    x = torch.randn(32, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    opt = MasterSGD(m.parameters(), lr=0.05, momentum=0.9)
+    wt_cache.set_enabled(True)
+    hits = []
+    for i in range(3):
+        h0 = wt_cache.stats()["hit"]
+        loss = torch.nn.functional.cross_entropy(m(x).float(), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        hits.append(wt_cache.stats()["hit"] - h0)
+        flips = {k: e for k, e in wt_cache._GLOBAL.items() if len(k) > 2 and k[2] == "flip"}
+        assert flips, "no flipped weight entered the cache"
+        for k, e in flips.items():
+            w = e[0]()
+            assert torch.equal(e[1], w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1))
+    assert hits[-1] > hits[0], hits

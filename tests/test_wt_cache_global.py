@@ -54,3 +54,18 @@ def test_global_cache_drops_freed_weights():
     gc.collect()
     wt_cache.after_optimizer_step()
     assert len(wt_cache._GLOBAL) == n - 1
+
+
+def test_flip_fallback_matches_torch_on_cpu():
+    """The CPU form of the tap-wise flipped transpose (what the refresh falls
+    back to without the extension) against the torch expression it replaces."""
+    from distributed_model_parallel_amd.ops import wt_cache
+    w = torch.randn(8, 6, 3, 3).contiguous(memory_format=torch.channels_last).half()
+    src = wt_cache._flip_src(w)
+    d = torch.empty(6, 9 * 8, dtype=w.dtype)
+    wt_cache._native_transpose([src], [d], [-9])
+    assert torch.equal(d, w.flip(2, 3).permute(1, 2, 3, 0).reshape(6, -1))
+    d1 = torch.empty(6, 9 * 8, dtype=w.dtype)
+    wt_cache._native_transpose([src], [d1], [9])
+    assert torch.equal(d1, w.permute(1, 2, 3, 0).reshape(6, -1))
+    assert wt_cache._flip_src(torch.randn(8, 6, 3, 3)) is None  # not channels-last: no storage view

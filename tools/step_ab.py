@@ -12,6 +12,8 @@ arms:
   plain_xl   every plain GEMM on gemm_xl
   fold1 / fold2  BN-fold coefficient products on hipBLASLt / our fp32 MFMA GEMM
   xln128 / xln256  1x1-conv GEMMs with N = 128 (K >= 128) on gemm_xl_conv (the two-blocks-per-CU x2 kernel) / on gemm_nt
+  bnapply1k / 2k / 4k  target block count of the BN apply passes
+  flipc / flipt  3x3 data-gradient weights flipped once per optimizer step (cache) / per backward (torch)
   tnnarrow / tnwide  4-wave weight gradients with a side of 64 / 128 on narrow tiles / on 256 x 256
   fwdn128 / fwdnt  1x1 forwards with moments at N = 128 on the 4-wave 256 x 128 tile / on gemm_nt
   n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
@@ -26,7 +28,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_model_parallel_amd import _native  # noqa: E402
-from distributed_model_parallel_amd.ops import conv1x1, conv_igemm, linear  # noqa: E402
+from distributed_model_parallel_amd.ops import conv1x1, conv_igemm, linear, wt_cache  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
 from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed  # noqa: E402
 
@@ -53,6 +55,11 @@ def _arm(name):
         "miopen": lambda: setattr(conv_igemm, "_XL_N128", False),
         "xln128": lambda: setattr(conv1x1, "_XL_MIN_N", 128),
         "xln256": lambda: setattr(conv1x1, "_XL_MIN_N", 256),
+        "bnapply1k": lambda: C.set_bn_apply_blocks(1024),
+        "bnapply2k": lambda: C.set_bn_apply_blocks(2048),
+        "bnapply4k": lambda: C.set_bn_apply_blocks(4096),
+        "flipc": lambda: wt_cache._FLIP.__setitem__(0, True),
+        "flipt": lambda: wt_cache._FLIP.__setitem__(0, False),
         "tnnarrow": lambda: C.set_tn_narrow(True),
         "tnwide": lambda: C.set_tn_narrow(False),
         "fwdn128": lambda: setattr(conv1x1, "_XL_N128_FWD", True),
