@@ -226,6 +226,7 @@ _STATS["tn_xl"] = 0
 
 
 _TN_XL_MIN_ROWS = 16_384
+_TN_XL_MIN_CH = 64  # narrower sides take the 64-wide narrow tile (tools/step_ab.py arms tnch16 / tnch64)
 
 
 def _tn_xl(m: int, cout: int, cin: int) -> bool:
@@ -237,7 +238,7 @@ def _tn_xl(m: int, cout: int, cin: int) -> bool:
     loop) only >= 256-wide shapes from 100k rows took it.  (The 224-px
     convergence test lowers the row threshold so its batch-64 run trains this
     route.)"""
-    return _TN_XL and cout >= 64 and cin >= 64 and m >= _TN_XL_MIN_ROWS
+    return _TN_XL and cout >= _TN_XL_MIN_CH and cin >= _TN_XL_MIN_CH and m >= _TN_XL_MIN_ROWS
 
 
 _STATS["tn_xl_strided"] = 0

@@ -106,7 +106,8 @@ def test_strided_gather_over_2gb_input():
 
 @pytest.mark.parametrize("M,N,K", [(200000, 64, 256), (200000, 256, 64), (100000, 128, 512), (100000, 512, 128),
                                    (70000, 64, 64), (5000, 64, 320), (3000, 200, 120), (4133, 128, 256),
-                                   (64, 64, 256)])
+                                   (64, 64, 256), (40000, 24, 144), (40000, 144, 24), (33000, 16, 96),
+                                   (20000, 32, 32)])
 @pytest.mark.parametrize("narrow", [True, False])
 def test_gemm_tn_xl_narrow_tiles(M, N, K, narrow):
     """The 4-wave weight-gradient kernel's narrow tiles (64 x 256, 256 x 64,
