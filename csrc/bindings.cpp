@@ -135,7 +135,6 @@ std::vector<at::Tensor> conv3x3_c128(const at::Tensor& x, const at::Tensor& wmat
 bool conv3x3_c128_supported(int64_t c, int64_t h, int64_t w);
 at::Tensor conv3x3_c128_dgrad_s2(const at::Tensor& dy, const at::Tensor& wt);
 void set_bn_streaming(bool on);
-void set_bn_apply_blocks(int n);
 at::Tensor conv_xl_dgrad_s2(const at::Tensor& dy, const std::vector<at::Tensor>& wph, int64_t hi, int64_t wi);
 void set_pool_generic(bool on);
 at::Tensor wgrad3x3(const at::Tensor& dy, const at::Tensor& x, int64_t stride);
@@ -365,8 +364,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "data gradient of a 3x3/s2/p1 conv as four stride-phase implicit GEMMs on the ping-pong kernel; "
         "returns dx [N*hi*wi, Cin]",
         py::call_guard<py::gil_scoped_release>());
-  m.def("set_bn_apply_blocks", &dmp::set_bn_apply_blocks, py::arg("n"),
-        "A/B: target block count of the BN apply passes (forward apply, backward apply)");
   m.def("set_bn_streaming", &dmp::set_bn_streaming, py::arg("on"),
         "A/B: non-temporal streaming in the BN apply passes over > 256 MB tensors (default on)");
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),

@@ -558,11 +558,6 @@ Grid plan(int64_t M, int C, int vec, int target = 1024, int64_t min_rows_per_lan
   return g;
 }
 
-// blocks of the partial-free apply passes (forward apply without output
-// moments, backward apply): more than the moments passes' 1024, so that more
-// 16-B loads per CU are in flight (set_bn_apply_blocks, A/B)
-int g_bn_apply_blocks = 1024;
-
 void check_input(const at::Tensor& x, int64_t C, const char* name) {
   TORCH_CHECK(x.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16,
@@ -670,7 +665,7 @@ std::vector<at::Tensor> bn_forward_apply(const at::Tensor& x, const at::Tensor& 
     bn_reduce_partials_launch(part.data_ptr<float>(), (int)g.grid.x, (int)C, osums.data_ptr<double>(),
                               (double)M, stream);
   } else if (M > 0) {
-    Grid g = plan(M, (int)C, vec_of(x), g_bn_apply_blocks);
+    Grid g = plan(M, (int)C, vec_of(x));
     dispatch_t(x, [&](auto tag) {
       using T = decltype(tag);
       const T* r = has_res ? ptr<T>(*residual) : nullptr;
@@ -823,7 +818,7 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
   at::Tensor dres;
   if (want_dres) dres = at::empty_like(x);
   if (M > 0) {
-    Grid g = plan(M, (int)C, vec_of(x), g_bn_apply_blocks);
+    Grid g = plan(M, (int)C, vec_of(x));
     dispatch_t(x, [&](auto tag) {
       using T = decltype(tag);
       const bool from_y = relu && y.has_value() && y->defined();
@@ -853,9 +848,5 @@ std::vector<at::Tensor> bn_backward_apply(const at::Tensor& dy, const at::Tensor
 }
 
 void set_bn_streaming(bool on) { g_bn_streaming = on; }
-void set_bn_apply_blocks(int n) {
-  TORCH_CHECK(n >= 256 && n <= 16384, "set_bn_apply_blocks: 256..16384");
-  g_bn_apply_blocks = n;
-}
 
 }  // namespace dmp

@@ -2047,9 +2047,7 @@ void launch_x2(const XlArgs& a, hipStream_t s) {
 template <int EPI>
 void dispatch_bn(const XlArgs& a, int bn, hipStream_t s) {
   if constexpr (EPI == XL_MOMENTS || EPI == XL_AFFINE || is_bnbwd(EPI) || EPI == XL_ADD) {
-    // N = 128 with a light epilogue: the 4-wave kernel's 256 x 128 tile
-    const bool w4n128 = w4_epi(EPI) && g_xl_pipe == 11 && a.N == 128 && w4_ok(a);
-    if (use_x2(a) && !w4n128) {
+    if (use_x2(a)) {
       launch_x2<is_bnbwd(EPI) ? (int)XL_BNBWD : EPI>(a, s);  // the x2 kernel keeps the runtime operand flags
       return;
     }

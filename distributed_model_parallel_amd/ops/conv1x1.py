@@ -66,17 +66,10 @@ def _xl(n: int, k: int) -> bool:
     conv1 forward (N = 256, K = 1024) runs 1.24x faster on it at batch 2048 and
     1.31x at 256 (profiles/raw_r4/fold_dgrad_ab_r4ac.md).  Narrow N (<= 128)
     and K = 64 stay on NT."""
-    return _XL and k >= 128 and k % 64 == 0 and n >= _XL_MIN_N
-
-
-_XL_MIN_N = 256  # (tools/step_ab.py arms xln128 / xln256)
-
-# forward with the BN moments at N = 128 (ResNet-50 layer-2 conv1) on the
-# 4-wave kernel's 256 x 128 tile (tools/step_ab.py arms fwdn128 / fwdnt):
-# off, it measured no faster than gemm_nt's 128 x 128 tile, which is at the
-# HBM roofline's reach there (114.18 vs 114.08 ms at batch 2048, 20.187 vs
-# 20.184 at 256); the x2 kernel was slower still (xln128: 113.45 vs 113.28)
-_XL_N128_FWD = False
+    return _XL and k >= 128 and k % 64 == 0 and n >= 256
+# (N = 128 stays on gemm_nt's 128 x 128 tile: on the 4-wave 256 x 128 tile
+# the forward with moments measured no faster, 114.18 vs 114.08 ms at batch
+# 2048, and the x2 kernel slower, 113.45 vs 113.28: finding 75)
 
 
 def _geom(stride: int, hi: int, wi: int):
@@ -95,8 +88,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         ho, wo = (geom[1], geom[2]) if geom else (h, w)
         w2 = weight.reshape(weight.shape[0], cin)
         # strided convs read the sampled rows in place (no subsample copy)
-        if moments and not geom and (_xl(w2.shape[0], cin) or (_XL_N128_FWD and _xl(256, cin)
-                                                                and w2.shape[0] == 128)):
+        if moments and not geom and _xl(w2.shape[0], cin):
             _STATS["xl"] += 1
             y2, mom = C.gemm_xl_conv(_rows(x), w2, "moments")
         else:

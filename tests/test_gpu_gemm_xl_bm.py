@@ -288,28 +288,3 @@ def test_w4_n128_plain():
     b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
     c = C.gemm_xl(a, b, "store")
     torch.testing.assert_close(c.float(), a.float() @ b.float().t(), atol=6e-2, rtol=2e-2)
-
-
-@pytest.mark.parametrize("mode", ["moments", "add"])
-def test_w4_n128_gemm_xl_conv(mode):
-    """1x1-conv epilogues at N = 128 on the 256 x 128 tile (dispatch_bn skips
-    the x2 kernel for them): output, moments / residual add vs fp32."""
-    C = _native.require("gemm_xl n128")
-    torch.manual_seed(10)
-    M, K, N = 50 * 256 + 19, 512, 128
-    a = torch.randn(M, K, device=DEV).bfloat16()
-    b = (torch.randn(N, K, device=DEV) * 0.03).bfloat16()
-    ref = a.float() @ b.float().t()
-    if mode == "moments":
-        y, s = C.gemm_xl_conv(a, b, "moments")
-        torch.cuda.synchronize()
-        torch.testing.assert_close(y.float(), ref, atol=6e-2, rtol=2e-2)
-        f = y.float()
-        torch.testing.assert_close(s[:N].float(), f.sum(0), atol=2e-2 * M ** 0.5, rtol=1e-3)
-        torch.testing.assert_close(s[N:2 * N].float(), (f * f).sum(0), atol=2e-2 * M ** 0.5, rtol=1e-3)
-        assert s[2 * N].item() == M
-    else:
-        r = torch.randn(M, N, device=DEV).bfloat16()
-        y, _ = C.gemm_xl_conv(a, b, "add", residual=r)
-        torch.testing.assert_close(y.float(), ref.bfloat16().float() + r.float(), atol=6e-2, rtol=2e-2)
-

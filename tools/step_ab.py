@@ -11,13 +11,10 @@ arms:
   plain_fwd  qkv forward on gemm_xl, data gradients on hipBLASLt
   plain_xl   every plain GEMM on gemm_xl
   fold1 / fold2  BN-fold coefficient products on hipBLASLt / our fp32 MFMA GEMM
-  xln128 / xln256  1x1-conv GEMMs with N = 128 (K >= 128) on gemm_xl_conv (the two-blocks-per-CU x2 kernel) / on gemm_nt
-  bnapply1k / 2k / 4k  target block count of the BN apply passes
   flipc / flipt  3x3 data-gradient weights flipped once per optimizer step (cache) / per backward (torch)
   tnmin16k / 8k / 4k  row threshold of the 4-wave TN weight gradients (below: the split-M gemm_tn kernel)
   tnch64 / tnch16  narrowest 1x1 weight-gradient side on the 4-wave TN kernel
   tnnarrow / tnwide  4-wave weight gradients with a side of 64 / 128 on narrow tiles / on 256 x 256
-  fwdn128 / fwdnt  1x1 forwards with moments at N = 128 on the 4-wave 256 x 128 tile / on gemm_nt
   n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
 
   python tools/step_ab.py --model vit_b_16 --batch 256 --arms plain_fwd,plain_xl [--steps 10] [--rounds 3]
@@ -55,11 +52,6 @@ def _arm(name):
         "fold2": lambda: C.set_fold_gemm(2),
         "n128": lambda: setattr(conv_igemm, "_XL_N128", True),
         "miopen": lambda: setattr(conv_igemm, "_XL_N128", False),
-        "xln128": lambda: setattr(conv1x1, "_XL_MIN_N", 128),
-        "xln256": lambda: setattr(conv1x1, "_XL_MIN_N", 256),
-        "bnapply1k": lambda: C.set_bn_apply_blocks(1024),
-        "bnapply2k": lambda: C.set_bn_apply_blocks(2048),
-        "bnapply4k": lambda: C.set_bn_apply_blocks(4096),
         "flipc": lambda: wt_cache._FLIP.__setitem__(0, True),
         "flipt": lambda: wt_cache._FLIP.__setitem__(0, False),
         "tnmin16k": lambda: setattr(conv1x1, "_TN_XL_MIN_ROWS", 16384),
@@ -69,8 +61,6 @@ def _arm(name):
         "tnch16": lambda: setattr(conv1x1, "_TN_XL_MIN_CH", 16),
         "tnnarrow": lambda: C.set_tn_narrow(True),
         "tnwide": lambda: C.set_tn_narrow(False),
-        "fwdn128": lambda: setattr(conv1x1, "_XL_N128_FWD", True),
-        "fwdnt": lambda: setattr(conv1x1, "_XL_N128_FWD", False),
     }
     return table[name]
 
