@@ -217,7 +217,10 @@ _TN_XL = not _native.disabled("tn_xl")
 _STATS["tn_xl"] = 0
 
 
-_TN_XL_MIN_ROWS = 16_384
+# (16k -> 8k rows with the narrow tiles: ResNet-50 layer 4 at batch 256,
+# 12544 rows, joins the 4-wave kernel; tools/step_ab.py tnmin8k 19.95 vs
+# tnmin16k 20.02 ms, tnmin4k 19.94)
+_TN_XL_MIN_ROWS = 8_192
 _TN_XL_MIN_CH = 64  # narrower sides take the 64-wide narrow tile (tools/step_ab.py arms tnch16 / tnch64)
 
 
