@@ -306,11 +306,15 @@ class _BatchNormActFn(torch.autograd.Function):
                 yd = y2.double()
                 osums = torch.cat([yd.sum(0), (yd * yd).sum(0), yd.new_tensor([float(y2.shape[0])])])
             ctx.mark_non_differentiable(osums)
+            # osums never gets a gradient: no zero [2C+1] fp64 fill per backward
+            ctx.set_materialize_grads(False)
             return back(y2), osums
         return back(y2)
 
     @staticmethod
     def backward(ctx, dy, _dosums=None):
+        if dy is None:
+            return (None,) * 16
         x2, y2, w32, b32, mean, invstd, count = ctx.saved_tensors
         (native, training, relu, has_res, back, has_w, has_b, reduce_grads, wdtype,
          ndim, clip) = ctx.meta
