@@ -149,6 +149,7 @@ bool wgrad3x3_supported(int64_t C, int64_t H, int64_t W, int64_t stride);
 void set_wgrad3x3_waves(int64_t nw);
 void set_tn_xl_rounds(int r);
 void set_tn_narrow(bool on);
+void set_gemm_xl_trim_heavy(bool on);
 at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, int64_t kw, int64_t stride,
                          int64_t pad, int64_t ho, int64_t wo, at::ScalarType out_dtype,
                          const c10::optional<at::Tensor>& out);
@@ -168,7 +169,8 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
                                      const std::vector<int64_t>& a2_map);
 // bn_fold.hip
 bool bn_fold_supported(int64_t cout, int64_t cin);
-std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums);
+std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
+                                    const c10::optional<at::Tensor>& Wf);
 at::Tensor bn_fold_bwd_sums(const at::Tensor& D, const at::Tensor& W, const at::Tensor& sdz,
                             const at::Tensor& mean);
 std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tensor& local, const at::Tensor& count,
@@ -218,6 +220,7 @@ at::Tensor maxpool2d_backward(const at::Tensor& dy, const at::Tensor& idx, int64
 void multi_copy(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
                      const std::vector<int64_t>& taps);
+void multi_cast_bf16_f32(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts);
 void reduce_add_into(const std::vector<at::Tensor>& inputs, at::Tensor& out);
 void gather_slabs(const std::vector<at::Tensor>& inputs, at::Tensor& out, bool along_inner);
 std::vector<std::vector<bool>> enable_peer_access(int64_t num_devices);
@@ -369,6 +372,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_pool_generic", &dmp::set_pool_generic, py::arg("on"),
         "A/B: route every max-pool geometry through the runtime-k kernels (default off)");
   m.def("set_tn_xl_rounds", &dmp::set_tn_xl_rounds, py::arg("rounds"));
+  m.def("set_gemm_xl_trim_heavy", &dmp::set_gemm_xl_trim_heavy, py::arg("on"),
+        "A/B: trimmed (192..240-row) tiles for the PIPE-10 heavy-epilogue GEMMs at any K (default on)");
   m.def("set_tn_narrow", &dmp::set_tn_narrow, py::arg("on"),
         "A/B: 4-wave weight-gradient tiles of 64 / 128 on an output side that narrow (default on)");
   m.def("gemm_tn_xl", &dmp::gemm_tn_xl, py::arg("A"), py::arg("B"), py::arg("out_dtype"), py::arg("out") = py::none(),
@@ -411,7 +416,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- BN folded through an expanding 1x1 conv (ops/bn_fold.py) ----
   m.def("bn_fold_supported", &dmp::bn_fold_supported, py::arg("cout"), py::arg("cin"));
-  m.def("bn_fold_fwd", &dmp::bn_fold_fwd, py::arg("W"), py::arg("G"), py::arg("asums"),
+  m.def("bn_fold_fwd", &dmp::bn_fold_fwd, py::arg("W"), py::arg("G"), py::arg("asums"), py::arg("Wf") = py::none(),
         "(sums fp64 [2Cout+1], WG fp32 [Cout, Cin]) of y = a W^T from G = a^T a and colsum(a)",
         py::call_guard<py::gil_scoped_release>());
   m.def("bn_fold_bwd_sums", &dmp::bn_fold_bwd_sums, py::arg("D"), py::arg("W"), py::arg("sdz"), py::arg("mean"),
@@ -487,6 +492,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- coalesced movement ----
   m.def("multi_copy", &dmp::multi_copy,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("multi_cast_bf16_f32", &dmp::multi_cast_bf16_f32, py::arg("srcs"), py::arg("dsts"),
+        "dst[i] (fp32) = src[i] (bf16) for contiguous tensors, up to 64 per launch",
         py::call_guard<py::gil_scoped_release>());
   m.def("multi_transpose", &dmp::multi_transpose, py::arg("srcs"), py::arg("dsts"),
         py::arg("taps") = std::vector<int64_t>{},

@@ -551,7 +551,10 @@ bool bn_fold_supported(int64_t cout, int64_t cin) {
 
 // Forward: (sums fp64 [2Cout+1], WG fp32 [Cout, Cin]) from W, G = a^T a and
 // asums = (colsum a, colsum a^2, rows) fp64 [2Cin+1].
-std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums) {
+// Wf (optional): fp32 W, e.g. the copy the optimizer keeps (ops/wt_cache.py),
+// read by the library product instead of a cast per call (fold_gemm mode 1)
+std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
+                                    const c10::optional<at::Tensor>& Wf) {
   check_w(W);
   const int64_t Cout = W.size(0), Cin = W.size(1);
   check_f32(G, Cin * Cin, "G");
@@ -570,7 +573,11 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
     return {sums, WG};
   }
   if (g_fold_gemm == 1) {
-    auto WG = at::mm(W.to(at::kFloat), G.view({Cin, Cin}));
+    const bool cached = Wf.has_value() && Wf->defined();
+    if (cached)
+      TORCH_CHECK(Wf->scalar_type() == at::kFloat && Wf->numel() == Cout * Cin && Wf->is_contiguous() &&
+                      Wf->device() == W.device(), "bn_fold_fwd: Wf must be a contiguous fp32 [Cout, Cin]");
+    auto WG = at::mm(cached ? Wf->view({Cout, Cin}) : W.to(at::kFloat), G.view({Cin, Cin}));
     hipLaunchKernelGGL(fold_fwd_sums_kernel, dim3((unsigned)((Cout + 3) / 4)), dim3(kFoldThreads), 0,
                        at::hip::getCurrentHIPStream(), reinterpret_cast<const bf16*>(W.data_ptr()),
                        WG.data_ptr<float>(), asums.data_ptr<double>(), (int)Cout, (int)Cin, sums.data_ptr<double>());

@@ -126,6 +126,38 @@ __global__ __launch_bounds__(256) void multi_transpose_kernel(const TransTable t
   }
 }
 
+
+// ---- multi_cast: many bf16 -> fp32 casts in one launch (the fp32 weights the
+// BN-fold coefficient products read, refreshed once per optimizer step by
+// ops/wt_cache.py instead of one cast kernel per folded layer per forward).
+constexpr int kMaxCast = 64, kCastPerBlock = 256 * 8;
+struct CastTable {
+  const __bf16* src[kMaxCast];
+  float* dst[kMaxCast];
+  int64_t n[kMaxCast];
+  int first_block[kMaxCast + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void multi_cast_kernel(const CastTable t) {
+  const int bid = blockIdx.x;
+  int lo = 0, hi = t.count - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.first_block[mid] <= bid) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t base = (int64_t)(bid - t.first_block[lo]) * kCastPerBlock;
+  const __bf16* s = t.src[lo];
+  float* d = t.dst[lo];
+  const int64_t n = t.n[lo];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = base + (int64_t)k * 256 + threadIdx.x;
+    if (i < n) d[i] = (float)s[i];
+  }
+}
+
 constexpr int kMaxReduceInputs = 16;
 struct PtrPack {
   const void* p[kMaxReduceInputs];
@@ -246,6 +278,45 @@ at::Tensor upload_table(const std::vector<T>& host, const at::Device& dev) {
 // launches as the table size allows (one for up to 64 matrices).  taps[i]
 // (optional): T > 1 transposes tap by tap (src [R, T*C] -> dst [C, T*R]),
 // -T also reverses the tap order (the flipped weight of a conv data gradient).
+
+// dst[i] (fp32) = src[i] (bf16), same element counts, in as few launches as the
+// table allows (one for up to 64 tensors)
+void multi_cast_bf16_f32(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size(), "multi_cast: list length mismatch");
+  if (srcs.empty()) return;
+  const at::Device dev = dsts[0].device();
+  auto stream = at::hip::getCurrentHIPStream(dev.index());
+  CastTable t{};
+  int blocks = 0;
+  auto flush = [&]() {
+    if (t.count == 0) return;
+    t.first_block[t.count] = blocks;
+    hipLaunchKernelGGL(multi_cast_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, t);
+    DMP_HIP_CHECK(hipGetLastError());
+    t = CastTable{};
+    blocks = 0;
+  };
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const auto& s = srcs[i];
+    const auto& d = dsts[i];
+    TORCH_CHECK(s.is_cuda() && s.device() == dev && d.device() == dev && s.is_contiguous() && d.is_contiguous() &&
+                    s.scalar_type() == at::kBFloat16 && d.scalar_type() == at::kFloat && s.numel() == d.numel(),
+                "multi_cast: contiguous bf16 -> fp32 pairs of equal size on one device");
+    const int64_t n = s.numel();
+    if (n == 0) continue;
+    const int64_t nb = (n + kCastPerBlock - 1) / kCastPerBlock;
+    TORCH_CHECK(nb < (1 << 30), "multi_cast: tensor too large");
+    if (t.count == kMaxCast || blocks + nb >= (1LL << 31) - 1) flush();
+    t.src[t.count] = reinterpret_cast<const __bf16*>(s.data_ptr());
+    t.dst[t.count] = d.data_ptr<float>();
+    t.n[t.count] = n;
+    t.first_block[t.count] = blocks;
+    blocks += (int)nb;
+    ++t.count;
+  }
+  flush();
+}
+
 void multi_transpose(const std::vector<at::Tensor>& srcs, const std::vector<at::Tensor>& dsts,
                      const std::vector<int64_t>& taps) {
   TORCH_CHECK(srcs.size() == dsts.size(), "multi_transpose: list length mismatch");

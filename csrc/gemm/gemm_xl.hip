@@ -1928,11 +1928,18 @@ int pick_bm_w4(int64_t M, int64_t N) {
   return cost(224) * 100 <= cost(256) * 90 ? 224 : 256;
 }
 
+// the heavy-epilogue GEMMs the 4-wave default leaves on PIPE 10 (folded-BN
+// affine, BN backward) are short-K: their tile time is mostly the epilogue,
+// which scales with the tile's rows, so trimmed tiles pay there too
+// (set_gemm_xl_trim_heavy, A/B)
+int g_xl_trim_heavy = 1;
+
 int pick_bm(int64_t M, int64_t N, int64_t K, int epi) {
   if (g_xl_pipe == 11 && w4_epi(epi)) return pick_bm_w4(M, N);
-  if (g_xl_pipe != 10) return 256;
+  const bool heavy = g_xl_pipe == 11 && g_xl_trim_heavy;
+  if (g_xl_pipe != 10 && !heavy) return 256;
   if (g_xl_bm > 0) return g_xl_bm;
-  if (g_xl_bm < 0 || K < 768) return 256;
+  if (g_xl_bm < 0 || (K < 768 && !heavy)) return 256;
   const int64_t cus = num_cus(), nt = (N + 255) / 256;
   int best = 256;
   int64_t best_cost = ((M + 255) / 256 * nt + cus - 1) / cus * 256;
@@ -2604,6 +2611,7 @@ at::Tensor conv_wgrad_xl(const at::Tensor& dy, const at::Tensor& x, int64_t kh, 
 
 void set_tn_xl_rounds(int r) { g_tn_xl_rounds = r; }
 void set_tn_narrow(bool on) { g_tn_narrow = on ? 1 : 0; }
+void set_gemm_xl_trim_heavy(bool on) { g_xl_trim_heavy = on ? 1 : 0; }
 
 int get_gemm_xl_pipe() { return g_xl_pipe; }
 void set_gemm_xl_x2(int mode) {

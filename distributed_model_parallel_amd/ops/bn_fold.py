@@ -44,6 +44,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
+from . import wt_cache
 
 _STATS = {"fold": 0, "fold_fused_bwd": 0, "fold_bnbwd_epilogue": 0}
 ENABLED = not _native.disabled("bn_fold")
@@ -133,14 +134,15 @@ class _ConvBNFoldFn(torch.autograd.Function):
         n, cin, h, w = a.shape
         cout = w3.shape[0]
         a2 = _rows(a)
-        br = [dict(inp=a2, asums=a_sums, W=w3.reshape(cout, cin), g=g3, b=b3, spec=meta.bn[0], geom=[])]
+        br = [dict(inp=a2, asums=a_sums, W=w3.reshape(cout, cin), Wp=w3, g=g3, b=b3, spec=meta.bn[0], geom=[])]
         if x is not None:
             cx, hi, wi = x.shape[1], x.shape[2], x.shape[3]
             from .conv1x1 import _geom
             geom = _geom(meta.stride, hi, wi)
             x2 = _rows(x)
             xs = C.bn_fold_colsum(x2, geom) if native else _cpu_moments(_map_rows(x2, geom, n))
-            br.append(dict(inp=x2, asums=xs, W=wd.reshape(cout, cx), g=gd, b=bd, spec=meta.bn[1], geom=geom))
+            br.append(dict(inp=x2, asums=xs, W=wd.reshape(cout, cx), Wp=wd, g=gd, b=bd, spec=meta.bn[1],
+                           geom=geom))
         for b in br:
             b.update(_fold_branch_forward(C, b, n, native))
         if native:
@@ -288,7 +290,8 @@ def _fold_branch_forward(C, b, n, native):
     rm, rv, momentum, eps, nbt, rmom, _ = b["spec"]
     G = _gram(C, b["inp"], geom, native, n)
     if native and C.bn_fold_supported(cout, cin):
-        sums, WG = C.bn_fold_fwd(W, G, asums)   # one launch: W G and the row dots
+        # W G and the row dots (the fp32 W from the optimizer-driven cache when it holds one)
+        sums, WG = C.bn_fold_fwd(W, G, asums, wt_cache.as_f32(b["Wp"]) if "Wp" in b else None)
     else:
         sums, WG = _fold_stats(W, G, asums[:cin], asums[2 * cin:2 * cin + 1])
     if rmom is not None:

@@ -27,6 +27,10 @@ pipeline micro-batch: ~35).  Two caches serve those operands:
   refresh forms it tap by tap in the same single ``multi_transpose`` launch.
   Channels-last weights only (their [Cout][kh][kw][Cin] storage is the
   [Cout, T*Cin] matrix the tap-wise transpose reads).
+* **fp32 copies (optimizer-driven).** The BN-fold coefficient product reads
+  the conv weight in fp32 (ops/bn_fold.py, one cast kernel per folded layer
+  per forward); :func:`as_f32` keeps that cast (key kind ``"f32"``),
+  refreshed by one ``multi_cast_bf16_f32`` launch per step.
 * **Per-step (pipeline).** :class:`WTCache` holds buffers for a stage's
   weights, refreshed by the pipeline before a step's first micro-batch.
   This covers any optimizer, since the pipeline itself refreshes.
@@ -98,6 +102,7 @@ def after_optimizer_step(params: Iterable[torch.Tensor] = ()) -> None:
     _GEN[0] += 1
     if not _ENABLED[0] or not (_GLOBAL or _WANTED):
         return
+    params = list(params)  # walked twice (transposes, then casts)
     srcs, dsts, taps = [], [], []
     with torch.no_grad():
         for k in [k for k, e in _GLOBAL.items()
@@ -128,8 +133,37 @@ def after_optimizer_step(params: Iterable[torch.Tensor] = ()) -> None:
                 dsts.append(e[1])
                 taps.append(tp)
                 e[2], e[3] = _GEN[0], p._version
+        csrc, cdst = [], []
+        for p in params:
+            if p.element_size() != 2 or p.dtype != torch.bfloat16:
+                continue
+            k = _key(p, "f32")
+            e = _GLOBAL.get(k)
+            if e is None and k in _WANTED:
+                e = _GLOBAL[k] = [weakref.ref(p), torch.empty(p.shape[0], p.numel() // max(1, p.shape[0]),
+                                                              dtype=torch.float32, device=p.device), -1, -1]
+            if e is None or e[0]() is not p:
+                continue
+            csrc.append(p.detach().reshape(p.shape[0], -1))
+            cdst.append(e[1])
+            e[2], e[3] = _GEN[0], p._version
         _WANTED.clear()
         _native_transpose(srcs, dsts, taps)
+        _native_cast(csrc, cdst)
+
+
+def _native_cast(srcs: List[torch.Tensor], dsts: List[torch.Tensor]) -> None:
+    if not srcs:
+        return
+    from .. import _native
+    C = _native.native()
+    if C is not None and srcs[0].is_cuda and hasattr(C, "multi_cast_bf16_f32") \
+            and all(s.is_contiguous() for s in srcs):
+        C.multi_cast_bf16_f32(srcs, dsts)
+        _STATS["refresh_launches"] += 1
+        return
+    for s, d in zip(srcs, dsts):
+        d.copy_(s)
 
 
 class WTCache:
@@ -214,6 +248,22 @@ def flipped(w: torch.Tensor) -> torch.Tensor:
             _WANTED.add(k)
     _STATS["miss"] += 1
     return w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1).contiguous()
+
+
+def as_f32(w: torch.Tensor) -> Optional[torch.Tensor]:
+    """fp32 copy [out, in] of a bf16 weight parameter from the optimizer-driven
+    cache, or None (the caller casts) -- and then noted for the next refresh."""
+    if not _ENABLED[0] or w.dtype != torch.bfloat16:
+        return None
+    k = _key(w, "f32")
+    e = _GLOBAL.get(k)
+    if e is not None and e[2] == _GEN[0] and e[3] == w._version and e[0]() is not None:
+        _STATS["hit"] += 1
+        return e[1]
+    if e is None and w.is_leaf and w.requires_grad:
+        _WANTED.add(k)
+    _STATS["miss"] += 1
+    return None
 
 
 def stats() -> dict:

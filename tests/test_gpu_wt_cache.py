@@ -102,4 +102,21 @@ def test_flipped_weights_cached_by_the_optimizer():
         for k, e in flips.items():
             w = e[0]()
             assert torch.equal(e[1], w.flip(2, 3).permute(1, 2, 3, 0).reshape(w.shape[1], -1))
+        # the fp32 copies the BN-fold coefficient products read (ops/bn_fold.py)
+        f32 = {k: e for k, e in wt_cache._GLOBAL.items() if len(k) > 2 and k[2] == "f32"}
+        assert f32, "no fp32 weight copy entered the cache"
+        for k, e in f32.items():
+            w = e[0]()
+            assert torch.equal(e[1], w.float().reshape(w.shape[0], -1))
     assert hits[-1] > hits[0], hits
+
+
+def test_multi_cast_matches_torch():
+    from distributed_model_parallel_amd import _native
+    C = _native.require("multi_cast_bf16_f32")
+    torch.manual_seed(2)
+    srcs = [torch.randn(n, device="cuda").bfloat16() for n in (1, 7, 2048, 2049, 5000, 1 << 20)] * 12
+    dsts = [torch.empty(s.numel(), device="cuda") for s in srcs]
+    C.multi_cast_bf16_f32(srcs, dsts)
+    for s, d in zip(srcs, dsts):
+        assert torch.equal(d, s.float())

@@ -14,6 +14,8 @@ arms:
   flipc / flipt  3x3 data-gradient weights flipped once per optimizer step (cache) / per backward (torch)
   tnmin16k / 8k / 4k  row threshold of the 4-wave TN weight gradients (below: the split-M gemm_tn kernel)
   tnch64 / tnch16  narrowest 1x1 weight-gradient side on the 4-wave TN kernel
+  trimh / notrimh  trimmed row tiles for the PIPE-10 heavy-epilogue (short-K) GEMMs / 256 rows
+  f32c / f32t  BN-fold fp32 weights from the optimizer-driven cache / a cast per forward
   tnnarrow / tnwide  4-wave weight gradients with a side of 64 / 128 on narrow tiles / on 256 x 256
   n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
 
@@ -30,6 +32,9 @@ from distributed_model_parallel_amd import _native  # noqa: E402
 from distributed_model_parallel_amd.ops import conv1x1, conv_igemm, linear, wt_cache  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
 from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed  # noqa: E402
+
+
+_AS_F32 = [None]
 
 
 def _plain(mode):
@@ -59,6 +64,10 @@ def _arm(name):
         "tnmin4k": lambda: setattr(conv1x1, "_TN_XL_MIN_ROWS", 4096),
         "tnch64": lambda: setattr(conv1x1, "_TN_XL_MIN_CH", 64),
         "tnch16": lambda: setattr(conv1x1, "_TN_XL_MIN_CH", 16),
+        "trimh": lambda: C.set_gemm_xl_trim_heavy(True),
+        "notrimh": lambda: C.set_gemm_xl_trim_heavy(False),
+        "f32c": lambda: setattr(wt_cache, "as_f32", _AS_F32[0]),
+        "f32t": lambda: setattr(wt_cache, "as_f32", lambda w: None),
         "tnnarrow": lambda: C.set_tn_narrow(True),
         "tnwide": lambda: C.set_tn_narrow(False),
     }
@@ -77,6 +86,7 @@ def main():
     os.environ.setdefault("WORLD_SIZE", "1")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")
+    _AS_F32[0] = wt_cache.as_f32
     env = init_distributed()
     st = build_train_state(StepConfig(model=args.model, batch_size=args.batch), env.device)
     arms = args.arms.split(",")
