@@ -114,11 +114,11 @@ def after_optimizer_step(params: Iterable[torch.Tensor] = ()) -> None:
             for kind in ("t", "flip"):
                 k = _key(p, kind)
                 e = _GLOBAL.get(k)
+                if e is None and k not in _WANTED:
+                    continue  # (no source view either: reshaping a channels-last 3x3 weight copies it)
                 if kind == "t":
                     src, tp = p.detach().reshape(p.shape[0], -1), 1
                 else:
-                    if e is None and k not in _WANTED:
-                        continue
                     src, tp = _flip_src(p), -(p.shape[2] * p.shape[3])
                     if src is None:  # no longer channels-last: drop the entry
                         _GLOBAL.pop(k, None)
