@@ -17,6 +17,9 @@ task.  Set DMP_CONVERGENCE_OUT=<file.json> to dump the curves.
 import copy
 import json
 import os
+import subprocess
+import sys
+import tempfile
 
 import pytest
 import torch
@@ -126,6 +129,46 @@ def _mean(v):
     return sum(v) / len(v)
 
 
+# The stock fp32 reference trains in a CHILD process: a fresh process holds
+# none of the earlier GPU tests' state.  (Run inside the suite, the reference
+# backward aborted -- SIGABRT in the autograd device thread, message lost to
+# pytest's capture -- in 2 of 4 full-suite runs of one build, never when this
+# file ran alone: profiles/README.md finding 77.  An abort here took the whole
+# suite down; a failing child fails only this test.)
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _reference_in_child(kind, model, arch, ncls, steps, batch, lr, **data):
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "ref.pt")
+        torch.save(dict(kind=kind, arch=arch, ncls=ncls, steps=steps, batch=batch, lr=lr,
+                        state={k: v.detach().cpu() for k, v in model.state_dict().items()}, **data), path)
+        code = ("import sys; sys.path.insert(0, %r); import importlib.util as u; "
+                "s = u.spec_from_file_location('conv_child', %r); m = u.module_from_spec(s); "
+                "s.loader.exec_module(m); m._child_main(%r)") % (_ROOT, os.path.abspath(__file__), path)
+        r = subprocess.run([sys.executable, "-c", code], cwd=_ROOT, capture_output=True, text=True, timeout=1500)
+        assert r.returncode == 0, f"reference child rc={r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+        with open(path + ".json") as f:
+            return json.load(f)
+
+
+def _child_main(path):
+    p = torch.load(path, weights_only=True)
+    m = build_model(p["arch"], num_classes=p["ncls"])
+    m.load_state_dict(p["state"])
+    out = {}
+    if p["kind"] == "small":
+        ref, out["losses"] = _train_reference(m, p["xs"], p["ys"], p["steps"], p["batch"], p["lr"])
+        out["acc"] = _accuracy(ref, p["xh"], p["yh"], False)
+    else:
+        data = _Templates(p["ncls"], p["size"], noise=p["noise"])
+        out["losses"] = _train_reference_fn(m, data, p["steps"], p["batch"], p["lr"])
+    with open(path + ".json", "w") as f:
+        json.dump(out, f)
+
+
 def _steps_to(v, thr, k=5):
     """First step whose k-step mean is below thr (None if never)."""
     for i in range(len(v) - k + 1):
@@ -146,12 +189,13 @@ def test_native_training_tracks_stock_pytorch(arch, shape, ncls, steps, batch, l
     base = build_model(arch, num_classes=ncls)
     ref0 = copy.deepcopy(base)
     nat, l_nat = _train_native(base, xs, ys, steps, batch, lr)
-    ref, l_ref = _train_reference(ref0, xs, ys, steps, batch, lr)
     # held-out samples: the same class templates (seed 1), labels and noise re-drawn
     xh, yh = _task(ncls, shape, 9216, seed=1, noise=noise)
     xh, yh = xh[8192:], yh[8192:]
     xh = xh + 0.25 * torch.randn(xh.shape, generator=gv)
-    acc_nat, acc_ref = _accuracy(nat, xh, yh, True), _accuracy(ref, xh, yh, False)
+    acc_nat = _accuracy(nat, xh, yh, True)
+    r = _reference_in_child("small", ref0, arch, ncls, steps, batch, lr, xs=xs, ys=ys, xh=xh, yh=yh)
+    l_ref, acc_ref = r["losses"], r["acc"]
     out = os.environ.get("DMP_CONVERGENCE_OUT")
     if out:
         rec = {}
@@ -283,7 +327,7 @@ def test_resnet50_224_training_covers_bench_routes_and_tracks_stock():
     trained = routes.active(routes.diff(routes.route_counts(), r0))
     del base
     torch.cuda.empty_cache()
-    l_ref = _train_reference_fn(ref0, data, steps, batch, lr)
+    l_ref = _reference_in_child("t224", ref0, "resnet50", ncls, steps, batch, lr, size=224, noise=4.0)["losses"]
     del ref0
     torch.cuda.empty_cache()
     bench = _bench_routes()
