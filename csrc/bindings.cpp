@@ -171,6 +171,13 @@ std::vector<at::Tensor> gemm_xl_conv(const at::Tensor& A, const at::Tensor& B, c
 bool bn_fold_supported(int64_t cout, int64_t cin);
 std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
                                     const c10::optional<at::Tensor>& Wf);
+std::vector<at::Tensor> bn_fold_fwd_finalize(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
+                                             const c10::optional<at::Tensor>& Wf,
+                                             const c10::optional<at::Tensor>& weight,
+                                             const c10::optional<at::Tensor>& bias,
+                                             const c10::optional<at::Tensor>& running_mean,
+                                             const c10::optional<at::Tensor>& running_var, double momentum,
+                                             double eps, const c10::optional<at::Tensor>& num_batches_tracked);
 at::Tensor bn_fold_bwd_sums(const at::Tensor& D, const at::Tensor& W, const at::Tensor& sdz,
                             const at::Tensor& mean);
 std::vector<at::Tensor> bn_fold_bwd_coef(const at::Tensor& sums, const at::Tensor& local, const at::Tensor& count,
@@ -416,6 +423,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 
   // ---- BN folded through an expanding 1x1 conv (ops/bn_fold.py) ----
   m.def("bn_fold_supported", &dmp::bn_fold_supported, py::arg("cout"), py::arg("cin"));
+  m.def("bn_fold_fwd_finalize", &dmp::bn_fold_fwd_finalize, py::arg("W"), py::arg("G"), py::arg("asums"),
+        py::arg("Wf"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"), py::arg("running_var"),
+        py::arg("momentum"), py::arg("eps"), py::arg("num_batches_tracked"),
+        "bn_fold_fwd + the BN finalize of its moments in one launch: (sums, WG, coef[4, Cout])");
   m.def("bn_fold_fwd", &dmp::bn_fold_fwd, py::arg("W"), py::arg("G"), py::arg("asums"), py::arg("Wf") = py::none(),
         "(sums fp64 [2Cout+1], WG fp32 [Cout, Cin]) of y = a W^T from G = a^T a and colsum(a)",
         py::call_guard<py::gil_scoped_release>());

@@ -240,10 +240,23 @@ __global__ __launch_bounds__(kFoldThreads) void fold_sgemm_kernel(const bf16* __
 
 // Forward row sums from WG = W G (fold_gemm modes 1, 2): one wave per
 // output channel, sums = [W s, rowdot(WG, W)] in fp64, plus the row count.
+// Finalize fused in (FoldFin set, no cross-rank moment reduce in between):
+// the same per-channel coefficients as batchnorm.hip's bn_finalize_kernel
+// (coef = [scale, shift, mean, invstd] x Cout, running statistics and the
+// step counter) from the moments this wave just formed -- one launch fewer
+// per folded BN.
+struct FoldFin {
+  const float *w, *b;
+  float *rm, *rv, *coef;
+  int64_t* nbt;
+  float momentum, eps;
+};
+
 __global__ __launch_bounds__(kFoldThreads) void fold_fwd_sums_kernel(const bf16* __restrict__ W,
                                                                      const float* __restrict__ WG,
                                                                      const double* __restrict__ asums, int Cout,
-                                                                     int Cin, double* __restrict__ sums) {
+                                                                     int Cin, double* __restrict__ sums,
+                                                                     FoldFin fin) {
   const int k = blockIdx.x * (kFoldThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (k >= Cout) return;
   double qd = 0.0, md = 0.0;
@@ -255,9 +268,28 @@ __global__ __launch_bounds__(kFoldThreads) void fold_fwd_sums_kernel(const bf16*
   qd = wave_sum(qd);
   md = wave_sum(md);
   if (lane == 0) {
+    const double n = asums[2 * Cin];  // rows
     sums[k] = md;          // sum_m y[m, k]
     sums[Cout + k] = qd;   // sum_m y[m, k]^2
-    if (k == 0) sums[2 * Cout] = asums[2 * Cin];  // rows
+    if (k == 0) sums[2 * Cout] = n;
+    if (fin.coef) {
+      const double m = md / n;
+      double v = qd / n - m * m;
+      v = v < 0.0 ? 0.0 : v;
+      const float mean = (float)m, var_b = (float)v, invstd = (float)(1.0 / sqrt(v + (double)fin.eps));
+      const float ww = fin.w ? fin.w[k] : 1.f, bb = fin.b ? fin.b[k] : 0.f;
+      const float sc = ww * invstd;
+      fin.coef[k] = sc;
+      fin.coef[Cout + k] = bb - mean * sc;
+      fin.coef[2 * Cout + k] = mean;
+      fin.coef[3 * Cout + k] = invstd;
+      if (fin.rm) {
+        const float unb = n > 1.0 ? (float)((double)var_b * n / (n - 1.0)) : var_b;
+        fin.rm[k] = (1.f - fin.momentum) * fin.rm[k] + fin.momentum * mean;
+        fin.rv[k] = (1.f - fin.momentum) * fin.rv[k] + fin.momentum * unb;
+      }
+      if (fin.nbt && k == 0) *fin.nbt += 1;
+    }
   }
 }
 
@@ -553,8 +585,9 @@ bool bn_fold_supported(int64_t cout, int64_t cin) {
 // asums = (colsum a, colsum a^2, rows) fp64 [2Cin+1].
 // Wf (optional): fp32 W, e.g. the copy the optimizer keeps (ops/wt_cache.py),
 // read by the library product instead of a cast per call (fold_gemm mode 1)
-std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
-                                    const c10::optional<at::Tensor>& Wf) {
+namespace {
+std::vector<at::Tensor> fold_fwd_impl(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
+                                      const c10::optional<at::Tensor>& Wf, const FoldFin& fin) {
   check_w(W);
   const int64_t Cout = W.size(0), Cin = W.size(1);
   check_f32(G, Cin * Cin, "G");
@@ -568,7 +601,7 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
                        nullptr, nullptr, (int)Cout, (int)Cin, (int)Cin, WG.data_ptr<float>(), nullptr, 0, 0, nullptr);
     hipLaunchKernelGGL(fold_fwd_sums_kernel, dim3((unsigned)((Cout + 3) / 4)), dim3(kFoldThreads), 0, stream,
                        reinterpret_cast<const bf16*>(W.data_ptr()), WG.data_ptr<float>(), asums.data_ptr<double>(),
-                       (int)Cout, (int)Cin, sums.data_ptr<double>());
+                       (int)Cout, (int)Cin, sums.data_ptr<double>(), fin);
     DMP_HIP_CHECK(hipGetLastError());
     return {sums, WG};
   }
@@ -580,7 +613,8 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
     auto WG = at::mm(cached ? Wf->view({Cout, Cin}) : W.to(at::kFloat), G.view({Cin, Cin}));
     hipLaunchKernelGGL(fold_fwd_sums_kernel, dim3((unsigned)((Cout + 3) / 4)), dim3(kFoldThreads), 0,
                        at::hip::getCurrentHIPStream(), reinterpret_cast<const bf16*>(W.data_ptr()),
-                       WG.data_ptr<float>(), asums.data_ptr<double>(), (int)Cout, (int)Cin, sums.data_ptr<double>());
+                       WG.data_ptr<float>(), asums.data_ptr<double>(), (int)Cout, (int)Cin, sums.data_ptr<double>(),
+                       fin);
     DMP_HIP_CHECK(hipGetLastError());
     return {sums, WG};
   }
@@ -596,6 +630,50 @@ std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, co
   else go(fold_fwd_kernel<4>);
   DMP_HIP_CHECK(hipGetLastError());
   return {sums, WG};
+}
+}  // namespace
+
+std::vector<at::Tensor> bn_fold_fwd(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
+                                    const c10::optional<at::Tensor>& Wf) {
+  return fold_fwd_impl(W, G, asums, Wf, FoldFin{});
+}
+
+// bn_fold_fwd plus the BN finalize of its moments in the same launch (fold_gemm
+// modes 1 / 2; no cross-rank moment reduce may sit in between): returns (sums,
+// WG, coef [4, Cout] = scale, shift, mean, invstd), updates the running
+// statistics and num_batches_tracked as bn_finalize does.
+std::vector<at::Tensor> bn_fold_fwd_finalize(const at::Tensor& W, const at::Tensor& G, const at::Tensor& asums,
+                                             const c10::optional<at::Tensor>& Wf,
+                                             const c10::optional<at::Tensor>& weight,
+                                             const c10::optional<at::Tensor>& bias,
+                                             const c10::optional<at::Tensor>& running_mean,
+                                             const c10::optional<at::Tensor>& running_var, double momentum,
+                                             double eps, const c10::optional<at::Tensor>& num_batches_tracked) {
+  const int64_t Cout = W.size(0);
+  TORCH_CHECK(g_fold_gemm == 1 || g_fold_gemm == 2, "bn_fold_fwd_finalize: fold_gemm modes 1 / 2 only");
+  auto f32 = [&](const c10::optional<at::Tensor>& t, const char* name) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == Cout, name,
+                " must be a contiguous fp32 [Cout] GPU tensor");
+    return t->data_ptr<float>();
+  };
+  auto coef = at::empty({4, Cout}, W.options().dtype(at::kFloat));
+  FoldFin fin{};
+  fin.w = f32(weight, "weight");
+  fin.b = f32(bias, "bias");
+  fin.rm = f32(running_mean, "running_mean");
+  fin.rv = f32(running_var, "running_var");
+  TORCH_CHECK((fin.rm == nullptr) == (fin.rv == nullptr), "running_mean and running_var together");
+  fin.coef = coef.data_ptr<float>();
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong && num_batches_tracked->numel() == 1,
+                "num_batches_tracked must be a 1-element int64 tensor");
+    fin.nbt = num_batches_tracked->data_ptr<int64_t>();
+  }
+  fin.momentum = (float)momentum;
+  fin.eps = (float)eps;
+  auto r = fold_fwd_impl(W, G, asums, Wf, fin);
+  return {r[0], r[1], coef};
 }
 
 // Backward local sums [sdz, sum dz*(y - mean)] fp64 [2Cout] from D = dz^T a.

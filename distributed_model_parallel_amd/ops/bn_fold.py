@@ -70,6 +70,11 @@ def _fold_stats(W: torch.Tensor, G: torch.Tensor, s: torch.Tensor, count: torch.
     return torch.cat([Wd @ s, (WG * Wd).sum(1), count.reshape(1)]), WG
 
 
+# finalize fused into the folded-moments kernel (bn_fold_fwd_finalize) when no
+# SyncBN reduce sits between them (tools/step_ab.py arms finf / finsep)
+_FUSED_FINALIZE = True
+
+
 def _finalize(sums, w32, b32, rm, rv, momentum, eps, cout, nbt, native):
     if native:
         coef = _native.require("bn_fold").bn_finalize(sums, w32, b32, rm, rv, float(momentum), float(eps),
@@ -289,18 +294,24 @@ def _fold_branch_forward(C, b, n, native):
     cout, cin = W.shape
     rm, rv, momentum, eps, nbt, rmom, _ = b["spec"]
     G = _gram(C, b["inp"], geom, native, n)
-    if native and C.bn_fold_supported(cout, cin):
-        # W G and the row dots (the fp32 W from the optimizer-driven cache when it holds one)
-        sums, WG = C.bn_fold_fwd(W, G, asums, wt_cache.as_f32(b["Wp"]) if "Wp" in b else None)
-    else:
-        sums, WG = _fold_stats(W, G, asums[:cin], asums[2 * cin:2 * cin + 1])
-    if rmom is not None:
-        sums = rmom(sums)
     w32 = b["g"].float() if b["g"] is not None else None
     b32 = b["b"].float() if b["b"] is not None else None
     rm = rm if (rm is not None and rm.dtype == torch.float32) else None
     rv = rv if rm is not None else None
-    scale, shift, mean, invstd = _finalize(sums, w32, b32, rm, rv, momentum, eps, cout, nbt, native)
+    Wf = wt_cache.as_f32(b["Wp"]) if (native and "Wp" in b) else None
+    if native and C.bn_fold_supported(cout, cin) and rmom is None and _FUSED_FINALIZE and C.get_fold_gemm() in (1, 2):
+        # W G, the row dots and the BN finalize in one launch (no cross-rank moment reduce in between)
+        sums, WG, coef = C.bn_fold_fwd_finalize(W, G, asums, Wf, w32, b32, rm, rv, float(momentum), float(eps), nbt)
+        scale, shift, mean, invstd = coef[0], coef[1], coef[2], coef[3]
+    else:
+        if native and C.bn_fold_supported(cout, cin):
+            # W G and the row dots (the fp32 W from the optimizer-driven cache when it holds one)
+            sums, WG = C.bn_fold_fwd(W, G, asums, Wf)
+        else:
+            sums, WG = _fold_stats(W, G, asums[:cin], asums[2 * cin:2 * cin + 1])
+        if rmom is not None:
+            sums = rmom(sums)
+        scale, shift, mean, invstd = _finalize(sums, w32, b32, rm, rv, momentum, eps, cout, nbt, native)
     return dict(WG=WG.float(), scale=scale.contiguous(), shift=shift.contiguous(), mean=mean, invstd=invstd,
                 w32=w32, count=sums[-1:])
 

@@ -386,3 +386,37 @@ def test_fold_statistics_at_headline_rows(positive_w):
     ref = torch.relu((y - mean) / torch.sqrt(var + bn.eps) * bn.weight.double() + bn.bias.double())
     got = out.permute(0, 2, 3, 1).reshape(-1, cout)[rows].double()
     assert ((got - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("cout,cin", [(256, 64), (1024, 256), (2048, 512)])
+def test_fold_fwd_finalize_matches_separate_launches(cout, cin):
+    """bn_fold_fwd_finalize (moments + BN finalize in one launch) against
+    bn_fold_fwd followed by bn_finalize: moments and step counter bitwise,
+    coefficients and running statistics to fp32 rounding."""
+    from distributed_model_parallel_amd import _native
+    C = _native.require("bn_fold")
+    torch.manual_seed(3)
+    dev = "cuda"
+    W = (torch.randn(cout, cin, device=dev) * 0.05).bfloat16()
+    a = torch.relu(torch.randn(4096, cin, device=dev)).bfloat16()
+    G = a.float().t() @ a.float()
+    af = a.double()
+    asums = torch.cat([af.sum(0), (af * af).sum(0), af.new_tensor([float(a.shape[0])])])
+    w32 = torch.rand(cout, device=dev) + 0.5
+    b32 = torch.randn(cout, device=dev) * 0.1
+    outs = []
+    for fused in (True, False):
+        rm, rv = torch.zeros(cout, device=dev), torch.ones(cout, device=dev)
+        nbt = torch.zeros(1, dtype=torch.long, device=dev)
+        if fused:
+            sums, WG, coef = C.bn_fold_fwd_finalize(W, G, asums, None, w32, b32, rm, rv, 0.1, 1e-5, nbt)
+        else:
+            sums, WG = C.bn_fold_fwd(W, G, asums)
+            coef = C.bn_finalize(sums, w32, b32, rm, rv, 0.1, 1e-5, cout, nbt)
+        torch.cuda.synchronize()
+        outs.append((sums, WG, coef, rm, rv, nbt))
+    (s1, w1, c1, rm1, rv1, n1), (s0, w0, c0, rm0, rv0, n0) = outs
+    assert torch.equal(s1, s0) and torch.equal(w1, w0) and torch.equal(n1, n0)
+    # (same formulas; only the compiler's fma contraction may differ between the two kernels)
+    for x, y in ((c1, c0), (rm1, rm0), (rv1, rv0)):
+        torch.testing.assert_close(x, y, rtol=1e-6, atol=1e-7)

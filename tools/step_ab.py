@@ -16,6 +16,7 @@ arms:
   tnch64 / tnch16  narrowest 1x1 weight-gradient side on the 4-wave TN kernel
   trimh / notrimh  trimmed row tiles for the PIPE-10 heavy-epilogue (short-K) GEMMs / 256 rows
   f32c / f32t  BN-fold fp32 weights from the optimizer-driven cache / a cast per forward
+  finf / finsep  BN-fold finalize fused into the folded-moments launch / a separate bn_finalize
   tnnarrow / tnwide  4-wave weight gradients with a side of 64 / 128 on narrow tiles / on 256 x 256
   n128 / miopen  Cout = 128 3x3 forwards (ResNet-50 layer-2 stride 2) on the 4-wave 256 x 128 tile / MIOpen
 
@@ -29,7 +30,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from distributed_model_parallel_amd import _native  # noqa: E402
-from distributed_model_parallel_amd.ops import conv1x1, conv_igemm, linear, wt_cache  # noqa: E402
+from distributed_model_parallel_amd.ops import bn_fold, conv1x1, conv_igemm, linear, wt_cache  # noqa: E402
 from distributed_model_parallel_amd.train.step import StepConfig, build_train_state  # noqa: E402
 from distributed_model_parallel_amd.utils.env import init_distributed, destroy_distributed  # noqa: E402
 
@@ -68,6 +69,8 @@ def _arm(name):
         "notrimh": lambda: C.set_gemm_xl_trim_heavy(False),
         "f32c": lambda: setattr(wt_cache, "as_f32", _AS_F32[0]),
         "f32t": lambda: setattr(wt_cache, "as_f32", lambda w: None),
+        "finf": lambda: setattr(bn_fold, "_FUSED_FINALIZE", True),
+        "finsep": lambda: setattr(bn_fold, "_FUSED_FINALIZE", False),
         "tnnarrow": lambda: C.set_tn_narrow(True),
         "tnwide": lambda: C.set_tn_narrow(False),
     }
