@@ -117,13 +117,21 @@ def init_distributed(backend: Optional[str] = None, dist_url: Optional[str] = No
 
 def destroy_distributed() -> None:
     if dist.is_initialized():
+        linger = False
         if dist.get_backend() == "gloo" and dist.get_world_size() > 1:
             # every rank reaches the teardown before any closes its pairs: a gloo
             # process group destroyed while a peer still drains the last
             # collective aborted that peer ("terminate called without an active
             # exception", ~1 in 4 four-rank CPU pipeline benches)
             dist.barrier()
+            # and rank 0 hosts the TCP store: if it exits first, a peer still
+            # tearing down polls a dead store ("... could not be retrieved.
+            # err=-3") and aborts the same way (seen once in a round-6 CPU suite)
+            linger = dist.get_rank() == 0
         dist.destroy_process_group()
+        if linger:
+            import time
+            time.sleep(1.0)
 
 
 def seed_everything(seed: int) -> None:
