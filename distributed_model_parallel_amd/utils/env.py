@@ -122,8 +122,13 @@ def destroy_distributed() -> None:
             # every rank reaches the teardown before any closes its pairs: a gloo
             # process group destroyed while a peer still drains the last
             # collective aborted that peer ("terminate called without an active
-            # exception", ~1 in 4 four-rank CPU pipeline benches)
-            dist.barrier()
+            # exception", ~1 in 4 four-rank CPU pipeline benches).  Bounded: a
+            # peer that failed never arrives, and then we tear down anyway.
+            try:
+                import datetime
+                dist.monitored_barrier(timeout=datetime.timedelta(seconds=60))
+            except RuntimeError:
+                pass
             # and rank 0 hosts the TCP store: if it exits first, a peer still
             # tearing down polls a dead store ("... could not be retrieved.
             # err=-3") and aborts the same way (seen once in a round-6 CPU suite)

@@ -21,18 +21,26 @@ def _entry(rank, world, port, fn, args, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     torch.set_num_threads(1)
+    ok = False
     try:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         res = fn(rank, world, *args)
         torch.save({"ok": True, "res": res}, os.path.join(outdir, f"r{rank}.pt"))
+        ok = True
     except Exception:  # noqa: BLE001
         torch.save({"ok": False, "err": traceback.format_exc()}, os.path.join(outdir, f"r{rank}.pt"))
         raise
     finally:
         if dist.is_initialized():
             from distributed_model_parallel_amd.comm.rccl import reset_default_communicator
+            from distributed_model_parallel_amd.utils.env import destroy_distributed
             reset_default_communicator()
-            dist.destroy_process_group()
+            if ok:
+                # barrier + rank-0 store linger (a peer tearing down against a dead
+                # store aborted with "terminate called without an active exception")
+                destroy_distributed()
+            else:  # a failed rank: its peers may never reach a barrier
+                dist.destroy_process_group()
 
 
 def run_world(fn, world: int, *args):
