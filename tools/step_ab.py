@@ -7,6 +7,7 @@ HIP events around --steps steps after 3 untimed ones.
 arms:
   bm256      4-wave GEMMs always on 256-row tiles (_C.set_gemm_xl_bm(-1))
   bmauto     224-row tiles where they fill the last round (pick_bm_w4, default)
+  bm224      224-row tiles for every 4-wave GEMM
   plain_lib  ViT plain GEMMs (qkv forward, N = 768 data gradients) on hipBLASLt
   plain_fwd  qkv forward on gemm_xl, data gradients on hipBLASLt
   plain_xl   every plain GEMM on gemm_xl
@@ -51,6 +52,7 @@ def _arm(name):
     table = {
         "bm256": lambda: C.set_gemm_xl_bm(-1),
         "bmauto": lambda: C.set_gemm_xl_bm(0),
+        "bm224": lambda: C.set_gemm_xl_bm(224),
         "plain_lib": _plain("lib"),
         "plain_fwd": _plain("fwd"),
         "plain_xl": _plain("xl"),
